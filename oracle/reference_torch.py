@@ -1,0 +1,281 @@
+"""ORACLE (test infrastructure only) — stock-PyTorch CPU restatement of the
+reference training step. Never imported by the product package.
+
+Every function cites the reference file:line whose behaviour it restates.
+Arithmetic is stock ATen on CPU (the same ops the reference calls), in the
+dtype of the inputs (fp32 for parity, fp64 for gradchecks).
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+# ---------------------------------------------------------------------------
+# Synthetic data — SURVEY.md §8(c) generator (the one the pinned observation
+# was taken on): per-sample union of random discs + noisy image, min-max.
+# ---------------------------------------------------------------------------
+
+
+def synthetic_batch(B: int, H: int, W: int, seed: int = 42) -> Tuple[torch.Tensor, torch.Tensor]:
+    g = torch.Generator().manual_seed(seed)
+    rows, cols = torch.meshgrid(torch.arange(H), torch.arange(W), indexing="ij")
+    masks = torch.zeros(B, 1, H, W)
+    for b in range(B):
+        n_discs = int(torch.randint(5, 15, (1,), generator=g))
+        cx = torch.rand(n_discs, generator=g) * W
+        cy = torch.rand(n_discs, generator=g) * H
+        rad = (0.03 + 0.07 * torch.rand(n_discs, generator=g)) * min(H, W)
+        inside = torch.zeros(H, W, dtype=torch.bool)
+        for k in range(n_discs):
+            inside |= (cols - cx[k]) ** 2 + (rows - cy[k]) ** 2 <= rad[k] ** 2
+        masks[b, 0] = inside.float()
+    img = 0.2 + 0.6 * masks + 0.1 * torch.randn(B, 1, H, W, generator=g)
+    lo = img.amin(dim=(1, 2, 3), keepdim=True)
+    hi = img.amax(dim=(1, 2, 3), keepdim=True)
+    # src/dataset.py:82 per-image min-max normalisation
+    img = (img - lo) / (hi - lo + 1e-8)
+    return img, masks
+
+
+# ---------------------------------------------------------------------------
+# U-Net — src/unet.py:19-216. Module tree, parameter names and creation order
+# match the reference exactly so torch.manual_seed(s) yields identical weights
+# and state_dict keys.
+# ---------------------------------------------------------------------------
+
+# (name, cin_mult, cout_mult, dropout_mult) in creation order, src/unet.py:120-154
+_BLOCKS = (
+    ("enc1", None, 1, 0.0),
+    ("enc2", 1, 2, 0.5),
+    ("enc3", 2, 4, 1.0),
+    ("enc4", 4, 8, 1.0),
+    ("bottleneck", 8, 8, 1.0),
+    ("dec4", 16, 8, 1.0),
+    ("dec3", 8, 4, 0.5),
+    ("dec2", 4, 2, 0.5),
+    ("dec1", 2, 1, 0.0),
+)
+
+
+class _Block(nn.Module):
+    """conv3x3 -> ReLU -> [Dropout2d] -> conv3x3 -> ReLU (src/unet.py:28-42)."""
+
+    def __init__(self, cin: int, cout: int, p: float):
+        super().__init__()
+        act = nn.ReLU(inplace=True)
+        seq: List[nn.Module] = [nn.Conv2d(cin, cout, 3, padding=1), act]
+        if p > 0:
+            seq.append(nn.Dropout2d(p))
+        seq += [nn.Conv2d(cout, cout, 3, padding=1), act]
+        self.conv = nn.Sequential(*seq)
+        self.p = p
+
+    @property
+    def conv0(self) -> nn.Conv2d:
+        return self.conv[0]
+
+    @property
+    def conv1(self) -> nn.Conv2d:
+        return self.conv[3] if self.p > 0 else self.conv[2]
+
+
+class UNetRef(nn.Module):
+    """Restatement of ``UNet(in,out,base,dropout)`` (src/unet.py:108-167)."""
+
+    def __init__(self, in_channels: int = 1, out_channels: int = 1, base_channels: int = 64,
+                 dropout: float = 0.2):
+        super().__init__()
+        c = base_channels
+        specs = {name: (cm, om, dm) for name, cm, om, dm in _BLOCKS}
+        # creation order (RNG order) = enc1, enc2, enc3, enc4, bottleneck,
+        # up4, dec4, up3, dec3, up2, dec2, up1, dec1, out_conv
+        def blk(name):
+            cm, om, dm = specs[name]
+            cin = in_channels if cm is None else cm * c
+            return _Block(cin, om * c, dropout * dm)
+        self.enc1 = blk("enc1")
+        self.enc2 = blk("enc2")
+        self.enc3 = blk("enc3")
+        self.enc4 = blk("enc4")
+        self.pool = nn.MaxPool2d(2, 2)
+        self.bottleneck = blk("bottleneck")
+        self.up4 = nn.ConvTranspose2d(8 * c, 8 * c, 2, stride=2)
+        self.dec4 = blk("dec4")
+        self.up3 = nn.ConvTranspose2d(8 * c, 4 * c, 2, stride=2)
+        self.dec3 = blk("dec3")
+        self.up2 = nn.ConvTranspose2d(4 * c, 2 * c, 2, stride=2)
+        self.dec2 = blk("dec2")
+        self.up1 = nn.ConvTranspose2d(2 * c, c, 2, stride=2)
+        self.dec1 = blk("dec1")
+        self.out_conv = nn.Conv2d(c, out_channels, 1)
+
+    def block_names(self) -> Sequence[str]:
+        return [b[0] for b in _BLOCKS]
+
+    def forward(self, x: torch.Tensor, drop_scales: Optional[Dict[str, torch.Tensor]] = None,
+                return_logits: bool = False):
+        return unet_forward(self, x, drop_scales, return_logits)
+
+
+def _block_forward(blk: _Block, x: torch.Tensor, scale: Optional[torch.Tensor], training: bool):
+    y = F.relu(F.conv2d(x, blk.conv0.weight, blk.conv0.bias, padding=1))
+    if blk.p > 0:
+        if scale is not None:  # injected Dropout2d keep-scale (B, C): 0 or 1/(1-p)
+            y = y * scale[:, :, None, None].to(y.dtype)
+        elif training:
+            y = F.dropout2d(y, blk.p, True)
+    return F.relu(F.conv2d(y, blk.conv1.weight, blk.conv1.bias, padding=1))
+
+
+def unet_forward(m: UNetRef, x: torch.Tensor, drop_scales=None, return_logits=False):
+    """src/unet.py:169-216; concat order is [upsampled, skip] (:190-202)."""
+    s = drop_scales or {}
+    tr = m.training
+    e1 = _block_forward(m.enc1, x, s.get("enc1"), tr)
+    e2 = _block_forward(m.enc2, F.max_pool2d(e1, 2, 2), s.get("enc2"), tr)
+    e3 = _block_forward(m.enc3, F.max_pool2d(e2, 2, 2), s.get("enc3"), tr)
+    e4 = _block_forward(m.enc4, F.max_pool2d(e3, 2, 2), s.get("enc4"), tr)
+    bn = _block_forward(m.bottleneck, F.max_pool2d(e4, 2, 2), s.get("bottleneck"), tr)
+    d = bn
+    for up, dec, skip, name in ((m.up4, m.dec4, e4, "dec4"), (m.up3, m.dec3, e3, "dec3"),
+                                (m.up2, m.dec2, e2, "dec2"), (m.up1, m.dec1, e1, "dec1")):
+        u = F.conv_transpose2d(d, up.weight, up.bias, stride=2)
+        d = _block_forward(dec, torch.cat([u, skip], dim=1), s.get(name), tr)
+    z = F.conv2d(d, m.out_conv.weight, m.out_conv.bias)
+    p = torch.sigmoid(z)
+    return (p, z) if return_logits else p
+
+
+def make_drop_scales(m: UNetRef, B: int, generator: torch.Generator) -> Dict[str, torch.Tensor]:
+    """Dropout2d keep-scales per block: bernoulli(1-p)/(1-p) of shape (B, C)
+    (same draw ATen's feature_dropout makes: noise (B,C,1,1).bernoulli_(1-p).div_(1-p))."""
+    out = {}
+    for name in m.block_names():
+        blk = getattr(m, name)
+        if blk.p > 0:
+            C = blk.conv0.out_channels
+            keep = torch.bernoulli(torch.full((B, C), 1.0 - blk.p), generator=generator)
+            out[name] = keep / (1.0 - blk.p)
+    return out
+
+
+def count_parameters(m: nn.Module) -> int:
+    return sum(p.numel() for p in m.parameters() if p.requires_grad)
+
+
+# ---------------------------------------------------------------------------
+# PDE terms — src/pde.py:24-212 (reflect pad + cross-correlation stencils)
+# ---------------------------------------------------------------------------
+
+_LAP = torch.tensor([[0.0, 1.0, 0.0], [1.0, -4.0, 1.0], [0.0, 1.0, 0.0]])
+_GX = torch.tensor([[0.0, 0.0, 0.0], [-0.5, 0.0, 0.5], [0.0, 0.0, 0.0]])
+_GY = torch.tensor([[0.0, -0.5, 0.0], [0.0, 0.0, 0.0], [0.0, 0.5, 0.0]])
+
+
+def _stencil(u: torch.Tensor, k: torch.Tensor) -> torch.Tensor:
+    up = F.pad(u, (1, 1, 1, 1), mode="reflect")  # src/pde.py:67,164
+    return F.conv2d(up, k.to(u.dtype)[None, None], padding=0)
+
+
+def laplacian(u):  # src/pde.py:49-79
+    return _stencil(u, _LAP)
+
+
+def reaction(u, a):  # src/pde.py:81-99
+    return u * (1.0 - u) * (u - a)
+
+
+def rd_residual(u, D, a):  # src/pde.py:101-122
+    return D * laplacian(u) + reaction(u, a)
+
+
+def rd_loss(u, D, a):  # src/pde.py:124-145
+    return torch.mean(rd_residual(u, D, a) ** 2)
+
+
+def grad_mag_sq(u):  # src/pde.py:147-178
+    return _stencil(u, _GX) ** 2 + _stencil(u, _GY) ** 2
+
+
+def pf_loss(u, eps):  # src/pde.py:180-212
+    return torch.mean((eps / 2.0) * grad_mag_sq(u) + (1.0 / eps) * (u ** 2) * ((1.0 - u) ** 2))
+
+
+# ---------------------------------------------------------------------------
+# Losses — src/loss.py:36-68 (DiceBCELoss) and :114-162 (DiceBCEPDELoss)
+# ---------------------------------------------------------------------------
+
+
+def dice_loss(p, t, smooth=1e-6):  # src/loss.py:51-60 (whole-batch ratio)
+    pf, tf = p.reshape(-1), t.reshape(-1)
+    return 1 - (2.0 * (pf * tf).sum() + smooth) / (pf.sum() + tf.sum() + smooth)
+
+
+def bce_loss(p, t):  # nn.BCELoss() mean, log clamped at -100
+    return F.binary_cross_entropy(p, t)
+
+
+def loss_terms(p, t, dice_w=0.5, bce_w=0.5, rd_w=0.0, pf_w=0.0, smooth=1e-6, D=1.0, a=0.5, eps=0.05):
+    """Per-term dict + total, gating identical to src/loss.py:144-160."""
+    ld = dice_loss(p, t, smooth)
+    lb = bce_loss(p, t)
+    total = dice_w * ld + bce_w * lb
+    out = {"dice_loss": ld, "bce_loss": lb}
+    if rd_w > 0:
+        out["pde_loss"] = rd_loss(p, D, a)
+        total = total + rd_w * out["pde_loss"]
+    if pf_w > 0:
+        out["phase_field_loss"] = pf_loss(p, eps)
+        total = total + pf_w * out["phase_field_loss"]
+    out["loss"] = total
+    return out
+
+
+# ---------------------------------------------------------------------------
+# Metrics — src/metrics.py:4-73 (Dice), src/evaluate.py:26-97 (IoU)
+# ---------------------------------------------------------------------------
+
+
+def dice_score(p, t, thr=0.5, smooth=1e-6):
+    pb = (p > thr).float().reshape(-1)
+    tf = t.reshape(-1)
+    return (2.0 * (pb * tf).sum() + smooth) / (pb.sum() + tf.sum() + smooth)
+
+
+def dice_score_batch(p, t, thr=0.5, smooth=1e-6):
+    return torch.stack([dice_score(p[i], t[i], thr, smooth) for i in range(p.shape[0])])
+
+
+def iou(p, t, thr=0.5, smooth=1e-6):
+    pb = (p > thr).float().reshape(-1)
+    tf = t.reshape(-1)
+    inter = (pb * tf).sum()
+    return (inter + smooth) / (pb.sum() + tf.sum() - inter + smooth)
+
+
+def iou_batch(p, t, thr=0.5, smooth=1e-6):
+    return torch.stack([iou(p[i], t[i], thr, smooth) for i in range(p.shape[0])])
+
+
+# ---------------------------------------------------------------------------
+# One training step — src/train.py:108-167 (zero_grad, fwd, loss, bwd, AdamW)
+# ---------------------------------------------------------------------------
+
+
+def make_adamw(m: nn.Module, lr: float, weight_decay: float = 1e-5):
+    """src/train.py:658-662 / :722-726."""
+    return torch.optim.AdamW(m.parameters(), lr=lr, weight_decay=weight_decay)
+
+
+def train_step(m: UNetRef, opt, x, t, loss_kw: dict, drop_scales=None):
+    m.train()
+    opt.zero_grad()
+    p = m(x, drop_scales)
+    terms = loss_terms(p, t, **loss_kw)
+    terms["loss"].backward()
+    opt.step()
+    return p.detach(), {k: float(v) for k, v in terms.items()}

@@ -1,0 +1,60 @@
+// Shared helpers for the gfx950 kernels behind the pis_* C-ABI.
+// Conventions (include/pis_capi.h): every entry point returns 0 or a negative
+// code, never throws, never allocates, never synchronises; it launches on the
+// caller's stream. pis_last_error() returns the last message of this thread.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+
+#include "../../include/pis_capi.h"
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+namespace pis {
+
+void set_error(const char* fmt, ...);
+
+inline int launch_status(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    set_error("%s: %s", what, hipGetErrorString(e));
+    return PIS_ERR_LAUNCH;
+  }
+  return PIS_OK;
+}
+
+inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// Bijective XCD-aware remap (cdna_hip_programming.md §5 'XCD swizzle must be
+// bijective'): blocks dealt round-robin over 8 XCDs get consecutive logical
+// ids per XCD, so neighbouring tiles share an L2.
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int q = nwg / 8, r = nwg % 8;
+  const int xcd = bid % 8, loc = bid / 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+}  // namespace pis
+
+#define PIS_CHECK_ARG(cond, ...)      \
+  do {                                \
+    if (!(cond)) {                    \
+      pis::set_error(__VA_ARGS__);    \
+      return PIS_ERR_ARG;             \
+    }                                 \
+  } while (0)
