@@ -1,0 +1,159 @@
+/*
+ * pis_capi.h — C-ABI of the MI355X (gfx950) training-step kernels for the
+ * PDE-constrained U-Net (seemapoudel58/Physics_informed_image_segmentation).
+ *
+ * The reference is pure Python/PyTorch: its "operator API" is the module
+ * surface of src/unet.py, src/pde.py, src/loss.py, src/metrics.py and the step
+ * loop of src/train.py. Every entry point below replaces the ATen op(s) the
+ * reference reaches at the cited line; the Python mirror of the reference
+ * interface (physics_informed_image_segmentation_amd/) binds them with ctypes
+ * (INTEGRATION.md).
+ *
+ * Conventions
+ *  - Activations are pixel-major NHWC fp32. "ld*" is the channel stride of a
+ *    tensor (elements between consecutive pixels), so a producer can write
+ *    straight into a channel slice of a concat buffer (src/unet.py:190-202).
+ *  - Conv weights are KRSC ([Cout][3][3][Cin]) = the physical layout of an
+ *    OIHW channels_last parameter; ConvTranspose weights are stored
+ *    [2][2][Cout][Cin] (logical (Cin, Cout, 2, 2), state_dict compatible).
+ *  - The caller owns every buffer (workspace included); nothing allocates,
+ *    nothing synchronises; kernels are launched on `stream` (a hipStream_t).
+ *  - Return 0 on success, a negative PIS_ERR_* otherwise; the message is in
+ *    pis_last_error() (thread-local). No C++ exception crosses the ABI.
+ */
+#ifndef PIS_CAPI_H
+#define PIS_CAPI_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* pis_stream_t; /* hipStream_t */
+
+#define PIS_OK 0
+#define PIS_ERR_ARG (-1)
+#define PIS_ERR_LAUNCH (-2)
+#define PIS_ERR_WORKSPACE (-3)
+
+/* epilogue / behaviour flags */
+#define PIS_RELU 1       /* y = max(y, 0)                                     */
+#define PIS_SCALE 2      /* y *= scale[b*C + c]  (Dropout2d keep-scale)       */
+#define PIS_MASK 4       /* y *= (mask[pix*ldm + c] > 0)  (ReLU backward)     */
+#define PIS_ACCUMULATE 8 /* dst += result instead of dst = result             */
+
+const char* pis_last_error(void);
+int pis_version(void);
+
+/* ---- 3x3 convolution, padding 1, stride 1 (src/unet.py:29,38 nn.Conv2d) ----
+ * fwd:  y[p][n] = epi(bias[n] + sum_{r,s,c} x[p+(r-1,s-1)][c] * w[n][r][s][c])
+ *       flags: PIS_RELU, PIS_SCALE (scale is [B][Cout]).   Cin==1 or Cin%4==0. */
+int pis_conv3x3_fwd(const float* x, int ldx, const float* w_krsc, const float* bias,
+                    const float* scale, float* y, int ldy, int B, int H, int W, int Cin,
+                    int Cout, int flags, pis_stream_t stream);
+/* w_flip[c][r][s][n] = w[n][2-r][2-s][c]  (dgrad operand, rebuilt each step) */
+int pis_conv3x3_flip(const float* w_krsc, float* w_flip, int Cin, int Cout, pis_stream_t stream);
+/* dgrad: dx[p][c] = epi(sum_{r,s,n} dz[p+(r-1,s-1)][n] * w_flip[c][r][s][n])
+ *        flags: PIS_MASK (mask = this conv's input x), PIS_SCALE ([B][Cin]). */
+int pis_conv3x3_dgrad(const float* dz, int ldz, const float* w_flip, const float* mask, int ldm,
+                      const float* scale, float* dx, int lddx, int B, int H, int W, int Cin,
+                      int Cout, int flags, pis_stream_t stream);
+/* wgrad: dw[n][r][s][c] (+)= sum_p dz[p][n] x[p+(r-1,s-1)][c];  db[n] (+)= sum_p dz[p][n]
+ *        (db may be NULL). flags: PIS_ACCUMULATE. */
+size_t pis_conv3x3_wgrad_ws(int B, int H, int W, int Cin, int Cout);
+int pis_conv3x3_wgrad(const float* x, int ldx, const float* dz, int ldz, float* dw_krsc, float* db,
+                      int B, int H, int W, int Cin, int Cout, int flags, void* ws, size_t ws_bytes,
+                      pis_stream_t stream);
+
+/* ---- 2x2 stride-2 transposed convolution (src/unet.py:132-153) ----
+ * H, W are the INPUT resolution; the output is 2H x 2W.
+ * fwd: y[(2h+i,2w+j)][o] = bias[o] + sum_c x[(h,w)][c] * w[i][j][o][c]          */
+int pis_convt2x2_fwd(const float* x, int ldx, const float* w_ijoc, const float* bias, float* y,
+                     int ldy, int B, int H, int W, int Cin, int Cout, pis_stream_t stream);
+/* w_cijo[c][i][j][o] = w_ijoc[i][j][o][c]  (dgrad operand) */
+int pis_convt2x2_prep(const float* w_ijoc, float* w_cijo, int Cin, int Cout, pis_stream_t stream);
+/* dgrad: dx[(h,w)][c] = epi(sum_{i,j,o} dy[(2h+i,2w+j)][o] * w[i][j][o][c]); flags: PIS_MASK */
+int pis_convt2x2_dgrad(const float* dy, int lddy, const float* w_cijo, const float* mask, int ldm,
+                       float* dx, int lddx, int B, int H, int W, int Cin, int Cout, int flags,
+                       pis_stream_t stream);
+/* wgrad: dw[i][j][o][c] (+)= sum_(h,w) dy[(2h+i,2w+j)][o] x[(h,w)][c]; db[o] (+)= sum dy[.][o] */
+size_t pis_convt2x2_wgrad_ws(int B, int H, int W, int Cin, int Cout);
+int pis_convt2x2_wgrad(const float* x, int ldx, const float* dy, int lddy, float* dw_ijoc,
+                       float* db, int B, int H, int W, int Cin, int Cout, int flags, void* ws,
+                       size_t ws_bytes, pis_stream_t stream);
+
+/* ---- 2x2 max pooling (src/unet.py:126,181-186) ----
+ * H, W are the INPUT resolution. y is contiguous (ld = C).
+ * bwd (fused with the skip-gradient sum and the ReLU backward of the pooled
+ * block's output):  dx[p][c] = (dskip[p][c] + [p = argmax] dy[q][c]) * (x[p][c] > 0)
+ * dskip may be NULL; dx has ld = lddx.                                            */
+int pis_maxpool2x2_fwd(const float* x, int ldx, float* y, int B, int H, int W, int C,
+                       pis_stream_t stream);
+int pis_maxpool2x2_bwd(const float* x, int ldx, const float* dy, const float* dskip, int ldskip,
+                       float* dx, int lddx, int B, int H, int W, int C, pis_stream_t stream);
+
+/* ---- output head: 1x1 conv C->1 + sigmoid (src/unet.py:157,206-210) ----
+ * fwd: z[p] = b + sum_c x[p][c] w[c];  u[p] = 1 / (1 + exp(-z[p]))
+ * bwd: dx[p][c] = dz[p] w[c] (x[p][c] > 0)  (ReLU backward of dec1 fused);
+ *      dw[c] (+)= sum_p dz[p] x[p][c];  db (+)= sum_p dz[p]                       */
+int pis_head_fwd(const float* x, int ldx, const float* w, const float* b, float* z, float* u,
+                 int64_t npix, int C, pis_stream_t stream);
+size_t pis_head_bwd_ws(int64_t npix, int C);
+int pis_head_bwd(const float* x, int ldx, const float* w, const float* dz, float* dx, int lddx,
+                 float* dw, float* db, int64_t npix, int C, int flags, void* ws, size_t ws_bytes,
+                 pis_stream_t stream);
+
+/* ---- fused Dice + BCE + reaction-diffusion + phase-field loss ----
+ * src/loss.py:114-162, src/pde.py:49-212, src/metrics.py:38-73, src/evaluate.py:62-97.
+ * p, t: (B, H, W) fp32 (C = 1). Terms are whole-batch means (src/loss.py:130-143). */
+typedef struct pis_loss_params {
+  float dice_w, bce_w;   /* src/loss.py:144-147                        */
+  float rd_w, pf_w;      /* lambda_RD, lambda_PF; a term enters the total only if > 0 */
+  float smooth;          /* Dice smoothing (1e-6)                      */
+  float D, a;            /* diffusion coefficient, reaction threshold   */
+  float eps;             /* phase-field interface width                */
+  float thr;             /* metric threshold (0.5, strict '>')         */
+  int flags;             /* PIS_LOSS_ALL_TERMS: compute RD/PF even at weight 0 */
+} pis_loss_params;
+#define PIS_LOSS_ALL_TERMS 1
+#define PIS_LOSS_CHAIN_SIGMOID 2 /* bwd writes dL/dz = dL/dp * p (1 - p) */
+/* out_terms: [0] total [1] dice_loss [2] bce_loss [3] rd_loss [4] pf_loss [5] I=sum p t
+ *            [6] P=sum p [7] T=sum t.
+ * counts: [B][3] = exact (I_hat, P_hat, T) of the thresholded prediction per sample.
+ * scores: [B][2] = (Dice, IoU) per sample (src/metrics.py:67-70, src/evaluate.py:91-94). */
+#define PIS_LOSS_NTERMS 8
+size_t pis_loss_ws(int B, int H, int W);
+int pis_loss_fwd(const float* p, const float* t, int B, int H, int W, const pis_loss_params* prm,
+                 float* out_terms, int* counts, float* scores, void* ws, size_t ws_bytes,
+                 pis_stream_t stream);
+/* dst = grad_out * dL/dp (or dL/dz with PIS_LOSS_CHAIN_SIGMOID); grad_out is a device
+ * scalar (NULL = 1).  terms = out_terms of the forward on the same p, t.          */
+int pis_loss_bwd(const float* p, const float* t, int B, int H, int W, const pis_loss_params* prm,
+                 const float* terms, const float* grad_out, float* dst, int flags,
+                 pis_stream_t stream);
+
+/* Per-pixel PDE fields of src/pde.py (forward only; any output may be NULL):
+ * lap = Lap(u) (:49-79), residual = D Lap(u) + u(1-u)(u-a) (:101-122),
+ * gradmag2 = gx^2 + gy^2 (:147-178), all on reflect-padded stencils.           */
+int pis_pde_fields(const float* u, int B, int H, int W, float D, float a, float* lap,
+                   float* residual, float* gradmag2, pis_stream_t stream);
+
+/* ---- decoupled AdamW over one flat parameter arena (src/train.py:658-662) ----
+ * torch.optim.AdamW single-tensor semantics (torch/optim/adam.py):
+ *   p *= 1 - lr*wd;  m += (1-b1)(g' - m);  v = b2 v + (1-b2) g'^2;
+ *   p -= step_size * m / (sqrt(v)/bc2_sqrt + eps)     with g' = g * grad_scale.   */
+int pis_adamw_step(float* p, const float* g, float* m, float* v, int64_t n, double lr, double beta1,
+                   double beta2, double eps, double weight_decay, double step_size, double bc2_sqrt,
+                   double grad_scale, pis_stream_t stream);
+
+/* ---- channel sums (bias gradients): out[c] (+)= sum_p src[p*ld + c] ---- */
+size_t pis_colsum_ws(int64_t npix, int C);
+int pis_colsum(const float* src, int ld, int64_t npix, int C, float* out, int flags, void* ws,
+               size_t ws_bytes, pis_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PIS_CAPI_H */

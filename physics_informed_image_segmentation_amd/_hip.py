@@ -1,0 +1,108 @@
+"""ctypes binding of the gfx950 C-ABI (include/pis_capi.h).
+
+This is the only door to the kernels: there is no CPU or eager-PyTorch
+fallback. If ``_lib/libpis.so`` is missing (not built) or no GPU is visible,
+every call raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import c_double, c_float, c_int, c_int64, c_size_t, c_void_p
+from typing import Optional
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "_lib", "libpis.so")
+
+PIS_RELU, PIS_SCALE, PIS_MASK, PIS_ACCUMULATE = 1, 2, 4, 8
+PIS_LOSS_ALL_TERMS, PIS_LOSS_CHAIN_SIGMOID = 1, 2
+LOSS_NTERMS = 8
+TERM_TOTAL, TERM_DICE, TERM_BCE, TERM_RD, TERM_PF, TERM_I, TERM_P, TERM_T = range(8)
+
+
+class LossParams(ctypes.Structure):
+    _fields_ = [("dice_w", c_float), ("bce_w", c_float), ("rd_w", c_float), ("pf_w", c_float),
+                ("smooth", c_float), ("D", c_float), ("a", c_float), ("eps", c_float),
+                ("thr", c_float), ("flags", c_int)]
+
+
+P, I, L, Z, Dbl = c_void_p, c_int, c_int64, c_size_t, c_double
+_SIGNATURES = {
+    "pis_version": ([], c_int),
+    "pis_last_error": ([], ctypes.c_char_p),
+    "pis_conv3x3_fwd": ([P, I, P, P, P, P, I, I, I, I, I, I, I, P], c_int),
+    "pis_conv3x3_flip": ([P, P, I, I, P], c_int),
+    "pis_conv3x3_dgrad": ([P, I, P, P, I, P, P, I, I, I, I, I, I, I, P], c_int),
+    "pis_conv3x3_wgrad_ws": ([I, I, I, I, I], c_size_t),
+    "pis_conv3x3_wgrad": ([P, I, P, I, P, P, I, I, I, I, I, I, P, Z, P], c_int),
+    "pis_convt2x2_fwd": ([P, I, P, P, P, I, I, I, I, I, I, P], c_int),
+    "pis_convt2x2_prep": ([P, P, I, I, P], c_int),
+    "pis_convt2x2_dgrad": ([P, I, P, P, I, P, I, I, I, I, I, I, I, P], c_int),
+    "pis_convt2x2_wgrad_ws": ([I, I, I, I, I], c_size_t),
+    "pis_convt2x2_wgrad": ([P, I, P, I, P, P, I, I, I, I, I, I, P, Z, P], c_int),
+    "pis_maxpool2x2_fwd": ([P, I, P, I, I, I, I, P], c_int),
+    "pis_maxpool2x2_bwd": ([P, I, P, P, I, P, I, I, I, I, I, P], c_int),
+    "pis_head_fwd": ([P, I, P, P, P, P, L, I, P], c_int),
+    "pis_head_bwd_ws": ([L, I], c_size_t),
+    "pis_head_bwd": ([P, I, P, P, P, I, P, P, L, I, I, P, Z, P], c_int),
+    "pis_loss_ws": ([I, I, I], c_size_t),
+    "pis_loss_fwd": ([P, P, I, I, I, ctypes.POINTER(LossParams), P, P, P, P, Z, P], c_int),
+    "pis_loss_bwd": ([P, P, I, I, I, ctypes.POINTER(LossParams), P, P, P, I, P], c_int),
+    "pis_adamw_step": ([P, P, P, P, L, Dbl, Dbl, Dbl, Dbl, Dbl, Dbl, Dbl, Dbl, P], c_int),
+    "pis_colsum_ws": ([L, I], c_size_t),
+    "pis_colsum": ([P, I, L, I, P, I, P, Z, P], c_int),
+    "pis_pde_fields": ([P, I, I, I, c_float, c_float, P, P, P, P], c_int),
+}
+
+_lib: Optional[ctypes.CDLL] = None
+
+
+class HipError(RuntimeError):
+    pass
+
+
+def lib() -> ctypes.CDLL:
+    """Load (once) and return the kernel library. Raises if it is missing."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise HipError(f"HIP extension not built: {LIB_PATH} is missing "
+                           "(run __graft_entry__.build() or `python -m physics_informed_image_segmentation_amd.build`)")
+        import torch  # noqa: F401  (torch's libamdhip64.so.7 must be the runtime we bind to)
+        so = ctypes.CDLL(LIB_PATH)
+        for name, (argtypes, restype) in _SIGNATURES.items():
+            fn = getattr(so, name)
+            fn.argtypes = argtypes
+            fn.restype = restype
+        _lib = so
+    return _lib
+
+
+def exported_symbols():
+    return list(_SIGNATURES)
+
+
+def ptr(t: Optional[torch.Tensor]) -> int:
+    return 0 if t is None else t.data_ptr()
+
+
+def stream_handle(device: Optional[torch.device] = None) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = lib().pis_last_error()
+        raise HipError(f"{what} failed ({rc}): {msg.decode() if msg else ''}")
+
+
+def call(name: str, *args) -> None:
+    check(getattr(lib(), name)(*args), name)
+
+
+def require_cuda(t: torch.Tensor, what: str) -> None:
+    if not t.is_cuda:
+        raise HipError(f"{what}: the MI355X path needs a GPU tensor (got {t.device}); "
+                       "this build has no CPU fallback")

@@ -1,0 +1,374 @@
+// Implicit-GEMM fp32 MFMA kernels (gfx950, v_mfma_f32_32x32x2_f32) for the
+// U-Net contractions of src/unet.py: 3x3 conv forward / input-gradient and
+// 2x2-stride-2 transposed-conv forward / input-gradient.
+//
+//   C[m][n] = sum_k A[m][k] * Bt[n][k]      m = output pixel (NHWC row),
+//                                            n = output channel,
+//                                            k = (tap, source channel)
+//
+// A is gathered on the fly from an NHWC source (zero padding outside the
+// image), Bt is the K-contiguous weight operand. Tiles are staged through LDS
+// (register-staged double buffer, one barrier per K-step) and read back as
+// 16-byte rows: lane (i, h) of a wave supplies A[i][k] for k = 8g + 4h + t,
+// t = 0..3, i.e. one ds_read_b128 feeds four MFMAs (the k-permutation is
+// applied identically to A and Bt, so the sum is unchanged).
+#include "common.h"
+
+namespace pis {
+
+enum TapMode { TAP_CONV3 = 0, TAP_UP2 = 1, TAP_ONE = 2 };
+enum EpiMode { EPI_NHWC = 0, EPI_SCATTER2 = 1 };
+
+struct IGemmArgs {
+  const float* src;  // NHWC source
+  int lds;           // channel stride of src
+  int Hs, Ws;        // source spatial dims
+  int H, W;          // output pixel grid
+  int M;             // B*H*W
+  int Csrc;          // channels read per tap
+  int ntaps;
+  int tap_mode;
+  const float* wt;   // Bt[N][ntaps*Csrc]
+  int ldw;
+  int N;
+  // epilogue
+  int epi;
+  const float* bias;
+  const float* scale;  // [B][N]
+  const float* mask;   // [M][ldm]
+  int ldm;
+  float* dst;
+  int ldd;
+  int flags;
+  int cout_t;          // EPI_SCATTER2: n = (i*2+j)*cout_t + o
+};
+
+__device__ __forceinline__ void tap_offset(int mode, int t, int& dr, int& ds, int& st) {
+  if (mode == TAP_CONV3) { dr = t / 3 - 1; ds = t % 3 - 1; st = 1; }
+  else if (mode == TAP_UP2) { dr = t >> 1; ds = t & 1; st = 2; }
+  else { dr = 0; ds = 0; st = 1; }
+}
+
+template <int BM, int BN>
+__global__ __launch_bounds__(256) void igemm_f32_kernel(IGemmArgs g) {
+  constexpr int BK = 16, LDS_ROW = BK + 4;  // 80-byte rows: conflict-free ds_read_b128
+  constexpr int TM = BM / 64, TN = BN / 64;  // 32x32 tiles per wave (2x2 waves)
+  constexpr int AL = BM / 64, BL = BN / 64;  // float4 staging loads per thread
+  __shared__ __attribute__((aligned(16))) float sA[2][BM * LDS_ROW];
+  __shared__ __attribute__((aligned(16))) float sB[2][BN * LDS_ROW];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave & 1, wn = wave >> 1;
+  const int ntn = (g.N + BN - 1) / BN;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int m0 = (bid / ntn) * BM, n0 = (bid % ntn) * BN;
+
+  // per-thread staging rows (fixed over the K loop)
+  int a_b[AL], a_h[AL], a_w[AL];
+  bool a_ok[AL];
+  const int HW = g.H * g.W;
+#pragma unroll
+  for (int i = 0; i < AL; ++i) {
+    const int row = (tid + i * 256) >> 2;
+    const int m = m0 + row;
+    a_ok[i] = m < g.M;
+    const int mm = a_ok[i] ? m : 0;
+    a_b[i] = mm / HW;
+    const int rem = mm - a_b[i] * HW;
+    a_h[i] = rem / g.W;
+    a_w[i] = rem - a_h[i] * g.W;
+  }
+  const int q4 = (tid & 3) * 4;  // channel offset inside the BK chunk
+
+  const int nchunks = (g.Csrc + BK - 1) / BK;
+  const int KT = g.ntaps * nchunks;
+
+  f32x4 ra[AL], rb[BL];
+  auto gload = [&](int kt) {
+    const int tap = kt / nchunks;
+    const int c = (kt - tap * nchunks) * BK + q4;
+    int dr, dsh, st;
+    tap_offset(g.tap_mode, tap, dr, dsh, st);
+    const bool cok = c < g.Csrc;
+#pragma unroll
+    for (int i = 0; i < AL; ++i) {
+      const int hs = a_h[i] * st + dr, ws = a_w[i] * st + dsh;
+      const bool ok = a_ok[i] && cok && hs >= 0 && hs < g.Hs && ws >= 0 && ws < g.Ws;
+      ra[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (ok) {
+        const size_t pix = ((size_t)a_b[i] * g.Hs + hs) * g.Ws + ws;
+        ra[i] = *reinterpret_cast<const f32x4*>(g.src + pix * g.lds + c);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < BL; ++i) {
+      const int n = n0 + ((tid + i * 256) >> 2);
+      rb[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (n < g.N && cok)
+        rb[i] = *reinterpret_cast<const f32x4*>(g.wt + (size_t)n * g.ldw + tap * g.Csrc + c);
+    }
+  };
+  auto lstore = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < AL; ++i) {
+      const int row = (tid + i * 256) >> 2;
+      *reinterpret_cast<f32x4*>(&sA[buf][row * LDS_ROW + q4]) = ra[i];
+    }
+#pragma unroll
+    for (int i = 0; i < BL; ++i) {
+      const int row = (tid + i * 256) >> 2;
+      *reinterpret_cast<f32x4*>(&sB[buf][row * LDS_ROW + q4]) = rb[i];
+    }
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int b = 0; b < TN; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+
+  gload(0);
+  lstore(0);
+  __syncthreads();
+  const int li = lane & 31, lh = lane >> 5;
+  for (int kt = 0; kt < KT; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < KT) gload(kt + 1);
+    const float* As = sA[cur];
+    const float* Bs = sB[cur];
+#pragma unroll
+    for (int gg = 0; gg < BK / 8; ++gg) {
+      f32x4 af[TM], bf[TN];
+#pragma unroll
+      for (int a = 0; a < TM; ++a)
+        af[a] = *reinterpret_cast<const f32x4*>(
+            &As[(wm * (BM / 2) + a * 32 + li) * LDS_ROW + 8 * gg + 4 * lh]);
+#pragma unroll
+      for (int b = 0; b < TN; ++b)
+        bf[b] = *reinterpret_cast<const f32x4*>(
+            &Bs[(wn * (BN / 2) + b * 32 + li) * LDS_ROW + 8 * gg + 4 * lh]);
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int a = 0; a < TM; ++a)
+#pragma unroll
+          for (int b = 0; b < TN; ++b)
+            acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[a][t], bf[b][t], acc[a][b], 0, 0, 0);
+    }
+    if (kt + 1 < KT) lstore(cur ^ 1);
+    __syncthreads();
+  }
+
+  // epilogue: lane owns column n = ... + li, rows i = (r&3) + 8(r>>2) + 4 lh
+#pragma unroll
+  for (int b = 0; b < TN; ++b) {
+    const int n = n0 + wn * (BN / 2) + b * 32 + li;
+    if (n >= g.N) continue;
+    float bias_n = 0.f;
+    int o = n, ij = 0;
+    if (g.epi == EPI_SCATTER2) { ij = n / g.cout_t; o = n - ij * g.cout_t; }
+    if (g.bias) bias_n = g.bias[o];
+#pragma unroll
+    for (int a = 0; a < TM; ++a) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm * (BM / 2) + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        if (m >= g.M) continue;
+        float v = acc[a][b][r] + bias_n;
+        if (g.flags & PIS_RELU) v = fmaxf(v, 0.f);
+        if (g.flags & PIS_MASK) v = (g.mask[(size_t)m * g.ldm + n] > 0.f) ? v : 0.f;
+        if (g.flags & PIS_SCALE) v *= g.scale[(size_t)(m / HW) * g.N + n];
+        size_t off;
+        if (g.epi == EPI_SCATTER2) {
+          const int bb = m / HW, rem = m - bb * HW, h = rem / g.W, w = rem - h * g.W;
+          const int oh = 2 * h + (ij >> 1), ow = 2 * w + (ij & 1);
+          off = (((size_t)bb * 2 * g.H + oh) * (2 * g.W) + ow) * g.ldd + o;
+        } else {
+          off = (size_t)m * g.ldd + n;
+        }
+        if (g.flags & PIS_ACCUMULATE) v += g.dst[off];
+        g.dst[off] = v;
+      }
+    }
+  }
+}
+
+static int launch_igemm(const IGemmArgs& a, hipStream_t s) {
+  // tile choice: BN=64 for narrow outputs, BM=128
+  const int ntm = (int)cdiv(a.M, 128);
+  if (a.N <= 64) {
+    const int grid = ntm * (int)cdiv(a.N, 64);
+    hipLaunchKernelGGL((igemm_f32_kernel<128, 64>), dim3(grid), dim3(256), 0, s, a);
+  } else {
+    const int grid = ntm * (int)cdiv(a.N, 128);
+    hipLaunchKernelGGL((igemm_f32_kernel<128, 128>), dim3(grid), dim3(256), 0, s, a);
+  }
+  return launch_status("igemm_f32");
+}
+
+__global__ void conv3x3_c1_fwd_kernel(const float* __restrict__ x, int ldx,
+                                      const float* __restrict__ w, const float* __restrict__ bias,
+                                      const float* __restrict__ scale, float* __restrict__ y,
+                                      int ldy, int B, int H, int W, int Cout, int flags) {
+  // Cin == 1 (enc1.conv0): 16 lanes per pixel, each lane 4 output channels.
+  extern __shared__ float sw[];  // [9][Cout] + bias
+  for (int i = threadIdx.x; i < 9 * Cout; i += blockDim.x) {
+    const int n = i / 9, t = i - n * 9;
+    sw[t * Cout + n] = w[i];
+  }
+  for (int i = threadIdx.x; i < Cout; i += blockDim.x) sw[9 * Cout + i] = bias ? bias[i] : 0.f;
+  __syncthreads();
+  const int64_t npix = (int64_t)B * H * W;
+  const int lanes_per_pix = Cout / 4;
+  const int64_t gtid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t p = gtid / lanes_per_pix;
+  const int c4 = (int)(gtid - p * lanes_per_pix) * 4;
+  if (p >= npix) return;
+  const int HW = H * W;
+  const int b = (int)(p / HW), rem = (int)(p - (int64_t)b * HW), h = rem / W, wc = rem - h * W;
+  float xv[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {
+    const int hh = h + t / 3 - 1, ww = wc + t % 3 - 1;
+    xv[t] = (hh >= 0 && hh < H && ww >= 0 && ww < W) ? x[((int64_t)b * HW + hh * W + ww) * ldx] : 0.f;
+  }
+  f32x4 acc;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) acc[j] = sw[9 * Cout + c4 + j];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[j] = fmaf(xv[t], sw[t * Cout + c4 + j], acc[j]);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    float v = acc[j];
+    if (flags & PIS_RELU) v = fmaxf(v, 0.f);
+    if (flags & PIS_SCALE) v *= scale[(size_t)b * Cout + c4 + j];
+    acc[j] = v;
+  }
+  *reinterpret_cast<f32x4*>(y + p * ldy + c4) = acc;
+}
+
+__global__ void conv3x3_flip_kernel(const float* __restrict__ w, float* __restrict__ wf, int Cin,
+                                    int Cout) {
+  const int64_t n_el = (int64_t)Cin * 9 * Cout;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_el;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    // destination index i = ((c*3 + r)*3 + s)*Cout + n
+    const int n = (int)(i % Cout);
+    const int64_t rest = i / Cout;
+    const int rs = (int)(rest % 9);
+    const int c = (int)(rest / 9);
+    const int r = rs / 3, s = rs % 3;
+    wf[i] = w[(((int64_t)n * 3 + (2 - r)) * 3 + (2 - s)) * Cin + c];
+  }
+}
+
+__global__ void convt_prep_kernel(const float* __restrict__ w, float* __restrict__ wc, int Cin,
+                                  int Cout) {
+  // w[i][j][o][c] -> wc[c][i][j][o]
+  const int64_t n_el = (int64_t)4 * Cout * Cin;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n_el;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int o = (int)(e % Cout);
+    const int64_t rest = e / Cout;
+    const int ij = (int)(rest % 4);
+    const int c = (int)(rest / 4);
+    wc[e] = w[((int64_t)ij * Cout + o) * Cin + c];
+  }
+}
+
+}  // namespace pis
+
+using namespace pis;
+
+extern "C" int pis_conv3x3_fwd(const float* x, int ldx, const float* w_krsc, const float* bias,
+                               const float* scale, float* y, int ldy, int B, int H, int W, int Cin,
+                               int Cout, int flags, pis_stream_t stream) {
+  PIS_CHECK_ARG(x && w_krsc && y && B > 0 && H > 0 && W > 0 && Cin > 0 && Cout > 0,
+                "pis_conv3x3_fwd: bad arguments");
+  PIS_CHECK_ARG(!(flags & PIS_SCALE) || scale, "pis_conv3x3_fwd: PIS_SCALE without scale");
+  PIS_CHECK_ARG(ldy % 4 == 0 && Cout % 4 == 0, "pis_conv3x3_fwd: ldy/Cout must be multiples of 4");
+  hipStream_t s = (hipStream_t)stream;
+  if (Cin == 1) {
+    PIS_CHECK_ARG(Cout <= 1024, "pis_conv3x3_fwd: Cin==1 path supports Cout<=1024");
+    const int64_t threads = (int64_t)B * H * W * (Cout / 4);
+    hipLaunchKernelGGL(conv3x3_c1_fwd_kernel, dim3((unsigned)cdiv(threads, 256)), dim3(256),
+                       (size_t)10 * Cout * sizeof(float), s, x, ldx, w_krsc, bias, scale, y, ldy, B,
+                       H, W, Cout, flags);
+    return launch_status("conv3x3_c1_fwd");
+  }
+  PIS_CHECK_ARG(Cin % 4 == 0 && ldx % 4 == 0, "pis_conv3x3_fwd: Cin/ldx must be multiples of 4");
+  IGemmArgs a{};
+  a.src = x; a.lds = ldx; a.Hs = H; a.Ws = W; a.H = H; a.W = W; a.M = B * H * W;
+  a.Csrc = Cin; a.ntaps = 9; a.tap_mode = TAP_CONV3; a.wt = w_krsc; a.ldw = 9 * Cin; a.N = Cout;
+  a.epi = EPI_NHWC; a.bias = bias; a.scale = scale; a.dst = y; a.ldd = ldy;
+  a.flags = flags & (PIS_RELU | PIS_SCALE | PIS_ACCUMULATE);
+  return launch_igemm(a, s);
+}
+
+extern "C" int pis_conv3x3_flip(const float* w_krsc, float* w_flip, int Cin, int Cout,
+                                pis_stream_t stream) {
+  PIS_CHECK_ARG(w_krsc && w_flip && Cin > 0 && Cout > 0, "pis_conv3x3_flip: bad arguments");
+  const int64_t n = (int64_t)Cin * 9 * Cout;
+  const int grid = (int)std::min<int64_t>(cdiv(n, 256), 4096);
+  hipLaunchKernelGGL(conv3x3_flip_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, w_krsc,
+                     w_flip, Cin, Cout);
+  return launch_status("conv3x3_flip");
+}
+
+extern "C" int pis_conv3x3_dgrad(const float* dz, int ldz, const float* w_flip, const float* mask,
+                                 int ldm, const float* scale, float* dx, int lddx, int B, int H,
+                                 int W, int Cin, int Cout, int flags, pis_stream_t stream) {
+  PIS_CHECK_ARG(dz && w_flip && dx && B > 0 && H > 0 && W > 0 && Cin > 0 && Cout > 0,
+                "pis_conv3x3_dgrad: bad arguments");
+  PIS_CHECK_ARG(Cout % 4 == 0 && ldz % 4 == 0, "pis_conv3x3_dgrad: Cout/ldz must be multiples of 4");
+  PIS_CHECK_ARG(!(flags & PIS_MASK) || mask, "pis_conv3x3_dgrad: PIS_MASK without mask");
+  PIS_CHECK_ARG(!(flags & PIS_SCALE) || scale, "pis_conv3x3_dgrad: PIS_SCALE without scale");
+  IGemmArgs a{};
+  a.src = dz; a.lds = ldz; a.Hs = H; a.Ws = W; a.H = H; a.W = W; a.M = B * H * W;
+  a.Csrc = Cout; a.ntaps = 9; a.tap_mode = TAP_CONV3; a.wt = w_flip; a.ldw = 9 * Cout; a.N = Cin;
+  a.epi = EPI_NHWC; a.mask = mask; a.ldm = ldm; a.scale = scale; a.dst = dx; a.ldd = lddx;
+  a.flags = flags & (PIS_MASK | PIS_SCALE | PIS_ACCUMULATE);
+  return launch_igemm(a, (hipStream_t)stream);
+}
+
+extern "C" int pis_convt2x2_fwd(const float* x, int ldx, const float* w_ijoc, const float* bias,
+                                float* y, int ldy, int B, int H, int W, int Cin, int Cout,
+                                pis_stream_t stream) {
+  PIS_CHECK_ARG(x && w_ijoc && y && B > 0 && H > 0 && W > 0 && Cin > 0 && Cout > 0,
+                "pis_convt2x2_fwd: bad arguments");
+  PIS_CHECK_ARG(Cin % 4 == 0 && ldx % 4 == 0, "pis_convt2x2_fwd: Cin/ldx must be multiples of 4");
+  IGemmArgs a{};
+  a.src = x; a.lds = ldx; a.Hs = H; a.Ws = W; a.H = H; a.W = W; a.M = B * H * W;
+  a.Csrc = Cin; a.ntaps = 1; a.tap_mode = TAP_ONE; a.wt = w_ijoc; a.ldw = Cin; a.N = 4 * Cout;
+  a.epi = EPI_SCATTER2; a.cout_t = Cout; a.bias = bias; a.dst = y; a.ldd = ldy; a.flags = 0;
+  return launch_igemm(a, (hipStream_t)stream);
+}
+
+extern "C" int pis_convt2x2_prep(const float* w_ijoc, float* w_cijo, int Cin, int Cout,
+                                 pis_stream_t stream) {
+  PIS_CHECK_ARG(w_ijoc && w_cijo && Cin > 0 && Cout > 0, "pis_convt2x2_prep: bad arguments");
+  const int64_t n = (int64_t)4 * Cin * Cout;
+  const int grid = (int)std::min<int64_t>(cdiv(n, 256), 4096);
+  hipLaunchKernelGGL(convt_prep_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, w_ijoc,
+                     w_cijo, Cin, Cout);
+  return launch_status("convt2x2_prep");
+}
+
+extern "C" int pis_convt2x2_dgrad(const float* dy, int lddy, const float* w_cijo, const float* mask,
+                                  int ldm, float* dx, int lddx, int B, int H, int W, int Cin,
+                                  int Cout, int flags, pis_stream_t stream) {
+  PIS_CHECK_ARG(dy && w_cijo && dx && B > 0 && H > 0 && W > 0 && Cin > 0 && Cout > 0,
+                "pis_convt2x2_dgrad: bad arguments");
+  PIS_CHECK_ARG(Cout % 4 == 0 && lddy % 4 == 0, "pis_convt2x2_dgrad: Cout/lddy must be multiples of 4");
+  PIS_CHECK_ARG(!(flags & PIS_MASK) || mask, "pis_convt2x2_dgrad: PIS_MASK without mask");
+  IGemmArgs a{};
+  a.src = dy; a.lds = lddy; a.Hs = 2 * H; a.Ws = 2 * W; a.H = H; a.W = W; a.M = B * H * W;
+  a.Csrc = Cout; a.ntaps = 4; a.tap_mode = TAP_UP2; a.wt = w_cijo; a.ldw = 4 * Cout; a.N = Cin;
+  a.epi = EPI_NHWC; a.mask = mask; a.ldm = ldm; a.dst = dx; a.ldd = lddx;
+  a.flags = flags & (PIS_MASK | PIS_ACCUMULATE);
+  return launch_igemm(a, (hipStream_t)stream);
+}

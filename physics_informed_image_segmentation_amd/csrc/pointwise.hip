@@ -1,0 +1,267 @@
+// Bandwidth-bound kernels of the step: 2x2 max pooling (src/unet.py:126),
+// the 1x1 output head + sigmoid (src/unet.py:157,206-210) and decoupled AdamW
+// (src/train.py:658-662). NHWC fp32, 16-byte vector accesses.
+#include "common.h"
+
+namespace pis {
+
+__global__ void maxpool_fwd_kernel(const float* __restrict__ x, int ldx, float* __restrict__ y,
+                                   int B, int Ho, int Wo, int C) {
+  const int c4n = C / 4;
+  const int64_t n = (int64_t)B * Ho * Wo * c4n;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int c4 = (int)(e % c4n);
+    const int64_t q = e / c4n;  // pooled pixel
+    const int wo = (int)(q % Wo);
+    const int64_t bh = q / Wo;
+    const int ho = (int)(bh % Ho);
+    const int b = (int)(bh / Ho);
+    const int W = 2 * Wo;
+    const int64_t p00 = ((int64_t)b * 2 * Ho + 2 * ho) * W + 2 * wo;
+    const f32x4 v0 = *reinterpret_cast<const f32x4*>(x + p00 * ldx + 4 * c4);
+    const f32x4 v1 = *reinterpret_cast<const f32x4*>(x + (p00 + 1) * ldx + 4 * c4);
+    const f32x4 v2 = *reinterpret_cast<const f32x4*>(x + (p00 + W) * ldx + 4 * c4);
+    const f32x4 v3 = *reinterpret_cast<const f32x4*>(x + (p00 + W + 1) * ldx + 4 * c4);
+    f32x4 m;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) m[j] = fmaxf(fmaxf(v0[j], v1[j]), fmaxf(v2[j], v3[j]));
+    *reinterpret_cast<f32x4*>(y + q * C + 4 * c4) = m;
+  }
+}
+
+// dx = (dskip + route(dy)) * (x > 0); route = first max in (0,0),(0,1),(1,0),(1,1)
+// order, the tie-break of ATen's max_pool2d_with_indices.
+__global__ void maxpool_bwd_kernel(const float* __restrict__ x, int ldx, const float* __restrict__ dy,
+                                   const float* __restrict__ dskip, int ldskip,
+                                   float* __restrict__ dx, int lddx, int B, int Ho, int Wo, int C) {
+  const int c4n = C / 4;
+  const int64_t n = (int64_t)B * Ho * Wo * c4n;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int c4 = (int)(e % c4n);
+    const int64_t q = e / c4n;
+    const int wo = (int)(q % Wo);
+    const int64_t bh = q / Wo;
+    const int ho = (int)(bh % Ho);
+    const int b = (int)(bh / Ho);
+    const int W = 2 * Wo;
+    const int64_t p00 = ((int64_t)b * 2 * Ho + 2 * ho) * W + 2 * wo;
+    const int64_t pix[4] = {p00, p00 + 1, p00 + W, p00 + W + 1};
+    f32x4 v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = *reinterpret_cast<const f32x4*>(x + pix[k] * ldx + 4 * c4);
+    const f32x4 g = *reinterpret_cast<const f32x4*>(dy + q * C + 4 * c4);
+    int arg[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      int a = 0;
+      float best = v[0][j];
+#pragma unroll
+      for (int k = 1; k < 4; ++k)
+        if (v[k][j] > best) { best = v[k][j]; a = k; }
+      arg[j] = a;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      f32x4 o = dskip ? *reinterpret_cast<const f32x4*>(dskip + pix[k] * ldskip + 4 * c4)
+                      : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (arg[j] == k) o[j] += g[j];
+        o[j] = v[k][j] > 0.f ? o[j] : 0.f;
+      }
+      *reinterpret_cast<f32x4*>(dx + pix[k] * lddx + 4 * c4) = o;
+    }
+  }
+}
+
+// head fwd: 16 lanes per pixel (4 pixels per wave-instruction), float4 each
+__global__ __launch_bounds__(256) void head_fwd_kernel(const float* __restrict__ x, int ldx,
+                                                       const float* __restrict__ w,
+                                                       const float* __restrict__ b,
+                                                       float* __restrict__ z, float* __restrict__ u,
+                                                       int64_t npix, int C) {
+  const int sub = threadIdx.x & 15;
+  const int64_t p = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 4;
+  const bool ok = p < npix;
+  float s = 0.f;
+  if (ok)
+    for (int c = 4 * sub; c < C; c += 64) {
+      const f32x4 xv = *reinterpret_cast<const f32x4*>(x + p * ldx + c);
+      const f32x4 wv = *reinterpret_cast<const f32x4*>(w + c);
+      s = fmaf(xv[0], wv[0], s);
+      s = fmaf(xv[1], wv[1], s);
+      s = fmaf(xv[2], wv[2], s);
+      s = fmaf(xv[3], wv[3], s);
+    }
+#pragma unroll
+  for (int off = 8; off > 0; off >>= 1) s += __shfl_xor(s, off, 16);
+  if (ok && sub == 0) {
+    const float zz = s + b[0];
+    if (z) z[p] = zz;
+    u[p] = 1.f / (1.f + expf(-zz));
+  }
+}
+
+// head bwd: dx[p][c] = dz[p] w[c] (x[p][c] > 0); partial dw[c] per block
+__global__ __launch_bounds__(256) void head_bwd_kernel(const float* __restrict__ x, int ldx,
+                                                       const float* __restrict__ w,
+                                                       const float* __restrict__ dz,
+                                                       float* __restrict__ dx, int lddx,
+                                                       int64_t npix, int C, int64_t pix_per_block,
+                                                       float* __restrict__ part) {
+  // C % 4 == 0, C <= 1024: lane group of C/4 threads covers one pixel
+  const int c4n = C / 4;
+  const int rows = 256 / c4n;
+  const int r = threadIdx.x / c4n, c4 = threadIdx.x - r * c4n;
+  const int64_t p0 = (int64_t)blockIdx.x * pix_per_block;
+  const int64_t p1 = min(npix, p0 + pix_per_block);
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  if (r < rows) {
+    const f32x4 wv = *reinterpret_cast<const f32x4*>(w + 4 * c4);
+    for (int64_t p = p0 + r; p < p1; p += rows) {
+      const float d = dz[p];
+      const f32x4 xv = *reinterpret_cast<const f32x4*>(x + p * ldx + 4 * c4);
+      f32x4 o;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        o[j] = xv[j] > 0.f ? d * wv[j] : 0.f;
+        acc[j] = fmaf(d, xv[j], acc[j]);
+      }
+      *reinterpret_cast<f32x4*>(dx + p * lddx + 4 * c4) = o;
+    }
+  }
+  __shared__ f32x4 red[256];
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  if ((int)threadIdx.x < c4n) {
+    f32x4 t = red[threadIdx.x];
+    for (int k = 1; k < rows; ++k) t += red[k * c4n + threadIdx.x];
+    *reinterpret_cast<f32x4*>(part + (size_t)blockIdx.x * C + 4 * threadIdx.x) = t;
+  }
+}
+
+__global__ void adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
+                             float* __restrict__ m, float* __restrict__ v, int64_t n, float decay,
+                             float omb1, float beta2, float omb2, float eps, float step_size,
+                             float bc2_sqrt, float grad_scale) {
+  const int64_t n4 = n / 4;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4 + (n - n4 * 4);
+       i += (int64_t)gridDim.x * blockDim.x) {
+    if (i < n4) {
+      f32x4 pp = reinterpret_cast<f32x4*>(p)[i];
+      f32x4 gg = reinterpret_cast<const f32x4*>(g)[i];
+      f32x4 mm = reinterpret_cast<f32x4*>(m)[i];
+      f32x4 vv = reinterpret_cast<f32x4*>(v)[i];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float gj = gg[j] * grad_scale;
+        pp[j] = pp[j] * decay;
+        mm[j] = mm[j] + omb1 * (gj - mm[j]);
+        vv[j] = vv[j] * beta2 + omb2 * gj * gj;
+        const float denom = sqrtf(vv[j]) / bc2_sqrt + eps;
+        pp[j] = pp[j] + (-step_size) * (mm[j] / denom);
+      }
+      reinterpret_cast<f32x4*>(p)[i] = pp;
+      reinterpret_cast<f32x4*>(m)[i] = mm;
+      reinterpret_cast<f32x4*>(v)[i] = vv;
+    } else {
+      const int64_t k = n4 * 4 + (i - n4);
+      const float gj = g[k] * grad_scale;
+      float pp = p[k] * decay;
+      const float mm = m[k] + omb1 * (gj - m[k]);
+      const float vv = v[k] * beta2 + omb2 * gj * gj;
+      pp = pp + (-step_size) * (mm / (sqrtf(vv) / bc2_sqrt + eps));
+      p[k] = pp; m[k] = mm; v[k] = vv;
+    }
+  }
+}
+
+int reduce_slabs(const float* part, int splits, int64_t n, float* dst, int accumulate, hipStream_t s);
+int colsum(const float* src, int ld, int64_t npix, int C, float* out, int accumulate, void* ws,
+           size_t ws_bytes, hipStream_t s);
+size_t colsum_ws(int64_t npix, int C);
+
+static int64_t head_pix_per_block(int64_t npix) { return std::max<int64_t>(256, cdiv(npix, 2048)); }
+
+}  // namespace pis
+
+using namespace pis;
+
+static int grid_for(int64_t work) { return (int)std::max<int64_t>(1, std::min<int64_t>(cdiv(work, 256), 8192)); }
+
+extern "C" int pis_maxpool2x2_fwd(const float* x, int ldx, float* y, int B, int H, int W, int C,
+                                  pis_stream_t stream) {
+  PIS_CHECK_ARG(x && y && B > 0 && H >= 2 && W >= 2 && C > 0, "pis_maxpool2x2_fwd: bad arguments");
+  PIS_CHECK_ARG(H % 2 == 0 && W % 2 == 0 && C % 4 == 0 && ldx % 4 == 0,
+                "pis_maxpool2x2_fwd: H, W even and C, ldx multiples of 4 required");
+  const int64_t work = (int64_t)B * (H / 2) * (W / 2) * (C / 4);
+  hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(grid_for(work)), dim3(256), 0, (hipStream_t)stream,
+                     x, ldx, y, B, H / 2, W / 2, C);
+  return launch_status("maxpool2x2_fwd");
+}
+
+extern "C" int pis_maxpool2x2_bwd(const float* x, int ldx, const float* dy, const float* dskip,
+                                  int ldskip, float* dx, int lddx, int B, int H, int W, int C,
+                                  pis_stream_t stream) {
+  PIS_CHECK_ARG(x && dy && dx && B > 0 && H >= 2 && W >= 2 && C > 0, "pis_maxpool2x2_bwd: bad arguments");
+  PIS_CHECK_ARG(H % 2 == 0 && W % 2 == 0 && C % 4 == 0 && ldx % 4 == 0 && lddx % 4 == 0 &&
+                    (!dskip || ldskip % 4 == 0),
+                "pis_maxpool2x2_bwd: H, W even and C, ld multiples of 4 required");
+  const int64_t work = (int64_t)B * (H / 2) * (W / 2) * (C / 4);
+  hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(grid_for(work)), dim3(256), 0, (hipStream_t)stream,
+                     x, ldx, dy, dskip, ldskip, dx, lddx, B, H / 2, W / 2, C);
+  return launch_status("maxpool2x2_bwd");
+}
+
+extern "C" int pis_head_fwd(const float* x, int ldx, const float* w, const float* b, float* z,
+                            float* u, int64_t npix, int C, pis_stream_t stream) {
+  PIS_CHECK_ARG(x && w && b && u && npix > 0 && C > 0 && C % 4 == 0 && ldx % 4 == 0,
+                "pis_head_fwd: bad arguments");
+  hipLaunchKernelGGL(head_fwd_kernel, dim3((unsigned)cdiv(npix * 16, 256)), dim3(256), 0,
+                     (hipStream_t)stream, x, ldx, w, b, z, u, npix, C);
+  return launch_status("head_fwd");
+}
+
+extern "C" size_t pis_head_bwd_ws(int64_t npix, int C) {
+  const int64_t blocks = cdiv(npix, head_pix_per_block(npix));
+  return std::max<size_t>((size_t)blocks * C * sizeof(float), colsum_ws(npix, 1)) + 256;
+}
+
+extern "C" int pis_head_bwd(const float* x, int ldx, const float* w, const float* dz, float* dx,
+                            int lddx, float* dw, float* db, int64_t npix, int C, int flags,
+                            void* ws, size_t ws_bytes, pis_stream_t stream) {
+  PIS_CHECK_ARG(x && w && dz && dx && dw && npix > 0 && C % 4 == 0 && C / 4 <= 256 &&
+                    ldx % 4 == 0 && lddx % 4 == 0,
+                "pis_head_bwd: bad arguments");
+  PIS_CHECK_ARG(ws_bytes >= pis_head_bwd_ws(npix, C), "pis_head_bwd: workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  const int acc = flags & PIS_ACCUMULATE;
+  const int64_t ppb = head_pix_per_block(npix);
+  const int blocks = (int)cdiv(npix, ppb);
+  hipLaunchKernelGGL(head_bwd_kernel, dim3(blocks), dim3(256), 0, s, x, ldx, w, dz, dx, lddx, npix,
+                     C, ppb, (float*)ws);
+  int rc = launch_status("head_bwd");
+  if (!rc) rc = reduce_slabs((float*)ws, blocks, C, dw, acc, s);
+  if (!rc && db) rc = colsum(dz, 1, npix, 1, db, acc, ws, ws_bytes, s);
+  return rc;
+}
+
+extern "C" int pis_adamw_step(float* p, const float* g, float* m, float* v, int64_t n, double lr,
+                              double beta1, double beta2, double eps, double weight_decay,
+                              double step_size, double bc2_sqrt, double grad_scale,
+                              pis_stream_t stream) {
+  // scalars are rounded to fp32 exactly as torch's single-tensor AdamW rounds its Python floats
+  PIS_CHECK_ARG(p && g && m && v && n >= 0, "pis_adamw_step: bad arguments");
+  PIS_CHECK_ARG(((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) % 16 == 0,
+                "pis_adamw_step: buffers must be 16-byte aligned");
+  if (n == 0) return PIS_OK;
+  const float decay = (float)(1.0 - lr * weight_decay);
+  const float omb1 = (float)(1.0 - beta1);
+  const float omb2 = (float)(1.0 - beta2);
+  hipLaunchKernelGGL(adamw_kernel, dim3(grid_for(n / 4 + 4)), dim3(256), 0, (hipStream_t)stream, p,
+                     g, m, v, n, decay, omb1, (float)beta2, omb2, (float)eps, (float)step_size,
+                     (float)bc2_sqrt, (float)grad_scale);
+  return launch_status("adamw");
+}

@@ -1,0 +1,302 @@
+"""Per-kernel parity through the C-ABI on the GPU, against stock fp32 PyTorch on
+the CPU (the ATen ops the reference calls) and the float64 numpy loss oracle."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from oracle import loss_numpy as ln
+from oracle import reference_torch as rt
+
+pytestmark = pytest.mark.gpu
+
+RELU, SCALE, MASK, ACC = 1, 2, 4, 8
+
+
+def nhwc(t):
+    return t.permute(0, 2, 3, 1).contiguous()
+
+
+def nchw(t):
+    return t.permute(0, 3, 1, 2).contiguous()
+
+
+def rel_err(a, b):
+    a = a.detach().double().cpu()
+    b = b.detach().double().cpu()
+    return ((a - b).norm() / max(b.norm().item(), 1e-30)).item()
+
+
+def krsc(w):  # (O, I, 3, 3) -> [O][3][3][I]
+    return w.permute(0, 2, 3, 1).contiguous()
+
+
+def s():
+    return torch.cuda.current_stream().cuda_stream
+
+
+@pytest.mark.parametrize("B,H,W,Cin,Cout,ld_extra", [(2, 16, 24, 64, 64, 0), (1, 8, 8, 128, 256, 64),
+                                                      (3, 5, 7, 64, 128, 0), (2, 16, 16, 1, 64, 0)])
+def test_conv3x3_fwd(hip, B, H, W, Cin, Cout, ld_extra):
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(B, Cin, H, W, generator=g)
+    w = torch.randn(Cout, Cin, 3, 3, generator=g) / (3 * Cin ** 0.5)
+    b = torch.randn(Cout, generator=g)
+    scale = (torch.rand(B, Cout, generator=g) > 0.2).float() / 0.8
+    ref = F.relu(F.conv2d(x, w, b, padding=1)) * scale[:, :, None, None]
+    ldx = Cin + (ld_extra if Cin > 1 else 0)
+    xbuf = torch.zeros(B, H, W, ldx)
+    xbuf[..., :Cin] = nhwc(x)
+    xd = xbuf.cuda()
+    ldy = Cout + ld_extra
+    y = torch.full((B, H, W, ldy), 7.0, device="cuda")
+    wd, bd, sd = krsc(w).cuda(), b.cuda(), scale.cuda()
+    rc = hip.pis_conv3x3_fwd(xd.data_ptr(), ldx, wd.data_ptr(), bd.data_ptr(), sd.data_ptr(), y.data_ptr(), ldy,
+                             B, H, W, Cin, Cout, RELU | SCALE, s())
+    assert rc == 0, hip.pis_last_error()
+    torch.cuda.synchronize()
+    out = nchw(y[..., :Cout].cpu())
+    assert rel_err(out, ref) < 1e-5
+    if ld_extra:
+        assert torch.all(y[..., Cout:] == 7.0)  # untouched channel slice
+
+
+@pytest.mark.parametrize("B,H,W,Cin,Cout", [(2, 16, 24, 64, 64), (1, 8, 8, 256, 128), (2, 6, 10, 128, 64)])
+def test_conv3x3_dgrad_wgrad(hip, B, H, W, Cin, Cout):
+    g = torch.Generator().manual_seed(1)
+    x = F.relu(torch.randn(B, Cin, H, W, generator=g))
+    w = torch.randn(Cout, Cin, 3, 3, generator=g) / (3 * Cin ** 0.5)
+    dz = torch.randn(B, Cout, H, W, generator=g)
+    scale = (torch.rand(B, Cin, generator=g) > 0.2).float() / 0.8
+    dx_ref = torch.nn.grad.conv2d_input(x.shape, w, dz, padding=1) * (x > 0) * scale[:, :, None, None]
+    dw_ref = torch.nn.grad.conv2d_weight(x, w.shape, dz, padding=1)
+    db_ref = dz.sum(dim=(0, 2, 3))
+    xd, dzd, wd, sd = nhwc(x).cuda(), nhwc(dz).cuda(), krsc(w).cuda(), scale.cuda()
+    wf = torch.empty(Cin * 9 * Cout, device="cuda")
+    assert hip.pis_conv3x3_flip(wd.data_ptr(), wf.data_ptr(), Cin, Cout, s()) == 0
+    dx = torch.empty(B, H, W, Cin, device="cuda")
+    rc = hip.pis_conv3x3_dgrad(dzd.data_ptr(), Cout, wf.data_ptr(), xd.data_ptr(), Cin, sd.data_ptr(),
+                               dx.data_ptr(), Cin, B, H, W, Cin, Cout, MASK | SCALE, s())
+    assert rc == 0, hip.pis_last_error()
+    nws = hip.pis_conv3x3_wgrad_ws(B, H, W, Cin, Cout)
+    ws = torch.empty(nws // 4 + 1, device="cuda")
+    dw = torch.empty(Cout, 3, 3, Cin, device="cuda")
+    db = torch.empty(Cout, device="cuda")
+    rc = hip.pis_conv3x3_wgrad(xd.data_ptr(), Cin, dzd.data_ptr(), Cout, dw.data_ptr(), db.data_ptr(),
+                               B, H, W, Cin, Cout, 0, ws.data_ptr(), nws, s())
+    assert rc == 0, hip.pis_last_error()
+    torch.cuda.synchronize()
+    assert rel_err(nchw(dx.cpu()), dx_ref) < 1e-5
+    assert rel_err(dw.cpu().permute(0, 3, 1, 2), dw_ref) < 1e-5
+    assert rel_err(db.cpu(), db_ref) < 1e-5
+    # accumulate mode adds on top
+    rc = hip.pis_conv3x3_wgrad(xd.data_ptr(), Cin, dzd.data_ptr(), Cout, dw.data_ptr(), db.data_ptr(),
+                               B, H, W, Cin, Cout, ACC, ws.data_ptr(), nws, s())
+    torch.cuda.synchronize()
+    assert rel_err(dw.cpu().permute(0, 3, 1, 2), 2 * dw_ref) < 1e-5
+
+
+def test_conv3x3_c1_wgrad(hip):
+    B, H, W, Cout = 2, 32, 16, 64
+    g = torch.Generator().manual_seed(2)
+    x = torch.rand(B, 1, H, W, generator=g)
+    dz = torch.randn(B, Cout, H, W, generator=g)
+    w = torch.zeros(Cout, 1, 3, 3)
+    dw_ref = torch.nn.grad.conv2d_weight(x, w.shape, dz, padding=1)
+    xd, dzd = nhwc(x).cuda(), nhwc(dz).cuda()
+    nws = hip.pis_conv3x3_wgrad_ws(B, H, W, 1, Cout)
+    ws = torch.empty(nws // 4 + 1, device="cuda")
+    dw = torch.empty(Cout, 3, 3, 1, device="cuda")
+    db = torch.empty(Cout, device="cuda")
+    assert hip.pis_conv3x3_wgrad(xd.data_ptr(), 1, dzd.data_ptr(), Cout, dw.data_ptr(), db.data_ptr(),
+                                 B, H, W, 1, Cout, 0, ws.data_ptr(), nws, s()) == 0
+    torch.cuda.synchronize()
+    assert rel_err(dw.cpu().permute(0, 3, 1, 2), dw_ref) < 1e-5
+    assert rel_err(db.cpu(), dz.sum(dim=(0, 2, 3))) < 1e-5
+
+
+@pytest.mark.parametrize("B,H,W,Cin,Cout", [(2, 8, 12, 128, 64), (1, 4, 4, 512, 512), (2, 3, 5, 256, 128)])
+def test_convt2x2(hip, B, H, W, Cin, Cout):
+    g = torch.Generator().manual_seed(3)
+    x = F.relu(torch.randn(B, Cin, H, W, generator=g)).requires_grad_(True)
+    w = (torch.randn(Cin, Cout, 2, 2, generator=g) / Cin ** 0.5).requires_grad_(True)
+    b = torch.randn(Cout, generator=g).requires_grad_(True)
+    y = F.conv_transpose2d(x, w, b, stride=2)
+    dy = torch.randn(y.shape, generator=g)
+    y.backward(dy)
+    w_ijoc = w.detach().permute(2, 3, 1, 0).contiguous().cuda()  # [i][j][o][c]
+    xd, bd = nhwc(x.detach()).cuda(), b.detach().cuda()
+    ld = 2 * Cout  # write into the first half of a concat buffer
+    yb = torch.zeros(B, 2 * H, 2 * W, ld, device="cuda")
+    assert hip.pis_convt2x2_fwd(xd.data_ptr(), Cin, w_ijoc.data_ptr(), bd.data_ptr(), yb.data_ptr(), ld,
+                                B, H, W, Cin, Cout, s()) == 0
+    dyb = torch.zeros(B, 2 * H, 2 * W, ld, device="cuda")
+    dyb[..., :Cout] = nhwc(dy).cuda()
+    wc = torch.empty(Cin * 4 * Cout, device="cuda")
+    assert hip.pis_convt2x2_prep(w_ijoc.data_ptr(), wc.data_ptr(), Cin, Cout, s()) == 0
+    dx = torch.empty(B, H, W, Cin, device="cuda")
+    assert hip.pis_convt2x2_dgrad(dyb.data_ptr(), ld, wc.data_ptr(), xd.data_ptr(), Cin, dx.data_ptr(), Cin,
+                                  B, H, W, Cin, Cout, MASK, s()) == 0
+    nws = hip.pis_convt2x2_wgrad_ws(B, H, W, Cin, Cout)
+    ws = torch.empty(nws // 4 + 1, device="cuda")
+    dw = torch.empty(2, 2, Cout, Cin, device="cuda")
+    db = torch.empty(Cout, device="cuda")
+    assert hip.pis_convt2x2_wgrad(xd.data_ptr(), Cin, dyb.data_ptr(), ld, dw.data_ptr(), db.data_ptr(),
+                                  B, H, W, Cin, Cout, 0, ws.data_ptr(), nws, s()) == 0
+    torch.cuda.synchronize()
+    assert rel_err(nchw(yb[..., :Cout].cpu()), y.detach()) < 1e-5
+    assert torch.all(yb[..., Cout:] == 0)
+    assert rel_err(nchw(dx.cpu()), x.grad * (x.detach() > 0)) < 1e-5
+    assert rel_err(dw.cpu().permute(3, 2, 0, 1), w.grad) < 1e-5
+    assert rel_err(db.cpu(), b.grad) < 1e-5
+
+
+def test_maxpool(hip):
+    B, H, W, C = 2, 8, 12, 64
+    g = torch.Generator().manual_seed(4)
+    x = F.relu(torch.randn(B, C, H, W, generator=g))
+    x[0, :, 0:2, 0:2] = 0.5  # ties -> first occurrence, as ATen
+    x.requires_grad_(True)
+    y = F.max_pool2d(x, 2, 2)
+    dy = torch.randn(y.shape, generator=g)
+    y.backward(dy)
+    dskip = torch.randn(B, C, H, W, generator=g)
+    ld = 2 * C
+    xb = torch.zeros(B, H, W, ld)
+    xb[..., C:] = nhwc(x.detach())
+    xb = xb.cuda()
+    xs = xb[..., C:]
+    yd = torch.empty(B, H // 2, W // 2, C, device="cuda")
+    assert hip.pis_maxpool2x2_fwd(xs.data_ptr(), ld, yd.data_ptr(), B, H, W, C, s()) == 0
+    dsk = nhwc(dskip).cuda()
+    dx = torch.empty(B, H, W, C, device="cuda")
+    assert hip.pis_maxpool2x2_bwd(xs.data_ptr(), ld, nhwc(dy).cuda().data_ptr(), dsk.data_ptr(), C,
+                                  dx.data_ptr(), C, B, H, W, C, s()) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(nchw(yd.cpu()), y.detach())
+    ref = (x.grad + dskip) * (x.detach() > 0)
+    assert rel_err(nchw(dx.cpu()), ref) < 1e-6
+
+
+def test_head(hip):
+    B, H, W, C = 2, 16, 8, 64
+    g = torch.Generator().manual_seed(5)
+    x = F.relu(torch.randn(B, C, H, W, generator=g)).requires_grad_(True)
+    w = torch.randn(1, C, 1, 1, generator=g).requires_grad_(True)
+    b = torch.randn(1, generator=g).requires_grad_(True)
+    z = F.conv2d(x, w, b)
+    z.retain_grad()
+    u = torch.sigmoid(z)
+    du = torch.randn(u.shape, generator=g)
+    u.backward(du)
+    xd = nhwc(x.detach()).cuda()
+    wd, bd = w.detach().reshape(C).cuda(), b.detach().cuda()
+    zd = torch.empty(B * H * W, device="cuda")
+    ud = torch.empty(B * H * W, device="cuda")
+    assert hip.pis_head_fwd(xd.data_ptr(), C, wd.data_ptr(), bd.data_ptr(), zd.data_ptr(), ud.data_ptr(),
+                            B * H * W, C, s()) == 0
+    dz = z.grad.reshape(-1).cuda()
+    dx = torch.empty(B, H, W, C, device="cuda")
+    dw = torch.empty(C, device="cuda")
+    db = torch.empty(1, device="cuda")
+    nws = hip.pis_head_bwd_ws(B * H * W, C)
+    ws = torch.empty(nws // 4 + 1, device="cuda")
+    assert hip.pis_head_bwd(xd.data_ptr(), C, wd.data_ptr(), dz.data_ptr(), dx.data_ptr(), C, dw.data_ptr(),
+                            db.data_ptr(), B * H * W, C, 0, ws.data_ptr(), nws, s()) == 0
+    torch.cuda.synchronize()
+    assert rel_err(ud.cpu(), u.detach().reshape(-1)) < 1e-6
+    assert rel_err(zd.cpu(), z.detach().reshape(-1)) < 1e-6
+    assert rel_err(nchw(dx.cpu()), x.grad * (x.detach() > 0)) < 1e-6
+    assert rel_err(dw.cpu(), w.grad.reshape(C)) < 1e-5
+    assert rel_err(db.cpu(), b.grad) < 1e-5
+
+
+def _loss_call(hip, p, t, kw, chain=False, grad_out=None):
+    from physics_informed_image_segmentation_amd._hip import LossParams
+    import ctypes
+    B, H, W = p.shape[0], p.shape[-2], p.shape[-1]
+    prm = LossParams(kw.get("dice_w", 0.5), kw.get("bce_w", 0.5), kw.get("rd_w", 0.0), kw.get("pf_w", 0.0),
+                     kw.get("smooth", 1e-6), kw.get("D", 1.0), kw.get("a", 0.5), kw.get("eps", 0.05), 0.5, 1)
+    pd, td = p.contiguous().cuda(), t.contiguous().cuda()
+    terms = torch.empty(8, device="cuda")
+    counts = torch.empty(B, 3, dtype=torch.int32, device="cuda")
+    scores = torch.empty(B, 2, device="cuda")
+    nws = hip.pis_loss_ws(B, H, W)
+    ws = torch.empty(nws // 4 + 1, device="cuda")
+    assert hip.pis_loss_fwd(pd.data_ptr(), td.data_ptr(), B, H, W, ctypes.byref(prm), terms.data_ptr(),
+                            counts.data_ptr(), scores.data_ptr(), ws.data_ptr(), nws, s()) == 0
+    dst = torch.empty(B, H, W, device="cuda")
+    go = None if grad_out is None else torch.tensor([grad_out], device="cuda")
+    assert hip.pis_loss_bwd(pd.data_ptr(), td.data_ptr(), B, H, W, ctypes.byref(prm), terms.data_ptr(),
+                            0 if go is None else go.data_ptr(), dst.data_ptr(), 2 if chain else 0, s()) == 0
+    torch.cuda.synchronize()
+    return terms.cpu(), counts.cpu(), scores.cpu(), dst.cpu()
+
+
+@pytest.mark.parametrize("shape", [(2, 9, 11), (8, 64, 64), (1, 2, 3), (3, 130, 70)])
+@pytest.mark.parametrize("kw", [dict(), dict(rd_w=1e-4, pf_w=1e-4, D=5.0, a=0.5, eps=0.05),
+                                dict(rd_w=0.3, D=0.5, a=0.3), dict(pf_w=0.2, eps=0.1)])
+def test_fused_loss_vs_oracle(hip, shape, kw):
+    g = torch.Generator().manual_seed(6)
+    p = 0.02 + 0.96 * torch.rand(shape, generator=g)
+    t = (torch.rand(shape, generator=g) > 0.7).float()
+    terms, counts, scores, dp = _loss_call(hip, p, t, kw, grad_out=0.75)
+    f = ln.loss_forward(p.numpy(), t.numpy(), **kw)
+    assert terms[0].item() == pytest.approx(f["loss"], rel=1e-5)
+    assert terms[1].item() == pytest.approx(f["dice_loss"], rel=1e-5)
+    assert terms[2].item() == pytest.approx(f["bce_loss"], rel=1e-5)
+    assert terms[3].item() == pytest.approx(f["rd"], rel=1e-4, abs=1e-12)
+    assert terms[4].item() == pytest.approx(f["pf"], rel=1e-4, abs=1e-12)
+    gref = ln.loss_backward(p.numpy(), t.numpy(), grad_out=0.75, **kw)
+    err = np.linalg.norm(dp.numpy() - gref) / np.linalg.norm(gref)
+    assert err < 1e-5
+    i, ph, ts = ln.sample_counts(p.numpy(), t.numpy())
+    assert np.array_equal(counts.numpy(), np.stack([i, ph, ts], 1))
+    d, u = ln.dice_iou_from_counts(i, ph, ts)
+    np.testing.assert_allclose(scores.numpy(), np.stack([d, u], 1), rtol=1e-6)
+
+
+def test_fused_loss_chain_sigmoid(hip):
+    g = torch.Generator().manual_seed(8)
+    p = torch.sigmoid(torch.randn(2, 33, 17, generator=g))
+    t = (torch.rand(2, 33, 17, generator=g) > 0.5).float()
+    kw = dict(rd_w=1e-2, pf_w=1e-2, D=5.0, a=0.5, eps=0.05)
+    _, _, _, dz = _loss_call(hip, p, t, kw, chain=True)
+    gref = ln.loss_backward(p.numpy(), t.numpy(), chain_sigmoid=True, **kw)
+    assert np.linalg.norm(dz.numpy() - gref) / np.linalg.norm(gref) < 1e-5
+
+
+def test_pinned_observation_loss_terms(hip):
+    # the reference's own loss values on its own seed-42 batch via the fused kernel
+    img, mask = rt.synthetic_batch(2, 256, 256, seed=42)
+    torch.manual_seed(42)
+    net = rt.UNetRef(1, 1, 64).eval()
+    with torch.no_grad():
+        u = net(img)
+    kw = dict(rd_w=1e-4, pf_w=1e-4, D=5.0, a=0.5, eps=0.05)
+    terms, counts, scores, _ = _loss_call(hip, u[:, 0], mask[:, 0], kw)
+    assert terms[0].item() == pytest.approx(0.7671615481, rel=1e-5)
+    assert terms[3].item() == pytest.approx(2.58888e-05, rel=1e-4)
+    assert terms[4].item() == pytest.approx(1.24887013, rel=1e-5)
+
+
+def test_adamw_matches_torch(hip):
+    g = torch.Generator().manual_seed(9)
+    n = 1000 + 3
+    p0 = torch.randn(n, generator=g)
+    ref = p0.clone().requires_grad_(True)
+    opt = torch.optim.AdamW([ref], lr=1e-3, weight_decay=1e-5)
+    pd = p0.clone().cuda()
+    m = torch.zeros(n, device="cuda")
+    v = torch.zeros(n, device="cuda")
+    for step in range(1, 4):
+        grad = torch.randn(n, generator=g)
+        ref.grad = grad.clone()
+        opt.step()
+        gd = grad.cuda()
+        bc1 = 1 - 0.9 ** step
+        bc2 = 1 - 0.999 ** step
+        assert hip.pis_adamw_step(pd.data_ptr(), gd.data_ptr(), m.data_ptr(), v.data_ptr(), n, 1e-3, 0.9, 0.999,
+                                  1e-8, 1e-5, 1e-3 / bc1, bc2 ** 0.5, 1.0, s()) == 0
+    torch.cuda.synchronize()
+    assert rel_err(pd.cpu(), ref.detach()) < 1e-6
