@@ -1,0 +1,130 @@
+"""Benchmark: training images/sec of the PDE-constrained U-Net step on MI355X.
+
+Workload (BASELINE.json configs[1], "C2"): UNet(1,1,64), batch 8 per GPU,
+512x512 synthetic disc masks, Stage-II loss
+(0.5 Dice + 0.5 BCE + 1e-4 RD(D=5, a=0.5) + 1e-4 PF(eps=0.05)), AdamW
+lr=1e-5 (Stage II = 0.1 x 1e-4), wd=1e-5, train mode with Dropout2d.
+A step = zero_grad -> forward -> fused loss -> backward (+ RCCL bucketed
+all-reduce when N > 1) -> AdamW, inputs already resident in HBM.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...       (one rank per GPU)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+
+from physics_informed_image_segmentation_amd import AdamW, DiceBCEPDELoss, UNet  # noqa: E402
+from physics_informed_image_segmentation_amd.dataset import disc_sample  # noqa: E402
+from physics_informed_image_segmentation_amd.distributed import (GradBucketer, broadcast_parameters,  # noqa: E402
+                                                                 init_from_env)
+
+B, H, W = 8, 512, 512
+LOSS_KW = dict(pde_weight=1e-4, phase_field_weight=1e-4, diffusion_coeff=5.0, reaction_threshold=0.5, epsilon=0.05)
+LR = 1e-5
+
+
+def conv_flops_per_image(H: int, W: int, c: int = 64) -> float:
+    """Algorithmic FLOPs of one training image: 2 x MACs x 3
+    (fwd, dgrad, wgrad) over every conv / convT, minus the dgrad of enc1.conv0."""
+    macs = 0.0
+    first = 0.0
+    for l in range(1, 5):
+        hw = (H >> (l - 1)) * (W >> (l - 1))
+        cl = c << (l - 1)
+        cin0 = 1 if l == 1 else cl // 2
+        m0 = hw * cl * cin0 * 9
+        if l == 1:
+            first = m0
+        macs += m0 + hw * cl * cl * 9                    # enc conv0, conv1
+        macs += hw * cl * 2 * cl * 9 + hw * cl * cl * 9  # dec conv0 (2C in), conv1
+        cup = 8 * c if l == 4 else 2 * cl
+        macs += (hw // 4) * cup * cl * 4                 # convT into level l
+    hw5 = (H >> 4) * (W >> 4)
+    macs += 2 * hw5 * (8 * c) * (8 * c) * 9              # bottleneck
+    macs += H * W * c                                    # head 1x1
+    return 2.0 * macs * 3 - 2.0 * first
+
+
+def make_batch(rank: int, device):
+    g = torch.Generator().manual_seed(42 + rank)
+    imgs, masks = zip(*[disc_sample(H, W, g) for _ in range(B)])
+    return torch.stack(imgs).to(device), torch.stack(masks).to(device)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+    rank, local_rank, world = init_from_env("nccl")
+    device = torch.device("cuda", local_rank)
+    torch.cuda.set_device(device)
+
+    torch.manual_seed(42)
+    model = UNet(1, 1, 64).to(device).train()
+    broadcast_parameters(model)
+    if world > 1:
+        GradBucketer(model)
+    crit = DiceBCEPDELoss(**LOSS_KW)
+    opt = AdamW(model.parameters(), lr=LR, weight_decay=1e-5, grad_scale=1.0 / world)
+    x, t = make_batch(rank, device)
+
+    def step():
+        opt.zero_grad()
+        loss = crit(model(x), t)
+        loss.backward()
+        opt.step()
+        return loss
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([dt], device=device, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = tt.item()
+    ms = dt / args.steps * 1e3
+    imgs_per_s = world * B * args.steps / dt
+    if rank == 0:
+        flops = conv_flops_per_image(H, W) * B
+        out = {
+            "metric": "training images/sec (512x512, Stage-II RD+PF loss)",
+            "value": imgs_per_s, "unit": "images/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "fp32", "data": "synthetic",
+            "config": {"workload": "C2: UNet(1,1,64) bs=8/GPU 512x512 Stage-II (lambda_RD=lambda_PF=1e-4, D=5, a=0.5, eps=0.05) AdamW lr=1e-5",
+                       "global_batch": B * world, "image_size": [H, W], "parallelism": f"dp{world}"},
+            "step_tflops": flops / (ms * 1e-3) / 1e12,
+            "final_loss": float(loss.item()),
+        }
+        print(json.dumps(out))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -96,14 +96,15 @@ int pis_maxpool2x2_bwd(const float* x, int ldx, const float* dy, const float* ds
 
 /* ---- output head: 1x1 conv C->1 + sigmoid (src/unet.py:157,206-210) ----
  * fwd: z[p] = b + sum_c x[p][c] w[c];  u[p] = 1 / (1 + exp(-z[p]))
- * bwd: dx[p][c] = dz[p] w[c] (x[p][c] > 0)  (ReLU backward of dec1 fused);
- *      dw[c] (+)= sum_p dz[p] x[p][c];  db (+)= sum_p dz[p]                       */
+ * bwd: d[p] = g[p] * u[p] (1 - u[p]) when u != NULL (sigmoid backward), else g[p];
+ *      dx[p][c] = d[p] w[c] (x[p][c] > 0)  (ReLU backward of dec1 fused);
+ *      dw[c] (+)= sum_p d[p] x[p][c];  db (+)= sum_p d[p]                         */
 int pis_head_fwd(const float* x, int ldx, const float* w, const float* b, float* z, float* u,
                  int64_t npix, int C, pis_stream_t stream);
 size_t pis_head_bwd_ws(int64_t npix, int C);
-int pis_head_bwd(const float* x, int ldx, const float* w, const float* dz, float* dx, int lddx,
-                 float* dw, float* db, int64_t npix, int C, int flags, void* ws, size_t ws_bytes,
-                 pis_stream_t stream);
+int pis_head_bwd(const float* x, int ldx, const float* w, const float* g, const float* u, float* dx,
+                 int lddx, float* dw, float* db, int64_t npix, int C, int flags, void* ws,
+                 size_t ws_bytes, pis_stream_t stream);
 
 /* ---- fused Dice + BCE + reaction-diffusion + phase-field loss ----
  * src/loss.py:114-162, src/pde.py:49-212, src/metrics.py:38-73, src/evaluate.py:62-97.

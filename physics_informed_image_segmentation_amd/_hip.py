@@ -46,7 +46,7 @@ _SIGNATURES = {
     "pis_maxpool2x2_bwd": ([P, I, P, P, I, P, I, I, I, I, I, P], c_int),
     "pis_head_fwd": ([P, I, P, P, P, P, L, I, P], c_int),
     "pis_head_bwd_ws": ([L, I], c_size_t),
-    "pis_head_bwd": ([P, I, P, P, P, I, P, P, L, I, I, P, Z, P], c_int),
+    "pis_head_bwd": ([P, I, P, P, P, P, I, P, P, L, I, I, P, Z, P], c_int),
     "pis_loss_ws": ([I, I, I], c_size_t),
     "pis_loss_fwd": ([P, P, I, I, I, ctypes.POINTER(LossParams), P, P, P, P, Z, P], c_int),
     "pis_loss_bwd": ([P, P, I, I, I, ctypes.POINTER(LossParams), P, P, P, I, P], c_int),

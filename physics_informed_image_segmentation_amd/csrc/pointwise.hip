@@ -104,13 +104,15 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(const float* __restrict__
   }
 }
 
-// head bwd: dx[p][c] = dz[p] w[c] (x[p][c] > 0); partial dw[c] per block
+// head bwd: d = g u (1-u) (or g); dx[p][c] = d w[c] (x[p][c] > 0); per-block partial dw[c], db
 __global__ __launch_bounds__(256) void head_bwd_kernel(const float* __restrict__ x, int ldx,
                                                        const float* __restrict__ w,
-                                                       const float* __restrict__ dz,
+                                                       const float* __restrict__ gin,
+                                                       const float* __restrict__ u,
                                                        float* __restrict__ dx, int lddx,
                                                        int64_t npix, int C, int64_t pix_per_block,
-                                                       float* __restrict__ part) {
+                                                       float* __restrict__ part,
+                                                       float* __restrict__ part_b) {
   // C % 4 == 0, C <= 1024: lane group of C/4 threads covers one pixel
   const int c4n = C / 4;
   const int rows = 256 / c4n;
@@ -118,10 +120,13 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(const float* __restrict__
   const int64_t p0 = (int64_t)blockIdx.x * pix_per_block;
   const int64_t p1 = min(npix, p0 + pix_per_block);
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  float accb = 0.f;
   if (r < rows) {
     const f32x4 wv = *reinterpret_cast<const f32x4*>(w + 4 * c4);
     for (int64_t p = p0 + r; p < p1; p += rows) {
-      const float d = dz[p];
+      float d = gin[p];
+      if (u) { const float uu = u[p]; d = d * (1.f - uu) * uu; }
+      if (c4 == 0) accb += d;
       const f32x4 xv = *reinterpret_cast<const f32x4*>(x + p * ldx + 4 * c4);
       f32x4 o;
 #pragma unroll
@@ -133,12 +138,19 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(const float* __restrict__
     }
   }
   __shared__ f32x4 red[256];
+  __shared__ float redb[256];
   red[threadIdx.x] = acc;
+  redb[threadIdx.x] = accb;
   __syncthreads();
   if ((int)threadIdx.x < c4n) {
     f32x4 t = red[threadIdx.x];
     for (int k = 1; k < rows; ++k) t += red[k * c4n + threadIdx.x];
     *reinterpret_cast<f32x4*>(part + (size_t)blockIdx.x * C + 4 * threadIdx.x) = t;
+  }
+  if (threadIdx.x == 0) {
+    float t = 0.f;
+    for (int k = 0; k < rows; ++k) t += redb[k * c4n];
+    part_b[blockIdx.x] = t;
   }
 }
 
@@ -226,13 +238,13 @@ extern "C" int pis_head_fwd(const float* x, int ldx, const float* w, const float
 
 extern "C" size_t pis_head_bwd_ws(int64_t npix, int C) {
   const int64_t blocks = cdiv(npix, head_pix_per_block(npix));
-  return std::max<size_t>((size_t)blocks * C * sizeof(float), colsum_ws(npix, 1)) + 256;
+  return (size_t)blocks * (C + 1) * sizeof(float) + 256;
 }
 
-extern "C" int pis_head_bwd(const float* x, int ldx, const float* w, const float* dz, float* dx,
-                            int lddx, float* dw, float* db, int64_t npix, int C, int flags,
-                            void* ws, size_t ws_bytes, pis_stream_t stream) {
-  PIS_CHECK_ARG(x && w && dz && dx && dw && npix > 0 && C % 4 == 0 && C / 4 <= 256 &&
+extern "C" int pis_head_bwd(const float* x, int ldx, const float* w, const float* g, const float* u,
+                            float* dx, int lddx, float* dw, float* db, int64_t npix, int C,
+                            int flags, void* ws, size_t ws_bytes, pis_stream_t stream) {
+  PIS_CHECK_ARG(x && w && g && dx && dw && npix > 0 && C % 4 == 0 && C / 4 <= 256 &&
                     ldx % 4 == 0 && lddx % 4 == 0,
                 "pis_head_bwd: bad arguments");
   PIS_CHECK_ARG(ws_bytes >= pis_head_bwd_ws(npix, C), "pis_head_bwd: workspace too small");
@@ -240,11 +252,13 @@ extern "C" int pis_head_bwd(const float* x, int ldx, const float* w, const float
   const int acc = flags & PIS_ACCUMULATE;
   const int64_t ppb = head_pix_per_block(npix);
   const int blocks = (int)cdiv(npix, ppb);
-  hipLaunchKernelGGL(head_bwd_kernel, dim3(blocks), dim3(256), 0, s, x, ldx, w, dz, dx, lddx, npix,
-                     C, ppb, (float*)ws);
+  float* part = (float*)ws;
+  float* part_b = part + (size_t)blocks * C;
+  hipLaunchKernelGGL(head_bwd_kernel, dim3(blocks), dim3(256), 0, s, x, ldx, w, g, u, dx, lddx, npix,
+                     C, ppb, part, part_b);
   int rc = launch_status("head_bwd");
-  if (!rc) rc = reduce_slabs((float*)ws, blocks, C, dw, acc, s);
-  if (!rc && db) rc = colsum(dz, 1, npix, 1, db, acc, ws, ws_bytes, s);
+  if (!rc) rc = reduce_slabs(part, blocks, C, dw, acc, s);
+  if (!rc && db) rc = reduce_slabs(part_b, blocks, 1, db, acc, s);
   return rc;
 }
 

@@ -1,0 +1,117 @@
+"""Autograd wrapper of the fused Dice + BCE + reaction-diffusion + phase-field
+kernel (pis_loss_fwd / pis_loss_bwd). One forward launch pair computes every
+loss term, the whole-batch Dice sums and the per-sample thresholded metric
+counters; the backward is one elementwise launch.
+
+Used by src-compatible ``loss`` (src/loss.py:7-162), ``pde``
+(src/pde.py:124-212) and ``metrics`` (src/metrics.py:4-73) modules.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+from typing import Dict, Tuple
+
+import torch
+
+from . import _hip
+from ._hip import LossParams, PIS_LOSS_ALL_TERMS, call
+
+
+@dataclass(frozen=True)
+class LossConfig:
+    dice_w: float = 0.5
+    bce_w: float = 0.5
+    rd_w: float = 0.0
+    pf_w: float = 0.0
+    smooth: float = 1e-6
+    D: float = 1.0
+    a: float = 0.5
+    eps: float = 0.05
+    thr: float = 0.5
+    all_terms: bool = False
+
+    def params(self) -> LossParams:
+        return LossParams(self.dice_w, self.bce_w, self.rd_w, self.pf_w, self.smooth, self.D, self.a,
+                          self.eps, self.thr, PIS_LOSS_ALL_TERMS if self.all_terms else 0)
+
+
+_WS: Dict[Tuple, torch.Tensor] = {}
+
+
+def _workspace(B: int, H: int, W: int, dev: torch.device) -> torch.Tensor:
+    key = (B, H, W, dev)
+    ws = _WS.get(key)
+    if ws is None:
+        n = _hip.lib().pis_loss_ws(B, H, W)
+        ws = torch.empty((n + 3) // 4, dtype=torch.float32, device=dev)
+        _WS[key] = ws
+    return ws
+
+
+def _bhw(u: torch.Tensor) -> Tuple[int, int, int]:
+    if u.dim() < 2:
+        raise ValueError("expected (B, 1, H, W) or (B, H, W) tensors")
+    B, H, W = u.shape[0], u.shape[-2], u.shape[-1]
+    if u.numel() != B * H * W:
+        raise ValueError(f"single-channel maps expected, got {tuple(u.shape)}")
+    return B, H, W
+
+
+def _prep(u: torch.Tensor, t: torch.Tensor, what: str):
+    _hip.require_cuda(u, what)
+    if t.shape != u.shape and t.numel() != u.numel():
+        raise ValueError(f"{what}: target shape {tuple(t.shape)} does not match prediction {tuple(u.shape)}")
+    if u.dtype != torch.float32:
+        raise TypeError(f"{what}: float32 predictions expected")
+    u = u.detach().contiguous()
+    t = t.to(device=u.device, dtype=torch.float32).contiguous()
+    return u, t
+
+
+def loss_forward(u: torch.Tensor, t: torch.Tensor, cfg: LossConfig):
+    """-> (terms[8], counts (B,3) int32, scores (B,2)); all on the device, no sync."""
+    u, t = _prep(u, t, "fused loss")
+    B, H, W = _bhw(u)
+    dev = u.device
+    terms = torch.empty(_hip.LOSS_NTERMS, dtype=torch.float32, device=dev)
+    counts = torch.empty(B, 3, dtype=torch.int32, device=dev)
+    scores = torch.empty(B, 2, dtype=torch.float32, device=dev)
+    ws = _workspace(B, H, W, dev)
+    prm = cfg.params()
+    call("pis_loss_fwd", u.data_ptr(), t.data_ptr(), B, H, W, ctypes.byref(prm), terms.data_ptr(),
+         counts.data_ptr(), scores.data_ptr(), ws.data_ptr(), ws.numel() * 4, _hip.stream_handle())
+    return terms, counts, scores
+
+
+class _FusedLoss(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, u, t, cfg: LossConfig, sink: dict):
+        terms, counts, scores = loss_forward(u, t, cfg)
+        sink["terms"], sink["counts"], sink["scores"] = terms, counts, scores
+        ctx.cfg = cfg
+        ctx.shape = u.shape
+        ctx.save_for_backward(u.detach().contiguous(), t.to(torch.float32).contiguous(), terms)
+        return terms[0].clone()
+
+    @staticmethod
+    def backward(ctx, g):
+        u, t, terms = ctx.saved_tensors
+        B, H, W = _bhw(u)
+        du = torch.empty_like(u)
+        g = g.to(torch.float32).contiguous()
+        prm = ctx.cfg.params()
+        call("pis_loss_bwd", u.data_ptr(), t.data_ptr(), B, H, W, ctypes.byref(prm), terms.data_ptr(),
+             g.data_ptr(), du.data_ptr(), 0, _hip.stream_handle())
+        return du.view(ctx.shape), None, None, None
+
+
+def fused_loss(u: torch.Tensor, t: torch.Tensor, cfg: LossConfig, sink: dict = None) -> torch.Tensor:
+    """Differentiable total loss (0-dim); per-term values land in ``sink``."""
+    if sink is None:
+        sink = {}
+    if not (torch.is_grad_enabled() and u.requires_grad):
+        terms, counts, scores = loss_forward(u, t, cfg)
+        sink["terms"], sink["counts"], sink["scores"] = terms, counts, scores
+        return terms[0].clone()
+    return _FusedLoss.apply(u, t, cfg, sink)

@@ -1,0 +1,552 @@
+"""U-Net of src/unet.py on the MI355X kernel path.
+
+``UNet`` keeps the reference's constructor, module tree, parameter creation
+order (so ``torch.manual_seed`` gives identical weights), state_dict keys and
+shapes (src/unet.py:108-167). Its forward returns sigmoid probabilities
+(src/unet.py:169-216) but never runs an ATen convolution: the whole network
+is one autograd node whose forward/backward are sequences of HIP kernels
+(``UNetEngine``) over NHWC activations.
+
+Memory layout (MI355X-first):
+  * every parameter is a view into ONE flat fp32 arena; conv weights are
+    physically KRSC ([Cout][3][3][Cin] = OIHW channels_last) and ConvTranspose
+    weights [2][2][Cout][Cin], so the kernels read them directly and AdamW /
+    the RCCL all-reduce see one contiguous buffer;
+  * gradients land in a second arena with the same layout, in reverse
+    creation order during backward (out_conv first), which is what lets
+    data-parallel buckets be contiguous ranges all-reduced while backward runs;
+  * skip concatenation is free: the encoder block writes its output straight
+    into the second channel half of the decoder's concat buffer and the
+    transposed conv writes the first half (src/unet.py:190-202).
+"""
+from __future__ import annotations
+
+from typing import Callable, Dict, List, Optional, Sequence, Tuple
+
+import torch
+import torch.nn as nn
+
+from . import _hip
+from ._hip import PIS_ACCUMULATE, PIS_MASK, PIS_RELU, PIS_SCALE, call, ptr
+
+# block name -> dropout multiplier of UNet(dropout=d), src/unet.py:120-154
+_DROP_MULT = {"enc1": 0.0, "enc2": 0.5, "enc3": 1.0, "enc4": 1.0, "bottleneck": 1.0,
+              "dec4": 1.0, "dec3": 0.5, "dec2": 0.5, "dec1": 0.0}
+BLOCK_ORDER = ("enc1", "enc2", "enc3", "enc4", "bottleneck", "dec4", "dec3", "dec2", "dec1")
+_ALIGN = 64  # floats: every parameter starts on a 256-byte boundary of the arena
+
+
+class DoubleConv(nn.Module):
+    """Parameter container with the reference's layout (src/unet.py:19-42):
+    ``conv = Sequential(Conv2d, ReLU, [Dropout2d], Conv2d, ReLU)``. Its compute
+    only exists inside the fused ``UNet`` engine."""
+
+    def __init__(self, in_channels: int, out_channels: int, dropout: float = 0.0, activation: str = "relu"):
+        super().__init__()
+        if activation.lower() != "relu":
+            raise NotImplementedError(
+                f"intermediate_activation={activation!r}: only 'relu' is on the MI355X path "
+                "(the reference's configs never select another, src/ablation.py:44-45)")
+        act = nn.ReLU(inplace=True)
+        layers: List[nn.Module] = [nn.Conv2d(in_channels, out_channels, kernel_size=3, padding=1), act]
+        if dropout > 0:
+            layers.append(nn.Dropout2d(dropout))
+        layers += [nn.Conv2d(out_channels, out_channels, kernel_size=3, padding=1), act]
+        self.conv = nn.Sequential(*layers)
+        self.p = float(dropout)
+
+    @property
+    def conv0(self) -> nn.Conv2d:
+        return self.conv[0]
+
+    @property
+    def conv1(self) -> nn.Conv2d:
+        return self.conv[3] if self.p > 0 else self.conv[2]
+
+    def forward(self, x):  # pragma: no cover - guard against silent ATen fallbacks
+        raise RuntimeError("DoubleConv is evaluated only inside UNet.forward (HIP engine)")
+
+
+def count_parameters(model: nn.Module) -> int:
+    """src/unet.py:220-230."""
+    return sum(p.numel() for p in model.parameters() if p.requires_grad)
+
+
+def _phys_view(flat: torch.Tensor, logical: torch.Size, kind: str) -> torch.Tensor:
+    """View of the arena slice with the logical (reference) shape."""
+    if kind == "conv":  # logical (O, I, kh, kw) stored [O][kh][kw][I]
+        O, I_, kh, kw = logical
+        return flat.view(O, kh, kw, I_).permute(0, 3, 1, 2)
+    if kind == "convt":  # logical (Cin, Cout, 2, 2) stored [i][j][o][c]
+        Ci, Co, kh, kw = logical
+        return flat.view(kh, kw, Co, Ci).permute(3, 2, 0, 1)
+    return flat.view(logical)
+
+
+class UNet(nn.Module):
+    """Drop-in for ``src.unet.UNet`` (src/unet.py:79-216) on the HIP path."""
+
+    def __init__(self, in_channels: int = 1, out_channels: int = 1, base_channels: int = 64,
+                 dropout: float = 0.2, output_activation: str = "sigmoid",
+                 intermediate_activation: str = "relu"):
+        super().__init__()
+        if output_activation.lower() not in ("sigmoid", "tanh"):
+            raise ValueError(f"Unsupported output_activation: {output_activation}. Must be 'sigmoid' or 'tanh'")
+        if output_activation.lower() != "sigmoid":
+            raise NotImplementedError("output_activation='tanh' is not on the MI355X path (sigmoid only)")
+        if out_channels != 1:
+            raise NotImplementedError("out_channels must be 1 (single probability map, src/unet.py:157)")
+        if not (in_channels == 1 or in_channels % 4 == 0):
+            raise NotImplementedError("in_channels must be 1 or a multiple of 4")
+        if base_channels % 64 != 0:
+            raise NotImplementedError("base_channels must be a multiple of 64 on the MI355X path")
+        c = base_channels
+        self.in_channels, self.base_channels, self.dropout_rate = in_channels, c, float(dropout)
+        act = intermediate_activation
+        # creation order == RNG order == reference parameter order
+        self.enc1 = DoubleConv(in_channels, c, dropout=0.0, activation=act)
+        self.enc2 = DoubleConv(c, 2 * c, dropout=dropout * 0.5, activation=act)
+        self.enc3 = DoubleConv(2 * c, 4 * c, dropout=dropout, activation=act)
+        self.enc4 = DoubleConv(4 * c, 8 * c, dropout=dropout, activation=act)
+        self.pool = nn.MaxPool2d(kernel_size=2, stride=2)
+        self.bottleneck = DoubleConv(8 * c, 8 * c, dropout=dropout, activation=act)
+        self.up4 = nn.ConvTranspose2d(8 * c, 8 * c, kernel_size=2, stride=2)
+        self.dec4 = DoubleConv(16 * c, 8 * c, dropout=dropout, activation=act)
+        self.up3 = nn.ConvTranspose2d(8 * c, 4 * c, kernel_size=2, stride=2)
+        self.dec3 = DoubleConv(8 * c, 4 * c, dropout=dropout * 0.5, activation=act)
+        self.up2 = nn.ConvTranspose2d(4 * c, 2 * c, kernel_size=2, stride=2)
+        self.dec2 = DoubleConv(4 * c, 2 * c, dropout=dropout * 0.5, activation=act)
+        self.up1 = nn.ConvTranspose2d(2 * c, c, kernel_size=2, stride=2)
+        self.dec1 = DoubleConv(2 * c, c, dropout=0.0, activation=act)
+        self.out_conv = nn.Conv2d(c, out_channels, kernel_size=1)
+        self.output_activation = nn.Sigmoid()
+        self.activation_name = "sigmoid"
+        self._pack_arena()
+        self._engine: Optional[UNetEngine] = None
+        self._drop_override: Optional[Dict[str, torch.Tensor]] = None
+        self.grad_ready_hook = None  # object with on_ready(lo, hi) / finish(): DDP bucketer
+        self.last_logits: Optional[torch.Tensor] = None
+
+    # ---- arena -------------------------------------------------------------
+    def _param_kinds(self):
+        kinds = {}
+        for name, mod in self.named_modules():
+            if isinstance(mod, nn.ConvTranspose2d):
+                kinds[id(mod.weight)] = "convt"
+            elif isinstance(mod, nn.Conv2d) and mod.kernel_size == (3, 3):
+                kinds[id(mod.weight)] = "conv"
+        return kinds
+
+    def _pack_arena(self):
+        kinds = self._param_kinds()
+        entries = []  # (module, name, shape, kind, offset, numel)
+        off = 0
+        for mname, mod in self.named_modules():
+            for pname, p in list(mod._parameters.items()):
+                if p is None:
+                    continue
+                n = p.numel()
+                entries.append((mod, pname, p.shape, kinds.get(id(p), "plain"), off, n))
+                off += (n + _ALIGN - 1) // _ALIGN * _ALIGN
+        arena = torch.zeros(off, dtype=torch.float32)
+        for mod, pname, shape, kind, o, n in entries:
+            old = mod._parameters[pname]
+            view = _phys_view(arena[o:o + n], shape, kind)
+            view.copy_(old.detach())
+            mod._parameters[pname] = nn.Parameter(view, requires_grad=old.requires_grad)
+        self._arena = arena
+        self._entries = [(mod, pname, shape, kind, o, n) for mod, pname, shape, kind, o, n in entries]
+        self._grad_arena: Optional[torch.Tensor] = None
+
+    @property
+    def arena(self) -> torch.Tensor:
+        return self._arena
+
+    def grad_arena(self) -> torch.Tensor:
+        if self._grad_arena is None or self._grad_arena.device != self._arena.device:
+            self._grad_arena = torch.zeros_like(self._arena)
+        return self._grad_arena
+
+    def param_offset(self, p: torch.Tensor) -> int:
+        for mod, pname, shape, kind, o, n in self._entries:
+            if mod._parameters[pname] is p:
+                return o
+        raise KeyError("parameter does not belong to this UNet")
+
+    def arena_entries(self):
+        """[(qualified_name, offset, numel)] in arena order."""
+        names = {id(p): n for n, p in self.named_parameters()}
+        return [(names[id(mod._parameters[pn])], o, n) for mod, pn, _, _, o, n in self._entries]
+
+    def grad_views(self) -> List[torch.Tensor]:
+        g = self.grad_arena()
+        return [_phys_view(g[o:o + n], shape, kind) for _, _, shape, kind, o, n in self._entries]
+
+    def _rebind(self):
+        for mod, pname, shape, kind, o, n in self._entries:
+            mod._parameters[pname].data = _phys_view(self._arena[o:o + n], shape, kind)
+
+    def _apply(self, fn, recurse=True):
+        new = fn(self._arena)
+        if new.dtype != torch.float32:
+            raise NotImplementedError("the MI355X path is fp32 (reference parity); dtype casts are unsupported")
+        self._arena = new
+        self._rebind()
+        if self._grad_arena is not None:
+            self._grad_arena = fn(self._grad_arena)
+        for mod, pname, shape, kind, o, n in self._entries:
+            mod._parameters[pname].grad = None
+        for name, buf in self._buffers.items():
+            if buf is not None:
+                self._buffers[name] = fn(buf)
+        self._engine = None
+        return self
+
+    # ---- dropout control -----------------------------------------------------
+    def set_dropout_scales(self, scales: Optional[Dict[str, torch.Tensor]]):
+        """Inject Dropout2d keep-scales {block: (B, C) tensor of 0 or 1/(1-p)} for
+        the next training forward (parity runs); None restores the RNG draw."""
+        self._drop_override = scales
+
+    def block(self, name: str) -> DoubleConv:
+        return getattr(self, name)
+
+    # ---- forward -------------------------------------------------------------
+    def engine(self) -> "UNetEngine":
+        if self._engine is None:
+            self._engine = UNetEngine(self)
+        return self._engine
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        _hip.require_cuda(x, "UNet.forward")
+        if x.dim() != 4 or x.shape[1] != self.in_channels:
+            raise ValueError(f"expected input (B, {self.in_channels}, H, W), got {tuple(x.shape)}")
+        if x.dtype != torch.float32:
+            raise TypeError("UNet expects float32 input")
+        if x.shape[2] % 16 or x.shape[3] % 16:
+            raise ValueError("H and W must be divisible by 16 (four 2x2 max-pools, src/unet.py:180-186)")
+        if self._arena.device != x.device:
+            raise RuntimeError(f"model is on {self._arena.device}, input on {x.device}")
+        params = [mod._parameters[pn] for mod, pn, *_ in self._entries]
+        needs_grad = torch.is_grad_enabled() and any(p.requires_grad for p in params)
+        eng = self.engine()
+        scales = eng.dropout_scales(x.shape[0], self.training, self._drop_override)
+        if not needs_grad:
+            return eng.forward(x, scales, keep=False)
+        return _UNetFunction.apply(x, eng, scales, *params)
+
+
+class _UNetFunction(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, eng, scales, *params):
+        u = eng.forward(x, scales, keep=True)
+        ctx.eng = eng
+        ctx.gen = eng.generation
+        ctx.n_params = len(params)
+        return u
+
+    @staticmethod
+    def backward(ctx, du):
+        eng: UNetEngine = ctx.eng
+        if eng.generation != ctx.gen:
+            raise RuntimeError("UNet.backward: another forward ran since this graph was built "
+                               "(activations are kept in one set of engine buffers)")
+        grads = eng.backward(du.contiguous())
+        return (None, None, None) + tuple(grads)
+
+
+# =============================================================================
+#  Engine
+# =============================================================================
+
+class _Buf:
+    """NHWC activation: tensor + channel stride + channel offset."""
+    __slots__ = ("t", "ld", "off")
+
+    def __init__(self, t: torch.Tensor, ld: int, off: int = 0):
+        self.t, self.ld, self.off = t, ld, off
+
+    @property
+    def p(self) -> int:
+        return self.t.data_ptr() + 4 * self.off
+
+    def slice(self, off: int) -> "_Buf":
+        return _Buf(self.t, self.ld, self.off + off)
+
+
+class UNetEngine:
+    """Explicit forward/backward schedule of the U-Net over HIP kernels.
+
+    Forward keeps every activation the backward needs (no recomputation);
+    backward walks out_conv -> dec1 -> up1 -> ... -> enc1, writing each
+    layer's weight gradient into the gradient arena as soon as it is known and
+    reporting the finished arena range to ``model.grad_ready_hook`` (the DDP
+    bucket trigger)."""
+
+    def __init__(self, model: UNet):
+        self.m = model
+        self.c = model.base_channels
+        self.plan_key = None
+        self.generation = 0
+        self.bufs: Dict[str, torch.Tensor] = {}
+        self._offsets = {id(mod._parameters[pn]): (o, n) for mod, pn, _, _, o, n in model._entries}
+        self.last_grad_mode = None
+
+    # ---- planning -----------------------------------------------------------
+    def _plan(self, B: int, H: int, W: int, dev: torch.device):
+        key = (B, H, W, dev)
+        if key == self.plan_key:
+            return
+        c = self.c
+        f = lambda *shape: torch.empty(*shape, dtype=torch.float32, device=dev)
+        b = {}
+        for l in range(1, 5):
+            Hl, Wl, Cl = H >> (l - 1), W >> (l - 1), c << (l - 1)
+            b[f"a{l}"] = f(B, Hl, Wl, Cl)            # conv0 output of enc_l
+            b[f"cat{l}"] = f(B, Hl, Wl, 2 * Cl)      # [up_l | enc_l]
+            b[f"pool{l}"] = f(B, Hl // 2, Wl // 2, Cl)
+            b[f"d0_{l}"] = f(B, Hl, Wl, Cl)          # dec_l conv0 output
+            b[f"d1_{l}"] = f(B, Hl, Wl, Cl)          # dec_l conv1 output
+        H5, W5 = H >> 4, W >> 4
+        b["b0"] = f(B, H5, W5, 8 * c)
+        b["b1"] = f(B, H5, W5, 8 * c)
+        b["u"] = f(B, 1, H, W)
+        b["z"] = f(B, 1, H, W)  # pre-sigmoid logits of the last forward (out_conv output)
+        self.bufs = b
+        self.gbufs: Dict[str, torch.Tensor] = {}
+        self.plan_key = key
+        self.B, self.H, self.W = B, H, W
+        lib = _hip.lib()
+        ws = lib.pis_head_bwd_ws(B * H * W, c)
+        for l in range(1, 5):
+            Hl, Wl, Cl = H >> (l - 1), W >> (l - 1), c << (l - 1)
+            cin0 = self.m.in_channels if l == 1 else Cl // 2
+            ws = max(ws, lib.pis_conv3x3_wgrad_ws(B, Hl, Wl, cin0, Cl), lib.pis_conv3x3_wgrad_ws(B, Hl, Wl, Cl, Cl),
+                     lib.pis_conv3x3_wgrad_ws(B, Hl, Wl, 2 * Cl, Cl))
+            cup = 8 * c if l == 4 else 2 * Cl
+            ws = max(ws, lib.pis_convt2x2_wgrad_ws(B, Hl // 2, Wl // 2, cup, Cl))
+        ws = max(ws, lib.pis_conv3x3_wgrad_ws(B, H5, W5, 8 * c, 8 * c))
+        self.ws = torch.empty((ws + 15) // 4, dtype=torch.float32, device=dev)
+        self.ws_bytes = self.ws.numel() * 4
+
+    def _gbuf(self, name: str, *shape) -> torch.Tensor:
+        t = self.gbufs.get(name)
+        if t is None:
+            t = torch.empty(*shape, dtype=torch.float32, device=self.m.arena.device)
+            self.gbufs[name] = t
+        return t
+
+    # ---- dropout ------------------------------------------------------------
+    def dropout_scales(self, B: int, training: bool, override) -> Dict[str, Optional[torch.Tensor]]:
+        """Per-block (B, C) keep-scales. Drawn like ATen's feature_dropout
+        (noise.bernoulli_(1-p).div_(1-p), one draw per block in forward order)."""
+        out: Dict[str, Optional[torch.Tensor]] = {}
+        for name in BLOCK_ORDER:
+            blk = self.m.block(name)
+            if not training or blk.p <= 0:
+                out[name] = None
+                continue
+            if override is not None and name in override:
+                s = override[name].to(device=self.m.arena.device, dtype=torch.float32).contiguous()
+            elif blk.p >= 1.0:
+                s = torch.zeros(B, blk.conv0.out_channels, device=self.m.arena.device)
+            else:
+                s = torch.empty(B, blk.conv0.out_channels, device=self.m.arena.device)
+                s.bernoulli_(1.0 - blk.p).div_(1.0 - blk.p)
+            out[name] = s
+        return out
+
+    # ---- kernel helpers ------------------------------------------------------
+    def _stream(self):
+        return torch.cuda.current_stream().cuda_stream
+
+    def _conv_fwd(self, conv: nn.Conv2d, x: _Buf, y: _Buf, B, H, W, scale):
+        flags = PIS_RELU | (PIS_SCALE if scale is not None else 0)
+        call("pis_conv3x3_fwd", x.p, x.ld, conv.weight.data_ptr(), conv.bias.data_ptr(), ptr(scale),
+             y.p, y.ld, B, H, W, conv.in_channels, conv.out_channels, flags, self._stream())
+
+    def _grad_slot(self, p: torch.Tensor) -> Tuple[int, int]:
+        return self._offsets[id(p)]
+
+    def _gptr(self, p: torch.Tensor) -> int:
+        o, _ = self._offsets[id(p)]
+        return self.garena.data_ptr() + 4 * o
+
+    def _ready(self, *params):
+        hook = self.m.grad_ready_hook
+        if hook is None:
+            return
+        lo = min(self._offsets[id(p)][0] for p in params)
+        hi = max(self._offsets[id(p)][0] + self._offsets[id(p)][1] for p in params)
+        hook.on_ready(lo, hi)
+
+    # ---- forward -------------------------------------------------------------
+    @torch.no_grad()
+    def forward(self, x: torch.Tensor, scales: Dict[str, Optional[torch.Tensor]], keep: bool) -> torch.Tensor:
+        m, c = self.m, self.c
+        B, _, H, W = x.shape
+        self._plan(B, H, W, x.device)
+        x = x.contiguous()
+        bf = self.bufs
+        self.x = x
+        self.scales = scales
+        src = _Buf(x, m.in_channels)
+        for l in range(1, 5):
+            Hl, Wl, Cl = H >> (l - 1), W >> (l - 1), c << (l - 1)
+            blk = m.block(f"enc{l}")
+            a = _Buf(bf[f"a{l}"], Cl)
+            e = _Buf(bf[f"cat{l}"], 2 * Cl, Cl)         # enc output lives in the concat buffer
+            self._conv_fwd(blk.conv0, src, a, B, Hl, Wl, scales[f"enc{l}"])
+            self._conv_fwd(blk.conv1, a, e, B, Hl, Wl, None)
+            call("pis_maxpool2x2_fwd", e.p, e.ld, bf[f"pool{l}"].data_ptr(), B, Hl, Wl, Cl, self._stream())
+            src = _Buf(bf[f"pool{l}"], Cl)
+        H5, W5 = H >> 4, W >> 4
+        blk = m.bottleneck
+        self._conv_fwd(blk.conv0, src, _Buf(bf["b0"], 8 * c), B, H5, W5, scales["bottleneck"])
+        self._conv_fwd(blk.conv1, _Buf(bf["b0"], 8 * c), _Buf(bf["b1"], 8 * c), B, H5, W5, None)
+        d = _Buf(bf["b1"], 8 * c)
+        dC = 8 * c
+        for l in (4, 3, 2, 1):
+            Hl, Wl, Cl = H >> (l - 1), W >> (l - 1), c << (l - 1)
+            up = getattr(m, f"up{l}")
+            cat = _Buf(bf[f"cat{l}"], 2 * Cl)
+            call("pis_convt2x2_fwd", d.p, d.ld, up.weight.data_ptr(), up.bias.data_ptr(), cat.p, cat.ld,
+                 B, Hl // 2, Wl // 2, dC, Cl, self._stream())
+            blk = m.block(f"dec{l}")
+            d0 = _Buf(bf[f"d0_{l}"], Cl)
+            d1 = _Buf(bf[f"d1_{l}"], Cl)
+            self._conv_fwd(blk.conv0, cat, d0, B, Hl, Wl, scales[f"dec{l}"])
+            self._conv_fwd(blk.conv1, d0, d1, B, Hl, Wl, None)
+            d, dC = d1, Cl
+        u = bf["u"] if keep else torch.empty(B, 1, H, W, device=x.device)
+        z = bf["z"]
+        call("pis_head_fwd", d.p, d.ld, m.out_conv.weight.data_ptr(), m.out_conv.bias.data_ptr(), z.data_ptr(),
+             u.data_ptr(), B * H * W, c, self._stream())
+        m.last_logits = z
+        if keep:
+            self.generation += 1
+            self.u = u
+            return u
+        return u
+
+    # ---- backward ------------------------------------------------------------
+    def _grad_mode(self) -> str:
+        """'overwrite' when every .grad is None (zero_grad(set_to_none=True)),
+        'accumulate' when every .grad already views the gradient arena."""
+        params = [mod._parameters[pn] for mod, pn, *_ in self.m._entries]
+        if all(p.grad is None for p in params):
+            return "overwrite"
+        g = self.m.grad_arena()
+        lo, hi = g.data_ptr(), g.data_ptr() + 4 * g.numel()
+        if all(p.grad is not None and lo <= p.grad.data_ptr() < hi for p in params):
+            return "accumulate"
+        return "scratch"
+
+    @torch.no_grad()
+    def backward(self, du: torch.Tensor) -> List[Optional[torch.Tensor]]:
+        m, c = self.m, self.c
+        B, H, W = self.B, self.H, self.W
+        bf = self.bufs
+        mode = self._grad_mode()
+        self.last_grad_mode = mode
+        if mode == "scratch":
+            self.garena = torch.zeros_like(m.arena)
+        else:
+            self.garena = m.grad_arena()
+        acc = PIS_ACCUMULATE if mode == "accumulate" else 0
+        st = self._stream()
+        ws, wsb = self.ws.data_ptr(), self.ws_bytes
+        gb = self._gbuf
+
+        # dgrad operands, rebuilt from the current weights
+        flips = {}
+        for name in BLOCK_ORDER:
+            blk = m.block(name)
+            for conv in (blk.conv0, blk.conv1):
+                if conv.in_channels == 1 and conv is m.enc1.conv0:
+                    continue
+                t = gb(f"flip_{id(conv)}", conv.weight.numel())
+                call("pis_conv3x3_flip", conv.weight.data_ptr(), t.data_ptr(), conv.in_channels,
+                     conv.out_channels, st)
+                flips[id(conv)] = t
+        for l in (1, 2, 3, 4):
+            up = getattr(m, f"up{l}")
+            t = gb(f"prep_up{l}", up.weight.numel())
+            call("pis_convt2x2_prep", up.weight.data_ptr(), t.data_ptr(), up.in_channels, up.out_channels, st)
+            flips[id(up)] = t
+
+        def conv_bwd(conv, x: _Buf, dz: _Buf, dx: Optional[_Buf], Hl, Wl, mask: Optional[_Buf], scale):
+            call("pis_conv3x3_wgrad", x.p, x.ld, dz.p, dz.ld, self._gptr(conv.weight), self._gptr(conv.bias),
+                 B, Hl, Wl, conv.in_channels, conv.out_channels, acc, ws, wsb, st)
+            self._ready(conv.weight, conv.bias)
+            if dx is not None:
+                flags = (PIS_MASK if mask is not None else 0) | (PIS_SCALE if scale is not None else 0)
+                call("pis_conv3x3_dgrad", dz.p, dz.ld, flips[id(conv)].data_ptr(),
+                     mask.p if mask is not None else 0, mask.ld if mask is not None else 0, ptr(scale),
+                     dx.p, dx.ld, B, Hl, Wl, conv.in_channels, conv.out_channels, flags, st)
+
+        # head: sigmoid backward + 1x1 conv + ReLU backward of dec1.conv1
+        d1 = _Buf(bf["d1_1"], c)
+        g_d1 = _Buf(gb("g_d1_1", B, H, W, c), c)
+        call("pis_head_bwd", d1.p, d1.ld, m.out_conv.weight.data_ptr(), du.data_ptr(), self.u.data_ptr(),
+             g_d1.p, g_d1.ld, self._gptr(m.out_conv.weight), self._gptr(m.out_conv.bias), B * H * W, c, acc,
+             ws, wsb, st)
+        self._ready(m.out_conv.weight, m.out_conv.bias)
+
+        g_top = g_d1  # dz of dec_l.conv1
+        for l in (1, 2, 3, 4):
+            Hl, Wl, Cl = H >> (l - 1), W >> (l - 1), c << (l - 1)
+            blk = m.block(f"dec{l}")
+            d0 = _Buf(bf[f"d0_{l}"], Cl)
+            cat = _Buf(bf[f"cat{l}"], 2 * Cl)
+            g_d0 = _Buf(gb(f"g_d0_{l}", B, Hl, Wl, Cl), Cl)
+            conv_bwd(blk.conv1, d0, g_top, g_d0, Hl, Wl, d0, self.scales[f"dec{l}"])
+            g_cat = _Buf(gb(f"g_cat{l}", B, Hl, Wl, 2 * Cl), 2 * Cl)
+            conv_bwd(blk.conv0, cat, g_d0, g_cat, Hl, Wl, None, None)
+            # transposed conv up_l: its input is dec_{l+1} conv1 output (or bottleneck conv1)
+            up = getattr(m, f"up{l}")
+            if l == 4:
+                xin = _Buf(bf["b1"], 8 * c)
+            else:
+                xin = _Buf(bf[f"d1_{l + 1}"], up.in_channels)
+            Hh, Wh = Hl // 2, Wl // 2
+            call("pis_convt2x2_wgrad", xin.p, xin.ld, g_cat.p, g_cat.ld, self._gptr(up.weight), self._gptr(up.bias),
+                 B, Hh, Wh, up.in_channels, up.out_channels, acc, ws, wsb, st)
+            self._ready(up.weight, up.bias)
+            g_in = _Buf(gb(f"g_upin{l}", B, Hh, Wh, up.in_channels), up.in_channels)
+            call("pis_convt2x2_dgrad", g_cat.p, g_cat.ld, flips[id(up)].data_ptr(), xin.p, xin.ld, g_in.p, g_in.ld,
+                 B, Hh, Wh, up.in_channels, up.out_channels, PIS_MASK, st)
+            g_top = g_in
+        # bottleneck
+        H5, W5 = H >> 4, W >> 4
+        blk = m.bottleneck
+        b0 = _Buf(bf["b0"], 8 * c)
+        g_b0 = _Buf(gb("g_b0", B, H5, W5, 8 * c), 8 * c)
+        conv_bwd(blk.conv1, b0, g_top, g_b0, H5, W5, b0, self.scales["bottleneck"])
+        g_pool = _Buf(gb("g_pool4", B, H5, W5, 8 * c), 8 * c)
+        conv_bwd(blk.conv0, _Buf(bf["pool4"], 8 * c), g_b0, g_pool, H5, W5, None, None)
+        # encoder, deepest first
+        for l in (4, 3, 2, 1):
+            Hl, Wl, Cl = H >> (l - 1), W >> (l - 1), c << (l - 1)
+            blk = m.block(f"enc{l}")
+            e = _Buf(bf[f"cat{l}"], 2 * Cl, Cl)
+            g_skip = _Buf(self.gbufs[f"g_cat{l}"], 2 * Cl, Cl)
+            g_e = _Buf(gb(f"g_e{l}", B, Hl, Wl, Cl), Cl)
+            call("pis_maxpool2x2_bwd", e.p, e.ld, g_pool.p, g_skip.p, g_skip.ld, g_e.p, g_e.ld, B, Hl, Wl, Cl, st)
+            a = _Buf(bf[f"a{l}"], Cl)
+            g_a = _Buf(gb(f"g_a{l}", B, Hl, Wl, Cl), Cl)
+            conv_bwd(blk.conv1, a, g_e, g_a, Hl, Wl, a, self.scales[f"enc{l}"])
+            if l > 1:
+                g_pool = _Buf(gb(f"g_pool{l - 1}", B, Hl, Wl, Cl // 2), Cl // 2)
+                conv_bwd(blk.conv0, _Buf(bf[f"pool{l - 1}"], Cl // 2), g_a, g_pool, Hl, Wl, None, None)
+            else:
+                conv_bwd(blk.conv0, _Buf(self.x, m.in_channels), g_a, None, Hl, Wl, None, None)
+
+        if m.grad_ready_hook is not None:
+            if mode == "scratch":
+                raise RuntimeError("data-parallel gradients need zero_grad() before every backward")
+            m.grad_ready_hook.finish()
+        if mode == "accumulate":
+            return [None] * len(m._entries)
+        g = self.garena
+        return [_phys_view(g[o:o + n], shape, kind) for _, _, shape, kind, o, n in m._entries]

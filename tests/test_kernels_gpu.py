@@ -201,9 +201,19 @@ def test_head(hip):
     db = torch.empty(1, device="cuda")
     nws = hip.pis_head_bwd_ws(B * H * W, C)
     ws = torch.empty(nws // 4 + 1, device="cuda")
-    assert hip.pis_head_bwd(xd.data_ptr(), C, wd.data_ptr(), dz.data_ptr(), dx.data_ptr(), C, dw.data_ptr(),
+    assert hip.pis_head_bwd(xd.data_ptr(), C, wd.data_ptr(), dz.data_ptr(), 0, dx.data_ptr(), C, dw.data_ptr(),
                             db.data_ptr(), B * H * W, C, 0, ws.data_ptr(), nws, s()) == 0
+    # sigmoid-chained form: feed dL/du and u
+    dx2 = torch.empty_like(dx)
+    dw2 = torch.empty_like(dw)
+    db2 = torch.empty_like(db)
+    dud = du.reshape(-1).cuda()
+    assert hip.pis_head_bwd(xd.data_ptr(), C, wd.data_ptr(), dud.data_ptr(), ud.data_ptr(), dx2.data_ptr(), C,
+                            dw2.data_ptr(), db2.data_ptr(), B * H * W, C, 0, ws.data_ptr(), nws, s()) == 0
     torch.cuda.synchronize()
+    assert rel_err(nchw(dx2.cpu()), x.grad * (x.detach() > 0)) < 1e-5
+    assert rel_err(dw2.cpu(), w.grad.reshape(C)) < 1e-5
+    assert rel_err(db2.cpu(), b.grad) < 1e-5
     assert rel_err(ud.cpu(), u.detach().reshape(-1)) < 1e-6
     assert rel_err(zd.cpu(), z.detach().reshape(-1)) < 1e-6
     assert rel_err(nchw(dx.cpu()), x.grad * (x.detach() > 0)) < 1e-6

@@ -1,0 +1,161 @@
+"""Whole-network parity on the GPU: the HIP U-Net step vs the CPU restatement
+(oracle/reference_torch.py, stock fp32 ATen = the ops the reference runs).
+
+Tolerance (north star): 1e-4 relative fp32, checked per output, per loss term
+and per parameter gradient (norm-wise)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import reference_torch as rt
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-4
+PDE_KW = dict(rd_w=1e-4, pf_w=1e-4, D=5.0, a=0.5, eps=0.05)
+
+
+def rel(a, b):
+    a, b = a.detach().double().cpu(), b.detach().double().cpu()
+    return ((a - b).norm() / max(b.norm().item(), 1e-30)).item()
+
+
+def make_pair(seed=42):
+    from physics_informed_image_segmentation_amd import UNet
+    torch.manual_seed(seed)
+    ref = rt.UNetRef(1, 1, 64)
+    torch.manual_seed(seed)
+    net = UNet(1, 1, 64).cuda()
+    return net, ref
+
+
+def test_pinned_observation_forward(hip):
+    """The reference's own numbers on its seed-42 batch, now from the HIP path."""
+    from physics_informed_image_segmentation_amd import DiceBCELoss, DiceBCEPDELoss, compute_dice_score
+    img, mask = rt.synthetic_batch(2, 256, 256, seed=42)
+    net, _ = make_pair(42)
+    net.eval()
+    with torch.no_grad():
+        u = net(img.cuda())
+        l1 = DiceBCELoss()(u, mask.cuda()).item()
+        l2 = DiceBCEPDELoss(pde_weight=1e-4, phase_field_weight=1e-4, diffusion_coeff=5.0,
+                            reaction_threshold=0.5, epsilon=0.05)(u, mask.cuda()).item()
+        d = compute_dice_score(u, mask.cuda()).item()
+    assert u.min().item() == pytest.approx(0.5088648, rel=1e-5)
+    assert u.max().item() == pytest.approx(0.5125621, rel=1e-5)
+    assert u.mean().item() == pytest.approx(0.5106269, rel=1e-5)
+    assert l1 == pytest.approx(0.7670366764, rel=TOL)
+    assert l2 == pytest.approx(0.7671615481, rel=TOL)
+    assert d == pytest.approx(0.19274600, rel=TOL)
+
+
+@pytest.mark.parametrize("B,H,W", [(2, 64, 64), (1, 32, 48)])
+def test_forward_eval_logits(hip, B, H, W):
+    img, mask = rt.synthetic_batch(B, H, W, seed=3)
+    net, ref = make_pair(7)
+    net.eval(), ref.eval()
+    with torch.no_grad():
+        u = net(img.cuda())
+        p_ref, z_ref = ref(img, return_logits=True)
+    assert rel(net.last_logits, z_ref) < TOL
+    assert rel(u, p_ref) < TOL
+
+
+def _step_pair(B, H, W, loss_kw, seed=11):
+    from physics_informed_image_segmentation_amd import DiceBCELoss, DiceBCEPDELoss
+    img, mask = rt.synthetic_batch(B, H, W, seed=seed)
+    net, ref = make_pair(seed)
+    net.train(), ref.train()
+    gen = torch.Generator().manual_seed(seed)
+    scales = rt.make_drop_scales(ref, B, gen)
+    net.set_dropout_scales(scales)
+    # HIP side
+    if loss_kw.get("rd_w", 0) > 0 or loss_kw.get("pf_w", 0) > 0:
+        crit = DiceBCEPDELoss(pde_weight=loss_kw.get("rd_w", 0.0), phase_field_weight=loss_kw.get("pf_w", 0.0),
+                              diffusion_coeff=loss_kw.get("D", 1.0), reaction_threshold=loss_kw.get("a", 0.5),
+                              epsilon=loss_kw.get("eps", 0.05))
+    else:
+        crit = DiceBCELoss()
+    u = net(img.cuda())
+    loss = crit(u, mask.cuda())
+    loss.backward()
+    # oracle side
+    p_ref = ref(img, scales)
+    terms = rt.loss_terms(p_ref, mask, **loss_kw)
+    terms["loss"].backward()
+    return net, ref, u, crit, p_ref, terms
+
+
+@pytest.mark.parametrize("loss_kw", [dict(), PDE_KW, dict(rd_w=1e-2, pf_w=1e-2, D=5.0, a=0.5, eps=0.05)])
+def test_train_step_grads(hip, loss_kw):
+    net, ref, u, crit, p_ref, terms = _step_pair(2, 64, 64, loss_kw)
+    assert rel(u, p_ref) < TOL
+    got = crit.last["terms"].cpu()
+    assert got[0].item() == pytest.approx(terms["loss"].item(), rel=TOL)
+    assert got[1].item() == pytest.approx(terms["dice_loss"].item(), rel=TOL)
+    assert got[2].item() == pytest.approx(terms["bce_loss"].item(), rel=TOL)
+    if "pde_loss" in terms:
+        assert got[3].item() == pytest.approx(terms["pde_loss"].item(), rel=TOL)
+        assert got[4].item() == pytest.approx(terms["phase_field_loss"].item(), rel=TOL)
+    worst = []
+    for (n, p), (n2, q) in zip(net.named_parameters(), ref.named_parameters()):
+        assert n == n2
+        assert p.grad is not None, n
+        e = rel(p.grad, q.grad)
+        worst.append((e, n))
+    worst.sort(reverse=True)
+    assert worst[0][0] < TOL, worst[:5]
+
+
+def test_grad_accumulation_and_arena(hip):
+    net, ref, u, crit, p_ref, terms = _step_pair(1, 32, 32, dict())
+    g1 = {n: p.grad.clone() for n, p in net.named_parameters()}
+    garena = net.grad_arena()
+    assert all(garena.data_ptr() <= p.grad.data_ptr() < garena.data_ptr() + 4 * garena.numel()
+               for p in net.parameters())
+    # second backward without zero_grad accumulates (torch semantics)
+    img, mask = rt.synthetic_batch(1, 32, 32, seed=11)
+    out = net(img.cuda())
+    crit(out, mask.cuda()).backward()
+    assert net.engine().last_grad_mode == "accumulate"
+    for n, p in net.named_parameters():
+        assert rel(p.grad, 2 * g1[n]) < 1e-5, n
+
+
+def test_adamw_two_steps_match_torch(hip):
+    from physics_informed_image_segmentation_amd import AdamW, DiceBCEPDELoss
+    B, H, W = 2, 32, 32
+    img, mask = rt.synthetic_batch(B, H, W, seed=5)
+    net, ref = make_pair(5)
+    net.eval(), ref.eval()  # no dropout: pure optimizer parity
+    opt = AdamW(net.parameters(), lr=1e-3, weight_decay=1e-5)
+    opt_ref = rt.make_adamw(ref, lr=1e-3, weight_decay=1e-5)
+    crit = DiceBCEPDELoss(pde_weight=1e-4, phase_field_weight=1e-4, diffusion_coeff=5.0, epsilon=0.05)
+    kw = PDE_KW
+    for _ in range(2):
+        opt.zero_grad()
+        crit(net(img.cuda()), mask.cuda()).backward()
+        opt.step()
+        opt_ref.zero_grad()
+        rt.loss_terms(ref(img), mask, **kw)["loss"].backward()
+        opt_ref.step()
+    worst = max(rel(p, q) for p, q in zip(net.parameters(), ref.parameters()))
+    assert worst < 1e-5
+
+
+def test_train_epoch_keys_and_validate(hip):
+    from torch.utils.data import DataLoader
+
+    from physics_informed_image_segmentation_amd import (AdamW, DiceBCEPDELoss, SyntheticDiscDataset, train_epoch,
+                                                         validate)
+    net, _ = make_pair(1)
+    ds = SyntheticDiscDataset(4, (64, 64), seed=1)
+    dl = DataLoader(ds, batch_size=2)
+    crit = DiceBCEPDELoss(pde_weight=1e-4, phase_field_weight=1e-4, diffusion_coeff=5.0)
+    opt = AdamW(net.parameters(), lr=1e-4, weight_decay=1e-5)
+    tr = train_epoch(net, dl, crit, opt, torch.device("cuda"), return_components=True, compute_metrics=True)
+    assert set(tr) == {"loss", "dice_loss", "bce_loss", "pde_loss", "phase_field_loss", "dice_score",
+                       "iou_score", "boundary_f1_score"}
+    va = validate(net, dl, crit, torch.device("cuda"), return_components=True, compute_metrics=True)
+    assert {"loss", "dice_score", "dice_loss", "bce_loss", "pde_loss", "iou_score"} <= set(va)
+    assert np.isfinite(tr["loss"]) and np.isfinite(va["loss"])
