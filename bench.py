@@ -56,6 +56,91 @@ def conv_flops_per_image(H: int, W: int, c: int = 64) -> float:
     return 2.0 * macs * 3 - 2.0 * first
 
 
+IGEMM_CALLS = ("pis_conv3x3_fwd", "pis_conv3x3_dgrad", "pis_convt2x2_fwd", "pis_convt2x2_dgrad")
+DOMINANT = "igemm_f32_kernel<128, 128>"
+
+
+def igemm_shape(name, a):
+    """(M, N, K, kernel) of the implicit GEMM one C-ABI call launches (csrc/igemm.hip dispatch)."""
+    if name == "pis_conv3x3_fwd":
+        Bb, Hh, Ww, cin, cout = a[7:12]
+        if cin == 1:
+            return None
+        M, N, K = Bb * Hh * Ww, cout, 9 * cin
+    elif name == "pis_conv3x3_dgrad":
+        Bb, Hh, Ww, cin, cout = a[8:13]
+        M, N, K = Bb * Hh * Ww, cin, 9 * cout
+    elif name == "pis_convt2x2_fwd":
+        Bb, Hh, Ww, cin, cout = a[6:11]
+        M, N, K = Bb * Hh * Ww, 4 * cout, cin
+    else:
+        Bb, Hh, Ww, cin, cout = a[7:12]
+        M, N, K = Bb * Hh * Ww, cin, 4 * cout
+    return M, N, K, ("igemm_f32_kernel<128, 64>" if N <= 64 else DOMINANT)
+
+
+class LaunchTimer:
+    """HIP events around every launch of the dominant kernel, on the stream it runs on."""
+
+    def __init__(self, kernel=DOMINANT):
+        self.kernel = kernel
+        self.records = []
+
+    def begin(self, name, args):
+        if name not in IGEMM_CALLS:
+            return None
+        shp = igemm_shape(name, args)
+        if shp is None or shp[3] != self.kernel:
+            return None
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        return (e0, e1, 2.0 * shp[0] * shp[1] * shp[2])
+
+    def end(self, tok):
+        if tok is not None:
+            tok[1].record()
+            self.records.append(tok)
+
+    def summary(self):
+        torch.cuda.synchronize()
+        ms = [e0.elapsed_time(e1) for e0, e1, _ in self.records]
+        fl = [f for _, _, f in self.records]
+        return len(ms), sum(fl) / len(fl), sum(ms) / len(ms)
+
+
+def load_pmc_traffic():
+    """Per-launch HBM bytes of the dominant kernel from the committed rocprofv3 --pmc
+    summary (tools/pmc_summary.py, FETCH_SIZE x2 gfx950 correction + WRITE_SIZE)."""
+    path = os.path.join(HERE, "profiles", "pmc_dominant.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        return json.load(f).get("hbm_bytes_per_launch")
+
+
+def cpu_baseline(seconds: float = 15.0):
+    """The oracle (stock-PyTorch CPU restatement of the reference step) on the host cores."""
+    from oracle import reference_torch as rt
+    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    torch.set_num_threads(threads)
+    img, mask = rt.synthetic_batch(1, H, W, seed=42)
+    torch.manual_seed(42)
+    ref = rt.UNetRef(1, 1, 64).train()
+    opt = rt.make_adamw(ref, lr=LR)
+    kw = dict(rd_w=1e-4, pf_w=1e-4, D=5.0, a=0.5, eps=0.05)
+    rt.train_step(ref, opt, img, mask, kw)  # warm-up
+    n, t0 = 0, time.perf_counter()
+    while True:
+        rt.train_step(ref, opt, img, mask, kw)
+        n += 1
+        dt = time.perf_counter() - t0
+        if dt >= seconds or n >= 64:
+            break
+    return {"value": n / dt, "unit": "images/s", "cores": threads, "kind": "port",
+            "sample": f"{n} Stage-II training steps of 1 image 512x512 (oracle/reference_torch.py, torch "
+                      f"{torch.__version__} CPU, {threads} threads) after 1 warm-up step, {dt:.1f} s"}
+
+
 def make_batch(rank: int, device):
     g = torch.Generator().manual_seed(42 + rank)
     imgs, masks = zip(*[disc_sample(H, W, g) for _ in range(B)])
@@ -109,6 +194,17 @@ def main():
         dt = tt.item()
     ms = dt / args.steps * 1e3
     imgs_per_s = world * B * args.steps / dt
+
+    # roofline of the dominant kernel: one instrumented step after the timed region
+    timer = LaunchTimer()
+    from physics_informed_image_segmentation_amd import _hip
+    _hip.set_tracer(timer)
+    step()
+    _hip.set_tracer(None)
+    n_launch, flop_per_launch, ms_per_launch = timer.summary()
+    achieved = flop_per_launch / (ms_per_launch * 1e-3) / 1e12
+    peak = 157.3  # fp32 MFMA dense TFLOP/s (MI355X_MICROARCH.md)
+    traffic = load_pmc_traffic()
     if rank == 0:
         flops = conv_flops_per_image(H, W) * B
         out = {
@@ -118,9 +214,15 @@ def main():
             "vs_baseline": None, "dtype": "fp32", "data": "synthetic",
             "config": {"workload": "C2: UNet(1,1,64) bs=8/GPU 512x512 Stage-II (lambda_RD=lambda_PF=1e-4, D=5, a=0.5, eps=0.05) AdamW lr=1e-5",
                        "global_batch": B * world, "image_size": [H, W], "parallelism": f"dp{world}"},
+            "roofline": {"bound": "mfma", "kernel": DOMINANT, "achieved": achieved, "peak": peak,
+                         "unit": "TFLOP/s", "frac": achieved / peak, "traffic": traffic,
+                         "launches_per_step": n_launch, "avg_launch_ms": ms_per_launch,
+                         "flop_per_launch": flop_per_launch},
             "step_tflops": flops / (ms * 1e-3) / 1e12,
             "final_loss": float(loss.item()),
         }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline()
         print(json.dumps(out))
     if world > 1:
         dist.destroy_process_group()

@@ -98,8 +98,24 @@ def check(rc: int, what: str) -> None:
         raise HipError(f"{what} failed ({rc}): {msg.decode() if msg else ''}")
 
 
+_tracer = None
+
+
+def set_tracer(tracer) -> None:
+    """Install an object with begin(name, args) -> token / end(token) around every
+    C-ABI call (bench.py uses it to time launches with HIP events); None removes it."""
+    global _tracer
+    _tracer = tracer
+
+
 def call(name: str, *args) -> None:
+    tr = _tracer
+    if tr is None:
+        check(getattr(lib(), name)(*args), name)
+        return
+    tok = tr.begin(name, args)
     check(getattr(lib(), name)(*args), name)
+    tr.end(tok)
 
 
 def require_cuda(t: torch.Tensor, what: str) -> None:
