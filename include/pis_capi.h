@@ -47,6 +47,14 @@ typedef void* pis_stream_t; /* hipStream_t */
 const char* pis_last_error(void);
 int pis_version(void);
 
+/* Kernel-variant knobs (process-wide). value < 0 queries; returns the previous
+ * value or PIS_ERR_ARG. Defaults are the measured best on MI355X.            */
+#define PIS_TUNE_IGEMM_BK 1 /* implicit-GEMM K-step: 16 or 32 */
+#define PIS_TUNE_DEBUG_NOLOAD 2 /* timing only: implicit GEMM skips its global loads (wrong results) */
+#define PIS_TUNE_NKEYS 3
+#define PIS_DEBUG_NOLOAD (1 << 16)
+int pis_tune(int key, int value);
+
 /* ---- 3x3 convolution, padding 1, stride 1 (src/unet.py:29,38 nn.Conv2d) ----
  * fwd:  y[p][n] = epi(bias[n] + sum_{r,s,c} x[p+(r-1,s-1)][c] * w[n][r][s][c])
  *       flags: PIS_RELU, PIS_SCALE (scale is [B][Cout]).   Cin==1 or Cin%4==0. */

@@ -32,6 +32,7 @@ P, I, L, Z, Dbl = c_void_p, c_int, c_int64, c_size_t, c_double
 _SIGNATURES = {
     "pis_version": ([], c_int),
     "pis_last_error": ([], ctypes.c_char_p),
+    "pis_tune": ([I, I], c_int),
     "pis_conv3x3_fwd": ([P, I, P, P, P, P, I, I, I, I, I, I, I, P], c_int),
     "pis_conv3x3_flip": ([P, P, I, I, P], c_int),
     "pis_conv3x3_dgrad": ([P, I, P, P, I, P, P, I, I, I, I, I, I, I, P], c_int),

@@ -1,4 +1,5 @@
-// Error channel and version of the pis_* C-ABI (include/pis_capi.h).
+// Error channel, version and tuning table of the pis_* C-ABI (include/pis_capi.h).
+#include <atomic>
 #include <cstdarg>
 
 #include "common.h"
@@ -12,7 +13,26 @@ void set_error(const char* fmt, ...) {
   vsnprintf(g_last_error, sizeof(g_last_error), fmt, ap);
   va_end(ap);
 }
+
+// kernel-variant knobs (defaults = the measured best on MI355X)
+static std::atomic<int> g_tune[PIS_TUNE_NKEYS] = {0, 16, 0};
+
+int tune_get(int key) { return (key > 0 && key < PIS_TUNE_NKEYS) ? g_tune[key].load() : 0; }
 }  // namespace pis
 
 extern "C" const char* pis_last_error(void) { return pis::g_last_error; }
 extern "C" int pis_version(void) { return 1; }
+
+extern "C" int pis_tune(int key, int value) {
+  if (key <= 0 || key >= PIS_TUNE_NKEYS) {
+    pis::set_error("pis_tune: unknown key %d", key);
+    return PIS_ERR_ARG;
+  }
+  if (key == PIS_TUNE_IGEMM_BK && value >= 0 && value != 16 && value != 32) {
+    pis::set_error("pis_tune: igemm K-step must be 16 or 32");
+    return PIS_ERR_ARG;
+  }
+  const int prev = pis::g_tune[key].load();
+  if (value >= 0) pis::g_tune[key].store(value);
+  return prev;
+}

@@ -49,11 +49,13 @@ __device__ __forceinline__ void tap_offset(int mode, int t, int& dr, int& ds, in
   else { dr = 0; ds = 0; st = 1; }
 }
 
-template <int BM, int BN>
+template <int BM, int BN, int BK>
 __global__ __launch_bounds__(256) void igemm_f32_kernel(IGemmArgs g) {
-  constexpr int BK = 16, LDS_ROW = BK + 4;  // 80-byte rows: conflict-free ds_read_b128
-  constexpr int TM = BM / 64, TN = BN / 64;  // 32x32 tiles per wave (2x2 waves)
-  constexpr int AL = BM / 64, BL = BN / 64;  // float4 staging loads per thread
+  // row pitch BK+4 floats (80 or 144 bytes): 16 rows land on 16 distinct 16-B slots -> conflict-free ds_read_b128
+  constexpr int LDS_ROW = BK + 4;
+  constexpr int CPR = BK / 4;                           // float4 chunks per staged row
+  constexpr int TM = BM / 64, TN = BN / 64;             // 32x32 tiles per wave (2x2 waves)
+  constexpr int AL = BM * CPR / 256, BL = BN * CPR / 256;  // float4 staging loads per thread
   __shared__ __attribute__((aligned(16))) float sA[2][BM * LDS_ROW];
   __shared__ __attribute__((aligned(16))) float sB[2][BN * LDS_ROW];
 
@@ -69,7 +71,7 @@ __global__ __launch_bounds__(256) void igemm_f32_kernel(IGemmArgs g) {
   const int HW = g.H * g.W;
 #pragma unroll
   for (int i = 0; i < AL; ++i) {
-    const int row = (tid + i * 256) >> 2;
+    const int row = (tid + i * 256) / CPR;
     const int m = m0 + row;
     a_ok[i] = m < g.M;
     const int mm = a_ok[i] ? m : 0;
@@ -78,13 +80,15 @@ __global__ __launch_bounds__(256) void igemm_f32_kernel(IGemmArgs g) {
     a_h[i] = rem / g.W;
     a_w[i] = rem - a_h[i] * g.W;
   }
-  const int q4 = (tid & 3) * 4;  // channel offset inside the BK chunk
+  const int q4 = (tid % CPR) * 4;  // channel offset inside the BK chunk
 
   const int nchunks = (g.Csrc + BK - 1) / BK;
   const int KT = g.ntaps * nchunks;
 
   f32x4 ra[AL], rb[BL];
+  const bool noload = g.flags & PIS_DEBUG_NOLOAD;  // timing-only: LDS + MFMA ceiling of this loop
   auto gload = [&](int kt) {
+    if (noload && kt > 0) return;
     const int tap = kt / nchunks;
     const int c = (kt - tap * nchunks) * BK + q4;
     int dr, dsh, st;
@@ -102,7 +106,7 @@ __global__ __launch_bounds__(256) void igemm_f32_kernel(IGemmArgs g) {
     }
 #pragma unroll
     for (int i = 0; i < BL; ++i) {
-      const int n = n0 + ((tid + i * 256) >> 2);
+      const int n = n0 + (tid + i * 256) / CPR;
       rb[i] = f32x4{0.f, 0.f, 0.f, 0.f};
       if (n < g.N && cok)
         rb[i] = *reinterpret_cast<const f32x4*>(g.wt + (size_t)n * g.ldw + tap * g.Csrc + c);
@@ -111,12 +115,12 @@ __global__ __launch_bounds__(256) void igemm_f32_kernel(IGemmArgs g) {
   auto lstore = [&](int buf) {
 #pragma unroll
     for (int i = 0; i < AL; ++i) {
-      const int row = (tid + i * 256) >> 2;
+      const int row = (tid + i * 256) / CPR;
       *reinterpret_cast<f32x4*>(&sA[buf][row * LDS_ROW + q4]) = ra[i];
     }
 #pragma unroll
     for (int i = 0; i < BL; ++i) {
-      const int row = (tid + i * 256) >> 2;
+      const int row = (tid + i * 256) / CPR;
       *reinterpret_cast<f32x4*>(&sB[buf][row * LDS_ROW + q4]) = rb[i];
     }
   };
@@ -195,15 +199,26 @@ __global__ __launch_bounds__(256) void igemm_f32_kernel(IGemmArgs g) {
   }
 }
 
+int tune_get(int key);
+
 static int launch_igemm(const IGemmArgs& a, hipStream_t s) {
-  // tile choice: BN=64 for narrow outputs, BM=128
+  // tile choice: BN=64 for narrow outputs, BM=128; K-step from the tuning table
   const int ntm = (int)cdiv(a.M, 128);
+  const int bk = tune_get(PIS_TUNE_IGEMM_BK);
+  IGemmArgs& m = const_cast<IGemmArgs&>(a);
+  if (tune_get(PIS_TUNE_DEBUG_NOLOAD)) m.flags |= PIS_DEBUG_NOLOAD;
   if (a.N <= 64) {
     const int grid = ntm * (int)cdiv(a.N, 64);
-    hipLaunchKernelGGL((igemm_f32_kernel<128, 64>), dim3(grid), dim3(256), 0, s, a);
+    if (bk == 32)
+      hipLaunchKernelGGL((igemm_f32_kernel<128, 64, 32>), dim3(grid), dim3(256), 0, s, a);
+    else
+      hipLaunchKernelGGL((igemm_f32_kernel<128, 64, 16>), dim3(grid), dim3(256), 0, s, a);
   } else {
     const int grid = ntm * (int)cdiv(a.N, 128);
-    hipLaunchKernelGGL((igemm_f32_kernel<128, 128>), dim3(grid), dim3(256), 0, s, a);
+    if (bk == 32)
+      hipLaunchKernelGGL((igemm_f32_kernel<128, 128, 32>), dim3(grid), dim3(256), 0, s, a);
+    else
+      hipLaunchKernelGGL((igemm_f32_kernel<128, 128, 16>), dim3(grid), dim3(256), 0, s, a);
   }
   return launch_status("igemm_f32");
 }

@@ -1,34 +1,42 @@
-// Weight-gradient GEMMs (fp32 MFMA) for src/unet.py's 3x3 convs and 2x2
-// transposed convs, plus channel sums for bias gradients.
+// Weight- and bias-gradient GEMMs (fp32 MFMA) for src/unet.py's 3x3 convs and
+// 2x2 transposed convs, plus generic channel sums.
 //
 //   C[m'][n'] = sum_p A(p, m') * B(p, n')       p = pixel of the reduction grid
+//   bias[m']  = sum_p A(p, m')                  (fused: blocks of the first n'-tile)
 //
 // The pixel reduction (up to B*H*W = 2.1M at 512^2) is split over blocks
 // ("splits"); every block writes its partial C tile to a slab and a second
 // kernel sums the slabs in a fixed order, so the result is deterministic and
-// each fp32 accumulation chain is at most `pix_per_split` long.
+// each fp32 accumulation chain is at most `pix_per_split` long. Logical block
+// ids are XCD-remapped and split-major, so the tiles sharing one pixel range
+// (e.g. the 9 taps of a conv) run on one XCD and re-read their inputs from
+// that XCD's L2.
 //
 // conv3x3:  m' = n (Cout),        A(p, n)     = dz[p][n]
 //           n' = (tap, c),        B(p, tap,c) = x[p + off(tap)][c]    (zero pad)
+//           Cin == 1:  n' = tap (9 of 64 columns used)
 // convT2x2: m' = (i, j, o),       A(p, ijo)   = dy[(2h+i, 2w+j)][o]
 //           n' = c,               B(p, c)     = x[p][c]
 #include "common.h"
 
 namespace pis {
 
+enum BMode { B_PLAIN = 0, B_CONV3 = 1, B_CONV3_C1 = 2 };
+
 struct WgradArgs {
   const float* a; int lda; int a_up2; int Ca;   // Ca: channels per (i,j) group when a_up2
-  const float* b; int ldb; int b_conv3; int Cb;  // Cb: channels per tap when b_conv3
+  const float* b; int ldb; int b_mode; int Cb;   // Cb: channels per tap when B_CONV3
   int B, H, W;                                   // reduction pixel grid
   int P;                                         // B*H*W
-  int Mp, Np;                                    // output dims
+  int Mp, Np;                                    // output dims (Np padded for B_CONV3_C1)
   int pix_per_split;
   float* part;                                   // [splits][Mp][Np]
+  float* part_bias;                              // [splits][Mp] or NULL
 };
 
-template <int BM, int BN>
+// BKP pixels per stage: 32 MFMAs per wave between barriers for every tile shape
+template <int BM, int BN, int BKP>
 __global__ __launch_bounds__(256) void wgrad_f32_kernel(WgradArgs g) {
-  constexpr int BKP = 16;                     // pixels per stage
   constexpr int TM = BM / 64, TN = BN / 64;   // 32x32 tiles per wave
   constexpr int AL = BKP * BM / 4 / 256, BL = BKP * BN / 4 / 256;
   __shared__ __attribute__((aligned(16))) float sA[2][BKP * BM];
@@ -38,17 +46,20 @@ __global__ __launch_bounds__(256) void wgrad_f32_kernel(WgradArgs g) {
   const int wm = wave & 1, wn = wave >> 1;
   const int ntm = g.Mp / BM, ntn = g.Np / BN;
   const int tiles = ntm * ntn;
-  const int split = blockIdx.x / tiles;
-  const int tile = blockIdx.x - split * tiles;
-  const int m0 = (tile / ntn) * BM, n0 = (tile % ntn) * BN;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = bid / tiles;
+  const int tile = bid - split * tiles;
+  const int tm = tile / ntn, tn = tile % ntn;
+  const int m0 = tm * BM, n0 = tn * BN;
   const int p_begin = split * g.pix_per_split;
   const int p_end = min(g.P, p_begin + g.pix_per_split);
+  const bool do_bias = g.part_bias != nullptr && tn == 0;
 
   // tap of this tile (tiles never straddle a tap)
   int a_dr = 0, a_ds = 0, a_c0 = m0;
   if (g.a_up2) { const int ij = m0 / g.Ca; a_dr = ij >> 1; a_ds = ij & 1; a_c0 = m0 - ij * g.Ca; }
   int b_dr = 0, b_ds = 0, b_c0 = n0;
-  if (g.b_conv3) { const int t = n0 / g.Cb; b_dr = t / 3 - 1; b_ds = t % 3 - 1; b_c0 = n0 - t * g.Cb; }
+  if (g.b_mode == B_CONV3) { const int t = n0 / g.Cb; b_dr = t / 3 - 1; b_ds = t % 3 - 1; b_c0 = n0 - t * g.Cb; }
   const int HW = g.H * g.W;
 
   f32x4 ra[AL], rb[BL];
@@ -74,16 +85,26 @@ __global__ __launch_bounds__(256) void wgrad_f32_kernel(WgradArgs g) {
       const int prow = idx / (BN / 4), c = (idx % (BN / 4)) * 4;
       const int p = p0 + prow;
       rb[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (p < p_end) {
-        bool ok = true;
-        size_t pix = p;
-        if (g.b_conv3) {
-          const int bb = p / HW, rem = p - bb * HW, h = rem / g.W, w = rem - h * g.W;
+      if (p >= p_end) continue;
+      if (g.b_mode == B_PLAIN) {
+        rb[i] = *reinterpret_cast<const f32x4*>(g.b + (size_t)p * g.ldb + b_c0 + c);
+      } else {
+        const int bb = p / HW, rem = p - bb * HW, h = rem / g.W, w = rem - h * g.W;
+        if (g.b_mode == B_CONV3) {
           const int hs = h + b_dr, ws = w + b_ds;
-          ok = hs >= 0 && hs < g.H && ws >= 0 && ws < g.W;
-          pix = ((size_t)bb * g.H + hs) * g.W + ws;
+          if (hs >= 0 && hs < g.H && ws >= 0 && ws < g.W)
+            rb[i] = *reinterpret_cast<const f32x4*>(g.b + (((size_t)bb * g.H + hs) * g.W + ws) * g.ldb + b_c0 + c);
+        } else {  // B_CONV3_C1: columns are taps 0..8 of a single input channel
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int t = n0 + c + j;
+            if (t < 9) {
+              const int hs = h + t / 3 - 1, ws = w + t % 3 - 1;
+              if (hs >= 0 && hs < g.H && ws >= 0 && ws < g.W)
+                rb[i][j] = g.b[(((size_t)bb * g.H + hs) * g.W + ws) * g.ldb];
+            }
+          }
         }
-        if (ok) rb[i] = *reinterpret_cast<const f32x4*>(g.b + pix * g.ldb + b_c0 + c);
       }
     }
   };
@@ -101,6 +122,7 @@ __global__ __launch_bounds__(256) void wgrad_f32_kernel(WgradArgs g) {
     for (int b = 0; b < TN; ++b)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+  float bsum = 0.f;
 
   const int li = lane & 31, lh = lane >> 5;
   const int nst = (p_end - p_begin + BKP - 1) / BKP;
@@ -114,6 +136,10 @@ __global__ __launch_bounds__(256) void wgrad_f32_kernel(WgradArgs g) {
     if (st + 1 < nst) gload(p_begin + (st + 1) * BKP);
     const float* As = sA[cur];
     const float* Bs = sB[cur];
+    if (do_bias && tid < BM) {
+#pragma unroll
+      for (int r = 0; r < BKP; ++r) bsum += As[r * BM + tid];
+    }
 #pragma unroll
     for (int kk = 0; kk < BKP / 2; ++kk) {
       const int prow = 2 * kk + lh;
@@ -144,33 +170,173 @@ __global__ __launch_bounds__(256) void wgrad_f32_kernel(WgradArgs g) {
         out[(size_t)m * g.Np + n] = acc[a][b][r];
       }
     }
+  if (do_bias && tid < BM) g.part_bias[(size_t)split * g.Mp + m0 + tid] = bsum;
 }
 
-// dst[i] = (acc ? dst[i] : 0) + sum_s part[s][i], fixed order (deterministic)
-__global__ void reduce_slabs_kernel(const float* __restrict__ part, int splits, int64_t n,
-                                    float* __restrict__ dst, int accumulate) {
-  const int64_t n4 = n / 4;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    f32x4 s = accumulate ? reinterpret_cast<f32x4*>(dst)[i] : f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int k = 0; k < splits; ++k) s += reinterpret_cast<const f32x4*>(part + (size_t)k * n)[i];
-    reinterpret_cast<f32x4*>(dst)[i] = s;
+// ---------------------------------------------------------------------------
+// conv3x3 weight gradient, all 9 taps per block from one staged halo.
+//
+// Block tile: 64 output channels (m0) x 64 input channels (c0) x 9 taps; the
+// four waves own the (32-row, 32-col) quadrants, each with 9 accumulators (one
+// per tap, 144 AGPRs). The pixel reduction walks 16-pixel segments of image
+// rows: per stage the block stages dz[16 px][64] and the three input rows
+// h-1..h+1, columns w0-1..w0+16 ([3][18][64], zero padded) once, and every
+// tap reads its shifted window from LDS. 72 MFMAs per wave per barrier; each
+// input element is fetched 3x per block (once per kernel row) instead of 9x.
+// ---------------------------------------------------------------------------
+struct W3Args {
+  const float* x; int ldx;
+  const float* dz; int ldz;
+  int B, H, W, Cin, Cout;
+  int seg_per_split;   // 16-pixel row segments per split
+  int nseg;            // B*H*W/16
+  float* part;         // [splits][Cout][9][Cin]
+  float* part_bias;    // [splits][Cout] or NULL
+};
+
+__global__ __launch_bounds__(256, 2) void wgrad3x3_halo_kernel(W3Args g) {
+  constexpr int SEG = 16, HW_ = SEG + 2, CH = 64;
+  constexpr int X_F4 = 3 * HW_ * CH / 4;  // 864 float4 of halo per stage
+  constexpr int XL = (X_F4 + 255) / 256;  // 4
+  __shared__ __attribute__((aligned(16))) float sD[2][SEG * CH];
+  __shared__ __attribute__((aligned(16))) float sX[2][3 * HW_ * CH];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave & 1, wn = wave >> 1;
+  const int ntc = g.Cin / CH, ntm = g.Cout / CH;
+  const int tiles = ntc * ntm;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = bid / tiles;
+  const int tile = bid - split * tiles;
+  const int m0 = (tile / ntc) * CH, c0 = (tile % ntc) * CH;
+  const int s_begin = split * g.seg_per_split;
+  const int s_end = min(g.nseg, s_begin + g.seg_per_split);
+  const bool do_bias = g.part_bias != nullptr && c0 == 0;
+  const int segs_per_row = g.W / SEG;
+
+  f32x4 rd, rx[XL];
+  auto gload = [&](int sg) {
+    const int row_id = sg / segs_per_row;  // b*H + h
+    const int w0 = (sg - row_id * segs_per_row) * SEG;
+    const int b = row_id / g.H, h = row_id - b * g.H;
+    {
+      const int px = tid >> 4, c4 = (tid & 15) * 4;
+      rd = *reinterpret_cast<const f32x4*>(g.dz + ((size_t)row_id * g.W + w0 + px) * g.ldz + m0 + c4);
+    }
+#pragma unroll
+    for (int i = 0; i < XL; ++i) {
+      const int idx = tid + i * 256;
+      rx[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (idx < X_F4) {
+        const int r = idx / (HW_ * 16), rem = idx - r * (HW_ * 16);
+        const int px = rem >> 4, c4 = (rem & 15) * 4;
+        const int hs = h + r - 1, ws = w0 + px - 1;
+        if (hs >= 0 && hs < g.H && ws >= 0 && ws < g.W)
+          rx[i] = *reinterpret_cast<const f32x4*>(g.x + (((size_t)b * g.H + hs) * g.W + ws) * g.ldx + c0 + c4);
+      }
+    }
+  };
+  auto lstore = [&](int buf) {
+    *reinterpret_cast<f32x4*>(&sD[buf][tid * 4]) = rd;
+#pragma unroll
+    for (int i = 0; i < XL; ++i) {
+      const int idx = tid + i * 256;
+      if (idx < X_F4) *reinterpret_cast<f32x4*>(&sX[buf][idx * 4]) = rx[i];
+    }
+  };
+
+  f32x16 acc[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+  float bsum = 0.f;
+  const int li = lane & 31, lh = lane >> 5;
+  const int nst = s_end - s_begin;
+  if (nst > 0) {
+    gload(s_begin);
+    lstore(0);
   }
-  const int64_t tail0 = n4 * 4;
-  for (int64_t i = tail0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    float s = accumulate ? dst[i] : 0.f;
-    for (int k = 0; k < splits; ++k) s += part[(size_t)k * n + i];
-    dst[i] = s;
+  __syncthreads();
+  for (int st = 0; st < nst; ++st) {
+    const int cur = st & 1;
+    if (st + 1 < nst) gload(s_begin + st + 1);
+    const float* D = sD[cur];
+    const float* X = sX[cur];
+    if (do_bias && tid < CH) {
+#pragma unroll
+      for (int r = 0; r < SEG; ++r) bsum += D[r * CH + tid];
+    }
+#pragma unroll
+    for (int kk = 0; kk < SEG / 2; ++kk) {
+      const int px = 2 * kk + lh;
+      const float a = D[px * CH + wm * 32 + li];
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int r = t / 3, s = t % 3;  // x at (h + r - 1, w + s - 1) = halo (r, px + s)
+        const float bv = X[(r * HW_ + px + s) * CH + wn * 32 + li];
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bv, acc[t], 0, 0, 0);
+      }
+    }
+    if (st + 1 < nst) lstore(cur ^ 1);
+    __syncthreads();
+  }
+  float* out = g.part + (size_t)split * g.Cout * 9 * g.Cin;
+  const int c = c0 + wn * 32 + li;
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int n = m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+      out[((size_t)n * 9 + t) * g.Cin + c] = acc[t][r];
+    }
+  if (do_bias && tid < CH) g.part_bias[(size_t)split * g.Cout + m0 + tid] = bsum;
+}
+
+// dst[i] = (acc ? dst[i] : 0) + sum_s part[s*pitch + i]: every thread sums the
+// slabs of its residue class (fixed order), then a fixed LDS tree: deterministic.
+template <int VEC>
+__global__ __launch_bounds__(256) void reduce_slabs_kernel(const float* __restrict__ part, int splits,
+                                                           int64_t n, int64_t pitch,
+                                                           float* __restrict__ dst, int accumulate,
+                                                           int cols) {
+  typedef float vec __attribute__((ext_vector_type(VEC)));
+  const int groups = 256 / cols;
+  const int gi = threadIdx.x / cols, c = threadIdx.x - gi * cols;
+  const int64_t nv = n / VEC;
+  const int64_t col = (int64_t)blockIdx.x * cols + c;
+  vec s = (vec)(0.f);
+  if (col < nv)
+    for (int k = gi; k < splits; k += groups)
+      s += *reinterpret_cast<const vec*>(part + (size_t)k * pitch + col * VEC);
+  __shared__ vec red[256];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  if (gi == 0 && col < nv) {
+    vec t = accumulate ? *reinterpret_cast<vec*>(dst + col * VEC) : (vec)(0.f);
+    for (int k = 0; k < groups; ++k) t += red[k * cols + c];
+    *reinterpret_cast<vec*>(dst + col * VEC) = t;
   }
 }
 
-int reduce_slabs(const float* part, int splits, int64_t n, float* dst, int accumulate,
-                 hipStream_t s) {
-  const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(cdiv(n / 4 + 1, 256), 2048));
-  hipLaunchKernelGGL(reduce_slabs_kernel, dim3(grid), dim3(256), 0, s, part, splits, n, dst,
-                     accumulate);
+int reduce_slabs_pitched(const float* part, int splits, int64_t n, int64_t pitch, float* dst,
+                         int accumulate, hipStream_t s) {
+  const bool v4 = (n % 4 == 0) && (pitch % 4 == 0) && ((uintptr_t)part % 16 == 0) && ((uintptr_t)dst % 16 == 0);
+  const int64_t nv = v4 ? n / 4 : n;
+  int cols = 64;
+  while (cols > 1 && cols / 2 >= nv) cols /= 2;  // small outputs: more threads per column
+  const int grid = (int)cdiv(nv, cols);
+  if (v4)
+    hipLaunchKernelGGL(reduce_slabs_kernel<4>, dim3(grid), dim3(256), 0, s, part, splits, n, pitch, dst,
+                       accumulate, cols);
+  else
+    hipLaunchKernelGGL(reduce_slabs_kernel<1>, dim3(grid), dim3(256), 0, s, part, splits, n, pitch, dst,
+                       accumulate, cols);
   return launch_status("reduce_slabs");
+}
+
+int reduce_slabs(const float* part, int splits, int64_t n, float* dst, int accumulate, hipStream_t s) {
+  return reduce_slabs_pitched(part, splits, n, n, dst, accumulate, s);
 }
 
 // Column sums: part[split][c] = sum_{p in split} src[p*ld + c]
@@ -197,7 +363,7 @@ __global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ s
   }
 }
 
-// Scalar column sum for C not a multiple of 4 (C = 1 head bias): one sum per block
+// Scalar column sum for C not a multiple of 4: one sum per block and channel
 __global__ __launch_bounds__(256) void colsum1_kernel(const float* __restrict__ src, int ld,
                                                       int64_t npix, int C, int64_t pix_per_split,
                                                       float* __restrict__ part) {
@@ -216,7 +382,7 @@ __global__ __launch_bounds__(256) void colsum1_kernel(const float* __restrict__ 
 }
 
 static void colsum_plan(int64_t npix, int C, int& splits, int64_t& pps) {
-  pps = std::max<int64_t>(1024, cdiv(npix, 1024));
+  pps = std::max<int64_t>(2048, cdiv(npix, 512));
   splits = (int)cdiv(npix, pps);
 }
 
@@ -250,7 +416,7 @@ size_t colsum_ws(int64_t npix, int C) {
 // ---- wgrad planning -------------------------------------------------------
 struct WgradPlan {
   int bm, bn, splits, pps;
-  size_t part_bytes;
+  size_t part_bytes, bias_bytes;
 };
 
 static WgradPlan plan_wgrad(int Mp, int Np, int P, int group_m, int group_n) {
@@ -260,70 +426,40 @@ static WgradPlan plan_wgrad(int Mp, int Np, int P, int group_m, int group_n) {
   p.bn = (Np % 128 == 0 && group_n % 128 == 0) ? 128 : 64;
   const int tiles = (Mp / p.bm) * (Np / p.bn);
   // >= ~2 blocks per CU, fp32 chains of at most 8192 pixels, at least 64 pixels per split
-  const int64_t want_splits = std::max<int64_t>(1, cdiv(512, tiles));
-  int64_t pps = std::max<int64_t>(64, cdiv(P, want_splits));
+  // >= ~8 blocks per CU so the tail wave is short; partial-slab traffic stays
+  // ~2 bytes per 1000 FLOP at >= 512 pixels per split
+  const int64_t want_splits = std::max<int64_t>(1, cdiv(2048, tiles));
+  int64_t pps = std::max<int64_t>(512, cdiv(P, want_splits));
   pps = std::min<int64_t>(pps, 8192);
-  pps = cdiv(pps, 16) * 16;
+  pps = cdiv(pps, 64) * 64;
   p.pps = (int)pps;
   p.splits = (int)cdiv(P, pps);
   p.part_bytes = (size_t)p.splits * Mp * Np * sizeof(float);
+  p.bias_bytes = (size_t)p.splits * Mp * sizeof(float);
   return p;
 }
 
-static int run_wgrad(const WgradArgs& base, const WgradPlan& pl, float* dst, int accumulate,
-                     hipStream_t s) {
+// part slabs at ws, bias slabs right after them (16-byte aligned)
+static float* bias_slabs(void* ws, const WgradPlan& pl) {
+  return (float*)((char*)ws + cdiv(pl.part_bytes, 256) * 256);
+}
+
+static size_t wgrad_ws_bytes(const WgradPlan& pl) { return cdiv(pl.part_bytes, 256) * 256 + pl.bias_bytes + 256; }
+
+static int run_wgrad(const WgradArgs& base, const WgradPlan& pl, hipStream_t s) {
   WgradArgs a = base;
   a.pix_per_split = pl.pps;
   const int tiles = (a.Mp / pl.bm) * (a.Np / pl.bn);
   const dim3 grid(tiles * pl.splits);
   if (pl.bm == 128 && pl.bn == 128)
-    hipLaunchKernelGGL((wgrad_f32_kernel<128, 128>), grid, dim3(256), 0, s, a);
+    hipLaunchKernelGGL((wgrad_f32_kernel<128, 128, 16>), grid, dim3(256), 0, s, a);
   else if (pl.bm == 128)
-    hipLaunchKernelGGL((wgrad_f32_kernel<128, 64>), grid, dim3(256), 0, s, a);
+    hipLaunchKernelGGL((wgrad_f32_kernel<128, 64, 32>), grid, dim3(256), 0, s, a);
   else if (pl.bn == 128)
-    hipLaunchKernelGGL((wgrad_f32_kernel<64, 128>), grid, dim3(256), 0, s, a);
+    hipLaunchKernelGGL((wgrad_f32_kernel<64, 128, 32>), grid, dim3(256), 0, s, a);
   else
-    hipLaunchKernelGGL((wgrad_f32_kernel<64, 64>), grid, dim3(256), 0, s, a);
-  int rc = launch_status("wgrad_f32");
-  if (rc) return rc;
-  return reduce_slabs(a.part, pl.splits, (int64_t)a.Mp * a.Np, dst, accumulate, s);
-}
-
-// Cin == 1 conv wgrad (enc1.conv0): dw[n][t] = sum_p dz[p][n] * x[p+off(t)]
-__global__ __launch_bounds__(256) void wgrad_c1_kernel(const float* __restrict__ x, int ldx,
-                                                       const float* __restrict__ dz, int ldz,
-                                                       int B, int H, int W, int Cout,
-                                                       int pix_per_split, float* __restrict__ part) {
-  // thread owns output channel n = tid % Cout for a subset of rows; Cout <= 256
-  const int HW = H * W, P = B * HW;
-  const int p0 = blockIdx.x * pix_per_split, p1 = min(P, p0 + pix_per_split);
-  const int rows = 256 / Cout;
-  const int n = threadIdx.x % Cout, r = threadIdx.x / Cout;
-  float s[9];
-#pragma unroll
-  for (int t = 0; t < 9; ++t) s[t] = 0.f;
-  if (r < rows) {
-    for (int p = p0 + r; p < p1; p += rows) {
-      const int bb = p / HW, rem = p - bb * HW, h = rem / W, w = rem - h * W;
-      const float d = dz[(size_t)p * ldz + n];
-#pragma unroll
-      for (int t = 0; t < 9; ++t) {
-        const int hh = h + t / 3 - 1, ww = w + t % 3 - 1;
-        const float xv = (hh >= 0 && hh < H && ww >= 0 && ww < W) ? x[((size_t)bb * HW + hh * W + ww) * ldx] : 0.f;
-        s[t] = fmaf(d, xv, s[t]);
-      }
-    }
-  }
-  __shared__ float red[256 * 9];
-#pragma unroll
-  for (int t = 0; t < 9; ++t) red[t * 256 + threadIdx.x] = s[t];
-  __syncthreads();
-  for (int o = threadIdx.x; o < Cout * 9; o += 256) {
-    const int nn = o / 9, t = o - nn * 9;
-    float v = 0.f;
-    for (int k = 0; k < rows; ++k) v += red[t * 256 + k * Cout + nn];
-    part[(size_t)blockIdx.x * Cout * 9 + o] = v;
-  }
+    hipLaunchKernelGGL((wgrad_f32_kernel<64, 64, 32>), grid, dim3(256), 0, s, a);
+  return launch_status("wgrad_f32");
 }
 
 }  // namespace pis
@@ -339,22 +475,53 @@ extern "C" int pis_colsum(const float* src, int ld, int64_t npix, int C, float* 
   return colsum(src, ld, npix, C, out, flags & PIS_ACCUMULATE, ws, ws_bytes, (hipStream_t)stream);
 }
 
-static size_t c1_part_bytes(int P, int Cout, int& splits, int& pps) {
-  pps = std::max(1024, (int)cdiv(P, 512));
-  splits = (int)cdiv(P, pps);
-  return (size_t)splits * Cout * 9 * sizeof(float);
+static WgradPlan conv_plan(int B, int H, int W, int Cin, int Cout) {
+  const int P = B * H * W;
+  if (Cin == 1) return plan_wgrad(Cout, 64, P, Cout, 64);
+  return plan_wgrad(Cout, 9 * Cin, P, Cout, Cin);
+}
+
+struct HaloPlan {
+  bool use;
+  int splits, seg_per_split, nseg;
+  size_t part_bytes, bias_bytes;
+};
+
+static HaloPlan halo_plan(int B, int H, int W, int Cin, int Cout) {
+  HaloPlan p{};
+  p.use = Cin % 64 == 0 && Cout % 64 == 0 && W % 16 == 0;
+  if (!p.use) return p;
+  p.nseg = (int)((int64_t)B * H * W / 16);
+  const int tiles = (Cout / 64) * (Cin / 64);
+  const size_t slab = (size_t)Cout * 9 * Cin * sizeof(float);
+  // ~4 blocks per CU-slot round, 512..8192 pixels per split, <= ~160 MB of partial slabs
+  int64_t splits = cdiv(1024, tiles);
+  splits = std::min<int64_t>(splits, std::max<int64_t>(1, (int64_t)((160u << 20) / slab)));
+  int64_t sps = cdiv(p.nseg, splits);
+  sps = std::max<int64_t>(32, std::min<int64_t>(512, sps));
+  p.seg_per_split = (int)sps;
+  p.splits = (int)cdiv(p.nseg, sps);
+  p.part_bytes = (size_t)p.splits * slab;
+  p.bias_bytes = (size_t)p.splits * Cout * sizeof(float);
+  return p;
 }
 
 extern "C" size_t pis_conv3x3_wgrad_ws(int B, int H, int W, int Cin, int Cout) {
-  const int P = B * H * W;
-  size_t wbytes;
-  if (Cin == 1) {
-    int sp, pps;
-    wbytes = c1_part_bytes(P, Cout, sp, pps);
-  } else {
-    wbytes = plan_wgrad(Cout, 9 * Cin, P, Cout, Cin).part_bytes;
-  }
-  return std::max(wbytes, colsum_ws(P, Cout)) + 256;
+  const HaloPlan hp = halo_plan(B, H, W, Cin, Cout);
+  if (hp.use) return cdiv(hp.part_bytes, 256) * 256 + hp.bias_bytes + 256;
+  const WgradPlan pl = conv_plan(B, H, W, Cin, Cout);
+  // Cin == 1 computes a padded [Cout][64] tile and compacts it through a staging slab
+  const size_t stage = Cin == 1 ? (size_t)Cout * 64 * sizeof(float) + 256 : 0;
+  return wgrad_ws_bytes(pl) + stage;
+}
+
+__global__ void compact_c1_kernel(const float* __restrict__ full, float* __restrict__ dw, int Cout,
+                                  int accumulate) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= Cout * 9) return;
+  const int n = i / 9, t = i - n * 9;
+  const float v = full[n * 64 + t];
+  dw[i] = accumulate ? dw[i] + v : v;
 }
 
 extern "C" int pis_conv3x3_wgrad(const float* x, int ldx, const float* dz, int ldz, float* dw_krsc,
@@ -362,38 +529,54 @@ extern "C" int pis_conv3x3_wgrad(const float* x, int ldx, const float* dz, int l
                                  void* ws, size_t ws_bytes, pis_stream_t stream) {
   PIS_CHECK_ARG(x && dz && dw_krsc && B > 0 && H > 0 && W > 0 && Cin > 0 && Cout > 0,
                 "pis_conv3x3_wgrad: bad arguments");
-  PIS_CHECK_ARG(ws_bytes >= pis_conv3x3_wgrad_ws(B, H, W, Cin, Cout),
+  PIS_CHECK_ARG(ws && ws_bytes >= pis_conv3x3_wgrad_ws(B, H, W, Cin, Cout),
                 "pis_conv3x3_wgrad: workspace too small");
+  PIS_CHECK_ARG(Cout % 64 == 0 && (Cin == 1 || Cin % 64 == 0),
+                "pis_conv3x3_wgrad: Cout must be a multiple of 64 and Cin 1 or a multiple of 64");
+  PIS_CHECK_ARG((Cin == 1 || ldx % 4 == 0) && ldz % 4 == 0, "pis_conv3x3_wgrad: ld must be multiples of 4");
   hipStream_t s = (hipStream_t)stream;
   const int acc = flags & PIS_ACCUMULATE;
-  const int P = B * H * W;
-  int rc;
+  const HaloPlan hp = halo_plan(B, H, W, Cin, Cout);
+  if (hp.use && ldx % 4 == 0) {
+    W3Args a{};
+    a.x = x; a.ldx = ldx; a.dz = dz; a.ldz = ldz;
+    a.B = B; a.H = H; a.W = W; a.Cin = Cin; a.Cout = Cout;
+    a.seg_per_split = hp.seg_per_split; a.nseg = hp.nseg;
+    a.part = (float*)ws;
+    a.part_bias = db ? (float*)((char*)ws + cdiv(hp.part_bytes, 256) * 256) : nullptr;
+    const int tiles = (Cout / 64) * (Cin / 64);
+    hipLaunchKernelGGL(wgrad3x3_halo_kernel, dim3(tiles * hp.splits), dim3(256), 0, s, a);
+    int rc = launch_status("wgrad3x3_halo");
+    if (!rc) rc = reduce_slabs(a.part, hp.splits, (int64_t)Cout * 9 * Cin, dw_krsc, acc, s);
+    if (rc || !db) return rc;
+    return reduce_slabs(a.part_bias, hp.splits, Cout, db, acc, s);
+  }
+  const WgradPlan pl = conv_plan(B, H, W, Cin, Cout);
+  WgradArgs a{};
+  a.a = dz; a.lda = ldz; a.a_up2 = 0; a.Ca = Cout;
+  a.b = x; a.ldb = ldx; a.b_mode = Cin == 1 ? B_CONV3_C1 : B_CONV3; a.Cb = Cin;
+  a.B = B; a.H = H; a.W = W; a.P = B * H * W; a.Mp = Cout; a.Np = Cin == 1 ? 64 : 9 * Cin;
+  a.part = (float*)ws;
+  a.part_bias = db ? bias_slabs(ws, pl) : nullptr;
+  int rc = run_wgrad(a, pl, s);
+  if (rc) return rc;
   if (Cin == 1) {
-    PIS_CHECK_ARG(Cout <= 256, "pis_conv3x3_wgrad: Cin==1 path supports Cout<=256");
-    int splits, pps;
-    c1_part_bytes(P, Cout, splits, pps);
-    hipLaunchKernelGGL(wgrad_c1_kernel, dim3(splits), dim3(256), 0, s, x, ldx, dz, ldz, B, H, W,
-                       Cout, pps, (float*)ws);
-    rc = launch_status("wgrad_c1");
-    if (!rc) rc = reduce_slabs((float*)ws, splits, (int64_t)Cout * 9, dw_krsc, acc, s);
+    float* full = (float*)((char*)ws + wgrad_ws_bytes(pl));
+    rc = reduce_slabs(a.part, pl.splits, (int64_t)Cout * 64, full, 0, s);
+    if (!rc) {
+      hipLaunchKernelGGL(compact_c1_kernel, dim3((unsigned)cdiv(Cout * 9, 256)), dim3(256), 0, s, full,
+                         dw_krsc, Cout, acc);
+      rc = launch_status("compact_c1");
+    }
   } else {
-    PIS_CHECK_ARG(Cin % 64 == 0 && Cout % 64 == 0, "pis_conv3x3_wgrad: Cin/Cout must be multiples of 64");
-    PIS_CHECK_ARG(ldx % 4 == 0 && ldz % 4 == 0, "pis_conv3x3_wgrad: ld must be multiples of 4");
-    WgradPlan pl = plan_wgrad(Cout, 9 * Cin, P, Cout, Cin);
-    WgradArgs a{};
-    a.a = dz; a.lda = ldz; a.a_up2 = 0; a.Ca = Cout;
-    a.b = x; a.ldb = ldx; a.b_conv3 = 1; a.Cb = Cin;
-    a.B = B; a.H = H; a.W = W; a.P = P; a.Mp = Cout; a.Np = 9 * Cin; a.part = (float*)ws;
-    rc = run_wgrad(a, pl, dw_krsc, acc, s);
+    rc = reduce_slabs(a.part, pl.splits, (int64_t)a.Mp * a.Np, dw_krsc, acc, s);
   }
   if (rc || !db) return rc;
-  return colsum(dz, ldz, P, Cout, db, acc, ws, ws_bytes, s);
+  return reduce_slabs(a.part_bias, pl.splits, Cout, db, acc, s);
 }
 
 extern "C" size_t pis_convt2x2_wgrad_ws(int B, int H, int W, int Cin, int Cout) {
-  const int P = B * H * W;
-  const size_t wbytes = plan_wgrad(4 * Cout, Cin, P, Cout, Cin).part_bytes;
-  return std::max(wbytes, colsum_ws((int64_t)4 * P, Cout)) + 256;
+  return wgrad_ws_bytes(plan_wgrad(4 * Cout, Cin, B * H * W, Cout, Cin));
 }
 
 extern "C" int pis_convt2x2_wgrad(const float* x, int ldx, const float* dy, int lddy, float* dw_ijoc,
@@ -403,17 +586,20 @@ extern "C" int pis_convt2x2_wgrad(const float* x, int ldx, const float* dy, int 
                 "pis_convt2x2_wgrad: bad arguments");
   PIS_CHECK_ARG(Cin % 64 == 0 && Cout % 64 == 0, "pis_convt2x2_wgrad: Cin/Cout must be multiples of 64");
   PIS_CHECK_ARG(ldx % 4 == 0 && lddy % 4 == 0, "pis_convt2x2_wgrad: ld must be multiples of 4");
-  PIS_CHECK_ARG(ws_bytes >= pis_convt2x2_wgrad_ws(B, H, W, Cin, Cout),
+  PIS_CHECK_ARG(ws && ws_bytes >= pis_convt2x2_wgrad_ws(B, H, W, Cin, Cout),
                 "pis_convt2x2_wgrad: workspace too small");
   hipStream_t s = (hipStream_t)stream;
   const int acc = flags & PIS_ACCUMULATE;
   const int P = B * H * W;
-  WgradPlan pl = plan_wgrad(4 * Cout, Cin, P, Cout, Cin);
+  const WgradPlan pl = plan_wgrad(4 * Cout, Cin, P, Cout, Cin);
   WgradArgs a{};
   a.a = dy; a.lda = lddy; a.a_up2 = 1; a.Ca = Cout;
-  a.b = x; a.ldb = ldx; a.b_conv3 = 0; a.Cb = Cin;
+  a.b = x; a.ldb = ldx; a.b_mode = B_PLAIN; a.Cb = Cin;
   a.B = B; a.H = H; a.W = W; a.P = P; a.Mp = 4 * Cout; a.Np = Cin; a.part = (float*)ws;
-  int rc = run_wgrad(a, pl, dw_ijoc, acc, s);
+  a.part_bias = db ? bias_slabs(ws, pl) : nullptr;
+  int rc = run_wgrad(a, pl, s);
+  if (!rc) rc = reduce_slabs(a.part, pl.splits, (int64_t)a.Mp * a.Np, dw_ijoc, acc, s);
   if (rc || !db) return rc;
-  return colsum(dy, lddy, (int64_t)4 * P, Cout, db, acc, ws, ws_bytes, s);
+  // bias slabs are [split][i][j][o]: 4*splits slabs of Cout
+  return reduce_slabs(a.part_bias, pl.splits * 4, Cout, db, acc, s);
 }

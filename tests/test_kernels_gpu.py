@@ -61,8 +61,10 @@ def test_conv3x3_fwd(hip, B, H, W, Cin, Cout, ld_extra):
         assert torch.all(y[..., Cout:] == 7.0)  # untouched channel slice
 
 
-@pytest.mark.parametrize("B,H,W,Cin,Cout", [(2, 16, 24, 64, 64), (1, 8, 8, 256, 128), (2, 6, 10, 128, 64)])
+@pytest.mark.parametrize("B,H,W,Cin,Cout", [(2, 16, 24, 64, 64), (1, 8, 8, 256, 128), (2, 6, 10, 128, 64),
+                                           (2, 16, 32, 64, 128), (1, 32, 16, 128, 64), (3, 5, 48, 192, 64)])
 def test_conv3x3_dgrad_wgrad(hip, B, H, W, Cin, Cout):
+    """W % 16 == 0 shapes take the 9-tap halo wgrad kernel, the others the generic one."""
     g = torch.Generator().manual_seed(1)
     x = F.relu(torch.randn(B, Cin, H, W, generator=g))
     w = torch.randn(Cout, Cin, 3, 3, generator=g) / (3 * Cin ** 0.5)

@@ -1,0 +1,98 @@
+"""Per-layer kernel micro-benchmark on the GPU (C2 shapes: B=8, 512^2 input).
+
+Times conv3x3 fwd / dgrad / wgrad through the C-ABI with HIP events, for each
+implicit-GEMM variant in the tuning table, in interleaved rounds inside one
+process (cdna_hip_programming.md §5.4 rule 24). Prints TFLOP/s per layer.
+
+    python tools/bench_kernels.py [--rounds 3] [--variants 16,32]
+"""
+import argparse
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from physics_informed_image_segmentation_amd import _hip  # noqa: E402
+
+LAYERS = [  # name, H, Cin, Cout
+    ("enc1.conv1", 512, 64, 64), ("dec1.conv0", 512, 128, 64), ("enc2.conv1", 256, 128, 128),
+    ("dec2.conv0", 256, 256, 128), ("enc3.conv1", 128, 256, 256), ("dec3.conv0", 128, 512, 256),
+    ("enc4.conv1", 64, 512, 512), ("dec4.conv0", 64, 1024, 512), ("bottleneck", 32, 512, 512),
+]
+B = 8
+
+
+def timed(fn, reps=3):
+    fn()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--variants", default="16,32")
+    ap.add_argument("--layers", default="")
+    ap.add_argument("--noload", action="store_true", help="also time the igemm loop without global loads")
+    args = ap.parse_args()
+    lib = _hip.lib()
+    variants = [int(v) for v in args.variants.split(",")]
+    s = torch.cuda.current_stream().cuda_stream
+    dev = torch.device("cuda")
+    sel = [l for l in LAYERS if not args.layers or l[0] in args.layers.split(",")]
+    results = {}
+    for name, H, cin, cout in sel:
+        x = torch.rand(B, H, H, cin, device=dev)
+        dz = torch.randn(B, H, H, cout, device=dev)
+        w = torch.randn(cout, 3, 3, cin, device=dev) * 0.05
+        bias = torch.randn(cout, device=dev)
+        wf = torch.empty(cin * 9 * cout, device=dev)
+        lib.pis_conv3x3_flip(w.data_ptr(), wf.data_ptr(), cin, cout, s)
+        y = torch.empty(B, H, H, cout, device=dev)
+        dx = torch.empty(B, H, H, cin, device=dev)
+        nws = lib.pis_conv3x3_wgrad_ws(B, H, H, cin, cout)
+        ws = torch.empty(nws // 4 + 1, device=dev)
+        dw = torch.empty(cout * 9 * cin, device=dev)
+        db = torch.empty(cout, device=dev)
+        flops = 2.0 * B * H * H * cout * cin * 9
+        ops = {
+            "fwd": lambda: lib.pis_conv3x3_fwd(x.data_ptr(), cin, w.data_ptr(), bias.data_ptr(), 0, y.data_ptr(), cout,
+                                               B, H, H, cin, cout, 1, s),
+            "dgrad": lambda: lib.pis_conv3x3_dgrad(dz.data_ptr(), cout, wf.data_ptr(), x.data_ptr(), cin, 0,
+                                                   dx.data_ptr(), cin, B, H, H, cin, cout, 4, s),
+            "wgrad": lambda: lib.pis_conv3x3_wgrad(x.data_ptr(), cin, dz.data_ptr(), cout, dw.data_ptr(),
+                                                   db.data_ptr(), B, H, H, cin, cout, 0, ws.data_ptr(), nws, s),
+        }
+        vlist = list(variants) + ([-v for v in variants] if args.noload else [])
+        for r in range(args.rounds):
+            for v in vlist:
+                lib.pis_tune(1, abs(v))
+                lib.pis_tune(2, 1 if v < 0 else 0)
+                for op, fn in ops.items():
+                    if op == "wgrad" and v != vlist[0]:
+                        continue
+                    ms = timed(fn)
+                    results.setdefault((name, op, v), []).append(ms)
+        del x, dz, w, y, dx, ws, dw
+        torch.cuda.empty_cache()
+        for op in ("fwd", "dgrad", "wgrad"):
+            line = f"{name:12s} {op:6s}"
+            for v in vlist:
+                key = (name, op, v)
+                if key in results:
+                    ms = min(results[key])
+                    tag = f"bk{abs(v)}" + ("-noload" if v < 0 else "")
+                    line += f"  {tag}: {ms:7.3f} ms {flops / ms / 1e9:6.1f} TF/s"
+            print(line, flush=True)
+    lib.pis_tune(1, variants[0])
+    lib.pis_tune(2, 0)
+
+
+if __name__ == "__main__":
+    main()
