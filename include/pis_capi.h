@@ -51,7 +51,8 @@ int pis_version(void);
  * value or PIS_ERR_ARG. Defaults are the measured best on MI355X.            */
 #define PIS_TUNE_IGEMM_BK 1 /* implicit-GEMM K-step: 16 or 32 */
 #define PIS_TUNE_DEBUG_NOLOAD 2 /* timing only: implicit GEMM skips its global loads (wrong results) */
-#define PIS_TUNE_NKEYS 3
+#define PIS_TUNE_CONV_HALO 3 /* 1: 3x3 conv fwd/dgrad from a staged input halo (W%16==0, H%8==0) */
+#define PIS_TUNE_NKEYS 4
 #define PIS_DEBUG_NOLOAD (1 << 16)
 int pis_tune(int key, int value);
 

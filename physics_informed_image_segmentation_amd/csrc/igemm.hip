@@ -199,7 +199,153 @@ __global__ __launch_bounds__(256) void igemm_f32_kernel(IGemmArgs g) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// 3x3 conv (fwd, or dgrad on flipped weights) from a staged input halo.
+//
+// Block tile: 128 output pixels = an 8-row x 16-column window of one image,
+// x BN output channels; 2x2 waves, 64 px x BN/2 channels each. The K loop walks
+// 4-channel slices of the input: per stage the block stages the 10x18-pixel
+// input halo of the window ([2][180][2] floats: channel pairs split into two
+// planes so a lane's 8-byte read is conflict-free) and the weights of all 9
+// taps ([9][2][BN][2]) once, then every tap reads its shifted window from LDS:
+// 72 MFMAs per wave per barrier, and each input element is fetched once per
+// block instead of once per tap. MFMA t of a channel pair uses channel 2h + t
+// in lane half h for both operands, so the sum is unchanged.
+// ---------------------------------------------------------------------------
+template <int BN>
+__global__ __launch_bounds__(256) void conv3x3_halo_kernel(IGemmArgs g) {
+  constexpr int TR = 8, TC = 16, HR = TR + 2, HC = TC + 2, HP = HR * HC;  // 180 halo pixels
+  constexpr int TM = 2, TN = BN / 64;
+  constexpr int WL = (9 * BN + 255) / 256;  // weight float4 loads per thread per stage
+  __shared__ __attribute__((aligned(16))) float sX[2][2 * HP * 2];
+  __shared__ __attribute__((aligned(16))) float sW[2][9 * 2 * BN * 2];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave & 1, wn = wave >> 1;
+  const int li = lane & 31, lh = lane >> 5;
+  const int ntn = (g.N + BN - 1) / BN;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int tile = bid / ntn, n0 = (bid % ntn) * BN;
+  const int tpr = g.W / TC, tpi = (g.H / TR) * tpr;  // tiles per tile-row, per image
+  const int b = tile / tpi, trem = tile - b * tpi;
+  const int h0 = (trem / tpr) * TR, w0 = (trem % tpr) * TC;
+  const int nchunks = g.Csrc / 4;
+
+  // halo staging: thread t < 180 loads pixel t's 4 channels
+  const int hr = tid / HC, hc = tid - (tid / HC) * HC;
+  const int hs = h0 + hr - 1, ws = w0 + hc - 1;
+  const bool x_ok = tid < HP && hs >= 0 && hs < g.H && ws >= 0 && ws < g.W;
+  const float* xsrc = g.src + (((size_t)b * g.H + (x_ok ? hs : 0)) * g.W + (x_ok ? ws : 0)) * g.lds;
+
+  f32x4 rx, rw[WL];
+  auto gload = [&](int kc) {
+    const int c = kc * 4;
+    rx = x_ok ? *reinterpret_cast<const f32x4*>(xsrc + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < WL; ++i) {
+      const int idx = tid + i * 256;  // (tap, n) pair
+      const int t = idx / BN, nl = idx - t * BN;
+      rw[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (t < 9 && n0 + nl < g.N)
+        rw[i] = *reinterpret_cast<const f32x4*>(g.wt + (size_t)(n0 + nl) * g.ldw + t * g.Csrc + c);
+    }
+  };
+  auto lstore = [&](int buf) {
+    if (tid < HP) {
+      float* X = sX[buf];
+      *reinterpret_cast<float2*>(&X[(0 * HP + tid) * 2]) = make_float2(rx[0], rx[1]);
+      *reinterpret_cast<float2*>(&X[(1 * HP + tid) * 2]) = make_float2(rx[2], rx[3]);
+    }
+#pragma unroll
+    for (int i = 0; i < WL; ++i) {
+      const int idx = tid + i * 256;
+      const int t = idx / BN, nl = idx - t * BN;
+      if (t < 9) {
+        float* Wt = sW[buf];
+        *reinterpret_cast<float2*>(&Wt[((t * 2 + 0) * BN + nl) * 2]) = make_float2(rw[i][0], rw[i][1]);
+        *reinterpret_cast<float2*>(&Wt[((t * 2 + 1) * BN + nl) * 2]) = make_float2(rw[i][2], rw[i][3]);
+      }
+    }
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int c = 0; c < TN; ++c)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][c][r] = 0.f;
+
+  // this lane's output pixels (rows of its two 32-row MFMA tiles)
+  int pbase[TM];
+#pragma unroll
+  for (int a = 0; a < TM; ++a) {
+    const int idx = wm * 64 + a * 32 + li;
+    pbase[a] = (idx / TC) * HC + (idx % TC);
+  }
+
+  gload(0);
+  lstore(0);
+  __syncthreads();
+  for (int kc = 0; kc < nchunks; ++kc) {
+    const int cur = kc & 1;
+    if (kc + 1 < nchunks) gload(kc + 1);
+    const float* X = sX[cur] + lh * HP * 2;
+    const float* Wt = sW[cur];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int toff = (t / 3) * HC + (t % 3);
+      float2 af[TM], bf[TN];
+#pragma unroll
+      for (int a = 0; a < TM; ++a) af[a] = *reinterpret_cast<const float2*>(&X[(pbase[a] + toff) * 2]);
+#pragma unroll
+      for (int c = 0; c < TN; ++c)
+        bf[c] = *reinterpret_cast<const float2*>(&Wt[((t * 2 + lh) * BN + wn * (BN / 2) + c * 32 + li) * 2]);
+#pragma unroll
+      for (int a = 0; a < TM; ++a)
+#pragma unroll
+        for (int c = 0; c < TN; ++c) {
+          acc[a][c] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[a].x, bf[c].x, acc[a][c], 0, 0, 0);
+          acc[a][c] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[a].y, bf[c].y, acc[a][c], 0, 0, 0);
+        }
+    }
+    if (kc + 1 < nchunks) lstore(cur ^ 1);
+    __syncthreads();
+  }
+
+  const int HWimg = g.H * g.W;
+#pragma unroll
+  for (int c = 0; c < TN; ++c) {
+    const int n = n0 + wn * (BN / 2) + c * 32 + li;
+    if (n >= g.N) continue;
+    const float bias_n = g.bias ? g.bias[n] : 0.f;
+    const float sc = (g.flags & PIS_SCALE) ? g.scale[(size_t)b * g.N + n] : 1.f;
+#pragma unroll
+    for (int a = 0; a < TM; ++a) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int idx = wm * 64 + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        const size_t m = (size_t)b * HWimg + (size_t)(h0 + idx / TC) * g.W + w0 + idx % TC;
+        float v = acc[a][c][r] + bias_n;
+        if (g.flags & PIS_RELU) v = fmaxf(v, 0.f);
+        if (g.flags & PIS_MASK) v = (g.mask[m * g.ldm + n] > 0.f) ? v : 0.f;
+        v *= sc;
+        const size_t off = m * g.ldd + n;
+        if (g.flags & PIS_ACCUMULATE) v += g.dst[off];
+        g.dst[off] = v;
+      }
+    }
+  }
+}
+
+static bool halo_ok(const IGemmArgs& a) {
+  return a.tap_mode == TAP_CONV3 && a.epi == EPI_NHWC && a.W % 16 == 0 && a.H % 8 == 0 &&
+         a.Csrc % 4 == 0 && a.lds % 4 == 0 && a.ldw % 4 == 0;
+}
+
 int tune_get(int key);
+
+static int launch_conv3x3(const IGemmArgs& a, hipStream_t s);
 
 static int launch_igemm(const IGemmArgs& a, hipStream_t s) {
   // tile choice: BN=64 for narrow outputs, BM=128; K-step from the tuning table
@@ -221,6 +367,16 @@ static int launch_igemm(const IGemmArgs& a, hipStream_t s) {
       hipLaunchKernelGGL((igemm_f32_kernel<128, 128, 16>), dim3(grid), dim3(256), 0, s, a);
   }
   return launch_status("igemm_f32");
+}
+
+static int launch_conv3x3(const IGemmArgs& a, hipStream_t s) {
+  if (!halo_ok(a) || !tune_get(PIS_TUNE_CONV_HALO)) return launch_igemm(a, s);
+  const int tiles = (a.M / (8 * 16));
+  if (a.N <= 64)
+    hipLaunchKernelGGL((conv3x3_halo_kernel<64>), dim3(tiles * (int)cdiv(a.N, 64)), dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL((conv3x3_halo_kernel<128>), dim3(tiles * (int)cdiv(a.N, 128)), dim3(256), 0, s, a);
+  return launch_status("conv3x3_halo");
 }
 
 __global__ void conv3x3_c1_fwd_kernel(const float* __restrict__ x, int ldx,
@@ -321,7 +477,7 @@ extern "C" int pis_conv3x3_fwd(const float* x, int ldx, const float* w_krsc, con
   a.Csrc = Cin; a.ntaps = 9; a.tap_mode = TAP_CONV3; a.wt = w_krsc; a.ldw = 9 * Cin; a.N = Cout;
   a.epi = EPI_NHWC; a.bias = bias; a.scale = scale; a.dst = y; a.ldd = ldy;
   a.flags = flags & (PIS_RELU | PIS_SCALE | PIS_ACCUMULATE);
-  return launch_igemm(a, s);
+  return launch_conv3x3(a, s);
 }
 
 extern "C" int pis_conv3x3_flip(const float* w_krsc, float* w_flip, int Cin, int Cout,
@@ -347,7 +503,7 @@ extern "C" int pis_conv3x3_dgrad(const float* dz, int ldz, const float* w_flip, 
   a.Csrc = Cout; a.ntaps = 9; a.tap_mode = TAP_CONV3; a.wt = w_flip; a.ldw = 9 * Cout; a.N = Cin;
   a.epi = EPI_NHWC; a.mask = mask; a.ldm = ldm; a.scale = scale; a.dst = dx; a.ldd = lddx;
   a.flags = flags & (PIS_MASK | PIS_SCALE | PIS_ACCUMULATE);
-  return launch_igemm(a, (hipStream_t)stream);
+  return launch_conv3x3(a, (hipStream_t)stream);
 }
 
 extern "C" int pis_convt2x2_fwd(const float* x, int ldx, const float* w_ijoc, const float* bias,

@@ -36,8 +36,11 @@ def s():
 
 
 @pytest.mark.parametrize("B,H,W,Cin,Cout,ld_extra", [(2, 16, 24, 64, 64, 0), (1, 8, 8, 128, 256, 64),
-                                                      (3, 5, 7, 64, 128, 0), (2, 16, 16, 1, 64, 0)])
+                                                      (3, 5, 7, 64, 128, 0), (2, 16, 16, 1, 64, 0),
+                                                      (2, 16, 32, 64, 128, 64), (1, 8, 16, 132, 64, 0),
+                                                      (2, 24, 48, 256, 192, 0)])
 def test_conv3x3_fwd(hip, B, H, W, Cin, Cout, ld_extra):
+    """H % 8 == 0 and W % 16 == 0 shapes take the halo kernel, the others the generic one."""
     g = torch.Generator().manual_seed(0)
     x = torch.randn(B, Cin, H, W, generator=g)
     w = torch.randn(Cout, Cin, 3, 3, generator=g) / (3 * Cin ** 0.5)

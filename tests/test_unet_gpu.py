@@ -79,16 +79,30 @@ def _step_pair(B, H, W, loss_kw, seed=11):
     u = net(img.cuda())
     loss = crit(u, mask.cuda())
     loss.backward()
-    # oracle side
+    # oracle side: the fp32 restatement (the ATen ops the reference runs) ...
     p_ref = ref(img, scales)
     terms = rt.loss_terms(p_ref, mask, **loss_kw)
     terms["loss"].backward()
-    return net, ref, u, crit, p_ref, terms
+    # ... and the same restatement in float64, the exact-arithmetic target for gradients
+    ref64 = rt.UNetRef().double().train()
+    ref64.load_state_dict(ref.state_dict())
+    p64 = ref64(img.double(), {k: v.double() for k, v in scales.items()})
+    rt.loss_terms(p64, mask.double(), **loss_kw)["loss"].backward()
+    return net, ref, u, crit, p_ref, terms, ref64
 
 
 @pytest.mark.parametrize("loss_kw", [dict(), PDE_KW, dict(rd_w=1e-2, pf_w=1e-2, D=5.0, a=0.5, eps=0.05)])
-def test_train_step_grads(hip, loss_kw):
-    net, ref, u, crit, p_ref, terms = _step_pair(2, 64, 64, loss_kw)
+@pytest.mark.parametrize("shape", [(2, 64, 64), (1, 48, 80)])
+def test_train_step_grads(hip, loss_kw, shape):
+    """Outputs and every loss term vs the fp32 oracle; every parameter gradient vs the
+    float64 oracle, all at the north-star 1e-4 relative tolerance (norm-wise per tensor).
+
+    Why float64 for gradients: a ReLU pre-activation within ~1e-7 of zero flips its
+    mask under fp32 rounding, and the flip propagates to every deeper gradient. On
+    this seed the reference's own fp32 CPU path (oneDNN) flips one dec1.conv0
+    element and one enc2 max-pool argmax and lands 8e-4 from the exact gradients
+    (tools/diag_grads.py); the HIP path is within ~1e-6 of them."""
+    net, ref, u, crit, p_ref, terms, ref64 = _step_pair(*shape, loss_kw)
     assert rel(u, p_ref) < TOL
     got = crit.last["terms"].cpu()
     assert got[0].item() == pytest.approx(terms["loss"].item(), rel=TOL)
@@ -98,17 +112,16 @@ def test_train_step_grads(hip, loss_kw):
         assert got[3].item() == pytest.approx(terms["pde_loss"].item(), rel=TOL)
         assert got[4].item() == pytest.approx(terms["phase_field_loss"].item(), rel=TOL)
     worst = []
-    for (n, p), (n2, q) in zip(net.named_parameters(), ref.named_parameters()):
+    for (n, p), (n2, q) in zip(net.named_parameters(), ref64.named_parameters()):
         assert n == n2
         assert p.grad is not None, n
-        e = rel(p.grad, q.grad)
-        worst.append((e, n))
+        worst.append((rel(p.grad, q.grad), n))
     worst.sort(reverse=True)
     assert worst[0][0] < TOL, worst[:5]
 
 
 def test_grad_accumulation_and_arena(hip):
-    net, ref, u, crit, p_ref, terms = _step_pair(1, 32, 32, dict())
+    net, ref, u, crit, p_ref, terms, _ = _step_pair(1, 32, 32, dict())
     g1 = {n: p.grad.clone() for n, p in net.named_parameters()}
     garena = net.grad_arena()
     assert all(garena.data_ptr() <= p.grad.data_ptr() < garena.data_ptr() + 4 * garena.numel()
@@ -123,24 +136,26 @@ def test_grad_accumulation_and_arena(hip):
 
 
 def test_adamw_two_steps_match_torch(hip):
+    """Two full steps; torch.optim.AdamW on the CPU replica is fed the HIP step's own
+    gradients, so this isolates optimizer + arena plumbing (AdamW's g/sqrt(v)
+    normalisation would amplify the chaotic fp32 gradient noise discussed above)."""
     from physics_informed_image_segmentation_amd import AdamW, DiceBCEPDELoss
     B, H, W = 2, 32, 32
     img, mask = rt.synthetic_batch(B, H, W, seed=5)
     net, ref = make_pair(5)
-    net.eval(), ref.eval()  # no dropout: pure optimizer parity
+    net.eval(), ref.eval()  # no dropout
     opt = AdamW(net.parameters(), lr=1e-3, weight_decay=1e-5)
     opt_ref = rt.make_adamw(ref, lr=1e-3, weight_decay=1e-5)
     crit = DiceBCEPDELoss(pde_weight=1e-4, phase_field_weight=1e-4, diffusion_coeff=5.0, epsilon=0.05)
-    kw = PDE_KW
     for _ in range(2):
         opt.zero_grad()
         crit(net(img.cuda()), mask.cuda()).backward()
+        for p, q in zip(net.parameters(), ref.parameters()):
+            q.grad = p.grad.detach().cpu().clone()
         opt.step()
-        opt_ref.zero_grad()
-        rt.loss_terms(ref(img), mask, **kw)["loss"].backward()
         opt_ref.step()
     worst = max(rel(p, q) for p, q in zip(net.parameters(), ref.parameters()))
-    assert worst < 1e-5
+    assert worst < 1e-6
 
 
 def test_train_epoch_keys_and_validate(hip):
