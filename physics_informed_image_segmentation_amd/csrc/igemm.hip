@@ -49,13 +49,16 @@ __device__ __forceinline__ void tap_offset(int mode, int t, int& dr, int& ds, in
   else { dr = 0; ds = 0; st = 1; }
 }
 
-template <int BM, int BN, int BK>
+// T2D: the 128 rows of an M tile are an 8 x 16 pixel window of one image
+// (needs H % 8 == 0, W % 16 == 0), so pixel coordinates are shifts, not divisions.
+template <int BM, int BN, int BK, bool T2D>
 __global__ __launch_bounds__(256) void igemm_f32_kernel(IGemmArgs g) {
   // row pitch BK+4 floats (80 or 144 bytes): 16 rows land on 16 distinct 16-B slots -> conflict-free ds_read_b128
   constexpr int LDS_ROW = BK + 4;
   constexpr int CPR = BK / 4;                           // float4 chunks per staged row
   constexpr int TM = BM / 64, TN = BN / 64;             // 32x32 tiles per wave (2x2 waves)
   constexpr int AL = BM * CPR / 256, BL = BN * CPR / 256;  // float4 staging loads per thread
+  static_assert(!T2D || BM == 128, "2-D tiles are 8 x 16 pixels");
   __shared__ __attribute__((aligned(16))) float sA[2][BM * LDS_ROW];
   __shared__ __attribute__((aligned(16))) float sB[2][BN * LDS_ROW];
 
@@ -64,6 +67,14 @@ __global__ __launch_bounds__(256) void igemm_f32_kernel(IGemmArgs g) {
   const int ntn = (g.N + BN - 1) / BN;
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int m0 = (bid / ntn) * BM, n0 = (bid % ntn) * BN;
+  int tb = 0, th0 = 0, tw0 = 0;
+  if (T2D) {
+    const int tile = bid / ntn, tpr = g.W / 16, tpi = (g.H / 8) * tpr;
+    tb = tile / tpi;
+    const int trem = tile - tb * tpi;
+    th0 = (trem / tpr) * 8;
+    tw0 = (trem % tpr) * 16;
+  }
 
   // per-thread staging rows (fixed over the K loop)
   int a_b[AL], a_h[AL], a_w[AL];
@@ -72,6 +83,13 @@ __global__ __launch_bounds__(256) void igemm_f32_kernel(IGemmArgs g) {
 #pragma unroll
   for (int i = 0; i < AL; ++i) {
     const int row = (tid + i * 256) / CPR;
+    if (T2D) {
+      a_ok[i] = true;
+      a_b[i] = tb;
+      a_h[i] = th0 + (row >> 4);
+      a_w[i] = tw0 + (row & 15);
+      continue;
+    }
     const int m = m0 + row;
     a_ok[i] = m < g.M;
     const int mm = a_ok[i] ? m : 0;
@@ -178,15 +196,27 @@ __global__ __launch_bounds__(256) void igemm_f32_kernel(IGemmArgs g) {
     for (int a = 0; a < TM; ++a) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int m = m0 + wm * (BM / 2) + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-        if (m >= g.M) continue;
+        const int ridx = wm * (BM / 2) + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        int m, bb, h, w;
+        if (T2D) {
+          bb = tb;
+          h = th0 + (ridx >> 4);
+          w = tw0 + (ridx & 15);
+          m = (bb * g.H + h) * g.W + w;
+        } else {
+          m = m0 + ridx;
+          if (m >= g.M) continue;
+          bb = m / HW;
+          const int rem = m - bb * HW;
+          h = rem / g.W;
+          w = rem - h * g.W;
+        }
         float v = acc[a][b][r] + bias_n;
         if (g.flags & PIS_RELU) v = fmaxf(v, 0.f);
         if (g.flags & PIS_MASK) v = (g.mask[(size_t)m * g.ldm + n] > 0.f) ? v : 0.f;
-        if (g.flags & PIS_SCALE) v *= g.scale[(size_t)(m / HW) * g.N + n];
+        if (g.flags & PIS_SCALE) v *= g.scale[(size_t)bb * g.N + n];
         size_t off;
         if (g.epi == EPI_SCATTER2) {
-          const int bb = m / HW, rem = m - bb * HW, h = rem / g.W, w = rem - h * g.W;
           const int oh = 2 * h + (ij >> 1), ow = 2 * w + (ij & 1);
           off = (((size_t)bb * 2 * g.H + oh) * (2 * g.W) + ow) * g.ldd + o;
         } else {
@@ -238,7 +268,9 @@ __global__ __launch_bounds__(256) void conv3x3_halo_kernel(IGemmArgs g) {
   const float* xsrc = g.src + (((size_t)b * g.H + (x_ok ? hs : 0)) * g.W + (x_ok ? ws : 0)) * g.lds;
 
   f32x4 rx, rw[WL];
+  const bool noload = g.flags & PIS_DEBUG_NOLOAD;  // timing-only: LDS + MFMA ceiling of this loop
   auto gload = [&](int kc) {
+    if (noload && kc > 0) return;
     const int c = kc * 4;
     rx = x_ok ? *reinterpret_cast<const f32x4*>(xsrc + c) : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -353,24 +385,30 @@ static int launch_igemm(const IGemmArgs& a, hipStream_t s) {
   const int bk = tune_get(PIS_TUNE_IGEMM_BK);
   IGemmArgs& m = const_cast<IGemmArgs&>(a);
   if (tune_get(PIS_TUNE_DEBUG_NOLOAD)) m.flags |= PIS_DEBUG_NOLOAD;
+  const bool t2d = a.W % 16 == 0 && a.H % 8 == 0 && bk != 32;
   if (a.N <= 64) {
     const int grid = ntm * (int)cdiv(a.N, 64);
     if (bk == 32)
-      hipLaunchKernelGGL((igemm_f32_kernel<128, 64, 32>), dim3(grid), dim3(256), 0, s, a);
+      hipLaunchKernelGGL((igemm_f32_kernel<128, 64, 32, false>), dim3(grid), dim3(256), 0, s, a);
+    else if (t2d)
+      hipLaunchKernelGGL((igemm_f32_kernel<128, 64, 16, true>), dim3(grid), dim3(256), 0, s, a);
     else
-      hipLaunchKernelGGL((igemm_f32_kernel<128, 64, 16>), dim3(grid), dim3(256), 0, s, a);
+      hipLaunchKernelGGL((igemm_f32_kernel<128, 64, 16, false>), dim3(grid), dim3(256), 0, s, a);
   } else {
     const int grid = ntm * (int)cdiv(a.N, 128);
     if (bk == 32)
-      hipLaunchKernelGGL((igemm_f32_kernel<128, 128, 32>), dim3(grid), dim3(256), 0, s, a);
+      hipLaunchKernelGGL((igemm_f32_kernel<128, 128, 32, false>), dim3(grid), dim3(256), 0, s, a);
+    else if (t2d)
+      hipLaunchKernelGGL((igemm_f32_kernel<128, 128, 16, true>), dim3(grid), dim3(256), 0, s, a);
     else
-      hipLaunchKernelGGL((igemm_f32_kernel<128, 128, 16>), dim3(grid), dim3(256), 0, s, a);
+      hipLaunchKernelGGL((igemm_f32_kernel<128, 128, 16, false>), dim3(grid), dim3(256), 0, s, a);
   }
   return launch_status("igemm_f32");
 }
 
 static int launch_conv3x3(const IGemmArgs& a, hipStream_t s) {
   if (!halo_ok(a) || !tune_get(PIS_TUNE_CONV_HALO)) return launch_igemm(a, s);
+  if (tune_get(PIS_TUNE_DEBUG_NOLOAD)) const_cast<IGemmArgs&>(a).flags |= PIS_DEBUG_NOLOAD;
   const int tiles = (a.M / (8 * 16));
   if (a.N <= 64)
     hipLaunchKernelGGL((conv3x3_halo_kernel<64>), dim3(tiles * (int)cdiv(a.N, 64)), dim3(256), 0, s, a);

@@ -306,9 +306,22 @@ __global__ __launch_bounds__(256) void reduce_slabs_kernel(const float* __restri
   const int64_t nv = n / VEC;
   const int64_t col = (int64_t)blockIdx.x * cols + c;
   vec s = (vec)(0.f);
-  if (col < nv)
-    for (int k = gi; k < splits; k += groups)
-      s += *reinterpret_cast<const vec*>(part + (size_t)k * pitch + col * VEC);
+  if (col < nv) {
+    // 8 independent partial sums keep 8 loads in flight per thread; combined in a fixed order
+    vec s8[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s8[u] = (vec)(0.f);
+    int k = gi;
+    for (; k + 7 * groups < splits; k += 8 * groups) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        s8[u] += *reinterpret_cast<const vec*>(part + (size_t)(k + u * groups) * pitch + col * VEC);
+    }
+    for (int u = 0; k < splits; k += groups, ++u)
+      s8[u & 7] += *reinterpret_cast<const vec*>(part + (size_t)k * pitch + col * VEC);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s += s8[u];
+  }
   __shared__ vec red[256];
   red[threadIdx.x] = s;
   __syncthreads();
@@ -323,8 +336,11 @@ int reduce_slabs_pitched(const float* part, int splits, int64_t n, int64_t pitch
                          int accumulate, hipStream_t s) {
   const bool v4 = (n % 4 == 0) && (pitch % 4 == 0) && ((uintptr_t)part % 16 == 0) && ((uintptr_t)dst % 16 == 0);
   const int64_t nv = v4 ? n / 4 : n;
-  int cols = 64;
-  while (cols > 1 && cols / 2 >= nv) cols /= 2;  // small outputs: more threads per column
+  // threads per column-block: up to 64 slab groups for many slabs, narrower blocks for small outputs
+  int gwant = 1;
+  while (gwant < 64 && gwant < splits) gwant *= 2;
+  int cols = std::max(4, 256 / gwant);
+  while (cols > 1 && cols / 2 >= nv) cols /= 2;
   const int grid = (int)cdiv(nv, cols);
   if (v4)
     hipLaunchKernelGGL(reduce_slabs_kernel<4>, dim3(grid), dim3(256), 0, s, part, splits, n, pitch, dst,

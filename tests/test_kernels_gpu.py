@@ -120,8 +120,10 @@ def test_conv3x3_c1_wgrad(hip):
     assert rel_err(db.cpu(), dz.sum(dim=(0, 2, 3))) < 1e-5
 
 
-@pytest.mark.parametrize("B,H,W,Cin,Cout", [(2, 8, 12, 128, 64), (1, 4, 4, 512, 512), (2, 3, 5, 256, 128)])
+@pytest.mark.parametrize("B,H,W,Cin,Cout", [(2, 8, 12, 128, 64), (1, 4, 4, 512, 512), (2, 3, 5, 256, 128),
+                                           (2, 8, 16, 128, 64), (1, 16, 32, 256, 128)])
 def test_convt2x2(hip, B, H, W, Cin, Cout):
+    """H % 8 == 0 and W % 16 == 0 inputs use 8x16-pixel tiles (shift-only pixel indexing)."""
     g = torch.Generator().manual_seed(3)
     x = F.relu(torch.randn(B, Cin, H, W, generator=g)).requires_grad_(True)
     w = (torch.randn(Cin, Cout, 2, 2, generator=g) / Cin ** 0.5).requires_grad_(True)
