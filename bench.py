@@ -57,26 +57,35 @@ def conv_flops_per_image(H: int, W: int, c: int = 64) -> float:
 
 
 IGEMM_CALLS = ("pis_conv3x3_fwd", "pis_conv3x3_dgrad", "pis_convt2x2_fwd", "pis_convt2x2_dgrad")
-DOMINANT = "igemm_f32_kernel<128, 128>"
+DOMINANT = "conv3x3_halo_kernel<128, 4>"
 
 
 def igemm_shape(name, a):
-    """(M, N, K, kernel) of the implicit GEMM one C-ABI call launches (csrc/igemm.hip dispatch)."""
-    if name == "pis_conv3x3_fwd":
-        Bb, Hh, Ww, cin, cout = a[7:12]
-        if cin == 1:
-            return None
-        M, N, K = Bb * Hh * Ww, cout, 9 * cin
-    elif name == "pis_conv3x3_dgrad":
-        Bb, Hh, Ww, cin, cout = a[8:13]
-        M, N, K = Bb * Hh * Ww, cin, 9 * cout
-    elif name == "pis_convt2x2_fwd":
+    """(M, N, K, kernel) of the implicit GEMM one C-ABI call launches (mirrors the
+    dispatch in csrc/igemm.hip: 3x3 convs on H%8 == 0, W%16 == 0 grids take the
+    halo kernel, BN = 64 for <= 64 output channels)."""
+    if name in ("pis_conv3x3_fwd", "pis_conv3x3_dgrad"):
+        if name == "pis_conv3x3_fwd":
+            Bb, Hh, Ww, cin, cout = a[7:12]
+            if cin == 1:
+                return None
+            M, N, K, csrc, flags = Bb * Hh * Ww, cout, 9 * cin, cin, a[12]
+        else:
+            Bb, Hh, Ww, cin, cout = a[8:13]
+            M, N, K, csrc, flags = Bb * Hh * Ww, cin, 9 * cout, cout, a[13]
+        bn = 64 if N <= 64 else 128
+        if Hh % 8 == 0 and Ww % 16 == 0 and csrc % 4 == 0:
+            ck = 8 if bn == 64 and csrc % 8 == 0 and not flags & 4 else 4  # PIS_MASK -> 4-channel slices
+            return M, N, K, f"conv3x3_halo_kernel<{bn}, {ck}>"
+        return M, N, K, f"igemm_f32_kernel<128, {bn}, 16, false>"
+    if name == "pis_convt2x2_fwd":
         Bb, Hh, Ww, cin, cout = a[6:11]
         M, N, K = Bb * Hh * Ww, 4 * cout, cin
     else:
         Bb, Hh, Ww, cin, cout = a[7:12]
         M, N, K = Bb * Hh * Ww, cin, 4 * cout
-    return M, N, K, ("igemm_f32_kernel<128, 64>" if N <= 64 else DOMINANT)
+    t2d = "true" if (Hh % 8 == 0 and Ww % 16 == 0) else "false"
+    return M, N, K, f"igemm_f32_kernel<128, {64 if N <= 64 else 128}, 16, {t2d}>"
 
 
 class LaunchTimer:

@@ -52,7 +52,8 @@ int pis_version(void);
 #define PIS_TUNE_IGEMM_BK 1 /* implicit-GEMM K-step: 16 or 32 */
 #define PIS_TUNE_DEBUG_NOLOAD 2 /* timing only: implicit GEMM skips its global loads (wrong results) */
 #define PIS_TUNE_CONV_HALO 3 /* 1: 3x3 conv fwd/dgrad from a staged input halo (W%16==0, H%8==0) */
-#define PIS_TUNE_NKEYS 4
+#define PIS_TUNE_HALO_VARIANT 4 /* 0: auto, 1: 4-channel slices for BN=64, 2: BN=256 tiles when N >= 256, 3: 8-channel slices for BN=64 */
+#define PIS_TUNE_NKEYS 5
 #define PIS_DEBUG_NOLOAD (1 << 16)
 int pis_tune(int key, int value);
 

@@ -234,21 +234,24 @@ __global__ __launch_bounds__(256) void igemm_f32_kernel(IGemmArgs g) {
 //
 // Block tile: 128 output pixels = an 8-row x 16-column window of one image,
 // x BN output channels; 2x2 waves, 64 px x BN/2 channels each. The K loop walks
-// 4-channel slices of the input: per stage the block stages the 10x18-pixel
-// input halo of the window ([2][180][2] floats: channel pairs split into two
-// planes so a lane's 8-byte read is conflict-free) and the weights of all 9
-// taps ([9][2][BN][2]) once, then every tap reads its shifted window from LDS:
-// 72 MFMAs per wave per barrier, and each input element is fetched once per
-// block instead of once per tap. MFMA t of a channel pair uses channel 2h + t
-// in lane half h for both operands, so the sum is unchanged.
+// CK-channel slices of the input: per stage the block stages the 10x18-pixel
+// input halo of the window and the weights of all 9 taps once, then every tap
+// reads its shifted window from LDS (9 * CK/2 * TN * 2 MFMAs per wave per
+// barrier), so each input element is fetched once per block instead of once
+// per tap. Both LDS images split the slice into two halves by MFMA lane half:
+// X[h][pixel][CK/2], W[tap][h][n][CK/2]; lane half h supplies channel
+// h*CK/2 + s to MFMA s of the slice for both operands, so the sum is unchanged
+// and every fragment is one contiguous 8- or 16-byte read per lane.
 // ---------------------------------------------------------------------------
-template <int BN>
-__global__ __launch_bounds__(256) void conv3x3_halo_kernel(IGemmArgs g) {
+template <int BN, int CK>
+__global__ __launch_bounds__(256, (BN >= 256 ? 2 : 1)) void conv3x3_halo_kernel(IGemmArgs g) {
   constexpr int TR = 8, TC = 16, HR = TR + 2, HC = TC + 2, HP = HR * HC;  // 180 halo pixels
-  constexpr int TM = 2, TN = BN / 64;
-  constexpr int WL = (9 * BN + 255) / 256;  // weight float4 loads per thread per stage
-  __shared__ __attribute__((aligned(16))) float sX[2][2 * HP * 2];
-  __shared__ __attribute__((aligned(16))) float sW[2][9 * 2 * BN * 2];
+  constexpr int TM = 2, TN = BN / 64, HK = CK / 2;  // HK channels per lane half
+  constexpr int XF4 = HP * CK / 4, WF4 = 9 * BN * CK / 4;  // float4 per stage
+  constexpr int XL = (XF4 + 255) / 256, WL = (WF4 + 255) / 256;
+  typedef float hvec __attribute__((ext_vector_type(HK)));
+  __shared__ __attribute__((aligned(16))) float sX[2][HP * CK];
+  __shared__ __attribute__((aligned(16))) float sW[2][9 * BN * CK];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave & 1, wn = wave >> 1;
@@ -259,43 +262,58 @@ __global__ __launch_bounds__(256) void conv3x3_halo_kernel(IGemmArgs g) {
   const int tpr = g.W / TC, tpi = (g.H / TR) * tpr;  // tiles per tile-row, per image
   const int b = tile / tpi, trem = tile - b * tpi;
   const int h0 = (trem / tpr) * TR, w0 = (trem % tpr) * TC;
-  const int nchunks = g.Csrc / 4;
+  const int nchunks = g.Csrc / CK;
 
-  // halo staging: thread t < 180 loads pixel t's 4 channels
-  const int hr = tid / HC, hc = tid - (tid / HC) * HC;
-  const int hs = h0 + hr - 1, ws = w0 + hc - 1;
-  const bool x_ok = tid < HP && hs >= 0 && hs < g.H && ws >= 0 && ws < g.W;
-  const float* xsrc = g.src + (((size_t)b * g.H + (x_ok ? hs : 0)) * g.W + (x_ok ? ws : 0)) * g.lds;
-
-  f32x4 rx, rw[WL];
+  f32x4 rx[XL], rw[WL];
   const bool noload = g.flags & PIS_DEBUG_NOLOAD;  // timing-only: LDS + MFMA ceiling of this loop
   auto gload = [&](int kc) {
     if (noload && kc > 0) return;
-    const int c = kc * 4;
-    rx = x_ok ? *reinterpret_cast<const f32x4*>(xsrc + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+    const int c = kc * CK;
+#pragma unroll
+    for (int i = 0; i < XL; ++i) {
+      const int idx = tid + i * 256;  // (pixel, 4-channel chunk)
+      const int px = idx / (CK / 4), q = idx - px * (CK / 4);
+      const int hs = h0 + px / HC - 1, ws = w0 + px % HC - 1;
+      rx[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (idx < XF4 && hs >= 0 && hs < g.H && ws >= 0 && ws < g.W)
+        rx[i] = *reinterpret_cast<const f32x4*>(g.src + (((size_t)b * g.H + hs) * g.W + ws) * g.lds + c + 4 * q);
+    }
 #pragma unroll
     for (int i = 0; i < WL; ++i) {
-      const int idx = tid + i * 256;  // (tap, n) pair
-      const int t = idx / BN, nl = idx - t * BN;
+      const int idx = tid + i * 256;  // (tap, n, 4-channel chunk)
+      const int q = idx % (CK / 4), tn = idx / (CK / 4);
+      const int t = tn / BN, nl = tn - t * BN;
       rw[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (t < 9 && n0 + nl < g.N)
-        rw[i] = *reinterpret_cast<const f32x4*>(g.wt + (size_t)(n0 + nl) * g.ldw + t * g.Csrc + c);
+      if (idx < WF4 && n0 + nl < g.N)
+        rw[i] = *reinterpret_cast<const f32x4*>(g.wt + (size_t)(n0 + nl) * g.ldw + t * g.Csrc + c + 4 * q);
     }
   };
   auto lstore = [&](int buf) {
-    if (tid < HP) {
+#pragma unroll
+    for (int i = 0; i < XL; ++i) {
+      const int idx = tid + i * 256;
+      if (idx >= XF4) continue;
+      const int px = idx / (CK / 4), q = idx - px * (CK / 4);
       float* X = sX[buf];
-      *reinterpret_cast<float2*>(&X[(0 * HP + tid) * 2]) = make_float2(rx[0], rx[1]);
-      *reinterpret_cast<float2*>(&X[(1 * HP + tid) * 2]) = make_float2(rx[2], rx[3]);
+      if (CK == 4) {
+        *reinterpret_cast<float2*>(&X[(0 * HP + px) * 2]) = make_float2(rx[i][0], rx[i][1]);
+        *reinterpret_cast<float2*>(&X[(1 * HP + px) * 2]) = make_float2(rx[i][2], rx[i][3]);
+      } else {  // CK == 8: chunk q is lane half q
+        *reinterpret_cast<f32x4*>(&X[(q * HP + px) * 4]) = rx[i];
+      }
     }
 #pragma unroll
     for (int i = 0; i < WL; ++i) {
       const int idx = tid + i * 256;
-      const int t = idx / BN, nl = idx - t * BN;
-      if (t < 9) {
-        float* Wt = sW[buf];
+      if (idx >= WF4) continue;
+      const int q = idx % (CK / 4), tn = idx / (CK / 4);
+      const int t = tn / BN, nl = tn - t * BN;
+      float* Wt = sW[buf];
+      if (CK == 4) {
         *reinterpret_cast<float2*>(&Wt[((t * 2 + 0) * BN + nl) * 2]) = make_float2(rw[i][0], rw[i][1]);
         *reinterpret_cast<float2*>(&Wt[((t * 2 + 1) * BN + nl) * 2]) = make_float2(rw[i][2], rw[i][3]);
+      } else {
+        *reinterpret_cast<f32x4*>(&Wt[((t * 2 + q) * BN + nl) * 4]) = rw[i];
       }
     }
   };
@@ -308,7 +326,7 @@ __global__ __launch_bounds__(256) void conv3x3_halo_kernel(IGemmArgs g) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[a][c][r] = 0.f;
 
-  // this lane's output pixels (rows of its two 32-row MFMA tiles)
+  // this lane's output pixels (rows of its two 32-row MFMA tiles) in halo coordinates
   int pbase[TM];
 #pragma unroll
   for (int a = 0; a < TM; ++a) {
@@ -322,24 +340,24 @@ __global__ __launch_bounds__(256) void conv3x3_halo_kernel(IGemmArgs g) {
   for (int kc = 0; kc < nchunks; ++kc) {
     const int cur = kc & 1;
     if (kc + 1 < nchunks) gload(kc + 1);
-    const float* X = sX[cur] + lh * HP * 2;
+    const float* X = sX[cur] + lh * HP * HK;
     const float* Wt = sW[cur];
 #pragma unroll
     for (int t = 0; t < 9; ++t) {
       const int toff = (t / 3) * HC + (t % 3);
-      float2 af[TM], bf[TN];
+      hvec af[TM], bf[TN];
 #pragma unroll
-      for (int a = 0; a < TM; ++a) af[a] = *reinterpret_cast<const float2*>(&X[(pbase[a] + toff) * 2]);
+      for (int a = 0; a < TM; ++a) af[a] = *reinterpret_cast<const hvec*>(&X[(pbase[a] + toff) * HK]);
 #pragma unroll
       for (int c = 0; c < TN; ++c)
-        bf[c] = *reinterpret_cast<const float2*>(&Wt[((t * 2 + lh) * BN + wn * (BN / 2) + c * 32 + li) * 2]);
+        bf[c] = *reinterpret_cast<const hvec*>(&Wt[((t * 2 + lh) * BN + wn * (BN / 2) + c * 32 + li) * HK]);
 #pragma unroll
-      for (int a = 0; a < TM; ++a)
+      for (int s = 0; s < HK; ++s)
 #pragma unroll
-        for (int c = 0; c < TN; ++c) {
-          acc[a][c] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[a].x, bf[c].x, acc[a][c], 0, 0, 0);
-          acc[a][c] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[a].y, bf[c].y, acc[a][c], 0, 0, 0);
-        }
+        for (int a = 0; a < TM; ++a)
+#pragma unroll
+          for (int c = 0; c < TN; ++c)
+            acc[a][c] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[a][s], bf[c][s], acc[a][c], 0, 0, 0);
     }
     if (kc + 1 < nchunks) lstore(cur ^ 1);
     __syncthreads();
@@ -410,10 +428,20 @@ static int launch_conv3x3(const IGemmArgs& a, hipStream_t s) {
   if (!halo_ok(a) || !tune_get(PIS_TUNE_CONV_HALO)) return launch_igemm(a, s);
   if (tune_get(PIS_TUNE_DEBUG_NOLOAD)) const_cast<IGemmArgs&>(a).flags |= PIS_DEBUG_NOLOAD;
   const int tiles = (a.M / (8 * 16));
-  if (a.N <= 64)
-    hipLaunchKernelGGL((conv3x3_halo_kernel<64>), dim3(tiles * (int)cdiv(a.N, 64)), dim3(256), 0, s, a);
-  else
-    hipLaunchKernelGGL((conv3x3_halo_kernel<128>), dim3(tiles * (int)cdiv(a.N, 128)), dim3(256), 0, s, a);
+  const int variant = tune_get(PIS_TUNE_HALO_VARIANT);
+  if (a.N <= 64) {
+    // 8-channel slices measured faster for the forward convs, 4-channel slices for
+    // the masked dgrad epilogue (tools/bench_kernels.py --key 4 --variants 0,1,3)
+    const bool ck4 = variant == 1 || (variant == 0 && (a.flags & PIS_MASK));
+    if (ck4 || a.Csrc % 8 != 0)
+      hipLaunchKernelGGL((conv3x3_halo_kernel<64, 4>), dim3(tiles * (int)cdiv(a.N, 64)), dim3(256), 0, s, a);
+    else
+      hipLaunchKernelGGL((conv3x3_halo_kernel<64, 8>), dim3(tiles * (int)cdiv(a.N, 64)), dim3(256), 0, s, a);
+  } else if (a.N >= 256 && variant == 2) {
+    hipLaunchKernelGGL((conv3x3_halo_kernel<256, 4>), dim3(tiles * (int)cdiv(a.N, 256)), dim3(256), 0, s, a);
+  } else {
+    hipLaunchKernelGGL((conv3x3_halo_kernel<128, 4>), dim3(tiles * (int)cdiv(a.N, 128)), dim3(256), 0, s, a);
+  }
   return launch_status("conv3x3_halo");
 }
 

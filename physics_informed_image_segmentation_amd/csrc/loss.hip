@@ -4,10 +4,11 @@
 // stencils (src/pde.py:49-212), plus the per-sample thresholded counters the
 // step loop turns into Dice and IoU (src/metrics.py:57-71, src/evaluate.py:81-95).
 //
-// Forward: one pass over p and t (8 B/px from HBM; the stencil neighbours are
-// cache hits) -> per-block partial sums -> one finalize block that reduces the
-// partials in a fixed order (deterministic) and forms every term.
-// Backward: elementwise dL/dp (12 B/px), including the exact adjoint of
+// Forward: one pass over p and t (8 B/px from HBM) in 16x128 pixel tiles, u
+// staged in LDS with a 1-pixel reflect halo -> per-tile partial sums -> one
+// finalize block that reduces the partials in a fixed order (deterministic).
+// Backward: dL/dp (12 B/px) per tile from u staged with a 2-pixel halo and the
+// RD residual of the tile (+1 ring) in LDS, including the exact adjoint of
 // "reflect-pad then stencil": ghost row -1 is row 1 and ghost row n is row
 // n-2, so rows 1 and n-2 receive the boundary residual twice.
 // No MFMA anywhere: these are bandwidth-bound stencils.
@@ -16,51 +17,108 @@
 namespace pis {
 
 __device__ __forceinline__ int refl(int i, int n) { return i < 0 ? -i : (i >= n ? 2 * n - 2 - i : i); }
+__device__ __forceinline__ int clampi(int i, int lo, int hi) { return i < lo ? lo : (i > hi ? hi : i); }
+
+// Tiles of LT_Y x LT_X pixels of one sample; u is staged once in LDS with a
+// reflect-resolved halo, so every stencil neighbour is an LDS read and HBM sees
+// p and t exactly once (rows of the halo are L2 hits of the neighbouring tile).
+constexpr int LT_X = 128, LT_Y = 16, LT_S = LT_X + 8;  // LDS row stride; interior at column 4
+constexpr int LT_Q = LT_X / 4;                          // float4 chunks per tile row
+
+// s[r * LT_S + 4 + c] = u[refl(y0 - halo + r)][refl(x0 + c)],  c in [-halo, LT_X + halo)
+__device__ __forceinline__ void stage_tile(const float* __restrict__ u, int H, int W, int y0,
+                                           int x0, int halo, float* __restrict__ s) {
+  const int rows = LT_Y + 2 * halo;
+  if ((W & 3) == 0 && x0 + LT_X <= W) {
+    for (int k = threadIdx.x; k < rows * LT_Q; k += blockDim.x) {
+      const int r = k / LT_Q, q = k % LT_Q;
+      const int gy = clampi(refl(y0 - halo + r, H), 0, H - 1);
+      *(f32x4*)(s + r * LT_S + 4 + 4 * q) = *(const f32x4*)(u + (size_t)gy * W + x0 + 4 * q);
+    }
+    for (int k = threadIdx.x; k < rows * 2 * halo; k += blockDim.x) {
+      const int r = k / (2 * halo), j = k % (2 * halo);
+      const int c = j < halo ? j - halo : LT_X + j - halo;
+      const int gy = clampi(refl(y0 - halo + r, H), 0, H - 1);
+      s[r * LT_S + 4 + c] = u[(size_t)gy * W + clampi(refl(x0 + c, W), 0, W - 1)];
+    }
+  } else {  // ragged or last tile: element-wise with reflect on both axes
+    const int cols = LT_X + 2 * halo;
+    for (int k = threadIdx.x; k < rows * cols; k += blockDim.x) {
+      const int r = k / cols, c = k % cols - halo;
+      const int gy = clampi(refl(y0 - halo + r, H), 0, H - 1);
+      s[r * LT_S + 4 + c] = u[(size_t)gy * W + clampi(refl(x0 + c, W), 0, W - 1)];
+    }
+  }
+}
+
+// 4 consecutive target values of row y starting at column xb (guarded for ragged W)
+__device__ __forceinline__ f32x4 load4(const float* __restrict__ row, int xb, int W) {
+  if ((W & 3) == 0) return *(const f32x4*)(row + xb);
+  f32x4 v = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    if (xb + i < W) v[i] = row[xb + i];
+  return v;
+}
 
 struct LossArgs {
   const float* p;
   const float* t;
   int B, H, W;
   float dice_w, bce_w, rd_w, pf_w, smooth, D, a, eps, thr;
-  int rows_per_block, blocks_per_sample;
+  int tiles_x, tiles_y;
   float* fpart;  // [nblk][6]: I, P, T, bce_sum, rd_sum, pf_sum
   int* ipart;    // [nblk][3]: I_hat, P_hat, T_hat
 };
 
 template <bool RD, bool PF>
 __global__ __launch_bounds__(256) void loss_fwd_kernel(LossArgs g) {
-  const int b = blockIdx.y;
-  const int y0 = blockIdx.x * g.rows_per_block;
-  const int y1 = min(g.H, y0 + g.rows_per_block);
+  constexpr bool ST = RD || PF;
+  constexpr int HALO = ST ? 1 : 0;
+  __shared__ __attribute__((aligned(16))) float su[ST ? (LT_Y + 2) * LT_S : 1];
+  const int b = blockIdx.z, y0 = blockIdx.y * LT_Y, x0 = blockIdx.x * LT_X;
   const int H = g.H, W = g.W;
   const float* u = g.p + (size_t)b * H * W;
   const float* tt = g.t + (size_t)b * H * W;
+  if (ST) {
+    stage_tile(u, H, W, y0, x0, 1, su);
+    __syncthreads();
+  }
   float s_it = 0.f, s_p = 0.f, s_t = 0.f, s_bce = 0.f, s_rd = 0.f, s_pf = 0.f;
   int c_i = 0, c_p = 0, c_t = 0;
-  const int npx = (y1 - y0) * W;
-  for (int k = threadIdx.x; k < npx; k += blockDim.x) {
-    const int y = y0 + k / W, x = k % W;
-    const float p = u[y * W + x], t = tt[y * W + x];
-    s_it = fmaf(p, t, s_it);
-    s_p += p;
-    s_t += t;
-    s_bce += (t - 1.f) * fmaxf(log1pf(-p), -100.f) - t * fmaxf(logf(p), -100.f);
-    const bool pb = p > g.thr;
-    c_p += pb;
-    c_t += t > 0.5f;
-    c_i += pb && (t > 0.5f);
-    if (RD || PF) {
-      const float uu = u[refl(y - 1, H) * W + x], ud = u[refl(y + 1, H) * W + x];
-      const float ul = u[y * W + refl(x - 1, W)], ur = u[y * W + refl(x + 1, W)];
-      if (RD) {
-        const float lap = uu + ud + ul + ur - 4.f * p;
-        const float r = g.D * lap + p * (1.f - p) * (p - g.a);
-        s_rd = fmaf(r, r, s_rd);
-      }
-      if (PF) {
-        const float gx = 0.5f * (ur - ul), gy = 0.5f * (ud - uu);
-        const float q = p * (1.f - p);
-        s_pf += 0.5f * g.eps * (gx * gx + gy * gy) + q * q / g.eps;
+  for (int k = threadIdx.x; k < LT_Y * LT_Q; k += blockDim.x) {
+    const int r = k / LT_Q, q = k % LT_Q;
+    const int y = y0 + r, xb = x0 + 4 * q;
+    if (y >= H || xb >= W) continue;
+    const f32x4 tv = load4(tt + (size_t)y * W, xb, W);
+    f32x4 pv;
+    if (ST) pv = *(const f32x4*)(su + (r + HALO) * LT_S + 4 + 4 * q);
+    else pv = load4(u + (size_t)y * W, xb, W);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if (xb + i >= W) break;
+      const float p = pv[i], t = tv[i];
+      s_it = fmaf(p, t, s_it);
+      s_p += p;
+      s_t += t;
+      s_bce += (t - 1.f) * fmaxf(log1pf(-p), -100.f) - t * fmaxf(logf(p), -100.f);
+      const bool pb = p > g.thr;
+      c_p += pb;
+      c_t += t > 0.5f;
+      c_i += pb && (t > 0.5f);
+      if (ST) {
+        const float* sc = su + (r + 1) * LT_S + 4 + 4 * q + i;
+        const float uu = sc[-LT_S], ud = sc[LT_S], ul = sc[-1], ur = sc[1];
+        if (RD) {
+          const float lap = uu + ud + ul + ur - 4.f * p;
+          const float rr = g.D * lap + p * (1.f - p) * (p - g.a);
+          s_rd = fmaf(rr, rr, s_rd);
+        }
+        if (PF) {
+          const float gx = 0.5f * (ur - ul), gy = 0.5f * (ud - uu);
+          const float qq = p * (1.f - p);
+          s_pf += 0.5f * g.eps * (gx * gx + gy * gy) + qq * qq / g.eps;
+        }
       }
     }
   }
@@ -83,7 +141,7 @@ __global__ __launch_bounds__(256) void loss_fwd_kernel(LossArgs g) {
     for (int j = 0; j < 3; ++j) ir[wave][j] = c[j];
   }
   __syncthreads();
-  const int blk = b * g.blocks_per_sample + blockIdx.x;
+  const int blk = (b * g.tiles_y + blockIdx.y) * g.tiles_x + blockIdx.x;
   if (threadIdx.x < 6)
     g.fpart[blk * 6 + threadIdx.x] = fr[0][threadIdx.x] + fr[1][threadIdx.x] + fr[2][threadIdx.x] + fr[3][threadIdx.x];
   else if (threadIdx.x < 9) {
@@ -95,7 +153,8 @@ __global__ __launch_bounds__(256) void loss_fwd_kernel(LossArgs g) {
 __global__ __launch_bounds__(256) void loss_finalize_kernel(LossArgs g, float* __restrict__ terms,
                                                             int* __restrict__ counts,
                                                             float* __restrict__ scores) {
-  const int nblk = g.B * g.blocks_per_sample;
+  const int bps = g.tiles_x * g.tiles_y;
+  const int nblk = g.B * bps;
   double s[6] = {0, 0, 0, 0, 0, 0};
   for (int k = threadIdx.x; k < nblk; k += 256)
 #pragma unroll
@@ -107,6 +166,35 @@ __global__ __launch_bounds__(256) void loss_finalize_kernel(LossArgs g, float* _
   if (lane == 0)
 #pragma unroll
     for (int j = 0; j < 6; ++j) red[wave][j] = s[j];
+  // per-sample counters: one wave per sample, lanes stride over the sample's tiles
+  for (int b = wave; b < g.B; b += 4) {
+    long long ci = 0, cp = 0, ct = 0;
+    for (int k = lane; k < bps; k += 64) {
+      const int blk = b * bps + k;
+      ci += g.ipart[blk * 3 + 0];
+      cp += g.ipart[blk * 3 + 1];
+      ct += g.ipart[blk * 3 + 2];
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      ci += __shfl_xor(ci, off, 64);
+      cp += __shfl_xor(cp, off, 64);
+      ct += __shfl_xor(ct, off, 64);
+    }
+    if (lane == 0) {
+      if (counts) {
+        counts[b * 3 + 0] = (int)ci;
+        counts[b * 3 + 1] = (int)cp;
+        counts[b * 3 + 2] = (int)ct;
+      }
+      if (scores) {
+        // fp32 arithmetic exactly as the reference metric (src/metrics.py:67-70, evaluate.py:91-94)
+        const float fi = (float)ci, fp = (float)cp, ft = (float)ct, sm = g.smooth;
+        scores[b * 2 + 0] = (2.f * fi + sm) / (fp + ft + sm);
+        scores[b * 2 + 1] = (fi + sm) / (fp + ft - fi + sm);
+      }
+    }
+  }
   __syncthreads();
   if (threadIdx.x == 0) {
     double tot[6];
@@ -128,26 +216,6 @@ __global__ __launch_bounds__(256) void loss_finalize_kernel(LossArgs g, float* _
     terms[6] = (float)P;
     terms[7] = (float)T;
   }
-  for (int b = threadIdx.x; b < g.B; b += 256) {
-    long long ci = 0, cp = 0, ct = 0;
-    for (int k = 0; k < g.blocks_per_sample; ++k) {
-      const int blk = b * g.blocks_per_sample + k;
-      ci += g.ipart[blk * 3 + 0];
-      cp += g.ipart[blk * 3 + 1];
-      ct += g.ipart[blk * 3 + 2];
-    }
-    if (counts) {
-      counts[b * 3 + 0] = (int)ci;
-      counts[b * 3 + 1] = (int)cp;
-      counts[b * 3 + 2] = (int)ct;
-    }
-    if (scores) {
-      // fp32 arithmetic exactly as the reference metric (src/metrics.py:67-70, evaluate.py:91-94)
-      const float fi = (float)ci, fp = (float)cp, ft = (float)ct, sm = g.smooth;
-      scores[b * 2 + 0] = (2.f * fi + sm) / (fp + ft + sm);
-      scores[b * 2 + 1] = (fi + sm) / (fp + ft - fi + sm);
-    }
-  }
 }
 
 struct LossBwdArgs {
@@ -163,56 +231,88 @@ struct LossBwdArgs {
 
 template <bool RD, bool PF>
 __global__ __launch_bounds__(256) void loss_bwd_kernel(LossBwdArgs g) {
+  constexpr bool ST = RD || PF;
+  __shared__ __attribute__((aligned(16))) float su[ST ? (LT_Y + 4) * LT_S : 1];
+  __shared__ __attribute__((aligned(16))) float sr[RD ? (LT_Y + 2) * LT_S : 1];
+  const int b = blockIdx.z, y0 = blockIdx.y * LT_Y, x0 = blockIdx.x * LT_X;
   const int H = g.H, W = g.W;
-  const int64_t HW = (int64_t)H * W, N = (int64_t)g.B * HW;
+  const size_t HW = (size_t)H * W;
+  const float* u = g.p + b * HW;
+  const float* tt = g.t + b * HW;
+  float* dd = g.dst + b * HW;
   const float I = g.terms[5], P = g.terms[6], T = g.terms[7];
   const float S = P + T + g.smooth;
   const float two_i_s = 2.f * I + g.smooth;
   const float inv_s2 = 1.f / (S * S);
   const float go = g.grad_out ? g.grad_out[0] : 1.f;
-  const float inv_n = (float)(1.0 / (double)N);
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < N;
-       e += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t b = e / HW;
-    const int rem = (int)(e - b * HW);
-    const int y = rem / W, x = rem - y * W;
-    const float* u = g.p + b * HW;
-    const float p = u[rem], t = g.t[e];
-    float grad = g.dice_w * (-(2.f * t * S - two_i_s) * inv_s2);
-    grad += g.bce_w * ((p - t) / fmaxf(p * (1.f - p), 1e-12f) * inv_n);
-    if (RD) {
-      auto R = [&](int yy, int xx) {
-        const float c = u[yy * W + xx];
-        const float lap = u[refl(yy - 1, H) * W + xx] + u[refl(yy + 1, H) * W + xx] +
-                          u[yy * W + refl(xx - 1, W)] + u[yy * W + refl(xx + 1, W)] - 4.f * c;
-        return g.D * lap + c * (1.f - c) * (c - g.a);
-      };
-      const float rk = R(y, x);
-      // adjoint multiplicities of the reflect-padded 5-point stencil
-      const int wu = (y >= 1) + (y == 1), wd = (y <= H - 2) + (y == H - 2);
-      const int wl = (x >= 1) + (x == 1), wr = (x <= W - 2) + (x == W - 2);
-      float adj = -4.f * rk;
-      if (wu) adj += wu * R(y - 1, x);
-      if (wd) adj += wd * R(y + 1, x);
-      if (wl) adj += wl * R(y, x - 1);
-      if (wr) adj += wr * R(y, x + 1);
-      const float fp = -3.f * p * p + 2.f * (1.f + g.a) * p - g.a;
-      grad += g.rd_w * (2.f * inv_n) * (g.D * adj + rk * fp);
+  const float inv_n = (float)(1.0 / ((double)g.B * HW));
+  if (ST) {
+    stage_tile(u, H, W, y0, x0, 2, su);
+    __syncthreads();
+  }
+  if (RD) {
+    // residual r = D Lap(u) + u(1-u)(u-a) on rows y0-1 .. y0+LT_Y, columns x0-1 .. x0+LT_X
+    // (zero outside the image: those slots only meet zero adjoint weights)
+    constexpr int RC = LT_X + 2;
+    for (int k = threadIdx.x; k < (LT_Y + 2) * RC; k += blockDim.x) {
+      const int rr = k / RC, cc = k % RC - 1;
+      const int yy = y0 - 1 + rr, xx = x0 + cc;
+      float r = 0.f;
+      if (yy >= 0 && yy < H && xx >= 0 && xx < W) {
+        const float* sc = su + (rr + 1) * LT_S + 4 + cc;
+        const float c0 = sc[0];
+        const float lap = sc[-LT_S] + sc[LT_S] + sc[-1] + sc[1] - 4.f * c0;
+        r = g.D * lap + c0 * (1.f - c0) * (c0 - g.a);
+      }
+      sr[rr * LT_S + 4 + cc] = r;
     }
-    if (PF) {
-      auto GX = [&](int yy, int xx) { return 0.5f * (u[yy * W + refl(xx + 1, W)] - u[yy * W + refl(xx - 1, W)]); };
-      auto GY = [&](int yy, int xx) { return 0.5f * (u[refl(yy + 1, H) * W + xx] - u[refl(yy - 1, H) * W + xx]); };
-      // gx vanishes on columns 0 and W-1 (reflect), so the ghost folds cancel
-      float adj = 0.f;
-      if (x >= 1) adj += 0.5f * GX(y, x - 1);
-      if (x <= W - 2) adj -= 0.5f * GX(y, x + 1);
-      if (y >= 1) adj += 0.5f * GY(y - 1, x);
-      if (y <= H - 2) adj -= 0.5f * GY(y + 1, x);
-      grad += g.pf_w * inv_n * (g.eps * adj + 2.f * p * (1.f - p) * (1.f - 2.f * p) / g.eps);
+    __syncthreads();
+  }
+  for (int k = threadIdx.x; k < LT_Y * LT_Q; k += blockDim.x) {
+    const int r = k / LT_Q, q = k % LT_Q;
+    const int y = y0 + r, xb = x0 + 4 * q;
+    if (y >= H || xb >= W) continue;
+    const f32x4 tv = load4(tt + (size_t)y * W, xb, W);
+    const f32x4 pv = ST ? *(const f32x4*)(su + (r + 2) * LT_S + 4 + 4 * q) : load4(u + (size_t)y * W, xb, W);
+    f32x4 out;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int x = xb + i;
+      const float p = pv[i], t = tv[i];
+      float grad = g.dice_w * (-(2.f * t * S - two_i_s) * inv_s2);
+      grad += g.bce_w * ((p - t) / fmaxf(p * (1.f - p), 1e-12f) * inv_n);
+      if (RD) {
+        // adjoint multiplicities of the reflect-padded 5-point stencil: ghost row -1 is
+        // row 1 and ghost row H is row H-2, so rows 1 and H-2 receive the boundary twice
+        const float* sc = sr + (r + 1) * LT_S + 4 + 4 * q + i;
+        const float wu = (float)((y >= 1) + (y == 1)), wd = (float)((y <= H - 2) + (y == H - 2));
+        const float wl = (float)((x >= 1) + (x == 1)), wr = (float)((x <= W - 2) + (x == W - 2));
+        const float rk = sc[0];
+        const float adj = -4.f * rk + wu * sc[-LT_S] + wd * sc[LT_S] + wl * sc[-1] + wr * sc[1];
+        const float fp = -3.f * p * p + 2.f * (1.f + g.a) * p - g.a;
+        grad += g.rd_w * (2.f * inv_n) * (g.D * adj + rk * fp);
+      }
+      if (PF) {
+        // gx vanishes on columns 0 and W-1 (reflect), so the ghost folds cancel
+        const float* sc = su + (r + 2) * LT_S + 4 + 4 * q + i;
+        float adj = 0.f;
+        if (x >= 1) adj += 0.25f * (sc[0] - sc[-2]);
+        if (x <= W - 2) adj -= 0.25f * (sc[2] - sc[0]);
+        if (y >= 1) adj += 0.25f * (sc[0] - sc[-2 * LT_S]);
+        if (y <= H - 2) adj -= 0.25f * (sc[2 * LT_S] - sc[0]);
+        grad += g.pf_w * inv_n * (g.eps * adj + 2.f * p * (1.f - p) * (1.f - 2.f * p) / g.eps);
+      }
+      grad *= go;
+      if (g.chain) grad = grad * (1.f - p) * p;
+      out[i] = grad;
     }
-    grad *= go;
-    if (g.chain) grad = grad * (1.f - p) * p;
-    g.dst[e] = grad;
+    if ((W & 3) == 0) {
+      *(f32x4*)(dd + (size_t)y * W + xb) = out;
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (xb + i < W) dd[(size_t)y * W + xb + i] = out[i];
+    }
   }
 }
 
@@ -238,9 +338,9 @@ __global__ void pde_fields_kernel(const float* __restrict__ u0, int B, int H, in
   }
 }
 
-static void loss_plan(int B, int H, int W, int& rows, int& bps) {
-  rows = std::max(1, std::min(H, 4096 / std::max(1, W)));
-  bps = (H + rows - 1) / rows;
+static void loss_plan(int H, int W, int& tiles_x, int& tiles_y) {
+  tiles_x = (W + LT_X - 1) / LT_X;
+  tiles_y = (H + LT_Y - 1) / LT_Y;
 }
 
 }  // namespace pis
@@ -248,9 +348,9 @@ static void loss_plan(int B, int H, int W, int& rows, int& bps) {
 using namespace pis;
 
 extern "C" size_t pis_loss_ws(int B, int H, int W) {
-  int rows, bps;
-  loss_plan(B, H, W, rows, bps);
-  return (size_t)B * bps * (6 * sizeof(float) + 3 * sizeof(int)) + 256;
+  int tx, ty;
+  loss_plan(H, W, tx, ty);
+  return (size_t)B * tx * ty * (6 * sizeof(float) + 3 * sizeof(int)) + 256;
 }
 
 extern "C" int pis_loss_fwd(const float* p, const float* t, int B, int H, int W,
@@ -263,13 +363,13 @@ extern "C" int pis_loss_fwd(const float* p, const float* t, int B, int H, int W,
   g.p = p; g.t = t; g.B = B; g.H = H; g.W = W;
   g.dice_w = prm->dice_w; g.bce_w = prm->bce_w; g.rd_w = prm->rd_w; g.pf_w = prm->pf_w;
   g.smooth = prm->smooth; g.D = prm->D; g.a = prm->a; g.eps = prm->eps; g.thr = prm->thr;
-  loss_plan(B, H, W, g.rows_per_block, g.blocks_per_sample);
+  loss_plan(H, W, g.tiles_x, g.tiles_y);
   g.fpart = (float*)ws;
-  g.ipart = (int*)((char*)ws + (size_t)B * g.blocks_per_sample * 6 * sizeof(float));
+  g.ipart = (int*)((char*)ws + (size_t)B * g.tiles_x * g.tiles_y * 6 * sizeof(float));
   const bool all = prm->flags & PIS_LOSS_ALL_TERMS;
   const bool rd = all || prm->rd_w > 0.f, pf = all || prm->pf_w > 0.f;
   hipStream_t s = (hipStream_t)stream;
-  const dim3 grid(g.blocks_per_sample, B);
+  const dim3 grid(g.tiles_x, g.tiles_y, B);
   if (rd && pf) hipLaunchKernelGGL((loss_fwd_kernel<true, true>), grid, dim3(256), 0, s, g);
   else if (rd) hipLaunchKernelGGL((loss_fwd_kernel<true, false>), grid, dim3(256), 0, s, g);
   else if (pf) hipLaunchKernelGGL((loss_fwd_kernel<false, true>), grid, dim3(256), 0, s, g);
@@ -290,14 +390,15 @@ extern "C" int pis_loss_bwd(const float* p, const float* t, int B, int H, int W,
   g.dice_w = prm->dice_w; g.bce_w = prm->bce_w; g.rd_w = prm->rd_w; g.pf_w = prm->pf_w;
   g.smooth = prm->smooth; g.D = prm->D; g.a = prm->a; g.eps = prm->eps;
   g.terms = terms; g.grad_out = grad_out; g.dst = dst; g.chain = (flags & PIS_LOSS_CHAIN_SIGMOID) ? 1 : 0;
-  const int64_t n = (int64_t)B * H * W;
-  const int grid = (int)std::min<int64_t>(cdiv(n, 256), 8192);
+  int tx, ty;
+  loss_plan(H, W, tx, ty);
+  const dim3 grid(tx, ty, B);
   hipStream_t s = (hipStream_t)stream;
   const bool rd = prm->rd_w > 0.f, pf = prm->pf_w > 0.f;  // gradient only of terms in the total
-  if (rd && pf) hipLaunchKernelGGL((loss_bwd_kernel<true, true>), dim3(grid), dim3(256), 0, s, g);
-  else if (rd) hipLaunchKernelGGL((loss_bwd_kernel<true, false>), dim3(grid), dim3(256), 0, s, g);
-  else if (pf) hipLaunchKernelGGL((loss_bwd_kernel<false, true>), dim3(grid), dim3(256), 0, s, g);
-  else hipLaunchKernelGGL((loss_bwd_kernel<false, false>), dim3(grid), dim3(256), 0, s, g);
+  if (rd && pf) hipLaunchKernelGGL((loss_bwd_kernel<true, true>), grid, dim3(256), 0, s, g);
+  else if (rd) hipLaunchKernelGGL((loss_bwd_kernel<true, false>), grid, dim3(256), 0, s, g);
+  else if (pf) hipLaunchKernelGGL((loss_bwd_kernel<false, true>), grid, dim3(256), 0, s, g);
+  else hipLaunchKernelGGL((loss_bwd_kernel<false, false>), grid, dim3(256), 0, s, g);
   return launch_status("loss_bwd");
 }
 

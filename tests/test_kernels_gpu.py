@@ -250,7 +250,9 @@ def _loss_call(hip, p, t, kw, chain=False, grad_out=None):
     return terms.cpu(), counts.cpu(), scores.cpu(), dst.cpu()
 
 
-@pytest.mark.parametrize("shape", [(2, 9, 11), (8, 64, 64), (1, 2, 3), (3, 130, 70)])
+# shapes cover ragged widths (W % 4 != 0), partial 16x128 tiles, full vector tiles and
+# tiny reflect-padded images
+@pytest.mark.parametrize("shape", [(2, 9, 11), (8, 64, 64), (1, 2, 3), (3, 130, 70), (2, 40, 260), (1, 33, 256)])
 @pytest.mark.parametrize("kw", [dict(), dict(rd_w=1e-4, pf_w=1e-4, D=5.0, a=0.5, eps=0.05),
                                 dict(rd_w=0.3, D=0.5, a=0.3), dict(pf_w=0.2, eps=0.1)])
 def test_fused_loss_vs_oracle(hip, shape, kw):
@@ -267,6 +269,7 @@ def test_fused_loss_vs_oracle(hip, shape, kw):
     gref = ln.loss_backward(p.numpy(), t.numpy(), grad_out=0.75, **kw)
     err = np.linalg.norm(dp.numpy() - gref) / np.linalg.norm(gref)
     assert err < 1e-5
+    assert np.abs(dp.numpy() - gref).max() <= 1e-5 * np.abs(gref).max()  # every pixel, boundaries included
     i, ph, ts = ln.sample_counts(p.numpy(), t.numpy())
     assert np.array_equal(counts.numpy(), np.stack([i, ph, ts], 1))
     d, u = ln.dice_iou_from_counts(i, ph, ts)

@@ -1,10 +1,10 @@
 """Per-layer kernel micro-benchmark on the GPU (C2 shapes: B=8, 512^2 input).
 
 Times conv3x3 fwd / dgrad / wgrad through the C-ABI with HIP events, for each
-implicit-GEMM variant in the tuning table, in interleaved rounds inside one
+value of one tuning knob (pis_tune key), in interleaved rounds inside one
 process (cdna_hip_programming.md §5.4 rule 24). Prints TFLOP/s per layer.
 
-    python tools/bench_kernels.py [--rounds 3] [--variants 16,32]
+    python tools/bench_kernels.py [--key 4] [--variants 0,1,2] [--rounds 3] [--noload]
 """
 import argparse
 import os
@@ -21,6 +21,7 @@ LAYERS = [  # name, H, Cin, Cout
     ("enc4.conv1", 64, 512, 512), ("dec4.conv0", 64, 1024, 512), ("bottleneck", 32, 512, 512),
 ]
 B = 8
+NOLOAD_KEY = 2
 
 
 def timed(fn, reps=3):
@@ -37,16 +38,19 @@ def timed(fn, reps=3):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=3)
-    ap.add_argument("--variants", default="16,32")
+    ap.add_argument("--key", type=int, default=4)
+    ap.add_argument("--variants", default="0")
     ap.add_argument("--layers", default="")
-    ap.add_argument("--noload", action="store_true", help="also time the igemm loop without global loads")
+    ap.add_argument("--ops", default="fwd,dgrad,wgrad")
+    ap.add_argument("--noload", action="store_true", help="also time each variant without global loads")
     args = ap.parse_args()
     lib = _hip.lib()
     variants = [int(v) for v in args.variants.split(",")]
+    default = lib.pis_tune(args.key, -1)
     s = torch.cuda.current_stream().cuda_stream
     dev = torch.device("cuda")
     sel = [l for l in LAYERS if not args.layers or l[0] in args.layers.split(",")]
-    results = {}
+    opsel = args.ops.split(",")
     for name, H, cin, cout in sel:
         x = torch.rand(B, H, H, cin, device=dev)
         dz = torch.randn(B, H, H, cout, device=dev)
@@ -69,29 +73,24 @@ def main():
             "wgrad": lambda: lib.pis_conv3x3_wgrad(x.data_ptr(), cin, dz.data_ptr(), cout, dw.data_ptr(),
                                                    db.data_ptr(), B, H, H, cin, cout, 0, ws.data_ptr(), nws, s),
         }
-        vlist = list(variants) + ([-v for v in variants] if args.noload else [])
-        for r in range(args.rounds):
-            for v in vlist:
-                lib.pis_tune(1, abs(v))
-                lib.pis_tune(2, 1 if v < 0 else 0)
-                for op, fn in ops.items():
-                    if op == "wgrad" and v != vlist[0]:
-                        continue
-                    ms = timed(fn)
-                    results.setdefault((name, op, v), []).append(ms)
+        vlist = [(v, 0) for v in variants] + ([(v, 1) for v in variants] if args.noload else [])
+        results = {}
+        for _ in range(args.rounds):
+            for v, nl in vlist:
+                lib.pis_tune(args.key, v)
+                lib.pis_tune(NOLOAD_KEY, nl)
+                for op in opsel:
+                    results.setdefault((op, v, nl), []).append(timed(ops[op]))
+        lib.pis_tune(args.key, default)
+        lib.pis_tune(NOLOAD_KEY, 0)
+        for op in opsel:
+            line = f"{name:12s} {op:6s}"
+            for v, nl in vlist:
+                ms = min(results[(op, v, nl)])
+                line += f"  v{v}{'-nl' if nl else ''}: {ms:7.3f} ms {flops / ms / 1e9:6.1f} TF/s"
+            print(line, flush=True)
         del x, dz, w, y, dx, ws, dw
         torch.cuda.empty_cache()
-        for op in ("fwd", "dgrad", "wgrad"):
-            line = f"{name:12s} {op:6s}"
-            for v in vlist:
-                key = (name, op, v)
-                if key in results:
-                    ms = min(results[key])
-                    tag = f"bk{abs(v)}" + ("-noload" if v < 0 else "")
-                    line += f"  {tag}: {ms:7.3f} ms {flops / ms / 1e9:6.1f} TF/s"
-            print(line, flush=True)
-    lib.pis_tune(1, variants[0])
-    lib.pis_tune(2, 0)
 
 
 if __name__ == "__main__":
