@@ -25,27 +25,45 @@ __device__ __forceinline__ int clampi(int i, int lo, int hi) { return i < lo ? l
 constexpr int LT_X = 128, LT_Y = 16, LT_S = LT_X + 8;  // LDS row stride; interior at column 4
 constexpr int LT_Q = LT_X / 4;                          // float4 chunks per tile row
 
-// s[r * LT_S + 4 + c] = u[refl(y0 - halo + r)][refl(x0 + c)],  c in [-halo, LT_X + halo)
-__device__ __forceinline__ void stage_tile(const float* __restrict__ u, int H, int W, int y0,
-                                           int x0, int halo, float* __restrict__ s) {
-  const int rows = LT_Y + 2 * halo;
+// s[r * LT_S + 4 + c] = u[refl(y0 - HALO + r)][refl(x0 + c)],  c in [-HALO, LT_X + HALO).
+// Full tiles issue every global load of the tile before the first LDS store, so a
+// block has its whole footprint in flight at once (these kernels are one wave of
+// blocks deep: latency, not issue rate, is what bounds them).
+template <int HALO>
+__device__ __forceinline__ void stage_tile(const float* __restrict__ u, int H, int W, int y0, int x0,
+                                           float* __restrict__ s) {
+  constexpr int ROWS = LT_Y + 2 * HALO;
+  constexpr int NV = ROWS * LT_Q, NVI = (NV + 255) / 256, NH = ROWS * 2 * HALO;
+  static_assert(NH <= 256, "halo columns: one scalar per thread");
   if ((W & 3) == 0 && x0 + LT_X <= W) {
-    for (int k = threadIdx.x; k < rows * LT_Q; k += blockDim.x) {
-      const int r = k / LT_Q, q = k % LT_Q;
-      const int gy = clampi(refl(y0 - halo + r, H), 0, H - 1);
-      *(f32x4*)(s + r * LT_S + 4 + 4 * q) = *(const f32x4*)(u + (size_t)gy * W + x0 + 4 * q);
+    f32x4 v[NVI];
+    float h = 0.f;
+#pragma unroll
+    for (int j = 0; j < NVI; ++j) {
+      const int k = threadIdx.x + 256 * j;
+      if (k < NV) {
+        const int r = k / LT_Q, q = k % LT_Q;
+        const int gy = clampi(refl(y0 - HALO + r, H), 0, H - 1);
+        v[j] = *(const f32x4*)(u + (size_t)gy * W + x0 + 4 * q);
+      }
     }
-    for (int k = threadIdx.x; k < rows * 2 * halo; k += blockDim.x) {
-      const int r = k / (2 * halo), j = k % (2 * halo);
-      const int c = j < halo ? j - halo : LT_X + j - halo;
-      const int gy = clampi(refl(y0 - halo + r, H), 0, H - 1);
-      s[r * LT_S + 4 + c] = u[(size_t)gy * W + clampi(refl(x0 + c, W), 0, W - 1)];
+    const int hr = threadIdx.x / (2 * HALO), hj = threadIdx.x % (2 * HALO);
+    const int hc = hj < HALO ? hj - HALO : LT_X + hj - HALO;
+    if (threadIdx.x < NH) {
+      const int gy = clampi(refl(y0 - HALO + hr, H), 0, H - 1);
+      h = u[(size_t)gy * W + clampi(refl(x0 + hc, W), 0, W - 1)];
     }
+#pragma unroll
+    for (int j = 0; j < NVI; ++j) {
+      const int k = threadIdx.x + 256 * j;
+      if (k < NV) *(f32x4*)(s + (k / LT_Q) * LT_S + 4 + 4 * (k % LT_Q)) = v[j];
+    }
+    if (threadIdx.x < NH) s[hr * LT_S + 4 + hc] = h;
   } else {  // ragged or last tile: element-wise with reflect on both axes
-    const int cols = LT_X + 2 * halo;
-    for (int k = threadIdx.x; k < rows * cols; k += blockDim.x) {
-      const int r = k / cols, c = k % cols - halo;
-      const int gy = clampi(refl(y0 - halo + r, H), 0, H - 1);
+    constexpr int COLS = LT_X + 2 * HALO;
+    for (int k = threadIdx.x; k < ROWS * COLS; k += 256) {
+      const int r = k / COLS, c = k % COLS - HALO;
+      const int gy = clampi(refl(y0 - HALO + r, H), 0, H - 1);
       s[r * LT_S + 4 + c] = u[(size_t)gy * W + clampi(refl(x0 + c, W), 0, W - 1)];
     }
   }
@@ -80,20 +98,43 @@ __global__ __launch_bounds__(256) void loss_fwd_kernel(LossArgs g) {
   const int H = g.H, W = g.W;
   const float* u = g.p + (size_t)b * H * W;
   const float* tt = g.t + (size_t)b * H * W;
-  if (ST) {
-    stage_tile(u, H, W, y0, x0, 1, su);
+  constexpr int NI = LT_Y * LT_Q / 256;  // 4-pixel items per thread
+  f32x4 tvs[NI];
+#pragma unroll
+  for (int j = 0; j < NI; ++j) {  // targets in flight together with the tile of u
+    const int k = threadIdx.x + 256 * j;
+    const int y = y0 + k / LT_Q, xb = x0 + 4 * (k % LT_Q);
+    if (y < H && xb < W) tvs[j] = load4(tt + (size_t)y * W, xb, W);
+  }
+  if constexpr (ST) {
+    stage_tile<1>(u, H, W, y0, x0, su);
     __syncthreads();
   }
-  float s_it = 0.f, s_p = 0.f, s_t = 0.f, s_bce = 0.f, s_rd = 0.f, s_pf = 0.f;
+  // VALU budget is what bounds this kernel (a 4-cycle wave64 VALU op per pixel-term):
+  // BCE in log2 units with v_log_f32 (scaled by ln 2 once per thread), the PF
+  // terms accumulated unscaled, no divisions.
+  constexpr float kLn2 = 0.69314718055994531f, kClamp2 = -144.26950408889634f;  // -100 / ln 2
+  float s_it = 0.f, s_p = 0.f, s_t = 0.f, s_bce2 = 0.f, s_rd = 0.f, s_g2 = 0.f, s_q2 = 0.f;
   int c_i = 0, c_p = 0, c_t = 0;
-  for (int k = threadIdx.x; k < LT_Y * LT_Q; k += blockDim.x) {
+#pragma unroll
+  for (int j = 0; j < NI; ++j) {
+    const int k = threadIdx.x + 256 * j;
     const int r = k / LT_Q, q = k % LT_Q;
     const int y = y0 + r, xb = x0 + 4 * q;
     if (y >= H || xb >= W) continue;
-    const f32x4 tv = load4(tt + (size_t)y * W, xb, W);
-    f32x4 pv;
-    if (ST) pv = *(const f32x4*)(su + (r + HALO) * LT_S + 4 + 4 * q);
-    else pv = load4(u + (size_t)y * W, xb, W);
+    const f32x4 tv = tvs[j];
+    f32x4 pv, uv, dv;
+    float lft = 0.f, rgt = 0.f;
+    if constexpr (ST) {
+      const float* sc = su + (r + 1) * LT_S + 4 + 4 * q;
+      pv = *(const f32x4*)sc;
+      uv = *(const f32x4*)(sc - LT_S);
+      dv = *(const f32x4*)(sc + LT_S);
+      lft = sc[-1];
+      rgt = sc[4];
+    } else {
+      pv = load4(u + (size_t)y * W, xb, W);
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       if (xb + i >= W) break;
@@ -101,27 +142,31 @@ __global__ __launch_bounds__(256) void loss_fwd_kernel(LossArgs g) {
       s_it = fmaf(p, t, s_it);
       s_p += p;
       s_t += t;
-      s_bce += (t - 1.f) * fmaxf(log1pf(-p), -100.f) - t * fmaxf(logf(p), -100.f);
-      const bool pb = p > g.thr;
+      s_bce2 += (t - 1.f) * fmaxf(__builtin_amdgcn_logf(1.f - p), kClamp2) -
+                t * fmaxf(__builtin_amdgcn_logf(p), kClamp2);
+      const bool pb = p > g.thr, tb = t > 0.5f;
       c_p += pb;
-      c_t += t > 0.5f;
-      c_i += pb && (t > 0.5f);
-      if (ST) {
-        const float* sc = su + (r + 1) * LT_S + 4 + 4 * q + i;
-        const float uu = sc[-LT_S], ud = sc[LT_S], ul = sc[-1], ur = sc[1];
+      c_t += tb;
+      c_i += pb && tb;
+      if constexpr (ST) {
+        const float ul = i == 0 ? lft : pv[i - 1], ur = i == 3 ? rgt : pv[i + 1];
+        const float uu = uv[i], ud = dv[i];
+        const float qq = fmaf(-p, p, p);  // p (1 - p)
         if (RD) {
-          const float lap = uu + ud + ul + ur - 4.f * p;
-          const float rr = g.D * lap + p * (1.f - p) * (p - g.a);
+          const float lap = (uu + ud) + (ul + ur) - 4.f * p;
+          const float rr = fmaf(g.D, lap, qq * (p - g.a));
           s_rd = fmaf(rr, rr, s_rd);
         }
         if (PF) {
-          const float gx = 0.5f * (ur - ul), gy = 0.5f * (ud - uu);
-          const float qq = p * (1.f - p);
-          s_pf += 0.5f * g.eps * (gx * gx + gy * gy) + qq * qq / g.eps;
+          const float gx = ur - ul, gy = ud - uu;  // 2x the central differences
+          s_g2 = fmaf(gx, gx, fmaf(gy, gy, s_g2));
+          s_q2 = fmaf(qq, qq, s_q2);
         }
       }
     }
   }
+  const float s_bce = s_bce2 * kLn2;
+  const float s_pf = 0.125f * g.eps * s_g2 + s_q2 / g.eps;
   float v[6] = {s_it, s_p, s_t, s_bce, s_rd, s_pf};
   int c[3] = {c_i, c_p, c_t};
   __shared__ float fr[4][6];
@@ -240,70 +285,125 @@ __global__ __launch_bounds__(256) void loss_bwd_kernel(LossBwdArgs g) {
   const float* u = g.p + b * HW;
   const float* tt = g.t + b * HW;
   float* dd = g.dst + b * HW;
+  // block-uniform coefficients; dL/dp = cA + cT t + BCE + RD + PF, no divisions per pixel
   const float I = g.terms[5], P = g.terms[6], T = g.terms[7];
   const float S = P + T + g.smooth;
-  const float two_i_s = 2.f * I + g.smooth;
-  const float inv_s2 = 1.f / (S * S);
   const float go = g.grad_out ? g.grad_out[0] : 1.f;
   const float inv_n = (float)(1.0 / ((double)g.B * HW));
-  if (ST) {
-    stage_tile(u, H, W, y0, x0, 2, su);
+  const float inv_s2 = 1.f / (S * S);
+  const float cA = go * g.dice_w * (2.f * I + g.smooth) * inv_s2;
+  const float cT = -go * g.dice_w * 2.f * S * inv_s2;
+  const float cB = go * g.bce_w * inv_n;
+  const float cR = go * g.rd_w * 2.f * inv_n, cRD = cR * g.D;
+  const float cPa = go * g.pf_w * inv_n * g.eps * 0.25f, cPw = go * g.pf_w * inv_n * 2.f / g.eps;
+  const float fa = 2.f * (1.f + g.a);
+  constexpr int NI = LT_Y * LT_Q / 256;  // 4-pixel items per thread
+  f32x4 tvs[NI];
+#pragma unroll
+  for (int j = 0; j < NI; ++j) {  // targets in flight together with the tile of u
+    const int k = threadIdx.x + 256 * j;
+    const int y = y0 + k / LT_Q, xb = x0 + 4 * (k % LT_Q);
+    if (y < H && xb < W) tvs[j] = load4(tt + (size_t)y * W, xb, W);
+  }
+  if constexpr (ST) {
+    stage_tile<2>(u, H, W, y0, x0, su);
     __syncthreads();
   }
-  if (RD) {
+  if constexpr (RD) {
     // residual r = D Lap(u) + u(1-u)(u-a) on rows y0-1 .. y0+LT_Y, columns x0-1 .. x0+LT_X
     // (zero outside the image: those slots only meet zero adjoint weights)
-    constexpr int RC = LT_X + 2;
-    for (int k = threadIdx.x; k < (LT_Y + 2) * RC; k += blockDim.x) {
-      const int rr = k / RC, cc = k % RC - 1;
-      const int yy = y0 - 1 + rr, xx = x0 + cc;
-      float r = 0.f;
-      if (yy >= 0 && yy < H && xx >= 0 && xx < W) {
-        const float* sc = su + (rr + 1) * LT_S + 4 + cc;
-        const float c0 = sc[0];
-        const float lap = sc[-LT_S] + sc[LT_S] + sc[-1] + sc[1] - 4.f * c0;
-        r = g.D * lap + c0 * (1.f - c0) * (c0 - g.a);
+    constexpr int NR = (LT_Y + 2) * LT_Q;
+    for (int k = threadIdx.x; k < NR + (LT_Y + 2) * 2; k += 256) {
+      if (k < NR) {  // 4 interior columns
+        const int rr = k / LT_Q, q = k % LT_Q;
+        const int yy = y0 - 1 + rr;
+        const float* sc = su + (rr + 1) * LT_S + 4 + 4 * q;
+        const f32x4 c = *(const f32x4*)sc, up = *(const f32x4*)(sc - LT_S), dn = *(const f32x4*)(sc + LT_S);
+        const float lft = sc[-1], rgt = sc[4];
+        f32x4 out;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float c0 = c[i];
+          const float ul = i == 0 ? lft : c[i - 1], ur = i == 3 ? rgt : c[i + 1];
+          const float lap = (up[i] + dn[i]) + (ul + ur) - 4.f * c0;
+          const bool ok = yy >= 0 && yy < H && x0 + 4 * q + i < W;
+          out[i] = ok ? fmaf(g.D, lap, fmaf(-c0, c0, c0) * (c0 - g.a)) : 0.f;
+        }
+        *(f32x4*)(sr + rr * LT_S + 4 + 4 * q) = out;
+      } else {  // edge columns x0-1 and x0+LT_X
+        const int e = k - NR, rr = e >> 1, cc = (e & 1) ? LT_X : -1;
+        const int yy = y0 - 1 + rr, xx = x0 + cc;
+        float r = 0.f;
+        if (yy >= 0 && yy < H && xx >= 0 && xx < W) {
+          const float* sc = su + (rr + 1) * LT_S + 4 + cc;
+          const float c0 = sc[0];
+          const float lap = (sc[-LT_S] + sc[LT_S]) + (sc[-1] + sc[1]) - 4.f * c0;
+          r = fmaf(g.D, lap, fmaf(-c0, c0, c0) * (c0 - g.a));
+        }
+        sr[rr * LT_S + 4 + cc] = r;
       }
-      sr[rr * LT_S + 4 + cc] = r;
     }
     __syncthreads();
   }
-  for (int k = threadIdx.x; k < LT_Y * LT_Q; k += blockDim.x) {
+#pragma unroll
+  for (int j = 0; j < NI; ++j) {
+    const int k = threadIdx.x + 256 * j;
     const int r = k / LT_Q, q = k % LT_Q;
     const int y = y0 + r, xb = x0 + 4 * q;
     if (y >= H || xb >= W) continue;
-    const f32x4 tv = load4(tt + (size_t)y * W, xb, W);
-    const f32x4 pv = ST ? *(const f32x4*)(su + (r + 2) * LT_S + 4 + 4 * q) : load4(u + (size_t)y * W, xb, W);
+    const f32x4 tv = tvs[j];
+    const float* sc = su + (r + 2) * LT_S + 4 + 4 * q;
+    const f32x4 pv = ST ? *(const f32x4*)sc : load4(u + (size_t)y * W, xb, W);
+    f32x4 rc, ru, rd;
+    float rl = 0.f, rrt = 0.f;
+    if constexpr (RD) {
+      const float* sq = sr + (r + 1) * LT_S + 4 + 4 * q;
+      rc = *(const f32x4*)sq;
+      ru = *(const f32x4*)(sq - LT_S);
+      rd = *(const f32x4*)(sq + LT_S);
+      rl = sq[-1];
+      rrt = sq[4];
+    }
+    f32x4 u2, d2;
+    float l2[2] = {0.f, 0.f}, r2[2] = {0.f, 0.f};
+    if constexpr (PF) {
+      u2 = *(const f32x4*)(sc - 2 * LT_S);
+      d2 = *(const f32x4*)(sc + 2 * LT_S);
+      l2[0] = sc[-2];
+      l2[1] = sc[-1];
+      r2[0] = sc[4];
+      r2[1] = sc[5];
+    }
     f32x4 out;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int x = xb + i;
       const float p = pv[i], t = tv[i];
-      float grad = g.dice_w * (-(2.f * t * S - two_i_s) * inv_s2);
-      grad += g.bce_w * ((p - t) / fmaxf(p * (1.f - p), 1e-12f) * inv_n);
-      if (RD) {
-        // adjoint multiplicities of the reflect-padded 5-point stencil: ghost row -1 is
-        // row 1 and ghost row H is row H-2, so rows 1 and H-2 receive the boundary twice
-        const float* sc = sr + (r + 1) * LT_S + 4 + 4 * q + i;
-        const float wu = (float)((y >= 1) + (y == 1)), wd = (float)((y <= H - 2) + (y == H - 2));
-        const float wl = (float)((x >= 1) + (x == 1)), wr = (float)((x <= W - 2) + (x == W - 2));
-        const float rk = sc[0];
-        const float adj = -4.f * rk + wu * sc[-LT_S] + wd * sc[LT_S] + wl * sc[-1] + wr * sc[1];
-        const float fp = -3.f * p * p + 2.f * (1.f + g.a) * p - g.a;
-        grad += g.rd_w * (2.f * inv_n) * (g.D * adj + rk * fp);
+      const float qq = fmaf(-p, p, p);  // p (1 - p)
+      float grad = fmaf(cT, t, cA);
+      grad = fmaf(cB * (p - t), __builtin_amdgcn_rcpf(fmaxf(qq, 1e-12f)), grad);
+      if constexpr (RD) {
+        // adjoint of the reflect-padded 5-point stencil: ghost row -1 is row 1 and ghost
+        // row H is row H-2, so rows/columns 1 and n-2 receive the boundary residual twice
+        const float rk = rc[i];
+        const float rl_ = i == 0 ? rl : rc[i - 1], rr_ = i == 3 ? rrt : rc[i + 1];
+        float adj = (ru[i] + rd[i]) + (rl_ + rr_) - 4.f * rk;
+        adj += (y == 1 ? ru[i] : 0.f) + (y == H - 2 ? rd[i] : 0.f);
+        adj += (x == 1 ? rl_ : 0.f) + (x == W - 2 ? rr_ : 0.f);
+        const float fp = fmaf(p, fmaf(-3.f, p, fa), -g.a);
+        grad = fmaf(cRD, adj, fmaf(cR * rk, fp, grad));
       }
-      if (PF) {
+      if constexpr (PF) {
         // gx vanishes on columns 0 and W-1 (reflect), so the ghost folds cancel
-        const float* sc = su + (r + 2) * LT_S + 4 + 4 * q + i;
+        const float xm2 = i < 2 ? l2[i] : pv[i - 2], xp2 = i >= 2 ? r2[i - 2] : pv[i + 2];
         float adj = 0.f;
-        if (x >= 1) adj += 0.25f * (sc[0] - sc[-2]);
-        if (x <= W - 2) adj -= 0.25f * (sc[2] - sc[0]);
-        if (y >= 1) adj += 0.25f * (sc[0] - sc[-2 * LT_S]);
-        if (y <= H - 2) adj -= 0.25f * (sc[2 * LT_S] - sc[0]);
-        grad += g.pf_w * inv_n * (g.eps * adj + 2.f * p * (1.f - p) * (1.f - 2.f * p) / g.eps);
+        adj += x >= 1 ? p - xm2 : 0.f;
+        adj -= x <= W - 2 ? xp2 - p : 0.f;
+        adj += y >= 1 ? p - u2[i] : 0.f;
+        adj -= y <= H - 2 ? d2[i] - p : 0.f;
+        grad = fmaf(cPa, adj, fmaf(cPw * qq, 1.f - 2.f * p, grad));
       }
-      grad *= go;
-      if (g.chain) grad = grad * (1.f - p) * p;
+      if (g.chain) grad *= qq;
       out[i] = grad;
     }
     if ((W & 3) == 0) {
