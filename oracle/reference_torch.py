@@ -121,33 +121,91 @@ class UNetRef(nn.Module):
         return unet_forward(self, x, drop_scales, return_logits)
 
 
-def _block_forward(blk: _Block, x: torch.Tensor, scale: Optional[torch.Tensor], training: bool):
-    y = F.relu(F.conv2d(x, blk.conv0.weight, blk.conv0.bias, padding=1))
+def _relu(pre: torch.Tensor, name: str, decisions, record) -> torch.Tensor:
+    """ReLU, or — when ``decisions`` holds a mask for this site — the linear map
+    pre * mask, i.e. the same network evaluated on another run's activation
+    pattern (gradient parity conditioned on identical ReLU decisions)."""
+    if record is not None:
+        record[name] = pre.detach()
+    if decisions is not None and name in decisions:
+        return pre * decisions[name].to(pre.dtype)
+    return F.relu(pre)
+
+
+def _pool(x: torch.Tensor, name: str, decisions, record) -> torch.Tensor:
+    """2x2/2 max-pool (src/unet.py:181-187), or the gather of given window argmaxes
+    (index dy * 2 + dx per window) when ``decisions`` holds them for this site."""
+    if record is not None:
+        record[name] = x.detach()
+    if decisions is not None and name in decisions:
+        B, C, H, W = x.shape
+        win = x.reshape(B, C, H // 2, 2, W // 2, 2).permute(0, 1, 2, 4, 3, 5).reshape(B, C, H // 2, W // 2, 4)
+        return win.gather(-1, decisions[name].long().unsqueeze(-1)).squeeze(-1)
+    return F.max_pool2d(x, 2, 2)
+
+
+def _block_forward(blk: _Block, x: torch.Tensor, scale: Optional[torch.Tensor], training: bool,
+                   name: str = "", decisions=None, record=None):
+    y = _relu(F.conv2d(x, blk.conv0.weight, blk.conv0.bias, padding=1), f"{name}.0", decisions, record)
     if blk.p > 0:
         if scale is not None:  # injected Dropout2d keep-scale (B, C): 0 or 1/(1-p)
             y = y * scale[:, :, None, None].to(y.dtype)
         elif training:
             y = F.dropout2d(y, blk.p, True)
-    return F.relu(F.conv2d(y, blk.conv1.weight, blk.conv1.bias, padding=1))
+    return _relu(F.conv2d(y, blk.conv1.weight, blk.conv1.bias, padding=1), f"{name}.1", decisions, record)
 
 
-def unet_forward(m: UNetRef, x: torch.Tensor, drop_scales=None, return_logits=False):
-    """src/unet.py:169-216; concat order is [upsampled, skip] (:190-202)."""
+def unet_forward(m: UNetRef, x: torch.Tensor, drop_scales=None, return_logits=False, decisions=None,
+                 record=None):
+    """src/unet.py:169-216; concat order is [upsampled, skip] (:190-202).
+
+    ``decisions`` ({"enc1.0": relu mask, ..., "pool1": window argmax, ...}, NCHW)
+    pins every ReLU / max-pool decision to another run's; ``record`` collects the
+    pre-activations and pool inputs under the same keys."""
     s = drop_scales or {}
     tr = m.training
-    e1 = _block_forward(m.enc1, x, s.get("enc1"), tr)
-    e2 = _block_forward(m.enc2, F.max_pool2d(e1, 2, 2), s.get("enc2"), tr)
-    e3 = _block_forward(m.enc3, F.max_pool2d(e2, 2, 2), s.get("enc3"), tr)
-    e4 = _block_forward(m.enc4, F.max_pool2d(e3, 2, 2), s.get("enc4"), tr)
-    bn = _block_forward(m.bottleneck, F.max_pool2d(e4, 2, 2), s.get("bottleneck"), tr)
+    kw = dict(decisions=decisions, record=record)
+    e1 = _block_forward(m.enc1, x, s.get("enc1"), tr, "enc1", **kw)
+    e2 = _block_forward(m.enc2, _pool(e1, "pool1", **kw), s.get("enc2"), tr, "enc2", **kw)
+    e3 = _block_forward(m.enc3, _pool(e2, "pool2", **kw), s.get("enc3"), tr, "enc3", **kw)
+    e4 = _block_forward(m.enc4, _pool(e3, "pool3", **kw), s.get("enc4"), tr, "enc4", **kw)
+    bn = _block_forward(m.bottleneck, _pool(e4, "pool4", **kw), s.get("bottleneck"), tr, "bottleneck", **kw)
     d = bn
     for up, dec, skip, name in ((m.up4, m.dec4, e4, "dec4"), (m.up3, m.dec3, e3, "dec3"),
                                 (m.up2, m.dec2, e2, "dec2"), (m.up1, m.dec1, e1, "dec1")):
         u = F.conv_transpose2d(d, up.weight, up.bias, stride=2)
-        d = _block_forward(dec, torch.cat([u, skip], dim=1), s.get(name), tr)
+        d = _block_forward(dec, torch.cat([u, skip], dim=1), s.get(name), tr, name, **kw)
     z = F.conv2d(d, m.out_conv.weight, m.out_conv.bias)
     p = torch.sigmoid(z)
     return (p, z) if return_logits else p
+
+
+def decision_flips(decisions, record, drop_scales=None) -> Dict[str, Tuple[int, float]]:
+    """Where a run's ReLU / max-pool decisions differ from the ones this oracle makes
+    on ``record`` (its own pre-activations): per site (count, worst margin), the
+    margin being |pre-activation| for a ReLU and the gap between the window max and
+    the chosen element for a pool, relative to the site's max |value|. Channels a
+    Dropout2d keep-scale zeroes (``drop_scales``) carry no decision and are skipped."""
+    out = {}
+    drop_scales = drop_scales or {}
+    for name, dec in decisions.items():
+        ref = record[name]
+        scale = ref.abs().max().clamp_min(1e-30)
+        if name.startswith("pool"):
+            B, C, H, W = ref.shape
+            win = ref.reshape(B, C, H // 2, 2, W // 2, 2).permute(0, 1, 2, 4, 3, 5).reshape(B, C, H // 2, W // 2, 4)
+            chosen = win.gather(-1, dec.long().unsqueeze(-1)).squeeze(-1)
+            gap = win.amax(-1) - chosen
+            bad = gap > 0
+            margin = gap[bad]
+        else:
+            bad = dec.bool() != (ref > 0)
+            blk = name.rsplit(".", 1)[0]
+            if name.endswith(".0") and blk in drop_scales:
+                bad &= (drop_scales[blk] != 0)[:, :, None, None]
+            margin = ref[bad].abs()
+        out[name] = (int(bad.sum()), float(margin.max() / scale) if margin.numel() else 0.0)
+    return out
 
 
 def make_drop_scales(m: UNetRef, B: int, generator: torch.Generator) -> Dict[str, torch.Tensor]:

@@ -211,6 +211,33 @@ class UNet(nn.Module):
     def block(self, name: str) -> DoubleConv:
         return getattr(self, name)
 
+    @torch.no_grad()
+    def activation_decisions(self) -> Dict[str, torch.Tensor]:
+        """The ReLU masks and 2x2 max-pool window argmaxes (dy * 2 + dx, first max)
+        of the last forward, NCHW on the host, keyed like the oracle's sites
+        ("enc1.0", "enc1.1", "pool1", ..., "dec1.1"). Introspection for parity
+        tests: fp32 rounding decides ReLU pre-activations within ~1e-7 of zero, so
+        gradients are compared with float64 evaluated on the same decisions."""
+        eng = self._engine
+        if eng is None or not eng.bufs:
+            raise RuntimeError("activation_decisions: no forward has run")
+        bf, c = eng.bufs, self.base_channels
+        nchw = lambda t: t.permute(0, 3, 1, 2).contiguous()
+        out = {}
+        for l in range(1, 5):
+            Cl = c << (l - 1)
+            skip = nchw(bf[f"cat{l}"][..., Cl:])
+            out[f"enc{l}.0"] = nchw(bf[f"a{l}"]) > 0
+            out[f"enc{l}.1"] = skip > 0
+            B, C, H, W = skip.shape
+            win = skip.reshape(B, C, H // 2, 2, W // 2, 2).permute(0, 1, 2, 4, 3, 5).reshape(B, C, H // 2, W // 2, 4)
+            out[f"pool{l}"] = win.argmax(-1)
+            out[f"dec{l}.0"] = nchw(bf[f"d0_{l}"]) > 0
+            out[f"dec{l}.1"] = nchw(bf[f"d1_{l}"]) > 0
+        out["bottleneck.0"] = nchw(bf["b0"]) > 0
+        out["bottleneck.1"] = nchw(bf["b1"]) > 0
+        return {k: v.cpu() for k, v in out.items()}
+
     # ---- forward -------------------------------------------------------------
     def engine(self) -> "UNetEngine":
         if self._engine is None:

@@ -122,3 +122,31 @@ def test_counts_match_metric_restatement():
     dice, iou = ln.dice_iou_from_counts(inter, phat, tsum)
     np.testing.assert_allclose(dice, rt.dice_score_batch(p, mask).numpy(), rtol=1e-6)
     np.testing.assert_allclose(iou, rt.iou_batch(p, mask).numpy(), rtol=1e-6)
+
+
+def test_decision_conditioned_forward_matches_free_forward():
+    # pinning ReLU masks / pool argmaxes to the oracle's own decisions is the identity,
+    # and decision_flips() reports none (the mechanism the GPU gradient test relies on)
+    torch.manual_seed(3)
+    m = rt.UNetRef(1, 1, 8).double().eval()
+    x = torch.rand(2, 1, 32, 32, dtype=torch.float64)
+    rec = {}
+    p_free = rt.unet_forward(m, x, record=rec)
+    dec = {}
+    for k, v in rec.items():
+        if k.startswith("pool"):
+            B, C, H, W = v.shape
+            win = v.reshape(B, C, H // 2, 2, W // 2, 2).permute(0, 1, 2, 4, 3, 5).reshape(B, C, H // 2, W // 2, 4)
+            dec[k] = win.argmax(-1)
+        else:
+            dec[k] = v > 0
+    assert len(dec) == 22
+    rec2 = {}
+    p_pin = rt.unet_forward(m, x, decisions=dec, record=rec2)
+    assert torch.equal(p_free, p_pin)
+    assert all(n == 0 for n, _ in rt.decision_flips(dec, rec2).values())
+    flipped = dict(dec)
+    flipped["enc2.0"] = dec["enc2.0"].clone()
+    flipped["enc2.0"].view(-1)[0] ^= True
+    n, margin = rt.decision_flips(flipped, rec2)["enc2.0"]
+    assert n == 1 and margin > 0

@@ -28,19 +28,22 @@ def main(B=2, H=64, W=64, seed=11):
     rt.loss_terms(p64, mask.double())["loss"].backward()
     g32 = {n: q.grad for n, q in ref.named_parameters()}
     g64 = {n: q.grad for n, q in ref64.named_parameters()}
+    # (label, pis_tune settings): halo kernels with each channel-slice choice, generic igemm
+    configs = [("halo", {3: 1, 4: 0}), ("ck4", {3: 1, 4: 1}), ("ck8", {3: 1, 4: 3}), ("generic", {3: 0, 4: 0})]
     res = {}
-    for halo in (1, 0):
-        _hip.lib().pis_tune(3, halo)
+    for label, knobs in configs:
+        for k, v in knobs.items():
+            _hip.lib().pis_tune(k, v)
         net = UNet().cuda().train()
         net.load_state_dict(ref.state_dict())
         net.set_dropout_scales(scales)
         DiceBCELoss()(net(img.cuda()), mask.cuda()).backward()
-        res[halo] = {n: q.grad.clone() for n, q in net.named_parameters()}
+        res[label] = {n: q.grad.clone() for n, q in net.named_parameters()}
     _hip.lib().pis_tune(3, 1)
-    print(f"{'param':32s} {'cpu32/64':>10s} {'halo/64':>10s} {'gen/64':>10s} {'halo/cpu32':>10s}")
+    _hip.lib().pis_tune(4, 0)
+    print(f"{'param':32s} {'cpu32/64':>10s}" + "".join(f" {l + '/64':>10s}" for l, _ in configs))
     for n in g64:
-        print(f"{n:32s} {rel(g32[n], g64[n]):10.2e} {rel(res[1][n], g64[n]):10.2e} {rel(res[0][n], g64[n]):10.2e}"
-              f" {rel(res[1][n], g32[n]):10.2e}")
+        print(f"{n:32s} {rel(g32[n], g64[n]):10.2e}" + "".join(f" {rel(res[l][n], g64[n]):10.2e}" for l, _ in configs))
 
 
 if __name__ == "__main__":
