@@ -124,7 +124,10 @@ def load_pmc_traffic():
     if not os.path.exists(path):
         return None
     with open(path) as f:
-        return json.load(f).get("hbm_bytes_per_launch")
+        d = json.load(f)
+    if DOMINANT not in (d.get("dominant_kernel") or ""):
+        return None  # counters were taken on another kernel: report no traffic rather than a stale one
+    return d.get("hbm_bytes_per_launch")
 
 
 def cpu_baseline(seconds: float = 15.0):
