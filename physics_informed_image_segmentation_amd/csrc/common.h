@@ -17,6 +17,7 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 namespace pis {
 
 void set_error(const char* fmt, ...);
+int tune_get(int key);  // pis_tune() knob value (csrc/capi.hip)
 
 inline int launch_status(const char* what) {
   hipError_t e = hipGetLastError();

@@ -393,7 +393,6 @@ static bool halo_ok(const IGemmArgs& a) {
          a.Csrc % 4 == 0 && a.lds % 4 == 0 && a.ldw % 4 == 0;
 }
 
-int tune_get(int key);
 
 static int launch_conv3x3(const IGemmArgs& a, hipStream_t s);
 

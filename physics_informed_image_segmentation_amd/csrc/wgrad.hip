@@ -194,12 +194,15 @@ struct W3Args {
   float* part_bias;    // [splits][Cout] or NULL
 };
 
+// NSEG consecutive 16-pixel segments per stage (one barrier per NSEG * 72 MFMAs).
+template <int NSEG>
 __global__ __launch_bounds__(256, 2) void wgrad3x3_halo_kernel(W3Args g) {
   constexpr int SEG = 16, HW_ = SEG + 2, CH = 64;
-  constexpr int X_F4 = 3 * HW_ * CH / 4;  // 864 float4 of halo per stage
-  constexpr int XL = (X_F4 + 255) / 256;  // 4
-  __shared__ __attribute__((aligned(16))) float sD[2][SEG * CH];
-  __shared__ __attribute__((aligned(16))) float sX[2][3 * HW_ * CH];
+  constexpr int X_F4 = 3 * HW_ * CH / 4;          // 864 float4 of halo per segment
+  constexpr int XS = 3 * HW_ * CH;                 // floats of halo per segment
+  constexpr int XL = (NSEG * X_F4 + 255) / 256;    // float4 loads per thread per stage
+  __shared__ __attribute__((aligned(16))) float sD[2][NSEG * SEG * CH];
+  __shared__ __attribute__((aligned(16))) float sX[2][NSEG * XS];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave & 1, wn = wave >> 1;
@@ -214,34 +217,49 @@ __global__ __launch_bounds__(256, 2) void wgrad3x3_halo_kernel(W3Args g) {
   const bool do_bias = g.part_bias != nullptr && c0 == 0;
   const int segs_per_row = g.W / SEG;
 
-  f32x4 rd, rx[XL];
-  auto gload = [&](int sg) {
-    const int row_id = sg / segs_per_row;  // b*H + h
-    const int w0 = (sg - row_id * segs_per_row) * SEG;
-    const int b = row_id / g.H, h = row_id - b * g.H;
-    {
+  f32x4 rd[NSEG], rx[XL];
+  auto gload = [&](int sg0) {
+    int sb[NSEG], sh[NSEG], sw[NSEG];
+    bool sv[NSEG];
+#pragma unroll
+    for (int j = 0; j < NSEG; ++j) {  // block-uniform segment coordinates
+      const int sg = sg0 + j;
+      sv[j] = sg < s_end;
+      const int row_id = sg / segs_per_row;  // b*H + h
+      sw[j] = (sg - row_id * segs_per_row) * SEG;
+      sb[j] = row_id / g.H;
+      sh[j] = row_id - sb[j] * g.H;
       const int px = tid >> 4, c4 = (tid & 15) * 4;
-      rd = *reinterpret_cast<const f32x4*>(g.dz + ((size_t)row_id * g.W + w0 + px) * g.ldz + m0 + c4);
+      rd[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (sv[j])
+        rd[j] = *reinterpret_cast<const f32x4*>(g.dz + ((size_t)row_id * g.W + sw[j] + px) * g.ldz + m0 + c4);
     }
 #pragma unroll
     for (int i = 0; i < XL; ++i) {
       const int idx = tid + i * 256;
       rx[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (idx < X_F4) {
-        const int r = idx / (HW_ * 16), rem = idx - r * (HW_ * 16);
+      if (idx < NSEG * X_F4) {
+        const int j = NSEG == 1 ? 0 : idx / X_F4;
+        const int e = idx - j * X_F4;
+        const int r = e / (HW_ * 16), rem = e - r * (HW_ * 16);
         const int px = rem >> 4, c4 = (rem & 15) * 4;
+        const int b = NSEG == 1 ? sb[0] : (j ? sb[NSEG - 1] : sb[0]);
+        const int h = NSEG == 1 ? sh[0] : (j ? sh[NSEG - 1] : sh[0]);
+        const int w0 = NSEG == 1 ? sw[0] : (j ? sw[NSEG - 1] : sw[0]);
+        const bool v = NSEG == 1 ? sv[0] : (j ? sv[NSEG - 1] : sv[0]);
         const int hs = h + r - 1, ws = w0 + px - 1;
-        if (hs >= 0 && hs < g.H && ws >= 0 && ws < g.W)
+        if (v && hs >= 0 && hs < g.H && ws >= 0 && ws < g.W)
           rx[i] = *reinterpret_cast<const f32x4*>(g.x + (((size_t)b * g.H + hs) * g.W + ws) * g.ldx + c0 + c4);
       }
     }
   };
   auto lstore = [&](int buf) {
-    *reinterpret_cast<f32x4*>(&sD[buf][tid * 4]) = rd;
+#pragma unroll
+    for (int j = 0; j < NSEG; ++j) *reinterpret_cast<f32x4*>(&sD[buf][j * SEG * CH + tid * 4]) = rd[j];
 #pragma unroll
     for (int i = 0; i < XL; ++i) {
       const int idx = tid + i * 256;
-      if (idx < X_F4) *reinterpret_cast<f32x4*>(&sX[buf][idx * 4]) = rx[i];
+      if (idx < NSEG * X_F4) *reinterpret_cast<f32x4*>(&sX[buf][idx * 4]) = rx[i];
     }
   };
 
@@ -252,7 +270,7 @@ __global__ __launch_bounds__(256, 2) void wgrad3x3_halo_kernel(W3Args g) {
     for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
   float bsum = 0.f;
   const int li = lane & 31, lh = lane >> 5;
-  const int nst = s_end - s_begin;
+  const int nst = (s_end - s_begin + NSEG - 1) / NSEG;
   if (nst > 0) {
     gload(s_begin);
     lstore(0);
@@ -260,21 +278,22 @@ __global__ __launch_bounds__(256, 2) void wgrad3x3_halo_kernel(W3Args g) {
   __syncthreads();
   for (int st = 0; st < nst; ++st) {
     const int cur = st & 1;
-    if (st + 1 < nst) gload(s_begin + st + 1);
+    if (st + 1 < nst) gload(s_begin + (st + 1) * NSEG);
     const float* D = sD[cur];
     const float* X = sX[cur];
     if (do_bias && tid < CH) {
 #pragma unroll
-      for (int r = 0; r < SEG; ++r) bsum += D[r * CH + tid];
+      for (int r = 0; r < NSEG * SEG; ++r) bsum += D[r * CH + tid];
     }
 #pragma unroll
-    for (int kk = 0; kk < SEG / 2; ++kk) {
-      const int px = 2 * kk + lh;
-      const float a = D[px * CH + wm * 32 + li];
+    for (int kk = 0; kk < NSEG * SEG / 2; ++kk) {
+      const int j = kk / (SEG / 2);
+      const int px = 2 * (kk - j * (SEG / 2)) + lh;  // pixel within segment j
+      const float a = D[(j * SEG + px) * CH + wm * 32 + li];
 #pragma unroll
       for (int t = 0; t < 9; ++t) {
         const int r = t / 3, s = t % 3;  // x at (h + r - 1, w + s - 1) = halo (r, px + s)
-        const float bv = X[(r * HW_ + px + s) * CH + wn * 32 + li];
+        const float bv = X[j * XS + (r * HW_ + px + s) * CH + wn * 32 + li];
         acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bv, acc[t], 0, 0, 0);
       }
     }
@@ -510,8 +529,8 @@ static HaloPlan halo_plan(int B, int H, int W, int Cin, int Cout) {
   p.nseg = (int)((int64_t)B * H * W / 16);
   const int tiles = (Cout / 64) * (Cin / 64);
   const size_t slab = (size_t)Cout * 9 * Cin * sizeof(float);
-  // ~4 blocks per CU-slot round, 512..8192 pixels per split, <= ~160 MB of partial slabs
-  int64_t splits = cdiv(1024, tiles);
+  // one round of blocks (2 per CU), 512..8192 pixels per split, <= ~160 MB of partial slabs
+  int64_t splits = cdiv(std::max(64, tune_get(PIS_TUNE_WGRAD_BLOCKS)), tiles);
   splits = std::min<int64_t>(splits, std::max<int64_t>(1, (int64_t)((160u << 20) / slab)));
   int64_t sps = cdiv(p.nseg, splits);
   sps = std::max<int64_t>(32, std::min<int64_t>(512, sps));
@@ -561,7 +580,10 @@ extern "C" int pis_conv3x3_wgrad(const float* x, int ldx, const float* dz, int l
     a.part = (float*)ws;
     a.part_bias = db ? (float*)((char*)ws + cdiv(hp.part_bytes, 256) * 256) : nullptr;
     const int tiles = (Cout / 64) * (Cin / 64);
-    hipLaunchKernelGGL(wgrad3x3_halo_kernel, dim3(tiles * hp.splits), dim3(256), 0, s, a);
+    if (tune_get(PIS_TUNE_WGRAD_VARIANT) != 0)
+      hipLaunchKernelGGL((wgrad3x3_halo_kernel<2>), dim3(tiles * hp.splits), dim3(256), 0, s, a);
+    else
+      hipLaunchKernelGGL((wgrad3x3_halo_kernel<1>), dim3(tiles * hp.splits), dim3(256), 0, s, a);
     int rc = launch_status("wgrad3x3_halo");
     if (!rc) rc = reduce_slabs(a.part, hp.splits, (int64_t)Cout * 9 * Cin, dw_krsc, acc, s);
     if (rc || !db) return rc;

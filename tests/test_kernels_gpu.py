@@ -101,6 +101,22 @@ def test_conv3x3_dgrad_wgrad(hip, B, H, W, Cin, Cout):
     assert rel_err(dw.cpu().permute(0, 3, 1, 2), 2 * dw_ref) < 1e-5
 
 
+# every non-default kernel variant behind pis_tune (include/pis_capi.h) stays exact too
+TUNE_VARIANTS = [(4, 1), (4, 2), (4, 3), (5, 1), (3, 0)]
+
+
+@pytest.mark.parametrize("key,value", TUNE_VARIANTS)
+def test_conv3x3_tuned_variants(hip, key, value):
+    prev = hip.pis_tune(key, value)
+    try:
+        for shape in [(2, 16, 32, 64, 64, 0), (2, 16, 32, 128, 256, 64), (1, 8, 16, 256, 64, 0)]:
+            test_conv3x3_fwd(hip, *shape)
+        for shape in [(2, 16, 32, 64, 128), (1, 32, 16, 128, 64), (2, 16, 48, 256, 256)]:
+            test_conv3x3_dgrad_wgrad(hip, *shape)
+    finally:
+        hip.pis_tune(key, prev)
+
+
 def test_conv3x3_c1_wgrad(hip):
     B, H, W, Cout = 2, 32, 16, 64
     g = torch.Generator().manual_seed(2)

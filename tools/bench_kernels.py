@@ -65,11 +65,12 @@ def main():
         dw = torch.empty(cout * 9 * cin, device=dev)
         db = torch.empty(cout, device=dev)
         flops = 2.0 * B * H * H * cout * cin * 9
+        dflags = 0 if name.startswith("dec") and name.endswith("conv0") else 4  # ReLU mask unless a concat input
         ops = {
             "fwd": lambda: lib.pis_conv3x3_fwd(x.data_ptr(), cin, w.data_ptr(), bias.data_ptr(), 0, y.data_ptr(), cout,
                                                B, H, H, cin, cout, 1, s),
             "dgrad": lambda: lib.pis_conv3x3_dgrad(dz.data_ptr(), cout, wf.data_ptr(), x.data_ptr(), cin, 0,
-                                                   dx.data_ptr(), cin, B, H, H, cin, cout, 4, s),
+                                                   dx.data_ptr(), cin, B, H, H, cin, cout, dflags, s),
             "wgrad": lambda: lib.pis_conv3x3_wgrad(x.data_ptr(), cin, dz.data_ptr(), cout, dw.data_ptr(),
                                                    db.data_ptr(), B, H, H, cin, cout, 0, ws.data_ptr(), nws, s),
         }
