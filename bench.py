@@ -88,27 +88,62 @@ def igemm_shape(name, a):
     return M, N, K, f"igemm_f32_kernel<128, {64 if N <= 64 else 128}, 16, {t2d}>"
 
 
+def loss_call_bytes(name, a):
+    """Algorithmic HBM bytes of the fused-loss C-ABI calls: the loss
+    forward reads p and t (8 B/px); the loss backward fused into the head backward reads
+    the 64-channel head input, u and t and writes dx and dL/du (2 x 256 + 12 B/px)."""
+    if name == "pis_loss_fwd":
+        B, H, W = a[2:5]
+        return 8.0 * B * H * W
+    if name == "pis_head_loss_bwd":
+        B, H, W, C = a[6:10]
+        return (8.0 * C + 12.0) * B * H * W
+    return None
+
+
 class LaunchTimer:
-    """HIP events around every launch of the dominant kernel, on the stream it runs on."""
+    """HIP events around every launch of the dominant kernel (and of the fused-loss
+    calls), on the stream they run on."""
 
     def __init__(self, kernel=DOMINANT):
         self.kernel = kernel
         self.records = []
+        self.loss = {}
+
+    def _events(self):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        return e0, e1
 
     def begin(self, name, args):
+        nbytes = loss_call_bytes(name, args)
+        if nbytes is not None:
+            return ("loss", name, *self._events(), nbytes)
         if name not in IGEMM_CALLS:
             return None
         shp = igemm_shape(name, args)
         if shp is None or shp[3] != self.kernel:
             return None
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        return (e0, e1, 2.0 * shp[0] * shp[1] * shp[2])
+        return ("mfma", name, *self._events(), 2.0 * shp[0] * shp[1] * shp[2])
 
     def end(self, tok):
-        if tok is not None:
-            tok[1].record()
-            self.records.append(tok)
+        if tok is None:
+            return
+        kind, name, e0, e1, work = tok
+        e1.record()
+        if kind == "loss":
+            self.loss.setdefault(name, []).append((e0, e1, work))
+        else:
+            self.records.append((e0, e1, work))
+
+    def loss_summary(self):
+        torch.cuda.synchronize()
+        out = {}
+        for name, recs in self.loss.items():
+            ms = sum(e0.elapsed_time(e1) for e0, e1, _ in recs) / len(recs)
+            nbytes = recs[0][2]
+            out[name] = (ms, nbytes, nbytes / (ms * 1e-3) / 1e9)
+        return out
 
     def summary(self):
         torch.cuda.synchronize()
@@ -214,6 +249,7 @@ def main():
     step()
     _hip.set_tracer(None)
     n_launch, flop_per_launch, ms_per_launch = timer.summary()
+    loss_t = timer.loss_summary()
     achieved = flop_per_launch / (ms_per_launch * 1e-3) / 1e12
     peak = 157.3  # fp32 MFMA dense TFLOP/s (MI355X_MICROARCH.md)
     traffic = load_pmc_traffic()
@@ -231,6 +267,13 @@ def main():
                          "launches_per_step": n_launch, "avg_launch_ms": ms_per_launch,
                          "flop_per_launch": flop_per_launch},
             "step_tflops": flops / (ms * 1e-3) / 1e12,
+            # north-star HBM figure for the fused loss: the backward runs inside the head
+            # backward kernel (its reduce_slabs follow-ups inside the events); the forward's
+            # time includes its one-block finalize launch
+            "roofline_loss": {
+                name.replace("pis_", ""): {"bound": "hbm", "achieved": gbs, "peak": 8000.0, "unit": "GB/s",
+                                           "frac": gbs / 8000.0, "bytes_per_call": nb, "avg_call_ms": t}
+                for name, (t, nb, gbs) in loss_t.items()},
             "final_loss": float(loss.item()),
         }
         if world == 1 and not args.no_cpu_baseline:

@@ -150,6 +150,16 @@ int pis_loss_bwd(const float* p, const float* t, int B, int H, int W, const pis_
 /* Per-pixel PDE fields of src/pde.py (forward only; any output may be NULL):
  * lap = Lap(u) (:49-79), residual = D Lap(u) + u(1-u)(u-a) (:101-122),
  * gradmag2 = gx^2 + gy^2 (:147-178), all on reflect-padded stencils.           */
+/* Loss backward fused into the head backward (src/loss.py:114-162 + src/unet.py:210 out_conv +
+ * sigmoid): dz = dL/du u (1 - u) per pixel from u (B,H,W), t, terms of pis_loss_fwd, then
+ * dx = dz w (x > 0), dw = sum dz x, db = sum dz as pis_head_bwd. du_out (may be NULL) receives
+ * dL/du, i.e. what pis_loss_bwd writes.
+ * W <= 1024. flags: PIS_ACCUMULATE (dw, db). */
+size_t pis_head_loss_bwd_ws(int B, int H, int W, int C);
+int pis_head_loss_bwd(const float* x, int ldx, const float* w, const float* u, const float* t,
+                      float* du_out, int B, int H, int W, int C, const pis_loss_params* prm,
+                      const float* terms, const float* grad_out, float* dx, int lddx, float* dw,
+                      float* db, int flags, void* ws, size_t ws_bytes, pis_stream_t stream);
 int pis_pde_fields(const float* u, int B, int H, int W, float D, float a, float* lap,
                    float* residual, float* gradmag2, pis_stream_t stream);
 

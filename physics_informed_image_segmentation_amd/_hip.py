@@ -51,6 +51,9 @@ _SIGNATURES = {
     "pis_loss_ws": ([I, I, I], c_size_t),
     "pis_loss_fwd": ([P, P, I, I, I, ctypes.POINTER(LossParams), P, P, P, P, Z, P], c_int),
     "pis_loss_bwd": ([P, P, I, I, I, ctypes.POINTER(LossParams), P, P, P, I, P], c_int),
+    "pis_head_loss_bwd_ws": ([I, I, I, I], c_size_t),
+    "pis_head_loss_bwd": ([P, I, P, P, P, P, I, I, I, I, ctypes.POINTER(LossParams), P, P, P, I, P, P, I, P, Z,
+                           P], c_int),
     "pis_adamw_step": ([P, P, P, P, L, Dbl, Dbl, Dbl, Dbl, Dbl, Dbl, Dbl, Dbl, P], c_int),
     "pis_colsum_ws": ([L, I], c_size_t),
     "pis_colsum": ([P, I, L, I, P, I, P, Z, P], c_int),

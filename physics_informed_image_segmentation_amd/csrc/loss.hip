@@ -16,6 +16,8 @@
 
 namespace pis {
 
+int reduce_slabs(const float* part, int splits, int64_t n, float* dst, int accumulate, hipStream_t s);
+
 __device__ __forceinline__ int refl(int i, int n) { return i < 0 ? -i : (i >= n ? 2 * n - 2 - i : i); }
 __device__ __forceinline__ int clampi(int i, int lo, int hi) { return i < lo ? lo : (i > hi ? hi : i); }
 
@@ -416,6 +418,144 @@ __global__ __launch_bounds__(256) void loss_bwd_kernel(LossBwdArgs g) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// Loss backward fused into the head backward (the consumer of dL/du): one
+// block = R whole image rows. The block stages u for rows y0-2 .. y0+R+1 (reflect
+// resolved, 2 halo columns), the RD residual of rows y0-1 .. y0+R, and dL/dz of
+// its R*W pixels in LDS, then streams the 64-channel head input exactly like
+// head_bwd_kernel: dx = dz w (x > 0), dw/db partial sums per block. dL/dz never
+// goes to HBM and the loss costs no launch of its own.
+// ---------------------------------------------------------------------------
+struct HeadLossArgs {
+  const float* x; int ldx;
+  const float* w;
+  const float* u;
+  const float* t;
+  float* du_out;          // optional: dL/du (before the sigmoid chain) for autograd
+  int B, H, W, C, R;
+  float dice_w, bce_w, rd_w, pf_w, smooth, D, a, eps;
+  const float* terms;
+  const float* grad_out;
+  float* dx; int lddx;
+  float* part;    // [blocks][C]
+  float* part_b;  // [blocks]
+};
+
+template <bool RD, bool PF>
+__global__ __launch_bounds__(256) void head_loss_bwd_kernel(HeadLossArgs g) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int H = g.H, W = g.W, SW = W + 4, SR = W + 2;
+  const int b = blockIdx.y, y0 = blockIdx.x * g.R, nr = min(g.R, H - y0);
+  float* su = smem;                                     // [(R+4)][SW], column c at c + 2
+  float* sr = su + (g.R + 4) * SW;                      // [(R+2)][SR], column c at c + 1
+  float* sdz = sr + (RD ? (g.R + 2) * SR : 0);          // [R][W]
+  const size_t HW = (size_t)H * W;
+  const float* u = g.u + b * HW;
+  const float* tt = g.t + b * HW;
+
+  const float I = g.terms[5], P = g.terms[6], T = g.terms[7];
+  const float S = P + T + g.smooth;
+  const float go = g.grad_out ? g.grad_out[0] : 1.f;
+  const float inv_n = (float)(1.0 / ((double)g.B * HW));
+  const float inv_s2 = 1.f / (S * S);
+  const float cA = go * g.dice_w * (2.f * I + g.smooth) * inv_s2;
+  const float cT = -go * g.dice_w * 2.f * S * inv_s2;
+  const float cB = go * g.bce_w * inv_n;
+  const float cR = go * g.rd_w * 2.f * inv_n, cRD = cR * g.D;
+  const float cPa = go * g.pf_w * inv_n * g.eps * 0.25f, cPw = go * g.pf_w * inv_n * 2.f / g.eps;
+  const float fa = 2.f * (1.f + g.a);
+
+  for (int k = threadIdx.x; k < (nr + 4) * SW; k += 256) {
+    const int r = k / SW, c = k - r * SW - 2;
+    const int gy = clampi(refl(y0 - 2 + r, H), 0, H - 1), gx = clampi(refl(c, W), 0, W - 1);
+    su[k] = u[(size_t)gy * W + gx];
+  }
+  __syncthreads();
+  if constexpr (RD) {
+    for (int k = threadIdx.x; k < (nr + 2) * SR; k += 256) {
+      const int rr = k / SR, cc = k - rr * SR - 1;
+      const int yy = y0 - 1 + rr;
+      float r = 0.f;
+      if (yy >= 0 && yy < H && cc >= 0 && cc < W) {
+        const float* sc = su + (rr + 1) * SW + cc + 2;
+        const float c0 = sc[0];
+        const float lap = (sc[-SW] + sc[SW]) + (sc[-1] + sc[1]) - 4.f * c0;
+        r = fmaf(g.D, lap, fmaf(-c0, c0, c0) * (c0 - g.a));
+      }
+      sr[k] = r;
+    }
+    __syncthreads();
+  }
+  for (int k = threadIdx.x; k < nr * W; k += 256) {
+    const int r = k / W, x = k - r * W, y = y0 + r;
+    const float* sc = su + (r + 2) * SW + x + 2;
+    const float p = sc[0], t = tt[(size_t)y * W + x];
+    const float qq = fmaf(-p, p, p);
+    float grad = fmaf(cT, t, cA);
+    grad = fmaf(cB * (p - t), __builtin_amdgcn_rcpf(fmaxf(qq, 1e-12f)), grad);
+    if constexpr (RD) {
+      const float* sq = sr + (r + 1) * SR + x + 1;
+      const float rk = sq[0], ru = sq[-SR], rd = sq[SR], rl = sq[-1], rrt = sq[1];
+      float adj = (ru + rd) + (rl + rrt) - 4.f * rk;
+      adj += (y == 1 ? ru : 0.f) + (y == H - 2 ? rd : 0.f);
+      adj += (x == 1 ? rl : 0.f) + (x == W - 2 ? rrt : 0.f);
+      const float fp = fmaf(p, fmaf(-3.f, p, fa), -g.a);
+      grad = fmaf(cRD, adj, fmaf(cR * rk, fp, grad));
+    }
+    if constexpr (PF) {
+      float adj = 0.f;
+      adj += x >= 1 ? p - sc[-2] : 0.f;
+      adj -= x <= W - 2 ? sc[2] - p : 0.f;
+      adj += y >= 1 ? p - sc[-2 * SW] : 0.f;
+      adj -= y <= H - 2 ? sc[2 * SW] - p : 0.f;
+      grad = fmaf(cPa, adj, fmaf(cPw * qq, 1.f - 2.f * p, grad));
+    }
+    if (g.du_out) g.du_out[b * HW + (size_t)y * W + x] = grad;
+    sdz[k] = grad * qq;  // sigmoid chain: dz = dL/du * u (1 - u)
+  }
+  __syncthreads();
+
+  // head backward over the block's pixels (C/4 lanes per pixel, as head_bwd_kernel)
+  const int c4n = g.C / 4, rows = 256 / c4n;
+  const int pr = threadIdx.x / c4n, c4 = threadIdx.x - pr * c4n;
+  const int64_t p0 = (int64_t)b * HW + (int64_t)y0 * W;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  float accb = 0.f;
+  if (pr < rows) {
+    const f32x4 wv = *reinterpret_cast<const f32x4*>(g.w + 4 * c4);
+    for (int k = pr; k < nr * W; k += rows) {
+      const float d = sdz[k];
+      if (c4 == 0) accb += d;
+      const int64_t pix = p0 + k;
+      const f32x4 xv = *reinterpret_cast<const f32x4*>(g.x + pix * g.ldx + 4 * c4);
+      f32x4 o;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        o[j] = xv[j] > 0.f ? d * wv[j] : 0.f;
+        acc[j] = fmaf(d, xv[j], acc[j]);
+      }
+      *reinterpret_cast<f32x4*>(g.dx + pix * g.lddx + 4 * c4) = o;
+    }
+  }
+  __syncthreads();  // sdz is dead: reuse the staging area for the block reduction
+  f32x4* red = reinterpret_cast<f32x4*>(smem);
+  float* redb = reinterpret_cast<float*>(red + 256);
+  red[threadIdx.x] = acc;
+  redb[threadIdx.x] = accb;
+  __syncthreads();
+  const int blk = blockIdx.y * gridDim.x + blockIdx.x;
+  if ((int)threadIdx.x < c4n) {
+    f32x4 s4 = red[threadIdx.x];
+    for (int k = 1; k < rows; ++k) s4 += red[k * c4n + threadIdx.x];
+    *reinterpret_cast<f32x4*>(g.part + (size_t)blk * g.C + 4 * threadIdx.x) = s4;
+  }
+  if (threadIdx.x == 0) {
+    float s1 = 0.f;
+    for (int k = 0; k < rows; ++k) s1 += redb[k * c4n];
+    g.part_b[blk] = s1;
+  }
+}
+
 __global__ void pde_fields_kernel(const float* __restrict__ u0, int B, int H, int W, float D,
                                   float a, float* __restrict__ lap_o, float* __restrict__ res_o,
                                   float* __restrict__ gm_o) {
@@ -510,4 +650,51 @@ extern "C" int pis_pde_fields(const float* u, int B, int H, int W, float D, floa
   hipLaunchKernelGGL(pde_fields_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, u, B, H, W,
                      D, a, lap, residual, gradmag2);
   return launch_status("pde_fields");
+}
+
+static int head_loss_rows(int H, int W) { return std::max(1, std::min(H, 1024 / std::max(1, W))); }
+
+static size_t head_loss_smem(int R, int W, bool rd) {
+  const size_t f = (size_t)(R + 4) * (W + 4) + (rd ? (size_t)(R + 2) * (W + 2) : 0) + (size_t)R * W;
+  return std::max(f * sizeof(float), (size_t)256 * 20);  // >= the reduction scratch
+}
+
+extern "C" size_t pis_head_loss_bwd_ws(int B, int H, int W, int C) {
+  const int R = head_loss_rows(H, W);
+  const size_t blocks = (size_t)B * ((H + R - 1) / R);
+  return blocks * (C + 1) * sizeof(float) + 256;
+}
+
+extern "C" int pis_head_loss_bwd(const float* x, int ldx, const float* w, const float* u, const float* t,
+                                 float* du_out, int B, int H, int W, int C,
+                                 const pis_loss_params* prm, const float* terms, const float* grad_out,
+                                 float* dx, int lddx, float* dw, float* db, int flags, void* ws,
+                                 size_t ws_bytes, pis_stream_t stream) {
+  PIS_CHECK_ARG(x && w && u && t && prm && terms && dx && dw && B > 0 && H >= 2 && W >= 2,
+                "pis_head_loss_bwd: bad arguments");
+  PIS_CHECK_ARG(C % 4 == 0 && C / 4 <= 256 && ldx % 4 == 0 && lddx % 4 == 0,
+                "pis_head_loss_bwd: C and ld must be multiples of 4, C <= 1024");
+  PIS_CHECK_ARG(W <= 1024, "pis_head_loss_bwd: W > 1024 (stage rows do not fit LDS); use pis_loss_bwd + pis_head_bwd");
+  PIS_CHECK_ARG(ws && ws_bytes >= pis_head_loss_bwd_ws(B, H, W, C), "pis_head_loss_bwd: workspace too small");
+  HeadLossArgs g{};
+  g.x = x; g.ldx = ldx; g.w = w; g.u = u; g.t = t; g.du_out = du_out;
+  g.B = B; g.H = H; g.W = W; g.C = C; g.R = head_loss_rows(H, W);
+  g.dice_w = prm->dice_w; g.bce_w = prm->bce_w; g.rd_w = prm->rd_w; g.pf_w = prm->pf_w;
+  g.smooth = prm->smooth; g.D = prm->D; g.a = prm->a; g.eps = prm->eps;
+  g.terms = terms; g.grad_out = grad_out; g.dx = dx; g.lddx = lddx;
+  const dim3 grid((H + g.R - 1) / g.R, B);
+  g.part = (float*)ws;
+  g.part_b = g.part + (size_t)grid.x * grid.y * C;
+  hipStream_t s = (hipStream_t)stream;
+  const bool rd = prm->rd_w > 0.f, pf = prm->pf_w > 0.f;
+  const size_t smem = head_loss_smem(g.R, W, rd);
+  if (rd && pf) hipLaunchKernelGGL((head_loss_bwd_kernel<true, true>), grid, dim3(256), smem, s, g);
+  else if (rd) hipLaunchKernelGGL((head_loss_bwd_kernel<true, false>), grid, dim3(256), smem, s, g);
+  else if (pf) hipLaunchKernelGGL((head_loss_bwd_kernel<false, true>), grid, dim3(256), smem, s, g);
+  else hipLaunchKernelGGL((head_loss_bwd_kernel<false, false>), grid, dim3(256), smem, s, g);
+  int rc = launch_status("head_loss_bwd");
+  const int acc = flags & PIS_ACCUMULATE;
+  if (!rc) rc = reduce_slabs(g.part, (int)(grid.x * grid.y), C, dw, acc, s);
+  if (!rc && db) rc = reduce_slabs(g.part_b, (int)(grid.x * grid.y), 1, db, acc, s);
+  return rc;
 }

@@ -1,7 +1,8 @@
 """Autograd wrapper of the fused Dice + BCE + reaction-diffusion + phase-field
 kernel (pis_loss_fwd / pis_loss_bwd). One forward launch pair computes every
 loss term, the whole-batch Dice sums and the per-sample thresholded metric
-counters; the backward is one elementwise launch.
+counters; the backward is one elementwise launch — or, when the prediction is
+the U-Net's own output, part of the head backward kernel (pis_head_loss_bwd).
 
 Used by src-compatible ``loss`` (src/loss.py:7-162), ``pde``
 (src/pde.py:124-212) and ``metrics`` (src/metrics.py:4-73) modules.
@@ -91,16 +92,24 @@ class _FusedLoss(torch.autograd.Function):
         sink["terms"], sink["counts"], sink["scores"] = terms, counts, scores
         ctx.cfg = cfg
         ctx.shape = u.shape
-        ctx.save_for_backward(u.detach().contiguous(), t.to(torch.float32).contiguous(), terms)
+        # produced directly by the U-Net engine? then the backward runs fused with its head
+        ctx.eng = getattr(u.grad_fn, "eng", None)
+        ctx.gen = getattr(u.grad_fn, "gen", None)
+        ctx.save_for_backward(u.detach().contiguous(), t.to(device=u.device, dtype=torch.float32).contiguous(),
+                              terms)
         return terms[0].clone()
 
     @staticmethod
     def backward(ctx, g):
         u, t, terms = ctx.saved_tensors
         B, H, W = _bhw(u)
-        du = torch.empty_like(u)
         g = g.to(torch.float32).contiguous()
         prm = ctx.cfg.params()
+        eng = ctx.eng
+        if eng is not None and hasattr(eng, "can_fuse_loss") and eng.can_fuse_loss(u, ctx.gen):
+            du = eng.fuse_loss_backward(t, ctypes.byref(prm), terms, g)
+            return du.view(ctx.shape), None, None, None
+        du = torch.empty_like(u)
         call("pis_loss_bwd", u.data_ptr(), t.data_ptr(), B, H, W, ctypes.byref(prm), terms.data_ptr(),
              g.data_ptr(), du.data_ptr(), 0, _hip.stream_handle())
         return du.view(ctx.shape), None, None, None

@@ -278,7 +278,7 @@ class _UNetFunction(torch.autograd.Function):
         if eng.generation != ctx.gen:
             raise RuntimeError("UNet.backward: another forward ran since this graph was built "
                                "(activations are kept in one set of engine buffers)")
-        grads = eng.backward(du.contiguous())
+        grads = eng.backward(du)
         return (None, None, None) + tuple(grads)
 
 
@@ -318,6 +318,7 @@ class UNetEngine:
         self.bufs: Dict[str, torch.Tensor] = {}
         self._offsets = {id(mod._parameters[pn]): (o, n) for mod, pn, _, _, o, n in model._entries}
         self.last_grad_mode = None
+        self.pending_head = None  # dL/du tensor whose head backward already ran fused with the loss
 
     # ---- planning -----------------------------------------------------------
     def _plan(self, B: int, H: int, W: int, dev: torch.device):
@@ -345,6 +346,8 @@ class UNetEngine:
         self.B, self.H, self.W = B, H, W
         lib = _hip.lib()
         ws = lib.pis_head_bwd_ws(B * H * W, c)
+        if W <= 1024:
+            ws = max(ws, lib.pis_head_loss_bwd_ws(B, H, W, c))
         for l in range(1, 5):
             Hl, Wl, Cl = H >> (l - 1), W >> (l - 1), c << (l - 1)
             cin0 = self.m.in_channels if l == 1 else Cl // 2
@@ -456,6 +459,32 @@ class UNetEngine:
             return u
         return u
 
+    # ---- loss backward fused into the head backward ---------------------------
+    def can_fuse_loss(self, u: torch.Tensor, generation: int) -> bool:
+        return (generation == self.generation and self.pending_head is None and self.W <= 1024
+                and u.data_ptr() == self.u.data_ptr())
+
+    @torch.no_grad()
+    def fuse_loss_backward(self, t: torch.Tensor, prm, terms: torch.Tensor, g: torch.Tensor) -> torch.Tensor:
+        """Run the loss backward and the head backward as one kernel (pis_head_loss_bwd)
+        from inside the loss's autograd backward. Returns dL/du (written too, so any
+        other consumer of u sees the exact gradient); the U-Net backward recognises
+        that tensor and skips its own head step (only the head's dW/db still go into
+        the gradient arena, in the arena's accumulate/overwrite mode)."""
+        m, c = self.m, self.c
+        B, H, W = self.B, self.H, self.W
+        st = self._stream()
+        d1 = _Buf(self.bufs["d1_1"], c)
+        g_d1 = _Buf(self._gbuf("g_d1_1", B, H, W, c), c)
+        self.head_scratch = self._gbuf("head_scratch", c + 1)
+        hs = self.head_scratch.data_ptr()
+        du = torch.empty_like(self.u)
+        call("pis_head_loss_bwd", d1.p, d1.ld, m.out_conv.weight.data_ptr(), self.u.data_ptr(), t.data_ptr(),
+             du.data_ptr(), B, H, W, c, prm, terms.data_ptr(), g.data_ptr(), g_d1.p, g_d1.ld, hs, hs + 4 * c, 0,
+             self.ws.data_ptr(), self.ws_bytes, st)
+        self.pending_head = du
+        return du
+
     # ---- backward ------------------------------------------------------------
     def _grad_mode(self) -> str:
         """'overwrite' when every .grad is None (zero_grad(set_to_none=True)),
@@ -515,9 +544,18 @@ class UNetEngine:
         # head: sigmoid backward + 1x1 conv + ReLU backward of dec1.conv1
         d1 = _Buf(bf["d1_1"], c)
         g_d1 = _Buf(gb("g_d1_1", B, H, W, c), c)
-        call("pis_head_bwd", d1.p, d1.ld, m.out_conv.weight.data_ptr(), du.data_ptr(), self.u.data_ptr(),
-             g_d1.p, g_d1.ld, self._gptr(m.out_conv.weight), self._gptr(m.out_conv.bias), B * H * W, c, acc,
-             ws, wsb, st)
+        fused, self.pending_head = self.pending_head, None
+        if fused is not None and du.data_ptr() == fused.data_ptr():
+            # the loss backward already ran the head backward (pis_head_loss_bwd): g_d1 is
+            # written and the head's dW/db wait in the scratch; only their arena update is left
+            hs = self.head_scratch
+            call("pis_colsum", hs.data_ptr(), c, 1, c, self._gptr(m.out_conv.weight), acc, ws, wsb, st)
+            call("pis_colsum", hs.data_ptr() + 4 * c, 1, 1, 1, self._gptr(m.out_conv.bias), acc, ws, wsb, st)
+        else:
+            du = du.contiguous()
+            call("pis_head_bwd", d1.p, d1.ld, m.out_conv.weight.data_ptr(), du.data_ptr(), self.u.data_ptr(),
+                 g_d1.p, g_d1.ld, self._gptr(m.out_conv.weight), self._gptr(m.out_conv.bias), B * H * W, c, acc,
+                 ws, wsb, st)
         self._ready(m.out_conv.weight, m.out_conv.bias)
 
         g_top = g_d1  # dz of dec_l.conv1

@@ -132,6 +132,52 @@ def test_train_step_grads(hip, loss_kw, shape):
     assert worst[0][0] < TOL, worst[:5]
 
 
+def test_loss_backward_fused_with_head(hip):
+    """crit(net(x), t) runs the loss backward inside the head backward kernel; any other
+    use of u (a view, a second loss term) takes the unfused path — same gradients."""
+    from physics_informed_image_segmentation_amd import DiceBCEPDELoss, _hip as hipmod
+    img, mask = rt.synthetic_batch(2, 64, 64, seed=3)
+    img, mask = img.cuda(), mask.cuda()
+    net, _ = make_pair(3)
+    net.eval()  # no dropout: three identical forwards
+    crit = DiceBCEPDELoss(pde_weight=1e-2, phase_field_weight=1e-2, diffusion_coeff=5.0, epsilon=0.05)
+    calls = []
+
+    class Tracer:
+        def begin(self, name, args):
+            calls.append(name)
+
+        def end(self, tok):
+            pass
+
+    def grads(loss_fn):
+        net.zero_grad(set_to_none=True)
+        calls.clear()
+        hipmod.set_tracer(Tracer())
+        try:
+            u = net(img)
+            loss_fn(u).backward()
+        finally:
+            hipmod.set_tracer(None)
+        torch.cuda.synchronize()
+        return {n: p.grad.detach().clone() for n, p in net.named_parameters()}, list(calls)
+
+    g_fused, c_fused = grads(lambda u: crit(u, mask))
+    assert "pis_head_loss_bwd" in c_fused and "pis_head_bwd" not in c_fused and "pis_loss_bwd" not in c_fused
+    g_view, c_view = grads(lambda u: crit(u.view(u.shape), mask))
+    assert "pis_head_loss_bwd" not in c_view and "pis_head_bwd" in c_view
+    # same math, different fp32 summation grouping of the head's dW (row blocks vs pixel ranges)
+    # and u(1-u) as fma(-u, u, u): agreement to ~1e-6, far inside the 1e-4 parity bar
+    for n in g_fused:
+        assert rel(g_fused[n], g_view[n]) < 1e-5, n
+    # a second consumer of u: autograd sums dL/du, the engine sees a new tensor -> unfused head
+    g_two, c_two = grads(lambda u: crit(u, mask) + 0.5 * (u * u).mean())
+    g_ref, _ = grads(lambda u: crit(u.view(u.shape), mask) + 0.5 * (u * u).mean())
+    assert "pis_head_bwd" in c_two
+    for n in g_two:
+        assert rel(g_two[n], g_ref[n]) < 1e-5, n
+
+
 def test_grad_accumulation_and_arena(hip):
     net, ref, u, crit, p_ref, terms, _ = _step_pair(1, 32, 32, dict())
     g1 = {n: p.grad.clone() for n, p in net.named_parameters()}
