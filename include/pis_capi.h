@@ -55,7 +55,8 @@ int pis_version(void);
 #define PIS_TUNE_HALO_VARIANT 4 /* 0: auto, 1: 4-channel slices for BN=64, 2: BN=256 tiles when N >= 256, 3: 8-channel slices for BN=64 */
 #define PIS_TUNE_WGRAD_VARIANT 5 /* 0: one 16-pixel segment per stage, 1: two (default) */
 #define PIS_TUNE_WGRAD_BLOCKS 6  /* target workgroups of the split-K halo wgrad (default 512: one round at 2 per CU) */
-#define PIS_TUNE_NKEYS 7
+#define PIS_TUNE_C1_WGRAD 7      /* Cin == 1 weight gradient: 0 VALU stream kernel (default), 1 padded MFMA tile */
+#define PIS_TUNE_NKEYS 8
 #define PIS_DEBUG_NOLOAD (1 << 16)
 int pis_tune(int key, int value);
 

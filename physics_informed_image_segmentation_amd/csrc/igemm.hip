@@ -444,47 +444,49 @@ static int launch_conv3x3(const IGemmArgs& a, hipStream_t s) {
   return launch_status("conv3x3_halo");
 }
 
-__global__ void conv3x3_c1_fwd_kernel(const float* __restrict__ x, int ldx,
-                                      const float* __restrict__ w, const float* __restrict__ bias,
-                                      const float* __restrict__ scale, float* __restrict__ y,
-                                      int ldy, int B, int H, int W, int Cout, int flags) {
-  // Cin == 1 (enc1.conv0): 16 lanes per pixel, each lane 4 output channels.
-  extern __shared__ float sw[];  // [9][Cout] + bias
-  for (int i = threadIdx.x; i < 9 * Cout; i += blockDim.x) {
-    const int n = i / 9, t = i - n * 9;
-    sw[t * Cout + n] = w[i];
-  }
-  for (int i = threadIdx.x; i < Cout; i += blockDim.x) sw[9 * Cout + i] = bias ? bias[i] : 0.f;
-  __syncthreads();
-  const int64_t npix = (int64_t)B * H * W;
+__global__ __launch_bounds__(256) void conv3x3_c1_fwd_kernel(const float* __restrict__ x, int ldx,
+                                                             const float* __restrict__ w,
+                                                             const float* __restrict__ bias,
+                                                             const float* __restrict__ scale,
+                                                             float* __restrict__ y, int ldy, int B, int H,
+                                                             int W, int Cout, int flags) {
+  // Cin == 1 (enc1.conv0): an HBM-write-bound stream (4*Cout B per pixel). Cout/4 lanes per
+  // pixel, each owning 4 output channels whose 9 taps + bias live in registers; the grid
+  // strides over pixels so the weights are loaded once per thread.
   const int lanes_per_pix = Cout / 4;
-  const int64_t gtid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t p = gtid / lanes_per_pix;
-  const int c4 = (int)(gtid - p * lanes_per_pix) * 4;
-  if (p >= npix) return;
-  const int HW = H * W;
-  const int b = (int)(p / HW), rem = (int)(p - (int64_t)b * HW), h = rem / W, wc = rem - h * W;
-  float xv[9];
-#pragma unroll
-  for (int t = 0; t < 9; ++t) {
-    const int hh = h + t / 3 - 1, ww = wc + t % 3 - 1;
-    xv[t] = (hh >= 0 && hh < H && ww >= 0 && ww < W) ? x[((int64_t)b * HW + hh * W + ww) * ldx] : 0.f;
-  }
-  f32x4 acc;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) acc[j] = sw[9 * Cout + c4 + j];
-#pragma unroll
-  for (int t = 0; t < 9; ++t)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[j] = fmaf(xv[t], sw[t * Cout + c4 + j], acc[j]);
+  const int pix_per_block = 256 / lanes_per_pix;
+  const int lp = threadIdx.x / lanes_per_pix;
+  const int c4 = (threadIdx.x - lp * lanes_per_pix) * 4;
+  if (lp >= pix_per_block) return;
+  f32x4 wt[9], b4;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    float v = acc[j];
-    if (flags & PIS_RELU) v = fmaxf(v, 0.f);
-    if (flags & PIS_SCALE) v *= scale[(size_t)b * Cout + c4 + j];
-    acc[j] = v;
+    b4[j] = bias ? bias[c4 + j] : 0.f;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) wt[t][j] = w[(c4 + j) * 9 + t];
   }
-  *reinterpret_cast<f32x4*>(y + p * ldy + c4) = acc;
+  const int HW = H * W;
+  const int64_t npix = (int64_t)B * HW;
+  for (int64_t p = (int64_t)blockIdx.x * pix_per_block + lp; p < npix; p += (int64_t)gridDim.x * pix_per_block) {
+    const int b = (int)(p / HW), rem = (int)(p - (int64_t)b * HW), h = rem / W, wc = rem - h * W;
+    const float* xb = x + (int64_t)b * HW * ldx;
+    f32x4 acc = b4;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int hh = h + t / 3 - 1, ww = wc + t % 3 - 1;
+      const float xv = (hh >= 0 && hh < H && ww >= 0 && ww < W) ? xb[(int64_t)(hh * W + ww) * ldx] : 0.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[j] = fmaf(xv, wt[t][j], acc[j]);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float v = acc[j];
+      if (flags & PIS_RELU) v = fmaxf(v, 0.f);
+      if (flags & PIS_SCALE) v *= scale[(size_t)b * Cout + c4 + j];
+      acc[j] = v;
+    }
+    *reinterpret_cast<f32x4*>(y + p * ldy + c4) = acc;
+  }
 }
 
 __global__ void conv3x3_flip_kernel(const float* __restrict__ w, float* __restrict__ wf, int Cin,
@@ -531,9 +533,9 @@ extern "C" int pis_conv3x3_fwd(const float* x, int ldx, const float* w_krsc, con
   if (Cin == 1) {
     PIS_CHECK_ARG(Cout <= 1024, "pis_conv3x3_fwd: Cin==1 path supports Cout<=1024");
     const int64_t threads = (int64_t)B * H * W * (Cout / 4);
-    hipLaunchKernelGGL(conv3x3_c1_fwd_kernel, dim3((unsigned)cdiv(threads, 256)), dim3(256),
-                       (size_t)10 * Cout * sizeof(float), s, x, ldx, w_krsc, bias, scale, y, ldy, B,
-                       H, W, Cout, flags);
+    const int64_t blocks = std::min<int64_t>(cdiv(threads, 256), 4096);
+    hipLaunchKernelGGL(conv3x3_c1_fwd_kernel, dim3((unsigned)blocks), dim3(256), 0, s, x, ldx, w_krsc, bias,
+                       scale, y, ldy, B, H, W, Cout, flags);
     return launch_status("conv3x3_c1_fwd");
   }
   PIS_CHECK_ARG(Cin % 4 == 0 && ldx % 4 == 0, "pis_conv3x3_fwd: Cin/ldx must be multiples of 4");

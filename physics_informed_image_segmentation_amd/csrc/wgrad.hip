@@ -541,9 +541,58 @@ static HaloPlan halo_plan(int B, int H, int W, int Cin, int Cout) {
   return p;
 }
 
+// Cin == 1 (enc1.conv0): dw[n][t] = sum_p dz[p][n] x[p + tap t], db[n] = sum_p dz[p][n].
+// K = 9 is far too short for MFMA and the pass is a read of dz (4*Cout B/px): Cout/4 lanes
+// per pixel hold 4 channels x (9 taps + bias) fp32 accumulators, the grid walks contiguous
+// pixel ranges, per-block partials go through the deterministic slab reduction.
+constexpr int C1_BLOCKS = 1024;
+
+__global__ __launch_bounds__(256) void wgrad_c1_kernel(const float* __restrict__ x, int ldx,
+                                                       const float* __restrict__ dz, int ldz, int B, int H,
+                                                       int W, int Cout, int64_t pix_per_block,
+                                                       float* __restrict__ part, float* __restrict__ part_b) {
+  __shared__ f32x4 red[256][10];
+  const int lanes = Cout / 4, groups = 256 / lanes;
+  const int lp = threadIdx.x / lanes, q = threadIdx.x - lp * lanes, c4 = 4 * q;
+  f32x4 acc[10];
+#pragma unroll
+  for (int k = 0; k < 10; ++k) acc[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int HW = H * W;
+  const int64_t npix = (int64_t)B * HW;
+  const int64_t p0 = (int64_t)blockIdx.x * pix_per_block, p1 = min(npix, p0 + pix_per_block);
+  if (lp < groups) {
+    for (int64_t p = p0 + lp; p < p1; p += groups) {
+      const int b = (int)(p / HW), rem = (int)(p - (int64_t)b * HW), h = rem / W, wc = rem - h * W;
+      const f32x4 dv = *reinterpret_cast<const f32x4*>(dz + p * ldz + c4);
+      acc[9] += dv;
+      const float* xb = x + (int64_t)b * HW * ldx;
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int hh = h + t / 3 - 1, ww = wc + t % 3 - 1;
+        const float xv = (hh >= 0 && hh < H && ww >= 0 && ww < W) ? xb[(int64_t)(hh * W + ww) * ldx] : 0.f;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[t][j] = fmaf(xv, dv[j], acc[t][j]);
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 10; ++k) red[threadIdx.x][k] = acc[k];
+  __syncthreads();
+  // fixed-order sum over the pixel groups: output o = (n, k) with k = tap (0..8) or bias (9)
+  for (int o = threadIdx.x; o < 10 * Cout; o += 256) {
+    const int n = o / 10, k = o - n * 10, qq = n >> 2, j = n & 3;
+    float sum = 0.f;
+    for (int gi = 0; gi < groups; ++gi) sum += red[gi * lanes + qq][k][j];
+    if (k < 9) part[(size_t)blockIdx.x * 9 * Cout + n * 9 + k] = sum;
+    else if (part_b) part_b[(size_t)blockIdx.x * Cout + n] = sum;
+  }
+}
+
 extern "C" size_t pis_conv3x3_wgrad_ws(int B, int H, int W, int Cin, int Cout) {
   const HaloPlan hp = halo_plan(B, H, W, Cin, Cout);
   if (hp.use) return cdiv(hp.part_bytes, 256) * 256 + hp.bias_bytes + 256;
+  if (Cin == 1 && tune_get(PIS_TUNE_C1_WGRAD) == 0)
+    return (size_t)C1_BLOCKS * 10 * Cout * sizeof(float) + 512;
   const WgradPlan pl = conv_plan(B, H, W, Cin, Cout);
   // Cin == 1 computes a padded [Cout][64] tile and compacts it through a staging slab
   const size_t stage = Cin == 1 ? (size_t)Cout * 64 * sizeof(float) + 256 : 0;
@@ -588,6 +637,20 @@ extern "C" int pis_conv3x3_wgrad(const float* x, int ldx, const float* dz, int l
     if (!rc) rc = reduce_slabs(a.part, hp.splits, (int64_t)Cout * 9 * Cin, dw_krsc, acc, s);
     if (rc || !db) return rc;
     return reduce_slabs(a.part_bias, hp.splits, Cout, db, acc, s);
+  }
+  if (Cin == 1 && tune_get(PIS_TUNE_C1_WGRAD) == 0) {
+    PIS_CHECK_ARG(Cout <= 1024 && Cout % 4 == 0, "pis_conv3x3_wgrad: Cin == 1 needs Cout % 4 == 0, <= 1024");
+    const int64_t npix = (int64_t)B * H * W;
+    const int64_t ppb = cdiv(npix, C1_BLOCKS);
+    const int blocks = (int)cdiv(npix, ppb);
+    float* part = (float*)ws;
+    float* part_b = db ? part + (size_t)C1_BLOCKS * 9 * Cout : nullptr;
+    hipLaunchKernelGGL(wgrad_c1_kernel, dim3(blocks), dim3(256), 0, s, x, ldx, dz, ldz, B, H, W, Cout, ppb,
+                       part, part_b);
+    int rc = launch_status("wgrad_c1");
+    if (!rc) rc = reduce_slabs(part, blocks, (int64_t)9 * Cout, dw_krsc, acc, s);
+    if (!rc && db) rc = reduce_slabs(part_b, blocks, Cout, db, acc, s);
+    return rc;
   }
   const WgradPlan pl = conv_plan(B, H, W, Cin, Cout);
   WgradArgs a{};

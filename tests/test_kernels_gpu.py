@@ -102,7 +102,7 @@ def test_conv3x3_dgrad_wgrad(hip, B, H, W, Cin, Cout):
 
 
 # every non-default kernel variant behind pis_tune (include/pis_capi.h) stays exact too
-TUNE_VARIANTS = [(4, 1), (4, 2), (4, 3), (5, 0), (6, 2048), (3, 0)]
+TUNE_VARIANTS = [(4, 1), (4, 2), (4, 3), (5, 0), (6, 2048), (3, 0), (7, 1)]
 
 
 @pytest.mark.parametrize("key,value", TUNE_VARIANTS)
@@ -113,6 +113,7 @@ def test_conv3x3_tuned_variants(hip, key, value):
             test_conv3x3_fwd(hip, *shape)
         for shape in [(2, 16, 32, 64, 128), (1, 32, 16, 128, 64), (2, 16, 48, 256, 256)]:
             test_conv3x3_dgrad_wgrad(hip, *shape)
+        test_conv3x3_c1_wgrad(hip)
     finally:
         hip.pis_tune(key, prev)
 

@@ -22,6 +22,9 @@ LAYERS = [  # name, H, Cin, Cout
 ]
 B = 8
 NOLOAD_KEY = 2
+UP_LAYERS = [  # name, input H, Cin, Cout (2x2 stride-2 transposed convs)
+    ("up1", 256, 128, 64), ("up2", 128, 256, 128), ("up3", 64, 512, 256), ("up4", 32, 512, 512),
+]
 
 
 def timed(fn, reps=3):
@@ -43,14 +46,17 @@ def main():
     ap.add_argument("--layers", default="")
     ap.add_argument("--ops", default="fwd,dgrad,wgrad")
     ap.add_argument("--noload", action="store_true", help="also time each variant without global loads")
+    ap.add_argument("--convt", action="store_true", help="time the transposed convs instead")
     args = ap.parse_args()
     lib = _hip.lib()
     variants = [int(v) for v in args.variants.split(",")]
     default = lib.pis_tune(args.key, -1)
     s = torch.cuda.current_stream().cuda_stream
     dev = torch.device("cuda")
-    sel = [l for l in LAYERS if not args.layers or l[0] in args.layers.split(",")]
     opsel = args.ops.split(",")
+    if args.convt:
+        return bench_convt(lib, args, variants, default, s, dev, opsel)
+    sel = [l for l in LAYERS if not args.layers or l[0] in args.layers.split(",")]
     for name, H, cin, cout in sel:
         x = torch.rand(B, H, H, cin, device=dev)
         dz = torch.randn(B, H, H, cout, device=dev)
@@ -92,6 +98,44 @@ def main():
             print(line, flush=True)
         del x, dz, w, y, dx, ws, dw
         torch.cuda.empty_cache()
+
+
+def bench_convt(lib, args, variants, default, s, dev, opsel):
+    for name, H, cin, cout in UP_LAYERS:
+        x = torch.rand(B, H, H, cin, device=dev)
+        dy = torch.randn(B, 2 * H, 2 * H, cout, device=dev)
+        w = torch.randn(2, 2, cout, cin, device=dev) * 0.05
+        bias = torch.randn(cout, device=dev)
+        wc = torch.empty(cin * 4 * cout, device=dev)
+        lib.pis_convt2x2_prep(w.data_ptr(), wc.data_ptr(), cin, cout, s)
+        y = torch.empty(B, 2 * H, 2 * H, cout, device=dev)
+        dx = torch.empty(B, H, H, cin, device=dev)
+        nws = lib.pis_convt2x2_wgrad_ws(B, H, H, cin, cout)
+        ws = torch.empty(nws // 4 + 1, device=dev)
+        dw = torch.empty(4 * cout * cin, device=dev)
+        db = torch.empty(cout, device=dev)
+        flops = 2.0 * B * H * H * 4 * cout * cin
+        ops = {
+            "fwd": lambda: lib.pis_convt2x2_fwd(x.data_ptr(), cin, w.data_ptr(), bias.data_ptr(), y.data_ptr(), cout,
+                                                B, H, H, cin, cout, s),
+            "dgrad": lambda: lib.pis_convt2x2_dgrad(dy.data_ptr(), cout, wc.data_ptr(), x.data_ptr(), cin,
+                                                    dx.data_ptr(), cin, B, H, H, cin, cout, 4, s),
+            "wgrad": lambda: lib.pis_convt2x2_wgrad(x.data_ptr(), cin, dy.data_ptr(), cout, dw.data_ptr(),
+                                                    db.data_ptr(), B, H, H, cin, cout, 0, ws.data_ptr(), nws, s),
+        }
+        results = {}
+        for _ in range(args.rounds):
+            for v in variants:
+                lib.pis_tune(args.key, v)
+                for op in opsel:
+                    results.setdefault((op, v), []).append(timed(ops[op]))
+        lib.pis_tune(args.key, default)
+        for op in opsel:
+            line = f"{name:12s} {op:6s}"
+            for v in variants:
+                ms = min(results[(op, v)])
+                line += f"  v{v}: {ms:7.3f} ms {flops / ms / 1e9:6.1f} TF/s"
+            print(line, flush=True)
 
 
 if __name__ == "__main__":
