@@ -56,7 +56,8 @@ def conv_flops_per_image(H: int, W: int, c: int = 64) -> float:
     return 2.0 * macs * 3 - 2.0 * first
 
 
-IGEMM_CALLS = ("pis_conv3x3_fwd", "pis_conv3x3_dgrad", "pis_convt2x2_fwd", "pis_convt2x2_dgrad")
+IGEMM_CALLS = ("pis_conv3x3_fwd", "pis_conv3x3_dgrad", "pis_conv3x3_fwd_ex", "pis_conv3x3_dgrad_ex",
+               "pis_convt2x2_fwd", "pis_convt2x2_dgrad")
 DOMINANT = "conv3x3_halo_kernel<128, 4>"
 
 
@@ -64,8 +65,8 @@ def igemm_shape(name, a):
     """(M, N, K, kernel) of the implicit GEMM one C-ABI call launches (mirrors the
     dispatch in csrc/igemm.hip: 3x3 convs on H%8 == 0, W%16 == 0 grids take the
     halo kernel, BN = 64 for <= 64 output channels)."""
-    if name in ("pis_conv3x3_fwd", "pis_conv3x3_dgrad"):
-        if name == "pis_conv3x3_fwd":
+    if name.startswith("pis_conv3x3_"):
+        if name.startswith("pis_conv3x3_fwd"):
             Bb, Hh, Ww, cin, cout = a[7:12]
             if cin == 1:
                 return None
@@ -73,6 +74,8 @@ def igemm_shape(name, a):
         else:
             Bb, Hh, Ww, cin, cout = a[8:13]
             M, N, K, csrc, flags = Bb * Hh * Ww, cin, 9 * cout, cout, a[13]
+        if name.endswith("_ex") and min(csrc, N) >= 256 and Hh % 2 == 0 and Ww % 2 == 0:
+            return M, N, K, "winograd"  # csrc/igemm.hip:wino_wanted_dims (default policy)
         bn = 64 if N <= 64 else 128
         if Hh % 8 == 0 and Ww % 16 == 0 and csrc % 4 == 0:
             ck = 8 if bn == 64 and csrc % 8 == 0 and not flags & 4 else 4  # PIS_MASK -> 4-channel slices

@@ -56,7 +56,8 @@ int pis_version(void);
 #define PIS_TUNE_WGRAD_VARIANT 5 /* 0: one 16-pixel segment per stage, 1: two (default) */
 #define PIS_TUNE_WGRAD_BLOCKS 6  /* target workgroups of the split-K halo wgrad (default 512: one round at 2 per CU) */
 #define PIS_TUNE_C1_WGRAD 7      /* Cin == 1 weight gradient: 0 VALU stream kernel (default), 1 padded MFMA tile */
-#define PIS_TUNE_NKEYS 8
+#define PIS_TUNE_WINOGRAD 8      /* 3x3 conv *_ex calls: 0 direct only, 1 Winograd F(2x2,3x3) for >= 256 in/out channels (default), 2 Winograd whenever legal */
+#define PIS_TUNE_NKEYS 9
 #define PIS_DEBUG_NOLOAD (1 << 16)
 int pis_tune(int key, int value);
 
@@ -66,6 +67,13 @@ int pis_tune(int key, int value);
 int pis_conv3x3_fwd(const float* x, int ldx, const float* w_krsc, const float* bias,
                     const float* scale, float* y, int ldy, int B, int H, int W, int Cin,
                     int Cout, int flags, pis_stream_t stream);
+/* Same contraction as pis_conv3x3_fwd / pis_conv3x3_dgrad, with a workspace that admits the
+ * Winograd F(2x2,3x3) path for channel-heavy layers (2.25x fewer MFMA FLOPs: weight, input and
+ * output transforms around 16 batched GEMMs). ws may be NULL (direct path). */
+size_t pis_conv3x3_ex_ws(int B, int H, int W, int Cin, int Cout);
+int pis_conv3x3_fwd_ex(const float* x, int ldx, const float* w_krsc, const float* bias,
+                       const float* scale, float* y, int ldy, int B, int H, int W, int Cin, int Cout,
+                       int flags, void* ws, size_t ws_bytes, pis_stream_t stream);
 /* w_flip[c][r][s][n] = w[n][2-r][2-s][c]  (dgrad operand, rebuilt each step) */
 int pis_conv3x3_flip(const float* w_krsc, float* w_flip, int Cin, int Cout, pis_stream_t stream);
 /* dgrad: dx[p][c] = epi(sum_{r,s,n} dz[p+(r-1,s-1)][n] * w_flip[c][r][s][n])
@@ -73,6 +81,9 @@ int pis_conv3x3_flip(const float* w_krsc, float* w_flip, int Cin, int Cout, pis_
 int pis_conv3x3_dgrad(const float* dz, int ldz, const float* w_flip, const float* mask, int ldm,
                       const float* scale, float* dx, int lddx, int B, int H, int W, int Cin,
                       int Cout, int flags, pis_stream_t stream);
+int pis_conv3x3_dgrad_ex(const float* dz, int ldz, const float* w_flip, const float* mask, int ldm,
+                         const float* scale, float* dx, int lddx, int B, int H, int W, int Cin,
+                         int Cout, int flags, void* ws, size_t ws_bytes, pis_stream_t stream);
 /* wgrad: dw[n][r][s][c] (+)= sum_p dz[p][n] x[p+(r-1,s-1)][c];  db[n] (+)= sum_p dz[p][n]
  *        (db may be NULL). flags: PIS_ACCUMULATE. */
 size_t pis_conv3x3_wgrad_ws(int B, int H, int W, int Cin, int Cout);

@@ -1,0 +1,46 @@
+// Implicit-GEMM argument block shared by the direct (igemm.hip) and Winograd
+// (winograd.hip) 3x3-conv paths.
+#pragma once
+#include "common.h"
+
+namespace pis {
+
+enum TapMode { TAP_CONV3 = 0, TAP_UP2 = 1, TAP_ONE = 2 };
+enum EpiMode { EPI_NHWC = 0, EPI_SCATTER2 = 1 };
+
+struct IGemmArgs {
+  const float* src;  // NHWC source
+  int lds;           // channel stride of src
+  int Hs, Ws;        // source spatial dims
+  int H, W;          // output pixel grid
+  int M;             // B*H*W
+  int Csrc;          // channels read per tap
+  int ntaps;
+  int tap_mode;
+  const float* wt;   // Bt[N][ntaps*Csrc]
+  int ldw;
+  int N;
+  // epilogue
+  int epi;
+  const float* bias;
+  const float* scale;  // [B][N]
+  const float* mask;   // [M][ldm]
+  int ldm;
+  float* dst;
+  int ldd;
+  int flags;
+  int cout_t;          // EPI_SCATTER2: n = (i*2+j)*cout_t + o
+  // batched launches (gridDim.y > 1): per-batch element offsets
+  int64_t bs_src, bs_wt, bs_dst;
+};
+
+// generic implicit GEMM (all tap modes); `batches` independent problems via gridDim.y
+int launch_igemm(const IGemmArgs& a, hipStream_t s, int batches = 1);
+// 3x3 conv (fwd or dgrad-on-flipped-weights): halo kernel when the grid allows, else igemm
+int launch_conv3x3(const IGemmArgs& a, hipStream_t s);
+// Winograd F(2x2,3x3) path of the same conv (winograd.hip); B = images in a.src
+bool wino_ok(const IGemmArgs& a);
+size_t wino_ws_bytes(int B, int H, int W, int C, int N);
+int launch_wino3x3(const IGemmArgs& a, int B, void* ws, hipStream_t s);
+
+}  // namespace pis

@@ -12,36 +12,9 @@
 // 16-byte rows: lane (i, h) of a wave supplies A[i][k] for k = 8g + 4h + t,
 // t = 0..3, i.e. one ds_read_b128 feeds four MFMAs (the k-permutation is
 // applied identically to A and Bt, so the sum is unchanged).
-#include "common.h"
+#include "igemm.h"
 
 namespace pis {
-
-enum TapMode { TAP_CONV3 = 0, TAP_UP2 = 1, TAP_ONE = 2 };
-enum EpiMode { EPI_NHWC = 0, EPI_SCATTER2 = 1 };
-
-struct IGemmArgs {
-  const float* src;  // NHWC source
-  int lds;           // channel stride of src
-  int Hs, Ws;        // source spatial dims
-  int H, W;          // output pixel grid
-  int M;             // B*H*W
-  int Csrc;          // channels read per tap
-  int ntaps;
-  int tap_mode;
-  const float* wt;   // Bt[N][ntaps*Csrc]
-  int ldw;
-  int N;
-  // epilogue
-  int epi;
-  const float* bias;
-  const float* scale;  // [B][N]
-  const float* mask;   // [M][ldm]
-  int ldm;
-  float* dst;
-  int ldd;
-  int flags;
-  int cout_t;          // EPI_SCATTER2: n = (i*2+j)*cout_t + o
-};
 
 __device__ __forceinline__ void tap_offset(int mode, int t, int& dr, int& ds, int& st) {
   if (mode == TAP_CONV3) { dr = t / 3 - 1; ds = t % 3 - 1; st = 1; }
@@ -53,6 +26,11 @@ __device__ __forceinline__ void tap_offset(int mode, int t, int& dr, int& ds, in
 // (needs H % 8 == 0, W % 16 == 0), so pixel coordinates are shifts, not divisions.
 template <int BM, int BN, int BK, bool T2D>
 __global__ __launch_bounds__(256) void igemm_f32_kernel(IGemmArgs g) {
+  if (blockIdx.y) {  // batched launch (Winograd's 16 independent GEMMs): per-batch base offsets
+    g.src += blockIdx.y * g.bs_src;
+    g.wt += blockIdx.y * g.bs_wt;
+    g.dst += blockIdx.y * g.bs_dst;
+  }
   // row pitch BK+4 floats (80 or 144 bytes): 16 rows land on 16 distinct 16-B slots -> conflict-free ds_read_b128
   constexpr int LDS_ROW = BK + 4;
   constexpr int CPR = BK / 4;                           // float4 chunks per staged row
@@ -394,9 +372,7 @@ static bool halo_ok(const IGemmArgs& a) {
 }
 
 
-static int launch_conv3x3(const IGemmArgs& a, hipStream_t s);
-
-static int launch_igemm(const IGemmArgs& a, hipStream_t s) {
+int launch_igemm(const IGemmArgs& a, hipStream_t s, int batches) {
   // tile choice: BN=64 for narrow outputs, BM=128; K-step from the tuning table
   const int ntm = (int)cdiv(a.M, 128);
   const int bk = tune_get(PIS_TUNE_IGEMM_BK);
@@ -406,24 +382,24 @@ static int launch_igemm(const IGemmArgs& a, hipStream_t s) {
   if (a.N <= 64) {
     const int grid = ntm * (int)cdiv(a.N, 64);
     if (bk == 32)
-      hipLaunchKernelGGL((igemm_f32_kernel<128, 64, 32, false>), dim3(grid), dim3(256), 0, s, a);
+      hipLaunchKernelGGL((igemm_f32_kernel<128, 64, 32, false>), dim3(grid, batches), dim3(256), 0, s, a);
     else if (t2d)
-      hipLaunchKernelGGL((igemm_f32_kernel<128, 64, 16, true>), dim3(grid), dim3(256), 0, s, a);
+      hipLaunchKernelGGL((igemm_f32_kernel<128, 64, 16, true>), dim3(grid, batches), dim3(256), 0, s, a);
     else
-      hipLaunchKernelGGL((igemm_f32_kernel<128, 64, 16, false>), dim3(grid), dim3(256), 0, s, a);
+      hipLaunchKernelGGL((igemm_f32_kernel<128, 64, 16, false>), dim3(grid, batches), dim3(256), 0, s, a);
   } else {
     const int grid = ntm * (int)cdiv(a.N, 128);
     if (bk == 32)
-      hipLaunchKernelGGL((igemm_f32_kernel<128, 128, 32, false>), dim3(grid), dim3(256), 0, s, a);
+      hipLaunchKernelGGL((igemm_f32_kernel<128, 128, 32, false>), dim3(grid, batches), dim3(256), 0, s, a);
     else if (t2d)
-      hipLaunchKernelGGL((igemm_f32_kernel<128, 128, 16, true>), dim3(grid), dim3(256), 0, s, a);
+      hipLaunchKernelGGL((igemm_f32_kernel<128, 128, 16, true>), dim3(grid, batches), dim3(256), 0, s, a);
     else
-      hipLaunchKernelGGL((igemm_f32_kernel<128, 128, 16, false>), dim3(grid), dim3(256), 0, s, a);
+      hipLaunchKernelGGL((igemm_f32_kernel<128, 128, 16, false>), dim3(grid, batches), dim3(256), 0, s, a);
   }
   return launch_status("igemm_f32");
 }
 
-static int launch_conv3x3(const IGemmArgs& a, hipStream_t s) {
+int launch_conv3x3(const IGemmArgs& a, hipStream_t s) {
   if (!halo_ok(a) || !tune_get(PIS_TUNE_CONV_HALO)) return launch_igemm(a, s);
   if (tune_get(PIS_TUNE_DEBUG_NOLOAD)) const_cast<IGemmArgs&>(a).flags |= PIS_DEBUG_NOLOAD;
   const int tiles = (a.M / (8 * 16));
@@ -522,9 +498,36 @@ __global__ void convt_prep_kernel(const float* __restrict__ w, float* __restrict
 
 using namespace pis;
 
+// Winograd F(2x2,3x3) policy (winograd.hip): channel-heavy convs, where its GEMMs stay MFMA-bound
+static bool wino_wanted_dims(int H, int W, int C, int N) {
+  const int mode = tune_get(PIS_TUNE_WINOGRAD);
+  if (mode == 0 || H % 2 || W % 2 || C % 4 || N % 4) return false;
+  return mode == 2 || (C >= 256 && N >= 256);
+}
+
+static int dispatch_conv3x3(const IGemmArgs& a, int B, void* ws, size_t ws_bytes, hipStream_t s) {
+  if (ws && wino_ok(a) && wino_wanted_dims(a.H, a.W, a.Csrc, a.N) &&
+      ws_bytes >= wino_ws_bytes(B, a.H, a.W, a.Csrc, a.N))
+    return launch_wino3x3(a, B, ws, s);
+  return launch_conv3x3(a, s);
+}
+
+extern "C" size_t pis_conv3x3_ex_ws(int B, int H, int W, int Cin, int Cout) {
+  size_t need = 0;
+  if (wino_wanted_dims(H, W, Cin, Cout)) need = std::max(need, wino_ws_bytes(B, H, W, Cin, Cout));  // fwd
+  if (wino_wanted_dims(H, W, Cout, Cin)) need = std::max(need, wino_ws_bytes(B, H, W, Cout, Cin));  // dgrad
+  return need;
+}
+
 extern "C" int pis_conv3x3_fwd(const float* x, int ldx, const float* w_krsc, const float* bias,
                                const float* scale, float* y, int ldy, int B, int H, int W, int Cin,
                                int Cout, int flags, pis_stream_t stream) {
+  return pis_conv3x3_fwd_ex(x, ldx, w_krsc, bias, scale, y, ldy, B, H, W, Cin, Cout, flags, nullptr, 0, stream);
+}
+
+extern "C" int pis_conv3x3_fwd_ex(const float* x, int ldx, const float* w_krsc, const float* bias,
+                                  const float* scale, float* y, int ldy, int B, int H, int W, int Cin,
+                                  int Cout, int flags, void* ws, size_t ws_bytes, pis_stream_t stream) {
   PIS_CHECK_ARG(x && w_krsc && y && B > 0 && H > 0 && W > 0 && Cin > 0 && Cout > 0,
                 "pis_conv3x3_fwd: bad arguments");
   PIS_CHECK_ARG(!(flags & PIS_SCALE) || scale, "pis_conv3x3_fwd: PIS_SCALE without scale");
@@ -544,7 +547,7 @@ extern "C" int pis_conv3x3_fwd(const float* x, int ldx, const float* w_krsc, con
   a.Csrc = Cin; a.ntaps = 9; a.tap_mode = TAP_CONV3; a.wt = w_krsc; a.ldw = 9 * Cin; a.N = Cout;
   a.epi = EPI_NHWC; a.bias = bias; a.scale = scale; a.dst = y; a.ldd = ldy;
   a.flags = flags & (PIS_RELU | PIS_SCALE | PIS_ACCUMULATE);
-  return launch_conv3x3(a, s);
+  return dispatch_conv3x3(a, B, ws, ws_bytes, s);
 }
 
 extern "C" int pis_conv3x3_flip(const float* w_krsc, float* w_flip, int Cin, int Cout,
@@ -560,6 +563,14 @@ extern "C" int pis_conv3x3_flip(const float* w_krsc, float* w_flip, int Cin, int
 extern "C" int pis_conv3x3_dgrad(const float* dz, int ldz, const float* w_flip, const float* mask,
                                  int ldm, const float* scale, float* dx, int lddx, int B, int H,
                                  int W, int Cin, int Cout, int flags, pis_stream_t stream) {
+  return pis_conv3x3_dgrad_ex(dz, ldz, w_flip, mask, ldm, scale, dx, lddx, B, H, W, Cin, Cout, flags, nullptr, 0,
+                              stream);
+}
+
+extern "C" int pis_conv3x3_dgrad_ex(const float* dz, int ldz, const float* w_flip, const float* mask,
+                                    int ldm, const float* scale, float* dx, int lddx, int B, int H,
+                                    int W, int Cin, int Cout, int flags, void* ws, size_t ws_bytes,
+                                    pis_stream_t stream) {
   PIS_CHECK_ARG(dz && w_flip && dx && B > 0 && H > 0 && W > 0 && Cin > 0 && Cout > 0,
                 "pis_conv3x3_dgrad: bad arguments");
   PIS_CHECK_ARG(Cout % 4 == 0 && ldz % 4 == 0, "pis_conv3x3_dgrad: Cout/ldz must be multiples of 4");
@@ -570,7 +581,7 @@ extern "C" int pis_conv3x3_dgrad(const float* dz, int ldz, const float* w_flip, 
   a.Csrc = Cout; a.ntaps = 9; a.tap_mode = TAP_CONV3; a.wt = w_flip; a.ldw = 9 * Cout; a.N = Cin;
   a.epi = EPI_NHWC; a.mask = mask; a.ldm = ldm; a.scale = scale; a.dst = dx; a.ldd = lddx;
   a.flags = flags & (PIS_MASK | PIS_SCALE | PIS_ACCUMULATE);
-  return launch_conv3x3(a, (hipStream_t)stream);
+  return dispatch_conv3x3(a, B, ws, ws_bytes, (hipStream_t)stream);
 }
 
 extern "C" int pis_convt2x2_fwd(const float* x, int ldx, const float* w_ijoc, const float* bias,

@@ -1,0 +1,171 @@
+// Winograd F(2x2, 3x3) for the deep 3x3 convs (fwd, and dgrad on flipped weights).
+//
+// A 2x2 output tile needs 16 multiply-adds per (input, output) channel pair
+// instead of 36: with U = G g G^T (weights), V = B^T d B (4x4 input patch) and
+// M_xi = sum_c V_xi[tile][c] U_xi[n][c] for the 16 positions xi, the outputs are
+// Y = A^T M A. The 16 contractions are ordinary fp32 GEMMs (T tiles x N x C)
+// on the MFMA path (batched igemm, 1/2.25 of the direct conv's FLOPs); the
+// transforms are bandwidth-bound streams with only +-1 and 1/2 coefficients:
+//   B^T = [1 0 -1 0; 0 1 1 0; 0 -1 1 0; 0 1 0 -1]
+//   G   = [1 0 0; 1/2 1/2 1/2; 1/2 -1/2 1/2; 0 0 1]
+//   A^T = [1 1 1 0; 0 1 -1 -1]
+// It pays where the channel counts are large enough for the GEMMs to stay
+// MFMA-bound while V and M make one HBM round trip each (levels 3-4 and the
+// bottleneck of the U-Net: tools/bench_kernels.py --key 8).
+//
+// Workspace (floats): U[16][N][C], V[16][T][C], M[16][T][N], T = B*(H/2)*(W/2).
+#include "igemm.h"
+
+namespace pis {
+
+// U[xi][n][c] = (G g G^T)[xi] for g = w[n][tap][c] (KRSC, ldw = 9*C)
+__global__ __launch_bounds__(256) void wino_filter_kernel(const float* __restrict__ w, int ldw, int N, int C,
+                                                          float* __restrict__ U) {
+  const int64_t NC = (int64_t)N * C;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < NC; e += (int64_t)gridDim.x * blockDim.x) {
+    const int n = (int)(e / C), c = (int)(e - (int64_t)n * C);
+    float g[3][3];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) g[t / 3][t % 3] = w[(size_t)n * ldw + t * C + c];
+    float gg[4][3];  // G g
+#pragma unroll
+    for (int s = 0; s < 3; ++s) {
+      gg[0][s] = g[0][s];
+      gg[1][s] = 0.5f * (g[0][s] + g[1][s] + g[2][s]);
+      gg[2][s] = 0.5f * (g[0][s] - g[1][s] + g[2][s]);
+      gg[3][s] = g[2][s];
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float u0 = gg[i][0], u1 = 0.5f * (gg[i][0] + gg[i][1] + gg[i][2]);
+      const float u2 = 0.5f * (gg[i][0] - gg[i][1] + gg[i][2]), u3 = gg[i][2];
+      U[(size_t)(i * 4 + 0) * NC + e] = u0;
+      U[(size_t)(i * 4 + 1) * NC + e] = u1;
+      U[(size_t)(i * 4 + 2) * NC + e] = u2;
+      U[(size_t)(i * 4 + 3) * NC + e] = u3;
+    }
+  }
+}
+
+// V[xi][t][c] = (B^T d B)[xi], d = the 4x4 input patch at rows 2ty-1.., cols 2tx-1.. (zero padded)
+__global__ __launch_bounds__(256) void wino_input_kernel(const float* __restrict__ x, int ldx, int B, int H, int W,
+                                                         int C, float* __restrict__ V) {
+  const int c4n = C / 4, TW = W / 2, TH = H / 2;
+  const int64_t T = (int64_t)B * TH * TW, TC = T * C;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < T * c4n; e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t t = e / c4n;
+    const int c = (int)(e - t * c4n) * 4;
+    const int b = (int)(t / (TH * TW)), rem = (int)(t - (int64_t)b * TH * TW);
+    const int ty = rem / TW, tx = rem - ty * TW;
+    f32x4 d[4][4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int h = 2 * ty - 1 + r;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const int ww = 2 * tx - 1 + s;
+        d[r][s] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (h >= 0 && h < H && ww >= 0 && ww < W)
+          d[r][s] = *reinterpret_cast<const f32x4*>(x + (((size_t)b * H + h) * W + ww) * ldx + c);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      f32x4 tr[4];  // row i of B^T d
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        tr[s] = i == 0 ? d[0][s] - d[2][s] : i == 1 ? d[1][s] + d[2][s] : i == 2 ? d[2][s] - d[1][s] : d[1][s] - d[3][s];
+      }
+      const f32x4 v0 = tr[0] - tr[2], v1 = tr[1] + tr[2], v2 = tr[2] - tr[1], v3 = tr[1] - tr[3];
+      float* out = V + (size_t)(i * 4) * TC + t * C + c;
+      *reinterpret_cast<f32x4*>(out) = v0;
+      *reinterpret_cast<f32x4*>(out + TC) = v1;
+      *reinterpret_cast<f32x4*>(out + 2 * TC) = v2;
+      *reinterpret_cast<f32x4*>(out + 3 * TC) = v3;
+    }
+  }
+}
+
+// Y = A^T M A per tile and 4 output channels, then the conv epilogue of the direct
+// kernels (bias, ReLU, ReLU-backward mask, dropout keep-scale, accumulate).
+__global__ __launch_bounds__(256) void wino_output_kernel(const float* __restrict__ Mt, IGemmArgs g, int B) {
+  const int N = g.N, n4n = N / 4, TW = g.W / 2, TH = g.H / 2;
+  const int64_t T = (int64_t)B * TH * TW, TN = T * N;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < T * n4n; e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t t = e / n4n;
+    const int n = (int)(e - t * n4n) * 4;
+    const int b = (int)(t / (TH * TW)), rem = (int)(t - (int64_t)b * TH * TW);
+    const int ty = rem / TW, tx = rem - ty * TW;
+    f32x4 m[4][4];
+#pragma unroll
+    for (int xi = 0; xi < 16; ++xi) m[xi / 4][xi % 4] = *reinterpret_cast<const f32x4*>(Mt + xi * TN + t * N + n);
+    f32x4 tr[2][4];  // A^T M
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      tr[0][s] = m[0][s] + m[1][s] + m[2][s];
+      tr[1][s] = m[1][s] - m[2][s] - m[3][s];
+    }
+    f32x4 bias4 = {0.f, 0.f, 0.f, 0.f}, sc4 = {1.f, 1.f, 1.f, 1.f};
+    if (g.bias) bias4 = *reinterpret_cast<const f32x4*>(g.bias + n);
+    if (g.flags & PIS_SCALE) sc4 = *reinterpret_cast<const f32x4*>(g.scale + (size_t)b * N + n);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const f32x4 y0 = tr[i][0] + tr[i][1] + tr[i][2];
+      const f32x4 y1 = tr[i][1] - tr[i][2] - tr[i][3];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const size_t pix = ((size_t)b * g.H + 2 * ty + i) * g.W + 2 * tx + j;
+        f32x4 v = (j == 0 ? y0 : y1) + bias4;
+        if (g.flags & PIS_RELU) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) v[k] = fmaxf(v[k], 0.f);
+        }
+        if (g.flags & PIS_MASK) {
+          const f32x4 mk = *reinterpret_cast<const f32x4*>(g.mask + pix * g.ldm + n);
+#pragma unroll
+          for (int k = 0; k < 4; ++k) v[k] = mk[k] > 0.f ? v[k] : 0.f;
+        }
+        v *= sc4;
+        float* dst = g.dst + pix * g.ldd + n;
+        if (g.flags & PIS_ACCUMULATE) v += *reinterpret_cast<const f32x4*>(dst);
+        *reinterpret_cast<f32x4*>(dst) = v;
+      }
+    }
+  }
+}
+
+static int grid_of(int64_t work) { return (int)std::max<int64_t>(1, std::min<int64_t>(cdiv(work, 256), 16384)); }
+
+bool wino_ok(const IGemmArgs& a) {
+  return a.tap_mode == TAP_CONV3 && a.epi == EPI_NHWC && a.H % 2 == 0 && a.W % 2 == 0 && a.Csrc % 4 == 0 &&
+         a.N % 4 == 0 && a.lds % 4 == 0 && a.ldd % 4 == 0 && (!(a.flags & PIS_MASK) || a.ldm % 4 == 0);
+}
+
+size_t wino_ws_bytes(int B, int H, int W, int C, int N) {
+  const int64_t T = (int64_t)B * (H / 2) * (W / 2);
+  return (size_t)16 * ((int64_t)N * C + T * C + T * N) * sizeof(float) + 1024;
+}
+
+// a describes the direct conv (src/lds = input, wt/ldw = KRSC weights, N outputs, epilogue)
+int launch_wino3x3(const IGemmArgs& a, int B, void* ws, hipStream_t s) {
+  const int C = a.Csrc, N = a.N;
+  const int64_t T = (int64_t)B * (a.H / 2) * (a.W / 2);
+  float* U = (float*)ws;
+  float* V = U + (size_t)16 * N * C;
+  float* Mt = V + (size_t)16 * T * C;
+  hipLaunchKernelGGL(wino_filter_kernel, dim3(grid_of((int64_t)N * C)), dim3(256), 0, s, a.wt, a.ldw, N, C, U);
+  hipLaunchKernelGGL(wino_input_kernel, dim3(grid_of(T * (C / 4))), dim3(256), 0, s, a.src, a.lds, B, a.H, a.W, C, V);
+  int rc = launch_status("wino_transforms");
+  if (rc) return rc;
+  IGemmArgs gm{};
+  gm.src = V; gm.lds = C; gm.Hs = 1; gm.Ws = (int)T; gm.H = 1; gm.W = (int)T; gm.M = (int)T;
+  gm.Csrc = C; gm.ntaps = 1; gm.tap_mode = TAP_ONE; gm.wt = U; gm.ldw = C; gm.N = N;
+  gm.epi = EPI_NHWC; gm.dst = Mt; gm.ldd = N; gm.flags = 0;
+  gm.bs_src = T * C; gm.bs_wt = (int64_t)N * C; gm.bs_dst = T * N;
+  rc = launch_igemm(gm, s, 16);
+  if (rc) return rc;
+  hipLaunchKernelGGL(wino_output_kernel, dim3(grid_of(T * (N / 4))), dim3(256), 0, s, Mt, a, B);
+  return launch_status("wino_output");
+}
+
+}  // namespace pis

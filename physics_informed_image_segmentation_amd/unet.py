@@ -352,10 +352,11 @@ class UNetEngine:
             Hl, Wl, Cl = H >> (l - 1), W >> (l - 1), c << (l - 1)
             cin0 = self.m.in_channels if l == 1 else Cl // 2
             ws = max(ws, lib.pis_conv3x3_wgrad_ws(B, Hl, Wl, cin0, Cl), lib.pis_conv3x3_wgrad_ws(B, Hl, Wl, Cl, Cl),
-                     lib.pis_conv3x3_wgrad_ws(B, Hl, Wl, 2 * Cl, Cl))
+                     lib.pis_conv3x3_wgrad_ws(B, Hl, Wl, 2 * Cl, Cl), lib.pis_conv3x3_ex_ws(B, Hl, Wl, cin0, Cl),
+                     lib.pis_conv3x3_ex_ws(B, Hl, Wl, Cl, Cl), lib.pis_conv3x3_ex_ws(B, Hl, Wl, 2 * Cl, Cl))
             cup = 8 * c if l == 4 else 2 * Cl
             ws = max(ws, lib.pis_convt2x2_wgrad_ws(B, Hl // 2, Wl // 2, cup, Cl))
-        ws = max(ws, lib.pis_conv3x3_wgrad_ws(B, H5, W5, 8 * c, 8 * c))
+        ws = max(ws, lib.pis_conv3x3_wgrad_ws(B, H5, W5, 8 * c, 8 * c), lib.pis_conv3x3_ex_ws(B, H5, W5, 8 * c, 8 * c))
         self.ws = torch.empty((ws + 15) // 4, dtype=torch.float32, device=dev)
         self.ws_bytes = self.ws.numel() * 4
 
@@ -392,8 +393,9 @@ class UNetEngine:
 
     def _conv_fwd(self, conv: nn.Conv2d, x: _Buf, y: _Buf, B, H, W, scale):
         flags = PIS_RELU | (PIS_SCALE if scale is not None else 0)
-        call("pis_conv3x3_fwd", x.p, x.ld, conv.weight.data_ptr(), conv.bias.data_ptr(), ptr(scale),
-             y.p, y.ld, B, H, W, conv.in_channels, conv.out_channels, flags, self._stream())
+        call("pis_conv3x3_fwd_ex", x.p, x.ld, conv.weight.data_ptr(), conv.bias.data_ptr(), ptr(scale),
+             y.p, y.ld, B, H, W, conv.in_channels, conv.out_channels, flags, self.ws.data_ptr(), self.ws_bytes,
+             self._stream())
 
     def _grad_slot(self, p: torch.Tensor) -> Tuple[int, int]:
         return self._offsets[id(p)]
@@ -537,9 +539,9 @@ class UNetEngine:
             self._ready(conv.weight, conv.bias)
             if dx is not None:
                 flags = (PIS_MASK if mask is not None else 0) | (PIS_SCALE if scale is not None else 0)
-                call("pis_conv3x3_dgrad", dz.p, dz.ld, flips[id(conv)].data_ptr(),
+                call("pis_conv3x3_dgrad_ex", dz.p, dz.ld, flips[id(conv)].data_ptr(),
                      mask.p if mask is not None else 0, mask.ld if mask is not None else 0, ptr(scale),
-                     dx.p, dx.ld, B, Hl, Wl, conv.in_channels, conv.out_channels, flags, st)
+                     dx.p, dx.ld, B, Hl, Wl, conv.in_channels, conv.out_channels, flags, ws, wsb, st)
 
         # head: sigmoid backward + 1x1 conv + ReLU backward of dec1.conv1
         d1 = _Buf(bf["d1_1"], c)

@@ -118,6 +118,46 @@ def test_conv3x3_tuned_variants(hip, key, value):
         hip.pis_tune(key, prev)
 
 
+@pytest.mark.parametrize("B,H,W,Cin,Cout,mode", [(2, 8, 8, 256, 256, 1), (1, 4, 6, 512, 256, 1),
+                                                 (2, 16, 32, 64, 128, 2), (1, 6, 10, 132, 64, 2),
+                                                 (1, 5, 8, 256, 256, 2), (2, 8, 16, 256, 512, 0)])
+def test_conv3x3_ex_winograd(hip, B, H, W, Cin, Cout, mode):
+    """pis_conv3x3_fwd_ex / dgrad_ex with a workspace: Winograd F(2x2,3x3) where the policy
+    (pis_tune key 8: 1 = auto, 2 = whenever H, W are even) picks it, direct otherwise."""
+    prev = hip.pis_tune(8, mode)
+    try:
+        g = torch.Generator().manual_seed(12)
+        x = F.relu(torch.randn(B, Cin, H, W, generator=g))
+        w = torch.randn(Cout, Cin, 3, 3, generator=g) / (3 * Cin ** 0.5)
+        b = torch.randn(Cout, generator=g)
+        scale = (torch.rand(B, Cout, generator=g) > 0.2).float() / 0.8
+        dz = torch.randn(B, Cout, H, W, generator=g)
+        sc_in = (torch.rand(B, Cin, generator=g) > 0.2).float() / 0.8
+        y_ref = F.relu(F.conv2d(x, w, b, padding=1)) * scale[:, :, None, None]
+        dx_ref = torch.nn.grad.conv2d_input(x.shape, w, dz, padding=1) * (x > 0) * sc_in[:, :, None, None]
+        nws = hip.pis_conv3x3_ex_ws(B, H, W, Cin, Cout)
+        assert (nws > 0) == (mode == 2 and H % 2 == 0 and W % 2 == 0 or mode == 1 and min(Cin, Cout) >= 256)
+        ws = torch.empty(max(nws, 4) // 4 + 1, device="cuda")
+        xd, wd, bd, sd, dzd, sid = (nhwc(x).cuda(), krsc(w).cuda(), b.cuda(), scale.cuda(), nhwc(dz).cuda(),
+                                    sc_in.cuda())
+        y = torch.empty(B, H, W, Cout, device="cuda")
+        rc = hip.pis_conv3x3_fwd_ex(xd.data_ptr(), Cin, wd.data_ptr(), bd.data_ptr(), sd.data_ptr(), y.data_ptr(),
+                                    Cout, B, H, W, Cin, Cout, RELU | SCALE, ws.data_ptr(), nws, s())
+        assert rc == 0, hip.pis_last_error()
+        wf = torch.empty(Cin * 9 * Cout, device="cuda")
+        assert hip.pis_conv3x3_flip(wd.data_ptr(), wf.data_ptr(), Cin, Cout, s()) == 0
+        dx = torch.full((B, H, W, Cin), 0.5, device="cuda")
+        rc = hip.pis_conv3x3_dgrad_ex(dzd.data_ptr(), Cout, wf.data_ptr(), xd.data_ptr(), Cin, sid.data_ptr(),
+                                      dx.data_ptr(), Cin, B, H, W, Cin, Cout, MASK | SCALE | ACC, ws.data_ptr(), nws,
+                                      s())
+        assert rc == 0, hip.pis_last_error()
+        torch.cuda.synchronize()
+        assert rel_err(nchw(y.cpu()), y_ref) < 1e-5
+        assert rel_err(nchw(dx.cpu()) - 0.5, dx_ref) < 1e-5
+    finally:
+        hip.pis_tune(8, prev)
+
+
 def test_conv3x3_c1_wgrad(hip):
     B, H, W, Cout = 2, 32, 16, 64
     g = torch.Generator().manual_seed(2)

@@ -70,13 +70,18 @@ def main():
         ws = torch.empty(nws // 4 + 1, device=dev)
         dw = torch.empty(cout * 9 * cin, device=dev)
         db = torch.empty(cout, device=dev)
+        prev8 = lib.pis_tune(8, 2)  # workspace for the Winograd path whichever policy is timed
+        nwx = lib.pis_conv3x3_ex_ws(B, H, H, cin, cout)
+        lib.pis_tune(8, prev8)
+        wsx = torch.empty(max(nwx, 4) // 4 + 1, device=dev)
         flops = 2.0 * B * H * H * cout * cin * 9
         dflags = 0 if name.startswith("dec") and name.endswith("conv0") else 4  # ReLU mask unless a concat input
         ops = {
-            "fwd": lambda: lib.pis_conv3x3_fwd(x.data_ptr(), cin, w.data_ptr(), bias.data_ptr(), 0, y.data_ptr(), cout,
-                                               B, H, H, cin, cout, 1, s),
-            "dgrad": lambda: lib.pis_conv3x3_dgrad(dz.data_ptr(), cout, wf.data_ptr(), x.data_ptr(), cin, 0,
-                                                   dx.data_ptr(), cin, B, H, H, cin, cout, dflags, s),
+            "fwd": lambda: lib.pis_conv3x3_fwd_ex(x.data_ptr(), cin, w.data_ptr(), bias.data_ptr(), 0, y.data_ptr(),
+                                                  cout, B, H, H, cin, cout, 1, wsx.data_ptr(), nwx, s),
+            "dgrad": lambda: lib.pis_conv3x3_dgrad_ex(dz.data_ptr(), cout, wf.data_ptr(), x.data_ptr(), cin, 0,
+                                                      dx.data_ptr(), cin, B, H, H, cin, cout, dflags, wsx.data_ptr(),
+                                                      nwx, s),
             "wgrad": lambda: lib.pis_conv3x3_wgrad(x.data_ptr(), cin, dz.data_ptr(), cout, dw.data_ptr(),
                                                    db.data_ptr(), B, H, H, cin, cout, 0, ws.data_ptr(), nws, s),
         }
