@@ -42,5 +42,9 @@ int launch_conv3x3(const IGemmArgs& a, hipStream_t s);
 bool wino_ok(const IGemmArgs& a);
 size_t wino_ws_bytes(int B, int H, int W, int C, int N);
 int launch_wino3x3(const IGemmArgs& a, int B, void* ws, hipStream_t s);
+// Winograd weight-gradient pieces: V[16][T][C] of x, E[16][T][N] of dz, dW from M[16][N][C]
+int launch_wino_input(const float* x, int ldx, int B, int H, int W, int C, float* V, hipStream_t s);
+int launch_wino_dz(const float* dz, int ldz, int B, int H, int W, int N, float* E, hipStream_t s);
+int launch_wino_wgrad_out(const float* M, int N, int C, float* dw, int accumulate, hipStream_t s);
 
 }  // namespace pis

@@ -17,7 +17,7 @@
 //           Cin == 1:  n' = tap (9 of 64 columns used)
 // convT2x2: m' = (i, j, o),       A(p, ijo)   = dy[(2h+i, 2w+j)][o]
 //           n' = c,               B(p, c)     = x[p][c]
-#include "common.h"
+#include "igemm.h"
 
 namespace pis {
 
@@ -32,11 +32,18 @@ struct WgradArgs {
   int pix_per_split;
   float* part;                                   // [splits][Mp][Np]
   float* part_bias;                              // [splits][Mp] or NULL
+  // batched launches (gridDim.y > 1, Winograd's 16 GEMMs): per-batch offsets; slab pitch
+  int64_t bs_a, bs_b, bs_part, split_stride;     // split_stride 0 = Mp * Np
 };
 
 // BKP pixels per stage: 32 MFMAs per wave between barriers for every tile shape
 template <int BM, int BN, int BKP>
 __global__ __launch_bounds__(256) void wgrad_f32_kernel(WgradArgs g) {
+  if (blockIdx.y) {
+    g.a += blockIdx.y * g.bs_a;
+    g.b += blockIdx.y * g.bs_b;
+    g.part += blockIdx.y * g.bs_part;
+  }
   constexpr int TM = BM / 64, TN = BN / 64;   // 32x32 tiles per wave
   constexpr int AL = BKP * BM / 4 / 256, BL = BKP * BN / 4 / 256;
   __shared__ __attribute__((aligned(16))) float sA[2][BKP * BM];
@@ -158,7 +165,7 @@ __global__ __launch_bounds__(256) void wgrad_f32_kernel(WgradArgs g) {
     __syncthreads();
   }
 
-  float* out = g.part + (size_t)split * g.Mp * g.Np;
+  float* out = g.part + (size_t)split * (g.split_stride ? g.split_stride : (int64_t)g.Mp * g.Np);
 #pragma unroll
   for (int a = 0; a < TM; ++a)
 #pragma unroll
@@ -454,7 +461,7 @@ struct WgradPlan {
   size_t part_bytes, bias_bytes;
 };
 
-static WgradPlan plan_wgrad(int Mp, int Np, int P, int group_m, int group_n) {
+static WgradPlan plan_wgrad(int Mp, int Np, int P, int group_m, int group_n, int target_blocks = 2048) {
   // tile sizes must divide the per-tap group so tiles never straddle a tap
   WgradPlan p{};
   p.bm = (Mp % 128 == 0 && group_m % 128 == 0) ? 128 : 64;
@@ -463,7 +470,7 @@ static WgradPlan plan_wgrad(int Mp, int Np, int P, int group_m, int group_n) {
   // >= ~2 blocks per CU, fp32 chains of at most 8192 pixels, at least 64 pixels per split
   // >= ~8 blocks per CU so the tail wave is short; partial-slab traffic stays
   // ~2 bytes per 1000 FLOP at >= 512 pixels per split
-  const int64_t want_splits = std::max<int64_t>(1, cdiv(2048, tiles));
+  const int64_t want_splits = std::max<int64_t>(1, cdiv(target_blocks, tiles));
   int64_t pps = std::max<int64_t>(512, cdiv(P, want_splits));
   pps = std::min<int64_t>(pps, 8192);
   pps = cdiv(pps, 64) * 64;
@@ -481,11 +488,11 @@ static float* bias_slabs(void* ws, const WgradPlan& pl) {
 
 static size_t wgrad_ws_bytes(const WgradPlan& pl) { return cdiv(pl.part_bytes, 256) * 256 + pl.bias_bytes + 256; }
 
-static int run_wgrad(const WgradArgs& base, const WgradPlan& pl, hipStream_t s) {
+static int run_wgrad(const WgradArgs& base, const WgradPlan& pl, hipStream_t s, int batches = 1) {
   WgradArgs a = base;
   a.pix_per_split = pl.pps;
   const int tiles = (a.Mp / pl.bm) * (a.Np / pl.bn);
-  const dim3 grid(tiles * pl.splits);
+  const dim3 grid(tiles * pl.splits, batches);
   if (pl.bm == 128 && pl.bn == 128)
     hipLaunchKernelGGL((wgrad_f32_kernel<128, 128, 16>), grid, dim3(256), 0, s, a);
   else if (pl.bm == 128)
@@ -588,7 +595,66 @@ __global__ __launch_bounds__(256) void wgrad_c1_kernel(const float* __restrict__
   }
 }
 
+// Winograd F(3x3, 2x2) weight gradient (csrc/winograd.hip): V = B^T x B and E = A dz A^T per
+// 2x2 tile, M_xi[n][c] = sum_tiles E_xi[t][n] V_xi[t][c] as 16 batched split-K GEMMs over the
+// T tiles (slabs [split][xi][Cout][Cin], one fixed-order reduction), dW = G^T M G; the bias
+// gradient is a channel sum of dz.
+struct WinoWgradPlan {
+  bool use;
+  int64_t T;
+  WgradPlan gemm;
+  size_t off_E, off_part, off_M, off_cs, total;
+};
+
+static WinoWgradPlan wino_wgrad_plan(int B, int H, int W, int Cin, int Cout) {
+  WinoWgradPlan p{};
+  const int mode = tune_get(PIS_TUNE_WINOGRAD);
+  // auto: channel-heavy layers on >= 64x64 grids (the 32x32 bottleneck's 2048-tile GEMMs lose)
+  p.use = mode != 0 && H % 2 == 0 && W % 2 == 0 && Cin % 64 == 0 && Cout % 64 == 0 &&
+          (mode == 2 || (Cin >= 256 && Cout >= 256 && H * W >= 64 * 64));
+  if (!p.use) return p;
+  p.T = (int64_t)B * (H / 2) * (W / 2);
+  // the 16 GEMMs share one launch: split so all of them together make ~target blocks
+  p.gemm = plan_wgrad(Cout, Cin, (int)p.T, Cout, Cin, std::max(16, tune_get(PIS_TUNE_WINO_WGRAD_BLOCKS) / 16));
+  auto al = [](size_t b) { return cdiv(b, 256) * 256; };
+  const size_t V = al((size_t)16 * p.T * Cin * 4), E = al((size_t)16 * p.T * Cout * 4);
+  const size_t part = al((size_t)p.gemm.splits * 16 * Cout * Cin * 4), M = al((size_t)16 * Cout * Cin * 4);
+  p.off_E = V;
+  p.off_part = V + E;
+  p.off_M = p.off_part + part;
+  p.off_cs = p.off_M + M;
+  p.total = p.off_cs + colsum_ws((int64_t)B * H * W, Cout) + 256;
+  return p;
+}
+
+static int wino_wgrad(const float* x, int ldx, const float* dz, int ldz, float* dw, float* db, int B, int H, int W,
+                      int Cin, int Cout, int acc, const WinoWgradPlan& p, void* ws, hipStream_t s) {
+  char* base = (char*)ws;
+  float* V = (float*)base;
+  float* E = (float*)(base + p.off_E);
+  float* part = (float*)(base + p.off_part);
+  float* M = (float*)(base + p.off_M);
+  int rc = launch_wino_input(x, ldx, B, H, W, Cin, V, s);
+  if (!rc) rc = launch_wino_dz(dz, ldz, B, H, W, Cout, E, s);
+  if (rc) return rc;
+  WgradArgs a{};
+  a.a = E; a.lda = Cout; a.a_up2 = 0; a.Ca = Cout;
+  a.b = V; a.ldb = Cin; a.b_mode = B_PLAIN; a.Cb = Cin;
+  a.B = 1; a.H = 1; a.W = (int)p.T; a.P = (int)p.T; a.Mp = Cout; a.Np = Cin;
+  a.part = part; a.part_bias = nullptr;
+  a.bs_a = p.T * Cout; a.bs_b = p.T * Cin; a.bs_part = (int64_t)Cout * Cin;
+  a.split_stride = (int64_t)16 * Cout * Cin;
+  rc = run_wgrad(a, p.gemm, s, 16);
+  if (!rc) rc = reduce_slabs_pitched(part, p.gemm.splits, a.split_stride, a.split_stride, M, 0, s);
+  if (!rc) rc = launch_wino_wgrad_out(M, Cout, Cin, dw, acc, s);
+  if (!rc && db)
+    rc = colsum(dz, ldz, (int64_t)B * H * W, Cout, db, acc, base + p.off_cs, p.total - p.off_cs, s);
+  return rc;
+}
+
 extern "C" size_t pis_conv3x3_wgrad_ws(int B, int H, int W, int Cin, int Cout) {
+  const WinoWgradPlan wp = wino_wgrad_plan(B, H, W, Cin, Cout);
+  if (wp.use) return wp.total;
   const HaloPlan hp = halo_plan(B, H, W, Cin, Cout);
   if (hp.use) return cdiv(hp.part_bytes, 256) * 256 + hp.bias_bytes + 256;
   if (Cin == 1 && tune_get(PIS_TUNE_C1_WGRAD) == 0)
@@ -620,6 +686,9 @@ extern "C" int pis_conv3x3_wgrad(const float* x, int ldx, const float* dz, int l
   PIS_CHECK_ARG((Cin == 1 || ldx % 4 == 0) && ldz % 4 == 0, "pis_conv3x3_wgrad: ld must be multiples of 4");
   hipStream_t s = (hipStream_t)stream;
   const int acc = flags & PIS_ACCUMULATE;
+  const WinoWgradPlan wp = wino_wgrad_plan(B, H, W, Cin, Cout);
+  if (wp.use && ldx % 4 == 0 && ws_bytes >= wp.total)
+    return wino_wgrad(x, ldx, dz, ldz, dw_krsc, db, B, H, W, Cin, Cout, acc, wp, ws, s);
   const HaloPlan hp = halo_plan(B, H, W, Cin, Cout);
   if (hp.use && ldx % 4 == 0) {
     W3Args a{};

@@ -134,6 +134,78 @@ __global__ __launch_bounds__(256) void wino_output_kernel(const float* __restric
   }
 }
 
+// ---- weight gradient: the dual algorithm F(3x3, 2x2) -------------------------------
+// dW[r][s] = sum_tiles G^T (E (.) V) G per (n, c), with V = B^T d B (the forward's input
+// transform) and E = A e A^T from the 2x2 output-gradient tile e; the 16 contractions over
+// tiles run on the split-K MFMA weight-gradient GEMM (wgrad.hip).
+//   A = [1 0; 1 1; 1 -1; 0 -1],  G^T = [1 1/2 1/2 0; 0 1/2 -1/2 0; 0 1/2 1/2 1]
+
+// E[xi][t][n] = (A e A^T)[xi], e = dz at output pixels (2ty + i, 2tx + j)
+__global__ __launch_bounds__(256) void wino_dz_kernel(const float* __restrict__ dz, int ldz, int B, int H, int W,
+                                                      int N, float* __restrict__ E) {
+  const int n4n = N / 4, TW = W / 2, TH = H / 2;
+  const int64_t T = (int64_t)B * TH * TW, TN = T * N;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < T * n4n; e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t t = e / n4n;
+    const int n = (int)(e - t * n4n) * 4;
+    const int b = (int)(t / (TH * TW)), rem = (int)(t - (int64_t)b * TH * TW);
+    const int ty = rem / TW, tx = rem - ty * TW;
+    f32x4 g[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        g[i][j] = *reinterpret_cast<const f32x4*>(dz + (((size_t)b * H + 2 * ty + i) * W + 2 * tx + j) * ldz + n);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      f32x4 tr[2];  // row k of A e
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        tr[j] = k == 0 ? g[0][j] : k == 1 ? g[0][j] + g[1][j] : k == 2 ? g[0][j] - g[1][j] : -g[1][j];
+      float* out = E + (size_t)(k * 4) * TN + t * N + n;
+      *reinterpret_cast<f32x4*>(out) = tr[0];
+      *reinterpret_cast<f32x4*>(out + TN) = tr[0] + tr[1];
+      *reinterpret_cast<f32x4*>(out + 2 * TN) = tr[0] - tr[1];
+      *reinterpret_cast<f32x4*>(out + 3 * TN) = -tr[1];
+    }
+  }
+}
+
+// dw[n][r][s][c] (+)= (G^T M G)[r][s], M[xi][n][c] the reduced tile sums
+__global__ __launch_bounds__(256) void wino_wgrad_out_kernel(const float* __restrict__ M, int N, int C,
+                                                             float* __restrict__ dw, int accumulate) {
+  const int64_t NC = (int64_t)N * C;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < NC; e += (int64_t)gridDim.x * blockDim.x) {
+    const int n = (int)(e / C), c = (int)(e - (int64_t)n * C);
+    float m[4][4];
+#pragma unroll
+    for (int xi = 0; xi < 16; ++xi) m[xi / 4][xi % 4] = M[xi * NC + e];
+    float tr[3][4];  // G^T M
+#pragma unroll
+    for (int l = 0; l < 4; ++l) {
+      tr[0][l] = m[0][l] + 0.5f * (m[1][l] + m[2][l]);
+      tr[1][l] = 0.5f * (m[1][l] - m[2][l]);
+      tr[2][l] = 0.5f * (m[1][l] + m[2][l]) + m[3][l];
+    }
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      const float w0 = tr[r][0] + 0.5f * (tr[r][1] + tr[r][2]);
+      const float w1 = 0.5f * (tr[r][1] - tr[r][2]);
+      const float w2 = 0.5f * (tr[r][1] + tr[r][2]) + tr[r][3];
+      float* o = dw + ((size_t)n * 9 + r * 3) * C + c;
+      if (accumulate) {
+        o[0] += w0;
+        o[C] += w1;
+        o[2 * C] += w2;
+      } else {
+        o[0] = w0;
+        o[C] = w1;
+        o[2 * C] = w2;
+      }
+    }
+  }
+}
+
 static int grid_of(int64_t work) { return (int)std::max<int64_t>(1, std::min<int64_t>(cdiv(work, 256), 16384)); }
 
 bool wino_ok(const IGemmArgs& a) {
@@ -166,6 +238,23 @@ int launch_wino3x3(const IGemmArgs& a, int B, void* ws, hipStream_t s) {
   if (rc) return rc;
   hipLaunchKernelGGL(wino_output_kernel, dim3(grid_of(T * (N / 4))), dim3(256), 0, s, Mt, a, B);
   return launch_status("wino_output");
+}
+
+int launch_wino_input(const float* x, int ldx, int B, int H, int W, int C, float* V, hipStream_t s) {
+  const int64_t T = (int64_t)B * (H / 2) * (W / 2);
+  hipLaunchKernelGGL(wino_input_kernel, dim3(grid_of(T * (C / 4))), dim3(256), 0, s, x, ldx, B, H, W, C, V);
+  return launch_status("wino_input");
+}
+
+int launch_wino_dz(const float* dz, int ldz, int B, int H, int W, int N, float* E, hipStream_t s) {
+  const int64_t T = (int64_t)B * (H / 2) * (W / 2);
+  hipLaunchKernelGGL(wino_dz_kernel, dim3(grid_of(T * (N / 4))), dim3(256), 0, s, dz, ldz, B, H, W, N, E);
+  return launch_status("wino_dz");
+}
+
+int launch_wino_wgrad_out(const float* M, int N, int C, float* dw, int accumulate, hipStream_t s) {
+  hipLaunchKernelGGL(wino_wgrad_out_kernel, dim3(grid_of((int64_t)N * C)), dim3(256), 0, s, M, N, C, dw, accumulate);
+  return launch_status("wino_wgrad_out");
 }
 
 }  // namespace pis

@@ -120,10 +120,11 @@ def test_conv3x3_tuned_variants(hip, key, value):
 
 @pytest.mark.parametrize("B,H,W,Cin,Cout,mode", [(2, 8, 8, 256, 256, 1), (1, 4, 6, 512, 256, 1),
                                                  (2, 16, 32, 64, 128, 2), (1, 6, 10, 132, 64, 2),
-                                                 (1, 5, 8, 256, 256, 2), (2, 8, 16, 256, 512, 0)])
+                                                 (1, 5, 8, 256, 256, 2), (2, 8, 16, 256, 512, 0),
+                                                 (3, 10, 6, 128, 64, 2)])
 def test_conv3x3_ex_winograd(hip, B, H, W, Cin, Cout, mode):
-    """pis_conv3x3_fwd_ex / dgrad_ex with a workspace: Winograd F(2x2,3x3) where the policy
-    (pis_tune key 8: 1 = auto, 2 = whenever H, W are even) picks it, direct otherwise."""
+    """pis_conv3x3_fwd_ex / dgrad_ex with a workspace, and pis_conv3x3_wgrad: Winograd where the
+    policy (pis_tune key 8: 1 = auto, 2 = whenever H, W are even) picks it, direct otherwise."""
     prev = hip.pis_tune(8, mode)
     try:
         g = torch.Generator().manual_seed(12)
@@ -154,6 +155,20 @@ def test_conv3x3_ex_winograd(hip, B, H, W, Cin, Cout, mode):
         torch.cuda.synchronize()
         assert rel_err(nchw(y.cpu()), y_ref) < 1e-5
         assert rel_err(nchw(dx.cpu()) - 0.5, dx_ref) < 1e-5
+        if Cin % 64 or Cout % 64:
+            return  # the weight-gradient API takes multiples of 64 channels
+        # weight gradient (Winograd F(3x3,2x2) under the same policy)
+        dw_ref = torch.nn.grad.conv2d_weight(x, w.shape, dz, padding=1)
+        nwg = hip.pis_conv3x3_wgrad_ws(B, H, W, Cin, Cout)
+        wsg = torch.empty(nwg // 4 + 1, device="cuda")
+        dw = torch.full((Cout, 3, 3, Cin), 0.25, device="cuda")
+        db = torch.full((Cout,), 0.25, device="cuda")
+        rc = hip.pis_conv3x3_wgrad(xd.data_ptr(), Cin, dzd.data_ptr(), Cout, dw.data_ptr(), db.data_ptr(), B, H, W,
+                                   Cin, Cout, ACC, wsg.data_ptr(), nwg, s())
+        assert rc == 0, hip.pis_last_error()
+        torch.cuda.synchronize()
+        assert rel_err(dw.cpu().permute(0, 3, 1, 2) - 0.25, dw_ref) < 1e-5
+        assert rel_err(db.cpu() - 0.25, dz.sum(dim=(0, 2, 3))) < 1e-5
     finally:
         hip.pis_tune(8, prev)
 

@@ -66,7 +66,11 @@ def main():
         lib.pis_conv3x3_flip(w.data_ptr(), wf.data_ptr(), cin, cout, s)
         y = torch.empty(B, H, H, cout, device=dev)
         dx = torch.empty(B, H, H, cin, device=dev)
-        nws = lib.pis_conv3x3_wgrad_ws(B, H, H, cin, cout)
+        nws = 0
+        for v in variants:  # the weight-gradient workspace depends on the knob being timed
+            pv = lib.pis_tune(args.key, v)
+            nws = max(nws, lib.pis_conv3x3_wgrad_ws(B, H, H, cin, cout))
+            lib.pis_tune(args.key, pv)
         ws = torch.empty(nws // 4 + 1, device=dev)
         dw = torch.empty(cout * 9 * cin, device=dev)
         db = torch.empty(cout, device=dev)
