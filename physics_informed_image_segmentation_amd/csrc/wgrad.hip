@@ -393,8 +393,17 @@ __global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ s
   const int64_t p0 = (int64_t)blockIdx.x * pix_per_split;
   const int64_t p1 = min(npix, p0 + pix_per_split);
   f32x4 s = {0.f, 0.f, 0.f, 0.f};
-  if (r < rows)
-    for (int64_t p = p0 + r; p < p1; p += rows) s += *reinterpret_cast<const f32x4*>(src + p * ld + 4 * c4);
+  if (r < rows) {
+    // 4 independent partial sums keep 4 loads in flight per thread (fixed combine order)
+    f32x4 s4[4] = {s, s, s, s};
+    int64_t p = p0 + r;
+    for (; p + 3 * rows < p1; p += 4 * rows) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) s4[u] += *reinterpret_cast<const f32x4*>(src + (p + u * rows) * ld + 4 * c4);
+    }
+    for (int u = 0; p < p1; p += rows, ++u) s4[u & 3] += *reinterpret_cast<const f32x4*>(src + p * ld + 4 * c4);
+    s = (s4[0] + s4[1]) + (s4[2] + s4[3]);
+  }
   __shared__ f32x4 red[256];
   red[tid] = s;
   __syncthreads();
@@ -424,7 +433,8 @@ __global__ __launch_bounds__(256) void colsum1_kernel(const float* __restrict__ 
 }
 
 static void colsum_plan(int64_t npix, int C, int& splits, int64_t& pps) {
-  pps = std::max<int64_t>(2048, cdiv(npix, 512));
+  // ~1024 blocks (4 per CU) whatever the size: the pass is one read of the source
+  pps = std::max<int64_t>(64, cdiv(npix, 1024));
   splits = (int)cdiv(npix, pps);
 }
 
