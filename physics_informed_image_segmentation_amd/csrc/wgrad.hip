@@ -619,9 +619,10 @@ struct WinoWgradPlan {
 static WinoWgradPlan wino_wgrad_plan(int B, int H, int W, int Cin, int Cout) {
   WinoWgradPlan p{};
   const int mode = tune_get(PIS_TUNE_WINOGRAD);
-  // auto: channel-heavy layers on >= 64x64 grids (the 32x32 bottleneck's 2048-tile GEMMs lose)
+  // auto: >= 128 input and output channels (measured: 4-36 % faster from level 2 down,
+  // slower on the 64-channel level; tools/bench_kernels.py --key 8 --variants 1,2 --ops wgrad)
   p.use = mode != 0 && H % 2 == 0 && W % 2 == 0 && Cin % 64 == 0 && Cout % 64 == 0 &&
-          (mode == 2 || (Cin >= 256 && Cout >= 256 && H * W >= 64 * 64));
+          (mode == 2 || (Cin >= 128 && Cout >= 128));
   if (!p.use) return p;
   p.T = (int64_t)B * (H / 2) * (W / 2);
   // the 16 GEMMs share one launch: split so all of them together make ~target blocks
