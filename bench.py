@@ -74,7 +74,7 @@ def igemm_shape(name, a):
         else:
             Bb, Hh, Ww, cin, cout = a[8:13]
             M, N, K, csrc, flags = Bb * Hh * Ww, cin, 9 * cout, cout, a[13]
-        if name.endswith("_ex") and min(csrc, N) >= 256 and Hh % 2 == 0 and Ww % 2 == 0:
+        if name.endswith("_ex") and csrc >= 256 and N >= 128 and Hh % 2 == 0 and Ww % 2 == 0:
             return M, N, K, "winograd"  # csrc/igemm.hip:wino_wanted_dims (default policy)
         bn = 64 if N <= 64 else 128
         if Hh % 8 == 0 and Ww % 16 == 0 and csrc % 4 == 0:

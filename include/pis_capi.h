@@ -56,8 +56,9 @@ int pis_version(void);
 #define PIS_TUNE_WGRAD_VARIANT 5 /* 0: one 16-pixel segment per stage, 1: two (default) */
 #define PIS_TUNE_WGRAD_BLOCKS 6  /* target workgroups of the split-K halo wgrad (default 512: one round at 2 per CU) */
 #define PIS_TUNE_C1_WGRAD 7      /* Cin == 1 weight gradient: 0 VALU stream kernel (default), 1 padded MFMA tile */
-#define PIS_TUNE_WINOGRAD 8      /* 3x3 convs: 0 direct only; 1 (default) Winograd for fwd/dgrad (*_ex) with >= 256 in and out
-                                    channels and for wgrad with >= 128; 2 Winograd whenever legal */
+#define PIS_TUNE_WINOGRAD 8      /* 3x3 convs: 0 direct only; 1 (default) Winograd for fwd/dgrad (*_ex) with >= 256
+                                    contraction and >= 128 output channels, for wgrad with >= 128 in and out;
+                                    2 Winograd whenever legal */
 #define PIS_TUNE_WINO_WGRAD_BLOCKS 9 /* target workgroups of the 16 batched Winograd weight-gradient GEMMs */
 #define PIS_TUNE_NKEYS 10
 #define PIS_DEBUG_NOLOAD (1 << 16)

@@ -19,6 +19,7 @@ LAYERS = [  # name, H, Cin, Cout
     ("enc1.conv1", 512, 64, 64), ("dec1.conv0", 512, 128, 64), ("enc2.conv1", 256, 128, 128),
     ("dec2.conv0", 256, 256, 128), ("enc3.conv1", 128, 256, 256), ("dec3.conv0", 128, 512, 256),
     ("enc4.conv1", 64, 512, 512), ("dec4.conv0", 64, 1024, 512), ("bottleneck", 32, 512, 512),
+    ("enc2.conv0", 256, 64, 128), ("enc3.conv0", 128, 128, 256), ("enc4.conv0", 64, 256, 512),
 ]
 B = 8
 NOLOAD_KEY = 2
