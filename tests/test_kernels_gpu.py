@@ -102,7 +102,7 @@ def test_conv3x3_dgrad_wgrad(hip, B, H, W, Cin, Cout):
 
 
 # every non-default kernel variant behind pis_tune (include/pis_capi.h) stays exact too
-TUNE_VARIANTS = [(4, 1), (4, 2), (4, 3), (5, 0), (6, 2048), (3, 0), (7, 1)]
+TUNE_VARIANTS = [(4, 1), (4, 2), (4, 3), (5, 0), (6, 2048), (3, 0), (7, 1), (8, 0), (8, 2)]
 
 
 @pytest.mark.parametrize("key,value", TUNE_VARIANTS)
@@ -114,6 +114,10 @@ def test_conv3x3_tuned_variants(hip, key, value):
         for shape in [(2, 16, 32, 64, 128), (1, 32, 16, 128, 64), (2, 16, 48, 256, 256)]:
             test_conv3x3_dgrad_wgrad(hip, *shape)
         test_conv3x3_c1_wgrad(hip)
+        for shape in [(2, 8, 12, 128, 64), (1, 16, 32, 256, 128)]:
+            test_convt2x2(hip, *shape)
+        for shape in [(2, 8, 8, 256, 256, 2), (1, 6, 10, 132, 64, 2)]:
+            test_conv3x3_ex_winograd(hip, *shape)
     finally:
         hip.pis_tune(key, prev)
 
