@@ -56,39 +56,11 @@ def conv_flops_per_image(H: int, W: int, c: int = 64) -> float:
     return 2.0 * macs * 3 - 2.0 * first
 
 
-IGEMM_CALLS = ("pis_conv3x3_fwd", "pis_conv3x3_dgrad", "pis_conv3x3_fwd_ex", "pis_conv3x3_dgrad_ex",
-               "pis_convt2x2_fwd", "pis_convt2x2_dgrad")
-DOMINANT = "conv3x3_halo_kernel<128, 4>"
-
-
-def igemm_shape(name, a):
-    """(M, N, K, kernel) of the implicit GEMM one C-ABI call launches (mirrors the
-    dispatch in csrc/igemm.hip: 3x3 convs on H%8 == 0, W%16 == 0 grids take the
-    halo kernel, BN = 64 for <= 64 output channels)."""
-    if name.startswith("pis_conv3x3_"):
-        if name.startswith("pis_conv3x3_fwd"):
-            Bb, Hh, Ww, cin, cout = a[7:12]
-            if cin == 1:
-                return None
-            M, N, K, csrc, flags = Bb * Hh * Ww, cout, 9 * cin, cin, a[12]
-        else:
-            Bb, Hh, Ww, cin, cout = a[8:13]
-            M, N, K, csrc, flags = Bb * Hh * Ww, cin, 9 * cout, cout, a[13]
-        if name.endswith("_ex") and csrc >= 256 and N >= 128 and Hh % 2 == 0 and Ww % 2 == 0:
-            return M, N, K, "winograd"  # csrc/igemm.hip:wino_wanted_dims (default policy)
-        bn = 64 if N <= 64 else 128
-        if Hh % 8 == 0 and Ww % 16 == 0 and csrc % 4 == 0:
-            ck = 8 if bn == 64 and csrc % 8 == 0 and not flags & 4 else 4  # PIS_MASK -> 4-channel slices
-            return M, N, K, f"conv3x3_halo_kernel<{bn}, {ck}>"
-        return M, N, K, f"igemm_f32_kernel<128, {bn}, 16, false>"
-    if name == "pis_convt2x2_fwd":
-        Bb, Hh, Ww, cin, cout = a[6:11]
-        M, N, K = Bb * Hh * Ww, 4 * cout, cin
-    else:
-        Bb, Hh, Ww, cin, cout = a[7:12]
-        M, N, K = Bb * Hh * Ww, cin, 4 * cout
-    t2d = "true" if (Hh % 8 == 0 and Ww % 16 == 0) else "false"
-    return M, N, K, f"igemm_f32_kernel<128, {64 if N <= 64 else 128}, 16, {t2d}>"
+# The dominant kernel of the step (profiles/r1_*_kernel_stats.csv): the batched fp32 MFMA GEMM
+# of the Winograd 3x3 convs (forward + input gradient), launched as "wino_gemm" by the C-ABI
+# (csrc/winograd.hip) and named igemm_f32_kernel<128, 128, 16, false> by rocprofv3.
+DOMINANT = "wino_gemm"
+DOMINANT_KERNEL = "igemm_f32_kernel<128, 128, 16, false>"
 
 
 def loss_call_bytes(name, a):
@@ -104,42 +76,53 @@ def loss_call_bytes(name, a):
     return None
 
 
-class LaunchTimer:
-    """HIP events around every launch of the dominant kernel (and of the fused-loss
-    calls), on the stream they run on."""
+class KernelTimer:
+    """HIP events recorded on the launch stream right before / after each launch of the
+    dominant kernel (pis_set_launch_hook), with the MFMA FLOPs that launch executes."""
 
     def __init__(self, kernel=DOMINANT):
         self.kernel = kernel
         self.records = []
-        self.loss = {}
+        self._open = None
 
-    def _events(self):
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        return e0, e1
+    def __call__(self, kernel, phase, stream, flop):
+        if kernel != self.kernel:
+            return
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record(torch.cuda.ExternalStream(stream) if stream else torch.cuda.current_stream())
+        if phase == 0:
+            self._open = (ev, flop)
+        else:
+            self.records.append((self._open[0], ev, flop))
+
+    def summary(self):
+        torch.cuda.synchronize()
+        ms = [e0.elapsed_time(e1) for e0, e1, _ in self.records]
+        fl = [f for _, _, f in self.records]
+        return len(ms), sum(fl) / len(fl), sum(ms) / len(ms)
+
+
+class LossCallTimer:
+    """HIP events around the fused-loss C-ABI calls (call tracer of _hip.call)."""
+
+    def __init__(self):
+        self.loss = {}
 
     def begin(self, name, args):
         nbytes = loss_call_bytes(name, args)
-        if nbytes is not None:
-            return ("loss", name, *self._events(), nbytes)
-        if name not in IGEMM_CALLS:
+        if nbytes is None:
             return None
-        shp = igemm_shape(name, args)
-        if shp is None or shp[3] != self.kernel:
-            return None
-        return ("mfma", name, *self._events(), 2.0 * shp[0] * shp[1] * shp[2])
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        return (name, e0, e1, nbytes)
 
     def end(self, tok):
-        if tok is None:
-            return
-        kind, name, e0, e1, work = tok
-        e1.record()
-        if kind == "loss":
-            self.loss.setdefault(name, []).append((e0, e1, work))
-        else:
-            self.records.append((e0, e1, work))
+        if tok is not None:
+            name, e0, e1, nbytes = tok
+            e1.record()
+            self.loss.setdefault(name, []).append((e0, e1, nbytes))
 
-    def loss_summary(self):
+    def summary(self):
         torch.cuda.synchronize()
         out = {}
         for name, recs in self.loss.items():
@@ -147,12 +130,6 @@ class LaunchTimer:
             nbytes = recs[0][2]
             out[name] = (ms, nbytes, nbytes / (ms * 1e-3) / 1e9)
         return out
-
-    def summary(self):
-        torch.cuda.synchronize()
-        ms = [e0.elapsed_time(e1) for e0, e1, _ in self.records]
-        fl = [f for _, _, f in self.records]
-        return len(ms), sum(fl) / len(fl), sum(ms) / len(ms)
 
 
 def load_pmc_traffic():
@@ -163,7 +140,7 @@ def load_pmc_traffic():
         return None
     with open(path) as f:
         d = json.load(f)
-    if DOMINANT not in (d.get("dominant_kernel") or ""):
+    if DOMINANT_KERNEL not in (d.get("dominant_kernel") or ""):
         return None  # counters were taken on another kernel: report no traffic rather than a stale one
     return d.get("hbm_bytes_per_launch")
 
@@ -246,13 +223,15 @@ def main():
     imgs_per_s = world * B * args.steps / dt
 
     # roofline of the dominant kernel: one instrumented step after the timed region
-    timer = LaunchTimer()
     from physics_informed_image_segmentation_amd import _hip
-    _hip.set_tracer(timer)
+    ktimer, ltimer = KernelTimer(), LossCallTimer()
+    _hip.set_launch_hook(ktimer)
+    _hip.set_tracer(ltimer)
     step()
     _hip.set_tracer(None)
-    n_launch, flop_per_launch, ms_per_launch = timer.summary()
-    loss_t = timer.loss_summary()
+    _hip.set_launch_hook(None)
+    n_launch, flop_per_launch, ms_per_launch = ktimer.summary()
+    loss_t = ltimer.summary()
     achieved = flop_per_launch / (ms_per_launch * 1e-3) / 1e12
     peak = 157.3  # fp32 MFMA dense TFLOP/s (MI355X_MICROARCH.md)
     traffic = load_pmc_traffic()
@@ -265,11 +244,13 @@ def main():
             "vs_baseline": None, "dtype": "fp32", "data": "synthetic",
             "config": {"workload": "C2: UNet(1,1,64) bs=8/GPU 512x512 Stage-II (lambda_RD=lambda_PF=1e-4, D=5, a=0.5, eps=0.05) AdamW lr=1e-5",
                        "global_batch": B * world, "image_size": [H, W], "parallelism": f"dp{world}"},
-            "roofline": {"bound": "mfma", "kernel": DOMINANT, "achieved": achieved, "peak": peak,
+            "roofline": {"bound": "mfma", "kernel": f"{DOMINANT_KERNEL} ({DOMINANT}: Winograd F(2x2,3x3) batched GEMMs)",
+                         "achieved": achieved, "peak": peak,
                          "unit": "TFLOP/s", "frac": achieved / peak, "traffic": traffic,
                          "launches_per_step": n_launch, "avg_launch_ms": ms_per_launch,
                          "flop_per_launch": flop_per_launch},
-            "step_tflops": flops / (ms * 1e-3) / 1e12,
+            # direct-convolution FLOPs of the step / step time (Winograd executes fewer)
+            "step_tflops_direct_equiv": flops / (ms * 1e-3) / 1e12,
             # north-star HBM figure for the fused loss: the backward runs inside the head
             # backward kernel (its reduce_slabs follow-ups inside the events); the forward's
             # time includes its one-block finalize launch

@@ -64,6 +64,14 @@ int pis_version(void);
 #define PIS_DEBUG_NOLOAD (1 << 16)
 int pis_tune(int key, int value);
 
+/* Profiling hook: called on the launching thread right before (phase 0) and after (phase 1)
+ * the enqueue of each heavy kernel ("conv3x3_halo", "wino_gemm", "wgrad3x3_halo",
+ * "wino_wgrad_gemm"), with its stream and the MFMA FLOPs it executes, so a profiler can
+ * record HIP events on that stream around exactly that kernel. NULL removes it. */
+typedef void (*pis_launch_hook_t)(const char* kernel, int phase, pis_stream_t stream, double flop,
+                                  void* user);
+void pis_set_launch_hook(pis_launch_hook_t fn, void* user);
+
 /* ---- 3x3 convolution, padding 1, stride 1 (src/unet.py:29,38 nn.Conv2d) ----
  * fwd:  y[p][n] = epi(bias[n] + sum_{r,s,c} x[p+(r-1,s-1)][c] * w[n][r][s][c])
  *       flags: PIS_RELU, PIS_SCALE (scale is [B][Cout]).   Cin==1 or Cin%4==0. */

@@ -29,7 +29,11 @@ class LossParams(ctypes.Structure):
 
 
 P, I, L, Z, Dbl = c_void_p, c_int, c_int64, c_size_t, c_double
+# void hook(const char* kernel, int phase, void* stream, double flop, void* user)
+LAUNCH_HOOK_T = ctypes.CFUNCTYPE(None, ctypes.c_char_p, c_int, c_void_p, ctypes.c_double, c_void_p)
+
 _SIGNATURES = {
+    "pis_set_launch_hook": ([LAUNCH_HOOK_T, P], None),
     "pis_version": ([], c_int),
     "pis_last_error": ([], ctypes.c_char_p),
     "pis_tune": ([I, I], c_int),
@@ -106,6 +110,21 @@ def check(rc: int, what: str) -> None:
 
 
 _tracer = None
+
+
+_hook_ref = None
+
+
+def set_launch_hook(fn) -> None:
+    """Install fn(kernel: str, phase: int, stream: int, flop: float) around the heavy kernel
+    launches of the C-ABI (pis_set_launch_hook); None removes it."""
+    global _hook_ref
+    if fn is None:
+        lib().pis_set_launch_hook(LAUNCH_HOOK_T(), None)
+        _hook_ref = None
+        return
+    _hook_ref = LAUNCH_HOOK_T(lambda k, ph, st, fl, user: fn(k.decode(), ph, st or 0, fl))
+    lib().pis_set_launch_hook(_hook_ref, None)
 
 
 def set_tracer(tracer) -> None:

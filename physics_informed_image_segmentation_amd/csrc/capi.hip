@@ -18,10 +18,23 @@ void set_error(const char* fmt, ...) {
 static std::atomic<int> g_tune[PIS_TUNE_NKEYS] = {0, 16, 0, 1, 0, 1, 512, 0, 1, 2048};
 
 int tune_get(int key) { return (key > 0 && key < PIS_TUNE_NKEYS) ? g_tune[key].load() : 0; }
+
+static std::atomic<pis_launch_hook_t> g_hook{nullptr};
+static std::atomic<void*> g_hook_user{nullptr};
+
+void launch_hook(const char* kernel, int phase, hipStream_t s, double flop) {
+  const pis_launch_hook_t fn = g_hook.load(std::memory_order_relaxed);
+  if (fn) fn(kernel, phase, (pis_stream_t)s, flop, g_hook_user.load(std::memory_order_relaxed));
+}
 }  // namespace pis
 
 extern "C" const char* pis_last_error(void) { return pis::g_last_error; }
 extern "C" int pis_version(void) { return 1; }
+
+extern "C" void pis_set_launch_hook(pis_launch_hook_t fn, void* user) {
+  pis::g_hook_user.store(user);
+  pis::g_hook.store(fn);
+}
 
 extern "C" int pis_tune(int key, int value) {
   if (key <= 0 || key >= PIS_TUNE_NKEYS) {

@@ -19,6 +19,10 @@ namespace pis {
 void set_error(const char* fmt, ...);
 int tune_get(int key);  // pis_tune() knob value (csrc/capi.hip)
 
+// Optional host callback around the heavy launches (pis_set_launch_hook): lets a
+// profiler record HIP events on the launch stream right before/after one kernel.
+void launch_hook(const char* kernel, int phase, hipStream_t s, double flop);
+
 inline int launch_status(const char* what) {
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) {

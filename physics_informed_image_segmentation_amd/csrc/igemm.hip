@@ -404,6 +404,8 @@ int launch_conv3x3(const IGemmArgs& a, hipStream_t s) {
   if (tune_get(PIS_TUNE_DEBUG_NOLOAD)) const_cast<IGemmArgs&>(a).flags |= PIS_DEBUG_NOLOAD;
   const int tiles = (a.M / (8 * 16));
   const int variant = tune_get(PIS_TUNE_HALO_VARIANT);
+  const double flop = 2.0 * a.M * a.N * 9.0 * a.Csrc;
+  launch_hook("conv3x3_halo", 0, s, flop);
   if (a.N <= 64) {
     // 8-channel slices measured faster for the forward convs, 4-channel slices for
     // the masked dgrad epilogue (tools/bench_kernels.py --key 4 --variants 0,1,3)
@@ -417,6 +419,7 @@ int launch_conv3x3(const IGemmArgs& a, hipStream_t s) {
   } else {
     hipLaunchKernelGGL((conv3x3_halo_kernel<128, 4>), dim3(tiles * (int)cdiv(a.N, 128)), dim3(256), 0, s, a);
   }
+  launch_hook("conv3x3_halo", 1, s, flop);
   return launch_status("conv3x3_halo");
 }
 

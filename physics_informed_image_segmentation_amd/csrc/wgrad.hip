@@ -655,7 +655,10 @@ static int wino_wgrad(const float* x, int ldx, const float* dz, int ldz, float* 
   a.part = part; a.part_bias = nullptr;
   a.bs_a = p.T * Cout; a.bs_b = p.T * Cin; a.bs_part = (int64_t)Cout * Cin;
   a.split_stride = (int64_t)16 * Cout * Cin;
+  const double flop = 2.0 * 16 * (double)p.T * Cout * Cin;
+  launch_hook("wino_wgrad_gemm", 0, s, flop);
   rc = run_wgrad(a, p.gemm, s, 16);
+  launch_hook("wino_wgrad_gemm", 1, s, flop);
   if (!rc) rc = reduce_slabs_pitched(part, p.gemm.splits, a.split_stride, a.split_stride, M, 0, s);
   if (!rc) rc = launch_wino_wgrad_out(M, Cout, Cin, dw, acc, s);
   if (!rc && db)
@@ -709,10 +712,13 @@ extern "C" int pis_conv3x3_wgrad(const float* x, int ldx, const float* dz, int l
     a.part = (float*)ws;
     a.part_bias = db ? (float*)((char*)ws + cdiv(hp.part_bytes, 256) * 256) : nullptr;
     const int tiles = (Cout / 64) * (Cin / 64);
+    const double flop = 2.0 * (double)B * H * W * Cout * 9.0 * Cin;
+    launch_hook("wgrad3x3_halo", 0, s, flop);
     if (tune_get(PIS_TUNE_WGRAD_VARIANT) != 0)
       hipLaunchKernelGGL((wgrad3x3_halo_kernel<2>), dim3(tiles * hp.splits), dim3(256), 0, s, a);
     else
       hipLaunchKernelGGL((wgrad3x3_halo_kernel<1>), dim3(tiles * hp.splits), dim3(256), 0, s, a);
+    launch_hook("wgrad3x3_halo", 1, s, flop);
     int rc = launch_status("wgrad3x3_halo");
     if (!rc) rc = reduce_slabs(a.part, hp.splits, (int64_t)Cout * 9 * Cin, dw_krsc, acc, s);
     if (rc || !db) return rc;

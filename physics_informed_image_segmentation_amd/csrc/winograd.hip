@@ -234,7 +234,10 @@ int launch_wino3x3(const IGemmArgs& a, int B, void* ws, hipStream_t s) {
   gm.Csrc = C; gm.ntaps = 1; gm.tap_mode = TAP_ONE; gm.wt = U; gm.ldw = C; gm.N = N;
   gm.epi = EPI_NHWC; gm.dst = Mt; gm.ldd = N; gm.flags = 0;
   gm.bs_src = T * C; gm.bs_wt = (int64_t)N * C; gm.bs_dst = T * N;
+  const double flop = 2.0 * 16 * (double)T * N * C;
+  launch_hook("wino_gemm", 0, s, flop);
   rc = launch_igemm(gm, s, 16);
+  launch_hook("wino_gemm", 1, s, flop);
   if (rc) return rc;
   hipLaunchKernelGGL(wino_output_kernel, dim3(grid_of(T * (N / 4))), dim3(256), 0, s, Mt, a, B);
   return launch_status("wino_output");
