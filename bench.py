@@ -58,9 +58,9 @@ def conv_flops_per_image(H: int, W: int, c: int = 64) -> float:
 
 # The dominant kernel of the step (profiles/r1_*_kernel_stats.csv): the batched fp32 MFMA GEMM
 # of the Winograd 3x3 convs (forward + input gradient), launched as "wino_gemm" by the C-ABI
-# (csrc/winograd.hip) and named igemm_f32_kernel<128, 128, 16, false> by rocprofv3.
+# (csrc/winograd.hip) and named gemm_nt_kernel<128, 128> by rocprofv3.
 DOMINANT = "wino_gemm"
-DOMINANT_KERNEL = "igemm_f32_kernel<128, 128, 16, false>"
+DOMINANT_KERNEL = "gemm_nt_kernel<128, 128>"
 
 
 def loss_call_bytes(name, a):

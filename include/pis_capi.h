@@ -60,7 +60,8 @@ int pis_version(void);
                                     contraction and >= 128 output channels, for wgrad with >= 128 in and out;
                                     2 Winograd whenever legal */
 #define PIS_TUNE_WINO_WGRAD_BLOCKS 9 /* target workgroups of the 16 batched Winograd weight-gradient GEMMs */
-#define PIS_TUNE_NKEYS 10
+#define PIS_TUNE_WINO_TILE 10    /* Winograd batched GEMM: 0 generic igemm, 1 lean NT GEMM 128x256 (N % 256 == 0), 2 lean NT GEMM 128x128 (default) */
+#define PIS_TUNE_NKEYS 11
 #define PIS_DEBUG_NOLOAD (1 << 16)
 int pis_tune(int key, int value);
 

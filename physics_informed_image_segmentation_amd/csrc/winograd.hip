@@ -206,6 +206,98 @@ __global__ __launch_bounds__(256) void wino_wgrad_out_kernel(const float* __rest
   }
 }
 
+// ---- the 16 batched GEMMs: C[z][m][n] = sum_k A[z][m][k] B[z][n][k] --------------------
+// Both operands K-contiguous ("NT"), plain row-major C, no epilogue: a lean kernel for the
+// Winograd contractions. Block tile BM x BN (4 waves, 2 x 2, each (BM/2) x (BN/2) as 32x32 MFMA
+// tiles), K-step 16 through a register-staged LDS double buffer; LDS rows padded to 20 floats
+// so the 16-byte fragment reads are conflict-free; one ds_read_b128 feeds 4 MFMAs.
+template <int BM, int BN>
+__global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const float* __restrict__ A, const float* __restrict__ Bm,
+                                                        float* __restrict__ Cm, int M, int N, int K,
+                                                        int64_t bsA, int64_t bsB, int64_t bsC) {
+  constexpr int BK = 16, ROW = BK + 4;
+  constexpr int TM = BM / 64, TN = BN / 64;
+  constexpr int AL = BM * 4 / 256, BL = BN * 4 / 256;  // float4 loads per thread per stage
+  __shared__ __attribute__((aligned(16))) float sA[2][BM * ROW];
+  __shared__ __attribute__((aligned(16))) float sB[2][BN * ROW];
+  A += blockIdx.y * bsA;
+  Bm += blockIdx.y * bsB;
+  Cm += blockIdx.y * bsC;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave & 1, wn = wave >> 1, li = lane & 31, lh = lane >> 5;
+  const int ntn = N / BN;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int m0 = (bid / ntn) * BM, n0 = (bid % ntn) * BN;
+  const int q4 = (tid & 3) * 4;
+  f32x4 ra[AL], rb[BL];
+  auto gload = [&](int k0) {
+    const int k = k0 + q4;
+#pragma unroll
+    for (int i = 0; i < AL; ++i) {
+      const int m = m0 + (tid + i * 256) / 4;
+      ra[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (m < M && k < K) ra[i] = *reinterpret_cast<const f32x4*>(A + (size_t)m * K + k);
+    }
+#pragma unroll
+    for (int i = 0; i < BL; ++i) {
+      const int n = n0 + (tid + i * 256) / 4;
+      rb[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (k < K) rb[i] = *reinterpret_cast<const f32x4*>(Bm + (size_t)n * K + k);
+    }
+  };
+  auto lstore = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < AL; ++i) *reinterpret_cast<f32x4*>(&sA[buf][((tid + i * 256) / 4) * ROW + q4]) = ra[i];
+#pragma unroll
+    for (int i = 0; i < BL; ++i) *reinterpret_cast<f32x4*>(&sB[buf][((tid + i * 256) / 4) * ROW + q4]) = rb[i];
+  };
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int b = 0; b < TN; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+  const int KT = (K + BK - 1) / BK;
+  gload(0);
+  lstore(0);
+  __syncthreads();
+  for (int kt = 0; kt < KT; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < KT) gload((kt + 1) * BK);
+#pragma unroll
+    for (int gg = 0; gg < BK / 8; ++gg) {
+      f32x4 af[TM], bf[TN];
+#pragma unroll
+      for (int a = 0; a < TM; ++a)
+        af[a] = *reinterpret_cast<const f32x4*>(&sA[cur][(wm * (BM / 2) + a * 32 + li) * ROW + 8 * gg + 4 * lh]);
+#pragma unroll
+      for (int b = 0; b < TN; ++b)
+        bf[b] = *reinterpret_cast<const f32x4*>(&sB[cur][(wn * (BN / 2) + b * 32 + li) * ROW + 8 * gg + 4 * lh]);
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int a = 0; a < TM; ++a)
+#pragma unroll
+          for (int b = 0; b < TN; ++b)
+            acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[a][t], bf[b][t], acc[a][b], 0, 0, 0);
+    }
+    if (kt + 1 < KT) lstore(cur ^ 1);
+    __syncthreads();
+  }
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int b = 0; b < TN; ++b) {
+      const int n = n0 + wn * (BN / 2) + b * 32 + li;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm * (BM / 2) + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        if (m < M) Cm[(size_t)m * N + n] = acc[a][b][r];
+      }
+    }
+}
+
 static int grid_of(int64_t work) { return (int)std::max<int64_t>(1, std::min<int64_t>(cdiv(work, 256), 16384)); }
 
 bool wino_ok(const IGemmArgs& a) {
@@ -229,14 +321,27 @@ int launch_wino3x3(const IGemmArgs& a, int B, void* ws, hipStream_t s) {
   hipLaunchKernelGGL(wino_input_kernel, dim3(grid_of(T * (C / 4))), dim3(256), 0, s, a.src, a.lds, B, a.H, a.W, C, V);
   int rc = launch_status("wino_transforms");
   if (rc) return rc;
-  IGemmArgs gm{};
-  gm.src = V; gm.lds = C; gm.Hs = 1; gm.Ws = (int)T; gm.H = 1; gm.W = (int)T; gm.M = (int)T;
-  gm.Csrc = C; gm.ntaps = 1; gm.tap_mode = TAP_ONE; gm.wt = U; gm.ldw = C; gm.N = N;
-  gm.epi = EPI_NHWC; gm.dst = Mt; gm.ldd = N; gm.flags = 0;
-  gm.bs_src = T * C; gm.bs_wt = (int64_t)N * C; gm.bs_dst = T * N;
   const double flop = 2.0 * 16 * (double)T * N * C;
   launch_hook("wino_gemm", 0, s, flop);
-  rc = launch_igemm(gm, s, 16);
+  const int v = tune_get(PIS_TUNE_WINO_TILE);
+  if (v == 1 && N % 256 == 0) {
+    const dim3 grid((int)cdiv(T, 128) * (N / 256), 16);
+    hipLaunchKernelGGL((gemm_nt_kernel<128, 256>), grid, dim3(256), 0, s, V, U, Mt, (int)T, N, C, T * C,
+                       (int64_t)N * C, T * N);
+    rc = launch_status("wino_gemm");
+  } else if (v == 2 && N % 128 == 0) {
+    const dim3 grid((int)cdiv(T, 128) * (N / 128), 16);
+    hipLaunchKernelGGL((gemm_nt_kernel<128, 128>), grid, dim3(256), 0, s, V, U, Mt, (int)T, N, C, T * C,
+                       (int64_t)N * C, T * N);
+    rc = launch_status("wino_gemm");
+  } else {
+    IGemmArgs gm{};
+    gm.src = V; gm.lds = C; gm.Hs = 1; gm.Ws = (int)T; gm.H = 1; gm.W = (int)T; gm.M = (int)T;
+    gm.Csrc = C; gm.ntaps = 1; gm.tap_mode = TAP_ONE; gm.wt = U; gm.ldw = C; gm.N = N;
+    gm.epi = EPI_NHWC; gm.dst = Mt; gm.ldd = N; gm.flags = 0;
+    gm.bs_src = T * C; gm.bs_wt = (int64_t)N * C; gm.bs_dst = T * N;
+    rc = launch_igemm(gm, s, 16);
+  }
   launch_hook("wino_gemm", 1, s, flop);
   if (rc) return rc;
   hipLaunchKernelGGL(wino_output_kernel, dim3(grid_of(T * (N / 4))), dim3(256), 0, s, Mt, a, B);

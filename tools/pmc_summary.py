@@ -25,7 +25,7 @@ def per_kernel(path, counter):
     return {k: (sum(v) / len(v), len(v)) for k, v in acc.items()}
 
 
-def main(fetch_csv, write_csv, out_json, dominant="igemm_f32_kernel<128, 128, 16, false>"):
+def main(fetch_csv, write_csv, out_json, dominant="gemm_nt_kernel<128, 128>"):
     f = per_kernel(fetch_csv, "FETCH_SIZE")
     w = per_kernel(write_csv, "WRITE_SIZE")
     table = {}
