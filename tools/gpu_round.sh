@@ -1,0 +1,37 @@
+#!/bin/bash
+# One GPU-box session: gpu tests, the default bench, a rocprofv3 kernel-trace summary of the
+# bench, and the two PMC passes (FETCH_SIZE, WRITE_SIZE) for HBM traffic.
+#   bash tools/gpu_round.sh TAG [tests|notests]
+# Every GPU step runs under its own time limit; a fault / abort / timeout ends the script.
+TAG=${1:-run}
+MODE=${2:-tests}
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+
+fatal() {  # exit statuses that mean the GPU step crashed or hung
+  case $1 in 124|134|137|139) return 0 ;; esac
+  [ "$1" -ge 128 ] && return 0
+  return 1
+}
+
+step() {  # step NAME SECONDS cmd...
+  local name=$1 secs=$2; shift 2
+  echo "== $name ($(date +%T))"
+  timeout -k 10 "$secs" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "== $name exit $rc"
+  tail -3 "$OUT/$name.log"
+  if fatal $rc; then echo "FATAL in $name"; exit $rc; fi
+  return 0
+}
+
+if [ "$MODE" = tests ]; then
+  step pytest_gpu 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
+fi
+step bench 300 python -u bench.py
+cp "$OUT/bench.log" "$OUT/bench.json.log"
+step rocprof_stats 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline
+step pmc_fetch 120 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline
+step pmc_write 120 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline
+echo "== done"
