@@ -61,7 +61,9 @@ int pis_version(void);
                                     2 Winograd whenever legal */
 #define PIS_TUNE_WINO_WGRAD_BLOCKS 9 /* target workgroups of the 16 batched Winograd weight-gradient GEMMs */
 #define PIS_TUNE_WINO_TILE 10    /* Winograd batched GEMM: 0 generic igemm, 1 lean NT GEMM 128x256 (N % 256 == 0), 2 lean NT GEMM 128x128 (default) */
-#define PIS_TUNE_NKEYS 11
+#define PIS_TUNE_WINO_F4 11      /* Winograd tile: 0 F(2x2,3x3) fwd/dgrad + F(3x3,2x2) wgrad; 1 (default) F(4x4,3x3) +
+                                    F(3x3,4x4) when H % 4 == W % 4 == 0 */
+#define PIS_TUNE_NKEYS 12
 #define PIS_DEBUG_NOLOAD (1 << 16)
 int pis_tune(int key, int value);
 

@@ -38,13 +38,16 @@ struct IGemmArgs {
 int launch_igemm(const IGemmArgs& a, hipStream_t s, int batches = 1);
 // 3x3 conv (fwd or dgrad-on-flipped-weights): halo kernel when the grid allows, else igemm
 int launch_conv3x3(const IGemmArgs& a, hipStream_t s);
-// Winograd F(2x2,3x3) path of the same conv (winograd.hip); B = images in a.src
+// Winograd F(4x4,3x3) / F(2x2,3x3) path of the same conv (winograd.hip); B = images in a.src
 bool wino_ok(const IGemmArgs& a);
+// output tile edge of the Winograd fwd/dgrad path for this grid: 4 (F(4x4,3x3)) or 2
+int wino_tile(int H, int W);
 size_t wino_ws_bytes(int B, int H, int W, int C, int N);
 int launch_wino3x3(const IGemmArgs& a, int B, void* ws, hipStream_t s);
-// Winograd weight-gradient pieces: V[16][T][C] of x, E[16][T][N] of dz, dW from M[16][N][C]
-int launch_wino_input(const float* x, int ldx, int B, int H, int W, int C, float* V, hipStream_t s);
-int launch_wino_dz(const float* dz, int ldz, int B, int H, int W, int N, float* E, hipStream_t s);
-int launch_wino_wgrad_out(const float* M, int N, int C, float* dw, int accumulate, hipStream_t s);
+// Winograd weight-gradient pieces for tile edge m (2: F(3x3,2x2), 4: F(3x3,4x4)), nxi = (m+2)^2:
+// V[nxi][T][C] of x, E[nxi][T][N] of dz, dW from M[nxi][N][C]
+int launch_wino_input(const float* x, int ldx, int B, int H, int W, int C, float* V, hipStream_t s, int m);
+int launch_wino_dz(const float* dz, int ldz, int B, int H, int W, int N, float* E, hipStream_t s, int m);
+int launch_wino_wgrad_out(const float* M, int N, int C, float* dw, int accumulate, hipStream_t s, int m);
 
 }  // namespace pis

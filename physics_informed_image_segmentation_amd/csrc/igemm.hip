@@ -501,13 +501,17 @@ __global__ void convt_prep_kernel(const float* __restrict__ w, float* __restrict
 
 using namespace pis;
 
-// Winograd F(2x2,3x3) policy (winograd.hip): channel-heavy convs, where its GEMMs stay MFMA-bound
+// Winograd policy (winograd.hip): where its GEMMs stay MFMA-bound and beat the direct kernels
 static bool wino_wanted_dims(int H, int W, int C, int N) {
   const int mode = tune_get(PIS_TUNE_WINOGRAD);
   if (mode == 0 || H % 2 || W % 2 || C % 4 || N % 4) return false;
-  // measured (tools/bench_kernels.py --key 8): the 16 GEMMs need >= 256 contraction channels;
-  // 128 output channels suffice then (dec2.conv0 fwd, enc3.conv0 dgrad: -7 %)
-  return mode == 2 || (C >= 256 && N >= 128);
+  if (mode == 2) return true;
+  // measured (tools/bench_kernels.py --key 8 --variants 1,2 --ops fwd,dgrad, B=8):
+  // F(4x4,3x3) beats the direct halo kernels from 128 channels on either side (dec1.conv0
+  // fwd -22 %, dgrad -27 %; enc2.conv1 -41 %) and only loses at 64 -> 64 (+1.5-3 %);
+  // F(2x2,3x3) needs >= 256 contraction channels and 128 outputs
+  if (wino_tile(H, W) == 4) return C >= 128 || N >= 128;
+  return C >= 256 && N >= 128;
 }
 
 static int dispatch_conv3x3(const IGemmArgs& a, int B, void* ws, size_t ws_bytes, hipStream_t s) {

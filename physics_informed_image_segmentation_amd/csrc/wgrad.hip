@@ -605,12 +605,14 @@ __global__ __launch_bounds__(256) void wgrad_c1_kernel(const float* __restrict__
   }
 }
 
-// Winograd F(3x3, 2x2) weight gradient (csrc/winograd.hip): V = B^T x B and E = A dz A^T per
-// 2x2 tile, M_xi[n][c] = sum_tiles E_xi[t][n] V_xi[t][c] as 16 batched split-K GEMMs over the
-// T tiles (slabs [split][xi][Cout][Cin], one fixed-order reduction), dW = G^T M G; the bias
-// gradient is a channel sum of dz.
+// Winograd weight gradient (csrc/winograd.hip), F(3x3, 4x4) when the 4x4 tile grid fits (pis_tune
+// key 11), else F(3x3, 2x2): V = B^T x B and E = G e G^T per tile, M_xi[n][c] = sum_tiles
+// E_xi[t][n] V_xi[t][c] as nxi = (m+2)^2 batched split-K GEMMs over the T tiles (slabs
+// [split][xi][Cout][Cin], one fixed-order reduction), dW = A^T M A; the bias gradient is a
+// channel sum of dz.
 struct WinoWgradPlan {
   bool use;
+  int m, nxi;
   int64_t T;
   WgradPlan gemm;
   size_t off_E, off_part, off_M, off_cs, total;
@@ -624,12 +626,14 @@ static WinoWgradPlan wino_wgrad_plan(int B, int H, int W, int Cin, int Cout) {
   p.use = mode != 0 && H % 2 == 0 && W % 2 == 0 && Cin % 64 == 0 && Cout % 64 == 0 &&
           (mode == 2 || (Cin >= 128 && Cout >= 128));
   if (!p.use) return p;
-  p.T = (int64_t)B * (H / 2) * (W / 2);
-  // the 16 GEMMs share one launch: split so all of them together make ~target blocks
-  p.gemm = plan_wgrad(Cout, Cin, (int)p.T, Cout, Cin, std::max(16, tune_get(PIS_TUNE_WINO_WGRAD_BLOCKS) / 16));
+  p.m = (tune_get(PIS_TUNE_WINO_F4) != 0 && H % 4 == 0 && W % 4 == 0) ? 4 : 2;
+  p.nxi = (p.m + 2) * (p.m + 2);
+  p.T = (int64_t)B * (H / p.m) * (W / p.m);
+  // the nxi GEMMs share one launch: split so all of them together make ~target blocks
+  p.gemm = plan_wgrad(Cout, Cin, (int)p.T, Cout, Cin, std::max(16, tune_get(PIS_TUNE_WINO_WGRAD_BLOCKS) / p.nxi));
   auto al = [](size_t b) { return cdiv(b, 256) * 256; };
-  const size_t V = al((size_t)16 * p.T * Cin * 4), E = al((size_t)16 * p.T * Cout * 4);
-  const size_t part = al((size_t)p.gemm.splits * 16 * Cout * Cin * 4), M = al((size_t)16 * Cout * Cin * 4);
+  const size_t V = al((size_t)p.nxi * p.T * Cin * 4), E = al((size_t)p.nxi * p.T * Cout * 4);
+  const size_t part = al((size_t)p.gemm.splits * p.nxi * Cout * Cin * 4), M = al((size_t)p.nxi * Cout * Cin * 4);
   p.off_E = V;
   p.off_part = V + E;
   p.off_M = p.off_part + part;
@@ -645,8 +649,8 @@ static int wino_wgrad(const float* x, int ldx, const float* dz, int ldz, float* 
   float* E = (float*)(base + p.off_E);
   float* part = (float*)(base + p.off_part);
   float* M = (float*)(base + p.off_M);
-  int rc = launch_wino_input(x, ldx, B, H, W, Cin, V, s);
-  if (!rc) rc = launch_wino_dz(dz, ldz, B, H, W, Cout, E, s);
+  int rc = launch_wino_input(x, ldx, B, H, W, Cin, V, s, p.m);
+  if (!rc) rc = launch_wino_dz(dz, ldz, B, H, W, Cout, E, s, p.m);
   if (rc) return rc;
   WgradArgs a{};
   a.a = E; a.lda = Cout; a.a_up2 = 0; a.Ca = Cout;
@@ -654,13 +658,13 @@ static int wino_wgrad(const float* x, int ldx, const float* dz, int ldz, float* 
   a.B = 1; a.H = 1; a.W = (int)p.T; a.P = (int)p.T; a.Mp = Cout; a.Np = Cin;
   a.part = part; a.part_bias = nullptr;
   a.bs_a = p.T * Cout; a.bs_b = p.T * Cin; a.bs_part = (int64_t)Cout * Cin;
-  a.split_stride = (int64_t)16 * Cout * Cin;
-  const double flop = 2.0 * 16 * (double)p.T * Cout * Cin;
+  a.split_stride = (int64_t)p.nxi * Cout * Cin;
+  const double flop = 2.0 * p.nxi * (double)p.T * Cout * Cin;
   launch_hook("wino_wgrad_gemm", 0, s, flop);
-  rc = run_wgrad(a, p.gemm, s, 16);
+  rc = run_wgrad(a, p.gemm, s, p.nxi);
   launch_hook("wino_wgrad_gemm", 1, s, flop);
   if (!rc) rc = reduce_slabs_pitched(part, p.gemm.splits, a.split_stride, a.split_stride, M, 0, s);
-  if (!rc) rc = launch_wino_wgrad_out(M, Cout, Cin, dw, acc, s);
+  if (!rc) rc = launch_wino_wgrad_out(M, Cout, Cin, dw, acc, s, p.m);
   if (!rc && db)
     rc = colsum(dz, ldz, (int64_t)B * H * W, Cout, db, acc, base + p.off_cs, p.total - p.off_cs, s);
   return rc;

@@ -86,6 +86,24 @@ __global__ __launch_bounds__(256) void wino_input_kernel(const float* __restrict
   }
 }
 
+// conv epilogue on 4 channels of one output pixel (v = conv + bias): ReLU, ReLU-backward
+// mask, dropout keep-scale, accumulate — the direct kernels' epilogue (igemm.hip)
+__device__ __forceinline__ void conv_epilogue4(const IGemmArgs& g, size_t pix, int n, f32x4 v, f32x4 sc4) {
+  if (g.flags & PIS_RELU) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = fmaxf(v[k], 0.f);
+  }
+  if (g.flags & PIS_MASK) {
+    const f32x4 mk = *reinterpret_cast<const f32x4*>(g.mask + pix * g.ldm + n);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = mk[k] > 0.f ? v[k] : 0.f;
+  }
+  v *= sc4;
+  float* dst = g.dst + pix * g.ldd + n;
+  if (g.flags & PIS_ACCUMULATE) v += *reinterpret_cast<const f32x4*>(dst);
+  *reinterpret_cast<f32x4*>(dst) = v;
+}
+
 // Y = A^T M A per tile and 4 output channels, then the conv epilogue of the direct
 // kernels (bias, ReLU, ReLU-backward mask, dropout keep-scale, accumulate).
 __global__ __launch_bounds__(256) void wino_output_kernel(const float* __restrict__ Mt, IGemmArgs g, int B) {
@@ -115,20 +133,7 @@ __global__ __launch_bounds__(256) void wino_output_kernel(const float* __restric
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const size_t pix = ((size_t)b * g.H + 2 * ty + i) * g.W + 2 * tx + j;
-        f32x4 v = (j == 0 ? y0 : y1) + bias4;
-        if (g.flags & PIS_RELU) {
-#pragma unroll
-          for (int k = 0; k < 4; ++k) v[k] = fmaxf(v[k], 0.f);
-        }
-        if (g.flags & PIS_MASK) {
-          const f32x4 mk = *reinterpret_cast<const f32x4*>(g.mask + pix * g.ldm + n);
-#pragma unroll
-          for (int k = 0; k < 4; ++k) v[k] = mk[k] > 0.f ? v[k] : 0.f;
-        }
-        v *= sc4;
-        float* dst = g.dst + pix * g.ldd + n;
-        if (g.flags & PIS_ACCUMULATE) v += *reinterpret_cast<const f32x4*>(dst);
-        *reinterpret_cast<f32x4*>(dst) = v;
+        conv_epilogue4(g, pix, n, (j == 0 ? y0 : y1) + bias4, sc4);
       }
     }
   }
@@ -203,6 +208,248 @@ __global__ __launch_bounds__(256) void wino_wgrad_out_kernel(const float* __rest
         o[2 * C] = w2;
       }
     }
+  }
+}
+
+// ---- F(4x4, 3x3): 6x6 input patches, 36 contractions, 2.25 MACs per output (direct: 9) ----
+// Cook-Toom points {0, 1, -1, 1/2, -2, inf}: fp32 error 1.8e-6 relative (norm, 512-channel
+// layers against float64) where the usual {0, +-1, +-2} gives 2.7e-6 and F(2x2,3x3) 0.4e-6.
+// V = BT d BT^T, U = G g G^T, Y = AT M AT^T. Per output pixel the transformed operands are
+// 36/16 = 2.25 floats per channel (F(2x2): 4), so the transforms stream less HBM too.
+// The tile grid needs H % 4 == W % 4 == 0.
+__host__ __device__ constexpr float w4_bt(int i, int k) {
+  constexpr float m[6][6] = {{1.f, -1.5f, -2.f, 1.5f, 1.f, 0.f},  {0.f, -1.f, 0.5f, 2.5f, 1.f, 0.f},
+                             {0.f, 1.f, -2.5f, 0.5f, 1.f, 0.f},   {0.f, -2.f, -1.f, 2.f, 1.f, 0.f},
+                             {0.f, 0.5f, -1.f, -0.5f, 1.f, 0.f},  {0.f, 1.f, -1.5f, -2.f, 1.5f, 1.f}};
+  return m[i][k];
+}
+__host__ __device__ constexpr float w4_g(int i, int k) {
+  constexpr float m[6][3] = {{1.f, 0.f, 0.f},
+                             {1.f / 3, 1.f / 3, 1.f / 3},
+                             {-1.f / 3, 1.f / 3, -1.f / 3},
+                             {-16.f / 15, -8.f / 15, -4.f / 15},
+                             {1.f / 15, -2.f / 15, 4.f / 15},
+                             {0.f, 0.f, 1.f}};
+  return m[i][k];
+}
+__host__ __device__ constexpr float w4_at(int i, int k) {
+  constexpr float m[4][6] = {{1.f, 1.f, 1.f, 1.f, 1.f, 0.f},
+                             {0.f, 1.f, -1.f, 0.5f, -2.f, 0.f},
+                             {0.f, 1.f, 1.f, 0.25f, 4.f, 0.f},
+                             {0.f, 1.f, -1.f, 0.125f, -8.f, 1.f}};
+  return m[i][k];
+}
+// acc += c * v with the compile-time coefficient c folded (0: nothing, +-1: add/sub)
+template <typename T>
+__device__ __forceinline__ void axpy_c(T& acc, float c, const T& v) {
+  if (c == 0.f) return;
+  if (c == 1.f) acc += v;
+  else if (c == -1.f) acc -= v;
+  else acc += c * v;
+}
+
+// U[xi][n][c] = (G g G^T)[xi], xi = 6 i + j
+__global__ __launch_bounds__(256) void wino4_filter_kernel(const float* __restrict__ w, int ldw, int N, int C,
+                                                           float* __restrict__ U) {
+  const int64_t NC = (int64_t)N * C;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < NC; e += (int64_t)gridDim.x * blockDim.x) {
+    const int n = (int)(e / C), c = (int)(e - (int64_t)n * C);
+    float g[3][3];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) g[t / 3][t % 3] = w[(size_t)n * ldw + t * C + c];
+    float gg[6][3];  // G g
+#pragma unroll
+    for (int i = 0; i < 6; ++i)
+#pragma unroll
+      for (int s = 0; s < 3; ++s) {
+        gg[i][s] = 0.f;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) axpy_c(gg[i][s], w4_g(i, k), g[k][s]);
+      }
+#pragma unroll
+    for (int i = 0; i < 6; ++i)
+#pragma unroll
+      for (int j = 0; j < 6; ++j) {
+        float u = 0.f;
+#pragma unroll
+        for (int s = 0; s < 3; ++s) axpy_c(u, w4_g(j, s), gg[i][s]);
+        U[(size_t)(i * 6 + j) * NC + e] = u;
+      }
+  }
+}
+
+// V[xi][t][c] = (BT d BT^T)[xi], d = the 6x6 input patch at rows 4ty-1.., cols 4tx-1.. (zero padded)
+__global__ __launch_bounds__(256) void wino4_input_kernel(const float* __restrict__ x, int ldx, int B, int H, int W,
+                                                          int C, float* __restrict__ V) {
+  const int c4n = C / 4, TW = W / 4, TH = H / 4;
+  const int64_t T = (int64_t)B * TH * TW, TC = T * C;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < T * c4n; e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t t = e / c4n;
+    const int c = (int)(e - t * c4n) * 4;
+    const int b = (int)(t / (TH * TW)), rem = (int)(t - (int64_t)b * TH * TW);
+    const int ty = rem / TW, tx = rem - ty * TW;
+    f32x4 v[6][6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i)
+#pragma unroll
+      for (int j = 0; j < 6; ++j) v[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {  // input row k: its row transform, then its share of every V row
+      const int h = 4 * ty - 1 + k;
+      f32x4 d[6];
+#pragma unroll
+      for (int l = 0; l < 6; ++l) {
+        const int ww = 4 * tx - 1 + l;
+        d[l] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (h >= 0 && h < H && ww >= 0 && ww < W)
+          d[l] = *reinterpret_cast<const f32x4*>(x + (((size_t)b * H + h) * W + ww) * ldx + c);
+      }
+#pragma unroll
+      for (int j = 0; j < 6; ++j) {
+        f32x4 r = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int l = 0; l < 6; ++l) axpy_c(r, w4_bt(j, l), d[l]);
+#pragma unroll
+        for (int i = 0; i < 6; ++i) axpy_c(v[i][j], w4_bt(i, k), r);
+      }
+    }
+#pragma unroll
+    for (int xi = 0; xi < 36; ++xi)
+      *reinterpret_cast<f32x4*>(V + (size_t)xi * TC + t * C + c) = v[xi / 6][xi % 6];
+  }
+}
+
+// Y = AT M AT^T per tile and 4 output channels, then the direct kernels' conv epilogue
+__global__ __launch_bounds__(256) void wino4_output_kernel(const float* __restrict__ Mt, IGemmArgs g, int B) {
+  const int N = g.N, n4n = N / 4, TW = g.W / 4, TH = g.H / 4;
+  const int64_t T = (int64_t)B * TH * TW, TN = T * N;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < T * n4n; e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t t = e / n4n;
+    const int n = (int)(e - t * n4n) * 4;
+    const int b = (int)(t / (TH * TW)), rem = (int)(t - (int64_t)b * TH * TW);
+    const int ty = rem / TW, tx = rem - ty * TW;
+    f32x4 y[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) y[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+      f32x4 m[6];
+#pragma unroll
+      for (int l = 0; l < 6; ++l) m[l] = *reinterpret_cast<const f32x4*>(Mt + (size_t)(k * 6 + l) * TN + t * N + n);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        f32x4 r = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int l = 0; l < 6; ++l) axpy_c(r, w4_at(j, l), m[l]);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) axpy_c(y[i][j], w4_at(i, k), r);
+      }
+    }
+    f32x4 bias4 = {0.f, 0.f, 0.f, 0.f}, sc4 = {1.f, 1.f, 1.f, 1.f};
+    if (g.bias) bias4 = *reinterpret_cast<const f32x4*>(g.bias + n);
+    if (g.flags & PIS_SCALE) sc4 = *reinterpret_cast<const f32x4*>(g.scale + (size_t)b * N + n);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const size_t pix = ((size_t)b * g.H + 4 * ty + i) * g.W + 4 * tx + j;
+        conv_epilogue4(g, pix, n, y[i][j] + bias4, sc4);
+      }
+  }
+}
+
+// ---- weight gradient F(3x3, 4x4): 4x4 output-gradient tiles, 36 contractions over tiles ----
+// dW[r] = sum_k x[4t - 1 + r + k] dz[4t + k] per tile is the correlation F(3, 4): 6 input
+// samples, 4 "filter" taps (the dz tile), 3 outputs (the weight taps). Same points
+// {0, 1, -1, 1/2, -2, inf}, so the input transform is the forward's BT (wino4_input_kernel);
+// E = G4 e G4^T with G4 (6x4), dW = AT3 M AT3^T with AT3 (3x6). fp32 error 1.3e-6 relative
+// (F(3x3,2x2): 0.4e-6, direct 0.6e-6; 256-channel layers against float64).
+__host__ __device__ constexpr float w4_g4(int i, int k) {
+  constexpr float m[6][4] = {{1.f, 0.f, 0.f, 0.f},
+                             {1.f / 3, 1.f / 3, 1.f / 3, 1.f / 3},
+                             {-1.f / 3, 1.f / 3, -1.f / 3, 1.f / 3},
+                             {-16.f / 15, -8.f / 15, -4.f / 15, -2.f / 15},
+                             {1.f / 15, -2.f / 15, 4.f / 15, -8.f / 15},
+                             {0.f, 0.f, 0.f, 1.f}};
+  return m[i][k];
+}
+__host__ __device__ constexpr float w4_at3(int i, int k) {
+  constexpr float m[3][6] = {{1.f, 1.f, 1.f, 1.f, 1.f, 0.f},
+                             {0.f, 1.f, -1.f, 0.5f, -2.f, 0.f},
+                             {0.f, 1.f, 1.f, 0.25f, 4.f, 1.f}};
+  return m[i][k];
+}
+
+// E[xi][t][n] = (G4 e G4^T)[xi], e = dz at output pixels (4ty + i, 4tx + j)
+__global__ __launch_bounds__(256) void wino4_dz_kernel(const float* __restrict__ dz, int ldz, int B, int H, int W,
+                                                       int N, float* __restrict__ E) {
+  const int n4n = N / 4, TW = W / 4, TH = H / 4;
+  const int64_t T = (int64_t)B * TH * TW, TN = T * N;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < T * n4n; e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t t = e / n4n;
+    const int n = (int)(e - t * n4n) * 4;
+    const int b = (int)(t / (TH * TW)), rem = (int)(t - (int64_t)b * TH * TW);
+    const int ty = rem / TW, tx = rem - ty * TW;
+    f32x4 v[6][6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i)
+#pragma unroll
+      for (int j = 0; j < 6; ++j) v[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      f32x4 d[4];
+#pragma unroll
+      for (int l = 0; l < 4; ++l)
+        d[l] = *reinterpret_cast<const f32x4*>(dz + (((size_t)b * H + 4 * ty + k) * W + 4 * tx + l) * ldz + n);
+#pragma unroll
+      for (int j = 0; j < 6; ++j) {
+        f32x4 r = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int l = 0; l < 4; ++l) axpy_c(r, w4_g4(j, l), d[l]);
+#pragma unroll
+        for (int i = 0; i < 6; ++i) axpy_c(v[i][j], w4_g4(i, k), r);
+      }
+    }
+#pragma unroll
+    for (int xi = 0; xi < 36; ++xi)
+      *reinterpret_cast<f32x4*>(E + (size_t)xi * TN + t * N + n) = v[xi / 6][xi % 6];
+  }
+}
+
+// dw[n][r][s][c] (+)= (AT3 M AT3^T)[r][s], M[xi][n][c] the reduced tile sums
+__global__ __launch_bounds__(256) void wino4_wgrad_out_kernel(const float* __restrict__ M, int N, int C,
+                                                              float* __restrict__ dw, int accumulate) {
+  const int64_t NC = (int64_t)N * C;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < NC; e += (int64_t)gridDim.x * blockDim.x) {
+    const int n = (int)(e / C), c = (int)(e - (int64_t)n * C);
+    float y[3][3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+      for (int j = 0; j < 3; ++j) y[i][j] = 0.f;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+      float m[6];
+#pragma unroll
+      for (int l = 0; l < 6; ++l) m[l] = M[(size_t)(k * 6 + l) * NC + e];
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        float r = 0.f;
+#pragma unroll
+        for (int l = 0; l < 6; ++l) axpy_c(r, w4_at3(j, l), m[l]);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) axpy_c(y[i][j], w4_at3(i, k), r);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        float* o = dw + ((size_t)n * 9 + i * 3 + j) * C + c;
+        *o = accumulate ? *o + y[i][j] : y[i][j];
+      }
   }
 }
 
@@ -300,37 +547,49 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const float* __restrict
 
 static int grid_of(int64_t work) { return (int)std::max<int64_t>(1, std::min<int64_t>(cdiv(work, 256), 16384)); }
 
+// F(4x4,3x3) when the 4x4 tile grid fits and pis_tune key 11 allows it, else F(2x2,3x3)
+int wino_tile(int H, int W) { return (tune_get(PIS_TUNE_WINO_F4) != 0 && H % 4 == 0 && W % 4 == 0) ? 4 : 2; }
+
 bool wino_ok(const IGemmArgs& a) {
   return a.tap_mode == TAP_CONV3 && a.epi == EPI_NHWC && a.H % 2 == 0 && a.W % 2 == 0 && a.Csrc % 4 == 0 &&
          a.N % 4 == 0 && a.lds % 4 == 0 && a.ldd % 4 == 0 && (!(a.flags & PIS_MASK) || a.ldm % 4 == 0);
 }
 
 size_t wino_ws_bytes(int B, int H, int W, int C, int N) {
-  const int64_t T = (int64_t)B * (H / 2) * (W / 2);
-  return (size_t)16 * ((int64_t)N * C + T * C + T * N) * sizeof(float) + 1024;
+  const int m = wino_tile(H, W), nxi = (m + 2) * (m + 2);
+  const int64_t T = (int64_t)B * (H / m) * (W / m);
+  return (size_t)nxi * ((int64_t)N * C + T * C + T * N) * sizeof(float) + 1024;
 }
 
 // a describes the direct conv (src/lds = input, wt/ldw = KRSC weights, N outputs, epilogue)
 int launch_wino3x3(const IGemmArgs& a, int B, void* ws, hipStream_t s) {
   const int C = a.Csrc, N = a.N;
-  const int64_t T = (int64_t)B * (a.H / 2) * (a.W / 2);
+  const int m = wino_tile(a.H, a.W), nxi = (m + 2) * (m + 2);
+  const int64_t T = (int64_t)B * (a.H / m) * (a.W / m);
   float* U = (float*)ws;
-  float* V = U + (size_t)16 * N * C;
-  float* Mt = V + (size_t)16 * T * C;
-  hipLaunchKernelGGL(wino_filter_kernel, dim3(grid_of((int64_t)N * C)), dim3(256), 0, s, a.wt, a.ldw, N, C, U);
-  hipLaunchKernelGGL(wino_input_kernel, dim3(grid_of(T * (C / 4))), dim3(256), 0, s, a.src, a.lds, B, a.H, a.W, C, V);
+  float* V = U + (size_t)nxi * N * C;
+  float* Mt = V + (size_t)nxi * T * C;
+  if (m == 4) {
+    hipLaunchKernelGGL(wino4_filter_kernel, dim3(grid_of((int64_t)N * C)), dim3(256), 0, s, a.wt, a.ldw, N, C, U);
+    hipLaunchKernelGGL(wino4_input_kernel, dim3(grid_of(T * (C / 4))), dim3(256), 0, s, a.src, a.lds, B, a.H, a.W,
+                       C, V);
+  } else {
+    hipLaunchKernelGGL(wino_filter_kernel, dim3(grid_of((int64_t)N * C)), dim3(256), 0, s, a.wt, a.ldw, N, C, U);
+    hipLaunchKernelGGL(wino_input_kernel, dim3(grid_of(T * (C / 4))), dim3(256), 0, s, a.src, a.lds, B, a.H, a.W,
+                       C, V);
+  }
   int rc = launch_status("wino_transforms");
   if (rc) return rc;
-  const double flop = 2.0 * 16 * (double)T * N * C;
+  const double flop = 2.0 * nxi * (double)T * N * C;
   launch_hook("wino_gemm", 0, s, flop);
   const int v = tune_get(PIS_TUNE_WINO_TILE);
   if (v == 1 && N % 256 == 0) {
-    const dim3 grid((int)cdiv(T, 128) * (N / 256), 16);
+    const dim3 grid((int)cdiv(T, 128) * (N / 256), nxi);
     hipLaunchKernelGGL((gemm_nt_kernel<128, 256>), grid, dim3(256), 0, s, V, U, Mt, (int)T, N, C, T * C,
                        (int64_t)N * C, T * N);
     rc = launch_status("wino_gemm");
   } else if (v == 2 && N % 128 == 0) {
-    const dim3 grid((int)cdiv(T, 128) * (N / 128), 16);
+    const dim3 grid((int)cdiv(T, 128) * (N / 128), nxi);
     hipLaunchKernelGGL((gemm_nt_kernel<128, 128>), grid, dim3(256), 0, s, V, U, Mt, (int)T, N, C, T * C,
                        (int64_t)N * C, T * N);
     rc = launch_status("wino_gemm");
@@ -340,28 +599,42 @@ int launch_wino3x3(const IGemmArgs& a, int B, void* ws, hipStream_t s) {
     gm.Csrc = C; gm.ntaps = 1; gm.tap_mode = TAP_ONE; gm.wt = U; gm.ldw = C; gm.N = N;
     gm.epi = EPI_NHWC; gm.dst = Mt; gm.ldd = N; gm.flags = 0;
     gm.bs_src = T * C; gm.bs_wt = (int64_t)N * C; gm.bs_dst = T * N;
-    rc = launch_igemm(gm, s, 16);
+    rc = launch_igemm(gm, s, nxi);
   }
   launch_hook("wino_gemm", 1, s, flop);
   if (rc) return rc;
-  hipLaunchKernelGGL(wino_output_kernel, dim3(grid_of(T * (N / 4))), dim3(256), 0, s, Mt, a, B);
+  if (m == 4)
+    hipLaunchKernelGGL(wino4_output_kernel, dim3(grid_of(T * (N / 4))), dim3(256), 0, s, Mt, a, B);
+  else
+    hipLaunchKernelGGL(wino_output_kernel, dim3(grid_of(T * (N / 4))), dim3(256), 0, s, Mt, a, B);
   return launch_status("wino_output");
 }
 
-int launch_wino_input(const float* x, int ldx, int B, int H, int W, int C, float* V, hipStream_t s) {
-  const int64_t T = (int64_t)B * (H / 2) * (W / 2);
-  hipLaunchKernelGGL(wino_input_kernel, dim3(grid_of(T * (C / 4))), dim3(256), 0, s, x, ldx, B, H, W, C, V);
+int launch_wino_input(const float* x, int ldx, int B, int H, int W, int C, float* V, hipStream_t s, int m) {
+  const int64_t T = (int64_t)B * (H / m) * (W / m);
+  if (m == 4)
+    hipLaunchKernelGGL(wino4_input_kernel, dim3(grid_of(T * (C / 4))), dim3(256), 0, s, x, ldx, B, H, W, C, V);
+  else
+    hipLaunchKernelGGL(wino_input_kernel, dim3(grid_of(T * (C / 4))), dim3(256), 0, s, x, ldx, B, H, W, C, V);
   return launch_status("wino_input");
 }
 
-int launch_wino_dz(const float* dz, int ldz, int B, int H, int W, int N, float* E, hipStream_t s) {
-  const int64_t T = (int64_t)B * (H / 2) * (W / 2);
-  hipLaunchKernelGGL(wino_dz_kernel, dim3(grid_of(T * (N / 4))), dim3(256), 0, s, dz, ldz, B, H, W, N, E);
+int launch_wino_dz(const float* dz, int ldz, int B, int H, int W, int N, float* E, hipStream_t s, int m) {
+  const int64_t T = (int64_t)B * (H / m) * (W / m);
+  if (m == 4)
+    hipLaunchKernelGGL(wino4_dz_kernel, dim3(grid_of(T * (N / 4))), dim3(256), 0, s, dz, ldz, B, H, W, N, E);
+  else
+    hipLaunchKernelGGL(wino_dz_kernel, dim3(grid_of(T * (N / 4))), dim3(256), 0, s, dz, ldz, B, H, W, N, E);
   return launch_status("wino_dz");
 }
 
-int launch_wino_wgrad_out(const float* M, int N, int C, float* dw, int accumulate, hipStream_t s) {
-  hipLaunchKernelGGL(wino_wgrad_out_kernel, dim3(grid_of((int64_t)N * C)), dim3(256), 0, s, M, N, C, dw, accumulate);
+int launch_wino_wgrad_out(const float* M, int N, int C, float* dw, int accumulate, hipStream_t s, int m) {
+  if (m == 4)
+    hipLaunchKernelGGL(wino4_wgrad_out_kernel, dim3(grid_of((int64_t)N * C)), dim3(256), 0, s, M, N, C, dw,
+                       accumulate);
+  else
+    hipLaunchKernelGGL(wino_wgrad_out_kernel, dim3(grid_of((int64_t)N * C)), dim3(256), 0, s, M, N, C, dw,
+                       accumulate);
   return launch_status("wino_wgrad_out");
 }
 

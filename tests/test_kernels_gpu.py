@@ -102,7 +102,8 @@ def test_conv3x3_dgrad_wgrad(hip, B, H, W, Cin, Cout):
 
 
 # every non-default kernel variant behind pis_tune (include/pis_capi.h) stays exact too
-TUNE_VARIANTS = [(4, 1), (4, 2), (4, 3), (5, 0), (6, 2048), (3, 0), (7, 1), (8, 0), (8, 2), (10, 0), (10, 1)]
+TUNE_VARIANTS = [(4, 1), (4, 2), (4, 3), (5, 0), (6, 2048), (3, 0), (7, 1), (8, 0), (8, 2), (10, 0), (10, 1),
+                 (11, 0)]
 
 
 @pytest.mark.parametrize("key,value", TUNE_VARIANTS)
@@ -123,6 +124,7 @@ def test_conv3x3_tuned_variants(hip, key, value):
 
 
 @pytest.mark.parametrize("B,H,W,Cin,Cout,mode", [(2, 8, 8, 256, 256, 1), (1, 4, 6, 512, 256, 1),
+                                                 (2, 8, 12, 128, 64, 1), (1, 12, 8, 64, 128, 1), (1, 8, 8, 64, 64, 1),
                                                  (2, 16, 32, 64, 128, 2), (1, 6, 10, 132, 64, 2),
                                                  (1, 5, 8, 256, 256, 2), (2, 8, 16, 256, 512, 0),
                                                  (3, 10, 6, 128, 64, 2)])
@@ -141,8 +143,11 @@ def test_conv3x3_ex_winograd(hip, B, H, W, Cin, Cout, mode):
         y_ref = F.relu(F.conv2d(x, w, b, padding=1)) * scale[:, :, None, None]
         dx_ref = torch.nn.grad.conv2d_input(x.shape, w, dz, padding=1) * (x > 0) * sc_in[:, :, None, None]
         nws = hip.pis_conv3x3_ex_ws(B, H, W, Cin, Cout)
-        wino_fwd = Cin >= 256 and Cout >= 128
-        wino_dgrad = Cout >= 256 and Cin >= 128
+        if hip.pis_tune(11, -1) != 0 and H % 4 == 0 and W % 4 == 0:  # F(4x4,3x3) policy
+            wino_fwd = wino_dgrad = max(Cin, Cout) >= 128
+        else:  # F(2x2,3x3) policy
+            wino_fwd = Cin >= 256 and Cout >= 128
+            wino_dgrad = Cout >= 256 and Cin >= 128
         assert (nws > 0) == (mode == 2 and H % 2 == 0 and W % 2 == 0 or mode == 1 and (wino_fwd or wino_dgrad))
         ws = torch.empty(max(nws, 4) // 4 + 1, device="cuda")
         xd, wd, bd, sd, dzd, sid = (nhwc(x).cuda(), krsc(w).cuda(), b.cuda(), scale.cuda(), nhwc(dz).cuda(),

@@ -75,8 +75,14 @@ def main():
         ws = torch.empty(nws // 4 + 1, device=dev)
         dw = torch.empty(cout * 9 * cin, device=dev)
         db = torch.empty(cout, device=dev)
-        prev8 = lib.pis_tune(8, 2)  # workspace for the Winograd path whichever policy is timed
-        nwx = lib.pis_conv3x3_ex_ws(B, H, H, cin, cout)
+        prev8 = lib.pis_tune(8, 2)  # workspace for the Winograd path whichever policy / tile is timed
+        nwx = 0
+        for v in variants:
+            pv = lib.pis_tune(args.key, v)
+            if args.key != 8:
+                nwx = max(nwx, lib.pis_conv3x3_ex_ws(B, H, H, cin, cout))
+            lib.pis_tune(args.key, pv)
+        nwx = max(nwx, lib.pis_conv3x3_ex_ws(B, H, H, cin, cout))
         lib.pis_tune(8, prev8)
         wsx = torch.empty(max(nwx, 4) // 4 + 1, device=dev)
         flops = 2.0 * B * H * H * cout * cin * 9
