@@ -58,9 +58,9 @@ def conv_flops_per_image(H: int, W: int, c: int = 64) -> float:
 
 # The dominant kernel of the step (profiles/r1_*_kernel_stats.csv): the batched fp32 MFMA GEMM
 # of the Winograd 3x3 convs (forward + input gradient), launched as "wino_gemm" by the C-ABI
-# (csrc/winograd.hip) and named gemm_nt_kernel<128, 128> by rocprofv3.
+# (csrc/winograd.hip) and named gemm_nt_kernel<128, 128> / <128, 64> by rocprofv3.
 DOMINANT = "wino_gemm"
-DOMINANT_KERNEL = "gemm_nt_kernel<128, 128>"
+DOMINANT_KERNEL = "gemm_nt_kernel<"
 
 
 def loss_call_bytes(name, a):
@@ -244,7 +244,7 @@ def main():
             "vs_baseline": None, "dtype": "fp32", "data": "synthetic",
             "config": {"workload": "C2: UNet(1,1,64) bs=8/GPU 512x512 Stage-II (lambda_RD=lambda_PF=1e-4, D=5, a=0.5, eps=0.05) AdamW lr=1e-5",
                        "global_batch": B * world, "image_size": [H, W], "parallelism": f"dp{world}"},
-            "roofline": {"bound": "mfma", "kernel": f"{DOMINANT_KERNEL} ({DOMINANT}: Winograd F(2x2,3x3) batched GEMMs)",
+            "roofline": {"bound": "mfma", "kernel": f"gemm_nt_kernel<128, 128|64> ({DOMINANT}: the 36 batched GEMMs of Winograd F(4x4,3x3) fwd/dgrad)",
                          "achieved": achieved, "peak": peak,
                          "unit": "TFLOP/s", "frac": achieved / peak, "traffic": traffic,
                          "launches_per_step": n_launch, "avg_launch_ms": ms_per_launch,

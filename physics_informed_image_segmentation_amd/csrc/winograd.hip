@@ -593,6 +593,11 @@ int launch_wino3x3(const IGemmArgs& a, int B, void* ws, hipStream_t s) {
     hipLaunchKernelGGL((gemm_nt_kernel<128, 128>), grid, dim3(256), 0, s, V, U, Mt, (int)T, N, C, T * C,
                        (int64_t)N * C, T * N);
     rc = launch_status("wino_gemm");
+  } else if (v == 2 && N % 64 == 0) {
+    const dim3 grid((int)cdiv(T, 128) * (N / 64), nxi);
+    hipLaunchKernelGGL((gemm_nt_kernel<128, 64>), grid, dim3(256), 0, s, V, U, Mt, (int)T, N, C, T * C,
+                       (int64_t)N * C, T * N);
+    rc = launch_status("wino_gemm");
   } else {
     IGemmArgs gm{};
     gm.src = V; gm.lds = C; gm.Hs = 1; gm.Ws = (int)T; gm.H = 1; gm.W = (int)T; gm.M = (int)T;

@@ -25,7 +25,7 @@ def per_kernel(path, counter):
     return {k: (sum(v) / len(v), len(v)) for k, v in acc.items()}
 
 
-def main(fetch_csv, write_csv, out_json, dominant="gemm_nt_kernel<128, 128>"):
+def main(fetch_csv, write_csv, out_json, dominant="gemm_nt_kernel<"):
     f = per_kernel(fetch_csv, "FETCH_SIZE")
     w = per_kernel(write_csv, "WRITE_SIZE")
     table = {}
@@ -37,8 +37,11 @@ def main(fetch_csv, write_csv, out_json, dominant="gemm_nt_kernel<128, 128>"):
                     "hbm_bytes_per_launch": 2.0 * fk * 1024 + wk * 1024,
                     "launches": max(f.get(k, (0, 0))[1], w.get(k, (0, 0))[1])}
     dom = [k for k in table if dominant in k]
-    out = {"dominant_kernel": dom[0] if dom else None,
-           "hbm_bytes_per_launch": table[dom[0]]["hbm_bytes_per_launch"] if dom else None,
+    # every instantiation of the dominant kernel, launch-weighted
+    nl = sum(table[k]["launches"] for k in dom)
+    per_launch = sum(table[k]["hbm_bytes_per_launch"] * table[k]["launches"] for k in dom) / nl if nl else None
+    out = {"dominant_kernel": " + ".join(dom) if dom else None,
+           "hbm_bytes_per_launch": per_launch,
            "note": "per-launch average over every launch of the kernel in the profiled run; "
                    "read bytes = 2 x FETCH_SIZE x 1024 (gfx950 correction), write = WRITE_SIZE x 1024",
            "kernels": table}
