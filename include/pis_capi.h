@@ -154,10 +154,12 @@ typedef struct pis_loss_params {
   float D, a;            /* diffusion coefficient, reaction threshold   */
   float eps;             /* phase-field interface width                */
   float thr;             /* metric threshold (0.5, strict '>')         */
-  int flags;             /* PIS_LOSS_ALL_TERMS: compute RD/PF even at weight 0 */
+  int flags;             /* PIS_LOSS_ALL_TERMS | PIS_LOSS_NO_REACTION                  */
 } pis_loss_params;
 #define PIS_LOSS_ALL_TERMS 1
 #define PIS_LOSS_CHAIN_SIGMOID 2 /* bwd writes dL/dz = dL/dp * p (1 - p) */
+#define PIS_LOSS_NO_REACTION 4   /* residual r = D Lap(u) only (src/ablation.py:53-86,107-154
+                                    DiffusionOnlyLoss, use_reaction_term=False)           */
 /* out_terms: [0] total [1] dice_loss [2] bce_loss [3] rd_loss [4] pf_loss [5] I=sum p t
  *            [6] P=sum p [7] T=sum t.
  * counts: [B][3] = exact (I_hat, P_hat, T) of the thresholded prediction per sample.

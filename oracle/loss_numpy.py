@@ -69,7 +69,8 @@ def stencil_adjoint(g, k):
     return _pad_reflect_adjoint(_correlate_adjoint(g, k))
 
 
-def loss_forward(p, t, dice_w=0.5, bce_w=0.5, rd_w=0.0, pf_w=0.0, smooth=1e-6, D=1.0, a=0.5, eps=0.05):
+def loss_forward(p, t, dice_w=0.5, bce_w=0.5, rd_w=0.0, pf_w=0.0, smooth=1e-6, D=1.0, a=0.5, eps=0.05,
+                 reaction=True):
     """p, t: arrays (B, H, W) or (B, 1, H, W). Returns dict of float64 terms and sums."""
     p = np.asarray(p, dtype=np.float64).reshape(p.shape[0], p.shape[-2], p.shape[-1])
     t = np.asarray(t, dtype=np.float64).reshape(p.shape)
@@ -80,7 +81,8 @@ def loss_forward(p, t, dice_w=0.5, bce_w=0.5, rd_w=0.0, pf_w=0.0, smooth=1e-6, D
                         - t * np.maximum(np.log(p), LOG_CLAMP)))
     out = {"I": I, "P": P, "T": T, "dice_loss": dice, "bce_loss": bce}
     total = dice_w * dice + bce_w * bce
-    r = D * stencil(p, _LAP) + p * (1.0 - p) * (p - a)
+    rx = 1.0 if reaction else 0.0  # src/ablation.py:75-86 (use_reaction_term=False: f(u) = 0)
+    r = D * stencil(p, _LAP) + rx * p * (1.0 - p) * (p - a)
     out["rd"] = float(np.mean(r * r))
     gx, gy = stencil(p, _GX), stencil(p, _GY)
     out["pf"] = float(np.mean(0.5 * eps * (gx * gx + gy * gy) + (p * p) * (1.0 - p) ** 2 / eps))
@@ -95,7 +97,7 @@ def loss_forward(p, t, dice_w=0.5, bce_w=0.5, rd_w=0.0, pf_w=0.0, smooth=1e-6, D
 
 
 def loss_backward(p, t, dice_w=0.5, bce_w=0.5, rd_w=0.0, pf_w=0.0, smooth=1e-6, D=1.0, a=0.5, eps=0.05,
-                  grad_out=1.0, chain_sigmoid=False):
+                  grad_out=1.0, chain_sigmoid=False, reaction=True):
     """dL/dp (or dL/dz through the sigmoid when chain_sigmoid) — SURVEY §8(a) A6-A8."""
     shape = p.shape
     p = np.asarray(p, dtype=np.float64).reshape(p.shape[0], p.shape[-2], p.shape[-1])
@@ -106,8 +108,9 @@ def loss_backward(p, t, dice_w=0.5, bce_w=0.5, rd_w=0.0, pf_w=0.0, smooth=1e-6, 
     g = dice_w * (-(2.0 * t * S - (2.0 * I + smooth)) / (S * S))
     g += bce_w * (p - t) / np.maximum(p * (1.0 - p), BCE_EPS) / n
     if rd_w > 0:
-        r = D * stencil(p, _LAP) + p * (1.0 - p) * (p - a)
-        fprime = -3.0 * p * p + 2.0 * (1.0 + a) * p - a
+        rx = 1.0 if reaction else 0.0
+        r = D * stencil(p, _LAP) + rx * p * (1.0 - p) * (p - a)
+        fprime = rx * (-3.0 * p * p + 2.0 * (1.0 + a) * p - a)
         g += rd_w * (2.0 / n) * (D * stencil_adjoint(r, _LAP) + r * fprime)
     if pf_w > 0:
         gx, gy = stencil(p, _GX), stencil(p, _GY)

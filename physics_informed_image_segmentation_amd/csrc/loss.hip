@@ -86,6 +86,7 @@ struct LossArgs {
   const float* t;
   int B, H, W;
   float dice_w, bce_w, rd_w, pf_w, smooth, D, a, eps, thr;
+  float rx;  // 1, or 0 for the diffusion-only residual (PIS_LOSS_NO_REACTION)
   int tiles_x, tiles_y;
   float* fpart;  // [nblk][6]: I, P, T, bce_sum, rd_sum, pf_sum
   int* ipart;    // [nblk][3]: I_hat, P_hat, T_hat
@@ -156,7 +157,7 @@ __global__ __launch_bounds__(256) void loss_fwd_kernel(LossArgs g) {
         const float qq = fmaf(-p, p, p);  // p (1 - p)
         if (RD) {
           const float lap = (uu + ud) + (ul + ur) - 4.f * p;
-          const float rr = fmaf(g.D, lap, qq * (p - g.a));
+          const float rr = fmaf(g.D, lap, g.rx * qq * (p - g.a));
           s_rd = fmaf(rr, rr, s_rd);
         }
         if (PF) {
@@ -270,6 +271,7 @@ struct LossBwdArgs {
   const float* t;
   int B, H, W;
   float dice_w, bce_w, rd_w, pf_w, smooth, D, a, eps;
+  float rx;  // 1, or 0 for the diffusion-only residual (PIS_LOSS_NO_REACTION)
   const float* terms;
   const float* grad_out;
   float* dst;
@@ -329,7 +331,7 @@ __global__ __launch_bounds__(256) void loss_bwd_kernel(LossBwdArgs g) {
           const float ul = i == 0 ? lft : c[i - 1], ur = i == 3 ? rgt : c[i + 1];
           const float lap = (up[i] + dn[i]) + (ul + ur) - 4.f * c0;
           const bool ok = yy >= 0 && yy < H && x0 + 4 * q + i < W;
-          out[i] = ok ? fmaf(g.D, lap, fmaf(-c0, c0, c0) * (c0 - g.a)) : 0.f;
+          out[i] = ok ? fmaf(g.D, lap, g.rx * fmaf(-c0, c0, c0) * (c0 - g.a)) : 0.f;
         }
         *(f32x4*)(sr + rr * LT_S + 4 + 4 * q) = out;
       } else {  // edge columns x0-1 and x0+LT_X
@@ -340,7 +342,7 @@ __global__ __launch_bounds__(256) void loss_bwd_kernel(LossBwdArgs g) {
           const float* sc = su + (rr + 1) * LT_S + 4 + cc;
           const float c0 = sc[0];
           const float lap = (sc[-LT_S] + sc[LT_S]) + (sc[-1] + sc[1]) - 4.f * c0;
-          r = fmaf(g.D, lap, fmaf(-c0, c0, c0) * (c0 - g.a));
+          r = fmaf(g.D, lap, g.rx * fmaf(-c0, c0, c0) * (c0 - g.a));
         }
         sr[rr * LT_S + 4 + cc] = r;
       }
@@ -392,7 +394,7 @@ __global__ __launch_bounds__(256) void loss_bwd_kernel(LossBwdArgs g) {
         float adj = (ru[i] + rd[i]) + (rl_ + rr_) - 4.f * rk;
         adj += (y == 1 ? ru[i] : 0.f) + (y == H - 2 ? rd[i] : 0.f);
         adj += (x == 1 ? rl_ : 0.f) + (x == W - 2 ? rr_ : 0.f);
-        const float fp = fmaf(p, fmaf(-3.f, p, fa), -g.a);
+        const float fp = g.rx * fmaf(p, fmaf(-3.f, p, fa), -g.a);
         grad = fmaf(cRD, adj, fmaf(cR * rk, fp, grad));
       }
       if constexpr (PF) {
@@ -434,6 +436,7 @@ struct HeadLossArgs {
   float* du_out;          // optional: dL/du (before the sigmoid chain) for autograd
   int B, H, W, C, R;
   float dice_w, bce_w, rd_w, pf_w, smooth, D, a, eps;
+  float rx;  // 1, or 0 for the diffusion-only residual (PIS_LOSS_NO_REACTION)
   const float* terms;
   const float* grad_out;
   float* dx; int lddx;
@@ -480,7 +483,7 @@ __global__ __launch_bounds__(256) void head_loss_bwd_kernel(HeadLossArgs g) {
         const float* sc = su + (rr + 1) * SW + cc + 2;
         const float c0 = sc[0];
         const float lap = (sc[-SW] + sc[SW]) + (sc[-1] + sc[1]) - 4.f * c0;
-        r = fmaf(g.D, lap, fmaf(-c0, c0, c0) * (c0 - g.a));
+        r = fmaf(g.D, lap, g.rx * fmaf(-c0, c0, c0) * (c0 - g.a));
       }
       sr[k] = r;
     }
@@ -499,7 +502,7 @@ __global__ __launch_bounds__(256) void head_loss_bwd_kernel(HeadLossArgs g) {
       float adj = (ru + rd) + (rl + rrt) - 4.f * rk;
       adj += (y == 1 ? ru : 0.f) + (y == H - 2 ? rd : 0.f);
       adj += (x == 1 ? rl : 0.f) + (x == W - 2 ? rrt : 0.f);
-      const float fp = fmaf(p, fmaf(-3.f, p, fa), -g.a);
+      const float fp = g.rx * fmaf(p, fmaf(-3.f, p, fa), -g.a);
       grad = fmaf(cRD, adj, fmaf(cR * rk, fp, grad));
     }
     if constexpr (PF) {
@@ -602,7 +605,8 @@ extern "C" int pis_loss_fwd(const float* p, const float* t, int B, int H, int W,
   LossArgs g{};
   g.p = p; g.t = t; g.B = B; g.H = H; g.W = W;
   g.dice_w = prm->dice_w; g.bce_w = prm->bce_w; g.rd_w = prm->rd_w; g.pf_w = prm->pf_w;
-  g.smooth = prm->smooth; g.D = prm->D; g.a = prm->a; g.eps = prm->eps; g.thr = prm->thr;
+  g.smooth = prm->smooth; g.D = prm->D; g.a = prm->a; g.eps = prm->eps;
+  g.rx = (prm->flags & PIS_LOSS_NO_REACTION) ? 0.f : 1.f; g.thr = prm->thr;
   loss_plan(H, W, g.tiles_x, g.tiles_y);
   g.fpart = (float*)ws;
   g.ipart = (int*)((char*)ws + (size_t)B * g.tiles_x * g.tiles_y * 6 * sizeof(float));
@@ -629,6 +633,7 @@ extern "C" int pis_loss_bwd(const float* p, const float* t, int B, int H, int W,
   g.p = p; g.t = t; g.B = B; g.H = H; g.W = W;
   g.dice_w = prm->dice_w; g.bce_w = prm->bce_w; g.rd_w = prm->rd_w; g.pf_w = prm->pf_w;
   g.smooth = prm->smooth; g.D = prm->D; g.a = prm->a; g.eps = prm->eps;
+  g.rx = (prm->flags & PIS_LOSS_NO_REACTION) ? 0.f : 1.f;
   g.terms = terms; g.grad_out = grad_out; g.dst = dst; g.chain = (flags & PIS_LOSS_CHAIN_SIGMOID) ? 1 : 0;
   int tx, ty;
   loss_plan(H, W, tx, ty);
@@ -681,6 +686,7 @@ extern "C" int pis_head_loss_bwd(const float* x, int ldx, const float* w, const 
   g.B = B; g.H = H; g.W = W; g.C = C; g.R = head_loss_rows(H, W);
   g.dice_w = prm->dice_w; g.bce_w = prm->bce_w; g.rd_w = prm->rd_w; g.pf_w = prm->pf_w;
   g.smooth = prm->smooth; g.D = prm->D; g.a = prm->a; g.eps = prm->eps;
+  g.rx = (prm->flags & PIS_LOSS_NO_REACTION) ? 0.f : 1.f;
   g.terms = terms; g.grad_out = grad_out; g.dx = dx; g.lddx = lddx;
   const dim3 grid((H + g.R - 1) / g.R, B);
   g.part = (float*)ws;

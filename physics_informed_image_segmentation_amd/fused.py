@@ -16,7 +16,7 @@ from typing import Dict, Tuple
 import torch
 
 from . import _hip
-from ._hip import LossParams, PIS_LOSS_ALL_TERMS, call
+from ._hip import LossParams, PIS_LOSS_ALL_TERMS, PIS_LOSS_NO_REACTION, call
 
 
 @dataclass(frozen=True)
@@ -31,10 +31,12 @@ class LossConfig:
     eps: float = 0.05
     thr: float = 0.5
     all_terms: bool = False
+    reaction: bool = True  # False: diffusion-only residual (src/ablation.py:53-86)
 
     def params(self) -> LossParams:
+        flags = (PIS_LOSS_ALL_TERMS if self.all_terms else 0) | (0 if self.reaction else PIS_LOSS_NO_REACTION)
         return LossParams(self.dice_w, self.bce_w, self.rd_w, self.pf_w, self.smooth, self.D, self.a,
-                          self.eps, self.thr, PIS_LOSS_ALL_TERMS if self.all_terms else 0)
+                          self.eps, self.thr, flags)
 
 
 _WS: Dict[Tuple, torch.Tensor] = {}

@@ -101,6 +101,7 @@ class _Meter:
         self.terms = torch.zeros(5, dtype=torch.float64, device=device)
         self.scores = torch.zeros(2, dtype=torch.float64, device=device)
         self.batch_dice = torch.zeros(1, dtype=torch.float64, device=device)
+        self.bf1 = torch.zeros(1, dtype=torch.float64, device=device)  # host-computed boundary F1 sums
         self.batches = 0
         self.samples = 0
 
@@ -114,12 +115,13 @@ class _Meter:
         self.batches += 1
 
     def reduce(self) -> Tuple[List[float], List[float], float, int, int]:
-        packed = torch.cat([self.terms, self.scores, self.batch_dice,
+        packed = torch.cat([self.terms, self.scores, self.batch_dice, self.bf1,
                             torch.tensor([self.batches, self.samples], dtype=torch.float64,
                                          device=self.terms.device)])
         packed = allreduce_scalars(packed)
         vals = packed.tolist()  # the epoch's single host synchronisation
-        return vals[0:5], vals[5:7], vals[7], int(vals[8]), int(vals[9])
+        self.bf1_total = vals[8]
+        return vals[0:5], vals[5:7], vals[7], int(vals[9]), int(vals[10])
 
 
 def _results(meter: _Meter, criterion, return_components: bool, compute_metrics: bool, val: bool):
@@ -140,13 +142,22 @@ def _results(meter: _Meter, criterion, return_components: bool, compute_metrics:
         if not val:
             out["dice_score"] = scores[0] / ns if ns else 0.0
         out["iou_score"] = scores[1] / ns if ns else 0.0
-        out["boundary_f1_score"] = 0.0
+        # 0.0 unless boundary_metrics=True (host-side, off the hot path): the reference's value
+        # without scores
+        out["boundary_f1_score"] = meter.bf1_total / ns if ns else 0.0
     return out
 
 
+def _boundary_sum(outputs, masks) -> float:
+    from .evaluate import compute_boundary_f1_batch
+    return float(compute_boundary_f1_batch(outputs, masks, threshold=0.5, tolerance=2).sum())
+
+
 def train_epoch(model, dataloader, criterion, optimizer, device, return_components: bool = False,
-                compute_metrics: bool = True) -> Dict[str, float]:
-    """One pass over ``dataloader`` (src/train.py:84-185); same result keys."""
+                compute_metrics: bool = True, boundary_metrics: bool = False) -> Dict[str, float]:
+    """One pass over ``dataloader`` (src/train.py:84-185); same result keys. The reference
+    computes boundary F1 on the host every step (src/train.py:152-160); here that is opt-in
+    (``boundary_metrics``, cv2-free, evaluate.py) so the step stays device-only."""
     model.train()
     meter = _Meter(device)
     for images, masks in dataloader:
@@ -157,6 +168,8 @@ def train_epoch(model, dataloader, criterion, optimizer, device, return_componen
         loss = criterion(outputs, masks)
         terms, scores = _criterion_terms(criterion, outputs, masks)
         meter.add(terms, scores if compute_metrics else None)
+        if compute_metrics and boundary_metrics:
+            meter.bf1 += _boundary_sum(outputs, masks)
         loss.backward()
         optimizer.step()
     return _results(meter, criterion, return_components, compute_metrics, val=False)
@@ -164,7 +177,7 @@ def train_epoch(model, dataloader, criterion, optimizer, device, return_componen
 
 @torch.no_grad()
 def validate(model, dataloader, criterion, device, return_components: bool = False,
-             compute_metrics: bool = True) -> Dict[str, float]:
+             compute_metrics: bool = True, boundary_metrics: bool = False) -> Dict[str, float]:
     """Eval-mode pass (src/train.py:188-286); ``dice_score`` is the mean of
     whole-batch thresholded Dice, as in the reference."""
     model.eval()
@@ -183,6 +196,8 @@ def validate(model, dataloader, criterion, device, return_components: bool = Fal
         s = criterion.smooth if hasattr(criterion, "smooth") else 1e-6
         batch_dice = (2.0 * tot[0] + 1e-6) / (tot[1] + tot[2] + 1e-6)
         meter.add(terms, scores if compute_metrics else None, batch_dice)
+        if compute_metrics and boundary_metrics:
+            meter.bf1 += _boundary_sum(outputs, masks)
     return _results(meter, criterion, return_components, compute_metrics, val=True)
 
 

@@ -1,0 +1,139 @@
+"""Boundary metrics (cv2-free restatement, evaluate.py) on shapes with known outer
+contours, the ablation study definitions against run_ablation.py:23-294, the diffusion-only
+loss against the float64 oracle, and (GPU) one tiny ablation variant end to end.
+
+Boundary-F1 / Hausdorff parity against OpenCV itself is unpinned (cv2 absent); these
+hand-drawn cases pin the RETR_EXTERNAL outer-contour semantics (src/evaluate.py:102-120)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import loss_numpy as ln
+
+
+def _ring(n):
+    b = np.zeros((n, n), np.float32)
+    b[0, :] = b[-1, :] = b[:, 0] = b[:, -1] = 1
+    return b
+
+
+def test_outer_contour_of_square_ring_and_border():
+    from physics_informed_image_segmentation_amd.evaluate import extract_boundaries
+    m = np.zeros((10, 10), np.float32)
+    m[2:7, 2:7] = 1
+    expect = np.zeros_like(m)
+    expect[2:7, 2:7] = _ring(5)
+    np.testing.assert_array_equal(extract_boundaries(m), expect)
+    # a component touching the image border: its contour runs along the border pixels
+    np.testing.assert_array_equal(extract_boundaries(np.ones((6, 6), np.float32)), _ring(6))
+    # one isolated pixel is its own contour; empty mask has none
+    d = np.zeros((5, 5), np.float32)
+    d[2, 2] = 1
+    np.testing.assert_array_equal(extract_boundaries(d), d)
+    assert extract_boundaries(np.zeros((4, 4))).sum() == 0
+
+
+def test_holes_and_nested_components_are_not_external():
+    from physics_informed_image_segmentation_amd.evaluate import extract_boundaries
+    m = np.zeros((11, 11), np.float32)
+    m[1:10, 1:10] = 1
+    m[3:8, 3:8] = 0   # hole: its border is not an external contour
+    m[5, 5] = 1       # component nested in the hole: dropped by RETR_EXTERNAL
+    expect = np.zeros_like(m)
+    expect[1:10, 1:10] = _ring(9)
+    np.testing.assert_array_equal(extract_boundaries(m), expect)
+    # diagonal staircase: pixels touching the background only diagonally are interior
+    s = np.zeros((6, 6), np.float32)
+    s[1:5, 1:5] = 1
+    s[1, 1] = 0
+    b = extract_boundaries(s)
+    assert b[2, 2] == 0 and b[1, 2] == 1 and b[2, 1] == 1
+
+
+def test_boundary_f1_and_hausdorff():
+    from physics_informed_image_segmentation_amd.evaluate import compute_boundary_f1, compute_hausdorff_distance
+    t = torch.zeros(1, 1, 32, 32)
+    t[..., 8:20, 8:20] = 1
+    p = t * 0.9 + 0.05
+    assert compute_boundary_f1(p, t).item() == pytest.approx(1.0, abs=1e-6)
+    shifted = torch.roll(p, 2, dims=-1)  # 2 px is inside the tolerance
+    assert compute_boundary_f1(shifted, t).item() == pytest.approx(1.0, abs=1e-6)
+    far = torch.roll(p, 3, dims=-1)      # 3 px: only the horizontal edges still match
+    f1 = compute_boundary_f1(far, t).item()
+    assert 0.3 < f1 < 0.9
+    assert compute_hausdorff_distance(far, t) == pytest.approx(3.0)
+    assert compute_hausdorff_distance(torch.zeros(1, 1, 8, 8), t[..., :8, :8]) == float("inf")
+
+
+def test_ablation_definitions_match_reference():
+    from physics_informed_image_segmentation_amd import ablation as ab
+    r1 = ab.define_ablation_r1()
+    assert [c.name for c in r1] == ["R1.0 Baseline", "R1.1 RD Only", "R1.2 Phase-Field Only", "R1.3 RD + Phase-Field"]
+    assert [(c.use_pde, c.pde_weight, c.phase_field_weight, c.use_two_stage) for c in r1] == [
+        (False, 0.0, 0.0, False), (True, 1e-4, 0.0, True), (True, 0.0, 1e-4, True), (True, 1e-4, 1e-4, True)]
+    s2 = ab.define_ablation_s2()
+    assert [c.diffusion_coeff for c in s2] == [0.5, 1.0, 2.0, 5.0, 10.0, 100.0]
+    assert [c.name for c in s2][-1] == "S2.5 D=100" and s2[0].name == "S2.0 D=0.5"
+    assert all(c.pde_weight == 1e-3 and c.phase_field_weight == 0.0 and c.train_fraction == 0.1 for c in s2)
+    assert [c.train_fraction for c in ab.define_ablation_r2()] == [0.1, 0.25, 0.5, 0.75, 1.0]
+    assert [c.reaction_threshold for c in ab.define_ablation_s1()] == [0.3, 0.4, 0.5, 0.6, 0.7]
+    assert [c.epsilon for c in ab.define_ablation_s3()] == [0.001, 0.01, 0.05, 0.1, 0.2]
+    assert ab.define_ablation_s3()[0].name == "S3.0 ε=0.001"
+    assert all(c.train_fraction == 0.1 for c in ab.define_ablation_r3())
+    assert isinstance(ab.create_ablation_loss(r1[0]), ab.DiceBCELoss)
+    assert isinstance(ab.create_ablation_loss(r1[3]), ab.DiceBCEPDELoss)
+    off = ab.AblationConfig(name="A3", description="", use_pde=True, use_reaction_term=False)
+    assert isinstance(ab.create_ablation_loss(off), ab.DiffusionOnlyLoss)
+
+
+def test_run_ablation_cli_flags():
+    import run_ablation
+    with pytest.raises(SystemExit):
+        run_ablation.main(["--ablation", "R9"])
+
+
+def test_diffusion_only_oracle_is_pure_diffusion():
+    g = np.random.default_rng(3)
+    p = 0.05 + 0.9 * g.random((2, 9, 12))
+    t = (g.random((2, 9, 12)) > 0.6).astype(np.float64)
+    f = ln.loss_forward(p, t, rd_w=1e-3, D=2.0, reaction=False)
+    lap = ln.stencil(p, ln._LAP)
+    assert f["rd"] == pytest.approx(float(np.mean((2.0 * lap) ** 2)), rel=1e-12)
+    # backward of the diffusion-only term is the adjoint stencil of the residual, nothing else
+    g0 = ln.loss_backward(p, t, rd_w=0.0)
+    g1 = ln.loss_backward(p, t, rd_w=1e-3, D=2.0, reaction=False)
+    adj = 1e-3 * (2.0 / p.size) * 2.0 * ln.stencil_adjoint(2.0 * lap, ln._LAP)
+    np.testing.assert_allclose(g1 - g0, adj, rtol=1e-10, atol=1e-16)
+
+
+@pytest.mark.gpu
+def test_diffusion_only_loss_hip(hip):
+    from physics_informed_image_segmentation_amd import ablation as ab
+    cfg = ab.AblationConfig(name="A3", description="", use_pde=True, pde_weight=0.3, diffusion_coeff=2.0,
+                            use_reaction_term=False)
+    crit = ab.create_ablation_loss(cfg)
+    g = torch.Generator().manual_seed(4)
+    p = (0.05 + 0.9 * torch.rand(2, 1, 40, 33, generator=g)).cuda().requires_grad_(True)
+    t = (torch.rand(2, 1, 40, 33, generator=g) > 0.6).float().cuda()
+    loss = crit(p, t)
+    loss.backward()
+    f = ln.loss_forward(p.detach().cpu().numpy(), t.cpu().numpy(), rd_w=0.3, D=2.0, reaction=False)
+    assert loss.item() == pytest.approx(f["loss"], rel=1e-5)
+    gref = ln.loss_backward(p.detach().cpu().numpy(), t.cpu().numpy(), rd_w=0.3, D=2.0, reaction=False)
+    gd = p.grad.cpu().double().numpy()
+    assert np.abs(gd - gref).max() <= 1e-5 * np.abs(gref).max()
+    reg = ab.PDERegularizationAblation(2.0, 0.5, use_reaction_term=False)
+    assert reg.compute_loss(p.detach()).item() == pytest.approx(f["rd"], rel=1e-5)
+
+
+@pytest.mark.gpu
+def test_ablation_variant_end_to_end(hip, tmp_path):
+    from physics_informed_image_segmentation_amd import ablation as ab
+    data = ab.DataSpec(synthetic=(4, 2, 2, 32, 32))
+    v = ab.define_ablation_r1()[3]
+    res = ab.run_ablation_study("R1", [v], data, torch.device("cuda"), batch_size=2, stage1_epochs=1,
+                                stage2_epochs=1, output_dir=tmp_path, num_workers=0)
+    r = res["results"][0]
+    assert r["stage1_best_epoch"] in (0, 1) and len(r["in_dist_metrics"]["dice_scores"]) == 2
+    assert set(r["in_dist_summary"]) == {"dice_scores", "iou_scores", "boundary_f1_scores", "hausdorff_distances"}
+    assert (tmp_path / res["folder"]).exists() and open(res["summary_csv"]).read().count("\n") == 3
