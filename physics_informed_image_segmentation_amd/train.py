@@ -30,7 +30,7 @@ import torch
 from torch.utils.data import DataLoader, Subset
 
 from . import _hip
-from .dataset import CellSegmentationDataset, SyntheticDiscDataset
+from .dataset import CellSegmentationDataset, DeviceDiscLoader, SyntheticDiscDataset
 from .distributed import GradBucketer, allreduce_scalars, broadcast_parameters, init_from_env
 from .fused import LossConfig, loss_forward
 from .loss import DiceBCELoss, DiceBCEPDELoss
@@ -308,11 +308,12 @@ def train(use_two_stage: bool = True, pde_weight: float = 1e-4, diffusion_coeff:
           batch_size: int = 8, learning_rate: float = 1e-4, stage1_epochs: int = 50, stage2_epochs: int = 50,
           early_stopping_patience: int = 10, train_fraction: Optional[float] = None, seed: int = 42,
           base_dir: Optional[str] = None, synthetic: Optional[Tuple[int, int, int, int]] = None,
-          num_workers: int = 2):
+          num_workers: int = 2, device_data: bool = True):
     """Two-stage training (src/train.py:531-915). Extra, build-only arguments:
     ``base_dir`` (where images/, output/, models/ live; default: cwd) and
     ``synthetic=(n_train, n_val, H, W)`` to train on the SURVEY §8(c) disc
-    generator when the cell dataset is not present."""
+    generator when the cell dataset is not present — rasterised on the GPU
+    (``DeviceDiscLoader``, sharded like DistributedSampler) unless ``device_data=False``."""
     rank, local_rank, world = init_from_env()
     if not torch.cuda.is_available():
         raise _hip.HipError("train(): the MI355X path needs a GPU (no CPU fallback in this build)")
@@ -346,7 +347,14 @@ def train(use_two_stage: bool = True, pde_weight: float = 1e-4, diffusion_coeff:
         say(f"Using {train_fraction * 100:.1f}% of training data ({int(len(train_ds) * train_fraction)} samples)")
         train_ds = create_subset_dataset(train_ds, train_fraction)
     frac = f"_frac{train_fraction:.2f}" if train_fraction is not None else ""
-    train_loader, val_loader = _loaders(train_ds, val_ds, batch_size, world, rank, num_workers)
+    if synthetic is not None and device_data:
+        subset = train_ds.indices if isinstance(train_ds, Subset) else None
+        train_loader = DeviceDiscLoader(n_tr, batch_size, (H, W), seed=seed, shuffle=True, rank=rank, world=world,
+                                        device=device, subset=subset)
+        val_loader = DeviceDiscLoader(n_va, batch_size, (H, W), seed=seed + 1, shuffle=False, rank=rank,
+                                      world=world, device=device)
+    else:
+        train_loader, val_loader = _loaders(train_ds, val_ds, batch_size, world, rank, num_workers)
     say(f"Training samples: {len(train_ds)}")
     say(f"Validation samples: {len(val_ds)}")
     say(f"Batch size: {batch_size} per GPU")
