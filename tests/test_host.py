@@ -147,3 +147,25 @@ def test_synthetic_dataset_deterministic():
     assert torch.equal(x1, x2) and torch.equal(m1, m2)
     assert x1.shape == (1, 32, 48) and set(m1.unique().tolist()) <= {0.0, 1.0}
     assert 0.0 <= x1.min() and x1.max() <= 1.0
+
+
+def test_checkpoint_roundtrip_with_reference_layout(tmp_path):
+    """.pth files are interchangeable with the reference's
+    (src/train.py:688-690,763-764 torch.save(state_dict); src/evaluate_comparison.py:61-76
+    load_state_dict(torch.load(...))), loadable with weights_only=True."""
+    from physics_informed_image_segmentation_amd import UNet
+    torch.manual_seed(3)
+    net = UNet(1, 1, 64)
+    torch.save(net.state_dict(), tmp_path / "ours.pth")
+    sd = torch.load(tmp_path / "ours.pth", weights_only=True)
+    ref = rt.UNetRef(1, 1, 64)
+    ref.load_state_dict(sd)
+    for (k, a), (k2, b) in zip(net.state_dict().items(), ref.state_dict().items()):
+        assert k == k2 and torch.equal(a, b), k
+    torch.manual_seed(11)
+    ref2 = rt.UNetRef(1, 1, 64)
+    torch.save(ref2.state_dict(), tmp_path / "ref.pth")
+    net.load_state_dict(torch.load(tmp_path / "ref.pth", weights_only=True))
+    for (k, a), (_, b) in zip(net.state_dict().items(), ref2.state_dict().items()):
+        assert torch.equal(a, b), k
+    assert (tmp_path / "ours.pth").stat().st_size < 1.05 * (tmp_path / "ref.pth").stat().st_size
