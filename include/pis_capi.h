@@ -100,6 +100,18 @@ int pis_conv3x3_dgrad_ex(const float* dz, int ldz, const float* w_flip, const fl
                          int Cout, int flags, void* ws, size_t ws_bytes, pis_stream_t stream);
 /* wgrad: dw[n][r][s][c] (+)= sum_p dz[p][n] x[p+(r-1,s-1)][c];  db[n] (+)= sum_p dz[p][n]
  *        (db may be NULL). flags: PIS_ACCUMULATE. */
+/* Kept input transform (training forward -> weight gradient of the same layer): where the
+ * forward runs Winograd F(4x4,3x3) and the weight gradient F(3x3,4x4), both transform the
+ * same input x with the same B^T; pis_conv3x3_fwd_keep leaves that transform in `keep`
+ * (pis_conv3x3_keep_bytes(), 0 = nothing to keep) and pis_conv3x3_wgrad_keep reads it instead
+ * of recomputing it. x must be unchanged in between. keep == NULL: plain _ex / wgrad. */
+size_t pis_conv3x3_keep_bytes(int B, int H, int W, int Cin, int Cout);
+int pis_conv3x3_fwd_keep(const float* x, int ldx, const float* w_krsc, const float* bias,
+                         const float* scale, float* y, int ldy, int B, int H, int W, int Cin, int Cout,
+                         int flags, void* ws, size_t ws_bytes, float* keep, pis_stream_t stream);
+int pis_conv3x3_wgrad_keep(const float* x, int ldx, const float* dz, int ldz, float* dw_krsc, float* db,
+                           int B, int H, int W, int Cin, int Cout, int flags, void* ws, size_t ws_bytes,
+                           const float* keep, pis_stream_t stream);
 size_t pis_conv3x3_wgrad_ws(int B, int H, int W, int Cin, int Cout);
 int pis_conv3x3_wgrad(const float* x, int ldx, const float* dz, int ldz, float* dw_krsc, float* db,
                       int B, int H, int W, int Cin, int Cout, int flags, void* ws, size_t ws_bytes,

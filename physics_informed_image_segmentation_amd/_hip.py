@@ -44,6 +44,9 @@ _SIGNATURES = {
     "pis_conv3x3_fwd_ex": ([P, I, P, P, P, P, I, I, I, I, I, I, I, P, Z, P], c_int),
     "pis_conv3x3_dgrad_ex": ([P, I, P, P, I, P, P, I, I, I, I, I, I, I, P, Z, P], c_int),
     "pis_conv3x3_wgrad_ws": ([I, I, I, I, I], c_size_t),
+    "pis_conv3x3_keep_bytes": ([I, I, I, I, I], c_size_t),
+    "pis_conv3x3_fwd_keep": ([P, I, P, P, P, P, I, I, I, I, I, I, I, P, Z, P, P], c_int),
+    "pis_conv3x3_wgrad_keep": ([P, I, P, I, P, P, I, I, I, I, I, I, P, Z, P, P], c_int),
     "pis_conv3x3_wgrad": ([P, I, P, I, P, P, I, I, I, I, I, I, P, Z, P], c_int),
     "pis_convt2x2_fwd": ([P, I, P, P, P, I, I, I, I, I, I, P], c_int),
     "pis_convt2x2_prep": ([P, P, I, I, P], c_int),

@@ -43,7 +43,9 @@ bool wino_ok(const IGemmArgs& a);
 // output tile edge of the Winograd fwd/dgrad path for this grid: 4 (F(4x4,3x3)) or 2
 int wino_tile(int H, int W);
 size_t wino_ws_bytes(int B, int H, int W, int C, int N);
-int launch_wino3x3(const IGemmArgs& a, int B, void* ws, hipStream_t s);
+// keep_v (optional, F(4x4) only): V is written there instead of the workspace and left for
+// the layer's weight gradient (pis_conv3x3_wgrad_keep)
+int launch_wino3x3(const IGemmArgs& a, int B, void* ws, hipStream_t s, float* keep_v = nullptr);
 // Winograd weight-gradient pieces for tile edge m (2: F(3x3,2x2), 4: F(3x3,4x4)), nxi = (m+2)^2:
 // V[nxi][T][C] of x, E[nxi][T][N] of dz, dW from M[nxi][N][C]
 int launch_wino_input(const float* x, int ldx, int B, int H, int W, int C, float* V, hipStream_t s, int m);

@@ -514,11 +514,15 @@ static bool wino_wanted_dims(int H, int W, int C, int N) {
   return C >= 256 && N >= 128;
 }
 
-static int dispatch_conv3x3(const IGemmArgs& a, int B, void* ws, size_t ws_bytes, hipStream_t s) {
+static int dispatch_conv3x3(const IGemmArgs& a, int B, void* ws, size_t ws_bytes, hipStream_t s,
+                            float* keep_v = nullptr) {
   if (ws && wino_ok(a) && wino_wanted_dims(a.H, a.W, a.Csrc, a.N) &&
       ws_bytes >= wino_ws_bytes(B, a.H, a.W, a.Csrc, a.N))
-    return launch_wino3x3(a, B, ws, s);
-  return launch_conv3x3(a, s);
+    return launch_wino3x3(a, B, ws, s, keep_v);
+  int rc = launch_conv3x3(a, s);
+  // direct path taken (e.g. a small workspace): the kept transform is still owed to the wgrad
+  if (!rc && keep_v) rc = launch_wino_input(a.src, a.lds, B, a.H, a.W, a.Csrc, keep_v, s, 4);
+  return rc;
 }
 
 extern "C" size_t pis_conv3x3_ex_ws(int B, int H, int W, int Cin, int Cout) {
@@ -532,6 +536,31 @@ extern "C" int pis_conv3x3_fwd(const float* x, int ldx, const float* w_krsc, con
                                const float* scale, float* y, int ldy, int B, int H, int W, int Cin,
                                int Cout, int flags, pis_stream_t stream) {
   return pis_conv3x3_fwd_ex(x, ldx, w_krsc, bias, scale, y, ldy, B, H, W, Cin, Cout, flags, nullptr, 0, stream);
+}
+
+size_t wino_wgrad_keep_bytes(int B, int H, int W, int Cin, int Cout);  // wgrad.hip
+
+extern "C" size_t pis_conv3x3_keep_bytes(int B, int H, int W, int Cin, int Cout) {
+  if (Cin % 4 || wino_tile(H, W) != 4 || !wino_wanted_dims(H, W, Cin, Cout)) return 0;
+  return wino_wgrad_keep_bytes(B, H, W, Cin, Cout);
+}
+
+extern "C" int pis_conv3x3_fwd_keep(const float* x, int ldx, const float* w_krsc, const float* bias,
+                                    const float* scale, float* y, int ldy, int B, int H, int W, int Cin,
+                                    int Cout, int flags, void* ws, size_t ws_bytes, float* keep,
+                                    pis_stream_t stream) {
+  const size_t kb = pis_conv3x3_keep_bytes(B, H, W, Cin, Cout);
+  if (!keep || kb == 0)
+    return pis_conv3x3_fwd_ex(x, ldx, w_krsc, bias, scale, y, ldy, B, H, W, Cin, Cout, flags, ws, ws_bytes, stream);
+  PIS_CHECK_ARG(x && w_krsc && y && B > 0 && ldx % 4 == 0 && ldy % 4 == 0 && Cout % 4 == 0,
+                "pis_conv3x3_fwd_keep: bad arguments");
+  PIS_CHECK_ARG(!(flags & PIS_SCALE) || scale, "pis_conv3x3_fwd_keep: PIS_SCALE without scale");
+  IGemmArgs a{};
+  a.src = x; a.lds = ldx; a.Hs = H; a.Ws = W; a.H = H; a.W = W; a.M = B * H * W;
+  a.Csrc = Cin; a.ntaps = 9; a.tap_mode = TAP_CONV3; a.wt = w_krsc; a.ldw = 9 * Cin; a.N = Cout;
+  a.epi = EPI_NHWC; a.bias = bias; a.scale = scale; a.dst = y; a.ldd = ldy;
+  a.flags = flags & (PIS_RELU | PIS_SCALE | PIS_ACCUMULATE);
+  return dispatch_conv3x3(a, B, ws, ws_bytes, (hipStream_t)stream, keep);
 }
 
 extern "C" int pis_conv3x3_fwd_ex(const float* x, int ldx, const float* w_krsc, const float* bias,

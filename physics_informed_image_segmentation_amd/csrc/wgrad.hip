@@ -644,14 +644,24 @@ static WinoWgradPlan wino_wgrad_plan(int B, int H, int W, int Cin, int Cout) {
   return p;
 }
 
+// bytes of the forward's F(4x4,3x3) input transform the weight gradient can take over
+// (pis_conv3x3_keep_bytes): the same B^T on the same 6x6 patches
+size_t wino_wgrad_keep_bytes(int B, int H, int W, int Cin, int Cout) {
+  const WinoWgradPlan p = wino_wgrad_plan(B, H, W, Cin, Cout);
+  return (p.use && p.m == 4) ? (size_t)p.nxi * p.T * Cin * sizeof(float) : 0;
+}
+
 static int wino_wgrad(const float* x, int ldx, const float* dz, int ldz, float* dw, float* db, int B, int H, int W,
-                      int Cin, int Cout, int acc, const WinoWgradPlan& p, void* ws, hipStream_t s) {
+                      int Cin, int Cout, int acc, const WinoWgradPlan& p, void* ws, hipStream_t s,
+                      const float* keep_v = nullptr) {
   char* base = (char*)ws;
   float* V = (float*)base;
   float* E = (float*)(base + p.off_E);
   float* part = (float*)(base + p.off_part);
   float* M = (float*)(base + p.off_M);
-  int rc = launch_wino_input(x, ldx, B, H, W, Cin, V, s, p.m);
+  int rc = 0;
+  if (keep_v && p.m == 4) V = const_cast<float*>(keep_v);  // the forward's transform of x
+  else rc = launch_wino_input(x, ldx, B, H, W, Cin, V, s, p.m);
   if (!rc) rc = launch_wino_dz(dz, ldz, B, H, W, Cout, E, s, p.m);
   if (rc) return rc;
   WgradArgs a{};
@@ -692,6 +702,18 @@ __global__ void compact_c1_kernel(const float* __restrict__ full, float* __restr
   const int n = i / 9, t = i - n * 9;
   const float v = full[n * 64 + t];
   dw[i] = accumulate ? dw[i] + v : v;
+}
+
+extern "C" int pis_conv3x3_wgrad_keep(const float* x, int ldx, const float* dz, int ldz, float* dw_krsc,
+                                      float* db, int B, int H, int W, int Cin, int Cout, int flags, void* ws,
+                                      size_t ws_bytes, const float* keep, pis_stream_t stream) {
+  const WinoWgradPlan wp = wino_wgrad_plan(B, H, W, Cin, Cout);
+  if (!keep || !(wp.use && wp.m == 4))
+    return pis_conv3x3_wgrad(x, ldx, dz, ldz, dw_krsc, db, B, H, W, Cin, Cout, flags, ws, ws_bytes, stream);
+  PIS_CHECK_ARG(x && dz && dw_krsc && ldz % 4 == 0, "pis_conv3x3_wgrad_keep: bad arguments");
+  PIS_CHECK_ARG(ws && ws_bytes >= wp.total, "pis_conv3x3_wgrad_keep: workspace too small");
+  return wino_wgrad(x, ldx, dz, ldz, dw_krsc, db, B, H, W, Cin, Cout, flags & PIS_ACCUMULATE, wp, ws,
+                    (hipStream_t)stream, keep);
 }
 
 extern "C" int pis_conv3x3_wgrad(const float* x, int ldx, const float* dz, int ldz, float* dw_krsc,

@@ -562,13 +562,14 @@ size_t wino_ws_bytes(int B, int H, int W, int C, int N) {
 }
 
 // a describes the direct conv (src/lds = input, wt/ldw = KRSC weights, N outputs, epilogue)
-int launch_wino3x3(const IGemmArgs& a, int B, void* ws, hipStream_t s) {
+int launch_wino3x3(const IGemmArgs& a, int B, void* ws, hipStream_t s, float* keep_v) {
   const int C = a.Csrc, N = a.N;
   const int m = wino_tile(a.H, a.W), nxi = (m + 2) * (m + 2);
   const int64_t T = (int64_t)B * (a.H / m) * (a.W / m);
   float* U = (float*)ws;
   float* V = U + (size_t)nxi * N * C;
   float* Mt = V + (size_t)nxi * T * C;
+  if (keep_v && m == 4) V = keep_v;
   if (m == 4) {
     hipLaunchKernelGGL(wino4_filter_kernel, dim3(grid_of((int64_t)N * C)), dim3(256), 0, s, a.wt, a.ldw, N, C, U);
     hipLaunchKernelGGL(wino4_input_kernel, dim3(grid_of(T * (C / 4))), dim3(256), 0, s, a.src, a.lds, B, a.H, a.W,

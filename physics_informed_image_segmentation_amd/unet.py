@@ -359,6 +359,17 @@ class UNetEngine:
         ws = max(ws, lib.pis_conv3x3_wgrad_ws(B, H5, W5, 8 * c, 8 * c), lib.pis_conv3x3_ex_ws(B, H5, W5, 8 * c, 8 * c))
         self.ws = torch.empty((ws + 15) // 4, dtype=torch.float32, device=dev)
         self.ws_bytes = self.ws.numel() * 4
+        # per-layer kept Winograd input transforms (training forward -> weight gradient);
+        # ~2.25x each layer's input activation, ~12 GB at B=8 512^2
+        self.keep: Dict[int, torch.Tensor] = {}
+        for name in BLOCK_ORDER:
+            blk = self.m.block(name)
+            lvl = 5 if name == "bottleneck" else int(name[-1])
+            Hl, Wl = H >> (lvl - 1), W >> (lvl - 1)
+            for conv in (blk.conv0, blk.conv1):
+                nb = lib.pis_conv3x3_keep_bytes(B, Hl, Wl, conv.in_channels, conv.out_channels)
+                if nb:
+                    self.keep[id(conv)] = torch.empty((nb + 3) // 4, dtype=torch.float32, device=dev)
 
     def _gbuf(self, name: str, *shape) -> torch.Tensor:
         t = self.gbufs.get(name)
@@ -393,9 +404,10 @@ class UNetEngine:
 
     def _conv_fwd(self, conv: nn.Conv2d, x: _Buf, y: _Buf, B, H, W, scale):
         flags = PIS_RELU | (PIS_SCALE if scale is not None else 0)
-        call("pis_conv3x3_fwd_ex", x.p, x.ld, conv.weight.data_ptr(), conv.bias.data_ptr(), ptr(scale),
+        keep = self.keep.get(id(conv)) if self._keeping else None
+        call("pis_conv3x3_fwd_keep", x.p, x.ld, conv.weight.data_ptr(), conv.bias.data_ptr(), ptr(scale),
              y.p, y.ld, B, H, W, conv.in_channels, conv.out_channels, flags, self.ws.data_ptr(), self.ws_bytes,
-             self._stream())
+             ptr(keep), self._stream())
 
     def _grad_slot(self, p: torch.Tensor) -> Tuple[int, int]:
         return self._offsets[id(p)]
@@ -420,6 +432,7 @@ class UNetEngine:
         self._plan(B, H, W, x.device)
         x = x.contiguous()
         bf = self.bufs
+        self._keeping = keep  # only a forward the backward will use may overwrite the kept transforms
         self.x = x
         self.scales = scales
         src = _Buf(x, m.in_channels)
@@ -455,10 +468,11 @@ class UNetEngine:
         call("pis_head_fwd", d.p, d.ld, m.out_conv.weight.data_ptr(), m.out_conv.bias.data_ptr(), z.data_ptr(),
              u.data_ptr(), B * H * W, c, self._stream())
         m.last_logits = z
+        # every forward overwrites the engine's activation buffers: a graph built before it
+        # can no longer be backpropagated (its backward raises instead of reading stale data)
+        self.generation += 1
         if keep:
-            self.generation += 1
             self.u = u
-            return u
         return u
 
     # ---- loss backward fused into the head backward ---------------------------
@@ -534,8 +548,8 @@ class UNetEngine:
             flips[id(up)] = t
 
         def conv_bwd(conv, x: _Buf, dz: _Buf, dx: Optional[_Buf], Hl, Wl, mask: Optional[_Buf], scale):
-            call("pis_conv3x3_wgrad", x.p, x.ld, dz.p, dz.ld, self._gptr(conv.weight), self._gptr(conv.bias),
-                 B, Hl, Wl, conv.in_channels, conv.out_channels, acc, ws, wsb, st)
+            call("pis_conv3x3_wgrad_keep", x.p, x.ld, dz.p, dz.ld, self._gptr(conv.weight), self._gptr(conv.bias),
+                 B, Hl, Wl, conv.in_channels, conv.out_channels, acc, ws, wsb, ptr(self.keep.get(id(conv))), st)
             self._ready(conv.weight, conv.bias)
             if dx is not None:
                 flags = (PIS_MASK if mask is not None else 0) | (PIS_SCALE if scale is not None else 0)

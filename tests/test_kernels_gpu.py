@@ -450,3 +450,38 @@ def test_adamw_matches_torch(hip):
                                   1e-8, 1e-5, 1e-3 / bc1, bc2 ** 0.5, 1.0, s()) == 0
     torch.cuda.synchronize()
     assert rel_err(pd.cpu(), ref.detach()) < 1e-6
+
+
+@pytest.mark.parametrize("B,H,W,Cin,Cout,small_ws", [(2, 8, 8, 128, 128, False), (1, 8, 12, 64, 128, False),
+                                                     (2, 12, 8, 128, 64, False), (1, 8, 8, 256, 128, True)])
+def test_conv3x3_kept_transform(hip, B, H, W, Cin, Cout, small_ws):
+    """pis_conv3x3_fwd_keep leaves the F(4x4,3x3) input transform for pis_conv3x3_wgrad_keep:
+    same outputs as the plain calls, also when the forward falls back to the direct kernel
+    (workspace too small) and has to write the transform separately."""
+    g = torch.Generator().manual_seed(21)
+    x = F.relu(torch.randn(B, Cin, H, W, generator=g))
+    w = torch.randn(Cout, Cin, 3, 3, generator=g) / (3 * Cin ** 0.5)
+    b = torch.randn(Cout, generator=g)
+    dz = torch.randn(B, Cout, H, W, generator=g)
+    nk = hip.pis_conv3x3_keep_bytes(B, H, W, Cin, Cout)
+    assert nk > 0
+    keep = torch.full((nk // 4,), float("nan"), device="cuda")
+    nws = 0 if small_ws else hip.pis_conv3x3_ex_ws(B, H, W, Cin, Cout)
+    ws = torch.empty(max(nws, 4) // 4 + 1, device="cuda")
+    xd, wd, bd, dzd = nhwc(x).cuda(), krsc(w).cuda(), b.cuda(), nhwc(dz).cuda()
+    y = torch.empty(B, H, W, Cout, device="cuda")
+    rc = hip.pis_conv3x3_fwd_keep(xd.data_ptr(), Cin, wd.data_ptr(), bd.data_ptr(), 0, y.data_ptr(), Cout, B, H, W,
+                                  Cin, Cout, RELU, ws.data_ptr(), nws, keep.data_ptr(), s())
+    assert rc == 0, hip.pis_last_error()
+    nwg = hip.pis_conv3x3_wgrad_ws(B, H, W, Cin, Cout)
+    wsg = torch.empty(nwg // 4 + 1, device="cuda")
+    dw = torch.empty(Cout, 3, 3, Cin, device="cuda")
+    db = torch.empty(Cout, device="cuda")
+    rc = hip.pis_conv3x3_wgrad_keep(xd.data_ptr(), Cin, dzd.data_ptr(), Cout, dw.data_ptr(), db.data_ptr(), B, H, W,
+                                    Cin, Cout, 0, wsg.data_ptr(), nwg, keep.data_ptr(), s())
+    assert rc == 0, hip.pis_last_error()
+    torch.cuda.synchronize()
+    assert torch.isfinite(keep).all()
+    assert rel_err(nchw(y.cpu()), F.relu(F.conv2d(x, w, b, padding=1))) < 1e-5
+    assert rel_err(dw.cpu().permute(0, 3, 1, 2), torch.nn.grad.conv2d_weight(x, w.shape, dz, padding=1)) < 1e-5
+    assert rel_err(db.cpu(), dz.sum(dim=(0, 2, 3))) < 1e-5
