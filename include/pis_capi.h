@@ -63,7 +63,10 @@ int pis_version(void);
 #define PIS_TUNE_WINO_TILE 10    /* Winograd batched GEMM: 0 generic igemm, 1 lean NT GEMM 128x256 (N % 256 == 0), 2 lean NT GEMM 128x128 (default) */
 #define PIS_TUNE_WINO_F4 11      /* Winograd tile: 0 F(2x2,3x3) fwd/dgrad + F(3x3,2x2) wgrad; 1 (default) F(4x4,3x3) +
                                     F(3x3,4x4) when H % 4 == W % 4 == 0 */
-#define PIS_TUNE_NKEYS 12
+#define PIS_TUNE_WINO_FUSED 12   /* F(4x4,3x3) fwd/dgrad as ONE fused kernel (transforms in LDS/registers): 0/1 off
+                                    (auto: measured slower than the 3-pass pipeline on every layer that keeps V),
+                                    2 whenever H % 16 == W % 64 == N % 16 == 0 */
+#define PIS_TUNE_NKEYS 13
 #define PIS_DEBUG_NOLOAD (1 << 16)
 int pis_tune(int key, int value);
 

@@ -250,7 +250,7 @@ __device__ __forceinline__ void axpy_c(T& acc, float c, const T& v) {
 
 // U[xi][n][c] = (G g G^T)[xi], xi = 6 i + j
 __global__ __launch_bounds__(256) void wino4_filter_kernel(const float* __restrict__ w, int ldw, int N, int C,
-                                                           float* __restrict__ U) {
+                                                           float* __restrict__ U, int transposed = 0) {
   const int64_t NC = (int64_t)N * C;
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < NC; e += (int64_t)gridDim.x * blockDim.x) {
     const int n = (int)(e / C), c = (int)(e - (int64_t)n * C);
@@ -273,7 +273,8 @@ __global__ __launch_bounds__(256) void wino4_filter_kernel(const float* __restri
         float u = 0.f;
 #pragma unroll
         for (int s = 0; s < 3; ++s) axpy_c(u, w4_g(j, s), gg[i][s]);
-        U[(size_t)(i * 6 + j) * NC + e] = u;
+        // [xi][n][c] for the batched GEMMs; [xi][c][n] for the fused kernel's B operand
+        U[(size_t)(i * 6 + j) * NC + (transposed ? (int64_t)c * N + n : e)] = u;
       }
   }
 }
@@ -356,6 +357,167 @@ __global__ __launch_bounds__(256) void wino4_output_kernel(const float* __restri
       for (int j = 0; j < 4; ++j) {
         const size_t pix = ((size_t)b * g.H + 4 * ty + i) * g.W + 4 * tx + j;
         conv_epilogue4(g, pix, n, y[i][j] + bias4, sc4);
+      }
+  }
+}
+
+// ---- fused F(4x4,3x3): transforms + the 36 contractions + output transform in one kernel ----
+// For channel counts where the non-fused pipeline is bound by the V / M round trips through
+// HBM. A block owns 4 x 16 output tiles (16 x 64 pixels) x 16 output channels; wave w owns
+// tile row w. Input channels are walked 4 at a time:
+//   * the 18 x 66 x 4 input patch and the 36 x 4 x 16 slice of Ut (= G g G^T, [xi][c][n]) are
+//     double-buffered in LDS (one barrier per step; the next step's global loads are in flight
+//     while the current one computes);
+//   * lane l transforms ITS OWN (tile l & 15, channel l >> 4) patch: V = BT d BT^T stays in
+//     registers and V[xi] is exactly lane l's A operand of v_mfma_f32_16x16x4_f32 (A[row l&15]
+//     [k l>>4]); each wave issues 36 MFMAs per step into 36 independent accumulators;
+//   * the C/D map (row 4 (l >> 4) + r, col l & 15) leaves all 36 xi of 4 (tile, channel) pairs
+//     in one lane: Y = AT M AT^T and the conv epilogue run in registers.
+// V and M never leave the CU. Needs H % 16 == 0, W % 64 == 0, N % 16 == 0, C % 4 == 0.
+constexpr int WF_TR = 4, WF_TC = 16, WF_NB = 16, WF_KC = 4;
+constexpr int WF_PR = 4 * WF_TR + 2, WF_PC = 4 * WF_TC + 2;  // 18 x 66 input patch
+constexpr int WF_PS = 5;                                      // LDS floats per patch pixel (4 + 1 pad)
+constexpr int WF_PBUF = WF_PR * WF_PC * WF_PS;                // 5940 floats
+constexpr int WF_UBUF = 36 * WF_KC * WF_NB;                   // 2304 floats
+
+__global__ __launch_bounds__(256, 2) void wino4_fused_kernel(const float* __restrict__ Ut, IGemmArgs g, int B) {
+  __shared__ __attribute__((aligned(16))) float sP[2][WF_PBUF];  // [row][col][k (+pad)]
+  __shared__ __attribute__((aligned(16))) float sU[2][WF_UBUF];  // [xi][k][n]
+  const int H = g.H, W = g.W, C = g.Csrc, N = g.N;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nbn = N / WF_NB, bx = W / (4 * WF_TC), by = H / (4 * WF_TR);
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int nb = bid % nbn;
+  int rest = bid / nbn;
+  const int bxi = rest % bx;
+  rest /= bx;
+  const int byi = rest % by, b = rest / by;
+  const int y0 = byi * 4 * WF_TR - 1, x0 = bxi * 4 * WF_TC - 1, n0 = nb * WF_NB;
+  const float* src = g.src + (size_t)b * H * W * g.lds;
+
+  constexpr int PPIX = WF_PR * WF_PC;                  // 1188 pixels
+  constexpr int PL = (PPIX + 255) / 256;               // 5
+  constexpr int UQ = WF_UBUF / 4;                      // 576 float4
+  constexpr int UL = (UQ + 255) / 256;                 // 3
+  f32x4 rp[PL], ru[UL];
+  auto gload = [&](int c0) {
+#pragma unroll
+    for (int i = 0; i < PL; ++i) {
+      const int px = tid + 256 * i;
+      rp[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (px < PPIX) {
+        const int yy = y0 + px / WF_PC, xx = x0 + px % WF_PC;
+        if (yy >= 0 && yy < H && xx >= 0 && xx < W)
+          rp[i] = *reinterpret_cast<const f32x4*>(src + ((size_t)yy * W + xx) * g.lds + c0);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < UL; ++i) {
+      const int q = tid + 256 * i;
+      if (q < UQ) {
+        const int xk = q / (WF_NB / 4), n4 = q % (WF_NB / 4);  // xk = xi * 4 + k
+        ru[i] = *reinterpret_cast<const f32x4*>(Ut + ((size_t)(xk >> 2) * C + c0 + (xk & 3)) * N + n0 + 4 * n4);
+      }
+    }
+  };
+  auto lstore = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < PL; ++i) {
+      const int px = tid + 256 * i;
+      if (px < PPIX) {
+        float* d = &sP[buf][px * WF_PS];
+        d[0] = rp[i][0];
+        d[1] = rp[i][1];
+        d[2] = rp[i][2];
+        d[3] = rp[i][3];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < UL; ++i) {
+      const int q = tid + 256 * i;
+      if (q < UQ) *reinterpret_cast<f32x4*>(&sU[buf][q * 4]) = ru[i];
+    }
+  };
+
+  f32x4 acc[36];
+#pragma unroll
+  for (int xi = 0; xi < 36; ++xi) acc[xi] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int tc = lane & 15, tk = lane >> 4;
+
+  const int nks = C / WF_KC;
+  gload(0);
+  lstore(0);
+  for (int ks = 0; ks < nks; ++ks) {
+    const int buf = ks & 1;
+    __syncthreads();
+    if (ks + 1 < nks) gload((ks + 1) * WF_KC);
+    const float* P = &sP[buf][((4 * wave) * WF_PC + 4 * tc) * WF_PS + tk];
+    const float* Ub = &sU[buf][tk * WF_NB + tc];
+    float r[6][6];  // r[a][j] = (d BT^T)[a][j]
+#pragma unroll
+    for (int a = 0; a < 6; ++a) {
+      float d[6];
+#pragma unroll
+      for (int bb = 0; bb < 6; ++bb) d[bb] = P[(a * WF_PC + bb) * WF_PS];
+#pragma unroll
+      for (int j = 0; j < 6; ++j) {
+        r[a][j] = 0.f;
+#pragma unroll
+        for (int bb = 0; bb < 6; ++bb) axpy_c(r[a][j], w4_bt(j, bb), d[bb]);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      float ub[6];
+#pragma unroll
+      for (int j = 0; j < 6; ++j) ub[j] = Ub[(i * 6 + j) * WF_KC * WF_NB];
+#pragma unroll
+      for (int j = 0; j < 6; ++j) {
+        float v = 0.f;
+#pragma unroll
+        for (int a = 0; a < 6; ++a) axpy_c(v, w4_bt(i, a), r[a][j]);
+        acc[i * 6 + j] = __builtin_amdgcn_mfma_f32_16x16x4f32(v, ub[j], acc[i * 6 + j], 0, 0, 0);
+      }
+    }
+    if (ks + 1 < nks) lstore(buf ^ 1);
+  }
+
+  // output transform + epilogue: lane holds M[xi] of tiles (row wave, col 4 (lane >> 4) + r), channel n
+  const int n = n0 + (lane & 15);
+  const float bias = g.bias ? g.bias[n] : 0.f;
+  const float sc = (g.flags & PIS_SCALE) ? g.scale[(size_t)b * N + n] : 1.f;
+  const int oy = byi * 4 * WF_TR + 4 * wave;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int ox = bxi * 4 * WF_TC + 4 * (4 * (lane >> 4) + r);
+    float y[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) y[i][j] = 0.f;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float q = 0.f;
+#pragma unroll
+        for (int l = 0; l < 6; ++l) axpy_c(q, w4_at(j, l), acc[k * 6 + l][r]);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) axpy_c(y[i][j], w4_at(i, k), q);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const size_t pix = ((size_t)b * H + oy + i) * W + ox + j;
+        float v = y[i][j] + bias;
+        if (g.flags & PIS_RELU) v = fmaxf(v, 0.f);
+        if (g.flags & PIS_MASK) v = g.mask[pix * g.ldm + n] > 0.f ? v : 0.f;
+        v *= sc;
+        float* dst = g.dst + pix * g.ldd + n;
+        if (g.flags & PIS_ACCUMULATE) v += *dst;
+        *dst = v;
       }
   }
 }
@@ -561,6 +723,16 @@ size_t wino_ws_bytes(int B, int H, int W, int C, int N) {
   return (size_t)nxi * ((int64_t)N * C + T * C + T * N) * sizeof(float) + 1024;
 }
 
+// fused F(4x4,3x3) (pis_tune key 12: 0 off, 1 auto, 2 whenever the shape allows)
+static bool wino_fused_wanted(int H, int W, int C, int N) {
+  const int mode = tune_get(PIS_TUNE_WINO_FUSED);
+  if (mode == 0 || H % (4 * WF_TR) || W % (4 * WF_TC) || N % WF_NB || C % WF_KC) return false;
+  // measured (tools/bench_kernels.py --key 12 --variants 0,2, B=8): faster only for dec1.conv0 fwd
+  // (-8 %) and enc2.conv0 fwd (-7 %) — the 4-channel steps re-fetch each input line 8x from
+  // L2/MALL — so auto uses it nowhere yet; 2 forces it (tests, experiments)
+  return mode == 2;
+}
+
 // a describes the direct conv (src/lds = input, wt/ldw = KRSC weights, N outputs, epilogue)
 int launch_wino3x3(const IGemmArgs& a, int B, void* ws, hipStream_t s, float* keep_v) {
   const int C = a.Csrc, N = a.N;
@@ -570,8 +742,19 @@ int launch_wino3x3(const IGemmArgs& a, int B, void* ws, hipStream_t s, float* ke
   float* V = U + (size_t)nxi * N * C;
   float* Mt = V + (size_t)nxi * T * C;
   if (keep_v && m == 4) V = keep_v;
+  const double flop = 2.0 * nxi * (double)T * N * C;
+  if (m == 4 && !keep_v && wino_fused_wanted(a.H, a.W, C, N)) {
+    hipLaunchKernelGGL(wino4_filter_kernel, dim3(grid_of((int64_t)N * C)), dim3(256), 0, s, a.wt, a.ldw, N, C, U, 1);
+    int rc = launch_status("wino_filter");
+    if (rc) return rc;
+    const int blocks = B * (a.H / (4 * WF_TR)) * (a.W / (4 * WF_TC)) * (N / WF_NB);
+    launch_hook("wino_fused", 0, s, flop);
+    hipLaunchKernelGGL(wino4_fused_kernel, dim3(blocks), dim3(256), 0, s, U, a, B);
+    launch_hook("wino_fused", 1, s, flop);
+    return launch_status("wino_fused");
+  }
   if (m == 4) {
-    hipLaunchKernelGGL(wino4_filter_kernel, dim3(grid_of((int64_t)N * C)), dim3(256), 0, s, a.wt, a.ldw, N, C, U);
+    hipLaunchKernelGGL(wino4_filter_kernel, dim3(grid_of((int64_t)N * C)), dim3(256), 0, s, a.wt, a.ldw, N, C, U, 0);
     hipLaunchKernelGGL(wino4_input_kernel, dim3(grid_of(T * (C / 4))), dim3(256), 0, s, a.src, a.lds, B, a.H, a.W,
                        C, V);
   } else {
@@ -581,8 +764,7 @@ int launch_wino3x3(const IGemmArgs& a, int B, void* ws, hipStream_t s, float* ke
   }
   int rc = launch_status("wino_transforms");
   if (rc) return rc;
-  const double flop = 2.0 * nxi * (double)T * N * C;
-  launch_hook("wino_gemm", 0, s, flop);
+    launch_hook("wino_gemm", 0, s, flop);
   const int v = tune_get(PIS_TUNE_WINO_TILE);
   if (v == 1 && N % 256 == 0) {
     const dim3 grid((int)cdiv(T, 128) * (N / 256), nxi);

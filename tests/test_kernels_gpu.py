@@ -103,7 +103,7 @@ def test_conv3x3_dgrad_wgrad(hip, B, H, W, Cin, Cout):
 
 # every non-default kernel variant behind pis_tune (include/pis_capi.h) stays exact too
 TUNE_VARIANTS = [(4, 1), (4, 2), (4, 3), (5, 0), (6, 2048), (3, 0), (7, 1), (8, 0), (8, 2), (10, 0), (10, 1),
-                 (11, 0)]
+                 (11, 0), (12, 0), (12, 2)]
 
 
 @pytest.mark.parametrize("key,value", TUNE_VARIANTS)
@@ -485,3 +485,16 @@ def test_conv3x3_kept_transform(hip, B, H, W, Cin, Cout, small_ws):
     assert rel_err(nchw(y.cpu()), F.relu(F.conv2d(x, w, b, padding=1))) < 1e-5
     assert rel_err(dw.cpu().permute(0, 3, 1, 2), torch.nn.grad.conv2d_weight(x, w.shape, dz, padding=1)) < 1e-5
     assert rel_err(db.cpu(), dz.sum(dim=(0, 2, 3))) < 1e-5
+
+
+@pytest.mark.parametrize("B,H,W,Cin,Cout", [(2, 32, 64, 128, 64), (1, 16, 32, 256, 128), (1, 16, 128, 64, 64),
+                                           (2, 48, 64, 64, 128), (1, 32, 64, 512, 16)])
+def test_conv3x3_winograd_fused(hip, B, H, W, Cin, Cout):
+    """pis_tune(12, 2): Winograd F(4x4,3x3) fwd / dgrad as the one fused kernel (transforms in
+    LDS and registers) wherever H % 16 == W % 64 == 0 and the output channels are a multiple
+    of 16; every epilogue (bias, ReLU, mask, keep-scale, accumulate) through it."""
+    prev = hip.pis_tune(12, 2)
+    try:
+        test_conv3x3_ex_winograd(hip, B, H, W, Cin, Cout, 2)
+    finally:
+        hip.pis_tune(12, prev)

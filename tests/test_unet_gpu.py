@@ -232,3 +232,35 @@ def test_train_epoch_keys_and_validate(hip):
     va = validate(net, dl, crit, torch.device("cuda"), return_components=True, compute_metrics=True)
     assert {"loss", "dice_score", "dice_loss", "bce_loss", "pde_loss", "iou_score"} <= set(va)
     assert np.isfinite(tr["loss"]) and np.isfinite(va["loss"])
+
+
+def test_full_size_forward_and_loss_c2_shape(hip):
+    """BASELINE config C2's image size (512 x 512) through the whole HIP forward (Winograd
+    F(4x4) on every >= 128-channel conv, halo kernels at 64 channels) and the fused Stage-II
+    loss, against the fp32 oracle on the CPU: logits/probabilities and every loss term within
+    the north-star 1e-4 relative tolerance. One image keeps the CPU side to a few seconds."""
+    from physics_informed_image_segmentation_amd import DiceBCEPDELoss
+    img, mask = rt.synthetic_batch(1, 512, 512, seed=42)
+    net, ref = make_pair(42)
+    net.eval(), ref.eval()
+    crit = DiceBCEPDELoss(pde_weight=1e-4, phase_field_weight=1e-4, diffusion_coeff=5.0, reaction_threshold=0.5,
+                          epsilon=0.05)
+    with torch.no_grad():
+        u = net(img.cuda())
+        crit(u, mask.cuda())
+        p_ref, z_ref = ref(img, return_logits=True)
+    assert rel(net.last_logits, z_ref) < TOL
+    assert rel(u, p_ref) < TOL
+    t = rt.loss_terms(p_ref, mask, **PDE_KW)
+    got = crit.last["terms"][:5].cpu()
+    # from the HIP probabilities: every term but L_RD, whose residual D Lap(u) + f(u) of a
+    # near-constant random-init u cancels to ~5e-3 and amplifies u's 1e-6 rounding ~1e3-fold
+    for i, k in enumerate(("loss", "dice_loss", "bce_loss", "pde_loss", "phase_field_loss")):
+        if k != "pde_loss":
+            assert abs(got[i].item() - t[k].item()) <= TOL * abs(t[k].item()), k
+    # the fused loss kernel itself at full size, on the oracle's own probabilities: all five
+    with torch.no_grad():
+        crit(p_ref.cuda(), mask.cuda())
+    got = crit.last["terms"][:5].cpu()
+    for i, k in enumerate(("loss", "dice_loss", "bce_loss", "pde_loss", "phase_field_loss")):
+        assert abs(got[i].item() - t[k].item()) <= TOL * abs(t[k].item()), k
