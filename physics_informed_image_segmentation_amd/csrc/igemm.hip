@@ -516,7 +516,9 @@ static bool wino_wanted_dims(int H, int W, int C, int N) {
 
 static int dispatch_conv3x3(const IGemmArgs& a, int B, void* ws, size_t ws_bytes, hipStream_t s,
                             float* keep_v = nullptr) {
-  if (ws && wino_ok(a) && wino_wanted_dims(a.H, a.W, a.Csrc, a.N) &&
+  // a kept transform is computed either way: then Winograd wins even where the plain policy
+  // prefers the direct kernel (64 -> 64 at 512^2: +2 % forward, -27 % weight gradient)
+  if (ws && wino_ok(a) && (keep_v || wino_wanted_dims(a.H, a.W, a.Csrc, a.N)) &&
       ws_bytes >= wino_ws_bytes(B, a.H, a.W, a.Csrc, a.N))
     return launch_wino3x3(a, B, ws, s, keep_v);
   int rc = launch_conv3x3(a, s);
@@ -525,9 +527,12 @@ static int dispatch_conv3x3(const IGemmArgs& a, int B, void* ws, size_t ws_bytes
   return rc;
 }
 
+size_t wino_wgrad_keep_bytes(int B, int H, int W, int Cin, int Cout);  // wgrad.hip
+
 extern "C" size_t pis_conv3x3_ex_ws(int B, int H, int W, int Cin, int Cout) {
   size_t need = 0;
-  if (wino_wanted_dims(H, W, Cin, Cout)) need = std::max(need, wino_ws_bytes(B, H, W, Cin, Cout));  // fwd
+  const bool keepable = Cin % 4 == 0 && wino_tile(H, W) == 4 && wino_wgrad_keep_bytes(B, H, W, Cin, Cout) > 0;
+  if (keepable || wino_wanted_dims(H, W, Cin, Cout)) need = std::max(need, wino_ws_bytes(B, H, W, Cin, Cout));  // fwd
   if (wino_wanted_dims(H, W, Cout, Cin)) need = std::max(need, wino_ws_bytes(B, H, W, Cout, Cin));  // dgrad
   return need;
 }
@@ -538,10 +543,8 @@ extern "C" int pis_conv3x3_fwd(const float* x, int ldx, const float* w_krsc, con
   return pis_conv3x3_fwd_ex(x, ldx, w_krsc, bias, scale, y, ldy, B, H, W, Cin, Cout, flags, nullptr, 0, stream);
 }
 
-size_t wino_wgrad_keep_bytes(int B, int H, int W, int Cin, int Cout);  // wgrad.hip
-
 extern "C" size_t pis_conv3x3_keep_bytes(int B, int H, int W, int Cin, int Cout) {
-  if (Cin % 4 || wino_tile(H, W) != 4 || !wino_wanted_dims(H, W, Cin, Cout)) return 0;
+  if (Cin % 4 || wino_tile(H, W) != 4 || tune_get(PIS_TUNE_WINOGRAD) == 0) return 0;
   return wino_wgrad_keep_bytes(B, H, W, Cin, Cout);
 }
 

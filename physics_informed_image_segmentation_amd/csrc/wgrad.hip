@@ -621,11 +621,12 @@ struct WinoWgradPlan {
 static WinoWgradPlan wino_wgrad_plan(int B, int H, int W, int Cin, int Cout) {
   WinoWgradPlan p{};
   const int mode = tune_get(PIS_TUNE_WINOGRAD);
-  // auto (tools/bench_kernels.py --key 8 --variants 1,2 --ops wgrad, B=8): F(3x3,4x4) from 128
-  // channels on either side (dec1.conv0 -25 %, enc2.conv0 -15 %; 64 -> 64 within 2 % of the
-  // halo kernel, which stays); F(3x3,2x2) only with >= 128 on both sides (4-36 % faster there)
+  // auto (tools/bench_kernels.py --key 8 --variants 1,2 --ops wgrad, B=8): dec1.conv0 -25 %,
+  // enc2.conv0 -15 %, 64 -> 64 -2 % against the halo kernel
   const int m = (tune_get(PIS_TUNE_WINO_F4) != 0 && H % 4 == 0 && W % 4 == 0) ? 4 : 2;
-  const bool wanted = m == 4 ? (Cin >= 128 || Cout >= 128) : (Cin >= 128 && Cout >= 128);
+  // F(3x3,4x4) everywhere on 4-aligned grids (64 -> 64 at 512^2: -2 % alone, -27 % with the
+  // forward's kept transform); F(3x3,2x2) only with >= 128 on both sides
+  const bool wanted = m == 4 || (Cin >= 128 && Cout >= 128);
   p.use = mode != 0 && H % 2 == 0 && W % 2 == 0 && Cin % 64 == 0 && Cout % 64 == 0 && (mode == 2 || wanted);
   if (!p.use) return p;
   p.m = m;
