@@ -49,7 +49,11 @@ int launch_wino3x3(const IGemmArgs& a, int B, void* ws, hipStream_t s, float* ke
 // Winograd weight-gradient pieces for tile edge m (2: F(3x3,2x2), 4: F(3x3,4x4)), nxi = (m+2)^2:
 // V[nxi][T][C] of x, E[nxi][T][N] of dz, dW from M[nxi][N][C]
 int launch_wino_input(const float* x, int ldx, int B, int H, int W, int C, float* V, hipStream_t s, int m);
-int launch_wino_dz(const float* dz, int ldz, int B, int H, int W, int N, float* E, hipStream_t s, int m);
+// bpart (m == 4 only, optional, N / 4 must divide 256): per-block channel sums of dz,
+// [wino_dz_blocks()][N], for the bias gradient
+int launch_wino_dz(const float* dz, int ldz, int B, int H, int W, int N, float* E, hipStream_t s, int m,
+                   float* bpart = nullptr);
+int wino_dz_blocks(int B, int H, int W, int N, int m);
 int launch_wino_wgrad_out(const float* M, int N, int C, float* dw, int accumulate, hipStream_t s, int m);
 
 }  // namespace pis

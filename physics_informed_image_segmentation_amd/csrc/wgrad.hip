@@ -611,7 +611,7 @@ __global__ __launch_bounds__(256) void wgrad_c1_kernel(const float* __restrict__
 // [split][xi][Cout][Cin], one fixed-order reduction), dW = A^T M A; the bias gradient is a
 // channel sum of dz.
 struct WinoWgradPlan {
-  bool use;
+  bool use, fused_bias;
   int m, nxi;
   int64_t T;
   WgradPlan gemm;
@@ -641,7 +641,11 @@ static WinoWgradPlan wino_wgrad_plan(int B, int H, int W, int Cin, int Cout) {
   p.off_part = V + E;
   p.off_M = p.off_part + part;
   p.off_cs = p.off_M + M;
-  p.total = p.off_cs + colsum_ws((int64_t)B * H * W, Cout) + 256;
+  // bias gradient: per-block sums out of the F(3x3,4x4) dz transform, else a channel-sum pass
+  p.fused_bias = p.m == 4 && 256 % (Cout / 4) == 0;
+  const size_t cs = p.fused_bias ? (size_t)wino_dz_blocks(B, H, W, Cout, 4) * Cout * sizeof(float)
+                                 : colsum_ws((int64_t)B * H * W, Cout);
+  p.total = p.off_cs + al(cs) + 256;
   return p;
 }
 
@@ -663,7 +667,8 @@ static int wino_wgrad(const float* x, int ldx, const float* dz, int ldz, float* 
   int rc = 0;
   if (keep_v && p.m == 4) V = const_cast<float*>(keep_v);  // the forward's transform of x
   else rc = launch_wino_input(x, ldx, B, H, W, Cin, V, s, p.m);
-  if (!rc) rc = launch_wino_dz(dz, ldz, B, H, W, Cout, E, s, p.m);
+  float* bpart = (db && p.fused_bias) ? (float*)(base + p.off_cs) : nullptr;
+  if (!rc) rc = launch_wino_dz(dz, ldz, B, H, W, Cout, E, s, p.m, bpart);
   if (rc) return rc;
   WgradArgs a{};
   a.a = E; a.lda = Cout; a.a_up2 = 0; a.Ca = Cout;
@@ -678,8 +683,10 @@ static int wino_wgrad(const float* x, int ldx, const float* dz, int ldz, float* 
   launch_hook("wino_wgrad_gemm", 1, s, flop);
   if (!rc) rc = reduce_slabs_pitched(part, p.gemm.splits, a.split_stride, a.split_stride, M, 0, s);
   if (!rc) rc = launch_wino_wgrad_out(M, Cout, Cin, dw, acc, s, p.m);
-  if (!rc && db)
-    rc = colsum(dz, ldz, (int64_t)B * H * W, Cout, db, acc, base + p.off_cs, p.total - p.off_cs, s);
+  if (!rc && db) {
+    if (bpart) rc = reduce_slabs(bpart, wino_dz_blocks(B, H, W, Cout, 4), Cout, db, acc, s);
+    else rc = colsum(dz, ldz, (int64_t)B * H * W, Cout, db, acc, base + p.off_cs, p.total - p.off_cs, s);
+  }
   return rc;
 }
 

@@ -545,10 +545,14 @@ __host__ __device__ constexpr float w4_at3(int i, int k) {
 }
 
 // E[xi][t][n] = (G4 e G4^T)[xi], e = dz at output pixels (4ty + i, 4tx + j)
+// With bpart != NULL it also leaves the bias gradient's per-block channel sums in
+// bpart[blockIdx.x][N] (every dz pixel belongs to exactly one tile): with 256 * gridDim.x a
+// multiple of N / 4 a thread's channels never change across its grid-stride items.
 __global__ __launch_bounds__(256) void wino4_dz_kernel(const float* __restrict__ dz, int ldz, int B, int H, int W,
-                                                       int N, float* __restrict__ E) {
+                                                       int N, float* __restrict__ E, float* __restrict__ bpart) {
   const int n4n = N / 4, TW = W / 4, TH = H / 4;
   const int64_t T = (int64_t)B * TH * TW, TN = T * N;
+  f32x4 bsum = {0.f, 0.f, 0.f, 0.f};
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < T * n4n; e += (int64_t)gridDim.x * blockDim.x) {
     const int64_t t = e / n4n;
     const int n = (int)(e - t * n4n) * 4;
@@ -565,6 +569,7 @@ __global__ __launch_bounds__(256) void wino4_dz_kernel(const float* __restrict__
 #pragma unroll
       for (int l = 0; l < 4; ++l)
         d[l] = *reinterpret_cast<const f32x4*>(dz + (((size_t)b * H + 4 * ty + k) * W + 4 * tx + l) * ldz + n);
+      bsum += (d[0] + d[1]) + (d[2] + d[3]);
 #pragma unroll
       for (int j = 0; j < 6; ++j) {
         f32x4 r = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -577,6 +582,16 @@ __global__ __launch_bounds__(256) void wino4_dz_kernel(const float* __restrict__
 #pragma unroll
     for (int xi = 0; xi < 36; ++xi)
       *reinterpret_cast<f32x4*>(E + (size_t)xi * TN + t * N + n) = v[xi / 6][xi % 6];
+  }
+  if (!bpart) return;
+  // fixed-order block reduction of the threads sharing a channel quad (tid mod n4n)
+  __shared__ f32x4 red[256];
+  red[threadIdx.x] = bsum;
+  __syncthreads();
+  if ((int)threadIdx.x < n4n) {
+    f32x4 acc = red[threadIdx.x];
+    for (int k = threadIdx.x + n4n; k < 256; k += n4n) acc += red[k];
+    *reinterpret_cast<f32x4*>(bpart + (size_t)blockIdx.x * N + 4 * threadIdx.x) = acc;
   }
 }
 
@@ -807,10 +822,15 @@ int launch_wino_input(const float* x, int ldx, int B, int H, int W, int C, float
   return launch_status("wino_input");
 }
 
-int launch_wino_dz(const float* dz, int ldz, int B, int H, int W, int N, float* E, hipStream_t s, int m) {
+int wino_dz_blocks(int B, int H, int W, int N, int m) {
+  return grid_of((int64_t)B * (H / m) * (W / m) * (N / 4));
+}
+
+int launch_wino_dz(const float* dz, int ldz, int B, int H, int W, int N, float* E, hipStream_t s, int m,
+                   float* bpart) {
   const int64_t T = (int64_t)B * (H / m) * (W / m);
   if (m == 4)
-    hipLaunchKernelGGL(wino4_dz_kernel, dim3(grid_of(T * (N / 4))), dim3(256), 0, s, dz, ldz, B, H, W, N, E);
+    hipLaunchKernelGGL(wino4_dz_kernel, dim3(grid_of(T * (N / 4))), dim3(256), 0, s, dz, ldz, B, H, W, N, E, bpart);
   else
     hipLaunchKernelGGL(wino_dz_kernel, dim3(grid_of(T * (N / 4))), dim3(256), 0, s, dz, ldz, B, H, W, N, E);
   return launch_status("wino_dz");
