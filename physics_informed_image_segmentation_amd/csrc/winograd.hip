@@ -635,13 +635,14 @@ __global__ __launch_bounds__(256) void wino4_wgrad_out_kernel(const float* __res
 // Winograd contractions. Block tile BM x BN (4 waves, 2 x 2, each (BM/2) x (BN/2) as 32x32 MFMA
 // tiles), K-step 16 through a register-staged LDS double buffer; LDS rows padded to 20 floats
 // so the 16-byte fragment reads are conflict-free; one ds_read_b128 feeds 4 MFMAs.
-template <int BM, int BN>
+// (BK = 32 measured within +-3 % of BK = 16 on every Winograd layer: tools/bench_kernels.py --key 10)
+template <int BM, int BN, int BK = 16>
 __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const float* __restrict__ A, const float* __restrict__ Bm,
                                                         float* __restrict__ Cm, int M, int N, int K,
                                                         int64_t bsA, int64_t bsB, int64_t bsC) {
-  constexpr int BK = 16, ROW = BK + 4;
+  constexpr int ROW = BK + 4, CPR = BK / 4;  // LDS row pitch; float4 chunks per staged row
   constexpr int TM = BM / 64, TN = BN / 64;
-  constexpr int AL = BM * 4 / 256, BL = BN * 4 / 256;  // float4 loads per thread per stage
+  constexpr int AL = BM * CPR / 256, BL = BN * CPR / 256;  // float4 loads per thread per stage
   __shared__ __attribute__((aligned(16))) float sA[2][BM * ROW];
   __shared__ __attribute__((aligned(16))) float sB[2][BN * ROW];
   A += blockIdx.y * bsA;
@@ -652,28 +653,28 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const float* __restrict
   const int ntn = N / BN;
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int m0 = (bid / ntn) * BM, n0 = (bid % ntn) * BN;
-  const int q4 = (tid & 3) * 4;
+  const int q4 = (tid % CPR) * 4;
   f32x4 ra[AL], rb[BL];
   auto gload = [&](int k0) {
     const int k = k0 + q4;
 #pragma unroll
     for (int i = 0; i < AL; ++i) {
-      const int m = m0 + (tid + i * 256) / 4;
+      const int m = m0 + (tid + i * 256) / CPR;
       ra[i] = f32x4{0.f, 0.f, 0.f, 0.f};
       if (m < M && k < K) ra[i] = *reinterpret_cast<const f32x4*>(A + (size_t)m * K + k);
     }
 #pragma unroll
     for (int i = 0; i < BL; ++i) {
-      const int n = n0 + (tid + i * 256) / 4;
+      const int n = n0 + (tid + i * 256) / CPR;
       rb[i] = f32x4{0.f, 0.f, 0.f, 0.f};
       if (k < K) rb[i] = *reinterpret_cast<const f32x4*>(Bm + (size_t)n * K + k);
     }
   };
   auto lstore = [&](int buf) {
 #pragma unroll
-    for (int i = 0; i < AL; ++i) *reinterpret_cast<f32x4*>(&sA[buf][((tid + i * 256) / 4) * ROW + q4]) = ra[i];
+    for (int i = 0; i < AL; ++i) *reinterpret_cast<f32x4*>(&sA[buf][((tid + i * 256) / CPR) * ROW + q4]) = ra[i];
 #pragma unroll
-    for (int i = 0; i < BL; ++i) *reinterpret_cast<f32x4*>(&sB[buf][((tid + i * 256) / 4) * ROW + q4]) = rb[i];
+    for (int i = 0; i < BL; ++i) *reinterpret_cast<f32x4*>(&sB[buf][((tid + i * 256) / CPR) * ROW + q4]) = rb[i];
   };
   f32x16 acc[TM][TN];
 #pragma unroll
