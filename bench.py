@@ -32,6 +32,21 @@ from physics_informed_image_segmentation_amd.distributed import (GradBucketer, b
 B, H, W = 8, 512, 512
 LOSS_KW = dict(pde_weight=1e-4, phase_field_weight=1e-4, diffusion_coeff=5.0, reaction_threshold=0.5, epsilon=0.05)
 LR = 1e-5
+# --config: C2 is the headline (BASELINE.json configs[1]); the others are BASELINE's C4 ablation
+# variants at C2 size (run_ablation.py R1, the fused loss kernel specialised per gating) and
+# C5's per-rank shape (S2 sweep: 1024^2, lambda_RD = 1e-3, no phase field; D does not change the work)
+CONFIGS = {
+    "c2": (512, dict(LOSS_KW), "C2: UNet(1,1,64) bs=8/GPU 512x512 Stage-II (lambda_RD=lambda_PF=1e-4, D=5, a=0.5, "
+                               "eps=0.05) AdamW lr=1e-5"),
+    "c4-baseline": (512, dict(pde_weight=0.0, phase_field_weight=0.0), "C4 R1.0: bs=8 512x512, Dice+BCE only"),
+    "c4-rd": (512, dict(pde_weight=1e-4, phase_field_weight=0.0, diffusion_coeff=5.0, reaction_threshold=0.5),
+              "C4 R1.1: bs=8 512x512, RD only (lambda_RD=1e-4)"),
+    "c4-pf": (512, dict(pde_weight=0.0, phase_field_weight=1e-4, epsilon=0.05),
+              "C4 R1.2: bs=8 512x512, PF only (lambda_PF=1e-4)"),
+    "c4-rdpf": (512, dict(LOSS_KW), "C4 R1.3: bs=8 512x512, RD+PF"),
+    "c5": (1024, dict(pde_weight=1e-3, phase_field_weight=0.0, diffusion_coeff=5.0, reaction_threshold=0.5),
+           "C5 (per rank): bs=8 1024x1024, S2 RD only (lambda_RD=1e-3, D=5)"),
+}
 
 
 def conv_flops_per_image(H: int, W: int, c: int = 64) -> float:
@@ -180,7 +195,11 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--config", choices=sorted(CONFIGS), default="c2")
     args = ap.parse_args()
+    global H, W
+    size, loss_kw, workload = CONFIGS[args.config]
+    H = W = size
     rank, local_rank, world = init_from_env("nccl")
     device = torch.device("cuda", local_rank)
     torch.cuda.set_device(device)
@@ -190,7 +209,7 @@ def main():
     broadcast_parameters(model)
     if world > 1:
         GradBucketer(model)
-    crit = DiceBCEPDELoss(**LOSS_KW)
+    crit = DiceBCEPDELoss(**loss_kw)
     opt = AdamW(model.parameters(), lr=LR, weight_decay=1e-5, grad_scale=1.0 / world)
     x, t = make_batch(rank, device)
 
@@ -238,11 +257,12 @@ def main():
     if rank == 0:
         flops = conv_flops_per_image(H, W) * B
         out = {
-            "metric": "training images/sec (512x512, Stage-II RD+PF loss)",
+            "metric": ("training images/sec (512x512, Stage-II RD+PF loss)" if args.config == "c2"
+                       else f"training images/sec ({H}x{W}, {args.config})"),
             "value": imgs_per_s, "unit": "images/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "fp32", "data": "synthetic",
-            "config": {"workload": "C2: UNet(1,1,64) bs=8/GPU 512x512 Stage-II (lambda_RD=lambda_PF=1e-4, D=5, a=0.5, eps=0.05) AdamW lr=1e-5",
+            "config": {"workload": workload,
                        "global_batch": B * world, "image_size": [H, W], "parallelism": f"dp{world}"},
             "roofline": {"bound": "mfma", "kernel": f"gemm_nt_kernel<128, 128|64> ({DOMINANT}: the 36 batched GEMMs of Winograd F(4x4,3x3) fwd/dgrad)",
                          "achieved": achieved, "peak": peak,
@@ -260,7 +280,7 @@ def main():
                 for name, (t, nb, gbs) in loss_t.items()},
             "final_loss": float(loss.item()),
         }
-        if world == 1 and not args.no_cpu_baseline:
+        if world == 1 and not args.no_cpu_baseline and args.config == "c2":
             out["cpu_baseline"] = cpu_baseline()
         print(json.dumps(out))
     if world > 1:
