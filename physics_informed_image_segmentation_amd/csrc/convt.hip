@@ -1,0 +1,192 @@
+// ConvTranspose2d(k=2, s=2) of the U-Net decoder (src/unet.py:132-153) as lean NT GEMMs on
+// fp32 MFMA (the Winograd GEMM's pipeline, csrc/winograd.hip:gemm_nt_kernel) with the
+// transposed conv's addressing folded into the operand loads and the epilogue:
+//
+//   forward  y[b, 2i+di, 2j+dj, o] = bias[o] + sum_c x[b,i,j,c] w[di][dj][o][c]
+//            GEMM M = B*h*w input pixels, N = 4*Cout (n = (2 di + dj) Cout + o), K = Cin;
+//            A = x rows (ldx), Bt = w_ijoc rows; the epilogue scatters each 2x2 pixel block
+//            into the concat slice (ldy) and adds the bias.
+//   dgrad    dx[b,i,j,c] = [x > 0] sum_{di,dj,o} dy[b, 2i+di, 2j+dj, o] w[di][dj][o][c]
+//            GEMM M = B*h*w, N = Cin, K = 4*Cout (k = (2 di + dj) Cout + o); A gathers the 2x2
+//            output-gradient block (a 16-wide K chunk never straddles a tap when Cout % 16 == 0),
+//            Bt = w_cijo rows (pis_convt2x2_prep); the epilogue applies the ReLU mask of the
+//            convT input and optionally accumulates.
+// Block tile 128 x 128, 4 waves of 64 x 64 (2 x 2 v_mfma_f32_32x32x2_f32 tiles), K-step 16
+// through a register-staged LDS double buffer; XCD-aware tile order.
+#include "igemm.h"
+
+namespace pis {
+
+struct ConvtGemmArgs {
+  const float* a;   // x (fwd) or dy (dgrad)
+  int lda;          // channel stride of a
+  const float* bt;  // w_ijoc [4 Cout][Cin] (fwd) or w_cijo [Cin][4 Cout] (dgrad)
+  int B, h, w;      // input-pixel grid (the GEMM rows)
+  int cin, cout;
+  int M, N, K;
+  // epilogue
+  const float* bias;  // fwd
+  const float* mask;  // dgrad (PIS_MASK)
+  int ldm;
+  float* dst;
+  int ldd;
+  int flags;
+};
+
+template <int MODE>  // 0 forward, 1 input gradient
+__global__ __launch_bounds__(256, 2) void convt_gemm_kernel(ConvtGemmArgs g) {
+  constexpr int BM = 128, BN = 128, BK = 16, ROW = BK + 4;
+  constexpr int AL = BM * 4 / 256, BL = BN * 4 / 256;
+  __shared__ __attribute__((aligned(16))) float sA[2][BM * ROW];
+  __shared__ __attribute__((aligned(16))) float sB[2][BN * ROW];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave & 1, wn = wave >> 1, li = lane & 31, lh = lane >> 5;
+  const int ntn = (g.N + BN - 1) / BN;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int m0 = (bid / ntn) * BM, n0 = (bid % ntn) * BN;
+  const int q4 = (tid & 3) * 4;
+  const int hw = g.h * g.w;
+
+  // per staged A row: the source pixel (fwd: the input pixel; dgrad: the top-left of its
+  // 2x2 block in the 2h x 2w output-gradient grid)
+  int64_t arow[AL];
+  bool aok[AL];
+#pragma unroll
+  for (int i = 0; i < AL; ++i) {
+    const int m = m0 + (tid + i * 256) / 4;
+    aok[i] = m < g.M;
+    const int mm = aok[i] ? m : 0;
+    if (MODE == 0) {
+      arow[i] = mm;
+    } else {
+      const int b = mm / hw, rem = mm - b * hw, y = rem / g.w, x = rem - y * g.w;
+      arow[i] = ((int64_t)b * 2 * g.h + 2 * y) * (2 * g.w) + 2 * x;
+    }
+  }
+  f32x4 ra[AL], rb[BL];
+  auto gload = [&](int k0) {
+    int64_t tap = 0;
+    int c = k0 + q4;
+    if (MODE == 1) {  // k = (2 di + dj) Cout + o; the 16-wide chunk stays inside one tap
+      const int ij = k0 / g.cout;
+      c = k0 - ij * g.cout + q4;
+      tap = (int64_t)(ij >> 1) * (2 * g.w) + (ij & 1);
+    }
+#pragma unroll
+    for (int i = 0; i < AL; ++i) {
+      ra[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (aok[i]) ra[i] = *reinterpret_cast<const f32x4*>(g.a + (arow[i] + tap) * g.lda + c);
+    }
+#pragma unroll
+    for (int i = 0; i < BL; ++i) {
+      const int n = n0 + (tid + i * 256) / 4;
+      rb[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (n < g.N) rb[i] = *reinterpret_cast<const f32x4*>(g.bt + (size_t)n * g.K + k0 + q4);
+    }
+  };
+  auto lstore = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < AL; ++i) *reinterpret_cast<f32x4*>(&sA[buf][((tid + i * 256) / 4) * ROW + q4]) = ra[i];
+#pragma unroll
+    for (int i = 0; i < BL; ++i) *reinterpret_cast<f32x4*>(&sB[buf][((tid + i * 256) / 4) * ROW + q4]) = rb[i];
+  };
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+  const int KT = g.K / BK;
+  gload(0);
+  lstore(0);
+  __syncthreads();
+  for (int kt = 0; kt < KT; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < KT) gload((kt + 1) * BK);
+#pragma unroll
+    for (int gg = 0; gg < BK / 8; ++gg) {
+      f32x4 af[2], bf[2];
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+        af[a] = *reinterpret_cast<const f32x4*>(&sA[cur][(wm * 64 + a * 32 + li) * ROW + 8 * gg + 4 * lh]);
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+        bf[b] = *reinterpret_cast<const f32x4*>(&sB[cur][(wn * 64 + b * 32 + li) * ROW + 8 * gg + 4 * lh]);
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+          for (int b = 0; b < 2; ++b)
+            acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[a][t], bf[b][t], acc[a][b], 0, 0, 0);
+    }
+    if (kt + 1 < KT) lstore(cur ^ 1);
+    __syncthreads();
+  }
+  // forward scatter: when w % 64 == 0 the wave's 64 rows sit in one image row, so the output
+  // pixel of row m0 + wm * 64 + off is a shift of one base pixel (no per-element division)
+  const bool rowconst = MODE == 0 && g.w % 64 == 0;
+  size_t obase = 0;
+  if (rowconst) {
+    const int mb = m0 + wm * 64;
+    const int bb = mb / hw, rem = mb - bb * hw, y = rem / g.w, x = rem - y * g.w;
+    obase = ((size_t)bb * 2 * g.h + 2 * y) * (2 * g.w) + 2 * x;
+  }
+#pragma unroll
+  for (int b = 0; b < 2; ++b) {
+    const int n = n0 + wn * 64 + b * 32 + li;
+    if (n >= g.N) continue;
+    int o = n, di = 0, dj = 0;
+    float bias = 0.f;
+    if (MODE == 0) {
+      const int ij = n / g.cout;
+      o = n - ij * g.cout;
+      di = ij >> 1;
+      dj = ij & 1;
+      bias = g.bias ? g.bias[o] : 0.f;
+    }
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm * 64 + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        if (m >= g.M) continue;
+        float v = acc[a][b][r];
+        if (MODE == 0) {
+          size_t pix;
+          if (rowconst) {
+            pix = obase + (size_t)di * (2 * g.w) + 2 * (a * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh) + dj;
+          } else {
+            const int bb = m / hw, rem = m - bb * hw, y = rem / g.w, x = rem - y * g.w;
+            pix = ((size_t)bb * 2 * g.h + 2 * y + di) * (2 * g.w) + 2 * x + dj;
+          }
+          g.dst[pix * g.ldd + o] = v + bias;
+        } else {
+          if (g.flags & PIS_MASK) v = g.mask[(size_t)m * g.ldm + n] > 0.f ? v : 0.f;
+          float* d = g.dst + (size_t)m * g.ldd + n;
+          if (g.flags & PIS_ACCUMULATE) v += *d;
+          *d = v;
+        }
+      }
+  }
+}
+
+// 0 = handled, 1 = shape not covered (caller falls back to the implicit GEMM)
+int launch_convt_gemm(int mode, const float* a, int lda, const float* bt, int B, int h, int w, int cin, int cout,
+                      const float* bias, const float* mask, int ldm, float* dst, int ldd, int flags,
+                      hipStream_t s) {
+  if (tune_get(PIS_TUNE_CONVT_GEMM) == 0 || cin % 16 || cout % 16 || lda % 4) return 1;
+  ConvtGemmArgs g{};
+  g.a = a; g.lda = lda; g.bt = bt; g.B = B; g.h = h; g.w = w; g.cin = cin; g.cout = cout;
+  g.M = B * h * w;
+  g.N = mode == 0 ? 4 * cout : cin;
+  g.K = mode == 0 ? cin : 4 * cout;
+  g.bias = bias; g.mask = mask; g.ldm = ldm; g.dst = dst; g.ldd = ldd; g.flags = flags;
+  const int grid = (int)(cdiv(g.M, 128) * cdiv(g.N, 128));
+  if (mode == 0) hipLaunchKernelGGL(convt_gemm_kernel<0>, dim3(grid), dim3(256), 0, s, g);
+  else hipLaunchKernelGGL(convt_gemm_kernel<1>, dim3(grid), dim3(256), 0, s, g);
+  return launch_status(mode == 0 ? "convt_gemm_fwd" : "convt_gemm_dgrad");
+}
+
+}  // namespace pis

@@ -56,4 +56,9 @@ int launch_wino_dz(const float* dz, int ldz, int B, int H, int W, int N, float* 
 int wino_dz_blocks(int B, int H, int W, int N, int m);
 int launch_wino_wgrad_out(const float* M, int N, int C, float* dw, int accumulate, hipStream_t s, int m);
 
+// transposed-conv GEMMs (convt.hip): 0 = launched, 1 = shape not covered, < 0 = error
+int launch_convt_gemm(int mode, const float* a, int lda, const float* bt, int B, int h, int w, int cin, int cout,
+                      const float* bias, const float* mask, int ldm, float* dst, int ldd, int flags,
+                      hipStream_t s);
+
 }  // namespace pis

@@ -631,6 +631,9 @@ extern "C" int pis_convt2x2_fwd(const float* x, int ldx, const float* w_ijoc, co
   PIS_CHECK_ARG(x && w_ijoc && y && B > 0 && H > 0 && W > 0 && Cin > 0 && Cout > 0,
                 "pis_convt2x2_fwd: bad arguments");
   PIS_CHECK_ARG(Cin % 4 == 0 && ldx % 4 == 0, "pis_convt2x2_fwd: Cin/ldx must be multiples of 4");
+  const int rc = launch_convt_gemm(0, x, ldx, w_ijoc, B, H, W, Cin, Cout, bias, nullptr, 0, y, ldy, 0,
+                                   (hipStream_t)stream);
+  if (rc <= 0) return rc;
   IGemmArgs a{};
   a.src = x; a.lds = ldx; a.Hs = H; a.Ws = W; a.H = H; a.W = W; a.M = B * H * W;
   a.Csrc = Cin; a.ntaps = 1; a.tap_mode = TAP_ONE; a.wt = w_ijoc; a.ldw = Cin; a.N = 4 * Cout;
@@ -655,6 +658,9 @@ extern "C" int pis_convt2x2_dgrad(const float* dy, int lddy, const float* w_cijo
                 "pis_convt2x2_dgrad: bad arguments");
   PIS_CHECK_ARG(Cout % 4 == 0 && lddy % 4 == 0, "pis_convt2x2_dgrad: Cout/lddy must be multiples of 4");
   PIS_CHECK_ARG(!(flags & PIS_MASK) || mask, "pis_convt2x2_dgrad: PIS_MASK without mask");
+  const int rc = launch_convt_gemm(1, dy, lddy, w_cijo, B, H, W, Cin, Cout, nullptr, mask, ldm, dx, lddx,
+                                   flags & (PIS_MASK | PIS_ACCUMULATE), (hipStream_t)stream);
+  if (rc <= 0) return rc;
   IGemmArgs a{};
   a.src = dy; a.lds = lddy; a.Hs = 2 * H; a.Ws = 2 * W; a.H = H; a.W = W; a.M = B * H * W;
   a.Csrc = Cout; a.ntaps = 4; a.tap_mode = TAP_UP2; a.wt = w_cijo; a.ldw = 4 * Cout; a.N = Cin;
