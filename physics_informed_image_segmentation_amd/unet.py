@@ -21,6 +21,7 @@ Memory layout (MI355X-first):
 """
 from __future__ import annotations
 
+import os
 from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
 import torch
@@ -310,6 +311,12 @@ class UNetEngine:
     reporting the finished arena range to ``model.grad_ready_hook`` (the DDP
     bucket trigger)."""
 
+    # weight gradients on a second HIP stream: they depend only on (x, dz) and write their own
+    # arena slice, so they overlap the input-gradient chain (the critical path), whose
+    # transforms are HBM-bound while the weight-gradient GEMMs are MFMA-bound
+    # (PIS_SIDE_STREAM=0 serialises them on the caller's stream, for A/B measurements)
+    side_stream = os.environ.get("PIS_SIDE_STREAM", "1") != "0"
+
     def __init__(self, model: UNet):
         self.m = model
         self.c = model.base_channels
@@ -359,6 +366,9 @@ class UNetEngine:
         ws = max(ws, lib.pis_conv3x3_wgrad_ws(B, H5, W5, 8 * c, 8 * c), lib.pis_conv3x3_ex_ws(B, H5, W5, 8 * c, 8 * c))
         self.ws = torch.empty((ws + 15) // 4, dtype=torch.float32, device=dev)
         self.ws_bytes = self.ws.numel() * 4
+        # weight gradients run on a second stream beside the input-gradient chain (backward)
+        self.ws2 = torch.empty_like(self.ws) if self.side_stream else self.ws
+        self.side = torch.cuda.Stream(device=dev) if self.side_stream else None
         # per-layer kept Winograd input transforms (training forward -> weight gradient);
         # ~2.25x each layer's input activation, ~12 GB at B=8 512^2
         self.keep: Dict[int, torch.Tensor] = {}
@@ -528,7 +538,24 @@ class UNetEngine:
         acc = PIS_ACCUMULATE if mode == "accumulate" else 0
         st = self._stream()
         ws, wsb = self.ws.data_ptr(), self.ws_bytes
+        ws2 = self.ws2.data_ptr()
+        main = torch.cuda.current_stream()
+        side = self.side if self.side is not None else main
+        sst = side.cuda_stream
+        if side is not main:
+            side.wait_stream(main)  # forward activations, kept transforms, a zeroed scratch arena
         gb = self._gbuf
+
+        def to_side():
+            """Order the side stream after everything enqueued on the main stream so far."""
+            if side is not main:
+                ev = torch.cuda.Event()
+                ev.record(main)
+                side.wait_event(ev)
+
+        def ready_on_side(*params):
+            with torch.cuda.stream(side):  # DDP buckets all-reduce after their weight gradients
+                self._ready(*params)
 
         # dgrad operands, rebuilt from the current weights
         flips = {}
@@ -548,9 +575,10 @@ class UNetEngine:
             flips[id(up)] = t
 
         def conv_bwd(conv, x: _Buf, dz: _Buf, dx: Optional[_Buf], Hl, Wl, mask: Optional[_Buf], scale):
+            to_side()
             call("pis_conv3x3_wgrad_keep", x.p, x.ld, dz.p, dz.ld, self._gptr(conv.weight), self._gptr(conv.bias),
-                 B, Hl, Wl, conv.in_channels, conv.out_channels, acc, ws, wsb, ptr(self.keep.get(id(conv))), st)
-            self._ready(conv.weight, conv.bias)
+                 B, Hl, Wl, conv.in_channels, conv.out_channels, acc, ws2, wsb, ptr(self.keep.get(id(conv))), sst)
+            ready_on_side(conv.weight, conv.bias)
             if dx is not None:
                 flags = (PIS_MASK if mask is not None else 0) | (PIS_SCALE if scale is not None else 0)
                 call("pis_conv3x3_dgrad_ex", dz.p, dz.ld, flips[id(conv)].data_ptr(),
@@ -591,9 +619,10 @@ class UNetEngine:
             else:
                 xin = _Buf(bf[f"d1_{l + 1}"], up.in_channels)
             Hh, Wh = Hl // 2, Wl // 2
+            to_side()
             call("pis_convt2x2_wgrad", xin.p, xin.ld, g_cat.p, g_cat.ld, self._gptr(up.weight), self._gptr(up.bias),
-                 B, Hh, Wh, up.in_channels, up.out_channels, acc, ws, wsb, st)
-            self._ready(up.weight, up.bias)
+                 B, Hh, Wh, up.in_channels, up.out_channels, acc, ws2, wsb, sst)
+            ready_on_side(up.weight, up.bias)
             g_in = _Buf(gb(f"g_upin{l}", B, Hh, Wh, up.in_channels), up.in_channels)
             call("pis_convt2x2_dgrad", g_cat.p, g_cat.ld, flips[id(up)].data_ptr(), xin.p, xin.ld, g_in.p, g_in.ld,
                  B, Hh, Wh, up.in_channels, up.out_channels, PIS_MASK, st)
@@ -626,7 +655,10 @@ class UNetEngine:
         if m.grad_ready_hook is not None:
             if mode == "scratch":
                 raise RuntimeError("data-parallel gradients need zero_grad() before every backward")
-            m.grad_ready_hook.finish()
+            with torch.cuda.stream(side):
+                m.grad_ready_hook.finish()
+        if side is not main:
+            main.wait_stream(side)  # the optimizer (and the next forward) see every weight gradient
         if mode == "accumulate":
             return [None] * len(m._entries)
         g = self.garena
