@@ -226,6 +226,13 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    # roofline of the dominant kernel, live over the timed region: HIP events recorded on the
+    # launch stream right around each of its launches (pis_set_launch_hook), and around the
+    # fused-loss C-ABI calls (host-side enqueue only; the GPU stays the bottleneck)
+    from physics_informed_image_segmentation_amd import _hip
+    ktimer, ltimer = KernelTimer(), LossCallTimer()
+    _hip.set_launch_hook(ktimer)
+    _hip.set_tracer(ltimer)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = step()
@@ -241,17 +248,22 @@ def main():
     ms = dt / args.steps * 1e3
     imgs_per_s = world * B * args.steps / dt
 
-    # roofline of the dominant kernel: one instrumented step after the timed region
-    from physics_informed_image_segmentation_amd import _hip
-    ktimer, ltimer = KernelTimer(), LossCallTimer()
-    _hip.set_launch_hook(ktimer)
-    _hip.set_tracer(ltimer)
-    step()
     _hip.set_tracer(None)
     _hip.set_launch_hook(None)
     n_launch, flop_per_launch, ms_per_launch = ktimer.summary()
+    n_launch //= args.steps
     loss_t = ltimer.summary()
     achieved = flop_per_launch / (ms_per_launch * 1e-3) / 1e12
+    # the same kernel with the weight gradients serialised on one stream (no concurrent
+    # kernel sharing the CUs): one extra instrumented step after the timed region
+    eng = model.engine()
+    side, eng.side = eng.side, None
+    iso = KernelTimer()
+    _hip.set_launch_hook(iso)
+    step()
+    _hip.set_launch_hook(None)
+    eng.side = side
+    _, iso_flop, iso_ms = iso.summary()
     peak = 157.3  # fp32 MFMA dense TFLOP/s (MI355X_MICROARCH.md)
     traffic = load_pmc_traffic()
     if rank == 0:
@@ -268,12 +280,17 @@ def main():
                          "achieved": achieved, "peak": peak,
                          "unit": "TFLOP/s", "frac": achieved / peak, "traffic": traffic,
                          "launches_per_step": n_launch, "avg_launch_ms": ms_per_launch,
-                         "flop_per_launch": flop_per_launch},
+                         "flop_per_launch": flop_per_launch,
+                         "measured": "live over the timed steps; the input-gradient launches share the GPU "
+                                     "with the weight-gradient stream",
+                         "isolated": {"achieved": iso_flop / (iso_ms * 1e-3) / 1e12,
+                                      "frac": iso_flop / (iso_ms * 1e-3) / 1e12 / peak, "avg_launch_ms": iso_ms,
+                                      "measured": "one extra step, weight gradients serialised"}},
             # direct-convolution FLOPs of the step / step time (Winograd executes fewer)
             "step_tflops_direct_equiv": flops / (ms * 1e-3) / 1e12,
-            # north-star HBM figure for the fused loss: the backward runs inside the head
-            # backward kernel (its reduce_slabs follow-ups inside the events); the forward's
-            # time includes its one-block finalize launch
+            # north-star HBM figure for the fused loss (live over the timed steps): the backward
+            # runs inside the head backward kernel (its reduce_slabs follow-ups inside the
+            # events); the forward's time includes its one-block finalize launch
             "roofline_loss": {
                 name.replace("pis_", ""): {"bound": "hbm", "achieved": gbs, "peak": 8000.0, "unit": "GB/s",
                                            "frac": gbs / 8000.0, "bytes_per_call": nb, "avg_call_ms": t}
