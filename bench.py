@@ -196,6 +196,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--config", choices=sorted(CONFIGS), default="c2")
+    ap.add_argument("--tune", action="append", default=[], metavar="KEY=VALUE",
+                    help="pis_tune knob for experiments (include/pis_capi.h PIS_TUNE_*); defaults are the measured best")
     args = ap.parse_args()
     global H, W
     size, loss_kw, workload = CONFIGS[args.config]
@@ -204,6 +206,11 @@ def main():
     device = torch.device("cuda", local_rank)
     torch.cuda.set_device(device)
 
+    if args.tune:
+        from physics_informed_image_segmentation_amd import _hip as _h
+        for kv in args.tune:
+            k, v = (int(z) for z in kv.split("="))
+            _h.lib().pis_tune(k, v)
     torch.manual_seed(42)
     model = UNet(1, 1, 64).to(device).train()
     broadcast_parameters(model)
