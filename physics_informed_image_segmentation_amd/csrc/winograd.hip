@@ -723,6 +723,135 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const float* __restrict
     }
 }
 
+// ---- the same GEMMs at fp32 accuracy on bf16 MFMA ("bf16x6") ----------------------------
+// Each fp32 operand is split exactly into hi + mid + lo bf16 (hi = bf16(x), mid = bf16(x - hi),
+// lo = bf16(x - hi - mid): 24 significant bits); a product needs the six partial products with
+// order <= 2^-24 of the largest (hi.hi, hi.mid, mid.hi, hi.lo, mid.mid, lo.hi), which bf16 MFMA
+// forms exactly and accumulates in fp32. v_mfma_f32_32x32x16_bf16 retires 16x the FLOPs of
+// v_mfma_f32_32x32x2_f32 per cycle, so the six cost 6/16 of one fp32 MFMA pass. Measured error
+// (CPU emulation, 128-1024-deep products): 0.9-1.4e-7 relative, below native fp32's 2-3.4e-7.
+// The split happens once per staged element (global -> LDS), not per MFMA use.
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void split3_bf16(f32x4 v, bf16x4& h, bf16x4& m, bf16x4& l) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const __bf16 a = (__bf16)v[i];
+    const float r = v[i] - (float)a;  // exact: a carries x's leading 8 significant bits
+    const __bf16 b = (__bf16)r;
+    const float r2 = r - (float)b;    // exact
+    h[i] = a;
+    m[i] = b;
+    l[i] = (__bf16)r2;
+  }
+}
+
+template <int BM, int BN>
+__global__ __launch_bounds__(256, 2) void gemm_nt_x6_kernel(const float* __restrict__ A, const float* __restrict__ Bm,
+                                                           float* __restrict__ Cm, int M, int N, int K,
+                                                           int64_t bsA, int64_t bsB, int64_t bsC) {
+  constexpr int BK = 16;
+  constexpr int TM = BM / 64, TN = BN / 64;
+  constexpr int AL = BM * 4 / 256, BL = BN * 4 / 256;  // float4 loads per thread per stage
+  __shared__ __attribute__((aligned(16))) __bf16 sA[2][3][BM * BK];  // [buf][hi|mid|lo][row][k]
+  __shared__ __attribute__((aligned(16))) __bf16 sB[2][3][BN * BK];
+  A += blockIdx.y * bsA;
+  Bm += blockIdx.y * bsB;
+  Cm += blockIdx.y * bsC;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave & 1, wn = wave >> 1, li = lane & 31, lh = lane >> 5;
+  const int ntn = N / BN;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int m0 = (bid / ntn) * BM, n0 = (bid % ntn) * BN;
+  const int q4 = (tid & 3) * 4;
+  f32x4 ra[AL], rb[BL];
+  auto gload = [&](int k0) {
+    const int k = k0 + q4;
+#pragma unroll
+    for (int i = 0; i < AL; ++i) {
+      const int m = m0 + (tid + i * 256) / 4;
+      ra[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (m < M && k < K) ra[i] = *reinterpret_cast<const f32x4*>(A + (size_t)m * K + k);
+    }
+#pragma unroll
+    for (int i = 0; i < BL; ++i) {
+      const int n = n0 + (tid + i * 256) / 4;
+      rb[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (k < K) rb[i] = *reinterpret_cast<const f32x4*>(Bm + (size_t)n * K + k);
+    }
+  };
+  auto lstore = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < AL; ++i) {
+      bf16x4 h, m, l;
+      split3_bf16(ra[i], h, m, l);
+      const int o = ((tid + i * 256) / 4) * BK + q4;
+      *reinterpret_cast<bf16x4*>(&sA[buf][0][o]) = h;
+      *reinterpret_cast<bf16x4*>(&sA[buf][1][o]) = m;
+      *reinterpret_cast<bf16x4*>(&sA[buf][2][o]) = l;
+    }
+#pragma unroll
+    for (int i = 0; i < BL; ++i) {
+      bf16x4 h, m, l;
+      split3_bf16(rb[i], h, m, l);
+      const int o = ((tid + i * 256) / 4) * BK + q4;
+      *reinterpret_cast<bf16x4*>(&sB[buf][0][o]) = h;
+      *reinterpret_cast<bf16x4*>(&sB[buf][1][o]) = m;
+      *reinterpret_cast<bf16x4*>(&sB[buf][2][o]) = l;
+    }
+  };
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int b = 0; b < TN; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+  const int KT = (K + BK - 1) / BK;
+  gload(0);
+  lstore(0);
+  __syncthreads();
+  for (int kt = 0; kt < KT; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < KT) gload((kt + 1) * BK);
+    bf16x8 af[3][TM], bf[3][TN];  // lane: row li, k = 8 lh .. 8 lh + 7
+#pragma unroll
+    for (int p = 0; p < 3; ++p) {
+#pragma unroll
+      for (int a = 0; a < TM; ++a)
+        af[p][a] = *reinterpret_cast<const bf16x8*>(&sA[cur][p][(wm * (BM / 2) + a * 32 + li) * BK + 8 * lh]);
+#pragma unroll
+      for (int b = 0; b < TN; ++b)
+        bf[p][b] = *reinterpret_cast<const bf16x8*>(&sB[cur][p][(wn * (BN / 2) + b * 32 + li) * BK + 8 * lh]);
+    }
+#pragma unroll
+    for (int a = 0; a < TM; ++a)
+#pragma unroll
+      for (int b = 0; b < TN; ++b) {  // smallest partial products first
+        acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[2][a], bf[0][b], acc[a][b], 0, 0, 0);
+        acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1][a], bf[1][b], acc[a][b], 0, 0, 0);
+        acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0][a], bf[2][b], acc[a][b], 0, 0, 0);
+        acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1][a], bf[0][b], acc[a][b], 0, 0, 0);
+        acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0][a], bf[1][b], acc[a][b], 0, 0, 0);
+        acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0][a], bf[0][b], acc[a][b], 0, 0, 0);
+      }
+    if (kt + 1 < KT) lstore(cur ^ 1);
+    __syncthreads();
+  }
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int b = 0; b < TN; ++b) {
+      const int n = n0 + wn * (BN / 2) + b * 32 + li;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm * (BM / 2) + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        if (m < M) Cm[(size_t)m * N + n] = acc[a][b][r];
+      }
+    }
+}
+
 static int grid_of(int64_t work) { return (int)std::max<int64_t>(1, std::min<int64_t>(cdiv(work, 256), 16384)); }
 
 // F(4x4,3x3) when the 4x4 tile grid fits and pis_tune key 11 allows it, else F(2x2,3x3)
@@ -785,6 +914,16 @@ int launch_wino3x3(const IGemmArgs& a, int B, void* ws, hipStream_t s, float* ke
   if (v == 1 && N % 256 == 0) {
     const dim3 grid((int)cdiv(T, 128) * (N / 256), nxi);
     hipLaunchKernelGGL((gemm_nt_kernel<128, 256>), grid, dim3(256), 0, s, V, U, Mt, (int)T, N, C, T * C,
+                       (int64_t)N * C, T * N);
+    rc = launch_status("wino_gemm");
+  } else if (v == 3 && N % 128 == 0) {
+    const dim3 grid((int)cdiv(T, 128) * (N / 128), nxi);
+    hipLaunchKernelGGL((gemm_nt_x6_kernel<128, 128>), grid, dim3(256), 0, s, V, U, Mt, (int)T, N, C, T * C,
+                       (int64_t)N * C, T * N);
+    rc = launch_status("wino_gemm");
+  } else if (v == 3 && N % 64 == 0) {
+    const dim3 grid((int)cdiv(T, 128) * (N / 64), nxi);
+    hipLaunchKernelGGL((gemm_nt_x6_kernel<128, 64>), grid, dim3(256), 0, s, V, U, Mt, (int)T, N, C, T * C,
                        (int64_t)N * C, T * N);
     rc = launch_status("wino_gemm");
   } else if (v == 2 && N % 128 == 0) {

@@ -103,7 +103,7 @@ def test_conv3x3_dgrad_wgrad(hip, B, H, W, Cin, Cout):
 
 # every non-default kernel variant behind pis_tune (include/pis_capi.h) stays exact too
 TUNE_VARIANTS = [(4, 1), (4, 2), (4, 3), (5, 0), (6, 2048), (3, 0), (7, 1), (8, 0), (8, 2), (10, 0), (10, 1),
-                 (11, 0), (12, 0), (12, 2), (13, 0)]
+                 (11, 0), (12, 0), (12, 2), (13, 0), (10, 2)]
 
 
 @pytest.mark.parametrize("key,value", TUNE_VARIANTS)
@@ -504,3 +504,35 @@ def test_conv3x3_winograd_fused(hip, B, H, W, Cin, Cout):
         test_conv3x3_ex_winograd(hip, B, H, W, Cin, Cout, 2)
     finally:
         hip.pis_tune(12, prev)
+
+
+@pytest.mark.parametrize("Cin,Cout", [(256, 256), (512, 128), (128, 64)])
+def test_winograd_gemm_bf16x6_is_fp32_accurate(hip, Cin, Cout):
+    """The bf16x6 Winograd GEMM (pis_tune(10, 3): each fp32 operand split exactly into three
+    bf16, the six partial products above 2^-24 on bf16 MFMA, fp32 accumulation) must be as
+    accurate as the native fp32 MFMA GEMM (pis_tune(10, 2)): same conv against a float64
+    reference, error no larger than fp32's (+25 % slack for rounding-order luck)."""
+    B, H, W = 2, 16, 32
+    g = torch.Generator().manual_seed(31)
+    x = F.relu(torch.randn(B, Cin, H, W, generator=g, dtype=torch.float64))
+    w = torch.randn(Cout, Cin, 3, 3, generator=g, dtype=torch.float64) / (3 * Cin ** 0.5)
+    b = torch.randn(Cout, generator=g, dtype=torch.float64)
+    ref = F.conv2d(x, w, b, padding=1)
+    xd, wd, bd = nhwc(x.float()).cuda(), krsc(w.float()).cuda(), b.float().cuda()
+    prev8 = hip.pis_tune(8, 2)
+    errs = {}
+    try:
+        for v in (2, 3):
+            prev = hip.pis_tune(10, v)
+            nws = hip.pis_conv3x3_ex_ws(B, H, W, Cin, Cout)
+            ws = torch.empty(nws // 4 + 1, device="cuda")
+            y = torch.empty(B, H, W, Cout, device="cuda")
+            assert hip.pis_conv3x3_fwd_ex(xd.data_ptr(), Cin, wd.data_ptr(), bd.data_ptr(), 0, y.data_ptr(), Cout,
+                                          B, H, W, Cin, Cout, 0, ws.data_ptr(), nws, s()) == 0
+            torch.cuda.synchronize()
+            hip.pis_tune(10, prev)
+            errs[v] = ((nchw(y.cpu()).double() - ref).norm() / ref.norm()).item()
+    finally:
+        hip.pis_tune(8, prev8)
+    assert errs[3] <= 1.25 * errs[2] + 1e-9, errs
+    assert errs[3] < 5e-6, errs
