@@ -75,7 +75,7 @@ def conv_flops_per_image(H: int, W: int, c: int = 64) -> float:
 # of the Winograd 3x3 convs (forward + input gradient), launched as "wino_gemm" by the C-ABI
 # (csrc/winograd.hip) and named gemm_nt_kernel<128, 128> / <128, 64> by rocprofv3.
 DOMINANT = "wino_gemm"
-DOMINANT_KERNEL = "gemm_nt_kernel<"
+DOMINANT_KERNEL = "gemm_nt_kernel<"  # rocprofv3 name stem; gemm_nt_x6_kernel< on the bf16x6 pipe (key 10 = 3)
 
 
 def loss_call_bytes(name, a):
@@ -147,7 +147,7 @@ class LossCallTimer:
         return out
 
 
-def load_pmc_traffic():
+def load_pmc_traffic(kernel=DOMINANT_KERNEL):
     """Per-launch HBM bytes of the dominant kernel from the committed rocprofv3 --pmc
     summary (tools/pmc_summary.py, FETCH_SIZE x2 gfx950 correction + WRITE_SIZE)."""
     path = os.path.join(HERE, "profiles", "pmc_dominant.json")
@@ -155,7 +155,7 @@ def load_pmc_traffic():
         return None
     with open(path) as f:
         d = json.load(f)
-    if DOMINANT_KERNEL not in (d.get("dominant_kernel") or ""):
+    if kernel not in (d.get("dominant_kernel") or ""):
         return None  # counters were taken on another kernel: report no traffic rather than a stale one
     return d.get("hbm_bytes_per_launch")
 
@@ -271,8 +271,16 @@ def main():
     _hip.set_launch_hook(None)
     eng.side = side
     _, iso_flop, iso_ms = iso.summary()
-    peak = 157.3  # fp32 MFMA dense TFLOP/s (MI355X_MICROARCH.md)
-    traffic = load_pmc_traffic()
+    # the pipe the dominant kernel runs on: fp32-accurate GEMMs via bf16x6 (pis_tune key 10 = 3,
+    # the default) execute six bf16 MFMAs per fp32 multiply-add, so their roofline is the dense
+    # bf16 MFMA peak (~2.5 PFLOP/s, MI355X_MICROARCH.md / the task's dense figure) / 6 in
+    # fp32-equivalent FLOPs; the native fp32 MFMA path (key 10 = 2) peaks at 157.3 TFLOP/s
+    x6 = _hip.lib().pis_tune(10, -1) == 3
+    peak = 2500.0 / 6.0 if x6 else 157.3
+    pipe = ("bf16 MFMA, fp32-accurate bf16x6 split (6 bf16 products per fp32 multiply-add); achieved/peak in "
+            "fp32-equivalent FLOPs" if x6 else "fp32 MFMA")
+    kname = "gemm_nt_x6_kernel<" if x6 else DOMINANT_KERNEL
+    traffic = load_pmc_traffic(kname)
     if rank == 0:
         flops = conv_flops_per_image(H, W) * B
         out = {
@@ -283,9 +291,10 @@ def main():
             "vs_baseline": None, "dtype": "fp32", "data": "synthetic",
             "config": {"workload": workload,
                        "global_batch": B * world, "image_size": [H, W], "parallelism": f"dp{world}"},
-            "roofline": {"bound": "mfma", "kernel": f"gemm_nt_kernel<128, 128|64> ({DOMINANT}: the 36 batched GEMMs of Winograd F(4x4,3x3) fwd/dgrad)",
+            "roofline": {"bound": "mfma", "kernel": f"{kname}128, 128|64> ({DOMINANT}: the 36 batched GEMMs of Winograd F(4x4,3x3) fwd/dgrad)",
                          "achieved": achieved, "peak": peak,
-                         "unit": "TFLOP/s", "frac": achieved / peak, "traffic": traffic,
+                         "unit": "TFLOP/s", "frac": achieved / peak, "traffic": traffic, "pipe": pipe,
+                         "fp32_mfma_peak_frac": achieved / 157.3,
                          "launches_per_step": n_launch, "avg_launch_ms": ms_per_launch,
                          "flop_per_launch": flop_per_launch,
                          "measured": "live over the timed steps; the input-gradient launches share the GPU "

@@ -68,9 +68,12 @@ int pis_version(void);
 #define PIS_TUNE_WINO_FUSED 12   /* F(4x4,3x3) fwd/dgrad as ONE fused kernel (transforms in LDS/registers): 0/1 off
                                     (auto: measured slower than the 3-pass pipeline on every layer that keeps V),
                                     2 whenever H % 16 == W % 64 == N % 16 == 0 */
-#define PIS_TUNE_CONVT_GEMM 13   /* transposed conv fwd/dgrad: 1 (default) lean NT GEMM with gather/scatter addressing
-                                    when Cin, Cout % 16 == 0; 0 generic implicit GEMM */
-#define PIS_TUNE_NKEYS 14
+#define PIS_TUNE_CONVT_GEMM 13   /* transposed conv fwd/dgrad: lean NT GEMM with gather/scatter addressing when
+                                    Cin, Cout % 16 == 0 — 1 (default) fp32-accurate bf16x6 on bf16 MFMA, 2 on fp32
+                                    MFMA; 0 generic implicit GEMM */
+#define PIS_TUNE_WGRAD_X6 14     /* Winograd and transposed-conv weight-gradient GEMMs: 1 (default) fp32-accurate
+                                    bf16x6 on bf16 MFMA, 0 fp32 MFMA */
+#define PIS_TUNE_NKEYS 15
 #define PIS_DEBUG_NOLOAD (1 << 16)
 int pis_tune(int key, int value);
 

@@ -11,8 +11,9 @@
 //            output-gradient block (a 16-wide K chunk never straddles a tap when Cout % 16 == 0),
 //            Bt = w_cijo rows (pis_convt2x2_prep); the epilogue applies the ReLU mask of the
 //            convT input and optionally accumulates.
-// Block tile 128 x 128, 4 waves of 64 x 64 (2 x 2 v_mfma_f32_32x32x2_f32 tiles), K-step 16
-// through a register-staged LDS double buffer; XCD-aware tile order.
+// Block tile 128 x 128, 4 waves of 64 x 64 (2 x 2 32x32 MFMA tiles), K-step 16 through a
+// register-staged LDS double buffer; XCD-aware tile order. pis_tune key 13: 1 (default) bf16x6
+// on bf16 MFMA (fp32-accurate), 2 native fp32 MFMA, 0 off (implicit-GEMM fallback).
 #include "igemm.h"
 
 namespace pis {
@@ -33,12 +34,32 @@ struct ConvtGemmArgs {
   int flags;
 };
 
-template <int MODE>  // 0 forward, 1 input gradient
+typedef __bf16 cbf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 cbf16x4 __attribute__((ext_vector_type(4)));
+
+// exact 3-way bf16 split of four fp32 values (as split3_bf16 in winograd.hip)
+__device__ __forceinline__ void csplit3(f32x4 v, cbf16x4& h, cbf16x4& m, cbf16x4& l) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const __bf16 a = (__bf16)v[i];
+    const float r = v[i] - (float)a;
+    const __bf16 b = (__bf16)r;
+    h[i] = a;
+    m[i] = b;
+    l[i] = (__bf16)(r - (float)b);
+  }
+}
+
+// X6: the operands are split into hi/mid/lo bf16 planes at LDS staging and every fp32
+// multiply-add becomes six bf16 MFMA partial products (fp32 accuracy, see gemm_nt_x6_kernel)
+template <int MODE, bool X6>  // MODE 0 forward, 1 input gradient
 __global__ __launch_bounds__(256, 2) void convt_gemm_kernel(ConvtGemmArgs g) {
   constexpr int BM = 128, BN = 128, BK = 16, ROW = BK + 4;
   constexpr int AL = BM * 4 / 256, BL = BN * 4 / 256;
-  __shared__ __attribute__((aligned(16))) float sA[2][BM * ROW];
-  __shared__ __attribute__((aligned(16))) float sB[2][BN * ROW];
+  // LDS image per buffer: fp32 [row][ROW], or (X6) bf16 [hi|mid|lo][row][16] in the same floats
+  constexpr int SA = X6 ? 3 * BM * BK / 2 : BM * ROW, SB = X6 ? 3 * BN * BK / 2 : BN * ROW;
+  __shared__ __attribute__((aligned(16))) float sA[2][SA];
+  __shared__ __attribute__((aligned(16))) float sB[2][SB];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave & 1, wn = wave >> 1, li = lane & 31, lh = lane >> 5;
   const int ntn = (g.N + BN - 1) / BN;
@@ -85,10 +106,33 @@ __global__ __launch_bounds__(256, 2) void convt_gemm_kernel(ConvtGemmArgs g) {
     }
   };
   auto lstore = [&](int buf) {
+    if constexpr (X6) {
+      __bf16* pa = reinterpret_cast<__bf16*>(sA[buf]);
+      __bf16* pb = reinterpret_cast<__bf16*>(sB[buf]);
 #pragma unroll
-    for (int i = 0; i < AL; ++i) *reinterpret_cast<f32x4*>(&sA[buf][((tid + i * 256) / 4) * ROW + q4]) = ra[i];
+      for (int i = 0; i < AL; ++i) {
+        cbf16x4 h, m, l;
+        csplit3(ra[i], h, m, l);
+        const int o = ((tid + i * 256) / 4) * BK + q4;
+        *reinterpret_cast<cbf16x4*>(pa + o) = h;
+        *reinterpret_cast<cbf16x4*>(pa + BM * BK + o) = m;
+        *reinterpret_cast<cbf16x4*>(pa + 2 * BM * BK + o) = l;
+      }
 #pragma unroll
-    for (int i = 0; i < BL; ++i) *reinterpret_cast<f32x4*>(&sB[buf][((tid + i * 256) / 4) * ROW + q4]) = rb[i];
+      for (int i = 0; i < BL; ++i) {
+        cbf16x4 h, m, l;
+        csplit3(rb[i], h, m, l);
+        const int o = ((tid + i * 256) / 4) * BK + q4;
+        *reinterpret_cast<cbf16x4*>(pb + o) = h;
+        *reinterpret_cast<cbf16x4*>(pb + BN * BK + o) = m;
+        *reinterpret_cast<cbf16x4*>(pb + 2 * BN * BK + o) = l;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < AL; ++i) *reinterpret_cast<f32x4*>(&sA[buf][((tid + i * 256) / 4) * ROW + q4]) = ra[i];
+#pragma unroll
+      for (int i = 0; i < BL; ++i) *reinterpret_cast<f32x4*>(&sB[buf][((tid + i * 256) / 4) * ROW + q4]) = rb[i];
+    }
   };
   f32x16 acc[2][2];
 #pragma unroll
@@ -104,6 +148,31 @@ __global__ __launch_bounds__(256, 2) void convt_gemm_kernel(ConvtGemmArgs g) {
   for (int kt = 0; kt < KT; ++kt) {
     const int cur = kt & 1;
     if (kt + 1 < KT) gload((kt + 1) * BK);
+    if constexpr (X6) {
+      const __bf16* pa = reinterpret_cast<const __bf16*>(sA[cur]);
+      const __bf16* pb = reinterpret_cast<const __bf16*>(sB[cur]);
+      cbf16x8 af[3][2], bf[3][2];  // lane: row li, k = 8 lh .. 8 lh + 7
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+          af[p][a] = *reinterpret_cast<const cbf16x8*>(pa + p * BM * BK + (wm * 64 + a * 32 + li) * BK + 8 * lh);
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+          bf[p][b] = *reinterpret_cast<const cbf16x8*>(pb + p * BN * BK + (wn * 64 + b * 32 + li) * BK + 8 * lh);
+      }
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {  // smallest partial products first
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[2][a], bf[0][b], acc[a][b], 0, 0, 0);
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1][a], bf[1][b], acc[a][b], 0, 0, 0);
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0][a], bf[2][b], acc[a][b], 0, 0, 0);
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1][a], bf[0][b], acc[a][b], 0, 0, 0);
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0][a], bf[1][b], acc[a][b], 0, 0, 0);
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0][a], bf[0][b], acc[a][b], 0, 0, 0);
+        }
+    } else {
 #pragma unroll
     for (int gg = 0; gg < BK / 8; ++gg) {
       f32x4 af[2], bf[2];
@@ -120,6 +189,7 @@ __global__ __launch_bounds__(256, 2) void convt_gemm_kernel(ConvtGemmArgs g) {
 #pragma unroll
           for (int b = 0; b < 2; ++b)
             acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[a][t], bf[b][t], acc[a][b], 0, 0, 0);
+    }
     }
     if (kt + 1 < KT) lstore(cur ^ 1);
     __syncthreads();
@@ -184,8 +254,11 @@ int launch_convt_gemm(int mode, const float* a, int lda, const float* bt, int B,
   g.K = mode == 0 ? cin : 4 * cout;
   g.bias = bias; g.mask = mask; g.ldm = ldm; g.dst = dst; g.ldd = ldd; g.flags = flags;
   const int grid = (int)(cdiv(g.M, 128) * cdiv(g.N, 128));
-  if (mode == 0) hipLaunchKernelGGL(convt_gemm_kernel<0>, dim3(grid), dim3(256), 0, s, g);
-  else hipLaunchKernelGGL(convt_gemm_kernel<1>, dim3(grid), dim3(256), 0, s, g);
+  const bool x6 = tune_get(PIS_TUNE_CONVT_GEMM) == 1;
+  if (mode == 0 && x6) hipLaunchKernelGGL((convt_gemm_kernel<0, true>), dim3(grid), dim3(256), 0, s, g);
+  else if (mode == 0) hipLaunchKernelGGL((convt_gemm_kernel<0, false>), dim3(grid), dim3(256), 0, s, g);
+  else if (x6) hipLaunchKernelGGL((convt_gemm_kernel<1, true>), dim3(grid), dim3(256), 0, s, g);
+  else hipLaunchKernelGGL((convt_gemm_kernel<1, false>), dim3(grid), dim3(256), 0, s, g);
   return launch_status(mode == 0 ? "convt_gemm_fwd" : "convt_gemm_dgrad");
 }
 

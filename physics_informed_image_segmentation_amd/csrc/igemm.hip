@@ -509,8 +509,10 @@ static bool wino_wanted_dims(int H, int W, int C, int N) {
   // measured (tools/bench_kernels.py --key 8 --variants 1,2 --ops fwd,dgrad, B=8):
   // F(4x4,3x3) beats the direct halo kernels from 128 channels on either side (dec1.conv0
   // fwd -22 %, dgrad -27 %; enc2.conv1 -41 %) and only loses at 64 -> 64 (+1.5-3 %);
-  // F(2x2,3x3) needs >= 256 contraction channels and 128 outputs
-  if (wino_tile(H, W) == 4) return C >= 128 || N >= 128;
+  // F(2x2,3x3) needs >= 256 contraction channels and 128 outputs. With the bf16x6 GEMMs
+  // (key 10 = 3) F(4x4,3x3) also wins at 64 -> 64 (enc1.conv1 fwd -13 %, dgrad -11 %).
+  if (wino_tile(H, W) == 4)
+    return C >= 128 || N >= 128 || (tune_get(PIS_TUNE_WINO_TILE) == 3 && C >= 64 && N >= 64);
   return C >= 256 && N >= 128;
 }
 

@@ -498,11 +498,184 @@ static float* bias_slabs(void* ws, const WgradPlan& pl) {
 
 static size_t wgrad_ws_bytes(const WgradPlan& pl) { return cdiv(pl.part_bytes, 256) * 256 + pl.bias_bytes + 256; }
 
+// The same split-K contraction at fp32 accuracy on bf16 MFMA (bf16x6, as gemm_nt_x6_kernel in
+// winograd.hip) for plain row operands B (the Winograd weight gradient: A = E[t][Cout],
+// B = V[t][Cin]). The pixel (K) axis is the row index in memory, so each thread
+// loads one column (m or n) over 8 (or 4) consecutive pixels with coalesced scalar loads and
+// writes the three bf16 planes K-contiguous ([m][16 k], one 16-B / 8-B LDS store per plane):
+// the MFMA operand fragment (8 consecutive k of one row) is then a single ds_read_b128.
+// Also the transposed-conv weight gradient (a_up2 rows, bias column sums of A).
+typedef __bf16 wbf16x8 __attribute__((ext_vector_type(8)));
+
+template <int E>
+__device__ __forceinline__ void wsplit_store(const float (&v)[E], __bf16* p0, __bf16* p1, __bf16* p2) {
+  __bf16 h[E], m[E], l[E];
+#pragma unroll
+  for (int i = 0; i < E; ++i) {
+    const __bf16 a = (__bf16)v[i];
+    const float r = v[i] - (float)a;
+    const __bf16 b = (__bf16)r;
+    h[i] = a;
+    m[i] = b;
+    l[i] = (__bf16)(r - (float)b);
+  }
+  if constexpr (E == 8) {
+    typedef __bf16 v8 __attribute__((ext_vector_type(8)));
+    v8 a, b, c;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) { a[i] = h[i]; b[i] = m[i]; c[i] = l[i]; }
+    *reinterpret_cast<v8*>(p0) = a;
+    *reinterpret_cast<v8*>(p1) = b;
+    *reinterpret_cast<v8*>(p2) = c;
+  } else {
+    typedef __bf16 v4 __attribute__((ext_vector_type(4)));
+    v4 a, b, c;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { a[i] = h[i]; b[i] = m[i]; c[i] = l[i]; }
+    *reinterpret_cast<v4*>(p0) = a;
+    *reinterpret_cast<v4*>(p1) = b;
+    *reinterpret_cast<v4*>(p2) = c;
+  }
+}
+
+template <int BM, int BN>
+__global__ __launch_bounds__(256, 2) void wgrad_x6_kernel(WgradArgs g) {
+  if (blockIdx.y) {
+    g.a += blockIdx.y * g.bs_a;
+    g.b += blockIdx.y * g.bs_b;
+    g.part += blockIdx.y * g.bs_part;
+  }
+  constexpr int BK = 16;
+  constexpr int TM = BM / 64, TN = BN / 64;
+  constexpr int EA = BM * BK / 256, EB = BN * BK / 256;  // pixels per thread per stage (8 or 4)
+  __shared__ __attribute__((aligned(16))) __bf16 sA[2][3][BM * BK];  // [buf][hi|mid|lo][m][k]
+  __shared__ __attribute__((aligned(16))) __bf16 sB[2][3][BN * BK];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave & 1, wn = wave >> 1, li = lane & 31, lh = lane >> 5;
+  const int ntm = g.Mp / BM, ntn = g.Np / BN;
+  const int tiles = ntm * ntn;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = bid / tiles;
+  const int tile = bid - split * tiles;
+  const int m0 = (tile / ntn) * BM, n0 = (tile % ntn) * BN;
+  const int p_begin = split * g.pix_per_split;
+  const int p_end = min(g.P, p_begin + g.pix_per_split);
+  const int am = tid % BM, ap = (tid / BM) * EA;  // this thread's column and pixel offset
+  const int bn = tid % BN, bp = (tid / BN) * EB;
+  const bool do_bias = g.part_bias != nullptr && n0 == 0;
+  // a_up2 (transposed-conv weight gradient): the tile's (i, j) tap of the 2x2 output block
+  int a_dr = 0, a_ds = 0, a_c0 = m0;
+  if (g.a_up2) { const int ij = m0 / g.Ca; a_dr = ij >> 1; a_ds = ij & 1; a_c0 = m0 - ij * g.Ca; }
+  const int HW = g.H * g.W;
+  float ra[EA], rb[EB];
+  float bsum = 0.f;
+  auto gload = [&](int p0) {
+    // a_up2: the EA pixels sit in one image row (W % EA == 0, checked by the launcher), two
+    // output pixels apart
+    size_t pix0 = p0 + ap;
+    int pstep = 1;
+    if (g.a_up2) {
+      const int p = p0 + ap;
+      const int bb = p / HW, rem = p - bb * HW, h = rem / g.W, w = rem - h * g.W;
+      pix0 = ((size_t)bb * 2 * g.H + 2 * h + a_dr) * (2 * g.W) + 2 * w + a_ds;
+      pstep = 2;
+    }
+#pragma unroll
+    for (int e = 0; e < EA; ++e) {
+      const int p = p0 + ap + e;
+      ra[e] = p < p_end ? g.a[(pix0 + (size_t)pstep * e) * g.lda + a_c0 + am] : 0.f;
+    }
+#pragma unroll
+    for (int e = 0; e < EB; ++e) {
+      const int p = p0 + bp + e;
+      rb[e] = p < p_end ? g.b[(size_t)p * g.ldb + n0 + bn] : 0.f;
+    }
+  };
+  auto lstore = [&](int buf) {
+    if (do_bias) {
+#pragma unroll
+      for (int e = 0; e < EA; ++e) bsum += ra[e];
+    }
+    wsplit_store<EA>(ra, &sA[buf][0][am * BK + ap], &sA[buf][1][am * BK + ap], &sA[buf][2][am * BK + ap]);
+    wsplit_store<EB>(rb, &sB[buf][0][bn * BK + bp], &sB[buf][1][bn * BK + bp], &sB[buf][2][bn * BK + bp]);
+  };
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int b = 0; b < TN; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+  const int nst = (p_end - p_begin + BK - 1) / BK;
+  if (nst > 0) {
+    gload(p_begin);
+    lstore(0);
+  }
+  __syncthreads();
+  for (int st = 0; st < nst; ++st) {
+    const int cur = st & 1;
+    if (st + 1 < nst) gload(p_begin + (st + 1) * BK);
+    wbf16x8 af[3][TM], bf[3][TN];
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl) {
+#pragma unroll
+      for (int a = 0; a < TM; ++a)
+        af[pl][a] = *reinterpret_cast<const wbf16x8*>(&sA[cur][pl][(wm * (BM / 2) + a * 32 + li) * BK + 8 * lh]);
+#pragma unroll
+      for (int b = 0; b < TN; ++b)
+        bf[pl][b] = *reinterpret_cast<const wbf16x8*>(&sB[cur][pl][(wn * (BN / 2) + b * 32 + li) * BK + 8 * lh]);
+    }
+#pragma unroll
+    for (int a = 0; a < TM; ++a)
+#pragma unroll
+      for (int b = 0; b < TN; ++b) {  // smallest partial products first
+        acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[2][a], bf[0][b], acc[a][b], 0, 0, 0);
+        acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1][a], bf[1][b], acc[a][b], 0, 0, 0);
+        acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0][a], bf[2][b], acc[a][b], 0, 0, 0);
+        acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1][a], bf[0][b], acc[a][b], 0, 0, 0);
+        acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0][a], bf[1][b], acc[a][b], 0, 0, 0);
+        acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0][a], bf[0][b], acc[a][b], 0, 0, 0);
+      }
+    if (st + 1 < nst) lstore(cur ^ 1);
+    __syncthreads();
+  }
+  float* out = g.part + (size_t)split * (g.split_stride ? g.split_stride : (int64_t)g.Mp * g.Np);
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int b = 0; b < TN; ++b) {
+      const int n = n0 + wn * (BN / 2) + b * 32 + li;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm * (BM / 2) + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        out[(size_t)m * g.Np + n] = acc[a][b][r];
+      }
+    }
+  if (do_bias) {  // column sums of A: 256 / BM partial sums per column, reduced through LDS
+    float* red = reinterpret_cast<float*>(&sA[0][0][0]);
+    red[tid] = bsum;
+    __syncthreads();
+    if (tid < BM) {
+      float t = 0.f;
+#pragma unroll
+      for (int q = 0; q < 256 / BM; ++q) t += red[q * BM + tid];
+      g.part_bias[(size_t)split * g.Mp + m0 + tid] = t;
+    }
+  }
+}
+
 static int run_wgrad(const WgradArgs& base, const WgradPlan& pl, hipStream_t s, int batches = 1) {
   WgradArgs a = base;
   a.pix_per_split = pl.pps;
   const int tiles = (a.Mp / pl.bm) * (a.Np / pl.bn);
   const dim3 grid(tiles * pl.splits, batches);
+  if (tune_get(PIS_TUNE_WGRAD_X6) != 0 && a.b_mode == B_PLAIN && pl.pps % 16 == 0 && (!a.a_up2 || a.W % 8 == 0)) {
+    if (pl.bm == 128 && pl.bn == 128) hipLaunchKernelGGL((wgrad_x6_kernel<128, 128>), grid, dim3(256), 0, s, a);
+    else if (pl.bm == 128) hipLaunchKernelGGL((wgrad_x6_kernel<128, 64>), grid, dim3(256), 0, s, a);
+    else if (pl.bn == 128) hipLaunchKernelGGL((wgrad_x6_kernel<64, 128>), grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((wgrad_x6_kernel<64, 64>), grid, dim3(256), 0, s, a);
+    return launch_status("wgrad_x6");
+  }
   if (pl.bm == 128 && pl.bn == 128)
     hipLaunchKernelGGL((wgrad_f32_kernel<128, 128, 16>), grid, dim3(256), 0, s, a);
   else if (pl.bm == 128)

@@ -103,7 +103,7 @@ def test_conv3x3_dgrad_wgrad(hip, B, H, W, Cin, Cout):
 
 # every non-default kernel variant behind pis_tune (include/pis_capi.h) stays exact too
 TUNE_VARIANTS = [(4, 1), (4, 2), (4, 3), (5, 0), (6, 2048), (3, 0), (7, 1), (8, 0), (8, 2), (10, 0), (10, 1),
-                 (11, 0), (12, 0), (12, 2), (13, 0), (10, 2)]
+                 (11, 0), (12, 0), (12, 2), (13, 0), (13, 2), (10, 2), (14, 0)]
 
 
 @pytest.mark.parametrize("key,value", TUNE_VARIANTS)
@@ -145,7 +145,7 @@ def test_conv3x3_ex_winograd(hip, B, H, W, Cin, Cout, mode):
         nws = hip.pis_conv3x3_ex_ws(B, H, W, Cin, Cout)
         f4 = hip.pis_tune(11, -1) != 0 and H % 4 == 0 and W % 4 == 0
         if f4:  # F(4x4,3x3) policy
-            wino_fwd = wino_dgrad = max(Cin, Cout) >= 128
+            wino_fwd = wino_dgrad = max(Cin, Cout) >= 128 or (hip.pis_tune(10, -1) == 3 and min(Cin, Cout) >= 64)
         else:  # F(2x2,3x3) policy
             wino_fwd = Cin >= 256 and Cout >= 128
             wino_dgrad = Cout >= 256 and Cin >= 128
@@ -536,3 +536,79 @@ def test_winograd_gemm_bf16x6_is_fp32_accurate(hip, Cin, Cout):
         hip.pis_tune(8, prev8)
     assert errs[3] <= 1.25 * errs[2] + 1e-9, errs
     assert errs[3] < 5e-6, errs
+
+
+@pytest.mark.parametrize("Cin,Cout", [(256, 256), (512, 128), (64, 128), (128, 64)])
+def test_winograd_wgrad_bf16x6_is_fp32_accurate(hip, Cin, Cout):
+    """The bf16x6 weight-gradient GEMM (pis_tune(14, 1), default) against the fp32 MFMA one
+    (pis_tune(14, 0)): dW and db of the same conv against a float64 reference, error no larger
+    than fp32's (+25 % slack)."""
+    B, H, W = 2, 16, 32
+    g = torch.Generator().manual_seed(37)
+    x = F.relu(torch.randn(B, Cin, H, W, generator=g, dtype=torch.float64))
+    dz = torch.randn(B, Cout, H, W, generator=g, dtype=torch.float64)
+    dw_ref = torch.nn.grad.conv2d_weight(x, (Cout, Cin, 3, 3), dz, padding=1)
+    db_ref = dz.sum(dim=(0, 2, 3))
+    xd, dzd = nhwc(x.float()).cuda(), nhwc(dz.float()).cuda()
+    errs = {}
+    for v in (0, 1):
+        prev = hip.pis_tune(14, v)
+        try:
+            nws = hip.pis_conv3x3_wgrad_ws(B, H, W, Cin, Cout)
+            ws = torch.empty(nws // 4 + 1, device="cuda")
+            dw = torch.empty(Cout, 3, 3, Cin, device="cuda")
+            db = torch.empty(Cout, device="cuda")
+            rc = hip.pis_conv3x3_wgrad(xd.data_ptr(), Cin, dzd.data_ptr(), Cout, dw.data_ptr(), db.data_ptr(),
+                                       B, H, W, Cin, Cout, 0, ws.data_ptr(), nws, s())
+            assert rc == 0, hip.pis_last_error()
+            torch.cuda.synchronize()
+        finally:
+            hip.pis_tune(14, prev)
+        dwc = dw.cpu().permute(0, 3, 1, 2).double()
+        errs[v] = ((dwc - dw_ref).norm() / dw_ref.norm()).item()
+        assert rel_err(db.cpu().double(), db_ref) < 1e-5
+    assert errs[1] <= 1.25 * errs[0] + 1e-9, errs
+    assert errs[1] < 5e-6, errs
+
+
+@pytest.mark.parametrize("Cin,Cout", [(128, 64), (512, 256)])
+def test_convt_bf16x6_is_fp32_accurate(hip, Cin, Cout):
+    """Transposed conv forward / input gradient (key 13: 1 bf16x6 vs 2 fp32 MFMA) and weight
+    gradient (key 14: 1 vs 0) against float64: the bf16x6 error no larger than fp32's (+25 %)."""
+    B, H, W = 2, 16, 32
+    g = torch.Generator().manual_seed(41)
+    x = F.relu(torch.randn(B, Cin, H, W, generator=g, dtype=torch.float64)).requires_grad_(True)
+    w = (torch.randn(Cin, Cout, 2, 2, generator=g, dtype=torch.float64) / Cin ** 0.5).requires_grad_(True)
+    b = torch.randn(Cout, generator=g, dtype=torch.float64).requires_grad_(True)
+    y = F.conv_transpose2d(x, w, b, stride=2)
+    dy = torch.randn(y.shape, generator=g, dtype=torch.float64)
+    y.backward(dy)
+    w_ijoc = w.detach().float().permute(2, 3, 1, 0).contiguous().cuda()
+    xd, bd, dyd = nhwc(x.detach().float()).cuda(), b.detach().float().cuda(), nhwc(dy.float()).cuda()
+    wc = torch.empty(Cin * 4 * Cout, device="cuda")
+    assert hip.pis_convt2x2_prep(w_ijoc.data_ptr(), wc.data_ptr(), Cin, Cout, s()) == 0
+    errs = {}
+    for name, (v13, v14) in {"x6": (1, 1), "f32": (2, 0)}.items():
+        p13, p14 = hip.pis_tune(13, v13), hip.pis_tune(14, v14)
+        try:
+            yd = torch.empty(B, 2 * H, 2 * W, Cout, device="cuda")
+            assert hip.pis_convt2x2_fwd(xd.data_ptr(), Cin, w_ijoc.data_ptr(), bd.data_ptr(), yd.data_ptr(), Cout,
+                                        B, H, W, Cin, Cout, s()) == 0
+            dx = torch.empty(B, H, W, Cin, device="cuda")
+            assert hip.pis_convt2x2_dgrad(dyd.data_ptr(), Cout, wc.data_ptr(), xd.data_ptr(), Cin, dx.data_ptr(),
+                                          Cin, B, H, W, Cin, Cout, 0, s()) == 0
+            nws = hip.pis_convt2x2_wgrad_ws(B, H, W, Cin, Cout)
+            ws = torch.empty(nws // 4 + 1, device="cuda")
+            dw = torch.empty(2, 2, Cout, Cin, device="cuda")
+            db = torch.empty(Cout, device="cuda")
+            assert hip.pis_convt2x2_wgrad(xd.data_ptr(), Cin, dyd.data_ptr(), Cout, dw.data_ptr(), db.data_ptr(),
+                                          B, H, W, Cin, Cout, 0, ws.data_ptr(), nws, s()) == 0
+            torch.cuda.synchronize()
+        finally:
+            hip.pis_tune(13, p13)
+            hip.pis_tune(14, p14)
+        errs[name] = [rel_err(nchw(yd.cpu()), y.detach()), rel_err(nchw(dx.cpu()), x.grad),
+                      rel_err(dw.cpu().permute(3, 2, 0, 1), w.grad), rel_err(db.cpu(), b.grad)]
+    for e6, e32 in zip(errs["x6"], errs["f32"]):
+        assert e6 <= 1.25 * e32 + 1e-9, errs
+        assert e6 < 5e-6, errs
