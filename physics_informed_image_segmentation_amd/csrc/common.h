@@ -43,6 +43,36 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
 }
 
+// ---- bf16x6: exact 3-way bf16 split of fp32 operands ------------------------
+// hi = bf16(x), mid = bf16(x - hi), lo = bf16(x - hi - mid); both subtractions are exact, and
+// hi + mid + lo == x (24 significant bits). Two values per step: one v_cvt_pk_bf16_f32 per level,
+// the bf16 pair widened back to fp32 by a shift / mask, one v_pk_add_f32 per residual (4.5 VALU
+// per value). Outputs are packed bf16 pairs (element 0 in the low half, memory order).
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 pis_bf16x2 __attribute__((ext_vector_type(2)));
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void split3_pair(f32x2 x, unsigned& h, unsigned& m, unsigned& l) {
+  const unsigned hu = __builtin_bit_cast(unsigned, __builtin_convertvector(x, pis_bf16x2));
+  const f32x2 r = x - f32x2{__builtin_bit_cast(float, hu << 16), __builtin_bit_cast(float, hu & 0xffff0000u)};
+  const unsigned mu = __builtin_bit_cast(unsigned, __builtin_convertvector(r, pis_bf16x2));
+  const f32x2 r2 = r - f32x2{__builtin_bit_cast(float, mu << 16), __builtin_bit_cast(float, mu & 0xffff0000u)};
+  h = hu;
+  m = mu;
+  l = __builtin_bit_cast(unsigned, __builtin_convertvector(r2, pis_bf16x2));
+}
+
+// four values -> three planes of 4 bf16 (8 bytes each)
+__device__ __forceinline__ void split3_x4(f32x4 v, u32x2& h, u32x2& m, u32x2& l) {
+  unsigned h0, m0, l0, h1, m1, l1;
+  split3_pair(f32x2{v[0], v[1]}, h0, m0, l0);
+  split3_pair(f32x2{v[2], v[3]}, h1, m1, l1);
+  h = u32x2{h0, h1};
+  m = u32x2{m0, m1};
+  l = u32x2{l0, l1};
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);

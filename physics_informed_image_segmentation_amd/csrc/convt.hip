@@ -35,20 +35,6 @@ struct ConvtGemmArgs {
 };
 
 typedef __bf16 cbf16x8 __attribute__((ext_vector_type(8)));
-typedef __bf16 cbf16x4 __attribute__((ext_vector_type(4)));
-
-// exact 3-way bf16 split of four fp32 values (as split3_bf16 in winograd.hip)
-__device__ __forceinline__ void csplit3(f32x4 v, cbf16x4& h, cbf16x4& m, cbf16x4& l) {
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const __bf16 a = (__bf16)v[i];
-    const float r = v[i] - (float)a;
-    const __bf16 b = (__bf16)r;
-    h[i] = a;
-    m[i] = b;
-    l[i] = (__bf16)(r - (float)b);
-  }
-}
 
 // X6: the operands are split into hi/mid/lo bf16 planes at LDS staging and every fp32
 // multiply-add becomes six bf16 MFMA partial products (fp32 accuracy, see gemm_nt_x6_kernel)
@@ -111,21 +97,21 @@ __global__ __launch_bounds__(256, 2) void convt_gemm_kernel(ConvtGemmArgs g) {
       __bf16* pb = reinterpret_cast<__bf16*>(sB[buf]);
 #pragma unroll
       for (int i = 0; i < AL; ++i) {
-        cbf16x4 h, m, l;
-        csplit3(ra[i], h, m, l);
+        u32x2 h, m, l;
+        split3_x4(ra[i], h, m, l);
         const int o = ((tid + i * 256) / 4) * BK + q4;
-        *reinterpret_cast<cbf16x4*>(pa + o) = h;
-        *reinterpret_cast<cbf16x4*>(pa + BM * BK + o) = m;
-        *reinterpret_cast<cbf16x4*>(pa + 2 * BM * BK + o) = l;
+        *reinterpret_cast<u32x2*>(pa + o) = h;
+        *reinterpret_cast<u32x2*>(pa + BM * BK + o) = m;
+        *reinterpret_cast<u32x2*>(pa + 2 * BM * BK + o) = l;
       }
 #pragma unroll
       for (int i = 0; i < BL; ++i) {
-        cbf16x4 h, m, l;
-        csplit3(rb[i], h, m, l);
+        u32x2 h, m, l;
+        split3_x4(rb[i], h, m, l);
         const int o = ((tid + i * 256) / 4) * BK + q4;
-        *reinterpret_cast<cbf16x4*>(pb + o) = h;
-        *reinterpret_cast<cbf16x4*>(pb + BN * BK + o) = m;
-        *reinterpret_cast<cbf16x4*>(pb + 2 * BN * BK + o) = l;
+        *reinterpret_cast<u32x2*>(pb + o) = h;
+        *reinterpret_cast<u32x2*>(pb + BN * BK + o) = m;
+        *reinterpret_cast<u32x2*>(pb + 2 * BN * BK + o) = l;
       }
     } else {
 #pragma unroll

@@ -507,34 +507,20 @@ static size_t wgrad_ws_bytes(const WgradPlan& pl) { return cdiv(pl.part_bytes, 2
 // Also the transposed-conv weight gradient (a_up2 rows, bias column sums of A).
 typedef __bf16 wbf16x8 __attribute__((ext_vector_type(8)));
 
-template <int E>
+template <int E>  // E = 8 or 4 consecutive-k values of one row -> one 16-B / 8-B store per plane
 __device__ __forceinline__ void wsplit_store(const float (&v)[E], __bf16* p0, __bf16* p1, __bf16* p2) {
-  __bf16 h[E], m[E], l[E];
-#pragma unroll
-  for (int i = 0; i < E; ++i) {
-    const __bf16 a = (__bf16)v[i];
-    const float r = v[i] - (float)a;
-    const __bf16 b = (__bf16)r;
-    h[i] = a;
-    m[i] = b;
-    l[i] = (__bf16)(r - (float)b);
-  }
+  u32x2 h0, m0, l0;
+  split3_x4(f32x4{v[0], v[1], v[2], v[3]}, h0, m0, l0);
   if constexpr (E == 8) {
-    typedef __bf16 v8 __attribute__((ext_vector_type(8)));
-    v8 a, b, c;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) { a[i] = h[i]; b[i] = m[i]; c[i] = l[i]; }
-    *reinterpret_cast<v8*>(p0) = a;
-    *reinterpret_cast<v8*>(p1) = b;
-    *reinterpret_cast<v8*>(p2) = c;
+    u32x2 h1, m1, l1;
+    split3_x4(f32x4{v[4], v[5], v[6], v[7]}, h1, m1, l1);
+    *reinterpret_cast<u32x4*>(p0) = u32x4{h0[0], h0[1], h1[0], h1[1]};
+    *reinterpret_cast<u32x4*>(p1) = u32x4{m0[0], m0[1], m1[0], m1[1]};
+    *reinterpret_cast<u32x4*>(p2) = u32x4{l0[0], l0[1], l1[0], l1[1]};
   } else {
-    typedef __bf16 v4 __attribute__((ext_vector_type(4)));
-    v4 a, b, c;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) { a[i] = h[i]; b[i] = m[i]; c[i] = l[i]; }
-    *reinterpret_cast<v4*>(p0) = a;
-    *reinterpret_cast<v4*>(p1) = b;
-    *reinterpret_cast<v4*>(p2) = c;
+    *reinterpret_cast<u32x2*>(p0) = h0;
+    *reinterpret_cast<u32x2*>(p1) = m0;
+    *reinterpret_cast<u32x2*>(p2) = l0;
   }
 }
 

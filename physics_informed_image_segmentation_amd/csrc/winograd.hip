@@ -734,23 +734,14 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const float* __restrict
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 
-__device__ __forceinline__ void split3_bf16(f32x4 v, bf16x4& h, bf16x4& m, bf16x4& l) {
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const __bf16 a = (__bf16)v[i];
-    const float r = v[i] - (float)a;  // exact: a carries x's leading 8 significant bits
-    const __bf16 b = (__bf16)r;
-    const float r2 = r - (float)b;    // exact
-    h[i] = a;
-    m[i] = b;
-    l[i] = (__bf16)r2;
-  }
-}
 
-template <int BM, int BN>
-__global__ __launch_bounds__(256, 2) void gemm_nt_x6_kernel(const float* __restrict__ A, const float* __restrict__ Bm,
-                                                           float* __restrict__ Cm, int M, int N, int K,
-                                                           int64_t bsA, int64_t bsB, int64_t bsC) {
+// DBG (timing only, wrong results): 1 no global loads, 2 no split.
+// PF: global-load prefetch depth in K-steps. PF = 2 keeps two register sets in flight, so a
+// load is consumed two K-steps (two MFMA phases of every wave on the SIMD) after its issue.
+template <int BM, int BN, int DBG = 0, int PF = 1>
+__global__ __launch_bounds__(256, BM * BN > 32768 ? 1 : 2) void gemm_nt_x6_kernel(
+    const float* __restrict__ A, const float* __restrict__ Bm, float* __restrict__ Cm, int M, int N, int K,
+    int64_t bsA, int64_t bsB, int64_t bsC) {
   constexpr int BK = 16;
   constexpr int TM = BM / 64, TN = BN / 64;
   constexpr int AL = BM * 4 / 256, BL = BN * 4 / 256;  // float4 loads per thread per stage
@@ -765,40 +756,65 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_x6_kernel(const float* __restr
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int m0 = (bid / ntn) * BM, n0 = (bid % ntn) * BN;
   const int q4 = (tid & 3) * 4;
-  f32x4 ra[AL], rb[BL];
-  auto gload = [&](int k0) {
+  const bool full = m0 + BM <= M && K % BK == 0;
+  struct Regs {
+    f32x4 a[AL], b[BL];
+  };
+  auto gload = [&](int k0, Regs& r) {
     const int k = k0 + q4;
+    if (DBG == 1) {
 #pragma unroll
-    for (int i = 0; i < AL; ++i) {
-      const int m = m0 + (tid + i * 256) / 4;
-      ra[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (m < M && k < K) ra[i] = *reinterpret_cast<const f32x4*>(A + (size_t)m * K + k);
+      for (int i = 0; i < AL; ++i) r.a[i] = f32x4{(float)k0, 1.f, 2.f, 3.f};
+#pragma unroll
+      for (int i = 0; i < BL; ++i) r.b[i] = f32x4{(float)k0, 1.f, 2.f, 3.f};
+      return;
+    }
+    if (full) {  // block-uniform: no per-load guards (exec masking) inside the tile
+#pragma unroll
+      for (int i = 0; i < AL; ++i)
+        r.a[i] = *reinterpret_cast<const f32x4*>(A + (size_t)(m0 + (tid + i * 256) / 4) * K + k);
+    } else {
+#pragma unroll
+      for (int i = 0; i < AL; ++i) {
+        const int m = m0 + (tid + i * 256) / 4;
+        r.a[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (m < M && k < K) r.a[i] = *reinterpret_cast<const f32x4*>(A + (size_t)m * K + k);
+      }
     }
 #pragma unroll
     for (int i = 0; i < BL; ++i) {
       const int n = n0 + (tid + i * 256) / 4;
-      rb[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (k < K) rb[i] = *reinterpret_cast<const f32x4*>(Bm + (size_t)n * K + k);
+      r.b[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (full || k < K) r.b[i] = *reinterpret_cast<const f32x4*>(Bm + (size_t)n * K + k);
     }
   };
-  auto lstore = [&](int buf) {
+  auto split = [&](f32x4 v, u32x2& h, u32x2& m, u32x2& l) {
+    if (DBG == 2) {
+      h = u32x2{__builtin_bit_cast(unsigned, v[0]), __builtin_bit_cast(unsigned, v[2])};
+      m = h;
+      l = h;
+    } else {
+      split3_x4(v, h, m, l);
+    }
+  };
+  auto lstore = [&](int buf, const Regs& r) {
 #pragma unroll
     for (int i = 0; i < AL; ++i) {
-      bf16x4 h, m, l;
-      split3_bf16(ra[i], h, m, l);
+      u32x2 h, m, l;
+      split(r.a[i], h, m, l);
       const int o = ((tid + i * 256) / 4) * BK + q4;
-      *reinterpret_cast<bf16x4*>(&sA[buf][0][o]) = h;
-      *reinterpret_cast<bf16x4*>(&sA[buf][1][o]) = m;
-      *reinterpret_cast<bf16x4*>(&sA[buf][2][o]) = l;
+      *reinterpret_cast<u32x2*>(&sA[buf][0][o]) = h;
+      *reinterpret_cast<u32x2*>(&sA[buf][1][o]) = m;
+      *reinterpret_cast<u32x2*>(&sA[buf][2][o]) = l;
     }
 #pragma unroll
     for (int i = 0; i < BL; ++i) {
-      bf16x4 h, m, l;
-      split3_bf16(rb[i], h, m, l);
+      u32x2 h, m, l;
+      split(r.b[i], h, m, l);
       const int o = ((tid + i * 256) / 4) * BK + q4;
-      *reinterpret_cast<bf16x4*>(&sB[buf][0][o]) = h;
-      *reinterpret_cast<bf16x4*>(&sB[buf][1][o]) = m;
-      *reinterpret_cast<bf16x4*>(&sB[buf][2][o]) = l;
+      *reinterpret_cast<u32x2*>(&sB[buf][0][o]) = h;
+      *reinterpret_cast<u32x2*>(&sB[buf][1][o]) = m;
+      *reinterpret_cast<u32x2*>(&sB[buf][2][o]) = l;
     }
   };
   f32x16 acc[TM][TN];
@@ -808,13 +824,7 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_x6_kernel(const float* __restr
     for (int b = 0; b < TN; ++b)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
-  const int KT = (K + BK - 1) / BK;
-  gload(0);
-  lstore(0);
-  __syncthreads();
-  for (int kt = 0; kt < KT; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < KT) gload((kt + 1) * BK);
+  auto compute = [&](int cur) {
     bf16x8 af[3][TM], bf[3][TN];  // lane: row li, k = 8 lh .. 8 lh + 7
 #pragma unroll
     for (int p = 0; p < 3; ++p) {
@@ -836,8 +846,37 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_x6_kernel(const float* __restr
         acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0][a], bf[1][b], acc[a][b], 0, 0, 0);
         acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0][a], bf[0][b], acc[a][b], 0, 0, 0);
       }
-    if (kt + 1 < KT) lstore(cur ^ 1);
+  };
+  const int KT = (K + BK - 1) / BK;
+  Regs x;
+  gload(0, x);
+  lstore(0, x);
+  if constexpr (PF == 1) {
     __syncthreads();
+    for (int kt = 0; kt < KT; ++kt) {
+      const int cur = kt & 1;
+      if (kt + 1 < KT) gload((kt + 1) * BK, x);
+      compute(cur);
+      if (kt + 1 < KT) lstore(cur ^ 1, x);
+      __syncthreads();
+    }
+  } else {
+    // stage j >= 1 lives in register set x (j odd) or y (j even) until its LDS store
+    Regs y;
+    if (KT > 1) gload(BK, x);
+    if (KT > 2) gload(2 * BK, y);
+    __syncthreads();
+    for (int kt = 0; kt < KT; kt += 2) {
+      compute(0);
+      if (kt + 1 < KT) lstore(1, x);
+      if (kt + 3 < KT) gload((kt + 3) * BK, x);
+      __syncthreads();
+      if (kt + 1 >= KT) break;
+      compute(1);
+      if (kt + 2 < KT) lstore(0, y);
+      if (kt + 4 < KT) gload((kt + 4) * BK, y);
+      __syncthreads();
+    }
   }
 #pragma unroll
   for (int a = 0; a < TM; ++a)
@@ -984,6 +1023,35 @@ int launch_wino_wgrad_out(const float* M, int N, int C, float* dw, int accumulat
     hipLaunchKernelGGL(wino_wgrad_out_kernel, dim3(grid_of((int64_t)N * C)), dim3(256), 0, s, M, N, C, dw,
                        accumulate);
   return launch_status("wino_wgrad_out");
+}
+
+// ---- tooling: time one batched NT GEMM variant (tools/bench_gemm.py) ----------------------
+// C[b] (M x N) = A[b] (M x K) . B[b]^T (N x K), batch b over gridDim.y, all row-major fp32.
+// variant: 0 bf16x6 128x128, 1 its no-global-load timing twin, 2 its no-split timing twin,
+// 3 fp32 MFMA 128x128, 4 bf16x6 128x64, 5 bf16x6 128x128 with two K-steps of load prefetch,
+// 6/7/8 bf16x6 256x128 / 128x256 / 256x256. Requires N % 128 == 0 (64 for 4), K % 16 == 0.
+extern "C" int pis_debug_gemm_nt(const float* A, const float* B, float* C, int M, int N, int K, int batch,
+                                 int variant, pis_stream_t stream) {
+  const int bm = variant == 6 || variant == 8 ? 256 : 128;
+  const int bn = variant == 4 ? 64 : variant == 7 || variant == 8 ? 256 : 128;
+  PIS_CHECK_ARG(A && B && C && M > 0 && N > 0 && K > 0 && batch > 0 && K % 16 == 0 && N % bn == 0,
+                "pis_debug_gemm_nt: bad arguments");
+  hipStream_t s = (hipStream_t)stream;
+  const dim3 grid((int)cdiv(M, bm) * (N / bn), batch);
+  const int64_t sa = (int64_t)M * K, sb = (int64_t)N * K, sc = (int64_t)M * N;
+  switch (variant) {
+    case 0: hipLaunchKernelGGL((gemm_nt_x6_kernel<128, 128>), grid, dim3(256), 0, s, A, B, C, M, N, K, sa, sb, sc); break;
+    case 1: hipLaunchKernelGGL((gemm_nt_x6_kernel<128, 128, 1>), grid, dim3(256), 0, s, A, B, C, M, N, K, sa, sb, sc); break;
+    case 2: hipLaunchKernelGGL((gemm_nt_x6_kernel<128, 128, 2>), grid, dim3(256), 0, s, A, B, C, M, N, K, sa, sb, sc); break;
+    case 3: hipLaunchKernelGGL((gemm_nt_kernel<128, 128>), grid, dim3(256), 0, s, A, B, C, M, N, K, sa, sb, sc); break;
+    case 4: hipLaunchKernelGGL((gemm_nt_x6_kernel<128, 64>), grid, dim3(256), 0, s, A, B, C, M, N, K, sa, sb, sc); break;
+    case 5: hipLaunchKernelGGL((gemm_nt_x6_kernel<128, 128, 0, 2>), grid, dim3(256), 0, s, A, B, C, M, N, K, sa, sb, sc); break;
+    case 6: hipLaunchKernelGGL((gemm_nt_x6_kernel<256, 128>), grid, dim3(256), 0, s, A, B, C, M, N, K, sa, sb, sc); break;
+    case 7: hipLaunchKernelGGL((gemm_nt_x6_kernel<128, 256>), grid, dim3(256), 0, s, A, B, C, M, N, K, sa, sb, sc); break;
+    case 8: hipLaunchKernelGGL((gemm_nt_x6_kernel<256, 256>), grid, dim3(256), 0, s, A, B, C, M, N, K, sa, sb, sc); break;
+    default: set_error("pis_debug_gemm_nt: unknown variant %d", variant); return PIS_ERR_ARG;
+  }
+  return launch_status("debug_gemm_nt");
 }
 
 }  // namespace pis
