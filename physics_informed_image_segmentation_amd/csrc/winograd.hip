@@ -736,10 +736,8 @@ typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 
 
 // DBG (timing only, wrong results): 1 no global loads, 2 no split.
-// PF: global-load prefetch depth in K-steps. PF = 2 keeps two register sets in flight, so a
-// load is consumed two K-steps (two MFMA phases of every wave on the SIMD) after its issue.
-template <int BM, int BN, int DBG = 0, int PF = 1>
-__global__ __launch_bounds__(256, BM * BN > 32768 ? 1 : 2) void gemm_nt_x6_kernel(
+template <int BM, int BN, int DBG = 0>
+__global__ __launch_bounds__(256, 2) void gemm_nt_x6_kernel(
     const float* __restrict__ A, const float* __restrict__ Bm, float* __restrict__ Cm, int M, int N, int K,
     int64_t bsA, int64_t bsB, int64_t bsC) {
   constexpr int BK = 16;
@@ -851,32 +849,13 @@ __global__ __launch_bounds__(256, BM * BN > 32768 ? 1 : 2) void gemm_nt_x6_kerne
   Regs x;
   gload(0, x);
   lstore(0, x);
-  if constexpr (PF == 1) {
+  __syncthreads();
+  for (int kt = 0; kt < KT; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < KT) gload((kt + 1) * BK, x);
+    compute(cur);
+    if (kt + 1 < KT) lstore(cur ^ 1, x);
     __syncthreads();
-    for (int kt = 0; kt < KT; ++kt) {
-      const int cur = kt & 1;
-      if (kt + 1 < KT) gload((kt + 1) * BK, x);
-      compute(cur);
-      if (kt + 1 < KT) lstore(cur ^ 1, x);
-      __syncthreads();
-    }
-  } else {
-    // stage j >= 1 lives in register set x (j odd) or y (j even) until its LDS store
-    Regs y;
-    if (KT > 1) gload(BK, x);
-    if (KT > 2) gload(2 * BK, y);
-    __syncthreads();
-    for (int kt = 0; kt < KT; kt += 2) {
-      compute(0);
-      if (kt + 1 < KT) lstore(1, x);
-      if (kt + 3 < KT) gload((kt + 3) * BK, x);
-      __syncthreads();
-      if (kt + 1 >= KT) break;
-      compute(1);
-      if (kt + 2 < KT) lstore(0, y);
-      if (kt + 4 < KT) gload((kt + 4) * BK, y);
-      __syncthreads();
-    }
   }
 #pragma unroll
   for (int a = 0; a < TM; ++a)
@@ -1028,16 +1007,14 @@ int launch_wino_wgrad_out(const float* M, int N, int C, float* dw, int accumulat
 // ---- tooling: time one batched NT GEMM variant (tools/bench_gemm.py) ----------------------
 // C[b] (M x N) = A[b] (M x K) . B[b]^T (N x K), batch b over gridDim.y, all row-major fp32.
 // variant: 0 bf16x6 128x128, 1 its no-global-load timing twin, 2 its no-split timing twin,
-// 3 fp32 MFMA 128x128, 4 bf16x6 128x64, 5 bf16x6 128x128 with two K-steps of load prefetch,
-// 6/7/8 bf16x6 256x128 / 128x256 / 256x256. Requires N % 128 == 0 (64 for 4), K % 16 == 0.
+// 3 fp32 MFMA 128x128, 4 bf16x6 128x64. Requires N % 128 == 0 (64 for 4), K % 16 == 0.
 extern "C" int pis_debug_gemm_nt(const float* A, const float* B, float* C, int M, int N, int K, int batch,
                                  int variant, pis_stream_t stream) {
-  const int bm = variant == 6 || variant == 8 ? 256 : 128;
-  const int bn = variant == 4 ? 64 : variant == 7 || variant == 8 ? 256 : 128;
+  const int bn = variant == 4 ? 64 : 128;
   PIS_CHECK_ARG(A && B && C && M > 0 && N > 0 && K > 0 && batch > 0 && K % 16 == 0 && N % bn == 0,
                 "pis_debug_gemm_nt: bad arguments");
   hipStream_t s = (hipStream_t)stream;
-  const dim3 grid((int)cdiv(M, bm) * (N / bn), batch);
+  const dim3 grid((int)cdiv(M, 128) * (N / bn), batch);
   const int64_t sa = (int64_t)M * K, sb = (int64_t)N * K, sc = (int64_t)M * N;
   switch (variant) {
     case 0: hipLaunchKernelGGL((gemm_nt_x6_kernel<128, 128>), grid, dim3(256), 0, s, A, B, C, M, N, K, sa, sb, sc); break;
@@ -1045,10 +1022,6 @@ extern "C" int pis_debug_gemm_nt(const float* A, const float* B, float* C, int M
     case 2: hipLaunchKernelGGL((gemm_nt_x6_kernel<128, 128, 2>), grid, dim3(256), 0, s, A, B, C, M, N, K, sa, sb, sc); break;
     case 3: hipLaunchKernelGGL((gemm_nt_kernel<128, 128>), grid, dim3(256), 0, s, A, B, C, M, N, K, sa, sb, sc); break;
     case 4: hipLaunchKernelGGL((gemm_nt_x6_kernel<128, 64>), grid, dim3(256), 0, s, A, B, C, M, N, K, sa, sb, sc); break;
-    case 5: hipLaunchKernelGGL((gemm_nt_x6_kernel<128, 128, 0, 2>), grid, dim3(256), 0, s, A, B, C, M, N, K, sa, sb, sc); break;
-    case 6: hipLaunchKernelGGL((gemm_nt_x6_kernel<256, 128>), grid, dim3(256), 0, s, A, B, C, M, N, K, sa, sb, sc); break;
-    case 7: hipLaunchKernelGGL((gemm_nt_x6_kernel<128, 256>), grid, dim3(256), 0, s, A, B, C, M, N, K, sa, sb, sc); break;
-    case 8: hipLaunchKernelGGL((gemm_nt_x6_kernel<256, 256>), grid, dim3(256), 0, s, A, B, C, M, N, K, sa, sb, sc); break;
     default: set_error("pis_debug_gemm_nt: unknown variant %d", variant); return PIS_ERR_ARG;
   }
   return launch_status("debug_gemm_nt");
