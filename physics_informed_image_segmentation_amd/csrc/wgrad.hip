@@ -840,8 +840,14 @@ static int wino_wgrad(const float* x, int ldx, const float* dz, int ldz, float* 
   launch_hook("wino_wgrad_gemm", 0, s, flop);
   rc = run_wgrad(a, p.gemm, s, p.nxi);
   launch_hook("wino_wgrad_gemm", 1, s, flop);
-  if (!rc) rc = reduce_slabs_pitched(part, p.gemm.splits, a.split_stride, a.split_stride, M, 0, s);
-  if (!rc) rc = launch_wino_wgrad_out(M, Cout, Cin, dw, acc, s, p.m);
+  // few slabs over many weights: the output transform sums them itself (no reduced copy of the
+  // 36 planes); many slabs over few weights keep the parallel slab reduction
+  if (p.m == 4 && p.gemm.splits <= 8 && (int64_t)Cout * Cin >= 65536) {
+    if (!rc) rc = launch_wino_wgrad_out(part, Cout, Cin, dw, acc, s, p.m, p.gemm.splits, a.split_stride);
+  } else {
+    if (!rc) rc = reduce_slabs_pitched(part, p.gemm.splits, a.split_stride, a.split_stride, M, 0, s);
+    if (!rc) rc = launch_wino_wgrad_out(M, Cout, Cin, dw, acc, s, p.m);
+  }
   if (!rc && db) {
     if (bpart) rc = reduce_slabs(bpart, wino_dz_blocks(B, H, W, Cout, 4), Cout, db, acc, s);
     else rc = colsum(dz, ldz, (int64_t)B * H * W, Cout, db, acc, base + p.off_cs, p.total - p.off_cs, s);

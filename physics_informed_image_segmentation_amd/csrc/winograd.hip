@@ -596,8 +596,11 @@ __global__ __launch_bounds__(256) void wino4_dz_kernel(const float* __restrict__
 }
 
 // dw[n][r][s][c] (+)= (AT3 M AT3^T)[r][s], M[xi][n][c] the reduced tile sums
+// M may arrive as `nsplit` split-K slabs `sstride` floats apart (summed here in slab order,
+// which saves the separate slab reduction's write + re-read of the 36 planes)
 __global__ __launch_bounds__(256) void wino4_wgrad_out_kernel(const float* __restrict__ M, int N, int C,
-                                                              float* __restrict__ dw, int accumulate) {
+                                                              float* __restrict__ dw, int accumulate, int nsplit,
+                                                              int64_t sstride) {
   const int64_t NC = (int64_t)N * C;
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < NC; e += (int64_t)gridDim.x * blockDim.x) {
     const int n = (int)(e / C), c = (int)(e - (int64_t)n * C);
@@ -610,7 +613,12 @@ __global__ __launch_bounds__(256) void wino4_wgrad_out_kernel(const float* __res
     for (int k = 0; k < 6; ++k) {
       float m[6];
 #pragma unroll
-      for (int l = 0; l < 6; ++l) m[l] = M[(size_t)(k * 6 + l) * NC + e];
+      for (int l = 0; l < 6; ++l) {
+        const float* src = M + (size_t)(k * 6 + l) * NC + e;
+        float v = src[0];
+        for (int sp = 1; sp < nsplit; ++sp) v += src[sp * sstride];
+        m[l] = v;
+      }
 #pragma unroll
       for (int j = 0; j < 3; ++j) {
         float r = 0.f;
@@ -994,13 +1002,16 @@ int launch_wino_dz(const float* dz, int ldz, int B, int H, int W, int N, float* 
   return launch_status("wino_dz");
 }
 
-int launch_wino_wgrad_out(const float* M, int N, int C, float* dw, int accumulate, hipStream_t s, int m) {
+int launch_wino_wgrad_out(const float* M, int N, int C, float* dw, int accumulate, hipStream_t s, int m,
+                          int nsplit, int64_t sstride) {
   if (m == 4)
     hipLaunchKernelGGL(wino4_wgrad_out_kernel, dim3(grid_of((int64_t)N * C)), dim3(256), 0, s, M, N, C, dw,
-                       accumulate);
-  else
+                       accumulate, nsplit, sstride);
+  else if (nsplit == 1)
     hipLaunchKernelGGL(wino_wgrad_out_kernel, dim3(grid_of((int64_t)N * C)), dim3(256), 0, s, M, N, C, dw,
                        accumulate);
+  else
+    return set_error("wino_wgrad_out: split slabs need F(3x3,4x4)"), PIS_ERR_ARG;
   return launch_status("wino_wgrad_out");
 }
 
