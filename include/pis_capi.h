@@ -73,7 +73,9 @@ int pis_version(void);
                                     MFMA; 0 generic implicit GEMM */
 #define PIS_TUNE_WGRAD_X6 14     /* Winograd and transposed-conv weight-gradient GEMMs: 1 (default) fp32-accurate
                                     bf16x6 on bf16 MFMA, 0 fp32 MFMA */
-#define PIS_TUNE_NKEYS 15
+#define PIS_TUNE_WINO_GEMM_OUT 15 /* F(4x4,3x3) 64 -> 64 channels: 1 (default) the 36 bf16x6 contractions fused with
+                                     the output transform (M stays on chip), 0 separate GEMM + output transform */
+#define PIS_TUNE_NKEYS 16
 #define PIS_DEBUG_NOLOAD (1 << 16)
 int pis_tune(int key, int value);
 /* Tooling (tools/bench_gemm.py): time one batched NT GEMM kernel variant in isolation,

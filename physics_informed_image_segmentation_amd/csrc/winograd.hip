@@ -249,8 +249,11 @@ __device__ __forceinline__ void axpy_c(T& acc, float c, const T& v) {
 }
 
 // U[xi][n][c] = (G g G^T)[xi], xi = 6 i + j
+// With Up != NULL the transform is written as the bf16x6 hi/mid/lo planes Up[p][xi][n][c] instead
+// (the fused GEMM + output-transform kernel reads its B fragments straight from them).
 __global__ __launch_bounds__(256) void wino4_filter_kernel(const float* __restrict__ w, int ldw, int N, int C,
-                                                           float* __restrict__ U, int transposed = 0) {
+                                                           float* __restrict__ U, int transposed = 0,
+                                                           __bf16* __restrict__ Up = nullptr) {
   const int64_t NC = (int64_t)N * C;
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < NC; e += (int64_t)gridDim.x * blockDim.x) {
     const int n = (int)(e / C), c = (int)(e - (int64_t)n * C);
@@ -273,6 +276,16 @@ __global__ __launch_bounds__(256) void wino4_filter_kernel(const float* __restri
         float u = 0.f;
 #pragma unroll
         for (int s = 0; s < 3; ++s) axpy_c(u, w4_g(j, s), gg[i][s]);
+        if (Up) {
+          const __bf16 h = (__bf16)u;
+          const float r = u - (float)h;
+          const __bf16 m = (__bf16)r;
+          const size_t o = (size_t)(i * 6 + j) * NC + e;
+          Up[o] = h;
+          Up[36 * NC + o] = m;
+          Up[72 * NC + o] = (__bf16)(r - (float)m);
+          continue;
+        }
         // [xi][n][c] for the batched GEMMs; [xi][c][n] for the fused kernel's B operand
         U[(size_t)(i * 6 + j) * NC + (transposed ? (int64_t)c * N + n : e)] = u;
       }
@@ -878,6 +891,195 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_x6_kernel(
     }
 }
 
+// ---- F(4x4,3x3) contraction fused with the output transform (bf16x6) --------------------
+// For the shallow, HBM-bound layers: the 36 products M[xi] = V[xi] U[xi]^T never go to HBM.
+// A block owns TB = 16 NWT tiles x all N = 16 NWN output channels (V is read exactly once) and
+// walks xi = 0..35; wave (wt, wn) computes the 16 x 16 product of tiles 16 wt.. and channels
+// 16 wn.. on v_mfma_f32_16x16x32_bf16 (bf16x6, fp32 accumulation) and folds it straight into
+// Y = AT M AT^T: per row a of the 6x6 grid the lane keeps R[j] = sum_b AT[j][b] M[a][b], then
+// Y[i][j] += AT[i][a] R[j] — 16 x 4 accumulators per lane (lane l: channel l & 15 of tiles
+// 4 (l >> 4) .. + 3). Per xi both operands are staged in LDS: V[xi] (TB x KC fp32, one
+// contiguous run) is loaded RING stages ahead into registers and split into hi/mid/lo at the
+// LDS store; U[xi] arrives pre-split (wino4_filter_kernel Up planes, L2-resident) and is copied
+// with coalesced 16-B loads two stages ahead. One barrier per xi. Then the direct kernels'
+// epilogue (bias, ReLU, mask, keep-scale, accumulate).
+typedef __bf16 bf16x8g __attribute__((ext_vector_type(8)));
+
+template <int NWN, int NWT, int KC>
+__global__ __launch_bounds__(64 * NWN * NWT) void wino4_gemm_out_x6_kernel(const float* __restrict__ V,
+                                                                          const __bf16* __restrict__ Up,
+                                                                          IGemmArgs g, int B) {
+  constexpr int NT = 64 * NWN * NWT, TB = 16 * NWT, NN = 16 * NWN, KP = KC + 8;  // KP: LDS row pitch (bf16)
+  constexpr int NV4 = TB * KC / 4, AL = (NV4 + NT - 1) / NT;  // float4 of V[xi] per thread
+  constexpr bool VPART = NV4 % NT != 0;                         // (then NV4 < NT: some threads idle)
+  constexpr int NU8 = 3 * NN * KC / 8, UL = NU8 / NT;          // 16-B chunks of the U[xi] planes per thread
+  static_assert((!VPART || NV4 < NT) && NU8 % NT == 0, "staging must tile the block");
+  constexpr int RING = 6, KS = KC / 32;
+  __shared__ __attribute__((aligned(16))) __bf16 sA[2][3][TB * KP];
+  __shared__ __attribute__((aligned(16))) __bf16 sU[2][3][NN * KP];
+  const int N = g.N, TW = g.W / 4, TH = g.H / 4;
+  const int64_t T = (int64_t)B * TH * TW;
+  const int64_t TK = T * KC, NK = (int64_t)N * KC;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wn = wave % NWN, wt = wave / NWN;
+  const int lr = lane & 15, lq = lane >> 4;
+  const int64_t t0 = (int64_t)xcd_remap(blockIdx.x, gridDim.x) * TB;
+  const int n = 16 * wn + lr;  // this lane's output channel
+  const float* vb = V + t0 * KC;
+  f32x4 vr[RING][AL];
+  auto gload = [&](int xi, f32x4 (&r)[AL]) {
+#pragma unroll
+    for (int i = 0; i < AL; ++i) {
+      if (!VPART || tid + i * NT < NV4) r[i] = *reinterpret_cast<const f32x4*>(vb + xi * TK + 4 * (tid + i * NT));
+    }
+  };
+  auto lstore = [&](int buf, const f32x4 (&r)[AL]) {
+#pragma unroll
+    for (int i = 0; i < AL; ++i) {
+      const int idx = tid + i * NT;
+      if (VPART && idx >= NV4) continue;
+      const int row = idx / (KC / 4), c = 4 * (idx % (KC / 4));
+      u32x2 h, m, l;
+      split3_x4(r[i], h, m, l);
+      *reinterpret_cast<u32x2*>(&sA[buf][0][row * KP + c]) = h;
+      *reinterpret_cast<u32x2*>(&sA[buf][1][row * KP + c]) = m;
+      *reinterpret_cast<u32x2*>(&sA[buf][2][row * KP + c]) = l;
+    }
+  };
+  u32x4 ur[2][UL];
+  auto uload = [&](int xi, u32x4 (&r)[UL]) {
+#pragma unroll
+    for (int i = 0; i < UL; ++i) {
+      const int c = tid + i * NT;  // (plane, channel, 8-k chunk), k fastest: contiguous per plane
+      const int pl = c / (NN * KC / 8), rem = c % (NN * KC / 8);
+      r[i] = *reinterpret_cast<const u32x4*>(Up + (pl * 36 + xi) * NK + 8 * rem);
+    }
+  };
+  auto ustore = [&](int buf, const u32x4 (&r)[UL]) {
+#pragma unroll
+    for (int i = 0; i < UL; ++i) {
+      const int c = tid + i * NT;
+      const int pl = c / (NN * KC / 8), rem = c % (NN * KC / 8);
+      const int row = rem / (KC / 8), k = 8 * (rem % (KC / 8));
+      *reinterpret_cast<u32x4*>(&sU[buf][pl][row * KP + k]) = r[i];
+    }
+  };
+  f32x4 y[4][4], rr[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    rr[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) y[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+#pragma unroll
+  for (int j = 0; j < RING; ++j) gload(j, vr[j]);
+  uload(0, ur[0]);
+  uload(1, ur[1]);
+  lstore(0, vr[0]);
+  ustore(0, ur[0]);
+  gload(RING, vr[0]);
+  uload(2, ur[0]);
+  __syncthreads();
+#pragma unroll 1
+  for (int a = 0; a < 6; ++a) {
+#pragma unroll
+    for (int b = 0; b < 6; ++b) {
+      const int xi = 6 * a + b, cur = b & 1;
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        const int k = 32 * s + 8 * lq;
+        bf16x8g af[3], bf[3];
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+          af[p] = *reinterpret_cast<const bf16x8g*>(&sA[cur][p][(16 * wt + lr) * KP + k]);
+          bf[p] = *reinterpret_cast<const bf16x8g*>(&sU[cur][p][n * KP + k]);
+        }
+        // smallest partial products first
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[2], bf[0], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[1], bf[1], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0], bf[2], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[1], bf[0], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0], bf[1], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0], bf[0], acc, 0, 0, 0);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) axpy_c(rr[j], w4_at(j, b), acc);
+      // stage xi + 1 (V from its ring slot, U from the register pair), then refill both
+      const int vslot = (b + 1) % RING;
+      if (xi + 1 < 36) {
+        lstore(cur ^ 1, vr[vslot]);
+        ustore(cur ^ 1, ur[cur ^ 1]);
+      }
+      if (xi + 1 + RING < 36) gload(xi + 1 + RING, vr[vslot]);
+      if (xi + 3 < 36) uload(xi + 3, ur[cur ^ 1]);
+      __syncthreads();
+    }
+    // Y[i][j] += AT[i][a] R[j] (a is a runtime row index: coefficients selected from the table)
+    float at[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float v = 0.f;
+#pragma unroll
+      for (int q = 0; q < 6; ++q) v = a == q ? w4_at(i, q) : v;
+      at[i] = v;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) y[i][j] += at[i] * rr[j];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) rr[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  // epilogue, one tile quarter q at a time: the lanes' (channel n, tiles t0 + 16 wt + 4 lq + q)
+  // values go through LDS (the operand buffers are free now) so that every thread finishes
+  // 4 consecutive channels of one pixel with float4 accesses (conv_epilogue4)
+  constexpr int QT = 4 * NWT, EP = NN + 4;  // tiles per quarter; LDS row pitch (floats)
+  static_assert(QT * 16 * EP * 4 <= (int)sizeof(sU), "epilogue staging must fit in the U buffers");
+  float* E = reinterpret_cast<float*>(&sU[0][0][0]);
+  auto eaddr = [&](int idx) -> float* { return E + idx; };
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) *eaddr(((4 * wt + lq) * 16 + 4 * i + j) * EP + n) = y[i][j][q];
+    __syncthreads();
+    for (int idx = tid; idx < QT * 16 * (NN / 4); idx += NT) {
+      const int c4 = idx % (NN / 4), pq = idx / (NN / 4);
+      const int tl = pq / 16, px = pq % 16;
+      const int64_t t = t0 + 16 * (tl / 4) + 4 * (tl % 4) + q;
+      const int b = (int)(t / (TH * TW)), rem = (int)(t - (int64_t)b * TH * TW);
+      const int ty = rem / TW, tx = rem - ty * TW;
+      const int nn = 4 * c4, i = px / 4, j = px % 4;
+      const f32x4 v = *reinterpret_cast<const f32x4*>(eaddr(pq * EP + nn));
+      f32x4 bias4 = {0.f, 0.f, 0.f, 0.f}, sc4 = {1.f, 1.f, 1.f, 1.f};
+      if (g.bias) bias4 = *reinterpret_cast<const f32x4*>(g.bias + nn);
+      if (g.flags & PIS_SCALE) sc4 = *reinterpret_cast<const f32x4*>(g.scale + (size_t)b * N + nn);
+      const size_t pix = ((size_t)b * g.H + 4 * ty + i) * g.W + 4 * tx + j;
+      conv_epilogue4(g, pix, nn, v + bias4, sc4);
+    }
+    __syncthreads();
+  }
+}
+
+// fused path eligibility (pis_tune key 15): F(4x4), bf16x6 GEMMs, 64 -> 64 channels. Measured
+// (tools/bench_kernels.py --key 15, C2): enc1.conv1 forward 1.13 -> 0.98 ms, input gradient
+// 1.30 -> 1.13 ms; with 128 input or output channels (dec1.conv0, enc2.conv0) it is 2-8 % slower
+// than the separate GEMM + output transform, so those keep the 3-pass pipeline.
+static bool wino_gemm_out_wanted(int m, int64_t T, int C, int N) {
+  return m == 4 && tune_get(PIS_TUNE_WINO_GEMM_OUT) != 0 && tune_get(PIS_TUNE_WINO_TILE) == 3 && T % 32 == 0 &&
+         T >= 2 * (int64_t)C &&  // the filter planes fit in the M region
+         N == 64 && C == 64;
+}
+
+static int launch_wino_gemm_out(const float* V, const __bf16* Up, const IGemmArgs& a, int B, int64_t T,
+                                hipStream_t s) {
+  // 8 waves: 32 tiles x 64 channels per block
+  hipLaunchKernelGGL((wino4_gemm_out_x6_kernel<4, 2, 64>), dim3((int)(T / 32)), dim3(512), 0, s, V, Up, a, B);
+  return launch_status("wino_gemm_out");
+}
+
 static int grid_of(int64_t work) { return (int)std::max<int64_t>(1, std::min<int64_t>(cdiv(work, 256), 16384)); }
 
 // F(4x4,3x3) when the 4x4 tile grid fits and pis_tune key 11 allows it, else F(2x2,3x3)
@@ -923,6 +1125,20 @@ int launch_wino3x3(const IGemmArgs& a, int B, void* ws, hipStream_t s, float* ke
     hipLaunchKernelGGL(wino4_fused_kernel, dim3(blocks), dim3(256), 0, s, U, a, B);
     launch_hook("wino_fused", 1, s, flop);
     return launch_status("wino_fused");
+  }
+  if (wino_gemm_out_wanted(m, T, C, N)) {
+    // the pre-split filter planes (1.5x U's bytes) go where M would have been
+    __bf16* Up = reinterpret_cast<__bf16*>(Mt);
+    hipLaunchKernelGGL(wino4_filter_kernel, dim3(grid_of((int64_t)N * C)), dim3(256), 0, s, a.wt, a.ldw, N, C, U, 0,
+                       Up);
+    hipLaunchKernelGGL(wino4_input_kernel, dim3(grid_of(T * (C / 4))), dim3(256), 0, s, a.src, a.lds, B, a.H, a.W,
+                       C, V);
+    int rc = launch_status("wino_transforms");
+    if (rc) return rc;
+    launch_hook("wino_gemm_out", 0, s, flop);
+    rc = launch_wino_gemm_out(V, Up, a, B, T, s);
+    launch_hook("wino_gemm_out", 1, s, flop);
+    return rc;
   }
   if (m == 4) {
     hipLaunchKernelGGL(wino4_filter_kernel, dim3(grid_of((int64_t)N * C)), dim3(256), 0, s, a.wt, a.ldw, N, C, U, 0);

@@ -103,7 +103,7 @@ def test_conv3x3_dgrad_wgrad(hip, B, H, W, Cin, Cout):
 
 # every non-default kernel variant behind pis_tune (include/pis_capi.h) stays exact too
 TUNE_VARIANTS = [(4, 1), (4, 2), (4, 3), (5, 0), (6, 2048), (3, 0), (7, 1), (8, 0), (8, 2), (10, 0), (10, 1),
-                 (11, 0), (12, 0), (12, 2), (13, 0), (13, 2), (10, 2), (14, 0)]
+                 (11, 0), (12, 0), (12, 2), (13, 0), (13, 2), (10, 2), (14, 0), (15, 0)]
 
 
 @pytest.mark.parametrize("key,value", TUNE_VARIANTS)
@@ -127,7 +127,12 @@ def test_conv3x3_tuned_variants(hip, key, value):
                                                  (2, 8, 12, 128, 64, 1), (1, 12, 8, 64, 128, 1), (1, 8, 8, 64, 64, 1),
                                                  (2, 16, 32, 64, 128, 2), (1, 6, 10, 132, 64, 2),
                                                  (1, 5, 8, 256, 256, 2), (2, 8, 16, 256, 512, 0),
-                                                 (3, 10, 6, 128, 64, 2)])
+                                                 (3, 10, 6, 128, 64, 2),
+                                                 # 64 -> 64 runs the fused contraction + output
+                                                 # transform (key 15); the others the 3-pass path
+                                                 (2, 32, 64, 64, 64, 1), (2, 32, 64, 128, 64, 1),
+                                                 (2, 32, 64, 64, 128, 1), (2, 64, 64, 256, 128, 1),
+                                                 (2, 32, 64, 128, 128, 1), (2, 64, 64, 128, 256, 1)])
 def test_conv3x3_ex_winograd(hip, B, H, W, Cin, Cout, mode):
     """pis_conv3x3_fwd_ex / dgrad_ex with a workspace, and pis_conv3x3_wgrad: Winograd where the
     policy (pis_tune key 8: 1 = auto, 2 = whenever H, W are even) picks it, direct otherwise."""
