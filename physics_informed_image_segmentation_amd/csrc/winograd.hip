@@ -980,8 +980,8 @@ __global__ __launch_bounds__(64 * NWN * NWT) void wino4_gemm_out_x6_kernel(const
   gload(RING, vr[0]);
   uload(2, ur[0]);
   __syncthreads();
-#pragma unroll 1
-  for (int a = 0; a < 6; ++a) {
+#pragma unroll
+  for (int a = 0; a < 6; ++a) {  // fully unrolled: the compiler keeps exact vmcnt counts across rows
 #pragma unroll
     for (int b = 0; b < 6; ++b) {
       const int xi = 6 * a + b, cur = b & 1;
