@@ -351,10 +351,14 @@ __global__ __launch_bounds__(256) void reduce_slabs_kernel(const float* __restri
   __shared__ vec red[256];
   red[threadIdx.x] = s;
   __syncthreads();
+  // fixed-order pairwise tree over the groups (deterministic; log2(groups) barrier steps)
+  for (int stride = groups / 2; stride >= 1; stride /= 2) {
+    if (gi < stride) red[gi * cols + c] += red[(gi + stride) * cols + c];
+    __syncthreads();
+  }
   if (gi == 0 && col < nv) {
     vec t = accumulate ? *reinterpret_cast<vec*>(dst + col * VEC) : (vec)(0.f);
-    for (int k = 0; k < groups; ++k) t += red[k * cols + c];
-    *reinterpret_cast<vec*>(dst + col * VEC) = t;
+    *reinterpret_cast<vec*>(dst + col * VEC) = t + red[c];
   }
 }
 
@@ -363,9 +367,12 @@ int reduce_slabs_pitched(const float* part, int splits, int64_t n, int64_t pitch
   const bool v4 = (n % 4 == 0) && (pitch % 4 == 0) && ((uintptr_t)part % 16 == 0) && ((uintptr_t)dst % 16 == 0);
   const int64_t nv = v4 ? n / 4 : n;
   // threads per column-block: up to 64 slab groups for many slabs, narrower blocks for small outputs
+  // thousands of slabs over a few columns (the bias partials of the dz transforms): all 256
+  // threads of a block walk slabs, so the per-thread chains stay short
+  const int gmax = splits >= 1024 ? 256 : 64;
   int gwant = 1;
-  while (gwant < 64 && gwant < splits) gwant *= 2;
-  int cols = std::max(4, 256 / gwant);
+  while (gwant < gmax && gwant < splits) gwant *= 2;
+  int cols = std::max(splits >= 1024 ? 1 : 4, 256 / gwant);
   while (cols > 1 && cols / 2 >= nv) cols /= 2;
   const int grid = (int)cdiv(nv, cols);
   if (v4)
