@@ -279,7 +279,8 @@ def main():
     peak = 2500.0 / 6.0 if x6 else 157.3
     pipe = ("bf16 MFMA, fp32-accurate bf16x6 split (6 bf16 products per fp32 multiply-add); achieved/peak in "
             "fp32-equivalent FLOPs" if x6 else "fp32 MFMA")
-    kname = "gemm_nt_x6_kernel<" if x6 else DOMINANT_KERNEL
+    # bf16x6: gemm_nt_x6_bk32_kernel (K % 32 == 0, every C2 layer) or gemm_nt_x6_kernel
+    kname = "gemm_nt_x6_" if x6 else DOMINANT_KERNEL
     traffic = load_pmc_traffic(kname)
     if rank == 0:
         flops = conv_flops_per_image(H, W) * B
@@ -291,7 +292,8 @@ def main():
             "vs_baseline": None, "dtype": "fp32", "data": "synthetic",
             "config": {"workload": workload,
                        "global_batch": B * world, "image_size": [H, W], "parallelism": f"dp{world}"},
-            "roofline": {"bound": "mfma", "kernel": f"{kname}128, 128|64> ({DOMINANT}: the 36 batched GEMMs of Winograd F(4x4,3x3) fwd/dgrad)",
+            "roofline": {"bound": "mfma", "kernel": ("gemm_nt_x6_bk32_kernel<128, 128|64>" if x6 else "gemm_nt_kernel<128, 128|64>")
+                         + f" ({DOMINANT}: the 36 batched GEMMs of Winograd F(4x4,3x3) fwd/dgrad)",
                          "achieved": achieved, "peak": peak,
                          "unit": "TFLOP/s", "frac": achieved / peak, "traffic": traffic, "pipe": pipe,
                          "fp32_mfma_peak_frac": achieved / 157.3,

@@ -891,6 +891,124 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_x6_kernel(
     }
 }
 
+// K-step 32 variant of gemm_nt_x6_kernel with ONE LDS buffer (48 KB at 128 x 128, so three
+// blocks still fit a CU): compute, barrier, store the next stage, barrier, issue the loads of
+// the stage after — a load has a whole 48-MFMA compute phase to land, and every 128-B line a
+// wave touches is consumed in the same stage. LDS rows padded to 40 bf16 (80 B: conflict-free
+// 16-B fragment reads).
+template <int BM, int BN, int OCC = 2>
+__global__ __launch_bounds__(256, OCC) void gemm_nt_x6_bk32_kernel(const float* __restrict__ A,
+                                                                const float* __restrict__ Bm, float* __restrict__ Cm,
+                                                                int M, int N, int K, int64_t bsA, int64_t bsB,
+                                                                int64_t bsC) {
+  constexpr int BK = 32, KP = 40;
+  constexpr int TM = BM / 64, TN = BN / 64;
+  constexpr int AL = BM * 8 / 256, BL = BN * 8 / 256;  // float4 loads per thread per stage
+  __shared__ __attribute__((aligned(16))) __bf16 sA[3][BM * KP];
+  __shared__ __attribute__((aligned(16))) __bf16 sB[3][BN * KP];
+  A += blockIdx.y * bsA;
+  Bm += blockIdx.y * bsB;
+  Cm += blockIdx.y * bsC;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave & 1, wn = wave >> 1, li = lane & 31, lh = lane >> 5;
+  const int ntn = N / BN;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int m0 = (bid / ntn) * BM, n0 = (bid % ntn) * BN;
+  const int q8 = (tid & 7) * 4;
+  const bool full = m0 + BM <= M && K % BK == 0;
+  f32x4 ra[AL], rb[BL];
+  auto gload = [&](int k0) {
+    const int k = k0 + q8;
+#pragma unroll
+    for (int i = 0; i < AL; ++i) {
+      const int m = m0 + (tid + i * 256) / 8;
+      ra[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (full || (m < M && k < K)) ra[i] = *reinterpret_cast<const f32x4*>(A + (size_t)m * K + k);
+    }
+#pragma unroll
+    for (int i = 0; i < BL; ++i) {
+      const int n = n0 + (tid + i * 256) / 8;
+      rb[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (full || k < K) rb[i] = *reinterpret_cast<const f32x4*>(Bm + (size_t)n * K + k);
+    }
+  };
+  auto lstore = [&]() {
+#pragma unroll
+    for (int i = 0; i < AL; ++i) {
+      u32x2 h, m, l;
+      split3_x4(ra[i], h, m, l);
+      const int o = ((tid + i * 256) / 8) * KP + q8;
+      *reinterpret_cast<u32x2*>(&sA[0][o]) = h;
+      *reinterpret_cast<u32x2*>(&sA[1][o]) = m;
+      *reinterpret_cast<u32x2*>(&sA[2][o]) = l;
+    }
+#pragma unroll
+    for (int i = 0; i < BL; ++i) {
+      u32x2 h, m, l;
+      split3_x4(rb[i], h, m, l);
+      const int o = ((tid + i * 256) / 8) * KP + q8;
+      *reinterpret_cast<u32x2*>(&sB[0][o]) = h;
+      *reinterpret_cast<u32x2*>(&sB[1][o]) = m;
+      *reinterpret_cast<u32x2*>(&sB[2][o]) = l;
+    }
+  };
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int b = 0; b < TN; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+  const int KT = (K + BK - 1) / BK;
+  gload(0);
+  lstore();
+  if (KT > 1) gload(BK);
+  __syncthreads();
+  for (int kt = 0; kt < KT; ++kt) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 af[3][TM], bf[3][TN];
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+#pragma unroll
+        for (int a = 0; a < TM; ++a)
+          af[p][a] = *reinterpret_cast<const bf16x8*>(&sA[p][(wm * (BM / 2) + a * 32 + li) * KP + 16 * ks + 8 * lh]);
+#pragma unroll
+        for (int b = 0; b < TN; ++b)
+          bf[p][b] = *reinterpret_cast<const bf16x8*>(&sB[p][(wn * (BN / 2) + b * 32 + li) * KP + 16 * ks + 8 * lh]);
+      }
+#pragma unroll
+      for (int a = 0; a < TM; ++a)
+#pragma unroll
+        for (int b = 0; b < TN; ++b) {  // smallest partial products first
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[2][a], bf[0][b], acc[a][b], 0, 0, 0);
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1][a], bf[1][b], acc[a][b], 0, 0, 0);
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0][a], bf[2][b], acc[a][b], 0, 0, 0);
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1][a], bf[0][b], acc[a][b], 0, 0, 0);
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0][a], bf[1][b], acc[a][b], 0, 0, 0);
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0][a], bf[0][b], acc[a][b], 0, 0, 0);
+        }
+    }
+    if (kt + 1 < KT) {
+      __syncthreads();
+      lstore();
+      __syncthreads();
+      if (kt + 2 < KT) gload((kt + 2) * BK);
+    }
+  }
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int b = 0; b < TN; ++b) {
+      const int n = n0 + wn * (BN / 2) + b * 32 + li;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm * (BM / 2) + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        if (m < M) Cm[(size_t)m * N + n] = acc[a][b][r];
+      }
+    }
+}
+
 // ---- F(4x4,3x3) contraction fused with the output transform (bf16x6) --------------------
 // For the shallow, HBM-bound layers: the 36 products M[xi] = V[xi] U[xi]^T never go to HBM.
 // A block owns TB = 16 NWT tiles x all N = 16 NWN output channels (V is read exactly once) and
@@ -1159,14 +1277,23 @@ int launch_wino3x3(const IGemmArgs& a, int B, void* ws, hipStream_t s, float* ke
                        (int64_t)N * C, T * N);
     rc = launch_status("wino_gemm");
   } else if (v == 3 && N % 128 == 0) {
+    // K-step 32 single-buffer variant where C allows: 2-9 % faster (tools/bench_gemm.py)
     const dim3 grid((int)cdiv(T, 128) * (N / 128), nxi);
-    hipLaunchKernelGGL((gemm_nt_x6_kernel<128, 128>), grid, dim3(256), 0, s, V, U, Mt, (int)T, N, C, T * C,
-                       (int64_t)N * C, T * N);
+    if (C % 32 == 0)
+      hipLaunchKernelGGL((gemm_nt_x6_bk32_kernel<128, 128, 3>), grid, dim3(256), 0, s, V, U, Mt, (int)T, N, C,
+                         T * C, (int64_t)N * C, T * N);
+    else
+      hipLaunchKernelGGL((gemm_nt_x6_kernel<128, 128>), grid, dim3(256), 0, s, V, U, Mt, (int)T, N, C, T * C,
+                         (int64_t)N * C, T * N);
     rc = launch_status("wino_gemm");
   } else if (v == 3 && N % 64 == 0) {
     const dim3 grid((int)cdiv(T, 128) * (N / 64), nxi);
-    hipLaunchKernelGGL((gemm_nt_x6_kernel<128, 64>), grid, dim3(256), 0, s, V, U, Mt, (int)T, N, C, T * C,
-                       (int64_t)N * C, T * N);
+    if (C % 32 == 0)
+      hipLaunchKernelGGL((gemm_nt_x6_bk32_kernel<128, 64, 3>), grid, dim3(256), 0, s, V, U, Mt, (int)T, N, C,
+                         T * C, (int64_t)N * C, T * N);
+    else
+      hipLaunchKernelGGL((gemm_nt_x6_kernel<128, 64>), grid, dim3(256), 0, s, V, U, Mt, (int)T, N, C, T * C,
+                         (int64_t)N * C, T * N);
     rc = launch_status("wino_gemm");
   } else if (v == 2 && N % 128 == 0) {
     const dim3 grid((int)cdiv(T, 128) * (N / 128), nxi);
@@ -1234,11 +1361,13 @@ int launch_wino_wgrad_out(const float* M, int N, int C, float* dw, int accumulat
 // ---- tooling: time one batched NT GEMM variant (tools/bench_gemm.py) ----------------------
 // C[b] (M x N) = A[b] (M x K) . B[b]^T (N x K), batch b over gridDim.y, all row-major fp32.
 // variant: 0 bf16x6 128x128, 1 its no-global-load timing twin, 2 its no-split timing twin,
-// 3 fp32 MFMA 128x128, 4 bf16x6 128x64. Requires N % 128 == 0 (64 for 4), K % 16 == 0.
+// 3 fp32 MFMA 128x128, 4 bf16x6 128x64, 5/6 the K-step-32 single-buffer bf16x6 128x128 at 2 / 3
+// waves per SIMD, 7 its 128x64. Requires N % 128 == 0 (64 for 4), K % 16 == 0.
 extern "C" int pis_debug_gemm_nt(const float* A, const float* B, float* C, int M, int N, int K, int batch,
                                  int variant, pis_stream_t stream) {
-  const int bn = variant == 4 ? 64 : 128;
-  PIS_CHECK_ARG(A && B && C && M > 0 && N > 0 && K > 0 && batch > 0 && K % 16 == 0 && N % bn == 0,
+  const int bn = variant == 4 || variant == 7 ? 64 : 128;
+  PIS_CHECK_ARG(A && B && C && M > 0 && N > 0 && K > 0 && batch > 0 && K % (variant >= 5 ? 32 : 16) == 0 &&
+                    N % bn == 0,
                 "pis_debug_gemm_nt: bad arguments");
   hipStream_t s = (hipStream_t)stream;
   const dim3 grid((int)cdiv(M, 128) * (N / bn), batch);
@@ -1249,6 +1378,9 @@ extern "C" int pis_debug_gemm_nt(const float* A, const float* B, float* C, int M
     case 2: hipLaunchKernelGGL((gemm_nt_x6_kernel<128, 128, 2>), grid, dim3(256), 0, s, A, B, C, M, N, K, sa, sb, sc); break;
     case 3: hipLaunchKernelGGL((gemm_nt_kernel<128, 128>), grid, dim3(256), 0, s, A, B, C, M, N, K, sa, sb, sc); break;
     case 4: hipLaunchKernelGGL((gemm_nt_x6_kernel<128, 64>), grid, dim3(256), 0, s, A, B, C, M, N, K, sa, sb, sc); break;
+    case 5: hipLaunchKernelGGL((gemm_nt_x6_bk32_kernel<128, 128>), grid, dim3(256), 0, s, A, B, C, M, N, K, sa, sb, sc); break;
+    case 6: hipLaunchKernelGGL((gemm_nt_x6_bk32_kernel<128, 128, 3>), grid, dim3(256), 0, s, A, B, C, M, N, K, sa, sb, sc); break;
+    case 7: hipLaunchKernelGGL((gemm_nt_x6_bk32_kernel<128, 64, 3>), grid, dim3(256), 0, s, A, B, C, M, N, K, sa, sb, sc); break;
     default: set_error("pis_debug_gemm_nt: unknown variant %d", variant); return PIS_ERR_ARG;
   }
   return launch_status("debug_gemm_nt");

@@ -25,7 +25,7 @@ def per_kernel(path, counter):
     return {k: (sum(v) / len(v), len(v)) for k, v in acc.items()}
 
 
-def main(fetch_csv, write_csv, out_json, dominant="gemm_nt_x6_kernel<"):
+def main(fetch_csv, write_csv, out_json, dominant="gemm_nt_x6_"):
     f = per_kernel(fetch_csv, "FETCH_SIZE")
     w = per_kernel(write_csv, "WRITE_SIZE")
     table = {}
