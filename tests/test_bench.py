@@ -1,0 +1,42 @@
+"""bench.py: the algorithmic work it prices the step with and, on the GPU, the
+one-line JSON contract (metric, whole-job value, roofline with the dominant kernel, cpu_baseline)."""
+import importlib.util
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _bench():
+    spec = importlib.util.spec_from_file_location("pis_bench", os.path.join(HERE, "bench.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+@pytest.mark.parametrize("size,gflop", [(256, 272.4), (512, 1089.5), (1024, 4357.9)])
+def test_conv_flops_per_image(size, gflop):
+    """2 x MACs x 3 over every conv / convT minus enc1.conv0's input gradient."""
+    assert abs(_bench().conv_flops_per_image(size, size) / 1e9 - gflop) < 0.1
+
+
+@pytest.mark.gpu
+def test_bench_json_contract():
+    out = subprocess.run([sys.executable, os.path.join(HERE, "bench.py"), "--steps", "2", "--warmup", "1",
+                          "--no-cpu-baseline"], capture_output=True, text=True, timeout=110, cwd=HERE)
+    assert out.returncode == 0, out.stderr[-2000:]
+    line = [ln for ln in out.stdout.splitlines() if ln.startswith("{")][-1]
+    d = json.loads(line)
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+              "scaling", "vs_baseline", "dtype", "data", "config", "roofline"):
+        assert k in d, k
+    assert d["n_gpus"] == 1 and d["steps"] == 2 and d["scaling"] == "weak" and d["higher_is_better"] is True
+    assert abs(d["value"] - 8 * 1000.0 / d["ms_per_step"]) < 1e-6 * d["value"]  # B = 8 images per step
+    r = d["roofline"]
+    assert r["bound"] == "mfma" and r["unit"] == "TFLOP/s" and 0 < r["frac"] < 1
+    assert abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-9
+    assert r["launches_per_step"] > 0 and r["avg_launch_ms"] > 0
