@@ -43,6 +43,8 @@ typedef void* pis_stream_t; /* hipStream_t */
 #define PIS_SCALE 2      /* y *= scale[b*C + c]  (Dropout2d keep-scale)       */
 #define PIS_MASK 4       /* y *= (mask[pix*ldm + c] > 0)  (ReLU backward)     */
 #define PIS_ACCUMULATE 8 /* dst += result instead of dst = result             */
+#define PIS_WINO_PREPARED 16 /* conv3x3 dgrad_ex / wgrad_keep: pis_conv3x3_bwd_prep already wrote this
+                                layer's dz transforms into the call's workspace          */
 
 const char* pis_last_error(void);
 int pis_version(void);
@@ -75,7 +77,8 @@ int pis_version(void);
                                     bf16x6 on bf16 MFMA, 0 fp32 MFMA */
 #define PIS_TUNE_WINO_GEMM_OUT 15 /* F(4x4,3x3) 64 -> 64 channels: 1 (default) the 36 bf16x6 contractions fused with
                                      the output transform (M stays on chip), 0 separate GEMM + output transform */
-#define PIS_TUNE_NKEYS 16
+#define PIS_TUNE_WINO_DZ2 16     /* pis_conv3x3_bwd_prep: 1 (default) one pass over dz for both transforms, 0 off */
+#define PIS_TUNE_NKEYS 17
 #define PIS_DEBUG_NOLOAD (1 << 16)
 int pis_tune(int key, int value);
 /* Tooling (tools/bench_gemm.py): time one batched NT GEMM kernel variant in isolation,
@@ -131,6 +134,14 @@ int pis_conv3x3_fwd_keep(const float* x, int ldx, const float* w_krsc, const flo
 int pis_conv3x3_wgrad_keep(const float* x, int ldx, const float* dz, int ldz, float* dw_krsc, float* db,
                            int B, int H, int W, int Cin, int Cout, int flags, void* ws, size_t ws_bytes,
                            const float* keep, pis_stream_t stream);
+/* One pass over a layer's dz for both backward products (no reference counterpart: the two
+ * reads of dz that conv2d's input- and weight-gradient make): writes the F(4x4,3x3) input
+ * transform into ws_dgrad (for pis_conv3x3_dgrad_ex) and the F(3x3,4x4) dz transform + bias
+ * partials into ws_wgrad (for pis_conv3x3_wgrad_keep); both calls then pass PIS_WINO_PREPARED.
+ * Returns 1 when done, 0 when this layer / workspace does not take that path (call without the
+ * flag), < 0 on error. ws_wgrad must stay untouched until its pis_conv3x3_wgrad_keep ran. */
+int pis_conv3x3_bwd_prep(const float* dz, int ldz, int B, int H, int W, int Cin, int Cout, void* ws_dgrad,
+                         size_t ws_dgrad_bytes, void* ws_wgrad, size_t ws_wgrad_bytes, pis_stream_t stream);
 size_t pis_conv3x3_wgrad_ws(int B, int H, int W, int Cin, int Cout);
 int pis_conv3x3_wgrad(const float* x, int ldx, const float* dz, int ldz, float* dw_krsc, float* db,
                       int B, int H, int W, int Cin, int Cout, int flags, void* ws, size_t ws_bytes,

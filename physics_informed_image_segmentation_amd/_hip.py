@@ -16,7 +16,7 @@ import torch
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "_lib", "libpis.so")
 
-PIS_RELU, PIS_SCALE, PIS_MASK, PIS_ACCUMULATE = 1, 2, 4, 8
+PIS_RELU, PIS_SCALE, PIS_MASK, PIS_ACCUMULATE, PIS_WINO_PREPARED = 1, 2, 4, 8, 16
 PIS_LOSS_ALL_TERMS, PIS_LOSS_CHAIN_SIGMOID, PIS_LOSS_NO_REACTION = 1, 2, 4
 LOSS_NTERMS = 8
 TERM_TOTAL, TERM_DICE, TERM_BCE, TERM_RD, TERM_PF, TERM_I, TERM_P, TERM_T = range(8)
@@ -38,6 +38,7 @@ _SIGNATURES = {
     "pis_last_error": ([], ctypes.c_char_p),
     "pis_tune": ([I, I], c_int),
     "pis_debug_gemm_nt": ([P, P, P, I, I, I, I, I, P], c_int),
+    "pis_conv3x3_bwd_prep": ([P, I, I, I, I, I, I, P, Z, P, Z, P], c_int),
     "pis_conv3x3_fwd": ([P, I, P, P, P, P, I, I, I, I, I, I, I, P], c_int),
     "pis_conv3x3_flip": ([P, P, I, I, P], c_int),
     "pis_conv3x3_dgrad": ([P, I, P, P, I, P, P, I, I, I, I, I, I, I, P], c_int),

@@ -45,7 +45,15 @@ int wino_tile(int H, int W);
 size_t wino_ws_bytes(int B, int H, int W, int C, int N);
 // keep_v (optional, F(4x4) only): V is written there instead of the workspace and left for
 // the layer's weight gradient (pis_conv3x3_wgrad_keep)
-int launch_wino3x3(const IGemmArgs& a, int B, void* ws, hipStream_t s, float* keep_v = nullptr);
+// v_ready: V (F(4x4) only) is already in the workspace (pis_conv3x3_bwd_prep)
+int launch_wino3x3(const IGemmArgs& a, int B, void* ws, hipStream_t s, float* keep_v = nullptr,
+                   bool v_ready = false);
+float* wino_v_slot(void* ws, int C, int N);
+// one pass over dz: V (input-gradient input transform) and E + bias partials (weight gradient)
+int launch_wino_dz2(const float* dz, int ldz, int B, int H, int W, int N, float* V, float* E, float* bpart,
+                    hipStream_t s);
+// does pis_conv3x3_dgrad_ex take F(4x4,3x3) Winograd for this layer with this workspace?
+bool dgrad_wino4_planned(int B, int H, int W, int Cin, int Cout, int ldz, size_t ws_bytes);
 // Winograd weight-gradient pieces for tile edge m (2: F(3x3,2x2), 4: F(3x3,4x4)), nxi = (m+2)^2:
 // V[nxi][T][C] of x, E[nxi][T][N] of dz, dW from M[nxi][N][C]
 int launch_wino_input(const float* x, int ldx, int B, int H, int W, int C, float* V, hipStream_t s, int m);

@@ -517,12 +517,16 @@ static bool wino_wanted_dims(int H, int W, int C, int N) {
 }
 
 static int dispatch_conv3x3(const IGemmArgs& a, int B, void* ws, size_t ws_bytes, hipStream_t s,
-                            float* keep_v = nullptr) {
+                            float* keep_v = nullptr, bool v_ready = false) {
   // a kept transform is computed either way: then Winograd wins even where the plain policy
   // prefers the direct kernel (64 -> 64 at 512^2: +2 % forward, -27 % weight gradient)
   if (ws && wino_ok(a) && (keep_v || wino_wanted_dims(a.H, a.W, a.Csrc, a.N)) &&
       ws_bytes >= wino_ws_bytes(B, a.H, a.W, a.Csrc, a.N))
-    return launch_wino3x3(a, B, ws, s, keep_v);
+    return launch_wino3x3(a, B, ws, s, keep_v, v_ready);
+  if (v_ready) {
+    set_error("pis_conv3x3_dgrad_ex: PIS_WINO_PREPARED but this call does not take the Winograd path");
+    return PIS_ERR_ARG;
+  }
   int rc = launch_conv3x3(a, s);
   // direct path taken (e.g. a small workspace): the kept transform is still owed to the wgrad
   if (!rc && keep_v) rc = launch_wino_input(a.src, a.lds, B, a.H, a.W, a.Csrc, keep_v, s, 4);
@@ -624,7 +628,15 @@ extern "C" int pis_conv3x3_dgrad_ex(const float* dz, int ldz, const float* w_fli
   a.Csrc = Cout; a.ntaps = 9; a.tap_mode = TAP_CONV3; a.wt = w_flip; a.ldw = 9 * Cout; a.N = Cin;
   a.epi = EPI_NHWC; a.mask = mask; a.ldm = ldm; a.scale = scale; a.dst = dx; a.ldd = lddx;
   a.flags = flags & (PIS_MASK | PIS_SCALE | PIS_ACCUMULATE);
-  return dispatch_conv3x3(a, B, ws, ws_bytes, (hipStream_t)stream);
+  return dispatch_conv3x3(a, B, ws, ws_bytes, (hipStream_t)stream, nullptr, (flags & PIS_WINO_PREPARED) != 0);
+}
+
+bool pis::dgrad_wino4_planned(int B, int H, int W, int Cin, int Cout, int ldz, size_t ws_bytes) {
+  IGemmArgs a{};  // as pis_conv3x3_dgrad_ex builds it (dx / mask rows 16-B aligned)
+  a.H = H; a.W = W; a.Csrc = Cout; a.N = Cin; a.lds = ldz; a.ldd = 4; a.ldm = 4;
+  a.tap_mode = TAP_CONV3; a.epi = EPI_NHWC;
+  return wino_ok(a) && wino_tile(H, W) == 4 && wino_wanted_dims(H, W, Cout, Cin) &&
+         ws_bytes >= wino_ws_bytes(B, H, W, Cout, Cin);
 }
 
 extern "C" int pis_convt2x2_fwd(const float* x, int ldx, const float* w_ijoc, const float* bias,

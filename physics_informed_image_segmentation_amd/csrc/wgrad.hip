@@ -824,7 +824,7 @@ size_t wino_wgrad_keep_bytes(int B, int H, int W, int Cin, int Cout) {
 
 static int wino_wgrad(const float* x, int ldx, const float* dz, int ldz, float* dw, float* db, int B, int H, int W,
                       int Cin, int Cout, int acc, const WinoWgradPlan& p, void* ws, hipStream_t s,
-                      const float* keep_v = nullptr) {
+                      const float* keep_v = nullptr, bool e_ready = false) {
   char* base = (char*)ws;
   float* V = (float*)base;
   float* E = (float*)(base + p.off_E);
@@ -834,7 +834,7 @@ static int wino_wgrad(const float* x, int ldx, const float* dz, int ldz, float* 
   if (keep_v && p.m == 4) V = const_cast<float*>(keep_v);  // the forward's transform of x
   else rc = launch_wino_input(x, ldx, B, H, W, Cin, V, s, p.m);
   float* bpart = (db && p.fused_bias) ? (float*)(base + p.off_cs) : nullptr;
-  if (!rc) rc = launch_wino_dz(dz, ldz, B, H, W, Cout, E, s, p.m, bpart);
+  if (!rc && !e_ready) rc = launch_wino_dz(dz, ldz, B, H, W, Cout, E, s, p.m, bpart);
   if (rc) return rc;
   WgradArgs a{};
   a.a = E; a.lda = Cout; a.a_up2 = 0; a.Ca = Cout;
@@ -888,12 +888,31 @@ extern "C" int pis_conv3x3_wgrad_keep(const float* x, int ldx, const float* dz, 
                                       float* db, int B, int H, int W, int Cin, int Cout, int flags, void* ws,
                                       size_t ws_bytes, const float* keep, pis_stream_t stream) {
   const WinoWgradPlan wp = wino_wgrad_plan(B, H, W, Cin, Cout);
+  const bool prepared = flags & PIS_WINO_PREPARED;
+  PIS_CHECK_ARG(!prepared || (keep && wp.use && wp.m == 4),
+                "pis_conv3x3_wgrad_keep: PIS_WINO_PREPARED needs the kept-transform F(3x3,4x4) path");
   if (!keep || !(wp.use && wp.m == 4))
     return pis_conv3x3_wgrad(x, ldx, dz, ldz, dw_krsc, db, B, H, W, Cin, Cout, flags, ws, ws_bytes, stream);
   PIS_CHECK_ARG(x && dz && dw_krsc && ldz % 4 == 0, "pis_conv3x3_wgrad_keep: bad arguments");
   PIS_CHECK_ARG(ws && ws_bytes >= wp.total, "pis_conv3x3_wgrad_keep: workspace too small");
   return wino_wgrad(x, ldx, dz, ldz, dw_krsc, db, B, H, W, Cin, Cout, flags & PIS_ACCUMULATE, wp, ws,
-                    (hipStream_t)stream, keep);
+                    (hipStream_t)stream, keep, prepared);
+}
+
+extern "C" int pis_conv3x3_bwd_prep(const float* dz, int ldz, int B, int H, int W, int Cin, int Cout,
+                                    void* ws_dgrad, size_t ws_dgrad_bytes, void* ws_wgrad, size_t ws_wgrad_bytes,
+                                    pis_stream_t stream) {
+  PIS_CHECK_ARG(dz && B > 0 && H > 0 && W > 0 && Cin > 0 && Cout > 0, "pis_conv3x3_bwd_prep: bad arguments");
+  const WinoWgradPlan wp = wino_wgrad_plan(B, H, W, Cin, Cout);
+  if (tune_get(PIS_TUNE_WINO_DZ2) == 0 || !ws_dgrad || !ws_wgrad || !(wp.use && wp.m == 4) ||
+      ws_wgrad_bytes < wp.total || ldz % 4 || !dgrad_wino4_planned(B, H, W, Cin, Cout, ldz, ws_dgrad_bytes))
+    return 0;  // not applicable: the two calls transform dz themselves
+  float* V = wino_v_slot(ws_dgrad, Cout, Cin);
+  char* base = (char*)ws_wgrad;
+  float* E = (float*)(base + wp.off_E);
+  float* bpart = wp.fused_bias ? (float*)(base + wp.off_cs) : nullptr;
+  const int rc = launch_wino_dz2(dz, ldz, B, H, W, Cout, V, E, bpart, (hipStream_t)stream);
+  return rc ? rc : 1;
 }
 
 extern "C" int pis_conv3x3_wgrad(const float* x, int ldx, const float* dz, int ldz, float* dw_krsc,

@@ -293,6 +293,39 @@ __global__ __launch_bounds__(256) void wino4_filter_kernel(const float* __restri
 }
 
 // V[xi][t][c] = (BT d BT^T)[xi], d = the 6x6 input patch at rows 4ty-1.., cols 4tx-1.. (zero padded)
+__device__ __forceinline__ void wino4_input_item(const float* __restrict__ x, int ldx, int H, int W, int C,
+                                                 float* __restrict__ V, int64_t TC, int64_t t, int b, int ty,
+                                                 int tx, int c) {
+  f32x4 v[6][6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i)
+#pragma unroll
+    for (int j = 0; j < 6; ++j) v[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int k = 0; k < 6; ++k) {  // input row k: its row transform, then its share of every V row
+    const int h = 4 * ty - 1 + k;
+    f32x4 d[6];
+#pragma unroll
+    for (int l = 0; l < 6; ++l) {
+      const int ww = 4 * tx - 1 + l;
+      d[l] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (h >= 0 && h < H && ww >= 0 && ww < W)
+        d[l] = *reinterpret_cast<const f32x4*>(x + (((size_t)b * H + h) * W + ww) * ldx + c);
+    }
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+      f32x4 r = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int l = 0; l < 6; ++l) axpy_c(r, w4_bt(j, l), d[l]);
+#pragma unroll
+      for (int i = 0; i < 6; ++i) axpy_c(v[i][j], w4_bt(i, k), r);
+    }
+  }
+#pragma unroll
+  for (int xi = 0; xi < 36; ++xi)
+    *reinterpret_cast<f32x4*>(V + (size_t)xi * TC + t * C + c) = v[xi / 6][xi % 6];
+}
+
 __global__ __launch_bounds__(256) void wino4_input_kernel(const float* __restrict__ x, int ldx, int B, int H, int W,
                                                           int C, float* __restrict__ V) {
   const int c4n = C / 4, TW = W / 4, TH = H / 4;
@@ -302,34 +335,7 @@ __global__ __launch_bounds__(256) void wino4_input_kernel(const float* __restric
     const int c = (int)(e - t * c4n) * 4;
     const int b = (int)(t / (TH * TW)), rem = (int)(t - (int64_t)b * TH * TW);
     const int ty = rem / TW, tx = rem - ty * TW;
-    f32x4 v[6][6];
-#pragma unroll
-    for (int i = 0; i < 6; ++i)
-#pragma unroll
-      for (int j = 0; j < 6; ++j) v[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int k = 0; k < 6; ++k) {  // input row k: its row transform, then its share of every V row
-      const int h = 4 * ty - 1 + k;
-      f32x4 d[6];
-#pragma unroll
-      for (int l = 0; l < 6; ++l) {
-        const int ww = 4 * tx - 1 + l;
-        d[l] = f32x4{0.f, 0.f, 0.f, 0.f};
-        if (h >= 0 && h < H && ww >= 0 && ww < W)
-          d[l] = *reinterpret_cast<const f32x4*>(x + (((size_t)b * H + h) * W + ww) * ldx + c);
-      }
-#pragma unroll
-      for (int j = 0; j < 6; ++j) {
-        f32x4 r = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int l = 0; l < 6; ++l) axpy_c(r, w4_bt(j, l), d[l]);
-#pragma unroll
-        for (int i = 0; i < 6; ++i) axpy_c(v[i][j], w4_bt(i, k), r);
-      }
-    }
-#pragma unroll
-    for (int xi = 0; xi < 36; ++xi)
-      *reinterpret_cast<f32x4*>(V + (size_t)xi * TC + t * C + c) = v[xi / 6][xi % 6];
+    wino4_input_item(x, ldx, H, W, C, V, TC, t, b, ty, tx, c);
   }
 }
 
@@ -557,10 +563,54 @@ __host__ __device__ constexpr float w4_at3(int i, int k) {
   return m[i][k];
 }
 
-// E[xi][t][n] = (G4 e G4^T)[xi], e = dz at output pixels (4ty + i, 4tx + j)
+// E[xi][t][n] = (G4 e G4^T)[xi], e = dz at output pixels (4ty + i, 4tx + j); bsum += the tile's
+// channel sums (the bias gradient)
+__device__ __forceinline__ void wino4_dz_item(const float* __restrict__ dz, int ldz, int H, int W, int N,
+                                              float* __restrict__ E, int64_t TN, int64_t t, int b, int ty, int tx,
+                                              int n, f32x4& bsum) {
+  f32x4 v[6][6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i)
+#pragma unroll
+    for (int j = 0; j < 6; ++j) v[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    f32x4 d[4];
+#pragma unroll
+    for (int l = 0; l < 4; ++l)
+      d[l] = *reinterpret_cast<const f32x4*>(dz + (((size_t)b * H + 4 * ty + k) * W + 4 * tx + l) * ldz + n);
+    bsum += (d[0] + d[1]) + (d[2] + d[3]);
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+      f32x4 r = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int l = 0; l < 4; ++l) axpy_c(r, w4_g4(j, l), d[l]);
+#pragma unroll
+      for (int i = 0; i < 6; ++i) axpy_c(v[i][j], w4_g4(i, k), r);
+    }
+  }
+#pragma unroll
+  for (int xi = 0; xi < 36; ++xi)
+    *reinterpret_cast<f32x4*>(E + (size_t)xi * TN + t * N + n) = v[xi / 6][xi % 6];
+}
+
+// bpart[blockIdx.x][N] = fixed-order block reduction of the threads sharing a channel quad
+// (tid mod n4n; with 256 * gridDim.x a multiple of N / 4 a thread's channels never change
+// across its grid-stride items)
+__device__ __forceinline__ void wino4_bias_partials(f32x4 bsum, int N, float* __restrict__ bpart) {
+  const int n4n = N / 4;
+  __shared__ f32x4 red[256];
+  red[threadIdx.x] = bsum;
+  __syncthreads();
+  if ((int)threadIdx.x < n4n) {
+    f32x4 acc = red[threadIdx.x];
+    for (int k = threadIdx.x + n4n; k < 256; k += n4n) acc += red[k];
+    *reinterpret_cast<f32x4*>(bpart + (size_t)blockIdx.x * N + 4 * threadIdx.x) = acc;
+  }
+}
+
 // With bpart != NULL it also leaves the bias gradient's per-block channel sums in
-// bpart[blockIdx.x][N] (every dz pixel belongs to exactly one tile): with 256 * gridDim.x a
-// multiple of N / 4 a thread's channels never change across its grid-stride items.
+// bpart[blockIdx.x][N] (every dz pixel belongs to exactly one tile).
 __global__ __launch_bounds__(256) void wino4_dz_kernel(const float* __restrict__ dz, int ldz, int B, int H, int W,
                                                        int N, float* __restrict__ E, float* __restrict__ bpart) {
   const int n4n = N / 4, TW = W / 4, TH = H / 4;
@@ -571,41 +621,30 @@ __global__ __launch_bounds__(256) void wino4_dz_kernel(const float* __restrict__
     const int n = (int)(e - t * n4n) * 4;
     const int b = (int)(t / (TH * TW)), rem = (int)(t - (int64_t)b * TH * TW);
     const int ty = rem / TW, tx = rem - ty * TW;
-    f32x4 v[6][6];
-#pragma unroll
-    for (int i = 0; i < 6; ++i)
-#pragma unroll
-      for (int j = 0; j < 6; ++j) v[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      f32x4 d[4];
-#pragma unroll
-      for (int l = 0; l < 4; ++l)
-        d[l] = *reinterpret_cast<const f32x4*>(dz + (((size_t)b * H + 4 * ty + k) * W + 4 * tx + l) * ldz + n);
-      bsum += (d[0] + d[1]) + (d[2] + d[3]);
-#pragma unroll
-      for (int j = 0; j < 6; ++j) {
-        f32x4 r = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int l = 0; l < 4; ++l) axpy_c(r, w4_g4(j, l), d[l]);
-#pragma unroll
-        for (int i = 0; i < 6; ++i) axpy_c(v[i][j], w4_g4(i, k), r);
-      }
-    }
-#pragma unroll
-    for (int xi = 0; xi < 36; ++xi)
-      *reinterpret_cast<f32x4*>(E + (size_t)xi * TN + t * N + n) = v[xi / 6][xi % 6];
+    wino4_dz_item(dz, ldz, H, W, N, E, TN, t, b, ty, tx, n, bsum);
   }
-  if (!bpart) return;
-  // fixed-order block reduction of the threads sharing a channel quad (tid mod n4n)
-  __shared__ f32x4 red[256];
-  red[threadIdx.x] = bsum;
-  __syncthreads();
-  if ((int)threadIdx.x < n4n) {
-    f32x4 acc = red[threadIdx.x];
-    for (int k = threadIdx.x + n4n; k < 256; k += n4n) acc += red[k];
-    *reinterpret_cast<f32x4*>(bpart + (size_t)blockIdx.x * N + 4 * threadIdx.x) = acc;
+  if (bpart) wino4_bias_partials(bsum, N, bpart);
+}
+
+// One pass over a layer's dz for both of its backward products: V = the input gradient's
+// F(4x4,3x3) input transform of dz (as wino4_input_kernel) and E = the weight gradient's
+// F(3x3,4x4) transform + bias partials (as wino4_dz_kernel); the second half re-reads the tile's
+// 4x4 interior from cache instead of HBM. Same grid as wino4_dz_kernel (bpart layout).
+__global__ __launch_bounds__(256) void wino4_dz2_kernel(const float* __restrict__ dz, int ldz, int B, int H, int W,
+                                                        int N, float* __restrict__ V, float* __restrict__ E,
+                                                        float* __restrict__ bpart) {
+  const int n4n = N / 4, TW = W / 4, TH = H / 4;
+  const int64_t T = (int64_t)B * TH * TW, TN = T * N;
+  f32x4 bsum = {0.f, 0.f, 0.f, 0.f};
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < T * n4n; e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t t = e / n4n;
+    const int n = (int)(e - t * n4n) * 4;
+    const int b = (int)(t / (TH * TW)), rem = (int)(t - (int64_t)b * TH * TW);
+    const int ty = rem / TW, tx = rem - ty * TW;
+    wino4_input_item(dz, ldz, H, W, N, V, TN, t, b, ty, tx, n);
+    wino4_dz_item(dz, ldz, H, W, N, E, TN, t, b, ty, tx, n, bsum);
   }
+  if (bpart) wino4_bias_partials(bsum, N, bpart);
 }
 
 // dw[n][r][s][c] (+)= (AT3 M AT3^T)[r][s], M[xi][n][c] the reduced tile sums
@@ -1208,6 +1247,9 @@ bool wino_ok(const IGemmArgs& a) {
          a.N % 4 == 0 && a.lds % 4 == 0 && a.ldd % 4 == 0 && (!(a.flags & PIS_MASK) || a.ldm % 4 == 0);
 }
 
+// where launch_wino3x3 keeps V inside its workspace (pis_conv3x3_bwd_prep writes it there)
+float* wino_v_slot(void* ws, int C, int N) { return (float*)ws + (size_t)36 * N * C; }
+
 size_t wino_ws_bytes(int B, int H, int W, int C, int N) {
   const int m = wino_tile(H, W), nxi = (m + 2) * (m + 2);
   const int64_t T = (int64_t)B * (H / m) * (W / m);
@@ -1225,7 +1267,7 @@ static bool wino_fused_wanted(int H, int W, int C, int N) {
 }
 
 // a describes the direct conv (src/lds = input, wt/ldw = KRSC weights, N outputs, epilogue)
-int launch_wino3x3(const IGemmArgs& a, int B, void* ws, hipStream_t s, float* keep_v) {
+int launch_wino3x3(const IGemmArgs& a, int B, void* ws, hipStream_t s, float* keep_v, bool v_ready) {
   const int C = a.Csrc, N = a.N;
   const int m = wino_tile(a.H, a.W), nxi = (m + 2) * (m + 2);
   const int64_t T = (int64_t)B * (a.H / m) * (a.W / m);
@@ -1249,8 +1291,9 @@ int launch_wino3x3(const IGemmArgs& a, int B, void* ws, hipStream_t s, float* ke
     __bf16* Up = reinterpret_cast<__bf16*>(Mt);
     hipLaunchKernelGGL(wino4_filter_kernel, dim3(grid_of((int64_t)N * C)), dim3(256), 0, s, a.wt, a.ldw, N, C, U, 0,
                        Up);
-    hipLaunchKernelGGL(wino4_input_kernel, dim3(grid_of(T * (C / 4))), dim3(256), 0, s, a.src, a.lds, B, a.H, a.W,
-                       C, V);
+    if (!v_ready)
+      hipLaunchKernelGGL(wino4_input_kernel, dim3(grid_of(T * (C / 4))), dim3(256), 0, s, a.src, a.lds, B, a.H, a.W,
+                         C, V);
     int rc = launch_status("wino_transforms");
     if (rc) return rc;
     launch_hook("wino_gemm_out", 0, s, flop);
@@ -1258,10 +1301,12 @@ int launch_wino3x3(const IGemmArgs& a, int B, void* ws, hipStream_t s, float* ke
     launch_hook("wino_gemm_out", 1, s, flop);
     return rc;
   }
+  if (v_ready && m != 4) return set_error("launch_wino3x3: prepared transforms need F(4x4,3x3)"), PIS_ERR_ARG;
   if (m == 4) {
     hipLaunchKernelGGL(wino4_filter_kernel, dim3(grid_of((int64_t)N * C)), dim3(256), 0, s, a.wt, a.ldw, N, C, U, 0);
-    hipLaunchKernelGGL(wino4_input_kernel, dim3(grid_of(T * (C / 4))), dim3(256), 0, s, a.src, a.lds, B, a.H, a.W,
-                       C, V);
+    if (!v_ready)
+      hipLaunchKernelGGL(wino4_input_kernel, dim3(grid_of(T * (C / 4))), dim3(256), 0, s, a.src, a.lds, B, a.H, a.W,
+                         C, V);
   } else {
     hipLaunchKernelGGL(wino_filter_kernel, dim3(grid_of((int64_t)N * C)), dim3(256), 0, s, a.wt, a.ldw, N, C, U);
     hipLaunchKernelGGL(wino_input_kernel, dim3(grid_of(T * (C / 4))), dim3(256), 0, s, a.src, a.lds, B, a.H, a.W,
@@ -1343,6 +1388,13 @@ int launch_wino_dz(const float* dz, int ldz, int B, int H, int W, int N, float* 
   else
     hipLaunchKernelGGL(wino_dz_kernel, dim3(grid_of(T * (N / 4))), dim3(256), 0, s, dz, ldz, B, H, W, N, E);
   return launch_status("wino_dz");
+}
+
+int launch_wino_dz2(const float* dz, int ldz, int B, int H, int W, int N, float* V, float* E, float* bpart,
+                    hipStream_t s) {
+  const int64_t T = (int64_t)B * (H / 4) * (W / 4);
+  hipLaunchKernelGGL(wino4_dz2_kernel, dim3(grid_of(T * (N / 4))), dim3(256), 0, s, dz, ldz, B, H, W, N, V, E, bpart);
+  return launch_status("wino_dz2");
 }
 
 int launch_wino_wgrad_out(const float* M, int N, int C, float* dw, int accumulate, hipStream_t s, int m,

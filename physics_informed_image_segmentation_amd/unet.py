@@ -28,7 +28,7 @@ import torch
 import torch.nn as nn
 
 from . import _hip
-from ._hip import PIS_ACCUMULATE, PIS_MASK, PIS_RELU, PIS_SCALE, call, ptr
+from ._hip import PIS_ACCUMULATE, PIS_MASK, PIS_RELU, PIS_SCALE, PIS_WINO_PREPARED, call, ptr
 
 # block name -> dropout multiplier of UNet(dropout=d), src/unet.py:120-154
 _DROP_MULT = {"enc1": 0.0, "enc2": 0.5, "enc3": 1.0, "enc4": 1.0, "bottleneck": 1.0,
@@ -369,6 +369,17 @@ class UNetEngine:
         # weight gradients run on a second stream beside the input-gradient chain (backward)
         self.ws2 = torch.empty_like(self.ws) if self.side_stream else self.ws
         self.side = torch.cuda.Stream(device=dev) if self.side_stream else None
+        # pis_conv3x3_bwd_prep writes a layer's weight-gradient dz transform from the MAIN stream
+        # while the side stream may still read the previous layer's: two alternating workspaces
+        # for those weight gradients, each reused only after the side stream has finished with it
+        ws3 = 0
+        for l in range(1, 6):
+            Hl, Wl, Cl = (H >> (l - 1), W >> (l - 1), c << (l - 1)) if l < 5 else (H5, W5, 8 * c)
+            for cin in (Cl // 2, Cl, 2 * Cl):
+                ws3 = max(ws3, lib.pis_conv3x3_wgrad_ws(B, Hl, Wl, cin, Cl))
+        self.ws3 = [torch.empty((ws3 + 15) // 4, dtype=torch.float32, device=dev) for _ in range(2)]
+        self.ws3_bytes = self.ws3[0].numel() * 4
+        self.ws3_free: List[Optional[torch.cuda.Event]] = [None, None]
         # per-layer kept Winograd input transforms (training forward -> weight gradient);
         # ~2.25x each layer's input activation, ~12 GB at B=8 512^2
         self.keep: Dict[int, torch.Tensor] = {}
@@ -574,16 +585,40 @@ class UNetEngine:
             call("pis_convt2x2_prep", up.weight.data_ptr(), t.data_ptr(), up.in_channels, up.out_channels, st)
             flips[id(up)] = t
 
+        lib = _hip.lib()
+        nprep = [0]
+
         def conv_bwd(conv, x: _Buf, dz: _Buf, dx: Optional[_Buf], Hl, Wl, mask: Optional[_Buf], scale):
+            kept = self.keep.get(id(conv))
+            prep, wsw, wswb = 0, ws2, wsb
+            if dx is not None and kept is not None:
+                # one pass over dz for both backward products (main stream): V into the dgrad
+                # workspace, E + bias partials into an alternating weight-gradient workspace
+                j = nprep[0] & 1
+                if self.ws3_free[j] is not None:
+                    main.wait_event(self.ws3_free[j])
+                prep = lib.pis_conv3x3_bwd_prep(dz.p, dz.ld, B, Hl, Wl, conv.in_channels, conv.out_channels, ws, wsb,
+                                                self.ws3[j].data_ptr(), self.ws3_bytes, st)
+                if prep < 0:
+                    raise RuntimeError(lib.pis_last_error().decode())
+                if prep:
+                    nprep[0] += 1
+                    wsw, wswb = self.ws3[j].data_ptr(), self.ws3_bytes
             to_side()
             call("pis_conv3x3_wgrad_keep", x.p, x.ld, dz.p, dz.ld, self._gptr(conv.weight), self._gptr(conv.bias),
-                 B, Hl, Wl, conv.in_channels, conv.out_channels, acc, ws2, wsb, ptr(self.keep.get(id(conv))), sst)
+                 B, Hl, Wl, conv.in_channels, conv.out_channels, acc | (PIS_WINO_PREPARED if prep else 0), wsw, wswb,
+                 ptr(kept), sst)
+            if prep and side is not main:
+                ev = torch.cuda.Event()
+                ev.record(side)
+                self.ws3_free[(nprep[0] - 1) & 1] = ev
             ready_on_side(conv.weight, conv.bias)
             if dx is not None:
                 flags = (PIS_MASK if mask is not None else 0) | (PIS_SCALE if scale is not None else 0)
                 call("pis_conv3x3_dgrad_ex", dz.p, dz.ld, flips[id(conv)].data_ptr(),
                      mask.p if mask is not None else 0, mask.ld if mask is not None else 0, ptr(scale),
-                     dx.p, dx.ld, B, Hl, Wl, conv.in_channels, conv.out_channels, flags, ws, wsb, st)
+                     dx.p, dx.ld, B, Hl, Wl, conv.in_channels, conv.out_channels,
+                     flags | (PIS_WINO_PREPARED if prep else 0), ws, wsb, st)
 
         # head: sigmoid backward + 1x1 conv + ReLU backward of dec1.conv1
         d1 = _Buf(bf["d1_1"], c)

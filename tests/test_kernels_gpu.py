@@ -103,7 +103,7 @@ def test_conv3x3_dgrad_wgrad(hip, B, H, W, Cin, Cout):
 
 # every non-default kernel variant behind pis_tune (include/pis_capi.h) stays exact too
 TUNE_VARIANTS = [(4, 1), (4, 2), (4, 3), (5, 0), (6, 2048), (3, 0), (7, 1), (8, 0), (8, 2), (10, 0), (10, 1),
-                 (11, 0), (12, 0), (12, 2), (13, 0), (13, 2), (10, 2), (14, 0), (15, 0)]
+                 (11, 0), (12, 0), (12, 2), (13, 0), (13, 2), (10, 2), (14, 0), (15, 0), (16, 0)]
 
 
 @pytest.mark.parametrize("key,value", TUNE_VARIANTS)
@@ -617,3 +617,64 @@ def test_convt_bf16x6_is_fp32_accurate(hip, Cin, Cout):
     for e6, e32 in zip(errs["x6"], errs["f32"]):
         assert e6 <= 1.25 * e32 + 1e-9, errs
         assert e6 < 5e-6, errs
+
+
+@pytest.mark.parametrize("B,H,W,Cin,Cout", [(2, 32, 64, 64, 64), (2, 16, 32, 128, 128), (1, 32, 32, 128, 64),
+                                           (2, 16, 16, 256, 256)])
+def test_conv3x3_bwd_prep(hip, B, H, W, Cin, Cout):
+    """pis_conv3x3_bwd_prep: one pass over dz writes both backward transforms; the dgrad_ex and
+    wgrad_keep calls that then pass PIS_WINO_PREPARED give the same results as without it (and
+    as the float64 reference), bias gradient included."""
+    PREP = 16
+    g = torch.Generator().manual_seed(23)
+    x = F.relu(torch.randn(B, Cin, H, W, generator=g))
+    w = torch.randn(Cout, Cin, 3, 3, generator=g) / (3 * Cin ** 0.5)
+    dz = torch.randn(B, Cout, H, W, generator=g)
+    xd, wd, dzd = nhwc(x).cuda(), krsc(w).cuda(), nhwc(dz).cuda()
+    mask = xd.clone()
+    nk = hip.pis_conv3x3_keep_bytes(B, H, W, Cin, Cout)
+    keep = torch.empty(nk // 4 + 1, device="cuda")
+    nws = hip.pis_conv3x3_ex_ws(B, H, W, Cin, Cout)
+    ws = torch.empty(nws // 4 + 1, device="cuda")
+    y = torch.empty(B, H, W, Cout, device="cuda")
+    assert hip.pis_conv3x3_fwd_keep(xd.data_ptr(), Cin, wd.data_ptr(), 0, 0, y.data_ptr(), Cout, B, H, W, Cin,
+                                    Cout, 0, ws.data_ptr(), nws, keep.data_ptr(), s()) == 0
+    wf = torch.empty(Cin * 9 * Cout, device="cuda")
+    assert hip.pis_conv3x3_flip(wd.data_ptr(), wf.data_ptr(), Cin, Cout, s()) == 0
+    nwg = hip.pis_conv3x3_wgrad_ws(B, H, W, Cin, Cout)
+    out = {}
+    for prep in (False, True):
+        wsg = torch.full((nwg // 4 + 1,), float("nan"), device="cuda")
+        wsd = torch.full((nws // 4 + 1,), float("nan"), device="cuda")
+        flag = 0
+        if prep:
+            rc = hip.pis_conv3x3_bwd_prep(dzd.data_ptr(), Cout, B, H, W, Cin, Cout, wsd.data_ptr(), nws,
+                                          wsg.data_ptr(), nwg, s())
+            assert rc == 1, hip.pis_last_error()
+            flag = PREP
+        dw = torch.empty(Cout, 3, 3, Cin, device="cuda")
+        db = torch.empty(Cout, device="cuda")
+        assert hip.pis_conv3x3_wgrad_keep(xd.data_ptr(), Cin, dzd.data_ptr(), Cout, dw.data_ptr(), db.data_ptr(), B,
+                                          H, W, Cin, Cout, flag, wsg.data_ptr(), nwg, keep.data_ptr(), s()) == 0
+        dx = torch.empty(B, H, W, Cin, device="cuda")
+        assert hip.pis_conv3x3_dgrad_ex(dzd.data_ptr(), Cout, wf.data_ptr(), mask.data_ptr(), Cin, 0, dx.data_ptr(),
+                                        Cin, B, H, W, Cin, Cout, MASK | flag, wsd.data_ptr(), nws, s()) == 0, \
+            hip.pis_last_error()
+        torch.cuda.synchronize()
+        out[prep] = (dw.cpu(), db.cpu(), dx.cpu())
+    for a, b in zip(out[False], out[True]):
+        assert torch.equal(a, b)  # the same arithmetic, only one read of dz fewer
+    dw_ref = torch.nn.grad.conv2d_weight(x.double(), w.shape, dz.double(), padding=1)
+    dx_ref = torch.nn.grad.conv2d_input(x.shape, w.double(), dz.double(), padding=1) * (x > 0)
+    assert rel_err(out[True][0].permute(0, 3, 1, 2), dw_ref) < 1e-5
+    assert rel_err(out[True][1], dz.sum(dim=(0, 2, 3))) < 1e-5
+    assert rel_err(nchw(out[True][2]), dx_ref) < 1e-5
+
+
+def test_conv3x3_bwd_prep_not_applicable(hip):
+    """Layers off the F(4x4) path (odd grid) return 0 and leave the calls to transform dz."""
+    B, H, W, Cin, Cout = 1, 6, 10, 64, 64
+    dz = torch.zeros(B, H, W, Cout, device="cuda")
+    ws = torch.empty(1 << 20, device="cuda")
+    assert hip.pis_conv3x3_bwd_prep(dz.data_ptr(), Cout, B, H, W, Cin, Cout, ws.data_ptr(), 4 << 20,
+                                    ws.data_ptr(), 4 << 20, s()) == 0
