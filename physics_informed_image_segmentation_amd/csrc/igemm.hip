@@ -423,6 +423,57 @@ int launch_conv3x3(const IGemmArgs& a, hipStream_t s) {
   return launch_status("conv3x3_halo");
 }
 
+// Cin == 1, Cout == 64, W % 64 == 0: block = one 64-pixel row segment of one image; the 3 x 66
+// input window is staged in LDS once, thread (pixel group pg = t / 16, channel quad t % 16)
+// computes pixels pg + 16 k (k < 4) and every wave stores 4 whole pixels (1 KB) per instruction
+// (no per-pixel index divisions, no redundant x loads).
+__global__ __launch_bounds__(256) void conv3x3_c1_row_kernel(const float* __restrict__ x, int ldx,
+                                                             const float* __restrict__ w,
+                                                             const float* __restrict__ bias,
+                                                             const float* __restrict__ scale,
+                                                             float* __restrict__ y, int ldy, int H, int W,
+                                                             int flags) {
+  constexpr int Cout = 64, SEG = 64;
+  __shared__ float xs[3][SEG + 2];
+  const int segs = W / SEG;
+  const int bh = blockIdx.x / segs, w0 = (blockIdx.x - bh * segs) * SEG;
+  const int b = bh / H, h = bh - b * H;
+  const int tid = threadIdx.x;
+  if (tid < 3 * (SEG + 2)) {
+    const int r = tid / (SEG + 2), c = tid - r * (SEG + 2);
+    const int hh = h + r - 1, ww = w0 + c - 1;
+    xs[r][c] = (hh >= 0 && hh < H && ww >= 0 && ww < W) ? x[(((size_t)b * H + hh) * W + ww) * ldx] : 0.f;
+  }
+  const int c4 = (tid & 15) * 4, pg = tid >> 4;
+  f32x4 wt[9], b4;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    b4[j] = bias ? bias[c4 + j] : 0.f;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) wt[t][j] = w[(c4 + j) * 9 + t];
+  }
+  f32x4 sc = {1.f, 1.f, 1.f, 1.f};
+  if (flags & PIS_SCALE) sc = *reinterpret_cast<const f32x4*>(scale + (size_t)b * Cout + c4);
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int px = pg + 16 * k;
+    f32x4 acc = b4;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const float xv = xs[t / 3][px + t % 3];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[j] = fmaf(xv, wt[t][j], acc[j]);
+    }
+    if (flags & PIS_RELU) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[j] = fmaxf(acc[j], 0.f);
+    }
+    acc *= sc;
+    *reinterpret_cast<f32x4*>(y + (((size_t)b * H + h) * W + w0 + px) * ldy + c4) = acc;
+  }
+}
+
 __global__ __launch_bounds__(256) void conv3x3_c1_fwd_kernel(const float* __restrict__ x, int ldx,
                                                              const float* __restrict__ w,
                                                              const float* __restrict__ bias,
@@ -580,6 +631,11 @@ extern "C" int pis_conv3x3_fwd_ex(const float* x, int ldx, const float* w_krsc, 
   PIS_CHECK_ARG(!(flags & PIS_SCALE) || scale, "pis_conv3x3_fwd: PIS_SCALE without scale");
   PIS_CHECK_ARG(ldy % 4 == 0 && Cout % 4 == 0, "pis_conv3x3_fwd: ldy/Cout must be multiples of 4");
   hipStream_t s = (hipStream_t)stream;
+  if (Cin == 1 && Cout == 64 && W % 64 == 0) {
+    hipLaunchKernelGGL(conv3x3_c1_row_kernel, dim3((unsigned)(B * H * (W / 64))), dim3(256), 0, s, x, ldx, w_krsc,
+                       bias, scale, y, ldy, H, W, flags);
+    return launch_status("conv3x3_c1_row");
+  }
   if (Cin == 1) {
     PIS_CHECK_ARG(Cout <= 1024, "pis_conv3x3_fwd: Cin==1 path supports Cout<=1024");
     const int64_t threads = (int64_t)B * H * W * (Cout / 4);

@@ -771,6 +771,60 @@ __global__ __launch_bounds__(256) void wgrad_c1_kernel(const float* __restrict__
   }
 }
 
+// Cin == 1, Cout == 64, W % 64 == 0: blocks walk 64-pixel row segments (grid-stride, fixed
+// grid so the partial slabs stay few); per segment the 3 x 66 input window is staged in LDS and
+// thread (pixel group t / 16, channel quad t % 16) accumulates pixels pg + 16 k: dz is read with
+// whole-pixel float4 rows (1 KB per wave instruction), no per-pixel index divisions.
+__global__ __launch_bounds__(256) void wgrad_c1_row_kernel(const float* __restrict__ x, int ldx,
+                                                           const float* __restrict__ dz, int ldz, int B, int H,
+                                                           int W, float* __restrict__ part,
+                                                           float* __restrict__ part_b) {
+  constexpr int Cout = 64, SEG = 64;
+  __shared__ float xs[3][SEG + 2];
+  __shared__ f32x4 red[256][10];
+  const int tid = threadIdx.x, c4 = (tid & 15) * 4, pg = tid >> 4;
+  f32x4 acc[10];
+#pragma unroll
+  for (int k = 0; k < 10; ++k) acc[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int segs = W / SEG;
+  const int nseg = B * H * segs;
+  for (int sg = blockIdx.x; sg < nseg; sg += gridDim.x) {
+    const int bh = sg / segs, w0 = (sg - bh * segs) * SEG;
+    const int b = bh / H, h = bh - b * H;
+    __syncthreads();  // the previous segment's window is no longer read
+    if (tid < 3 * (SEG + 2)) {
+      const int r = tid / (SEG + 2), c = tid - r * (SEG + 2);
+      const int hh = h + r - 1, ww = w0 + c - 1;
+      xs[r][c] = (hh >= 0 && hh < H && ww >= 0 && ww < W) ? x[(((size_t)b * H + hh) * W + ww) * ldx] : 0.f;
+    }
+    __syncthreads();
+    const float* dzr = dz + (((size_t)b * H + h) * W + w0) * ldz + c4;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int px = pg + 16 * k;
+      const f32x4 dv = *reinterpret_cast<const f32x4*>(dzr + (size_t)px * ldz);
+      acc[9] += dv;
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const float xv = xs[t / 3][px + t % 3];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[t][j] = fmaf(xv, dv[j], acc[t][j]);
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 10; ++k) red[tid][k] = acc[k];
+  __syncthreads();
+  // fixed-order sum over the 16 pixel groups: output o = (n, k), k = tap (0..8) or bias (9)
+  for (int o = tid; o < 10 * Cout; o += 256) {
+    const int n = o / 10, k = o - n * 10, qq = n >> 2, j = n & 3;
+    float sum = 0.f;
+    for (int gi = 0; gi < 16; ++gi) sum += red[gi * 16 + qq][k][j];
+    if (k < 9) part[(size_t)blockIdx.x * 9 * Cout + n * 9 + k] = sum;
+    else if (part_b) part_b[(size_t)blockIdx.x * Cout + n] = sum;
+  }
+}
+
 // Winograd weight gradient (csrc/winograd.hip), F(3x3, 4x4) when the 4x4 tile grid fits (pis_tune
 // key 11), else F(3x3, 2x2): V = B^T x B and E = G e G^T per tile, M_xi[n][c] = sum_tiles
 // E_xi[t][n] V_xi[t][c] as nxi = (m+2)^2 batched split-K GEMMs over the T tiles (slabs
@@ -958,11 +1012,17 @@ extern "C" int pis_conv3x3_wgrad(const float* x, int ldx, const float* dz, int l
     const int blocks = (int)cdiv(npix, ppb);
     float* part = (float*)ws;
     float* part_b = db ? part + (size_t)C1_BLOCKS * 9 * Cout : nullptr;
-    hipLaunchKernelGGL(wgrad_c1_kernel, dim3(blocks), dim3(256), 0, s, x, ldx, dz, ldz, B, H, W, Cout, ppb,
-                       part, part_b);
+    const bool row = Cout == 64 && W % 64 == 0 && ldz % 4 == 0;
+    if (row)
+      hipLaunchKernelGGL(wgrad_c1_row_kernel, dim3(C1_BLOCKS), dim3(256), 0, s, x, ldx, dz, ldz, B, H, W, part,
+                         part_b);
+    else
+      hipLaunchKernelGGL(wgrad_c1_kernel, dim3(blocks), dim3(256), 0, s, x, ldx, dz, ldz, B, H, W, Cout, ppb,
+                         part, part_b);
     int rc = launch_status("wgrad_c1");
-    if (!rc) rc = reduce_slabs(part, blocks, (int64_t)9 * Cout, dw_krsc, acc, s);
-    if (!rc && db) rc = reduce_slabs(part_b, blocks, Cout, db, acc, s);
+    const int nslab = row ? C1_BLOCKS : blocks;
+    if (!rc) rc = reduce_slabs(part, nslab, (int64_t)9 * Cout, dw_krsc, acc, s);
+    if (!rc && db) rc = reduce_slabs(part_b, nslab, Cout, db, acc, s);
     return rc;
   }
   const WgradPlan pl = conv_plan(B, H, W, Cin, Cout);

@@ -36,7 +36,7 @@ def s():
 
 
 @pytest.mark.parametrize("B,H,W,Cin,Cout,ld_extra", [(2, 16, 24, 64, 64, 0), (1, 8, 8, 128, 256, 64),
-                                                      (3, 5, 7, 64, 128, 0), (2, 16, 16, 1, 64, 0),
+                                                      (3, 5, 7, 64, 128, 0), (2, 16, 16, 1, 64, 0), (2, 8, 128, 1, 64, 64), (1, 5, 64, 1, 64, 0),
                                                       (2, 16, 32, 64, 128, 64), (1, 8, 16, 132, 64, 0),
                                                       (2, 24, 48, 256, 192, 0)])
 def test_conv3x3_fwd(hip, B, H, W, Cin, Cout, ld_extra):
@@ -195,7 +195,17 @@ def test_conv3x3_ex_winograd(hip, B, H, W, Cin, Cout, mode):
 
 
 def test_conv3x3_c1_wgrad(hip):
-    B, H, W, Cout = 2, 32, 16, 64
+    _check_c1_wgrad(hip, 2, 32, 16)
+
+
+@pytest.mark.parametrize("B,H,W", [(2, 24, 128), (1, 3, 64)])
+def test_conv3x3_c1_wgrad_rows(hip, B, H, W):
+    """W % 64 == 0: the row-segment Cin == 1 weight-gradient kernel."""
+    _check_c1_wgrad(hip, B, H, W)
+
+
+def _check_c1_wgrad(hip, B, H, W):
+    Cout = 64
     g = torch.Generator().manual_seed(2)
     x = torch.rand(B, 1, H, W, generator=g)
     dz = torch.randn(B, Cout, H, W, generator=g)
