@@ -131,6 +131,13 @@ size_t pis_conv3x3_keep_bytes(int B, int H, int W, int Cin, int Cout);
 int pis_conv3x3_fwd_keep(const float* x, int ldx, const float* w_krsc, const float* bias,
                          const float* scale, float* y, int ldy, int B, int H, int W, int Cin, int Cout,
                          int flags, void* ws, size_t ws_bytes, float* keep, pis_stream_t stream);
+/* The encoder's conv1 + MaxPool2d(2,2) (src/unet.py:126, :177-188): as pis_conv3x3_fwd_keep, and
+ * pool[b][h/2][w/2][c] (ld = Cout) = the 2x2 max of the y it wrote — in the F(4x4,3x3) output
+ * epilogue when that path runs (no second read of y), else by pis_maxpool2x2_fwd. H, W even; no
+ * PIS_ACCUMULATE. */
+int pis_conv3x3_fwd_pool(const float* x, int ldx, const float* w_krsc, const float* bias, const float* scale,
+                         float* y, int ldy, int B, int H, int W, int Cin, int Cout, int flags, void* ws,
+                         size_t ws_bytes, float* keep, float* pool, pis_stream_t stream);
 int pis_conv3x3_wgrad_keep(const float* x, int ldx, const float* dz, int ldz, float* dw_krsc, float* db,
                            int B, int H, int W, int Cin, int Cout, int flags, void* ws, size_t ws_bytes,
                            const float* keep, pis_stream_t stream);

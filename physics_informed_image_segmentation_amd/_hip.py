@@ -39,6 +39,7 @@ _SIGNATURES = {
     "pis_tune": ([I, I], c_int),
     "pis_debug_gemm_nt": ([P, P, P, I, I, I, I, I, P], c_int),
     "pis_conv3x3_bwd_prep": ([P, I, I, I, I, I, I, P, Z, P, Z, P], c_int),
+    "pis_conv3x3_fwd_pool": ([P, I, P, P, P, P, I, I, I, I, I, I, I, P, Z, P, P, P], c_int),
     "pis_conv3x3_fwd": ([P, I, P, P, P, P, I, I, I, I, I, I, I, P], c_int),
     "pis_conv3x3_flip": ([P, P, I, I, P], c_int),
     "pis_conv3x3_dgrad": ([P, I, P, P, I, P, P, I, I, I, I, I, I, I, P], c_int),

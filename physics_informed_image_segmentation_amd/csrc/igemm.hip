@@ -623,6 +623,34 @@ extern "C" int pis_conv3x3_fwd_keep(const float* x, int ldx, const float* w_krsc
   return dispatch_conv3x3(a, B, ws, ws_bytes, (hipStream_t)stream, keep);
 }
 
+extern "C" int pis_conv3x3_fwd_pool(const float* x, int ldx, const float* w_krsc, const float* bias,
+                                    const float* scale, float* y, int ldy, int B, int H, int W, int Cin,
+                                    int Cout, int flags, void* ws, size_t ws_bytes, float* keep, float* pool,
+                                    pis_stream_t stream) {
+  PIS_CHECK_ARG(pool && H % 2 == 0 && W % 2 == 0 && !(flags & PIS_ACCUMULATE),
+                "pis_conv3x3_fwd_pool: needs a pool buffer, even H and W, no PIS_ACCUMULATE");
+  PIS_CHECK_ARG(x && w_krsc && y && B > 0 && Cin > 0 && (Cin == 1 || ldx % 4 == 0) && ldy % 4 == 0 &&
+                    Cout % 4 == 0,
+                "pis_conv3x3_fwd_pool: bad arguments");
+  PIS_CHECK_ARG(!(flags & PIS_SCALE) || scale, "pis_conv3x3_fwd_pool: PIS_SCALE without scale");
+  const bool kept = keep && pis_conv3x3_keep_bytes(B, H, W, Cin, Cout) > 0;
+  IGemmArgs a{};
+  a.src = x; a.lds = ldx; a.Hs = H; a.Ws = W; a.H = H; a.W = W; a.M = B * H * W;
+  a.Csrc = Cin; a.ntaps = 9; a.tap_mode = TAP_CONV3; a.wt = w_krsc; a.ldw = 9 * Cin; a.N = Cout;
+  a.epi = EPI_NHWC; a.bias = bias; a.scale = scale; a.dst = y; a.ldd = ldy;
+  a.flags = flags & (PIS_RELU | PIS_SCALE);
+  // the F(4x4,3x3) output epilogues pool the tile they just wrote; every other path pools after
+  if (Cin > 1 && ws && wino_ok(a) && wino_tile(H, W) == 4 && (kept || wino_wanted_dims(H, W, Cin, Cout)) &&
+      ws_bytes >= wino_ws_bytes(B, H, W, Cin, Cout)) {
+    a.pool = pool;
+    return dispatch_conv3x3(a, B, ws, ws_bytes, (hipStream_t)stream, kept ? keep : nullptr);
+  }
+  int rc = pis_conv3x3_fwd_keep(x, ldx, w_krsc, bias, scale, y, ldy, B, H, W, Cin, Cout, flags, ws, ws_bytes,
+                                keep, stream);
+  if (rc) return rc;
+  return pis_maxpool2x2_fwd(y, ldy, pool, B, H, W, Cout, stream);
+}
+
 extern "C" int pis_conv3x3_fwd_ex(const float* x, int ldx, const float* w_krsc, const float* bias,
                                   const float* scale, float* y, int ldy, int B, int H, int W, int Cin,
                                   int Cout, int flags, void* ws, size_t ws_bytes, pis_stream_t stream) {

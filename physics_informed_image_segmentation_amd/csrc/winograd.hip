@@ -88,7 +88,7 @@ __global__ __launch_bounds__(256) void wino_input_kernel(const float* __restrict
 
 // conv epilogue on 4 channels of one output pixel (v = conv + bias): ReLU, ReLU-backward
 // mask, dropout keep-scale, accumulate — the direct kernels' epilogue (igemm.hip)
-__device__ __forceinline__ void conv_epilogue4(const IGemmArgs& g, size_t pix, int n, f32x4 v, f32x4 sc4) {
+__device__ __forceinline__ f32x4 conv_epilogue4(const IGemmArgs& g, size_t pix, int n, f32x4 v, f32x4 sc4) {
   if (g.flags & PIS_RELU) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) v[k] = fmaxf(v[k], 0.f);
@@ -102,6 +102,14 @@ __device__ __forceinline__ void conv_epilogue4(const IGemmArgs& g, size_t pix, i
   float* dst = g.dst + pix * g.ldd + n;
   if (g.flags & PIS_ACCUMULATE) v += *reinterpret_cast<const f32x4*>(dst);
   *reinterpret_cast<f32x4*>(dst) = v;
+  return v;
+}
+
+__device__ __forceinline__ f32x4 max4(f32x4 a, f32x4 b, f32x4 c, f32x4 d) {
+  f32x4 m;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) m[k] = fmaxf(fmaxf(a[k], b[k]), fmaxf(c[k], d[k]));
+  return m;
 }
 
 // Y = A^T M A per tile and 4 output channels, then the conv epilogue of the direct
@@ -370,13 +378,24 @@ __global__ __launch_bounds__(256) void wino4_output_kernel(const float* __restri
     f32x4 bias4 = {0.f, 0.f, 0.f, 0.f}, sc4 = {1.f, 1.f, 1.f, 1.f};
     if (g.bias) bias4 = *reinterpret_cast<const f32x4*>(g.bias + n);
     if (g.flags & PIS_SCALE) sc4 = *reinterpret_cast<const f32x4*>(g.scale + (size_t)b * N + n);
+    f32x4 o[4][4];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const size_t pix = ((size_t)b * g.H + 4 * ty + i) * g.W + 4 * tx + j;
-        conv_epilogue4(g, pix, n, y[i][j] + bias4, sc4);
+        o[i][j] = conv_epilogue4(g, pix, n, y[i][j] + bias4, sc4);
       }
+    if (g.pool) {  // the tile's four 2x2 max-pool outputs (the encoder's MaxPool2d)
+#pragma unroll
+      for (int qi = 0; qi < 2; ++qi)
+#pragma unroll
+        for (int qj = 0; qj < 2; ++qj) {
+          const size_t pp = ((size_t)b * (g.H / 2) + 2 * ty + qi) * (g.W / 2) + 2 * tx + qj;
+          *reinterpret_cast<f32x4*>(g.pool + pp * N + n) =
+              max4(o[2 * qi][2 * qj], o[2 * qi][2 * qj + 1], o[2 * qi + 1][2 * qj], o[2 * qi + 1][2 * qj + 1]);
+        }
+    }
   }
 }
 
@@ -1202,19 +1221,31 @@ __global__ __launch_bounds__(64 * NWN * NWT) void wino4_gemm_out_x6_kernel(const
 #pragma unroll
       for (int j = 0; j < 4; ++j) *eaddr(((4 * wt + lq) * 16 + 4 * i + j) * EP + n) = y[i][j][q];
     __syncthreads();
-    for (int idx = tid; idx < QT * 16 * (NN / 4); idx += NT) {
+    // one 2x2 pixel quad x 4 channels per item (the max pool of the quad when g.pool is set)
+    for (int idx = tid; idx < QT * 4 * (NN / 4); idx += NT) {
       const int c4 = idx % (NN / 4), pq = idx / (NN / 4);
-      const int tl = pq / 16, px = pq % 16;
+      const int tl = pq / 4, quad = pq % 4, qi = quad >> 1, qj = quad & 1;
       const int64_t t = t0 + 16 * (tl / 4) + 4 * (tl % 4) + q;
       const int b = (int)(t / (TH * TW)), rem = (int)(t - (int64_t)b * TH * TW);
       const int ty = rem / TW, tx = rem - ty * TW;
-      const int nn = 4 * c4, i = px / 4, j = px % 4;
-      const f32x4 v = *reinterpret_cast<const f32x4*>(eaddr(pq * EP + nn));
+      const int nn = 4 * c4;
       f32x4 bias4 = {0.f, 0.f, 0.f, 0.f}, sc4 = {1.f, 1.f, 1.f, 1.f};
       if (g.bias) bias4 = *reinterpret_cast<const f32x4*>(g.bias + nn);
       if (g.flags & PIS_SCALE) sc4 = *reinterpret_cast<const f32x4*>(g.scale + (size_t)b * N + nn);
-      const size_t pix = ((size_t)b * g.H + 4 * ty + i) * g.W + 4 * tx + j;
-      conv_epilogue4(g, pix, nn, v + bias4, sc4);
+      f32x4 o[2][2];
+#pragma unroll
+      for (int di = 0; di < 2; ++di)
+#pragma unroll
+        for (int dj = 0; dj < 2; ++dj) {
+          const int i = 2 * qi + di, j = 2 * qj + dj;
+          const f32x4 v = *reinterpret_cast<const f32x4*>(eaddr((tl * 16 + 4 * i + j) * EP + nn));
+          const size_t pix = ((size_t)b * g.H + 4 * ty + i) * g.W + 4 * tx + j;
+          o[di][dj] = conv_epilogue4(g, pix, nn, v + bias4, sc4);
+        }
+      if (g.pool) {
+        const size_t pp = ((size_t)b * (g.H / 2) + 2 * ty + qi) * (g.W / 2) + 2 * tx + qj;
+        *reinterpret_cast<f32x4*>(g.pool + pp * N + nn) = max4(o[0][0], o[0][1], o[1][0], o[1][1]);
+      }
     }
     __syncthreads();
   }

@@ -423,9 +423,14 @@ class UNetEngine:
     def _stream(self):
         return torch.cuda.current_stream().cuda_stream
 
-    def _conv_fwd(self, conv: nn.Conv2d, x: _Buf, y: _Buf, B, H, W, scale):
+    def _conv_fwd(self, conv: nn.Conv2d, x: _Buf, y: _Buf, B, H, W, scale, pool: Optional[torch.Tensor] = None):
         flags = PIS_RELU | (PIS_SCALE if scale is not None else 0)
         keep = self.keep.get(id(conv)) if self._keeping else None
+        if pool is not None:  # encoder conv1 + MaxPool2d in one call (pooled in the output epilogue)
+            call("pis_conv3x3_fwd_pool", x.p, x.ld, conv.weight.data_ptr(), conv.bias.data_ptr(), ptr(scale),
+                 y.p, y.ld, B, H, W, conv.in_channels, conv.out_channels, flags, self.ws.data_ptr(), self.ws_bytes,
+                 ptr(keep), pool.data_ptr(), self._stream())
+            return
         call("pis_conv3x3_fwd_keep", x.p, x.ld, conv.weight.data_ptr(), conv.bias.data_ptr(), ptr(scale),
              y.p, y.ld, B, H, W, conv.in_channels, conv.out_channels, flags, self.ws.data_ptr(), self.ws_bytes,
              ptr(keep), self._stream())
@@ -463,8 +468,7 @@ class UNetEngine:
             a = _Buf(bf[f"a{l}"], Cl)
             e = _Buf(bf[f"cat{l}"], 2 * Cl, Cl)         # enc output lives in the concat buffer
             self._conv_fwd(blk.conv0, src, a, B, Hl, Wl, scales[f"enc{l}"])
-            self._conv_fwd(blk.conv1, a, e, B, Hl, Wl, None)
-            call("pis_maxpool2x2_fwd", e.p, e.ld, bf[f"pool{l}"].data_ptr(), B, Hl, Wl, Cl, self._stream())
+            self._conv_fwd(blk.conv1, a, e, B, Hl, Wl, None, pool=bf[f"pool{l}"])
             src = _Buf(bf[f"pool{l}"], Cl)
         H5, W5 = H >> 4, W >> 4
         blk = m.bottleneck

@@ -688,3 +688,34 @@ def test_conv3x3_bwd_prep_not_applicable(hip):
     ws = torch.empty(1 << 20, device="cuda")
     assert hip.pis_conv3x3_bwd_prep(dz.data_ptr(), Cout, B, H, W, Cin, Cout, ws.data_ptr(), 4 << 20,
                                     ws.data_ptr(), 4 << 20, s()) == 0
+
+
+@pytest.mark.parametrize("B,H,W,Cin,Cout,keep", [(2, 32, 64, 64, 64, True), (2, 16, 32, 128, 128, True),
+                                                (2, 16, 32, 128, 128, False), (1, 6, 10, 64, 64, False),
+                                                (2, 16, 16, 1, 64, False), (1, 8, 8, 512, 256, True)])
+def test_conv3x3_fwd_pool(hip, B, H, W, Cin, Cout, keep):
+    """pis_conv3x3_fwd_pool = conv (bias, ReLU, keep-scale) + MaxPool2d(2,2) of its output: pooled in
+    the F(4x4) output epilogues (fused 64->64 kernel and the output-transform kernel), by the
+    pooling kernel on every other path; y lands in a concat slice (ldy = 2 Cout)."""
+    g = torch.Generator().manual_seed(29)
+    x = F.relu(torch.randn(B, Cin, H, W, generator=g))
+    w = torch.randn(Cout, Cin, 3, 3, generator=g) / (3 * Cin ** 0.5)
+    b = torch.randn(Cout, generator=g)
+    scale = (torch.rand(B, Cout, generator=g) > 0.2).float() / 0.8
+    y_ref = F.relu(F.conv2d(x, w, b, padding=1)) * scale[:, :, None, None]
+    p_ref = F.max_pool2d(y_ref, 2)
+    xd, wd, bd, sd = nhwc(x).cuda(), krsc(w).cuda(), b.cuda(), scale.cuda()
+    nws = hip.pis_conv3x3_ex_ws(B, H, W, Cin, Cout)
+    ws = torch.empty(max(nws, 4) // 4 + 1, device="cuda")
+    nk = hip.pis_conv3x3_keep_bytes(B, H, W, Cin, Cout)
+    kp = torch.empty(max(nk, 4) // 4 + 1, device="cuda") if keep and nk else None
+    y = torch.full((B, H, W, 2 * Cout), 7.0, device="cuda")
+    pool = torch.empty(B, H // 2, W // 2, Cout, device="cuda")
+    rc = hip.pis_conv3x3_fwd_pool(xd.data_ptr(), Cin, wd.data_ptr(), bd.data_ptr(), sd.data_ptr(), y.data_ptr(),
+                                  2 * Cout, B, H, W, Cin, Cout, RELU | SCALE, ws.data_ptr(), nws,
+                                  kp.data_ptr() if kp is not None else 0, pool.data_ptr(), s())
+    assert rc == 0, hip.pis_last_error()
+    torch.cuda.synchronize()
+    assert rel_err(nchw(y[..., :Cout].cpu()), y_ref) < 1e-5
+    assert torch.all(y[..., Cout:] == 7.0)
+    assert rel_err(nchw(pool.cpu()), p_ref) < 1e-5
