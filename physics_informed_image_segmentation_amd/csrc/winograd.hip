@@ -1,19 +1,24 @@
-// Winograd F(2x2, 3x3) for the deep 3x3 convs (fwd, and dgrad on flipped weights).
+// Winograd 3x3 convolutions (fwd, and dgrad on flipped weights) and weight gradients.
 //
-// A 2x2 output tile needs 16 multiply-adds per (input, output) channel pair
-// instead of 36: with U = G g G^T (weights), V = B^T d B (4x4 input patch) and
-// M_xi = sum_c V_xi[tile][c] U_xi[n][c] for the 16 positions xi, the outputs are
-// Y = A^T M A. The 16 contractions are ordinary fp32 GEMMs (T tiles x N x C)
-// on the MFMA path (batched igemm, 1/2.25 of the direct conv's FLOPs); the
-// transforms are bandwidth-bound streams with only +-1 and 1/2 coefficients:
+// Contents, in file order:
+//   * F(2x2,3x3) / F(3x3,2x2): transforms for grids not divisible by 4 (pis_tune(11, 0));
+//   * F(4x4,3x3) / F(3x3,4x4) (the default): filter, input, output, dz and merged-dz (dz2)
+//     transforms — bandwidth-bound streams, one thread per tile x 4 channels, compile-time
+//     Cook-Toom coefficients on the points {0, 1, -1, 1/2, -2, inf};
+//   * the opt-in fully fused F(4x4) kernel (pis_tune(12, 2));
+//   * the 36 batched NT GEMMs M_xi = V_xi U_xi^T: fp32 MFMA (gemm_nt_kernel) and fp32-accurate
+//     bf16x6 on bf16 MFMA (gemm_nt_x6_kernel; gemm_nt_x6_bk32_kernel, the default);
+//   * the fused 64->64 contraction + output transform (wino4_gemm_out_x6_kernel);
+//   * launchers (launch_wino3x3 ...) and the pis_debug_gemm_nt tooling entry.
+//
+// With U = G g G^T (weights), V = B^T d B (input patch) and M_xi = sum_c V_xi[tile][c] U_xi[n][c],
+// the outputs are Y = A^T M A: (m + 2)^2 / m^2 multiply-adds per output instead of 9.
+// Workspace (floats): U[nxi][N][C], V[nxi][T][C], M[nxi][T][N], T = B (H/m) (W/m) tiles.
+//
+// F(2x2,3x3) matrices:
 //   B^T = [1 0 -1 0; 0 1 1 0; 0 -1 1 0; 0 1 0 -1]
 //   G   = [1 0 0; 1/2 1/2 1/2; 1/2 -1/2 1/2; 0 0 1]
 //   A^T = [1 1 1 0; 0 1 -1 -1]
-// It pays where the channel counts are large enough for the GEMMs to stay
-// MFMA-bound while V and M make one HBM round trip each (levels 3-4 and the
-// bottleneck of the U-Net: tools/bench_kernels.py --key 8).
-//
-// Workspace (floats): U[16][N][C], V[16][T][C], M[16][T][N], T = B*(H/2)*(W/2).
 #include "igemm.h"
 
 namespace pis {
@@ -709,7 +714,7 @@ __global__ __launch_bounds__(256) void wino4_wgrad_out_kernel(const float* __res
   }
 }
 
-// ---- the 16 batched GEMMs: C[z][m][n] = sum_k A[z][m][k] B[z][n][k] --------------------
+// ---- the batched GEMMs (16 or 36): C[z][m][n] = sum_k A[z][m][k] B[z][n][k] ------------
 // Both operands K-contiguous ("NT"), plain row-major C, no epilogue: a lean kernel for the
 // Winograd contractions. Block tile BM x BN (4 waves, 2 x 2, each (BM/2) x (BN/2) as 32x32 MFMA
 // tiles), K-step 16 through a register-staged LDS double buffer; LDS rows padded to 20 floats
