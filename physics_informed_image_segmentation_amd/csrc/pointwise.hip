@@ -32,17 +32,19 @@ __global__ void maxpool_fwd_kernel(const float* __restrict__ x, int ldx, float* 
 
 // dx = (dskip + route(dy)) * (x > 0); route = first max in (0,0),(0,1),(1,0),(1,1)
 // order, the tie-break of ATen's max_pool2d_with_indices.
+// I: index type of the element loop (int when the item count fits: 32-bit divisions are a few
+// instructions, 64-bit ones a software routine per item)
+template <typename I>
 __global__ void maxpool_bwd_kernel(const float* __restrict__ x, int ldx, const float* __restrict__ dy,
                                    const float* __restrict__ dskip, int ldskip,
                                    float* __restrict__ dx, int lddx, int B, int Ho, int Wo, int C) {
   const int c4n = C / 4;
-  const int64_t n = (int64_t)B * Ho * Wo * c4n;
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n;
-       e += (int64_t)gridDim.x * blockDim.x) {
+  const I n = (I)B * Ho * Wo * c4n;
+  for (I e = (I)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (I)gridDim.x * blockDim.x) {
     const int c4 = (int)(e % c4n);
-    const int64_t q = e / c4n;
+    const I q = e / c4n;
     const int wo = (int)(q % Wo);
-    const int64_t bh = q / Wo;
+    const I bh = q / Wo;
     const int ho = (int)(bh % Ho);
     const int b = (int)(bh / Ho);
     const int W = 2 * Wo;
@@ -222,8 +224,12 @@ extern "C" int pis_maxpool2x2_bwd(const float* x, int ldx, const float* dy, cons
                     (!dskip || ldskip % 4 == 0),
                 "pis_maxpool2x2_bwd: H, W even and C, ld multiples of 4 required");
   const int64_t work = (int64_t)B * (H / 2) * (W / 2) * (C / 4);
-  hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(grid_for(work)), dim3(256), 0, (hipStream_t)stream,
-                     x, ldx, dy, dskip, ldskip, dx, lddx, B, H / 2, W / 2, C);
+  if (work < (int64_t)1 << 30)
+    hipLaunchKernelGGL(maxpool_bwd_kernel<int>, dim3(grid_for(work)), dim3(256), 0, (hipStream_t)stream,
+                       x, ldx, dy, dskip, ldskip, dx, lddx, B, H / 2, W / 2, C);
+  else
+    hipLaunchKernelGGL(maxpool_bwd_kernel<int64_t>, dim3(grid_for(work)), dim3(256), 0, (hipStream_t)stream,
+                       x, ldx, dy, dskip, ldskip, dx, lddx, B, H / 2, W / 2, C);
   return launch_status("maxpool2x2_bwd");
 }
 

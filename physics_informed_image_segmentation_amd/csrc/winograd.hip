@@ -261,6 +261,23 @@ __device__ __forceinline__ void axpy_c(T& acc, float c, const T& v) {
   else acc += c * v;
 }
 
+// (tile, channel-quad) item e -> tile t, first channel c, image b, tile index within the image;
+// 32-bit divisions while e fits (a few instructions; 64-bit ones are a software routine)
+__device__ __forceinline__ void tile_decode(int64_t e, int c4n, int tpi, int64_t& t, int& c, int& b, int& rem) {
+  if (e <= 0x7fffffff) {
+    const unsigned eu = (unsigned)e, tu = eu / (unsigned)c4n;
+    c = (int)(eu - tu * (unsigned)c4n) * 4;
+    t = tu;
+    b = (int)(tu / (unsigned)tpi);
+    rem = (int)(tu - (unsigned)b * (unsigned)tpi);
+  } else {
+    t = e / c4n;
+    c = (int)(e - t * c4n) * 4;
+    b = (int)(t / tpi);
+    rem = (int)(t - (int64_t)b * tpi);
+  }
+}
+
 // U[xi][n][c] = (G g G^T)[xi], xi = 6 i + j
 // With Up != NULL the transform is written as the bf16x6 hi/mid/lo planes Up[p][xi][n][c] instead
 // (the fused GEMM + output-transform kernel reads its B fragments straight from them).
@@ -344,9 +361,9 @@ __global__ __launch_bounds__(256) void wino4_input_kernel(const float* __restric
   const int c4n = C / 4, TW = W / 4, TH = H / 4;
   const int64_t T = (int64_t)B * TH * TW, TC = T * C;
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < T * c4n; e += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t t = e / c4n;
-    const int c = (int)(e - t * c4n) * 4;
-    const int b = (int)(t / (TH * TW)), rem = (int)(t - (int64_t)b * TH * TW);
+    int64_t t;
+    int c, b, rem;
+    tile_decode(e, c4n, TH * TW, t, c, b, rem);
     const int ty = rem / TW, tx = rem - ty * TW;
     wino4_input_item(x, ldx, H, W, C, V, TC, t, b, ty, tx, c);
   }
@@ -357,9 +374,9 @@ __global__ __launch_bounds__(256) void wino4_output_kernel(const float* __restri
   const int N = g.N, n4n = N / 4, TW = g.W / 4, TH = g.H / 4;
   const int64_t T = (int64_t)B * TH * TW, TN = T * N;
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < T * n4n; e += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t t = e / n4n;
-    const int n = (int)(e - t * n4n) * 4;
-    const int b = (int)(t / (TH * TW)), rem = (int)(t - (int64_t)b * TH * TW);
+    int64_t t;
+    int n, b, rem;
+    tile_decode(e, n4n, TH * TW, t, n, b, rem);
     const int ty = rem / TW, tx = rem - ty * TW;
     f32x4 y[4][4];
 #pragma unroll
@@ -641,9 +658,9 @@ __global__ __launch_bounds__(256) void wino4_dz_kernel(const float* __restrict__
   const int64_t T = (int64_t)B * TH * TW, TN = T * N;
   f32x4 bsum = {0.f, 0.f, 0.f, 0.f};
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < T * n4n; e += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t t = e / n4n;
-    const int n = (int)(e - t * n4n) * 4;
-    const int b = (int)(t / (TH * TW)), rem = (int)(t - (int64_t)b * TH * TW);
+    int64_t t;
+    int n, b, rem;
+    tile_decode(e, n4n, TH * TW, t, n, b, rem);
     const int ty = rem / TW, tx = rem - ty * TW;
     wino4_dz_item(dz, ldz, H, W, N, E, TN, t, b, ty, tx, n, bsum);
   }
@@ -661,9 +678,9 @@ __global__ __launch_bounds__(256) void wino4_dz2_kernel(const float* __restrict_
   const int64_t T = (int64_t)B * TH * TW, TN = T * N;
   f32x4 bsum = {0.f, 0.f, 0.f, 0.f};
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < T * n4n; e += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t t = e / n4n;
-    const int n = (int)(e - t * n4n) * 4;
-    const int b = (int)(t / (TH * TW)), rem = (int)(t - (int64_t)b * TH * TW);
+    int64_t t;
+    int n, b, rem;
+    tile_decode(e, n4n, TH * TW, t, n, b, rem);
     const int ty = rem / TW, tx = rem - ty * TW;
     wino4_input_item(dz, ldz, H, W, N, V, TN, t, b, ty, tx, n);
     wino4_dz_item(dz, ldz, H, W, N, E, TN, t, b, ty, tx, n, bsum);
