@@ -45,6 +45,8 @@ typedef void* pis_stream_t; /* hipStream_t */
 #define PIS_ACCUMULATE 8 /* dst += result instead of dst = result             */
 #define PIS_WINO_PREPARED 16 /* conv3x3 dgrad_ex / wgrad_keep: pis_conv3x3_bwd_prep already wrote this
                                 layer's dz transforms into the call's workspace          */
+#define PIS_W_UNFLIPPED 32   /* conv3x3 dgrad_ex with PIS_WINO_PREPARED: w_flip is the layer's ORIGINAL
+                                KRSC weight (the F(4x4) filter transform rotates it in place) */
 
 const char* pis_last_error(void);
 int pis_version(void);

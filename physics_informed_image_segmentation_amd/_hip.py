@@ -16,7 +16,7 @@ import torch
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "_lib", "libpis.so")
 
-PIS_RELU, PIS_SCALE, PIS_MASK, PIS_ACCUMULATE, PIS_WINO_PREPARED = 1, 2, 4, 8, 16
+PIS_RELU, PIS_SCALE, PIS_MASK, PIS_ACCUMULATE, PIS_WINO_PREPARED, PIS_W_UNFLIPPED = 1, 2, 4, 8, 16, 32
 PIS_LOSS_ALL_TERMS, PIS_LOSS_CHAIN_SIGMOID, PIS_LOSS_NO_REACTION = 1, 2, 4
 LOSS_NTERMS = 8
 TERM_TOTAL, TERM_DICE, TERM_BCE, TERM_RD, TERM_PF, TERM_I, TERM_P, TERM_T = range(8)

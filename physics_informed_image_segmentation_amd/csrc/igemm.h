@@ -31,6 +31,7 @@ struct IGemmArgs {
   int flags;
   int cout_t;          // EPI_SCATTER2: n = (i*2+j)*cout_t + o
   float* pool;         // F(4x4,3x3) forward only: also write the 2x2 max pool of dst here ([B][H/2][W/2][N])
+  int w_unflipped;     // F(4x4,3x3) input gradient: wt holds the original KRSC weights (no flipped copy)
   // batched launches (gridDim.y > 1): per-batch element offsets
   int64_t bs_src, bs_wt, bs_dst;
 };

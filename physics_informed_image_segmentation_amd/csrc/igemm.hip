@@ -712,6 +712,9 @@ extern "C" int pis_conv3x3_dgrad_ex(const float* dz, int ldz, const float* w_fli
   a.Csrc = Cout; a.ntaps = 9; a.tap_mode = TAP_CONV3; a.wt = w_flip; a.ldw = 9 * Cout; a.N = Cin;
   a.epi = EPI_NHWC; a.mask = mask; a.ldm = ldm; a.scale = scale; a.dst = dx; a.ldd = lddx;
   a.flags = flags & (PIS_MASK | PIS_SCALE | PIS_ACCUMULATE);
+  a.w_unflipped = (flags & PIS_W_UNFLIPPED) != 0;
+  PIS_CHECK_ARG(!a.w_unflipped || (flags & PIS_WINO_PREPARED),
+                "pis_conv3x3_dgrad_ex: PIS_W_UNFLIPPED needs the prepared F(4x4,3x3) path");
   return dispatch_conv3x3(a, B, ws, ws_bytes, (hipStream_t)stream, nullptr, (flags & PIS_WINO_PREPARED) != 0);
 }
 

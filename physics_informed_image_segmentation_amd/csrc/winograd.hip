@@ -281,15 +281,23 @@ __device__ __forceinline__ void tile_decode(int64_t e, int c4n, int tpi, int64_t
 // U[xi][n][c] = (G g G^T)[xi], xi = 6 i + j
 // With Up != NULL the transform is written as the bf16x6 hi/mid/lo planes Up[p][xi][n][c] instead
 // (the fused GEMM + output-transform kernel reads its B fragments straight from them).
+// unflipped: w holds the layer's ORIGINAL KRSC weights [C][9][N] and this is its input gradient
+// (N = Cin, C = Cout): g = the 180-degree-rotated, transposed filter read in place (no
+// pis_conv3x3_flip copy)
 __global__ __launch_bounds__(256) void wino4_filter_kernel(const float* __restrict__ w, int ldw, int N, int C,
                                                            float* __restrict__ U, int transposed = 0,
-                                                           __bf16* __restrict__ Up = nullptr) {
+                                                           __bf16* __restrict__ Up = nullptr, int unflipped = 0) {
   const int64_t NC = (int64_t)N * C;
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < NC; e += (int64_t)gridDim.x * blockDim.x) {
     const int n = (int)(e / C), c = (int)(e - (int64_t)n * C);
     float g[3][3];
+    if (unflipped) {
 #pragma unroll
-    for (int t = 0; t < 9; ++t) g[t / 3][t % 3] = w[(size_t)n * ldw + t * C + c];
+      for (int t = 0; t < 9; ++t) g[t / 3][t % 3] = w[((size_t)c * 9 + 8 - t) * N + n];
+    } else {
+#pragma unroll
+      for (int t = 0; t < 9; ++t) g[t / 3][t % 3] = w[(size_t)n * ldw + t * C + c];
+    }
     float gg[6][3];  // G g
 #pragma unroll
     for (int i = 0; i < 6; ++i)
@@ -1330,7 +1338,8 @@ int launch_wino3x3(const IGemmArgs& a, int B, void* ws, hipStream_t s, float* ke
   if (keep_v && m == 4) V = keep_v;
   const double flop = 2.0 * nxi * (double)T * N * C;
   if (m == 4 && !keep_v && wino_fused_wanted(a.H, a.W, C, N)) {
-    hipLaunchKernelGGL(wino4_filter_kernel, dim3(grid_of((int64_t)N * C)), dim3(256), 0, s, a.wt, a.ldw, N, C, U, 1);
+    hipLaunchKernelGGL(wino4_filter_kernel, dim3(grid_of((int64_t)N * C)), dim3(256), 0, s, a.wt, a.ldw, N, C, U, 1,
+                       nullptr, a.w_unflipped);
     int rc = launch_status("wino_filter");
     if (rc) return rc;
     const int blocks = B * (a.H / (4 * WF_TR)) * (a.W / (4 * WF_TC)) * (N / WF_NB);
@@ -1343,7 +1352,7 @@ int launch_wino3x3(const IGemmArgs& a, int B, void* ws, hipStream_t s, float* ke
     // the pre-split filter planes (1.5x U's bytes) go where M would have been
     __bf16* Up = reinterpret_cast<__bf16*>(Mt);
     hipLaunchKernelGGL(wino4_filter_kernel, dim3(grid_of((int64_t)N * C)), dim3(256), 0, s, a.wt, a.ldw, N, C, U, 0,
-                       Up);
+                       Up, a.w_unflipped);
     if (!v_ready)
       hipLaunchKernelGGL(wino4_input_kernel, dim3(grid_of(T * (C / 4))), dim3(256), 0, s, a.src, a.lds, B, a.H, a.W,
                          C, V);
@@ -1355,8 +1364,10 @@ int launch_wino3x3(const IGemmArgs& a, int B, void* ws, hipStream_t s, float* ke
     return rc;
   }
   if (v_ready && m != 4) return set_error("launch_wino3x3: prepared transforms need F(4x4,3x3)"), PIS_ERR_ARG;
+  if (a.w_unflipped && m != 4) return set_error("launch_wino3x3: unflipped weights need F(4x4,3x3)"), PIS_ERR_ARG;
   if (m == 4) {
-    hipLaunchKernelGGL(wino4_filter_kernel, dim3(grid_of((int64_t)N * C)), dim3(256), 0, s, a.wt, a.ldw, N, C, U, 0);
+    hipLaunchKernelGGL(wino4_filter_kernel, dim3(grid_of((int64_t)N * C)), dim3(256), 0, s, a.wt, a.ldw, N, C, U, 0,
+                       nullptr, a.w_unflipped);
     if (!v_ready)
       hipLaunchKernelGGL(wino4_input_kernel, dim3(grid_of(T * (C / 4))), dim3(256), 0, s, a.src, a.lds, B, a.H, a.W,
                          C, V);

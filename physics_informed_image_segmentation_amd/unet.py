@@ -28,7 +28,7 @@ import torch
 import torch.nn as nn
 
 from . import _hip
-from ._hip import PIS_ACCUMULATE, PIS_MASK, PIS_RELU, PIS_SCALE, PIS_WINO_PREPARED, call, ptr
+from ._hip import PIS_ACCUMULATE, PIS_MASK, PIS_RELU, PIS_SCALE, PIS_W_UNFLIPPED, PIS_WINO_PREPARED, call, ptr
 
 # block name -> dropout multiplier of UNet(dropout=d), src/unet.py:120-154
 _DROP_MULT = {"enc1": 0.0, "enc2": 0.5, "enc3": 1.0, "enc4": 1.0, "bottleneck": 1.0,
@@ -572,17 +572,17 @@ class UNetEngine:
             with torch.cuda.stream(side):  # DDP buckets all-reduce after their weight gradients
                 self._ready(*params)
 
-        # dgrad operands, rebuilt from the current weights
+        # dgrad operands, rebuilt from the current weights. A 3x3 layer whose input gradient runs
+        # on the prepared F(4x4,3x3) path reads its original weights (the filter transform rotates
+        # them); the others get a flipped copy right before their dgrad.
         flips = {}
-        for name in BLOCK_ORDER:
-            blk = m.block(name)
-            for conv in (blk.conv0, blk.conv1):
-                if conv.in_channels == 1 and conv is m.enc1.conv0:
-                    continue
-                t = gb(f"flip_{id(conv)}", conv.weight.numel())
-                call("pis_conv3x3_flip", conv.weight.data_ptr(), t.data_ptr(), conv.in_channels,
-                     conv.out_channels, st)
-                flips[id(conv)] = t
+
+        def flipped(conv):
+            t = gb(f"flip_{id(conv)}", conv.weight.numel())
+            call("pis_conv3x3_flip", conv.weight.data_ptr(), t.data_ptr(), conv.in_channels,
+                 conv.out_channels, st)
+            return t
+
         for l in (1, 2, 3, 4):
             up = getattr(m, f"up{l}")
             t = gb(f"prep_up{l}", up.weight.numel())
@@ -619,10 +619,13 @@ class UNetEngine:
             ready_on_side(conv.weight, conv.bias)
             if dx is not None:
                 flags = (PIS_MASK if mask is not None else 0) | (PIS_SCALE if scale is not None else 0)
-                call("pis_conv3x3_dgrad_ex", dz.p, dz.ld, flips[id(conv)].data_ptr(),
+                if prep:
+                    wf, flags = conv.weight.data_ptr(), flags | PIS_WINO_PREPARED | PIS_W_UNFLIPPED
+                else:
+                    wf = flipped(conv).data_ptr()
+                call("pis_conv3x3_dgrad_ex", dz.p, dz.ld, wf,
                      mask.p if mask is not None else 0, mask.ld if mask is not None else 0, ptr(scale),
-                     dx.p, dx.ld, B, Hl, Wl, conv.in_channels, conv.out_channels,
-                     flags | (PIS_WINO_PREPARED if prep else 0), ws, wsb, st)
+                     dx.p, dx.ld, B, Hl, Wl, conv.in_channels, conv.out_channels, flags, ws, wsb, st)
 
         # head: sigmoid backward + 1x1 conv + ReLU backward of dec1.conv1
         d1 = _Buf(bf["d1_1"], c)

@@ -635,7 +635,7 @@ def test_conv3x3_bwd_prep(hip, B, H, W, Cin, Cout):
     """pis_conv3x3_bwd_prep: one pass over dz writes both backward transforms; the dgrad_ex and
     wgrad_keep calls that then pass PIS_WINO_PREPARED give the same results as without it (and
     as the float64 reference), bias gradient included."""
-    PREP = 16
+    PREP, UNFLIPPED = 16, 32
     g = torch.Generator().manual_seed(23)
     x = F.relu(torch.randn(B, Cin, H, W, generator=g))
     w = torch.randn(Cout, Cin, 3, 3, generator=g) / (3 * Cin ** 0.5)
@@ -653,27 +653,34 @@ def test_conv3x3_bwd_prep(hip, B, H, W, Cin, Cout):
     assert hip.pis_conv3x3_flip(wd.data_ptr(), wf.data_ptr(), Cin, Cout, s()) == 0
     nwg = hip.pis_conv3x3_wgrad_ws(B, H, W, Cin, Cout)
     out = {}
-    for prep in (False, True):
+    for prep in (False, True, "unflipped"):
         wsg = torch.full((nwg // 4 + 1,), float("nan"), device="cuda")
         wsd = torch.full((nws // 4 + 1,), float("nan"), device="cuda")
-        flag = 0
+        flag, wdg = 0, wf
         if prep:
             rc = hip.pis_conv3x3_bwd_prep(dzd.data_ptr(), Cout, B, H, W, Cin, Cout, wsd.data_ptr(), nws,
                                           wsg.data_ptr(), nwg, s())
             assert rc == 1, hip.pis_last_error()
             flag = PREP
+        if prep == "unflipped":  # the dgrad reads the original weights and rotates them itself
+            wdg = wd
         dw = torch.empty(Cout, 3, 3, Cin, device="cuda")
         db = torch.empty(Cout, device="cuda")
         assert hip.pis_conv3x3_wgrad_keep(xd.data_ptr(), Cin, dzd.data_ptr(), Cout, dw.data_ptr(), db.data_ptr(), B,
                                           H, W, Cin, Cout, flag, wsg.data_ptr(), nwg, keep.data_ptr(), s()) == 0
         dx = torch.empty(B, H, W, Cin, device="cuda")
-        assert hip.pis_conv3x3_dgrad_ex(dzd.data_ptr(), Cout, wf.data_ptr(), mask.data_ptr(), Cin, 0, dx.data_ptr(),
-                                        Cin, B, H, W, Cin, Cout, MASK | flag, wsd.data_ptr(), nws, s()) == 0, \
+        dflag = MASK | flag | (UNFLIPPED if prep == "unflipped" else 0)
+        assert hip.pis_conv3x3_dgrad_ex(dzd.data_ptr(), Cout, wdg.data_ptr(), mask.data_ptr(), Cin, 0, dx.data_ptr(),
+                                        Cin, B, H, W, Cin, Cout, dflag, wsd.data_ptr(), nws, s()) == 0, \
             hip.pis_last_error()
         torch.cuda.synchronize()
         out[prep] = (dw.cpu(), db.cpu(), dx.cpu())
-    for a, b in zip(out[False], out[True]):
-        assert torch.equal(a, b)  # the same arithmetic, only one read of dz fewer
+    for variant in (True, "unflipped"):
+        for a, b in zip(out[False], out[variant]):
+            assert torch.equal(a, b)  # the same arithmetic, only one read of dz (or one weight flip) fewer
+    # unflipped weights are only understood on the prepared F(4x4) path
+    assert hip.pis_conv3x3_dgrad_ex(dzd.data_ptr(), Cout, wd.data_ptr(), 0, 0, 0, dx.data_ptr(), Cin, B, H, W,
+                                    Cin, Cout, UNFLIPPED, wsd.data_ptr(), nws, s()) != 0
     dw_ref = torch.nn.grad.conv2d_weight(x.double(), w.shape, dz.double(), padding=1)
     dx_ref = torch.nn.grad.conv2d_input(x.shape, w.double(), dz.double(), padding=1) * (x > 0)
     assert rel_err(out[True][0].permute(0, 3, 1, 2), dw_ref) < 1e-5
