@@ -959,6 +959,7 @@ extern "C" int pis_conv3x3_bwd_prep(const float* dz, int ldz, int B, int H, int 
   PIS_CHECK_ARG(dz && B > 0 && H > 0 && W > 0 && Cin > 0 && Cout > 0, "pis_conv3x3_bwd_prep: bad arguments");
   const WinoWgradPlan wp = wino_wgrad_plan(B, H, W, Cin, Cout);
   if (tune_get(PIS_TUNE_WINO_DZ2) == 0 || !ws_dgrad || !ws_wgrad || !(wp.use && wp.m == 4) ||
+      Cin % 64 || Cout % 64 ||  // pis_conv3x3_wgrad_keep's channel contract
       ws_wgrad_bytes < wp.total || ldz % 4 || !dgrad_wino4_planned(B, H, W, Cin, Cout, ldz, ws_dgrad_bytes))
     return 0;  // not applicable: the two calls transform dz themselves
   float* V = wino_v_slot(ws_dgrad, Cout, Cin);

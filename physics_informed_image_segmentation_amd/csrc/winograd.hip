@@ -278,55 +278,86 @@ __device__ __forceinline__ void tile_decode(int64_t e, int c4n, int tpi, int64_t
   }
 }
 
-// U[xi][n][c] = (G g G^T)[xi], xi = 6 i + j
+// U[xi][n][c] = (G g G^T)[xi], xi = 6 i + j, for the filter g of pair e = n C + c
 // With Up != NULL the transform is written as the bf16x6 hi/mid/lo planes Up[p][xi][n][c] instead
 // (the fused GEMM + output-transform kernel reads its B fragments straight from them).
-// unflipped: w holds the layer's ORIGINAL KRSC weights [C][9][N] and this is its input gradient
-// (N = Cin, C = Cout): g = the 180-degree-rotated, transposed filter read in place (no
-// pis_conv3x3_flip copy)
+__device__ __forceinline__ void wino4_filter_item(const float (&g)[3][3], int64_t e, int n, int c, int N,
+                                                  int64_t NC, float* __restrict__ U, int transposed,
+                                                  __bf16* __restrict__ Up) {
+  float gg[6][3];  // G g
+#pragma unroll
+  for (int i = 0; i < 6; ++i)
+#pragma unroll
+    for (int s = 0; s < 3; ++s) {
+      gg[i][s] = 0.f;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) axpy_c(gg[i][s], w4_g(i, k), g[k][s]);
+    }
+#pragma unroll
+  for (int i = 0; i < 6; ++i)
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+      float u = 0.f;
+#pragma unroll
+      for (int s = 0; s < 3; ++s) axpy_c(u, w4_g(j, s), gg[i][s]);
+      if (Up) {
+        const __bf16 h = (__bf16)u;
+        const float r = u - (float)h;
+        const __bf16 m = (__bf16)r;
+        const size_t o = (size_t)(i * 6 + j) * NC + e;
+        Up[o] = h;
+        Up[36 * NC + o] = m;
+        Up[72 * NC + o] = (__bf16)(r - (float)m);
+        continue;
+      }
+      // [xi][n][c] for the batched GEMMs; [xi][c][n] for the fused kernel's B operand
+      U[(size_t)(i * 6 + j) * NC + (transposed ? (int64_t)c * N + n : e)] = u;
+    }
+}
+
+// w: KRSC weights [N][9][C] (row pitch ldw), already in the operand's orientation (the forward's
+// own weights, or pis_conv3x3_flip's copy for an input gradient).
 __global__ __launch_bounds__(256) void wino4_filter_kernel(const float* __restrict__ w, int ldw, int N, int C,
                                                            float* __restrict__ U, int transposed = 0,
-                                                           __bf16* __restrict__ Up = nullptr, int unflipped = 0) {
+                                                           __bf16* __restrict__ Up = nullptr) {
   const int64_t NC = (int64_t)N * C;
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < NC; e += (int64_t)gridDim.x * blockDim.x) {
     const int n = (int)(e / C), c = (int)(e - (int64_t)n * C);
     float g[3][3];
-    if (unflipped) {
 #pragma unroll
-      for (int t = 0; t < 9; ++t) g[t / 3][t % 3] = w[((size_t)c * 9 + 8 - t) * N + n];
-    } else {
+    for (int t = 0; t < 9; ++t) g[t / 3][t % 3] = w[(size_t)n * ldw + t * C + c];
+    wino4_filter_item(g, e, n, c, N, NC, U, transposed, Up);
+  }
+}
+
+// The input-gradient filter transform straight from the layer's ORIGINAL KRSC weights [C][9][N]
+// (N = Cin, C = Cout; PIS_W_UNFLIPPED): g = the 180-degree-rotated, transposed filter, read in
+// place instead of from a pis_conv3x3_flip copy. N % 32 == 0, C % 32 == 0; a block owns
+// 32 n x 32 c; the 9 taps of that tile are read along n (128-B runs of the original [C][9][N]
+// weights) into LDS and each thread then transforms (n, c) pairs with c fastest, so the 36
+// output planes are written in runs along c as by wino4_filter_kernel.
+__global__ __launch_bounds__(256) void wino4_filter_rot_kernel(const float* __restrict__ w, int N, int C,
+                                                               float* __restrict__ U, int transposed,
+                                                               __bf16* __restrict__ Up) {
+  __shared__ float sg[9][32][33];  // [tap][c][n], padded: the transform reads along c conflict-free
+  const int nb = N / 32, n0 = 32 * (blockIdx.x % nb), c0 = 32 * (blockIdx.x / nb);
+  const int tid = threadIdx.x, lx = tid & 31, ly = tid >> 5;
 #pragma unroll
-      for (int t = 0; t < 9; ++t) g[t / 3][t % 3] = w[(size_t)n * ldw + t * C + c];
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c = ly + 8 * i;
+      sg[t][c][lx] = w[((size_t)(c0 + c) * 9 + t) * N + n0 + lx];
     }
-    float gg[6][3];  // G g
+  __syncthreads();
+  const int64_t NC = (int64_t)N * C;
+#pragma unroll 1
+  for (int i = 0; i < 4; ++i) {
+    const int c = lx, nl = ly + 8 * i, n = n0 + nl;
+    float g[3][3];
 #pragma unroll
-    for (int i = 0; i < 6; ++i)
-#pragma unroll
-      for (int s = 0; s < 3; ++s) {
-        gg[i][s] = 0.f;
-#pragma unroll
-        for (int k = 0; k < 3; ++k) axpy_c(gg[i][s], w4_g(i, k), g[k][s]);
-      }
-#pragma unroll
-    for (int i = 0; i < 6; ++i)
-#pragma unroll
-      for (int j = 0; j < 6; ++j) {
-        float u = 0.f;
-#pragma unroll
-        for (int s = 0; s < 3; ++s) axpy_c(u, w4_g(j, s), gg[i][s]);
-        if (Up) {
-          const __bf16 h = (__bf16)u;
-          const float r = u - (float)h;
-          const __bf16 m = (__bf16)r;
-          const size_t o = (size_t)(i * 6 + j) * NC + e;
-          Up[o] = h;
-          Up[36 * NC + o] = m;
-          Up[72 * NC + o] = (__bf16)(r - (float)m);
-          continue;
-        }
-        // [xi][n][c] for the batched GEMMs; [xi][c][n] for the fused kernel's B operand
-        U[(size_t)(i * 6 + j) * NC + (transposed ? (int64_t)c * N + n : e)] = u;
-      }
+    for (int t = 0; t < 9; ++t) g[t / 3][t % 3] = sg[8 - t][c][nl];
+    wino4_filter_item(g, (int64_t)n * C + c0 + c, n, c0 + c, N, NC, U, transposed, Up);
   }
 }
 
@@ -1281,6 +1312,19 @@ __global__ __launch_bounds__(64 * NWN * NWT) void wino4_gemm_out_x6_kernel(const
   }
 }
 
+static int grid_of(int64_t work) { return (int)std::max<int64_t>(1, std::min<int64_t>(cdiv(work, 256), 16384)); }
+
+// the F(4x4,3x3) filter transform of a's weights (the tiled kernel for unflipped 32-aligned shapes)
+static void launch_wino4_filter(const IGemmArgs& a, int N, int C, float* U, int transposed, __bf16* Up,
+                                hipStream_t s) {
+  if (a.w_unflipped)  // N, C % 32 == 0 checked by launch_wino3x3
+    hipLaunchKernelGGL(wino4_filter_rot_kernel, dim3((N / 32) * (C / 32)), dim3(256), 0, s, a.wt, N, C, U,
+                       transposed, Up);
+  else
+    hipLaunchKernelGGL(wino4_filter_kernel, dim3(grid_of((int64_t)N * C)), dim3(256), 0, s, a.wt, a.ldw, N, C, U,
+                       transposed, Up);
+}
+
 // fused path eligibility (pis_tune key 15): F(4x4), bf16x6 GEMMs, 64 -> 64 channels. Measured
 // (tools/bench_kernels.py --key 15, C2): enc1.conv1 forward 1.13 -> 0.98 ms, input gradient
 // 1.30 -> 1.13 ms; with 128 input or output channels (dec1.conv0, enc2.conv0) it is 2-8 % slower
@@ -1298,7 +1342,6 @@ static int launch_wino_gemm_out(const float* V, const __bf16* Up, const IGemmArg
   return launch_status("wino_gemm_out");
 }
 
-static int grid_of(int64_t work) { return (int)std::max<int64_t>(1, std::min<int64_t>(cdiv(work, 256), 16384)); }
 
 // F(4x4,3x3) when the 4x4 tile grid fits and pis_tune key 11 allows it, else F(2x2,3x3)
 int wino_tile(int H, int W) { return (tune_get(PIS_TUNE_WINO_F4) != 0 && H % 4 == 0 && W % 4 == 0) ? 4 : 2; }
@@ -1338,8 +1381,7 @@ int launch_wino3x3(const IGemmArgs& a, int B, void* ws, hipStream_t s, float* ke
   if (keep_v && m == 4) V = keep_v;
   const double flop = 2.0 * nxi * (double)T * N * C;
   if (m == 4 && !keep_v && wino_fused_wanted(a.H, a.W, C, N)) {
-    hipLaunchKernelGGL(wino4_filter_kernel, dim3(grid_of((int64_t)N * C)), dim3(256), 0, s, a.wt, a.ldw, N, C, U, 1,
-                       nullptr, a.w_unflipped);
+    launch_wino4_filter(a, N, C, U, 1, nullptr, s);
     int rc = launch_status("wino_filter");
     if (rc) return rc;
     const int blocks = B * (a.H / (4 * WF_TR)) * (a.W / (4 * WF_TC)) * (N / WF_NB);
@@ -1351,8 +1393,7 @@ int launch_wino3x3(const IGemmArgs& a, int B, void* ws, hipStream_t s, float* ke
   if (wino_gemm_out_wanted(m, T, C, N)) {
     // the pre-split filter planes (1.5x U's bytes) go where M would have been
     __bf16* Up = reinterpret_cast<__bf16*>(Mt);
-    hipLaunchKernelGGL(wino4_filter_kernel, dim3(grid_of((int64_t)N * C)), dim3(256), 0, s, a.wt, a.ldw, N, C, U, 0,
-                       Up, a.w_unflipped);
+    launch_wino4_filter(a, N, C, U, 0, Up, s);
     if (!v_ready)
       hipLaunchKernelGGL(wino4_input_kernel, dim3(grid_of(T * (C / 4))), dim3(256), 0, s, a.src, a.lds, B, a.H, a.W,
                          C, V);
@@ -1364,10 +1405,10 @@ int launch_wino3x3(const IGemmArgs& a, int B, void* ws, hipStream_t s, float* ke
     return rc;
   }
   if (v_ready && m != 4) return set_error("launch_wino3x3: prepared transforms need F(4x4,3x3)"), PIS_ERR_ARG;
-  if (a.w_unflipped && m != 4) return set_error("launch_wino3x3: unflipped weights need F(4x4,3x3)"), PIS_ERR_ARG;
+  if (a.w_unflipped && (m != 4 || N % 32 || C % 32))
+    return set_error("launch_wino3x3: unflipped weights need F(4x4,3x3) and 32-aligned channels"), PIS_ERR_ARG;
   if (m == 4) {
-    hipLaunchKernelGGL(wino4_filter_kernel, dim3(grid_of((int64_t)N * C)), dim3(256), 0, s, a.wt, a.ldw, N, C, U, 0,
-                       nullptr, a.w_unflipped);
+    launch_wino4_filter(a, N, C, U, 0, nullptr, s);
     if (!v_ready)
       hipLaunchKernelGGL(wino4_input_kernel, dim3(grid_of(T * (C / 4))), dim3(256), 0, s, a.src, a.lds, B, a.H, a.W,
                          C, V);

@@ -634,7 +634,9 @@ def test_convt_bf16x6_is_fp32_accurate(hip, Cin, Cout):
 def test_conv3x3_bwd_prep(hip, B, H, W, Cin, Cout):
     """pis_conv3x3_bwd_prep: one pass over dz writes both backward transforms; the dgrad_ex and
     wgrad_keep calls that then pass PIS_WINO_PREPARED give the same results as without it (and
-    as the float64 reference), bias gradient included."""
+    as the float64 reference), bias gradient included. With PIS_W_UNFLIPPED the input gradient
+    reads the original weights (the rotating filter transform) and matches the flipped-copy path
+    bit for bit."""
     PREP, UNFLIPPED = 16, 32
     g = torch.Generator().manual_seed(23)
     x = F.relu(torch.randn(B, Cin, H, W, generator=g))
@@ -694,6 +696,10 @@ def test_conv3x3_bwd_prep_not_applicable(hip):
     dz = torch.zeros(B, H, W, Cout, device="cuda")
     ws = torch.empty(1 << 20, device="cuda")
     assert hip.pis_conv3x3_bwd_prep(dz.data_ptr(), Cout, B, H, W, Cin, Cout, ws.data_ptr(), 4 << 20,
+                                    ws.data_ptr(), 4 << 20, s()) == 0
+    # nor channel counts the weight-gradient call rejects (Cin % 64 != 0)
+    dz = torch.zeros(1, 16, 16, 128, device="cuda")
+    assert hip.pis_conv3x3_bwd_prep(dz.data_ptr(), 128, 1, 16, 16, 144, 128, ws.data_ptr(), 4 << 20,
                                     ws.data_ptr(), 4 << 20, s()) == 0
 
 
