@@ -91,29 +91,35 @@ __global__ __launch_bounds__(256) void wino_input_kernel(const float* __restrict
   }
 }
 
-// conv epilogue on 4 channels of one output pixel (v = conv + bias): ReLU, ReLU-backward
+template <int VW>
+using fvec = float __attribute__((ext_vector_type(VW)));  // VW consecutive NHWC channels
+
+// conv epilogue on VW channels of one output pixel (v = conv + bias): ReLU, ReLU-backward
 // mask, dropout keep-scale, accumulate — the direct kernels' epilogue (igemm.hip)
-__device__ __forceinline__ f32x4 conv_epilogue4(const IGemmArgs& g, size_t pix, int n, f32x4 v, f32x4 sc4) {
+template <int VW = 4>
+__device__ __forceinline__ fvec<VW> conv_epilogue4(const IGemmArgs& g, size_t pix, int n, fvec<VW> v,
+                                                   fvec<VW> sc4) {
   if (g.flags & PIS_RELU) {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) v[k] = fmaxf(v[k], 0.f);
+    for (int k = 0; k < VW; ++k) v[k] = fmaxf(v[k], 0.f);
   }
   if (g.flags & PIS_MASK) {
-    const f32x4 mk = *reinterpret_cast<const f32x4*>(g.mask + pix * g.ldm + n);
+    const fvec<VW> mk = *reinterpret_cast<const fvec<VW>*>(g.mask + pix * g.ldm + n);
 #pragma unroll
-    for (int k = 0; k < 4; ++k) v[k] = mk[k] > 0.f ? v[k] : 0.f;
+    for (int k = 0; k < VW; ++k) v[k] = mk[k] > 0.f ? v[k] : 0.f;
   }
   v *= sc4;
   float* dst = g.dst + pix * g.ldd + n;
-  if (g.flags & PIS_ACCUMULATE) v += *reinterpret_cast<const f32x4*>(dst);
-  *reinterpret_cast<f32x4*>(dst) = v;
+  if (g.flags & PIS_ACCUMULATE) v += *reinterpret_cast<const fvec<VW>*>(dst);
+  *reinterpret_cast<fvec<VW>*>(dst) = v;
   return v;
 }
 
-__device__ __forceinline__ f32x4 max4(f32x4 a, f32x4 b, f32x4 c, f32x4 d) {
-  f32x4 m;
+template <int VW = 4>
+__device__ __forceinline__ fvec<VW> max4(fvec<VW> a, fvec<VW> b, fvec<VW> c, fvec<VW> d) {
+  fvec<VW> m;
 #pragma unroll
-  for (int k = 0; k < 4; ++k) m[k] = fmaxf(fmaxf(a[k], b[k]), fmaxf(c[k], d[k]));
+  for (int k = 0; k < VW; ++k) m[k] = fmaxf(fmaxf(a[k], b[k]), fmaxf(c[k], d[k]));
   return m;
 }
 
@@ -263,16 +269,17 @@ __device__ __forceinline__ void axpy_c(T& acc, float c, const T& v) {
 
 // (tile, channel-quad) item e -> tile t, first channel c, image b, tile index within the image;
 // 32-bit divisions while e fits (a few instructions; 64-bit ones are a software routine)
+template <int VW = 4>
 __device__ __forceinline__ void tile_decode(int64_t e, int c4n, int tpi, int64_t& t, int& c, int& b, int& rem) {
   if (e <= 0x7fffffff) {
     const unsigned eu = (unsigned)e, tu = eu / (unsigned)c4n;
-    c = (int)(eu - tu * (unsigned)c4n) * 4;
+    c = (int)(eu - tu * (unsigned)c4n) * VW;
     t = tu;
     b = (int)(tu / (unsigned)tpi);
     rem = (int)(tu - (unsigned)b * (unsigned)tpi);
   } else {
     t = e / c4n;
-    c = (int)(e - t * c4n) * 4;
+    c = (int)(e - t * c4n) * VW;
     b = (int)(t / tpi);
     rem = (int)(t - (int64_t)b * tpi);
   }
@@ -362,28 +369,29 @@ __global__ __launch_bounds__(256) void wino4_filter_rot_kernel(const float* __re
 }
 
 // V[xi][t][c] = (BT d BT^T)[xi], d = the 6x6 input patch at rows 4ty-1.., cols 4tx-1.. (zero padded)
+template <int VW = 4>
 __device__ __forceinline__ void wino4_input_item(const float* __restrict__ x, int ldx, int H, int W, int C,
                                                  float* __restrict__ V, int64_t TC, int64_t t, int b, int ty,
                                                  int tx, int c) {
-  f32x4 v[6][6];
+  fvec<VW> v[6][6];
 #pragma unroll
   for (int i = 0; i < 6; ++i)
 #pragma unroll
-    for (int j = 0; j < 6; ++j) v[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < 6; ++j) v[i][j] = (fvec<VW>)0.f;
 #pragma unroll
   for (int k = 0; k < 6; ++k) {  // input row k: its row transform, then its share of every V row
     const int h = 4 * ty - 1 + k;
-    f32x4 d[6];
+    fvec<VW> d[6];
 #pragma unroll
     for (int l = 0; l < 6; ++l) {
       const int ww = 4 * tx - 1 + l;
-      d[l] = f32x4{0.f, 0.f, 0.f, 0.f};
+      d[l] = (fvec<VW>)0.f;
       if (h >= 0 && h < H && ww >= 0 && ww < W)
-        d[l] = *reinterpret_cast<const f32x4*>(x + (((size_t)b * H + h) * W + ww) * ldx + c);
+        d[l] = *reinterpret_cast<const fvec<VW>*>(x + (((size_t)b * H + h) * W + ww) * ldx + c);
     }
 #pragma unroll
     for (int j = 0; j < 6; ++j) {
-      f32x4 r = f32x4{0.f, 0.f, 0.f, 0.f};
+      fvec<VW> r = (fvec<VW>)0.f;
 #pragma unroll
       for (int l = 0; l < 6; ++l) axpy_c(r, w4_bt(j, l), d[l]);
 #pragma unroll
@@ -392,60 +400,64 @@ __device__ __forceinline__ void wino4_input_item(const float* __restrict__ x, in
   }
 #pragma unroll
   for (int xi = 0; xi < 36; ++xi)
-    *reinterpret_cast<f32x4*>(V + (size_t)xi * TC + t * C + c) = v[xi / 6][xi % 6];
+    *reinterpret_cast<fvec<VW>*>(V + (size_t)xi * TC + t * C + c) = v[xi / 6][xi % 6];
 }
 
+// VW channels per thread (pis_tune key 17): 2 (default) = half the registers of 4 (float4 accesses)
+template <int VW>
 __global__ __launch_bounds__(256) void wino4_input_kernel(const float* __restrict__ x, int ldx, int B, int H, int W,
                                                           int C, float* __restrict__ V) {
-  const int c4n = C / 4, TW = W / 4, TH = H / 4;
+  const int c4n = C / VW, TW = W / 4, TH = H / 4;
   const int64_t T = (int64_t)B * TH * TW, TC = T * C;
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < T * c4n; e += (int64_t)gridDim.x * blockDim.x) {
     int64_t t;
     int c, b, rem;
-    tile_decode(e, c4n, TH * TW, t, c, b, rem);
+    tile_decode<VW>(e, c4n, TH * TW, t, c, b, rem);
     const int ty = rem / TW, tx = rem - ty * TW;
-    wino4_input_item(x, ldx, H, W, C, V, TC, t, b, ty, tx, c);
+    wino4_input_item<VW>(x, ldx, H, W, C, V, TC, t, b, ty, tx, c);
   }
 }
 
-// Y = AT M AT^T per tile and 4 output channels, then the direct kernels' conv epilogue
+// Y = AT M AT^T per tile and VW output channels (pis_tune key 17), then the direct kernels' conv
+// epilogue
+template <int VW>
 __global__ __launch_bounds__(256) void wino4_output_kernel(const float* __restrict__ Mt, IGemmArgs g, int B) {
-  const int N = g.N, n4n = N / 4, TW = g.W / 4, TH = g.H / 4;
+  const int N = g.N, n4n = N / VW, TW = g.W / 4, TH = g.H / 4;
   const int64_t T = (int64_t)B * TH * TW, TN = T * N;
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < T * n4n; e += (int64_t)gridDim.x * blockDim.x) {
     int64_t t;
     int n, b, rem;
-    tile_decode(e, n4n, TH * TW, t, n, b, rem);
+    tile_decode<VW>(e, n4n, TH * TW, t, n, b, rem);
     const int ty = rem / TW, tx = rem - ty * TW;
-    f32x4 y[4][4];
+    fvec<VW> y[4][4];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) y[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < 4; ++j) y[i][j] = (fvec<VW>)0.f;
 #pragma unroll
     for (int k = 0; k < 6; ++k) {
-      f32x4 m[6];
+      fvec<VW> m[6];
 #pragma unroll
-      for (int l = 0; l < 6; ++l) m[l] = *reinterpret_cast<const f32x4*>(Mt + (size_t)(k * 6 + l) * TN + t * N + n);
+      for (int l = 0; l < 6; ++l) m[l] = *reinterpret_cast<const fvec<VW>*>(Mt + (size_t)(k * 6 + l) * TN + t * N + n);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        f32x4 r = f32x4{0.f, 0.f, 0.f, 0.f};
+        fvec<VW> r = (fvec<VW>)0.f;
 #pragma unroll
         for (int l = 0; l < 6; ++l) axpy_c(r, w4_at(j, l), m[l]);
 #pragma unroll
         for (int i = 0; i < 4; ++i) axpy_c(y[i][j], w4_at(i, k), r);
       }
     }
-    f32x4 bias4 = {0.f, 0.f, 0.f, 0.f}, sc4 = {1.f, 1.f, 1.f, 1.f};
-    if (g.bias) bias4 = *reinterpret_cast<const f32x4*>(g.bias + n);
-    if (g.flags & PIS_SCALE) sc4 = *reinterpret_cast<const f32x4*>(g.scale + (size_t)b * N + n);
-    f32x4 o[4][4];
+    fvec<VW> bias4 = (fvec<VW>)0.f, sc4 = (fvec<VW>)1.f;
+    if (g.bias) bias4 = *reinterpret_cast<const fvec<VW>*>(g.bias + n);
+    if (g.flags & PIS_SCALE) sc4 = *reinterpret_cast<const fvec<VW>*>(g.scale + (size_t)b * N + n);
+    fvec<VW> o[4][4];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const size_t pix = ((size_t)b * g.H + 4 * ty + i) * g.W + 4 * tx + j;
-        o[i][j] = conv_epilogue4(g, pix, n, y[i][j] + bias4, sc4);
+        o[i][j] = conv_epilogue4<VW>(g, pix, n, y[i][j] + bias4, sc4);
       }
     if (g.pool) {  // the tile's four 2x2 max-pool outputs (the encoder's MaxPool2d)
 #pragma unroll
@@ -453,8 +465,8 @@ __global__ __launch_bounds__(256) void wino4_output_kernel(const float* __restri
 #pragma unroll
         for (int qj = 0; qj < 2; ++qj) {
           const size_t pp = ((size_t)b * (g.H / 2) + 2 * ty + qi) * (g.W / 2) + 2 * tx + qj;
-          *reinterpret_cast<f32x4*>(g.pool + pp * N + n) =
-              max4(o[2 * qi][2 * qj], o[2 * qi][2 * qj + 1], o[2 * qi + 1][2 * qj], o[2 * qi + 1][2 * qj + 1]);
+          *reinterpret_cast<fvec<VW>*>(g.pool + pp * N + n) =
+              max4<VW>(o[2 * qi][2 * qj], o[2 * qi][2 * qj + 1], o[2 * qi + 1][2 * qj], o[2 * qi + 1][2 * qj + 1]);
         }
     }
   }
@@ -1314,6 +1326,24 @@ __global__ __launch_bounds__(64 * NWN * NWT) void wino4_gemm_out_x6_kernel(const
 
 static int grid_of(int64_t work) { return (int)std::max<int64_t>(1, std::min<int64_t>(cdiv(work, 256), 16384)); }
 
+// the F(4x4,3x3) output transform, 2 (default) or 4 channels per thread (pis_tune key 17;
+// tools/bench_kernels.py --key 17: 2 channels halve the registers, +2-11 % on the 512^2-256^2 layers)
+static void launch_wino4_output(const float* Mt, const IGemmArgs& a, int B, int64_t T, int N, hipStream_t s) {
+  if (tune_get(PIS_TUNE_WINO_VW) != 4)
+    hipLaunchKernelGGL(wino4_output_kernel<2>, dim3(grid_of(T * (N / 2))), dim3(256), 0, s, Mt, a, B);
+  else
+    hipLaunchKernelGGL(wino4_output_kernel<4>, dim3(grid_of(T * (N / 4))), dim3(256), 0, s, Mt, a, B);
+}
+
+// the F(4x4,3x3) input transform, 2 (default) or 4 channels per thread (pis_tune key 17)
+static void launch_wino4_input(int64_t T, int C, hipStream_t s, const float* x, int ldx, int B, int H, int W, int,
+                               float* V) {
+  if (tune_get(PIS_TUNE_WINO_VW) != 4)
+    hipLaunchKernelGGL(wino4_input_kernel<2>, dim3(grid_of(T * (C / 2))), dim3(256), 0, s, x, ldx, B, H, W, C, V);
+  else
+    hipLaunchKernelGGL(wino4_input_kernel<4>, dim3(grid_of(T * (C / 4))), dim3(256), 0, s, x, ldx, B, H, W, C, V);
+}
+
 // the F(4x4,3x3) filter transform of a's weights (the tiled kernel for unflipped 32-aligned shapes)
 static void launch_wino4_filter(const IGemmArgs& a, int N, int C, float* U, int transposed, __bf16* Up,
                                 hipStream_t s) {
@@ -1395,7 +1425,7 @@ int launch_wino3x3(const IGemmArgs& a, int B, void* ws, hipStream_t s, float* ke
     __bf16* Up = reinterpret_cast<__bf16*>(Mt);
     launch_wino4_filter(a, N, C, U, 0, Up, s);
     if (!v_ready)
-      hipLaunchKernelGGL(wino4_input_kernel, dim3(grid_of(T * (C / 4))), dim3(256), 0, s, a.src, a.lds, B, a.H, a.W,
+      launch_wino4_input(T, C, s, a.src, a.lds, B, a.H, a.W,
                          C, V);
     int rc = launch_status("wino_transforms");
     if (rc) return rc;
@@ -1410,7 +1440,7 @@ int launch_wino3x3(const IGemmArgs& a, int B, void* ws, hipStream_t s, float* ke
   if (m == 4) {
     launch_wino4_filter(a, N, C, U, 0, nullptr, s);
     if (!v_ready)
-      hipLaunchKernelGGL(wino4_input_kernel, dim3(grid_of(T * (C / 4))), dim3(256), 0, s, a.src, a.lds, B, a.H, a.W,
+      launch_wino4_input(T, C, s, a.src, a.lds, B, a.H, a.W,
                          C, V);
   } else {
     hipLaunchKernelGGL(wino_filter_kernel, dim3(grid_of((int64_t)N * C)), dim3(256), 0, s, a.wt, a.ldw, N, C, U);
@@ -1466,7 +1496,7 @@ int launch_wino3x3(const IGemmArgs& a, int B, void* ws, hipStream_t s, float* ke
   launch_hook("wino_gemm", 1, s, flop);
   if (rc) return rc;
   if (m == 4)
-    hipLaunchKernelGGL(wino4_output_kernel, dim3(grid_of(T * (N / 4))), dim3(256), 0, s, Mt, a, B);
+    launch_wino4_output(Mt, a, B, T, N, s);
   else
     hipLaunchKernelGGL(wino_output_kernel, dim3(grid_of(T * (N / 4))), dim3(256), 0, s, Mt, a, B);
   return launch_status("wino_output");
@@ -1475,7 +1505,7 @@ int launch_wino3x3(const IGemmArgs& a, int B, void* ws, hipStream_t s, float* ke
 int launch_wino_input(const float* x, int ldx, int B, int H, int W, int C, float* V, hipStream_t s, int m) {
   const int64_t T = (int64_t)B * (H / m) * (W / m);
   if (m == 4)
-    hipLaunchKernelGGL(wino4_input_kernel, dim3(grid_of(T * (C / 4))), dim3(256), 0, s, x, ldx, B, H, W, C, V);
+    launch_wino4_input(T, C, s, x, ldx, B, H, W, C, V);
   else
     hipLaunchKernelGGL(wino_input_kernel, dim3(grid_of(T * (C / 4))), dim3(256), 0, s, x, ldx, B, H, W, C, V);
   return launch_status("wino_input");
