@@ -9,12 +9,22 @@ all-reduce when N > 1) -> AdamW, inputs already resident in HBM.
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...       (one rank per GPU)
+
+With ``--gpus N > 1`` and no torchrun environment (WORLD_SIZE unset), bench.py is
+its own launcher: before anything touches the GPU it starts N child processes of
+itself with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT
+set (one rank per GPU, RCCL), waits for them and exits with the first non-zero
+child status. Every rank checks WORLD_SIZE == --gpus and fails otherwise.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import signal
+import socket
+import statistics
+import subprocess
 import sys
 import time
 
@@ -27,7 +37,7 @@ sys.path.insert(0, HERE)
 from physics_informed_image_segmentation_amd import AdamW, DiceBCEPDELoss, UNet  # noqa: E402
 from physics_informed_image_segmentation_amd.dataset import disc_sample  # noqa: E402
 from physics_informed_image_segmentation_amd.distributed import (GradBucketer, broadcast_parameters,  # noqa: E402
-                                                                 init_from_env)
+                                                                 env_world, init_from_env)
 
 B, H, W = 8, 512, 512
 LOSS_KW = dict(pde_weight=1e-4, phase_field_weight=1e-4, diffusion_coeff=5.0, reaction_threshold=0.5, epsilon=0.05)
@@ -147,46 +157,120 @@ class LossCallTimer:
         return out
 
 
-def load_pmc_traffic(kernel=DOMINANT_KERNEL):
-    """Per-launch HBM bytes of the dominant kernel from the committed rocprofv3 --pmc
-    summary (tools/pmc_summary.py, FETCH_SIZE x2 gfx950 correction + WRITE_SIZE)."""
+# kernels whose MFMA-busy fraction the bench line quotes: the GEMM-shaped ones and the fused loss
+BUSY_REPORTED = ("gemm_nt", "wgrad_x6", "wino4_gemm_out", "convt_gemm", "loss_fwd", "head_loss_bwd", "loss_bwd")
+
+
+def load_pmc(kernel=DOMINANT_KERNEL):
+    """Per-launch HBM bytes and MFMA-busy fraction of the dominant kernel from the committed
+    rocprofv3 --pmc summary (tools/pmc_summary.py: FETCH_SIZE x2 gfx950 correction +
+    WRITE_SIZE; SQ_VALU_MFMA_BUSY_CYCLES over GRBM_GUI_ACTIVE / 8 x 1024 SIMDs)."""
     path = os.path.join(HERE, "profiles", "pmc_dominant.json")
     if not os.path.exists(path):
-        return None
+        return None, None, None
     with open(path) as f:
         d = json.load(f)
     if kernel not in (d.get("dominant_kernel") or ""):
-        return None  # counters were taken on another kernel: report no traffic rather than a stale one
-    return d.get("hbm_bytes_per_launch")
+        return None, None, None  # counters were taken on another kernel: report none rather than stale ones
+    busy = {k.split("(")[0].replace("void ", ""): v["mfma_busy_frac"] for k, v in d.get("kernels", {}).items()
+            if "mfma_busy_frac" in v and any(s in k for s in BUSY_REPORTED)}
+    return d.get("hbm_bytes_per_launch"), d.get("mfma_busy_frac"), busy
 
 
-def cpu_baseline(seconds: float = 15.0):
-    """The oracle (stock-PyTorch CPU restatement of the reference step) on the host cores."""
+def host_cpus():
+    """(usable CPUs, description) of this process: the affinity mask, capped by the cgroup
+    CPU quota when one is set (a container may see every core of the machine in its
+    affinity mask but be granted only a share of them)."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, period = f.read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) // int(period)))
+    except (OSError, ValueError):
+        pass
+    model = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            model = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")), "")
+    except OSError:
+        pass
+    n = min(aff, quota) if quota else aff
+    return n, {"affinity_cpus": aff, "cgroup_quota_cpus": quota, "cpu_model": model,
+               "machine_cpus": os.cpu_count()}
+
+
+def cpu_baseline(batch: int = 8, steps: int = 3, size: int = 512, loss_kw=None, lr: float = LR):
+    """The oracle (stock-PyTorch CPU restatement of the reference step) on the
+    host cores: the C2 batch (8 x 512^2, Stage II), 1 warm-up step, median of ``steps``."""
     from oracle import reference_torch as rt
-    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    threads, info = host_cpus()
     torch.set_num_threads(threads)
-    img, mask = rt.synthetic_batch(1, H, W, seed=42)
+    img, mask = rt.synthetic_batch(batch, size, size, seed=42)
     torch.manual_seed(42)
     ref = rt.UNetRef(1, 1, 64).train()
-    opt = rt.make_adamw(ref, lr=LR)
-    kw = dict(rd_w=1e-4, pf_w=1e-4, D=5.0, a=0.5, eps=0.05)
+    opt = rt.make_adamw(ref, lr=lr)
+    kw = dict(rd_w=1e-4, pf_w=1e-4, D=5.0, a=0.5, eps=0.05) if loss_kw is None else loss_kw
     rt.train_step(ref, opt, img, mask, kw)  # warm-up
-    n, t0 = 0, time.perf_counter()
-    while True:
+    times = []
+    for _ in range(steps):
+        t0 = time.perf_counter()
         rt.train_step(ref, opt, img, mask, kw)
-        n += 1
-        dt = time.perf_counter() - t0
-        if dt >= seconds or n >= 64:
-            break
-    return {"value": n / dt, "unit": "images/s", "cores": threads, "kind": "port",
-            "sample": f"{n} Stage-II training steps of 1 image 512x512 (oracle/reference_torch.py, torch "
-                      f"{torch.__version__} CPU, {threads} threads) after 1 warm-up step, {dt:.1f} s"}
+        times.append(time.perf_counter() - t0)
+    med = statistics.median(times)
+    out = {"value": batch / med, "unit": "images/s", "cores": threads, "kind": "port",
+           "sample": f"median of {steps} training steps of {batch} images {size}x{size} "
+                     f"({'Stage II' if kw.get('rd_w') or kw.get('pf_w') else 'Stage I'}; oracle/reference_torch.py, "
+                     f"torch {torch.__version__} CPU, {threads} threads) after 1 warm-up step; step times "
+                     + ", ".join(f"{t:.2f}" for t in times) + " s"}
+    out.update(info)
+    return out
 
 
 def make_batch(rank: int, device):
     g = torch.Generator().manual_seed(42 + rank)
     imgs, masks = zip(*[disc_sample(H, W, g) for _ in range(B)])
     return torch.stack(imgs).to(device), torch.stack(masks).to(device)
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch(n: int) -> int:
+    """Start ``n`` ranks of this script (one process per GPU) and wait for them. The parent
+    never touches the GPU; it only forwards signals and collects exit statuses."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+
+    def stop(*_):
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+
+    signal.signal(signal.SIGTERM, lambda *a: (stop(), sys.exit(143)))
+    rc = 0
+    pending = list(procs)
+    while pending:
+        for p in list(pending):
+            code = p.poll()
+            if code is None:
+                continue
+            pending.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 128 - code
+                stop()  # one rank failed: the others would hang in their next collective
+        time.sleep(0.2)
+    return rc
 
 
 def main():
@@ -196,15 +280,29 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--config", choices=sorted(CONFIGS), default="c2")
+    ap.add_argument("--backend", choices=("nccl", "gloo"), default="nccl",
+                    help="process-group backend for N > 1 (nccl = RCCL over xGMI; gloo only to rehearse "
+                         "several ranks on one GPU)")
     ap.add_argument("--tune", action="append", default=[], metavar="KEY=VALUE",
                     help="pis_tune knob for experiments (include/pis_capi.h PIS_TUNE_*); defaults are the measured best")
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch(args.gpus))
     global H, W
     size, loss_kw, workload = CONFIGS[args.config]
     H = W = size
-    rank, local_rank, world = init_from_env("nccl")
-    device = torch.device("cuda", local_rank)
+    _, local_rank, world = env_world()
+    if world != args.gpus:
+        print(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}", file=sys.stderr)
+        sys.exit(2)
+    ndev = torch.cuda.device_count()  # counts devices without initialising the runtime
+    if ndev == 0 or (local_rank >= ndev and args.backend == "nccl"):
+        print(f"bench.py: rank {local_rank} has no GPU of its own ({ndev} visible); RCCL needs one GPU per rank",
+              file=sys.stderr)
+        sys.exit(2)
+    device = torch.device("cuda", local_rank % ndev)
     torch.cuda.set_device(device)
+    rank, local_rank, world = init_from_env(args.backend)
 
     if args.tune:
         from physics_informed_image_segmentation_amd import _hip as _h
@@ -281,7 +379,7 @@ def main():
             "fp32-equivalent FLOPs" if x6 else "fp32 MFMA")
     # bf16x6: gemm_nt_x6_bk32_kernel (K % 32 == 0, every C2 layer) or gemm_nt_x6_kernel
     kname = "gemm_nt_x6_" if x6 else DOMINANT_KERNEL
-    traffic = load_pmc_traffic(kname)
+    traffic, mfma_busy, busy_by_kernel = load_pmc(kname)
     if rank == 0:
         flops = conv_flops_per_image(H, W) * B
         out = {
@@ -297,6 +395,9 @@ def main():
                          "achieved": achieved, "peak": peak,
                          "unit": "TFLOP/s", "frac": achieved / peak, "traffic": traffic, "pipe": pipe,
                          "fp32_mfma_peak_frac": achieved / 157.3,
+                         # rocprofv3 PMC (profiles/pmc_dominant.json): fraction of SIMD-cycles the
+                         # matrix pipe was busy in this kernel, and in the step's other kernels
+                         "mfma_busy_frac": mfma_busy, "mfma_busy_by_kernel": busy_by_kernel,
                          "launches_per_step": n_launch, "avg_launch_ms": ms_per_launch,
                          "flop_per_launch": flop_per_launch,
                          "measured": "live over the timed steps; the input-gradient launches share the GPU "

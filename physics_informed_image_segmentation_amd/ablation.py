@@ -233,14 +233,35 @@ def _summary(metrics: Dict[str, np.ndarray]) -> Dict[str, Dict[str, float]]:
     return out
 
 
-def run_ablation_variant(config: AblationConfig, data: DataSpec, device: torch.device, batch_size: int = 8,
+_PATH_ARGS = ("train_dir", "train_json", "val_dir", "val_json", "in_dist_test_dir", "in_dist_test_json",
+              "out_dist_test_dir", "out_dist_test_json")
+_DEFAULT_OUT = Path(__file__).resolve().parent.parent / "output" / "ablation"
+
+
+def _data_spec(first, paths) -> DataSpec:
+    """The reference passes eight directory/JSON paths (src/ablation.py:157-175); this build
+    also accepts one ``DataSpec`` (e.g. the synthetic generator) in the first path's place."""
+    if isinstance(first, DataSpec):
+        return first
+    return DataSpec(*(Path(p) if p is not None else None for p in (first,) + tuple(paths)))
+
+
+def run_ablation_variant(config: AblationConfig, train_dir, train_json=None, val_dir=None, val_json=None,
+                         in_dist_test_dir=None, in_dist_test_json=None, out_dist_test_dir=None,
+                         out_dist_test_json=None, device: Optional[torch.device] = None, batch_size: int = 8,
                          learning_rate: float = 1e-4, stage1_epochs: int = 50, stage2_epochs: int = 50,
-                         early_stopping_patience: int = 10, ablation_folder: Optional[Path] = None,
-                         num_workers: int = 2, boundary_metrics: bool = True, verbose: bool = False) -> Dict:
-    """Train one variant and evaluate it on both test sets (src/ablation.py:157-1237)."""
+                         early_stopping_patience: int = 10, output_dir: Optional[Path] = None,
+                         ablation_folder: Optional[Path] = None, num_workers: int = 2, boundary_metrics: bool = True,
+                         verbose: bool = False) -> Dict:
+    """Train one variant and evaluate it on both test sets (src/ablation.py:157-1237); same
+    positional signature as the reference (``train_dir`` may be a ``DataSpec`` instead)."""
+    data = _data_spec(train_dir, (train_json, val_dir, val_json, in_dist_test_dir, in_dist_test_json,
+                                  out_dist_test_dir, out_dist_test_json))
+    if device is None:
+        device = torch.device("cuda")
     if config.output_activation != "sigmoid" or config.intermediate_activation != "relu":
         raise ValueError("this build runs the reference configuration: sigmoid output, ReLU activations")
-    folder = Path(ablation_folder) if ablation_folder else Path.cwd() / "output" / "ablation"
+    folder = Path(ablation_folder) if ablation_folder else (Path(output_dir) if output_dir else _DEFAULT_OUT)
     folder.mkdir(parents=True, exist_ok=True)
     torch.manual_seed(config.seed)
     np.random.seed(config.seed)
@@ -299,18 +320,22 @@ def run_ablation_variant(config: AblationConfig, data: DataSpec, device: torch.d
     return result
 
 
-def run_ablation_study(ablation_name: str, variants: List[AblationConfig], data: DataSpec, device: torch.device,
-                       batch_size: int = 8, learning_rate: float = 1e-4, stage1_epochs: int = 50,
-                       stage2_epochs: int = 50, early_stopping_patience: int = 10,
-                       output_dir: Optional[Path] = None, **kw) -> Dict:
-    """One run per variant; results JSON + summary CSV (src/ablation.py:1240-1474)."""
-    root = Path(output_dir) if output_dir else Path.cwd() / "output" / "ablation"
+def run_ablation_study(ablation_name: str, variants: List[AblationConfig], train_dir, train_json=None, val_dir=None,
+                       val_json=None, in_dist_test_dir=None, in_dist_test_json=None, out_dist_test_dir=None,
+                       out_dist_test_json=None, device: Optional[torch.device] = None, batch_size: int = 8,
+                       learning_rate: float = 1e-4, stage1_epochs: int = 50, stage2_epochs: int = 50,
+                       early_stopping_patience: int = 10, output_dir: Optional[Path] = None, **kw) -> Dict:
+    """One run per variant; results JSON + summary CSV (src/ablation.py:1240-1474); same
+    positional signature as the reference (``train_dir`` may be a ``DataSpec`` instead)."""
+    data = _data_spec(train_dir, (train_json, val_dir, val_json, in_dist_test_dir, in_dist_test_json,
+                                  out_dist_test_dir, out_dist_test_json))
+    root = Path(output_dir) if output_dir else _DEFAULT_OUT
     folder = root / f"{ablation_name}_{datetime.now().strftime('%Y%m%d_%H%M%S')}"
     folder.mkdir(parents=True, exist_ok=True)
     results = []
     for v in variants:
         print(f"\n{'=' * 70}\nAblation {ablation_name}: {v.name}\n  {v.description}\n{'=' * 70}", flush=True)
-        results.append(run_ablation_variant(v, data, device, batch_size=batch_size, learning_rate=learning_rate,
+        results.append(run_ablation_variant(v, data, device=device, batch_size=batch_size, learning_rate=learning_rate,
                                             stage1_epochs=stage1_epochs, stage2_epochs=stage2_epochs,
                                             early_stopping_patience=early_stopping_patience, ablation_folder=folder,
                                             **kw))

@@ -45,6 +45,20 @@ def compute_iou_batch(predictions: torch.Tensor, targets: torch.Tensor, threshol
     return sample_counts(predictions, targets, threshold, smooth)[1][:, 1].contiguous()
 
 
+def _dilate4(x: np.ndarray, iterations: int = 1) -> np.ndarray:
+    """Binary dilation by the 4-neighbour cross (= ndimage.binary_dilation(x, _FOUR)), as
+    shifted ORs; two iterations give the Euclidean disk of radius 2 (|dx| + |dy| <= 2 and
+    dx^2 + dy^2 <= 4 select the same 13 offsets)."""
+    for _ in range(iterations):
+        y = x.copy()
+        y[1:] |= x[:-1]
+        y[:-1] |= x[1:]
+        y[:, 1:] |= x[:, :-1]
+        y[:, :-1] |= x[:, 1:]
+        x = y
+    return x
+
+
 def extract_boundaries(mask: np.ndarray) -> np.ndarray:
     """Outer-contour pixels of a binary (H, W) mask as float32 {0, 1} (src/evaluate.py:102-120)."""
     fg = np.asarray(mask) > 0
@@ -53,8 +67,16 @@ def extract_boundaries(mask: np.ndarray) -> np.ndarray:
     pad = np.pad(fg, 1, constant_values=False)
     lab, _ = ndimage.label(~pad, structure=_FOUR)
     outer = lab == lab[0, 0]  # the frame is background and connected to itself
-    near_outer = ndimage.binary_dilation(outer, structure=_FOUR)
-    return (pad & near_outer)[1:-1, 1:-1].astype(np.float32)
+    return (pad & _dilate4(outer))[1:-1, 1:-1].astype(np.float32)
+
+
+def _near(b: np.ndarray, tolerance: int) -> np.ndarray:
+    """Pixels within Euclidean distance ``tolerance`` of a boundary pixel."""
+    if tolerance <= 2:
+        return _dilate4(b, tolerance)
+    disk = np.array([[dy * dy + dx * dx <= tolerance * tolerance for dx in range(-tolerance, tolerance + 1)]
+                     for dy in range(-tolerance, tolerance + 1)])
+    return ndimage.binary_dilation(b, structure=disk)
 
 
 def _binary_np(x: torch.Tensor, threshold: float = None) -> np.ndarray:
@@ -66,11 +88,8 @@ def _binary_np(x: torch.Tensor, threshold: float = None) -> np.ndarray:
 
 def _boundary_f1_np(pred_b: np.ndarray, target_b: np.ndarray, tolerance: int, smooth: float) -> float:
     if tolerance > 0:
-        disk = _DISK2 if tolerance == 2 else np.array(
-            [[dy * dy + dx * dx <= tolerance * tolerance for dx in range(-tolerance, tolerance + 1)]
-             for dy in range(-tolerance, tolerance + 1)])
-        near_t = ndimage.binary_dilation(target_b > 0, structure=disk)
-        near_p = ndimage.binary_dilation(pred_b > 0, structure=disk)
+        near_t = _near(target_b > 0, tolerance)
+        near_p = _near(pred_b > 0, tolerance)
         precision = ((near_t * pred_b).sum() + smooth) / (pred_b.sum() + smooth)
         recall = ((near_p * target_b).sum() + smooth) / (target_b.sum() + smooth)
         return float((2.0 * precision * recall + smooth) / (precision + recall + smooth))
@@ -131,6 +150,76 @@ def evaluate_model(model, dataloader, device, threshold: float = 0.5,
     return out
 
 
+# ----------------------------------------------------------------------------
+# Statistics and test-set evaluation (src/evaluate.py:349-523) — host-side, after training
+# ----------------------------------------------------------------------------
+
+def compute_statistics(metric_array: np.ndarray) -> Dict[str, float]:
+    """Mean, sample std (ddof=1) and count over the non-NaN entries (src/evaluate.py:349-369)."""
+    a = np.asarray(metric_array, dtype=np.float64)
+    a = a[~np.isnan(a)]
+    if a.size == 0:
+        return {"mean": np.nan, "std": np.nan, "count": 0}
+    return {"mean": float(a.mean()), "std": float(a.std(ddof=1)), "count": int(a.size)}
+
+
+_NO_TEST = {"t_statistic": np.nan, "t_pvalue": np.nan, "wilcoxon_statistic": np.nan,
+            "wilcoxon_pvalue": np.nan, "significant": False}
+
+
+def compare_models_statistically(metrics_baseline: Dict[str, np.ndarray], metrics_pde: Dict[str, np.ndarray],
+                                 alpha: float = 0.05) -> Dict[str, Dict[str, float]]:
+    """Paired t-test + two-sided Wilcoxon signed-rank per metric over the images where both
+    models have a value; significant if either p < alpha (src/evaluate.py:372-438)."""
+    from scipy import stats
+    out = {}
+    for name, base in metrics_baseline.items():
+        b = np.asarray(base, dtype=np.float64)
+        p = np.asarray(metrics_pde[name], dtype=np.float64)
+        keep = ~(np.isnan(b) | np.isnan(p))
+        b, p = b[keep], p[keep]
+        if b.size < 2:
+            out[name] = dict(_NO_TEST)
+            continue
+        t_stat, t_p = stats.ttest_rel(b, p)
+        w_stat, w_p = stats.wilcoxon(b, p, alternative="two-sided")
+        sb, sp = compute_statistics(b), compute_statistics(p)
+        out[name] = {"t_statistic": float(t_stat), "t_pvalue": float(t_p), "wilcoxon_statistic": float(w_stat),
+                     "wilcoxon_pvalue": float(w_p), "significant": bool(t_p < alpha or w_p < alpha),
+                     "baseline_mean": sb["mean"], "baseline_std": sb["std"], "pde_mean": sp["mean"],
+                     "pde_std": sp["std"], "improvement": float(p.mean() - b.mean())}
+    return out
+
+
+def format_metric_report(metrics: Dict[str, np.ndarray], model_name: str = "Model") -> str:
+    """'<Metric Title>: mean ± std (n=count)' lines (src/evaluate.py:441-472)."""
+    lines = [f"\n{model_name} Performance:", "=" * 60]
+    for name, arr in metrics.items():
+        st = compute_statistics(arr)
+        title = name.replace("_", " ").title()
+        lines.append(f"{title}: {st['mean']:.4f} ± {st['std']:.4f} (n={st['count']})" if st["count"] > 0
+                     else f"{title}: N/A")
+    return "\n".join(lines)
+
+
+def evaluate_on_test_set(model, test_dir, test_json, device, batch_size: int = 8, threshold: float = 0.5,
+                         model_name: str = "Model") -> Dict[str, np.ndarray]:
+    """Per-image metrics of ``model`` on a COCO-annotated test folder (src/evaluate.py:476-522)."""
+    from torch.utils.data import DataLoader
+
+    from .dataset import CellSegmentationDataset
+    print(f"\nEvaluating {model_name} on test set...")
+    print("=" * 70)
+    ds = CellSegmentationDataset(test_dir, test_json)
+    loader = DataLoader(ds, batch_size=batch_size, shuffle=False, num_workers=2,
+                        pin_memory=torch.cuda.is_available())
+    print(f"Test samples: {len(ds)}")
+    metrics = evaluate_model(model, loader, device, threshold=threshold)
+    print(format_metric_report(metrics, model_name=model_name))
+    return metrics
+
+
 __all__ = ["compute_iou", "compute_iou_batch", "extract_boundaries", "compute_boundary_f1",
            "compute_boundary_f1_batch", "compute_hausdorff_distance", "evaluate_model",
-           "compute_dice_score_batch"]
+           "compute_dice_score_batch", "compute_statistics", "compare_models_statistically",
+           "format_metric_report", "evaluate_on_test_set"]

@@ -12,9 +12,9 @@ What changes underneath:
     of the one fused loss launch instead of a second logging recompute;
   * accumulators stay on the device; the host synchronises once per epoch
     (the reference calls ``.item()``/``.cpu()`` several times per step);
-  * optional data-parallel training (torchrun, RCCL), see ``distributed``.
-Boundary-F1 needs OpenCV (absent here) and is outside this path: it is
-reported as 0.0, the value the reference reports when it has no scores.
+  * optional data-parallel training (torchrun, RCCL), see ``distributed``;
+  * boundary F1 (OpenCV in the reference, a cv2-free restatement here) is
+    scored on host threads beside the GPU, not inside the step.
 """
 from __future__ import annotations
 
@@ -142,62 +142,137 @@ def _results(meter: _Meter, criterion, return_components: bool, compute_metrics:
         if not val:
             out["dice_score"] = scores[0] / ns if ns else 0.0
         out["iou_score"] = scores[1] / ns if ns else 0.0
-        # 0.0 unless boundary_metrics=True (host-side, off the hot path): the reference's value
-        # without scores
+        # host threads beside the GPU (_BoundaryF1Async); 0.0 with boundary_metrics=False
         out["boundary_f1_score"] = meter.bf1_total / ns if ns else 0.0
     return out
 
 
-def _boundary_sum(outputs, masks) -> float:
-    from .evaluate import compute_boundary_f1_batch
-    return float(compute_boundary_f1_batch(outputs, masks, threshold=0.5, tolerance=2).sum())
+class _BoundaryF1Async:
+    """Per-sample boundary F1 of every step (src/train.py:156,259), off the critical path: the
+    step's probabilities and masks are copied to pinned host memory on a copy stream (ordered
+    after the forward by an event) and scored by host threads (cv2-free ``evaluate``
+    restatement, scipy releases the GIL) while the GPU runs the backward and the next steps.
+    The only GPU-side cost is one stream wait before the next forward, so the engine's
+    probability buffer is not overwritten before its copy has landed."""
+
+    def __init__(self, device, workers: Optional[int] = None):
+        from concurrent.futures import ThreadPoolExecutor
+        n = workers or max(1, min(8, len(os.sched_getaffinity(0)) - 1))
+        self.pool = ThreadPoolExecutor(max_workers=n)
+        self.copy = torch.cuda.Stream(device=device)
+        self.fence: Optional[torch.cuda.Event] = None
+        self.futures = []
+        self.free = []  # pinned host buffers ready for reuse
+
+    def before_forward(self):
+        if self.fence is not None:
+            torch.cuda.current_stream().wait_event(self.fence)
+            self.fence = None
+
+    def _pinned(self, shape):
+        for i, (p, t) in enumerate(self.free):
+            if p.shape == shape:
+                return self.free.pop(i)
+        return (torch.empty(shape, dtype=torch.float32, pin_memory=True),
+                torch.empty(shape, dtype=torch.float32, pin_memory=True))
+
+    def submit(self, outputs: torch.Tensor, masks: torch.Tensor):
+        B, H, W = outputs.shape[0], outputs.shape[-2], outputs.shape[-1]
+        hp, ht = self._pinned((B, H, W))
+        ready = torch.cuda.Event()
+        ready.record(torch.cuda.current_stream())
+        self.copy.wait_event(ready)
+        with torch.cuda.stream(self.copy):
+            hp.copy_(outputs.detach().reshape(B, H, W), non_blocking=True)
+            ht.copy_(masks.detach().reshape(B, H, W), non_blocking=True)
+            masks.record_stream(self.copy)
+            done = torch.cuda.Event()
+            done.record(self.copy)
+        self.fence = done
+        self.futures.append(self.pool.submit(self._score, done, hp, ht))
+
+    def _score(self, done, hp, ht) -> Tuple[float, int]:
+        from .evaluate import _boundary_f1_np, extract_boundaries
+        done.synchronize()
+        p, t = hp.numpy() > 0.5, ht.numpy()
+        tot = sum(_boundary_f1_np(extract_boundaries(p[i]), extract_boundaries(t[i]), 2, 1e-6)
+                  for i in range(p.shape[0]))
+        self.free.append((hp, ht))
+        return tot, p.shape[0]
+
+    def collect(self) -> float:
+        """Sum of the per-sample scores submitted so far (waits for the host threads)."""
+        tot = sum(f.result()[0] for f in self.futures)
+        self.futures = []
+        return tot
+
+    def close(self):
+        self.pool.shutdown(wait=True)
 
 
 def train_epoch(model, dataloader, criterion, optimizer, device, return_components: bool = False,
-                compute_metrics: bool = True, boundary_metrics: bool = False) -> Dict[str, float]:
-    """One pass over ``dataloader`` (src/train.py:84-185); same result keys. The reference
-    computes boundary F1 on the host every step (src/train.py:152-160); here that is opt-in
-    (``boundary_metrics``, cv2-free, evaluate.py) so the step stays device-only."""
+                compute_metrics: bool = True, boundary_metrics: bool = True) -> Dict[str, float]:
+    """One pass over ``dataloader`` (src/train.py:84-185); same result keys and averaging:
+    loss terms averaged over batches, Dice / IoU / boundary F1 over samples. Boundary F1
+    (src/train.py:156) is scored on host threads beside the GPU (``_BoundaryF1Async``);
+    ``boundary_metrics=False`` reports 0.0 instead."""
     model.train()
     meter = _Meter(device)
-    for images, masks in dataloader:
-        images = images.to(device, non_blocking=True)
-        masks = masks.to(device, non_blocking=True)
-        optimizer.zero_grad()
-        outputs = model(images)
-        loss = criterion(outputs, masks)
-        terms, scores = _criterion_terms(criterion, outputs, masks)
-        meter.add(terms, scores if compute_metrics else None)
-        if compute_metrics and boundary_metrics:
-            meter.bf1 += _boundary_sum(outputs, masks)
-        loss.backward()
-        optimizer.step()
+    bf1 = _BoundaryF1Async(device) if compute_metrics and boundary_metrics else None
+    try:
+        for images, masks in dataloader:
+            images = images.to(device, non_blocking=True)
+            masks = masks.to(device, non_blocking=True)
+            optimizer.zero_grad()
+            if bf1 is not None:
+                bf1.before_forward()
+            outputs = model(images)
+            loss = criterion(outputs, masks)
+            terms, scores = _criterion_terms(criterion, outputs, masks)
+            meter.add(terms, scores if compute_metrics else None)
+            if bf1 is not None:
+                bf1.submit(outputs, masks)
+            loss.backward()
+            optimizer.step()
+        if bf1 is not None:
+            meter.bf1 += bf1.collect()
+    finally:
+        if bf1 is not None:
+            bf1.close()
     return _results(meter, criterion, return_components, compute_metrics, val=False)
 
 
 @torch.no_grad()
 def validate(model, dataloader, criterion, device, return_components: bool = False,
-             compute_metrics: bool = True, boundary_metrics: bool = False) -> Dict[str, float]:
+             compute_metrics: bool = True, boundary_metrics: bool = True) -> Dict[str, float]:
     """Eval-mode pass (src/train.py:188-286); ``dice_score`` is the mean of
     whole-batch thresholded Dice, as in the reference."""
     model.eval()
     meter = _Meter(device)
-    for images, masks in dataloader:
-        images = images.to(device, non_blocking=True)
-        masks = masks.to(device, non_blocking=True)
-        outputs = model(images)
-        criterion(outputs, masks)
-        terms, scores = _criterion_terms(criterion, outputs, masks)
-        last = getattr(criterion, "last", {})
-        counts = last.get("counts")
-        if counts is None:
-            _, counts, _ = loss_forward(outputs, masks, LossConfig(dice_w=0.0, bce_w=0.0))
-        tot = counts.sum(dim=0).to(torch.float32)
-        s = criterion.smooth if hasattr(criterion, "smooth") else 1e-6
-        batch_dice = (2.0 * tot[0] + 1e-6) / (tot[1] + tot[2] + 1e-6)
-        meter.add(terms, scores if compute_metrics else None, batch_dice)
-        if compute_metrics and boundary_metrics:
-            meter.bf1 += _boundary_sum(outputs, masks)
+    bf1 = _BoundaryF1Async(device) if compute_metrics and boundary_metrics else None
+    try:
+        for images, masks in dataloader:
+            images = images.to(device, non_blocking=True)
+            masks = masks.to(device, non_blocking=True)
+            if bf1 is not None:
+                bf1.before_forward()
+            outputs = model(images)
+            criterion(outputs, masks)
+            terms, scores = _criterion_terms(criterion, outputs, masks)
+            last = getattr(criterion, "last", {})
+            counts = last.get("counts")
+            if counts is None:
+                _, counts, _ = loss_forward(outputs, masks, LossConfig(dice_w=0.0, bce_w=0.0))
+            tot = counts.sum(dim=0).to(torch.float32)
+            batch_dice = (2.0 * tot[0] + 1e-6) / (tot[1] + tot[2] + 1e-6)  # src/metrics.py:4-35
+            meter.add(terms, scores if compute_metrics else None, batch_dice)
+            if bf1 is not None:
+                bf1.submit(outputs, masks)
+        if bf1 is not None:
+            meter.bf1 += bf1.collect()
+    finally:
+        if bf1 is not None:
+            bf1.close()
     return _results(meter, criterion, return_components, compute_metrics, val=True)
 
 
@@ -210,9 +285,10 @@ def train_stage(model, train_loader, val_loader, criterion, optimizer, device, n
     is_main = not (torch.distributed.is_available() and torch.distributed.is_initialized()) or \
         torch.distributed.get_rank() == 0
     for epoch in range(1, num_epochs + 1):
-        sampler = getattr(train_loader, "sampler", None)
-        if hasattr(sampler, "set_epoch"):
-            sampler.set_epoch(epoch)
+        # reshuffle per epoch like DataLoader(shuffle=True): DistributedSampler or DeviceDiscLoader
+        for obj in (train_loader, getattr(train_loader, "sampler", None)):
+            if hasattr(obj, "set_epoch"):
+                obj.set_epoch(epoch)
         tr = train_epoch(model, train_loader, criterion, optimizer, device, return_components=True,
                          compute_metrics=True)
         va = validate(model, val_loader, criterion, device, return_components=True, compute_metrics=True)
@@ -303,17 +379,28 @@ def _loaders(train_ds, val_ds, batch_size: int, world: int, rank: int, workers: 
             DataLoader(val_ds, batch_size=batch_size, shuffle=False, num_workers=workers, pin_memory=pin))
 
 
+_REPO_ROOT = Path(__file__).resolve().parent.parent
+
+
 def train(use_two_stage: bool = True, pde_weight: float = 1e-4, diffusion_coeff: float = 5.0,
           reaction_threshold: float = 0.5, phase_field_weight: float = 1e-4, epsilon: float = 0.05,
           batch_size: int = 8, learning_rate: float = 1e-4, stage1_epochs: int = 50, stage2_epochs: int = 50,
           early_stopping_patience: int = 10, train_fraction: Optional[float] = None, seed: int = 42,
           base_dir: Optional[str] = None, synthetic: Optional[Tuple[int, int, int, int]] = None,
           num_workers: int = 2, device_data: bool = True):
-    """Two-stage training (src/train.py:531-915). Extra, build-only arguments:
-    ``base_dir`` (where images/, output/, models/ live; default: cwd) and
-    ``synthetic=(n_train, n_val, H, W)`` to train on the SURVEY §8(c) disc
-    generator when the cell dataset is not present — rasterised on the GPU
-    (``DeviceDiscLoader``, sharded like DistributedSampler) unless ``device_data=False``."""
+    """Two-stage training (src/train.py:531-915), same control flow: Stage I (Dice+BCE) always
+    runs and saves models/unet_baseline.pth; then either Stage II (PDE loss at lr x 0.1) ->
+    unet_pde_regularized.pth, or, with ``use_two_stage=False``, a PDE-loss run at the full lr for
+    ``stage1_epochs`` on top of the Stage-I weights (src/train.py:777-832); finally the test-set
+    evaluation when images/testing and its annotation exist (src/train.py:848-911), writing
+    test_metrics_stage{1,2}_* / test_metrics_single_stage_* (JSON + CSV). The training plots
+    (src/plot.py) are not produced (out of scope).
+
+    Extra, build-only arguments: ``base_dir`` (where images/, output/, models/ live; default:
+    the repository root, like the reference's ``Path(__file__).parent.parent``),
+    ``synthetic=(n_train, n_val, H, W)`` to train on the SURVEY §8(c) disc generator when the
+    cell dataset is not present — rasterised on the GPU (``DeviceDiscLoader``, sharded like
+    DistributedSampler) unless ``device_data=False``."""
     rank, local_rank, world = init_from_env()
     if not torch.cuda.is_available():
         raise _hip.HipError("train(): the MI355X path needs a GPU (no CPU fallback in this build)")
@@ -324,10 +411,11 @@ def train(use_two_stage: bool = True, pde_weight: float = 1e-4, diffusion_coeff:
     torch.cuda.manual_seed(seed)
     is_main = rank == 0
 
-    base = Path(base_dir) if base_dir else Path.cwd()
+    base = Path(base_dir) if base_dir else _REPO_ROOT
     img_dir, out_dir = base / "images", base / "output"
     ann_dir = img_dir / "annotation"
-    out_dir.mkdir(exist_ok=True)
+    test_dir, test_json = img_dir / "testing", ann_dir / "testing_annotation.json"
+    out_dir.mkdir(parents=True, exist_ok=True)
     stamp = datetime.now().strftime("%Y%m%d_%H%M%S")
     say = print if is_main else (lambda *a, **k: None)
     say("=" * 70)
@@ -376,38 +464,83 @@ def train(use_two_stage: bool = True, pde_weight: float = 1e-4, diffusion_coeff:
                               phase_field_weight=phase_field_weight, diffusion_coeff=diffusion_coeff,
                               reaction_threshold=reaction_threshold, epsilon=epsilon).to(device)
 
+    def describe_pde():
+        say("Objective: L = L_Dice + L_BCE + λ_RD * L_RD + λ_PF * L_PF")
+        say(f"  λ_RD (reaction-diffusion): {pde_weight}")
+        say(f"  λ_PF (phase-field): {phase_field_weight}")
+        say(f"  Diffusion coefficient (D): {diffusion_coeff}")
+        say(f"  Reaction threshold (a): {reaction_threshold}")
+        if phase_field_weight > 0:
+            say(f"  Phase-field epsilon (ε): {epsilon}")
+
     models_dir = base / "models"
     result = {}
+    # ---- Stage I: always (src/train.py:651-691) ----
+    say("\n" + "=" * 70 + "\nSTAGE I: BASELINE TRAINING (Unconstrained)\n" + "=" * 70)
+    say("Objective: L = L_Dice + L_BCE")
+    csv1 = out_dir / f"metrics_stage1_{stamp}{frac}.csv"
+    best1, ep1, hist1 = run(DiceBCELoss(0.5, 0.5).to(device), learning_rate, stage1_epochs, "Stage I", csv1)
+    result["stage1"] = (best1, ep1, hist1)
+    if best1:
+        say(f"\nStage I complete. Best validation Dice: {best1['val']['dice_score']:.6f} at epoch {ep1}")
+    say(f"Stage I metrics saved to: {csv1}")
+    stage1_path = models_dir / "unet_baseline.pth"
+    if is_main:
+        models_dir.mkdir(parents=True, exist_ok=True)
+        torch.save(model.state_dict(), stage1_path)
+    say(f"Stage I model saved to: {stage1_path}")
     if use_two_stage:
-        say("\n" + "=" * 70 + "\nSTAGE I: BASELINE TRAINING (Unconstrained)\n" + "=" * 70)
-        csv1 = out_dir / f"metrics_stage1_{stamp}{frac}.csv"
-        best1, ep1, hist1 = run(DiceBCELoss(0.5, 0.5).to(device), learning_rate, stage1_epochs, "Stage I", csv1)
-        result["stage1"] = (best1, ep1, hist1)
-        if is_main:
-            models_dir.mkdir(exist_ok=True)
-            torch.save(model.state_dict(), models_dir / "unet_baseline.pth")
         say("\n" + "=" * 70 + "\nSTAGE II: PDE-CONSTRAINED FINE-TUNING\n" + "=" * 70)
+        describe_pde()
         lr2 = learning_rate * 0.1  # src/train.py:720
         say(f"  Learning rate for Stage II: {lr2:.2e} (reduced from {learning_rate:.2e})")
         csv2 = out_dir / f"metrics_stage2_{stamp}{frac}.csv"
         best2, ep2, hist2 = run(pde_loss(), lr2, stage2_epochs, "Stage II", csv2)
         result["stage2"] = (best2, ep2, hist2)
         if best2 and "val" in best2:
+            say(f"\nStage II complete. Best validation Dice: {best2['val']['dice_score']:.6f} at epoch {ep2}")
             say("\nStability checks:")
-            for key in ("pde_loss", "dice_loss", "bce_loss"):
-                if key in best2["val"]:
-                    say(f"  Final {key}: {best2['val'][key]:.6f}")
+            for key, label in (("pde_loss", "PDE"), ("dice_loss", "Dice"), ("bce_loss", "BCE")):
+                if key in best2["val"]:  # the reference raises KeyError when lambda_RD = 0
+                    say(f"  Final {label} loss: {best2['val'][key]:.6f}")
             if best1 and "val" in best1:
+                say("\nPDE regularization effect:")
                 say(f"  Dice score improvement: {best2['val']['dice_score'] - best1['val']['dice_score']:+.6f}")
-        if is_main:
-            torch.save(model.state_dict(), models_dir / "unet_pde_regularized.pth")
+        say(f"Stage II metrics saved to: {csv2}")
+        final_path = models_dir / "unet_pde_regularized.pth"
     else:
         say("\n" + "=" * 70 + "\nSINGLE-STAGE TRAINING (PDE from start)\n" + "=" * 70)
-        csv1 = out_dir / f"metrics_single_stage_{stamp}{frac}.csv"
-        best, ep, hist = run(pde_loss(), learning_rate, stage1_epochs, "Training", csv1)
+        describe_pde()
+        csv1s = out_dir / f"metrics_single_stage_{stamp}{frac}.csv"
+        best, ep, hist = run(pde_loss(), learning_rate, stage1_epochs, "Training", csv1s)
         result["single"] = (best, ep, hist)
-        if is_main:
-            models_dir.mkdir(exist_ok=True)
-            torch.save(model.state_dict(), models_dir / "unet_pde_regularized.pth")
+        say(f"Single-stage metrics saved to: {csv1s}")
+        final_path = models_dir / "unet_pde_regularized.pth"
+    if is_main:
+        torch.save(model.state_dict(), final_path)
+    say(f"Model saved to: {final_path}")
+
+    # ---- test-set evaluation (src/train.py:848-911), rank 0 ----
+    say("\n" + "=" * 70 + "\nTEST SET EVALUATION\n" + "=" * 70)
+    if is_main and test_json.exists() and test_dir.exists():
+        from .evaluate import evaluate_on_test_set
+        name = "PDE-Constrained (Stage II)" if use_two_stage else "Single-Stage PDE-Constrained"
+        m = evaluate_on_test_set(model, test_dir, test_json, device, batch_size=batch_size, threshold=0.5,
+                                 model_name=name)
+        tag = "stage2" if use_two_stage else "single_stage"
+        save_test_metrics(m, out_dir / f"test_metrics_{tag}_{stamp}{frac}", model_name=name)
+        result["test"] = m
+        if use_two_stage:
+            say("\n" + "=" * 70 + "\nEVALUATING STAGE I MODEL ON TEST SET\n" + "=" * 70)
+            stage1 = UNet(in_channels=1, out_channels=1, base_channels=64)
+            stage1.load_state_dict(torch.load(stage1_path, map_location="cpu", weights_only=True))
+            stage1 = stage1.to(device)
+            m1 = evaluate_on_test_set(stage1, test_dir, test_json, device, batch_size=batch_size, threshold=0.5,
+                                      model_name="Baseline (Stage I)")
+            save_test_metrics(m1, out_dir / f"test_metrics_stage1_{stamp}{frac}", model_name="Baseline (Stage I)")
+            result["test_stage1"] = m1
+    elif is_main:
+        say(f"Warning: Test set not found at {test_dir} or {test_json}")
+        say("Skipping test set evaluation.")
     say("\n" + "=" * 70 + "\nTRAINING COMPLETE\n" + "=" * 70)
     return model, result

@@ -54,7 +54,7 @@ def main(argv=None):
     out = {}
     for name in names:
         print(f"\n{'=' * 70}\nStarting Ablation Study: {name}\n{'=' * 70}")
-        res = run_ablation_study(name, ABLATIONS[name](), data, device, batch_size=args.batch_size,
+        res = run_ablation_study(name, ABLATIONS[name](), data, device=device, batch_size=args.batch_size,
                                  learning_rate=args.learning_rate, stage1_epochs=args.stage1_epochs,
                                  stage2_epochs=args.stage2_epochs,
                                  early_stopping_patience=args.early_stopping_patience,

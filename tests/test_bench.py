@@ -40,3 +40,35 @@ def test_bench_json_contract():
     assert r["bound"] == "mfma" and r["unit"] == "TFLOP/s" and 0 < r["frac"] < 1
     assert abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-9
     assert r["launches_per_step"] > 0 and r["avg_launch_ms"] > 0
+
+
+@pytest.mark.gpu
+def test_bench_launches_n_ranks():
+    """`bench.py --gpus 2` without a torchrun environment starts its own two ranks (here both on
+    the one GPU over gloo: RCCL needs a GPU per rank) and reports the whole job."""
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_PORT")}
+    out = subprocess.run([sys.executable, os.path.join(HERE, "bench.py"), "--gpus", "2", "--backend", "gloo",
+                          "--steps", "2", "--warmup", "1", "--no-cpu-baseline"],
+                         capture_output=True, text=True, timeout=110, cwd=HERE, env=env)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout[-2000:]  # rank 0 only
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "dp2" and d["config"]["global_batch"] == 16
+    assert abs(d["value"] - 16 * 1000.0 / d["ms_per_step"]) < 1e-6 * d["value"]  # 2 ranks x 8 images
+    assert "cpu_baseline" not in d
+
+
+def test_bench_rejects_world_mismatch():
+    """A rank whose WORLD_SIZE disagrees with --gpus exits non-zero before touching the GPU."""
+    env = dict(os.environ, RANK="0", LOCAL_RANK="0", WORLD_SIZE="2", MASTER_ADDR="127.0.0.1", MASTER_PORT="29999")
+    out = subprocess.run([sys.executable, os.path.join(HERE, "bench.py"), "--gpus", "4", "--steps", "1"],
+                         capture_output=True, text=True, timeout=300, cwd=HERE, env=env)
+    assert out.returncode == 2 and "WORLD_SIZE=2 but --gpus 4" in out.stderr
+
+
+def test_host_cpus_reports_quota():
+    n, info = _bench().host_cpus()
+    assert 1 <= n <= info["affinity_cpus"]
+    if info["cgroup_quota_cpus"]:
+        assert n <= info["cgroup_quota_cpus"]

@@ -131,7 +131,7 @@ def test_ablation_variant_end_to_end(hip, tmp_path):
     from physics_informed_image_segmentation_amd import ablation as ab
     data = ab.DataSpec(synthetic=(4, 2, 2, 32, 32))
     v = ab.define_ablation_r1()[3]
-    res = ab.run_ablation_study("R1", [v], data, torch.device("cuda"), batch_size=2, stage1_epochs=1,
+    res = ab.run_ablation_study("R1", [v], data, device=torch.device("cuda"), batch_size=2, stage1_epochs=1,
                                 stage2_epochs=1, output_dir=tmp_path, num_workers=0)
     r = res["results"][0]
     assert r["stage1_best_epoch"] in (0, 1) and len(r["in_dist_metrics"]["dice_scores"]) == 2
