@@ -82,7 +82,9 @@ int pis_version(void);
 #define PIS_TUNE_WINO_DZ2 16     /* pis_conv3x3_bwd_prep: 1 (default) one pass over dz for both transforms, 0 off */
 #define PIS_TUNE_WINO_VW 17      /* F(4x4) input / output transforms: 2 (default: half the registers, +2-11 % on the
                                     512^2-256^2 layers) or 4 channels per thread */
-#define PIS_TUNE_NKEYS 18
+#define PIS_TUNE_LOSS_ROWS 18     /* pis_loss_fwd with W % 4 == 0: 1 (default) one launch over whole-row bands, the
+                                    last block reducing the partials; 0 the tile kernel + finalize launch */
+#define PIS_TUNE_NKEYS 19
 #define PIS_DEBUG_NOLOAD (1 << 16)
 int pis_tune(int key, int value);
 /* Tooling (tools/bench_gemm.py): time one batched NT GEMM kernel variant in isolation,
@@ -218,6 +220,8 @@ typedef struct pis_loss_params {
  * counts: [B][3] = exact (I_hat, P_hat, T) of the thresholded prediction per sample.
  * scores: [B][2] = (Dice, IoU) per sample (src/metrics.py:67-70, src/evaluate.py:91-94). */
 #define PIS_LOSS_NTERMS 8
+/* ws: pis_loss_ws bytes; its first 16 bytes (a completion ticket) must be zero before the
+ * first call on a workspace — every call leaves them zero again. */
 size_t pis_loss_ws(int B, int H, int W);
 int pis_loss_fwd(const float* p, const float* t, int B, int H, int W, const pis_loss_params* prm,
                  float* out_terms, int* counts, float* scores, void* ws, size_t ws_bytes,
@@ -228,9 +232,6 @@ int pis_loss_bwd(const float* p, const float* t, int B, int H, int W, const pis_
                  const float* terms, const float* grad_out, float* dst, int flags,
                  pis_stream_t stream);
 
-/* Per-pixel PDE fields of src/pde.py (forward only; any output may be NULL):
- * lap = Lap(u) (:49-79), residual = D Lap(u) + u(1-u)(u-a) (:101-122),
- * gradmag2 = gx^2 + gy^2 (:147-178), all on reflect-padded stencils.           */
 /* Loss backward fused into the head backward (src/loss.py:114-162 + src/unet.py:210 out_conv +
  * sigmoid): dz = dL/du u (1 - u) per pixel from u (B,H,W), t, terms of pis_loss_fwd, then
  * dx = dz w (x > 0), dw = sum dz x, db = sum dz as pis_head_bwd. du_out (may be NULL) receives
@@ -241,8 +242,17 @@ int pis_head_loss_bwd(const float* x, int ldx, const float* w, const float* u, c
                       float* du_out, int B, int H, int W, int C, const pis_loss_params* prm,
                       const float* terms, const float* grad_out, float* dx, int lddx, float* dw,
                       float* db, int flags, void* ws, size_t ws_bytes, pis_stream_t stream);
+/* Per-pixel PDE fields of src/pde.py (any output may be NULL):
+ * lap = Lap(u) (:49-79), residual = D Lap(u) + u(1-u)(u-a) (:101-122),
+ * gradmag2 = gx^2 + gy^2 (:147-178), all on reflect-padded stencils.           */
 int pis_pde_fields(const float* u, int B, int H, int W, float D, float a, float* lap,
                    float* residual, float* gradmag2, pis_stream_t stream);
+/* Their adjoint: du = sum over the fields of (d field / du)^T g_field (any g may be NULL), so
+ * PDERegularization.compute_laplacian / reaction_term / compute_residual /
+ * compute_gradient_magnitude are differentiable as in the reference (src/pde.py:49-178). */
+int pis_pde_fields_bwd(const float* u, const float* g_lap, const float* g_residual,
+                       const float* g_gradmag2, int B, int H, int W, float D, float a, float* du,
+                       pis_stream_t stream);
 
 /* ---- decoupled AdamW over one flat parameter arena (src/train.py:658-662) ----
  * torch.optim.AdamW single-tensor semantics (torch/optim/adam.py):

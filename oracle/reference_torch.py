@@ -337,3 +337,80 @@ def train_step(m: UNetRef, opt, x, t, loss_kw: dict, drop_scales=None):
     terms["loss"].backward()
     opt.step()
     return p.detach(), {k: float(v) for k, v in terms.items()}
+
+
+# ---------------------------------------------------------------------------
+# Epoch loops — src/train.py:84-185 (train_epoch) and :188-286 (validate): loss terms
+# averaged over batches (via .item() per batch), Dice / IoU / boundary F1 averaged over
+# samples; validate's dice_score is the batch mean of the whole-batch thresholded Dice.
+# ``boundary_f1_batch`` is passed in (OpenCV, which the reference uses, is absent here).
+# ---------------------------------------------------------------------------
+
+
+def _components(p, t, loss_kw):
+    out = loss_terms(p, t, **loss_kw)
+    return {k: float(v) for k, v in out.items()}
+
+
+def train_epoch_ref(m: UNetRef, batches, opt, loss_kw: dict, drop_scales=None, boundary_f1_batch=None):
+    """src/train.py:84-185 with return_components=True, compute_metrics=True."""
+    m.train()
+    tot = {"loss": 0.0, "dice_loss": 0.0, "bce_loss": 0.0, "pde_loss": 0.0, "phase_field_loss": 0.0}
+    dice, iou, bf1 = [], [], []
+    for k, (x, t) in enumerate(batches):
+        opt.zero_grad()
+        p = m(x, None if drop_scales is None else drop_scales[k])
+        terms = loss_terms(p, t, **loss_kw)
+        with torch.no_grad():
+            c = {kk: float(v) for kk, v in terms.items()}
+            tot["dice_loss"] += c["dice_loss"]
+            tot["bce_loss"] += c["bce_loss"]
+            tot["pde_loss"] += c.get("pde_loss", 0.0)
+            tot["phase_field_loss"] += c.get("phase_field_loss", 0.0)
+            dice += dice_score_batch(p, t).tolist()
+            iou += iou_batch(p, t).tolist()
+            if boundary_f1_batch is not None:
+                bf1 += boundary_f1_batch(p.detach(), t).tolist()
+        terms["loss"].backward()
+        opt.step()
+        tot["loss"] += float(terms["loss"])
+    n = len(batches)
+    res = {"loss": tot["loss"] / n, "dice_loss": tot["dice_loss"] / n, "bce_loss": tot["bce_loss"] / n}
+    if loss_kw.get("rd_w", 0.0) > 0:
+        res["pde_loss"] = tot["pde_loss"] / n
+    if loss_kw.get("pf_w", 0.0) > 0:
+        res["phase_field_loss"] = tot["phase_field_loss"] / n
+    res["dice_score"] = float(sum(dice) / len(dice))
+    res["iou_score"] = float(sum(iou) / len(iou))
+    res["boundary_f1_score"] = float(sum(bf1) / len(bf1)) if bf1 else 0.0
+    return res
+
+
+@torch.no_grad()
+def validate_ref(m: UNetRef, batches, loss_kw: dict, boundary_f1_batch=None):
+    """src/train.py:188-286 with return_components=True, compute_metrics=True."""
+    m.eval()
+    tot = {"loss": 0.0, "dice_score": 0.0, "dice_loss": 0.0, "bce_loss": 0.0, "pde_loss": 0.0,
+           "phase_field_loss": 0.0}
+    iou, bf1 = [], []
+    for x, t in batches:
+        p = m(x)
+        c = _components(p, t, loss_kw)
+        tot["dice_score"] += float(dice_score(p, t))  # src/metrics.py:4-35, whole batch
+        for key in ("loss", "dice_loss", "bce_loss"):
+            tot[key] += c[key]
+        tot["pde_loss"] += c.get("pde_loss", 0.0)
+        tot["phase_field_loss"] += c.get("phase_field_loss", 0.0)
+        iou += iou_batch(p, t).tolist()
+        if boundary_f1_batch is not None:
+            bf1 += boundary_f1_batch(p, t).tolist()
+    n = len(batches)
+    res = {"loss": tot["loss"] / n, "dice_score": tot["dice_score"] / n, "dice_loss": tot["dice_loss"] / n,
+           "bce_loss": tot["bce_loss"] / n}
+    if loss_kw.get("rd_w", 0.0) > 0:
+        res["pde_loss"] = tot["pde_loss"] / n
+    if loss_kw.get("pf_w", 0.0) > 0:
+        res["phase_field_loss"] = tot["phase_field_loss"] / n
+    res["iou_score"] = float(sum(iou) / len(iou))
+    res["boundary_f1_score"] = float(sum(bf1) / len(bf1)) if bf1 else 0.0
+    return res

@@ -71,6 +71,7 @@ _SIGNATURES = {
     "pis_colsum_ws": ([L, I], c_size_t),
     "pis_colsum": ([P, I, L, I, P, I, P, Z, P], c_int),
     "pis_pde_fields": ([P, I, I, I, c_float, c_float, P, P, P, P], c_int),
+    "pis_pde_fields_bwd": ([P, P, P, P, I, I, I, c_float, c_float, P, P], c_int),
     "pis_synth_ws": ([I, I, I], c_size_t),
     "pis_synth_discs": ([P, P, I, ctypes.c_uint64, P, P, P, I, I, I, P, Z, P], c_int),
 }

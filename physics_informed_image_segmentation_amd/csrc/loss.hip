@@ -266,6 +266,217 @@ __global__ __launch_bounds__(256) void loss_finalize_kernel(LossArgs g, float* _
   }
 }
 
+// ---------------------------------------------------------------------------
+// Single-launch forward for W % 4 == 0 (the training shapes): a block owns `rows` whole
+// image rows of one sample (rows x W = ~4096 px, 16 per thread), so u needs a row halo only
+// (the left/right reflect ghosts are columns 1 and W-2 of the same staged rows) and every
+// HBM line of p and t is fetched once. Each block leaves its partial sums, then takes a
+// ticket (agent-scope acq_rel atomic); the block that takes the last ticket reduces all
+// partials in a fixed order (thread k sums blocks k, k+256, ... in double, then fixed
+// butterflies) — deterministic whichever block finishes last — writes terms / counts /
+// scores and resets the ticket to 0 for the next launch. No finalize launch.
+// ---------------------------------------------------------------------------
+struct LossRowArgs {
+  LossArgs g;
+  int rows;             // image rows per block
+  int bands;            // blocks per sample
+  unsigned* ticket;     // zero before the first launch on this workspace; left zero
+  float* terms;
+  int* counts;
+  float* scores;
+};
+
+__device__ __forceinline__ void loss_finalize_block(const LossArgs& g, int nblk, int bps, float* __restrict__ terms,
+                                                    int* __restrict__ counts, float* __restrict__ scores) {
+  double s[6] = {0, 0, 0, 0, 0, 0};
+  for (int k = threadIdx.x; k < nblk; k += blockDim.x)
+#pragma unroll
+    for (int j = 0; j < 6; ++j) s[j] += (double)g.fpart[k * 6 + j];
+  __shared__ double red[4][6];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int j = 0; j < 6; ++j) s[j] = wave_sum_d(s[j]);
+  if (lane == 0)
+#pragma unroll
+    for (int j = 0; j < 6; ++j) red[wave][j] = s[j];
+  for (int b = wave; b < g.B; b += 4) {  // per-sample counters: one wave per sample
+    long long ci = 0, cp = 0, ct = 0;
+    for (int k = lane; k < bps; k += 64) {
+      const int blk = b * bps + k;
+      ci += g.ipart[blk * 3 + 0];
+      cp += g.ipart[blk * 3 + 1];
+      ct += g.ipart[blk * 3 + 2];
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      ci += __shfl_xor(ci, off, 64);
+      cp += __shfl_xor(cp, off, 64);
+      ct += __shfl_xor(ct, off, 64);
+    }
+    if (lane == 0) {
+      if (counts) {
+        counts[b * 3 + 0] = (int)ci;
+        counts[b * 3 + 1] = (int)cp;
+        counts[b * 3 + 2] = (int)ct;
+      }
+      if (scores) {  // fp32 arithmetic exactly as the reference metric (src/metrics.py:67-70, evaluate.py:91-94)
+        const float fi = (float)ci, fp = (float)cp, ft = (float)ct, sm = g.smooth;
+        scores[b * 2 + 0] = (2.f * fi + sm) / (fp + ft + sm);
+        scores[b * 2 + 1] = (fi + sm) / (fp + ft - fi + sm);
+      }
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double tot[6];
+#pragma unroll
+    for (int j = 0; j < 6; ++j) tot[j] = ((red[0][j] + red[1][j]) + red[2][j]) + red[3][j];
+    const double n = (double)g.B * g.H * g.W;
+    const double I = tot[0], P = tot[1], T = tot[2];
+    const double dice = 1.0 - (2.0 * I + g.smooth) / (P + T + g.smooth);
+    const double bce = tot[3] / n, rd = tot[4] / n, pf = tot[5] / n;
+    double total = g.dice_w * dice + g.bce_w * bce;
+    if (g.rd_w > 0.f) total += g.rd_w * rd;
+    if (g.pf_w > 0.f) total += g.pf_w * pf;
+    terms[0] = (float)total;
+    terms[1] = (float)dice;
+    terms[2] = (float)bce;
+    terms[3] = (float)rd;
+    terms[4] = (float)pf;
+    terms[5] = (float)I;
+    terms[6] = (float)P;
+    terms[7] = (float)T;
+  }
+}
+
+template <bool RD, bool PF>
+__global__ __launch_bounds__(256) void loss_fwd_rows_kernel(LossRowArgs a) {
+  constexpr bool ST = RD || PF;
+  extern __shared__ __attribute__((aligned(16))) float su[];  // [rows + 2][W]: u rows y0-1 .. y0+nr
+  const LossArgs& g = a.g;
+  const int H = g.H, W = g.W, W4 = W >> 2;
+  const int band = blockIdx.x, b = blockIdx.y;
+  const int y0 = band * a.rows, nr = min(a.rows, H - y0);
+  const float* u = g.p + (size_t)b * H * W;
+  const float* tt = g.t + (size_t)b * H * W + (size_t)y0 * W;
+  const int items = nr * W4;  // float4 items of the block's interior
+  constexpr int MAXI = 4;     // rows * W / 4 <= 1024 (loss_rows): at most 4 per thread
+  f32x4 tvs[MAXI];
+#pragma unroll
+  for (int j = 0; j < MAXI; ++j) {
+    const int k = threadIdx.x + 256 * j;
+    if (k < items) tvs[j] = *(const f32x4*)(tt + 4 * (size_t)k);
+  }
+  f32x4 pin[MAXI];
+  if constexpr (ST) {
+    const int srows = nr + 2;
+    for (int k = threadIdx.x; k < srows * W4; k += 256) {
+      const int r = k / W4, q = k - r * W4;
+      const int gy = refl(y0 - 1 + r, H);
+      *(f32x4*)(su + r * W + 4 * q) = *(const f32x4*)(u + (size_t)gy * W + 4 * q);
+    }
+    __syncthreads();
+  } else {
+#pragma unroll
+    for (int j = 0; j < MAXI; ++j) {
+      const int k = threadIdx.x + 256 * j;
+      if (k < items) pin[j] = *(const f32x4*)(u + (size_t)y0 * W + 4 * (size_t)k);
+    }
+  }
+  constexpr float kLn2 = 0.69314718055994531f, kClamp2 = -144.26950408889634f;  // -100 / ln 2
+  float s_it = 0.f, s_p = 0.f, s_t = 0.f, s_bce2 = 0.f, s_rd = 0.f, s_g2 = 0.f, s_q2 = 0.f;
+  int c_i = 0, c_p = 0, c_t = 0;
+#pragma unroll
+  for (int j = 0; j < MAXI; ++j) {
+    const int k = threadIdx.x + 256 * j;
+    if (k >= items) continue;
+    const int r = k / W4, q = k - r * W4, xb = 4 * q;
+    const f32x4 tv = tvs[j];
+    f32x4 pv, uv, dv;
+    float lft = 0.f, rgt = 0.f;
+    if constexpr (ST) {
+      const float* row = su + (r + 1) * W;
+      pv = *(const f32x4*)(row + xb);
+      uv = *(const f32x4*)(row - W + xb);
+      dv = *(const f32x4*)(row + W + xb);
+      lft = row[xb == 0 ? 1 : xb - 1];               // reflect: ghost column -1 is column 1
+      rgt = row[xb + 4 == W ? W - 2 : xb + 4];       // ghost column W is column W-2
+    } else {
+      pv = pin[j];
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float p = pv[i], t = tv[i];
+      s_it = fmaf(p, t, s_it);
+      s_p += p;
+      s_t += t;
+      s_bce2 += (t - 1.f) * fmaxf(__builtin_amdgcn_logf(1.f - p), kClamp2) -
+                t * fmaxf(__builtin_amdgcn_logf(p), kClamp2);
+      const bool pb = p > g.thr, tb = t > 0.5f;
+      c_p += pb;
+      c_t += tb;
+      c_i += pb && tb;
+      if constexpr (ST) {
+        const float ul = i == 0 ? lft : pv[i - 1], ur = i == 3 ? rgt : pv[i + 1];
+        const float uu = uv[i], ud = dv[i];
+        const float qq = fmaf(-p, p, p);  // p (1 - p)
+        if (RD) {
+          const float lap = (uu + ud) + (ul + ur) - 4.f * p;
+          const float rr = fmaf(g.D, lap, g.rx * qq * (p - g.a));
+          s_rd = fmaf(rr, rr, s_rd);
+        }
+        if (PF) {
+          const float gx = ur - ul, gy = ud - uu;  // 2x the central differences
+          s_g2 = fmaf(gx, gx, fmaf(gy, gy, s_g2));
+          s_q2 = fmaf(qq, qq, s_q2);
+        }
+      }
+    }
+  }
+  float v[6] = {s_it, s_p, s_t, s_bce2 * kLn2, s_rd, 0.125f * g.eps * s_g2 + s_q2 / g.eps};
+  int c[3] = {c_i, c_p, c_t};
+  __shared__ float fr[4][6];
+  __shared__ int ir[4][3];
+  __shared__ int last;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int j = 0; j < 6; ++j) v[j] = wave_sum(v[j]);
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) c[j] += __shfl_xor(c[j], off, 64);
+  }
+  if (lane == 0) {
+#pragma unroll
+    for (int j = 0; j < 6; ++j) fr[wave][j] = v[j];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) ir[wave][j] = c[j];
+  }
+  __syncthreads();
+  const int blk = b * a.bands + band, nblk = g.B * a.bands;
+  if (threadIdx.x < 6) {
+    g.fpart[blk * 6 + threadIdx.x] = ((fr[0][threadIdx.x] + fr[1][threadIdx.x]) + fr[2][threadIdx.x]) + fr[3][threadIdx.x];
+  } else if (threadIdx.x < 9) {
+    const int j = threadIdx.x - 6;
+    g.ipart[blk * 3 + j] = ir[0][j] + ir[1][j] + ir[2][j] + ir[3][j];
+  }
+  __threadfence();  // the partials are visible device-wide before this block's ticket
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned prev = __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    last = prev == (unsigned)(nblk - 1);
+  }
+  __syncthreads();
+  if (!last) return;
+  __threadfence();  // acquire side for every wave of the last block
+  loss_finalize_block(g, nblk, a.bands, a.terms, a.counts, a.scores);
+  if (threadIdx.x == 0) __hip_atomic_store(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// rows per block of the single-launch forward: ~4096 pixels (16 per thread), <= 1024 float4
+static int loss_rows(int H, int W) { return std::max(1, std::min(H, 4096 / W)); }
+static bool loss_rows_ok(int H, int W) { return (W & 3) == 0 && W <= 4096 && H >= 2; }
+
 struct LossBwdArgs {
   const float* p;
   const float* t;
@@ -581,6 +792,54 @@ __global__ void pde_fields_kernel(const float* __restrict__ u0, int B, int H, in
   }
 }
 
+// Adjoint of pde_fields_kernel (src/pde.py:49-178 are differentiable in the reference): given
+// upstream gradients of the three fields (any may be NULL = zero),
+//   du = Lap*(g_lap + D g_res) + f'(u) g_res + sum_axis (G[k-1] - G[k+1]),  G = g_gm * (2 x the
+// central difference) / 2 per axis,
+// with Lap* the exact adjoint of the reflect-padded 5-point stencil (ghost row -1 = row 1 and
+// row n = row n-2, so rows/columns 1 and n-2 take the boundary value twice) and the reflect
+// central differences identically zero on the first/last row and column.
+__global__ void pde_fields_bwd_kernel(const float* __restrict__ u0, const float* __restrict__ gl0,
+                                      const float* __restrict__ gr0, const float* __restrict__ gg0, int B, int H,
+                                      int W, float D, float a, float* __restrict__ du) {
+  const int64_t HW = (int64_t)H * W, N = (int64_t)B * HW;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < N; e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t b = e / HW;
+    const int rem = (int)(e - b * HW), y = rem / W, x = rem - y * W;
+    const float* u = u0 + b * HW;
+    auto q = [&](int yy, int xx) -> float {  // Lap-adjoint input field, zero outside the image
+      if (yy < 0 || yy >= H || xx < 0 || xx >= W) return 0.f;
+      const int64_t o = b * HW + (int64_t)yy * W + xx;
+      return (gl0 ? gl0[o] : 0.f) + (gr0 ? D * gr0[o] : 0.f);
+    };
+    float g = 0.f;
+    if (gl0 || gr0) {
+      const float qu = q(y - 1, x), qd = q(y + 1, x), ql = q(y, x - 1), qr = q(y, x + 1);
+      g = (qu + qd) + (ql + qr) - 4.f * q(y, x);
+      g += (y == 1 ? qu : 0.f) + (y == H - 2 ? qd : 0.f);
+      g += (x == 1 ? ql : 0.f) + (x == W - 2 ? qr : 0.f);
+    }
+    if (gr0) {
+      const float c = u[rem];
+      g += gr0[e] * (c * (2.f * (1.f + a) - 3.f * c) - a);  // f'(u) = -3u^2 + 2(1+a)u - a
+    }
+    if (gg0) {
+      const float* gg = gg0 + b * HW;
+      auto gxw = [&](int yy, int xx) -> float {  // g_gm * gx at an interior column, else 0
+        if (yy < 0 || yy >= H || xx < 1 || xx > W - 2) return 0.f;
+        return gg[yy * W + xx] * (u[yy * W + xx + 1] - u[yy * W + xx - 1]);
+      };
+      auto gyw = [&](int yy, int xx) -> float {
+        if (xx < 0 || xx >= W || yy < 1 || yy > H - 2) return 0.f;
+        return gg[yy * W + xx] * (u[(yy + 1) * W + xx] - u[(yy - 1) * W + xx]);
+      };
+      // d(gx^2)/du[k] summed over the pixels whose difference touches k: 2 gx * (+-1/2) = +-gx
+      g += 0.5f * ((gxw(y, x - 1) - gxw(y, x + 1)) + (gyw(y - 1, x) - gyw(y + 1, x)));
+    }
+    du[e] = g;
+  }
+}
+
 static void loss_plan(int H, int W, int& tiles_x, int& tiles_y) {
   tiles_x = (W + LT_X - 1) / LT_X;
   tiles_y = (H + LT_Y - 1) / LT_Y;
@@ -590,10 +849,18 @@ static void loss_plan(int H, int W, int& tiles_x, int& tiles_y) {
 
 using namespace pis;
 
-extern "C" size_t pis_loss_ws(int B, int H, int W) {
+// workspace: [16 B ticket (zero-initialised by the caller once, left zero by every call)]
+// [fpart: nblk x 6 floats][ipart: nblk x 3 ints], nblk = the larger of the two plans
+static int64_t loss_nblk(int B, int H, int W) {
   int tx, ty;
   loss_plan(H, W, tx, ty);
-  return (size_t)B * tx * ty * (6 * sizeof(float) + 3 * sizeof(int)) + 256;
+  int64_t n = (int64_t)B * tx * ty;
+  if (loss_rows_ok(H, W)) n = std::max<int64_t>(n, (int64_t)B * cdiv(H, loss_rows(H, W)));
+  return n;
+}
+
+extern "C" size_t pis_loss_ws(int B, int H, int W) {
+  return 16 + (size_t)loss_nblk(B, H, W) * (6 * sizeof(float) + 3 * sizeof(int)) + 256;
 }
 
 extern "C" int pis_loss_fwd(const float* p, const float* t, int B, int H, int W,
@@ -607,12 +874,28 @@ extern "C" int pis_loss_fwd(const float* p, const float* t, int B, int H, int W,
   g.dice_w = prm->dice_w; g.bce_w = prm->bce_w; g.rd_w = prm->rd_w; g.pf_w = prm->pf_w;
   g.smooth = prm->smooth; g.D = prm->D; g.a = prm->a; g.eps = prm->eps;
   g.rx = (prm->flags & PIS_LOSS_NO_REACTION) ? 0.f : 1.f; g.thr = prm->thr;
-  loss_plan(H, W, g.tiles_x, g.tiles_y);
-  g.fpart = (float*)ws;
-  g.ipart = (int*)((char*)ws + (size_t)B * g.tiles_x * g.tiles_y * 6 * sizeof(float));
+  const int64_t nblk = loss_nblk(B, H, W);
+  g.fpart = (float*)((char*)ws + 16);
+  g.ipart = (int*)((char*)ws + 16 + (size_t)nblk * 6 * sizeof(float));
   const bool all = prm->flags & PIS_LOSS_ALL_TERMS;
   const bool rd = all || prm->rd_w > 0.f, pf = all || prm->pf_w > 0.f;
   hipStream_t s = (hipStream_t)stream;
+  if (loss_rows_ok(H, W) && tune_get(PIS_TUNE_LOSS_ROWS) != 0) {
+    LossRowArgs a{};
+    a.g = g;
+    a.rows = loss_rows(H, W);
+    a.bands = (int)cdiv(H, a.rows);
+    a.ticket = (unsigned*)ws;
+    a.terms = out_terms; a.counts = counts; a.scores = scores;
+    const dim3 grid(a.bands, B);
+    const size_t smem = (rd || pf) ? (size_t)(a.rows + 2) * W * sizeof(float) : 0;
+    if (rd && pf) hipLaunchKernelGGL((loss_fwd_rows_kernel<true, true>), grid, dim3(256), smem, s, a);
+    else if (rd) hipLaunchKernelGGL((loss_fwd_rows_kernel<true, false>), grid, dim3(256), smem, s, a);
+    else if (pf) hipLaunchKernelGGL((loss_fwd_rows_kernel<false, true>), grid, dim3(256), smem, s, a);
+    else hipLaunchKernelGGL((loss_fwd_rows_kernel<false, false>), grid, dim3(256), smem, s, a);
+    return launch_status("loss_fwd_rows");
+  }
+  loss_plan(H, W, g.tiles_x, g.tiles_y);
   const dim3 grid(g.tiles_x, g.tiles_y, B);
   if (rd && pf) hipLaunchKernelGGL((loss_fwd_kernel<true, true>), grid, dim3(256), 0, s, g);
   else if (rd) hipLaunchKernelGGL((loss_fwd_kernel<true, false>), grid, dim3(256), 0, s, g);
@@ -655,6 +938,17 @@ extern "C" int pis_pde_fields(const float* u, int B, int H, int W, float D, floa
   hipLaunchKernelGGL(pde_fields_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, u, B, H, W,
                      D, a, lap, residual, gradmag2);
   return launch_status("pde_fields");
+}
+
+extern "C" int pis_pde_fields_bwd(const float* u, const float* g_lap, const float* g_residual,
+                                  const float* g_gradmag2, int B, int H, int W, float D, float a, float* du,
+                                  pis_stream_t stream) {
+  PIS_CHECK_ARG(u && du && B > 0 && H >= 2 && W >= 2, "pis_pde_fields_bwd: bad arguments");
+  const int64_t n = (int64_t)B * H * W;
+  const int grid = (int)std::min<int64_t>(cdiv(n, 256), 8192);
+  hipLaunchKernelGGL(pde_fields_bwd_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, u, g_lap, g_residual,
+                     g_gradmag2, B, H, W, D, a, du);
+  return launch_status("pde_fields_bwd");
 }
 
 static int head_loss_rows(int H, int W) { return std::max(1, std::min(H, 1024 / std::max(1, W))); }

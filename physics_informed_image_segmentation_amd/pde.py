@@ -3,10 +3,11 @@
 ``PDERegularization`` keeps the reference's constructor checks, buffers and
 method names (src/pde.py:6-212). The two losses the training step uses,
 ``compute_loss`` (reaction-diffusion residual, :124-145) and
-``compute_phase_field_loss`` (:180-212), are the fused HIP kernel and are
-differentiable. The per-pixel field helpers (``compute_laplacian``,
-``reaction_term``, ``compute_residual``, ``compute_gradient_magnitude``)
-return detached fields from one HIP stencil kernel (inspection/plotting).
+``compute_phase_field_loss`` (:180-212), are the fused HIP kernel. The
+per-pixel field helpers (``compute_laplacian``, ``reaction_term``,
+``compute_residual``, ``compute_gradient_magnitude``, :49-178) are one HIP
+stencil kernel each way (``pis_pde_fields`` / ``pis_pde_fields_bwd``) and are
+differentiable, like the reference's F.pad + F.conv2d compositions.
 """
 from __future__ import annotations
 
@@ -15,6 +16,41 @@ import torch.nn as nn
 
 from . import _hip
 from .fused import LossConfig, fused_loss
+
+_LAP, _RES, _GM = 0, 1, 2
+
+
+class _PDEField(torch.autograd.Function):
+    """One reflect-padded stencil field of u and its exact adjoint."""
+
+    @staticmethod
+    def forward(ctx, u, which: int, D: float, a: float):
+        _hip.require_cuda(u, "PDERegularization")
+        if u.dtype != torch.float32:
+            raise TypeError("PDERegularization: float32 input expected")
+        uc = u.detach().contiguous()
+        B, H, W = uc.shape[0], uc.shape[-2], uc.shape[-1]
+        if uc.numel() != B * H * W:
+            raise ValueError(f"single-channel maps expected, got {tuple(u.shape)}")
+        out = torch.empty_like(uc)
+        ptrs = [0, 0, 0]
+        ptrs[which] = out.data_ptr()
+        _hip.call("pis_pde_fields", uc.data_ptr(), B, H, W, float(D), float(a), *ptrs, _hip.stream_handle())
+        ctx.save_for_backward(uc)
+        ctx.which, ctx.D, ctx.a = which, float(D), float(a)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        (u,) = ctx.saved_tensors
+        B, H, W = u.shape[0], u.shape[-2], u.shape[-1]
+        g = g.to(torch.float32).contiguous()
+        ptrs = [0, 0, 0]
+        ptrs[ctx.which] = g.data_ptr()
+        du = torch.empty_like(u)
+        _hip.call("pis_pde_fields_bwd", u.data_ptr(), *ptrs, B, H, W, ctx.D, ctx.a, du.data_ptr(),
+                  _hip.stream_handle())
+        return du, None, None, None
 
 
 class PDERegularization(nn.Module):
@@ -34,28 +70,22 @@ class PDERegularization(nn.Module):
         self.register_buffer("grad_x_kernel", gx[None, None].clone())
         self.register_buffer("grad_y_kernel", gx.t()[None, None].contiguous())
 
-    # ---- per-pixel fields (forward only) -------------------------------------
-    def _fields(self, u: torch.Tensor, lap=False, res=False, gm=False, D=None):
-        _hip.require_cuda(u, "PDERegularization")
-        u = u.detach().to(torch.float32).contiguous()
-        B, H, W = u.shape[0], u.shape[-2], u.shape[-1]
-        outs = [torch.empty_like(u) if f else None for f in (lap, res, gm)]
-        _hip.call("pis_pde_fields", u.data_ptr(), B, H, W, float(self.diffusion_coeff if D is None else D),
-                  float(self.reaction_threshold), _hip.ptr(outs[0]), _hip.ptr(outs[1]), _hip.ptr(outs[2]),
-                  _hip.stream_handle())
-        return outs
-
+    # ---- per-pixel fields (differentiable) ----------------------------------------
     def compute_laplacian(self, u: torch.Tensor) -> torch.Tensor:
-        return self._fields(u, lap=True)[0]
+        """5-point Laplacian with reflect padding (src/pde.py:49-79)."""
+        return _PDEField.apply(u, _LAP, 0.0, 0.0)
 
     def reaction_term(self, u: torch.Tensor) -> torch.Tensor:
-        return self._fields(u, res=True, D=0.0)[1]  # residual with D = 0 is exactly f(u)
+        """u (1 - u) (u - a) (src/pde.py:81-99): the residual with D = 0."""
+        return _PDEField.apply(u, _RES, 0.0, self.reaction_threshold)
 
     def compute_residual(self, u: torch.Tensor) -> torch.Tensor:
-        return self._fields(u, res=True)[1]
+        """D Lap(u) + u (1 - u) (u - a) (src/pde.py:101-122)."""
+        return _PDEField.apply(u, _RES, self.diffusion_coeff, self.reaction_threshold)
 
     def compute_gradient_magnitude(self, u: torch.Tensor) -> torch.Tensor:
-        return self._fields(u, gm=True)[2]
+        """gx^2 + gy^2 of the reflect-padded central differences (src/pde.py:147-178)."""
+        return _PDEField.apply(u, _GM, 0.0, 0.0)
 
     # ---- losses (fused kernel, differentiable) ----------------------------------
     def compute_loss(self, u: torch.Tensor) -> torch.Tensor:

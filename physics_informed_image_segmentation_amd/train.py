@@ -159,13 +159,14 @@ class _BoundaryF1Async:
         from concurrent.futures import ThreadPoolExecutor
         n = workers or max(1, min(8, len(os.sched_getaffinity(0)) - 1))
         self.pool = ThreadPoolExecutor(max_workers=n)
-        self.copy = torch.cuda.Stream(device=device)
+        self.cuda = torch.device(device).type == "cuda"  # host tensors (tests): no streams
+        self.copy = torch.cuda.Stream(device=device) if self.cuda else None
         self.fence: Optional[torch.cuda.Event] = None
         self.futures = []
         self.free = []  # pinned host buffers ready for reuse
 
     def before_forward(self):
-        if self.fence is not None:
+        if self.cuda and self.fence is not None:
             torch.cuda.current_stream().wait_event(self.fence)
             self.fence = None
 
@@ -178,6 +179,11 @@ class _BoundaryF1Async:
 
     def submit(self, outputs: torch.Tensor, masks: torch.Tensor):
         B, H, W = outputs.shape[0], outputs.shape[-2], outputs.shape[-1]
+        if not self.cuda:
+            hp = outputs.detach().reshape(B, H, W).float().clone()
+            ht = masks.detach().reshape(B, H, W).float().clone()
+            self.futures.append(self.pool.submit(self._score, None, hp, ht))
+            return
         hp, ht = self._pinned((B, H, W))
         ready = torch.cuda.Event()
         ready.record(torch.cuda.current_stream())
@@ -193,11 +199,13 @@ class _BoundaryF1Async:
 
     def _score(self, done, hp, ht) -> Tuple[float, int]:
         from .evaluate import _boundary_f1_np, extract_boundaries
-        done.synchronize()
+        if done is not None:
+            done.synchronize()
         p, t = hp.numpy() > 0.5, ht.numpy()
         tot = sum(_boundary_f1_np(extract_boundaries(p[i]), extract_boundaries(t[i]), 2, 1e-6)
                   for i in range(p.shape[0]))
-        self.free.append((hp, ht))
+        if done is not None:
+            self.free.append((hp, ht))
         return tot, p.shape[0]
 
     def collect(self) -> float:

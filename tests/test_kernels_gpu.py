@@ -347,7 +347,7 @@ def test_head_loss_bwd_fused(hip, B, H, W, ldx, kw):
     prm = LossParams(0.5, 0.5, kw.get("rd_w", 0.0), kw.get("pf_w", 0.0), 1e-6, kw.get("D", 1.0), kw.get("a", 0.5),
                      kw.get("eps", 0.05), 0.5, 0)
     terms = torch.empty(8, device="cuda")
-    lws = torch.empty(hip.pis_loss_ws(B, H, W) // 4 + 1, device="cuda")
+    lws = torch.zeros(hip.pis_loss_ws(B, H, W) // 4 + 1, device="cuda")
     assert hip.pis_loss_fwd(u.data_ptr(), t.data_ptr(), B, H, W, ctypes.byref(prm), terms.data_ptr(), 0, 0,
                             lws.data_ptr(), lws.numel() * 4, s()) == 0
     go = torch.tensor([0.75], device="cuda")
@@ -378,7 +378,7 @@ def test_head_loss_bwd_fused(hip, B, H, W, ldx, kw):
     assert rel_err(db.cpu(), (db_ref + 1).cpu()) < 1e-6
 
 
-def _loss_call(hip, p, t, kw, chain=False, grad_out=None):
+def _loss_call(hip, p, t, kw, chain=False, grad_out=None, ws=None):
     from physics_informed_image_segmentation_amd._hip import LossParams
     import ctypes
     B, H, W = p.shape[0], p.shape[-2], p.shape[-1]
@@ -389,7 +389,8 @@ def _loss_call(hip, p, t, kw, chain=False, grad_out=None):
     counts = torch.empty(B, 3, dtype=torch.int32, device="cuda")
     scores = torch.empty(B, 2, device="cuda")
     nws = hip.pis_loss_ws(B, H, W)
-    ws = torch.empty(nws // 4 + 1, device="cuda")
+    if ws is None:
+        ws = torch.zeros(nws // 4 + 1, device="cuda")  # completion ticket starts at zero
     assert hip.pis_loss_fwd(pd.data_ptr(), td.data_ptr(), B, H, W, ctypes.byref(prm), terms.data_ptr(),
                             counts.data_ptr(), scores.data_ptr(), ws.data_ptr(), nws, s()) == 0
     dst = torch.empty(B, H, W, device="cuda")
@@ -424,6 +425,35 @@ def test_fused_loss_vs_oracle(hip, shape, kw):
     assert np.array_equal(counts.numpy(), np.stack([i, ph, ts], 1))
     d, u = ln.dice_iou_from_counts(i, ph, ts)
     np.testing.assert_allclose(scores.numpy(), np.stack([d, u], 1), rtol=1e-6)
+
+
+@pytest.mark.parametrize("shape", [(16, 512, 512), (3, 130, 68), (2, 2, 8), (1, 37, 1024), (5, 64, 4096)])
+def test_loss_fwd_single_launch_matches_tile_path(hip, shape):
+    """The whole-row single-launch forward (last block finalises, PIS_TUNE_LOSS_ROWS = 1) and the
+    tile kernel + finalize launch give the same terms and exactly the same counters; the completion
+    ticket is left at zero, so repeated launches on one workspace keep agreeing."""
+    g = torch.Generator().manual_seed(12)
+    p = 0.02 + 0.96 * torch.rand(shape, generator=g)
+    t = (torch.rand(shape, generator=g) > 0.8).float()
+    kw = dict(rd_w=1e-4, pf_w=1e-4, D=5.0, a=0.5, eps=0.05)
+    prev = hip.pis_tune(18, 0)
+    try:
+        ref = _loss_call(hip, p, t, kw)
+    finally:
+        hip.pis_tune(18, prev)
+    assert hip.pis_tune(18, -1) == 1
+    ws = torch.zeros(hip.pis_loss_ws(*shape) // 4 + 1, device="cuda")
+    first = None
+    for _ in range(3):  # one workspace: each launch must leave the ticket at zero for the next
+        got = _loss_call(hip, p, t, kw, ws=ws)
+        np.testing.assert_allclose(got[0].numpy(), ref[0].numpy(), rtol=2e-6, atol=1e-12)
+        assert torch.equal(got[1], ref[1])
+        assert torch.equal(got[2], ref[2])
+        np.testing.assert_allclose(got[3].numpy(), ref[3].numpy(), rtol=1e-5, atol=1e-12)
+        if first is not None:
+            assert torch.equal(got[0], first)  # deterministic: fixed-order reduction
+        first = got[0]
+    assert ws[:4].abs().sum().item() == 0
 
 
 def test_fused_loss_chain_sigmoid(hip):
@@ -732,3 +762,30 @@ def test_conv3x3_fwd_pool(hip, B, H, W, Cin, Cout, keep):
     assert rel_err(nchw(y[..., :Cout].cpu()), y_ref) < 1e-5
     assert torch.all(y[..., Cout:] == 7.0)
     assert rel_err(nchw(pool.cpu()), p_ref) < 1e-5
+
+
+@pytest.mark.parametrize("shape", [(2, 1, 9, 11), (1, 1, 2, 3), (3, 1, 64, 48)])
+def test_pde_fields_and_their_gradients(hip, shape):
+    """PDERegularization's per-pixel fields (pis_pde_fields) equal the oracle's reflect-pad +
+    conv2d stencils (src/pde.py:49-178), and their gradients (pis_pde_fields_bwd) equal float64
+    autograd through the oracle for an arbitrary upstream gradient — odd sizes and the 2-pixel
+    minimum exercise every reflect fold."""
+    from physics_informed_image_segmentation_amd.pde import PDERegularization
+    g = torch.Generator().manual_seed(14)
+    u = torch.rand(shape, generator=g) * 0.9 + 0.05
+    up = torch.randn(shape, generator=g)
+    reg = PDERegularization(diffusion_coeff=5.0, reaction_threshold=0.3)
+    u64 = u.double().requires_grad_(True)
+    refs = {"compute_laplacian": rt.laplacian(u64), "reaction_term": rt.reaction(u64, 0.3),
+            "compute_residual": rt.rd_residual(u64, 5.0, 0.3), "compute_gradient_magnitude": rt.grad_mag_sq(u64)}
+    for name, ref in refs.items():
+        ud = u.cuda().requires_grad_(True)
+        f = getattr(reg, name)(ud)
+        assert f.shape == u.shape
+        (f * up.cuda()).sum().backward()
+        (gref,) = torch.autograd.grad((ref * up.double()).sum(), u64)
+        fa = f.detach().cpu().double()
+        assert (fa - ref.detach()).abs().max().item() <= 1e-5 * max(1.0, ref.abs().max().item()), name
+        ga = ud.grad.cpu().double()
+        assert ((ga - gref).norm() / gref.norm()).item() < 1e-6, name
+        assert (ga - gref).abs().max().item() <= 1e-5 * gref.abs().max().item(), name

@@ -37,7 +37,7 @@ def main():
     counts = torch.empty(B, 3, dtype=torch.int32, device="cuda")
     scores = torch.empty(B, 2, device="cuda")
     nws = lib.pis_loss_ws(B, H, W)
-    ws = torch.empty(nws // 4 + 1, device="cuda")
+    ws = torch.zeros(nws // 4 + 1, device="cuda")
     dst = torch.empty(B, H, W, device="cuda")
     flush = torch.empty(512 * 1024 * 1024 // 4, device="cuda")  # 512 MB: evict L2 + MALL between reps
 
