@@ -373,7 +373,7 @@ def train_epoch_ref(m: UNetRef, batches, opt, loss_kw: dict, drop_scales=None, b
                 bf1 += boundary_f1_batch(p.detach(), t).tolist()
         terms["loss"].backward()
         opt.step()
-        tot["loss"] += float(terms["loss"])
+        tot["loss"] += float(terms["loss"].detach())
     n = len(batches)
     res = {"loss": tot["loss"] / n, "dice_loss": tot["dice_loss"] / n, "bce_loss": tot["bce_loss"] / n}
     if loss_kw.get("rd_w", 0.0) > 0:

@@ -360,7 +360,7 @@ __global__ __launch_bounds__(256) void loss_fwd_rows_kernel(LossRowArgs a) {
   const float* u = g.p + (size_t)b * H * W;
   const float* tt = g.t + (size_t)b * H * W + (size_t)y0 * W;
   const int items = nr * W4;  // float4 items of the block's interior
-  constexpr int MAXI = 4;     // rows * W / 4 <= 1024 (loss_rows): at most 4 per thread
+  constexpr int MAXI = 8;     // rows * W / 4 <= 2048 (loss_rows): at most 8 per thread
   f32x4 tvs[MAXI];
 #pragma unroll
   for (int j = 0; j < MAXI; ++j) {
@@ -454,28 +454,36 @@ __global__ __launch_bounds__(256) void loss_fwd_rows_kernel(LossRowArgs a) {
   }
   __syncthreads();
   const int blk = b * a.bands + band, nblk = g.B * a.bands;
+  // hand-off of the partials to the last block (cdna_hip_programming.md Guideline 16, the split-K
+  // counter form): plain stores -> the storing wave drains -> barrier -> ONE lane: agent release
+  // fence, drain, relaxed ticket add; the last arriver: ONE agent acquire, drain, barrier, loads
   if (threadIdx.x < 6) {
     g.fpart[blk * 6 + threadIdx.x] = ((fr[0][threadIdx.x] + fr[1][threadIdx.x]) + fr[2][threadIdx.x]) + fr[3][threadIdx.x];
   } else if (threadIdx.x < 9) {
     const int j = threadIdx.x - 6;
     g.ipart[blk * 3 + j] = ir[0][j] + ir[1][j] + ir[2][j] + ir[3][j];
   }
-  __threadfence();  // the partials are visible device-wide before this block's ticket
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
-    const unsigned prev = __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // keep the write-back ahead of the ticket
+    const unsigned prev = __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     last = prev == (unsigned)(nblk - 1);
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
   }
   __syncthreads();
   if (!last) return;
-  __threadfence();  // acquire side for every wave of the last block
   loss_finalize_block(g, nblk, a.bands, a.terms, a.counts, a.scores);
   if (threadIdx.x == 0) __hip_atomic_store(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// rows per block of the single-launch forward: ~4096 pixels (16 per thread), <= 1024 float4
-static int loss_rows(int H, int W) { return std::max(1, std::min(H, 4096 / W)); }
-static bool loss_rows_ok(int H, int W) { return (W & 3) == 0 && W <= 4096 && H >= 2; }
+// rows per block of the single-launch forward: ~8192 pixels (32 per thread), <= 2048 float4
+static int loss_rows(int H, int W) { return std::max(1, std::min(H, 8192 / W)); }
+static bool loss_rows_ok(int H, int W) { return (W & 3) == 0 && W <= 8192 && H >= 2; }
 
 struct LossBwdArgs {
   const float* p;

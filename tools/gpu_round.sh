@@ -28,7 +28,7 @@ step() {  # step NAME SECONDS cmd...
 }
 
 if [ "$MODE" = tests ]; then
-  step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread
+  step pytest_gpu 1200 python -u -m pytest tests -m gpu -v --timeout 400 --timeout-method thread
 fi
 if [ "$BENCH" = bench ]; then
   step bench 400 python -u bench.py
