@@ -82,8 +82,8 @@ int pis_version(void);
 #define PIS_TUNE_WINO_DZ2 16     /* pis_conv3x3_bwd_prep: 1 (default) one pass over dz for both transforms, 0 off */
 #define PIS_TUNE_WINO_VW 17      /* F(4x4) input / output transforms: 2 (default: half the registers, +2-11 % on the
                                     512^2-256^2 layers) or 4 channels per thread */
-#define PIS_TUNE_LOSS_ROWS 18     /* pis_loss_fwd with W % 4 == 0: 1 (default) one launch over whole-row bands, the
-                                    last block reducing the partials; 0 the tile kernel + finalize launch */
+#define PIS_TUNE_LOSS_ROWS 18     /* pis_loss_fwd with W % 4 == 0: 1 (default) whole-row bands (no column halo),
+                                    0 16x128 tiles; both followed by the one-block fixed-order finalize */
 #define PIS_TUNE_NKEYS 19
 #define PIS_DEBUG_NOLOAD (1 << 16)
 int pis_tune(int key, int value);
@@ -220,8 +220,6 @@ typedef struct pis_loss_params {
  * counts: [B][3] = exact (I_hat, P_hat, T) of the thresholded prediction per sample.
  * scores: [B][2] = (Dice, IoU) per sample (src/metrics.py:67-70, src/evaluate.py:91-94). */
 #define PIS_LOSS_NTERMS 8
-/* ws: pis_loss_ws bytes; its first 16 bytes (a completion ticket) must be zero before the
- * first call on a workspace — every call leaves them zero again. */
 size_t pis_loss_ws(int B, int H, int W);
 int pis_loss_fwd(const float* p, const float* t, int B, int H, int W, const pis_loss_params* prm,
                  float* out_terms, int* counts, float* scores, void* ws, size_t ws_bytes,

@@ -267,20 +267,17 @@ __global__ __launch_bounds__(256) void loss_finalize_kernel(LossArgs g, float* _
 }
 
 // ---------------------------------------------------------------------------
-// Single-launch forward for W % 4 == 0 (the training shapes): a block owns `rows` whole
-// image rows of one sample (rows x W = ~4096 px, 16 per thread), so u needs a row halo only
-// (the left/right reflect ghosts are columns 1 and W-2 of the same staged rows) and every
-// HBM line of p and t is fetched once. Each block leaves its partial sums, then takes a
-// ticket (agent-scope acq_rel atomic); the block that takes the last ticket reduces all
-// partials in a fixed order (thread k sums blocks k, k+256, ... in double, then fixed
-// butterflies) — deterministic whichever block finishes last — writes terms / counts /
-// scores and resets the ticket to 0 for the next launch. No finalize launch.
+// Forward for W % 4 == 0 (the training shapes): a block owns `rows` whole image rows of one
+// sample (rows x W = ~8192 px, 32 per thread), so u needs a row halo only (the left/right
+// reflect ghosts are columns 1 and W-2 of the same staged rows: no scattered column-halo
+// loads) and every HBM line of p and t is fetched once; one block per CU at C2. A one-block
+// finalize launch then reduces the per-block partials in a fixed order (thread k sums blocks
+// k, k+256, ... in double, then fixed butterflies): deterministic.
 // ---------------------------------------------------------------------------
 struct LossRowArgs {
   LossArgs g;
   int rows;             // image rows per block
   int bands;            // blocks per sample
-  unsigned* ticket;     // zero before the first launch on this workspace; left zero
   float* terms;
   int* counts;
   float* scores;
@@ -437,7 +434,6 @@ __global__ __launch_bounds__(256) void loss_fwd_rows_kernel(LossRowArgs a) {
   int c[3] = {c_i, c_p, c_t};
   __shared__ float fr[4][6];
   __shared__ int ir[4][3];
-  __shared__ int last;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
   for (int j = 0; j < 6; ++j) v[j] = wave_sum(v[j]);
@@ -453,35 +449,23 @@ __global__ __launch_bounds__(256) void loss_fwd_rows_kernel(LossRowArgs a) {
     for (int j = 0; j < 3; ++j) ir[wave][j] = c[j];
   }
   __syncthreads();
-  const int blk = b * a.bands + band, nblk = g.B * a.bands;
-  // hand-off of the partials to the last block (cdna_hip_programming.md Guideline 16, the split-K
-  // counter form): plain stores -> the storing wave drains -> barrier -> ONE lane: agent release
-  // fence, drain, relaxed ticket add; the last arriver: ONE agent acquire, drain, barrier, loads
+  const int blk = b * a.bands + band;
   if (threadIdx.x < 6) {
     g.fpart[blk * 6 + threadIdx.x] = ((fr[0][threadIdx.x] + fr[1][threadIdx.x]) + fr[2][threadIdx.x]) + fr[3][threadIdx.x];
   } else if (threadIdx.x < 9) {
     const int j = threadIdx.x - 6;
     g.ipart[blk * 3 + j] = ir[0][j] + ir[1][j] + ir[2][j] + ir[3][j];
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // keep the write-back ahead of the ticket
-    const unsigned prev = __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    last = prev == (unsigned)(nblk - 1);
-    if (last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-  }
-  __syncthreads();
-  if (!last) return;
-  loss_finalize_block(g, nblk, a.bands, a.terms, a.counts, a.scores);
-  if (threadIdx.x == 0) __hip_atomic_store(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// rows per block of the single-launch forward: ~8192 pixels (32 per thread), <= 2048 float4
+// the fixed-order reduction of the row kernel's partials (one block; launch boundary = hand-off:
+// an in-kernel last-arriver hand-off costs one agent-scope L2 write-back per block, measured
+// 24 us vs 12 us at C2)
+__global__ __launch_bounds__(256) void loss_finalize_rows_kernel(LossRowArgs a) {
+  loss_finalize_block(a.g, a.g.B * a.bands, a.bands, a.terms, a.counts, a.scores);
+}
+
+// rows per block of the whole-row forward: ~8192 pixels (32 per thread), <= 2048 float4
 static int loss_rows(int H, int W) { return std::max(1, std::min(H, 8192 / W)); }
 static bool loss_rows_ok(int H, int W) { return (W & 3) == 0 && W <= 8192 && H >= 2; }
 
@@ -857,8 +841,8 @@ static void loss_plan(int H, int W, int& tiles_x, int& tiles_y) {
 
 using namespace pis;
 
-// workspace: [16 B ticket (zero-initialised by the caller once, left zero by every call)]
-// [fpart: nblk x 6 floats][ipart: nblk x 3 ints], nblk = the larger of the two plans
+// workspace: [16 B reserved][fpart: nblk x 6 floats][ipart: nblk x 3 ints], nblk = the larger
+// of the two plans
 static int64_t loss_nblk(int B, int H, int W) {
   int tx, ty;
   loss_plan(H, W, tx, ty);
@@ -893,7 +877,6 @@ extern "C" int pis_loss_fwd(const float* p, const float* t, int B, int H, int W,
     a.g = g;
     a.rows = loss_rows(H, W);
     a.bands = (int)cdiv(H, a.rows);
-    a.ticket = (unsigned*)ws;
     a.terms = out_terms; a.counts = counts; a.scores = scores;
     const dim3 grid(a.bands, B);
     const size_t smem = (rd || pf) ? (size_t)(a.rows + 2) * W * sizeof(float) : 0;
@@ -901,7 +884,10 @@ extern "C" int pis_loss_fwd(const float* p, const float* t, int B, int H, int W,
     else if (rd) hipLaunchKernelGGL((loss_fwd_rows_kernel<true, false>), grid, dim3(256), smem, s, a);
     else if (pf) hipLaunchKernelGGL((loss_fwd_rows_kernel<false, true>), grid, dim3(256), smem, s, a);
     else hipLaunchKernelGGL((loss_fwd_rows_kernel<false, false>), grid, dim3(256), smem, s, a);
-    return launch_status("loss_fwd_rows");
+    const int rc = launch_status("loss_fwd_rows");
+    if (rc) return rc;
+    hipLaunchKernelGGL(loss_finalize_rows_kernel, dim3(1), dim3(256), 0, s, a);
+    return launch_status("loss_finalize");
   }
   loss_plan(H, W, g.tiles_x, g.tiles_y);
   const dim3 grid(g.tiles_x, g.tiles_y, B);

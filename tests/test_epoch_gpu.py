@@ -70,7 +70,7 @@ def test_train_epoch_matches_reference_loop(hip):
     # after the epoch both models hold the same weights (three AdamW steps)
     for (n, p), q in zip(net.named_parameters(), ref.parameters()):
         err = ((p.detach().cpu() - q.detach()).norm() / q.detach().norm()).item()
-        assert err < 1e-5, (n, err)
+        assert err < TOL_W, (n, err)
 
 
 def test_validate_matches_reference_loop(hip):

@@ -82,7 +82,7 @@ def test_loss_golden_hip(hip, config):
         counts = torch.empty(B, 3, dtype=torch.int32, device="cuda")
         scores = torch.empty(B, 2, device="cuda")
         nws = hip.pis_loss_ws(B, H, W)
-        ws = torch.zeros(nws // 4 + 1, device="cuda")  # completion ticket starts at zero
+        ws = torch.zeros(nws // 4 + 1, device="cuda")
         assert hip.pis_loss_fwd(p.data_ptr(), t.data_ptr(), B, H, W, ctypes.byref(prm), terms.data_ptr(),
                                 counts.data_ptr(), scores.data_ptr(), ws.data_ptr(), nws, st) == 0
         dp = torch.empty(B, H, W, device="cuda")

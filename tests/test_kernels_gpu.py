@@ -390,7 +390,7 @@ def _loss_call(hip, p, t, kw, chain=False, grad_out=None, ws=None):
     scores = torch.empty(B, 2, device="cuda")
     nws = hip.pis_loss_ws(B, H, W)
     if ws is None:
-        ws = torch.zeros(nws // 4 + 1, device="cuda")  # completion ticket starts at zero
+        ws = torch.zeros(nws // 4 + 1, device="cuda")
     assert hip.pis_loss_fwd(pd.data_ptr(), td.data_ptr(), B, H, W, ctypes.byref(prm), terms.data_ptr(),
                             counts.data_ptr(), scores.data_ptr(), ws.data_ptr(), nws, s()) == 0
     dst = torch.empty(B, H, W, device="cuda")
@@ -428,10 +428,10 @@ def test_fused_loss_vs_oracle(hip, shape, kw):
 
 
 @pytest.mark.parametrize("shape", [(16, 512, 512), (3, 130, 68), (2, 2, 8), (1, 37, 1024), (5, 64, 4096)])
-def test_loss_fwd_single_launch_matches_tile_path(hip, shape):
-    """The whole-row single-launch forward (last block finalises, PIS_TUNE_LOSS_ROWS = 1) and the
-    tile kernel + finalize launch give the same terms and exactly the same counters; the completion
-    ticket is left at zero, so repeated launches on one workspace keep agreeing."""
+def test_loss_fwd_row_bands_match_tile_path(hip, shape):
+    """The whole-row forward (PIS_TUNE_LOSS_ROWS = 1) and the 16x128-tile forward give the same
+    terms and exactly the same counters; repeated launches on one workspace are bitwise identical
+    (fixed-order reductions)."""
     g = torch.Generator().manual_seed(12)
     p = 0.02 + 0.96 * torch.rand(shape, generator=g)
     t = (torch.rand(shape, generator=g) > 0.8).float()
@@ -444,7 +444,7 @@ def test_loss_fwd_single_launch_matches_tile_path(hip, shape):
     assert hip.pis_tune(18, -1) == 1
     ws = torch.zeros(hip.pis_loss_ws(*shape) // 4 + 1, device="cuda")
     first = None
-    for _ in range(3):  # one workspace: each launch must leave the ticket at zero for the next
+    for _ in range(3):  # one workspace, reused
         got = _loss_call(hip, p, t, kw, ws=ws)
         np.testing.assert_allclose(got[0].numpy(), ref[0].numpy(), rtol=2e-6, atol=1e-12)
         assert torch.equal(got[1], ref[1])
@@ -453,7 +453,6 @@ def test_loss_fwd_single_launch_matches_tile_path(hip, shape):
         if first is not None:
             assert torch.equal(got[0], first)  # deterministic: fixed-order reduction
         first = got[0]
-    assert ws[:4].abs().sum().item() == 0
 
 
 def test_fused_loss_chain_sigmoid(hip):
