@@ -91,7 +91,8 @@ int pis_tune(int key, int value);
  * C[b] = A[b] . B[b]^T row-major fp32 — 0 bf16x6 128x128 (the Winograd GEMM), 1/2 its
  * no-global-load / no-split timing twins (wrong results), 3 fp32 MFMA, 4 bf16x6 128x64, 5/6 the
  * K-step-32 single-LDS-buffer bf16x6 128x128 (2 / 3 waves per SIMD; 6 is the Winograd default), 7
- * its 128x64. 5-7 need K % 32 == 0. */
+ * its 128x64, 8 the 8-wave 256x128 two-stage pipelined bf16x6 kernel (9: its no-global-load twin).
+ * 5-9 need K % 32 == 0. */
 int pis_debug_gemm_nt(const float* A, const float* B, float* C, int M, int N, int K, int batch, int variant,
                       pis_stream_t stream);
 

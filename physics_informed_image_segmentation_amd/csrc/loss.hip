@@ -268,11 +268,12 @@ __global__ __launch_bounds__(256) void loss_finalize_kernel(LossArgs g, float* _
 
 // ---------------------------------------------------------------------------
 // Forward for W % 4 == 0 (the training shapes): a block owns `rows` whole image rows of one
-// sample (rows x W = ~8192 px, 32 per thread), so u needs a row halo only (the left/right
-// reflect ghosts are columns 1 and W-2 of the same staged rows: no scattered column-halo
-// loads) and every HBM line of p and t is fetched once; one block per CU at C2. A one-block
-// finalize launch then reduces the per-block partials in a fixed order (thread k sums blocks
-// k, k+256, ... in double, then fixed butterflies): deterministic.
+// sample (~4096 px); each thread streams float4 items with all loads of four items in flight
+// before their arithmetic (no LDS staging, no barrier): the up/down neighbour rows and the
+// left/right ghosts (reflect: column -1 is column 1, W is W-2) are re-reads of lines the block
+// itself fetches, served by L1/L2, so HBM sees p and t about once. A one-block finalize launch
+// reduces the per-block partials in a fixed order (double, four partials in flight per
+// thread, fixed butterflies): deterministic.
 // ---------------------------------------------------------------------------
 struct LossRowArgs {
   LossArgs g;
@@ -283,20 +284,33 @@ struct LossRowArgs {
   float* scores;
 };
 
+template <int NW>  // waves in the block
 __device__ __forceinline__ void loss_finalize_block(const LossArgs& g, int nblk, int bps, float* __restrict__ terms,
                                                     int* __restrict__ counts, float* __restrict__ scores) {
+  constexpr int NT = 64 * NW;
   double s[6] = {0, 0, 0, 0, 0, 0};
-  for (int k = threadIdx.x; k < nblk; k += blockDim.x)
+  // four independent partials in flight per thread (one round trip for nblk <= 4 NT)
+  for (int k0 = threadIdx.x; k0 < nblk; k0 += 4 * NT) {
+    float f[4][6];
 #pragma unroll
-    for (int j = 0; j < 6; ++j) s[j] += (double)g.fpart[k * 6 + j];
-  __shared__ double red[4][6];
+    for (int u = 0; u < 4; ++u) {
+      const int k = k0 + u * NT;
+#pragma unroll
+      for (int j = 0; j < 6; ++j) f[u][j] = k < nblk ? g.fpart[k * 6 + j] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int j = 0; j < 6; ++j) s[j] += (double)f[u][j];
+  }
+  __shared__ double red[NW][6];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
   for (int j = 0; j < 6; ++j) s[j] = wave_sum_d(s[j]);
   if (lane == 0)
 #pragma unroll
     for (int j = 0; j < 6; ++j) red[wave][j] = s[j];
-  for (int b = wave; b < g.B; b += 4) {  // per-sample counters: one wave per sample
+  for (int b = wave; b < g.B; b += NW) {  // per-sample counters: one wave per sample
     long long ci = 0, cp = 0, ct = 0;
     for (int k = lane; k < bps; k += 64) {
       const int blk = b * bps + k;
@@ -327,7 +341,10 @@ __device__ __forceinline__ void loss_finalize_block(const LossArgs& g, int nblk,
   if (threadIdx.x == 0) {
     double tot[6];
 #pragma unroll
-    for (int j = 0; j < 6; ++j) tot[j] = ((red[0][j] + red[1][j]) + red[2][j]) + red[3][j];
+    for (int j = 0; j < 6; ++j) {
+      tot[j] = red[0][j];
+      for (int w = 1; w < NW; ++w) tot[j] += red[w][j];
+    }
     const double n = (double)g.B * g.H * g.W;
     const double I = tot[0], P = tot[1], T = tot[2];
     const double dice = 1.0 - (2.0 * I + g.smooth) / (P + T + g.smooth);
@@ -349,83 +366,63 @@ __device__ __forceinline__ void loss_finalize_block(const LossArgs& g, int nblk,
 template <bool RD, bool PF>
 __global__ __launch_bounds__(256) void loss_fwd_rows_kernel(LossRowArgs a) {
   constexpr bool ST = RD || PF;
-  extern __shared__ __attribute__((aligned(16))) float su[];  // [rows + 2][W]: u rows y0-1 .. y0+nr
   const LossArgs& g = a.g;
   const int H = g.H, W = g.W, W4 = W >> 2;
   const int band = blockIdx.x, b = blockIdx.y;
   const int y0 = band * a.rows, nr = min(a.rows, H - y0);
   const float* u = g.p + (size_t)b * H * W;
-  const float* tt = g.t + (size_t)b * H * W + (size_t)y0 * W;
-  const int items = nr * W4;  // float4 items of the block's interior
-  constexpr int MAXI = 8;     // rows * W / 4 <= 2048 (loss_rows): at most 8 per thread
-  f32x4 tvs[MAXI];
-#pragma unroll
-  for (int j = 0; j < MAXI; ++j) {
-    const int k = threadIdx.x + 256 * j;
-    if (k < items) tvs[j] = *(const f32x4*)(tt + 4 * (size_t)k);
-  }
-  f32x4 pin[MAXI];
-  if constexpr (ST) {
-    const int srows = nr + 2;
-    for (int k = threadIdx.x; k < srows * W4; k += 256) {
-      const int r = k / W4, q = k - r * W4;
-      const int gy = refl(y0 - 1 + r, H);
-      *(f32x4*)(su + r * W + 4 * q) = *(const f32x4*)(u + (size_t)gy * W + 4 * q);
-    }
-    __syncthreads();
-  } else {
-#pragma unroll
-    for (int j = 0; j < MAXI; ++j) {
-      const int k = threadIdx.x + 256 * j;
-      if (k < items) pin[j] = *(const f32x4*)(u + (size_t)y0 * W + 4 * (size_t)k);
-    }
-  }
+  const float* tt = g.t + (size_t)b * H * W;
+  const int items = nr * W4;  // float4 items of the block's rows
   constexpr float kLn2 = 0.69314718055994531f, kClamp2 = -144.26950408889634f;  // -100 / ln 2
   float s_it = 0.f, s_p = 0.f, s_t = 0.f, s_bce2 = 0.f, s_rd = 0.f, s_g2 = 0.f, s_q2 = 0.f;
   int c_i = 0, c_p = 0, c_t = 0;
+  constexpr int U = 4;  // items per thread in flight
+  for (int k0 = threadIdx.x; k0 < items; k0 += U * 256) {
+    f32x4 tv[U], pv[U], uv[U], dv[U];
+    float lft[U], rgt[U];
 #pragma unroll
-  for (int j = 0; j < MAXI; ++j) {
-    const int k = threadIdx.x + 256 * j;
-    if (k >= items) continue;
-    const int r = k / W4, q = k - r * W4, xb = 4 * q;
-    const f32x4 tv = tvs[j];
-    f32x4 pv, uv, dv;
-    float lft = 0.f, rgt = 0.f;
-    if constexpr (ST) {
-      const float* row = su + (r + 1) * W;
-      pv = *(const f32x4*)(row + xb);
-      uv = *(const f32x4*)(row - W + xb);
-      dv = *(const f32x4*)(row + W + xb);
-      lft = row[xb == 0 ? 1 : xb - 1];               // reflect: ghost column -1 is column 1
-      rgt = row[xb + 4 == W ? W - 2 : xb + 4];       // ghost column W is column W-2
-    } else {
-      pv = pin[j];
+    for (int j = 0; j < U; ++j) {  // every load of U items first, then the arithmetic
+      const int k = min(k0 + 256 * j, items - 1);  // tail items recompute the last one, discarded below
+      const int r = k / W4, xb = 4 * (k - r * W4), y = y0 + r;
+      const float* row = u + (size_t)y * W;
+      tv[j] = *(const f32x4*)(tt + (size_t)y * W + xb);
+      pv[j] = *(const f32x4*)(row + xb);
+      if constexpr (ST) {
+        uv[j] = *(const f32x4*)(u + (size_t)refl(y - 1, H) * W + xb);  // reflect: row -1 is row 1
+        dv[j] = *(const f32x4*)(u + (size_t)refl(y + 1, H) * W + xb);  // row H is row H-2
+        lft[j] = row[xb == 0 ? 1 : xb - 1];                             // column -1 is column 1
+        rgt[j] = row[xb + 4 == W ? W - 2 : xb + 4];                     // column W is column W-2
+      }
     }
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const float p = pv[i], t = tv[i];
-      s_it = fmaf(p, t, s_it);
-      s_p += p;
-      s_t += t;
-      s_bce2 += (t - 1.f) * fmaxf(__builtin_amdgcn_logf(1.f - p), kClamp2) -
-                t * fmaxf(__builtin_amdgcn_logf(p), kClamp2);
-      const bool pb = p > g.thr, tb = t > 0.5f;
-      c_p += pb;
-      c_t += tb;
-      c_i += pb && tb;
-      if constexpr (ST) {
-        const float ul = i == 0 ? lft : pv[i - 1], ur = i == 3 ? rgt : pv[i + 1];
-        const float uu = uv[i], ud = dv[i];
-        const float qq = fmaf(-p, p, p);  // p (1 - p)
-        if (RD) {
-          const float lap = (uu + ud) + (ul + ur) - 4.f * p;
-          const float rr = fmaf(g.D, lap, g.rx * qq * (p - g.a));
-          s_rd = fmaf(rr, rr, s_rd);
-        }
-        if (PF) {
-          const float gx = ur - ul, gy = ud - uu;  // 2x the central differences
-          s_g2 = fmaf(gx, gx, fmaf(gy, gy, s_g2));
-          s_q2 = fmaf(qq, qq, s_q2);
+    for (int j = 0; j < U; ++j) {
+      if (k0 + 256 * j >= items) break;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float p = pv[j][i], t = tv[j][i];
+        s_it = fmaf(p, t, s_it);
+        s_p += p;
+        s_t += t;
+        s_bce2 += (t - 1.f) * fmaxf(__builtin_amdgcn_logf(1.f - p), kClamp2) -
+                  t * fmaxf(__builtin_amdgcn_logf(p), kClamp2);
+        const bool pb = p > g.thr, tb = t > 0.5f;
+        c_p += pb;
+        c_t += tb;
+        c_i += pb && tb;
+        if constexpr (ST) {
+          const float ul = i == 0 ? lft[j] : pv[j][i - 1], ur = i == 3 ? rgt[j] : pv[j][i + 1];
+          const float uu = uv[j][i], ud = dv[j][i];
+          const float qq = fmaf(-p, p, p);  // p (1 - p)
+          if (RD) {
+            const float lap = (uu + ud) + (ul + ur) - 4.f * p;
+            const float rr = fmaf(g.D, lap, g.rx * qq * (p - g.a));
+            s_rd = fmaf(rr, rr, s_rd);
+          }
+          if (PF) {
+            const float gx = ur - ul, gy = ud - uu;  // 2x the central differences
+            s_g2 = fmaf(gx, gx, fmaf(gy, gy, s_g2));
+            s_q2 = fmaf(qq, qq, s_q2);
+          }
         }
       }
     }
@@ -461,13 +458,13 @@ __global__ __launch_bounds__(256) void loss_fwd_rows_kernel(LossRowArgs a) {
 // the fixed-order reduction of the row kernel's partials (one block; launch boundary = hand-off:
 // an in-kernel last-arriver hand-off costs one agent-scope L2 write-back per block, measured
 // 24 us vs 12 us at C2)
-__global__ __launch_bounds__(256) void loss_finalize_rows_kernel(LossRowArgs a) {
-  loss_finalize_block(a.g, a.g.B * a.bands, a.bands, a.terms, a.counts, a.scores);
+__global__ __launch_bounds__(1024) void loss_finalize_rows_kernel(LossRowArgs a) {
+  loss_finalize_block<16>(a.g, a.g.B * a.bands, a.bands, a.terms, a.counts, a.scores);
 }
 
-// rows per block of the whole-row forward: ~8192 pixels (32 per thread), <= 2048 float4
-static int loss_rows(int H, int W) { return std::max(1, std::min(H, 8192 / W)); }
-static bool loss_rows_ok(int H, int W) { return (W & 3) == 0 && W <= 8192 && H >= 2; }
+// rows per block of the whole-row forward: ~4096 pixels (4 float4 items per thread)
+static int loss_rows(int H, int W) { return std::max(1, std::min(H, 4096 / W)); }
+static bool loss_rows_ok(int H, int W) { return (W & 3) == 0 && H >= 2 && W >= 8; }
 
 struct LossBwdArgs {
   const float* p;
@@ -879,14 +876,14 @@ extern "C" int pis_loss_fwd(const float* p, const float* t, int B, int H, int W,
     a.bands = (int)cdiv(H, a.rows);
     a.terms = out_terms; a.counts = counts; a.scores = scores;
     const dim3 grid(a.bands, B);
-    const size_t smem = (rd || pf) ? (size_t)(a.rows + 2) * W * sizeof(float) : 0;
+    const size_t smem = 0;
     if (rd && pf) hipLaunchKernelGGL((loss_fwd_rows_kernel<true, true>), grid, dim3(256), smem, s, a);
     else if (rd) hipLaunchKernelGGL((loss_fwd_rows_kernel<true, false>), grid, dim3(256), smem, s, a);
     else if (pf) hipLaunchKernelGGL((loss_fwd_rows_kernel<false, true>), grid, dim3(256), smem, s, a);
     else hipLaunchKernelGGL((loss_fwd_rows_kernel<false, false>), grid, dim3(256), smem, s, a);
     const int rc = launch_status("loss_fwd_rows");
     if (rc) return rc;
-    hipLaunchKernelGGL(loss_finalize_rows_kernel, dim3(1), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(loss_finalize_rows_kernel, dim3(1), dim3(1024), 0, s, a);
     return launch_status("loss_finalize");
   }
   loss_plan(H, W, g.tiles_x, g.tiles_y);

@@ -1140,6 +1140,142 @@ __global__ __launch_bounds__(256, OCC) void gemm_nt_x6_bk32_kernel(const float* 
     }
 }
 
+// ---- 8-wave, 256 x 128, two-stage pipelined bf16x6 NT GEMM --------------------------------
+// One block per CU (8 waves = 2 per SIMD, wave tile 64 x 64 = 2 x 2 v_mfma_f32_32x32x16_bf16).
+// Per K-step of 32: step k is computed from one of two LDS plane buffers, then step k+1's fp32
+// registers (loaded one K-step earlier) are split into hi/mid/lo planes in the other buffer and
+// the loads of step k+2 are issued into the same registers: ONE barrier per K-step, a global
+// load has a whole K-step of MFMAs (96 per SIMD) to land. LDS rows are 64 B (32 bf16) with the 16-B chunk XOR-swizzled by row bits
+// 2..3 (chunk ^= (row >> 2) & 3), so the 16 rows a ds_read_b128 lane group reads at one chunk
+// hit 16 distinct bank quads: 2 buffers x 3 planes x 384 rows x 64 B = 147 KB.
+__device__ __forceinline__ int x6w8_off(int row, int chunk) {  // bf16 element offset of a 16-B chunk
+  return row * 32 + 8 * (chunk ^ ((row >> 2) & 3));
+}
+
+template <int DBG = 0>
+__global__ __launch_bounds__(512, 1) void gemm_nt_x6_w8_kernel(const float* __restrict__ A,
+                                                               const float* __restrict__ Bm, float* __restrict__ Cm,
+                                                               int M, int N, int K, int64_t bsA, int64_t bsB,
+                                                               int64_t bsC) {
+  constexpr int BM = 256, BN = 128, BK = 32, ROWS = BM + BN;
+  constexpr int AL = BM * BK / 4 / 512, BL = BN * BK / 4 / 512;  // float4 loads per thread per stage: 4, 2
+  extern __shared__ __attribute__((aligned(16))) __bf16 smem_x6w8[];
+  __bf16* const buf0 = smem_x6w8;
+  __bf16* const buf1 = smem_x6w8 + 3 * ROWS * 32;
+  A += blockIdx.y * bsA;
+  Bm += blockIdx.y * bsB;
+  Cm += blockIdx.y * bsC;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave & 3, wn = wave >> 2, li = lane & 31, lh = lane >> 5;
+  const int ntn = N / BN;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int m0 = (bid / ntn) * BM, n0 = (bid % ntn) * BN;
+  const int q8 = (tid & 7) * 4;  // k offset of this thread's float4 within the 32-wide step
+  const bool full = m0 + BM <= M;
+  struct Regs {
+    f32x4 a[AL], b[BL];
+  };
+  auto gload = [&](int k0, Regs& r) {
+    const int k = k0 + q8;
+#pragma unroll
+    for (int i = 0; i < AL; ++i) {
+      const int m = m0 + (tid + i * 512) / 8;
+      if (DBG == 1) {
+        r.a[i] = f32x4{(float)k0, 1.f, 2.f, 3.f};
+        continue;
+      }
+      r.a[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (full || m < M) r.a[i] = *reinterpret_cast<const f32x4*>(A + (size_t)m * K + k);
+    }
+#pragma unroll
+    for (int i = 0; i < BL; ++i) {
+      if (DBG == 1) {
+        r.b[i] = f32x4{(float)k0, 1.f, 2.f, 3.f};
+        continue;
+      }
+      r.b[i] = *reinterpret_cast<const f32x4*>(Bm + (size_t)(n0 + (tid + i * 512) / 8) * K + k);
+    }
+  };
+  auto lstore = [&](__bf16* buf, const Regs& r) {
+    const int chunk = q8 >> 3, half = (q8 >> 2) & 1;
+#pragma unroll
+    for (int i = 0; i < AL + BL; ++i) {
+      const int row = i < AL ? (tid + i * 512) / 8 : BM + (tid + (i - AL) * 512) / 8;
+      u32x2 h, m, l;
+      split3_x4(i < AL ? r.a[i] : r.b[i - AL], h, m, l);
+      const int o = x6w8_off(row, chunk) + 4 * half;
+      *reinterpret_cast<u32x2*>(buf + o) = h;
+      *reinterpret_cast<u32x2*>(buf + ROWS * 32 + o) = m;
+      *reinterpret_cast<u32x2*>(buf + 2 * ROWS * 32 + o) = l;
+    }
+  };
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+  auto compute = [&](const __bf16* buf) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int chunk = 2 * ks + lh;
+      bf16x8 af[3][2], bf[3][2];
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+          af[p][a] = *reinterpret_cast<const bf16x8*>(buf + p * ROWS * 32 + x6w8_off(wm * 64 + a * 32 + li, chunk));
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+          bf[p][b] = *reinterpret_cast<const bf16x8*>(buf + p * ROWS * 32 +
+                                                      x6w8_off(BM + wn * 64 + b * 32 + li, chunk));
+      }
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {  // smallest partial products first
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[2][a], bf[0][b], acc[a][b], 0, 0, 0);
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1][a], bf[1][b], acc[a][b], 0, 0, 0);
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0][a], bf[2][b], acc[a][b], 0, 0, 0);
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1][a], bf[0][b], acc[a][b], 0, 0, 0);
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0][a], bf[1][b], acc[a][b], 0, 0, 0);
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0][a], bf[0][b], acc[a][b], 0, 0, 0);
+        }
+    }
+  };
+  const int KT = K / BK;
+  Regs r;
+  gload(0, r);
+  lstore(buf0, r);
+  if (KT > 1) gload(BK, r);
+  __syncthreads();
+  // the loads of step k+2 are issued right after step k+1's registers are split into LDS, and land
+  // during step k+1's MFMAs (a runtime buffer select: the 2-step unrolled form spills at 256 VGPRs)
+  for (int kt = 0; kt < KT; ++kt) {
+    const __bf16* cur = (kt & 1) ? buf1 : buf0;
+    __bf16* nxt = (kt & 1) ? buf0 : buf1;
+    compute(cur);
+    if (kt + 1 < KT) {
+      lstore(nxt, r);
+      if (kt + 2 < KT) gload((kt + 2) * BK, r);
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const int n = n0 + wn * 64 + b * 32 + li;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm * 64 + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        if (full || m < M) Cm[(size_t)m * N + n] = acc[a][b][r];
+      }
+    }
+}
+constexpr size_t X6W8_SMEM = 2 * 3 * 384 * 32 * sizeof(__bf16);  // 147,456 B
+
 // ---- F(4x4,3x3) contraction fused with the output transform (bf16x6) --------------------
 // For the shallow, HBM-bound layers: the 36 products M[xi] = V[xi] U[xi]^T never go to HBM.
 // A block owns TB = 16 NWT tiles x all N = 16 NWN output channels (V is read exactly once) and
@@ -1557,6 +1693,15 @@ extern "C" int pis_debug_gemm_nt(const float* A, const float* B, float* C, int M
                     N % bn == 0,
                 "pis_debug_gemm_nt: bad arguments");
   hipStream_t s = (hipStream_t)stream;
+  if (variant == 8 || variant == 9) {  // the 8-wave 256 x 128 pipelined bf16x6 kernel (9: no global loads)
+    const dim3 g8((int)cdiv(M, 256) * (N / 128), batch);
+    const int64_t sa = (int64_t)M * K, sb = (int64_t)N * K, sc = (int64_t)M * N;
+    if (variant == 8)
+      hipLaunchKernelGGL(gemm_nt_x6_w8_kernel<0>, g8, dim3(512), X6W8_SMEM, s, A, B, C, M, N, K, sa, sb, sc);
+    else
+      hipLaunchKernelGGL(gemm_nt_x6_w8_kernel<1>, g8, dim3(512), X6W8_SMEM, s, A, B, C, M, N, K, sa, sb, sc);
+    return launch_status("debug_gemm_nt");
+  }
   const dim3 grid((int)cdiv(M, 128) * (N / bn), batch);
   const int64_t sa = (int64_t)M * K, sb = (int64_t)N * K, sc = (int64_t)M * N;
   switch (variant) {

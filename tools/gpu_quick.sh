@@ -1,0 +1,27 @@
+#!/bin/bash
+# Short GPU session: selected gpu tests (pytest -k expression) + extras.
+#   bash tools/gpu_quick.sh TAG "pytest -k expr" [extras...]
+TAG=${1:-quick}; KEXPR=${2:-loss}
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+run() {  # run NAME SECONDS cmd...
+  local name=$1 secs=$2; shift 2
+  echo "== $name ($(date +%T))"
+  timeout -k 10 "$secs" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "== $name exit $rc"; tail -4 "$OUT/$name.log"
+  case $rc in 0|1) ;; *) echo "FATAL in $name"; exit $rc ;; esac
+}
+run pytest_sel 600 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread -k "$KEXPR"
+shift 2
+for x in "$@"; do
+  case $x in
+    ab) run ab_streams 300 python -u tools/ab_streams.py --rounds 4 --steps 10 ;;
+    loss) run loss_b64 120 python -u tools/bench_loss.py --B 64; run loss_c2 120 python -u tools/bench_loss.py --B 8 ;;
+    bench) run bench 300 python -u bench.py --no-cpu-baseline ;;
+    gemm) run bench_gemm 300 python -u tools/bench_gemm.py --variants 6,8,9 --rounds 3 --check ;;
+    lossprof) run lossprof 200 rocprofv3 --kernel-trace --stats -d "$OUT/lossprof" -o run --output-format csv -- python3 tools/bench_loss.py --B 64 --reps 20 ;;
+  esac
+done
+echo "== quick done"
