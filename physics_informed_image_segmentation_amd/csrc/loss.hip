@@ -284,85 +284,6 @@ struct LossRowArgs {
   float* scores;
 };
 
-template <int NW>  // waves in the block
-__device__ __forceinline__ void loss_finalize_block(const LossArgs& g, int nblk, int bps, float* __restrict__ terms,
-                                                    int* __restrict__ counts, float* __restrict__ scores) {
-  constexpr int NT = 64 * NW;
-  double s[6] = {0, 0, 0, 0, 0, 0};
-  // four independent partials in flight per thread (one round trip for nblk <= 4 NT)
-  for (int k0 = threadIdx.x; k0 < nblk; k0 += 4 * NT) {
-    float f[4][6];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int k = k0 + u * NT;
-#pragma unroll
-      for (int j = 0; j < 6; ++j) f[u][j] = k < nblk ? g.fpart[k * 6 + j] : 0.f;
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-#pragma unroll
-      for (int j = 0; j < 6; ++j) s[j] += (double)f[u][j];
-  }
-  __shared__ double red[NW][6];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-#pragma unroll
-  for (int j = 0; j < 6; ++j) s[j] = wave_sum_d(s[j]);
-  if (lane == 0)
-#pragma unroll
-    for (int j = 0; j < 6; ++j) red[wave][j] = s[j];
-  for (int b = wave; b < g.B; b += NW) {  // per-sample counters: one wave per sample
-    long long ci = 0, cp = 0, ct = 0;
-    for (int k = lane; k < bps; k += 64) {
-      const int blk = b * bps + k;
-      ci += g.ipart[blk * 3 + 0];
-      cp += g.ipart[blk * 3 + 1];
-      ct += g.ipart[blk * 3 + 2];
-    }
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-      ci += __shfl_xor(ci, off, 64);
-      cp += __shfl_xor(cp, off, 64);
-      ct += __shfl_xor(ct, off, 64);
-    }
-    if (lane == 0) {
-      if (counts) {
-        counts[b * 3 + 0] = (int)ci;
-        counts[b * 3 + 1] = (int)cp;
-        counts[b * 3 + 2] = (int)ct;
-      }
-      if (scores) {  // fp32 arithmetic exactly as the reference metric (src/metrics.py:67-70, evaluate.py:91-94)
-        const float fi = (float)ci, fp = (float)cp, ft = (float)ct, sm = g.smooth;
-        scores[b * 2 + 0] = (2.f * fi + sm) / (fp + ft + sm);
-        scores[b * 2 + 1] = (fi + sm) / (fp + ft - fi + sm);
-      }
-    }
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    double tot[6];
-#pragma unroll
-    for (int j = 0; j < 6; ++j) {
-      tot[j] = red[0][j];
-      for (int w = 1; w < NW; ++w) tot[j] += red[w][j];
-    }
-    const double n = (double)g.B * g.H * g.W;
-    const double I = tot[0], P = tot[1], T = tot[2];
-    const double dice = 1.0 - (2.0 * I + g.smooth) / (P + T + g.smooth);
-    const double bce = tot[3] / n, rd = tot[4] / n, pf = tot[5] / n;
-    double total = g.dice_w * dice + g.bce_w * bce;
-    if (g.rd_w > 0.f) total += g.rd_w * rd;
-    if (g.pf_w > 0.f) total += g.pf_w * pf;
-    terms[0] = (float)total;
-    terms[1] = (float)dice;
-    terms[2] = (float)bce;
-    terms[3] = (float)rd;
-    terms[4] = (float)pf;
-    terms[5] = (float)I;
-    terms[6] = (float)P;
-    terms[7] = (float)T;
-  }
-}
-
 template <bool RD, bool PF>
 __global__ __launch_bounds__(256) void loss_fwd_rows_kernel(LossRowArgs a) {
   constexpr bool ST = RD || PF;
@@ -455,16 +376,96 @@ __global__ __launch_bounds__(256) void loss_fwd_rows_kernel(LossRowArgs a) {
   }
 }
 
-// the fixed-order reduction of the row kernel's partials (one block; launch boundary = hand-off:
-// an in-kernel last-arriver hand-off costs one agent-scope L2 write-back per block, measured
-// 24 us vs 12 us at C2)
+// The fixed-order reduction of the row kernel's partials (one block of 1024 threads; the launch
+// boundary is the hand-off — an in-kernel last-arriver hand-off costs an agent-scope L2 write-back
+// per block, measured 2x slower at C2). Every partial is first copied to LDS with all loads in
+// flight (one memory round trip), then reduced from LDS: thread k sums blocks k, k + 1024, ... in
+// double, fixed butterflies; per-sample counters one wave per sample.
+constexpr int LOSS_MAX_BLOCKS = 2048;
+
 __global__ __launch_bounds__(1024) void loss_finalize_rows_kernel(LossRowArgs a) {
-  loss_finalize_block<16>(a.g, a.g.B * a.bands, a.bands, a.terms, a.counts, a.scores);
+  __shared__ float sf[LOSS_MAX_BLOCKS * 6];
+  __shared__ int si[LOSS_MAX_BLOCKS * 3];
+  const LossArgs& g = a.g;
+  const int nblk = g.B * a.bands, bps = a.bands;
+  for (int k = threadIdx.x; k < nblk * 6; k += 1024) sf[k] = g.fpart[k];
+  for (int k = threadIdx.x; k < nblk * 3; k += 1024) si[k] = g.ipart[k];
+  __syncthreads();
+  double s[6] = {0, 0, 0, 0, 0, 0};
+  for (int k = threadIdx.x; k < nblk; k += 1024)
+#pragma unroll
+    for (int j = 0; j < 6; ++j) s[j] += (double)sf[k * 6 + j];
+  __shared__ double red[16][6];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int j = 0; j < 6; ++j) s[j] = wave_sum_d(s[j]);
+  if (lane == 0)
+#pragma unroll
+    for (int j = 0; j < 6; ++j) red[wave][j] = s[j];
+  for (int b = wave; b < g.B; b += 16) {
+    long long ci = 0, cp = 0, ct = 0;
+    for (int k = lane; k < bps; k += 64) {
+      const int blk = b * bps + k;
+      ci += si[blk * 3 + 0];
+      cp += si[blk * 3 + 1];
+      ct += si[blk * 3 + 2];
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      ci += __shfl_xor(ci, off, 64);
+      cp += __shfl_xor(cp, off, 64);
+      ct += __shfl_xor(ct, off, 64);
+    }
+    if (lane == 0) {
+      if (a.counts) {
+        a.counts[b * 3 + 0] = (int)ci;
+        a.counts[b * 3 + 1] = (int)cp;
+        a.counts[b * 3 + 2] = (int)ct;
+      }
+      if (a.scores) {  // fp32 arithmetic exactly as the reference metric (src/metrics.py:67-70, evaluate.py:91-94)
+        const float fi = (float)ci, fp = (float)cp, ft = (float)ct, sm = g.smooth;
+        a.scores[b * 2 + 0] = (2.f * fi + sm) / (fp + ft + sm);
+        a.scores[b * 2 + 1] = (fi + sm) / (fp + ft - fi + sm);
+      }
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double tot[6];
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+      tot[j] = red[0][j];
+      for (int w = 1; w < 16; ++w) tot[j] += red[w][j];
+    }
+    const double n = (double)g.B * g.H * g.W;
+    const double I = tot[0], P = tot[1], T = tot[2];
+    const double dice = 1.0 - (2.0 * I + g.smooth) / (P + T + g.smooth);
+    const double bce = tot[3] / n, rd = tot[4] / n, pf = tot[5] / n;
+    double total = g.dice_w * dice + g.bce_w * bce;
+    if (g.rd_w > 0.f) total += g.rd_w * rd;
+    if (g.pf_w > 0.f) total += g.pf_w * pf;
+    float* terms = a.terms;
+    terms[0] = (float)total;
+    terms[1] = (float)dice;
+    terms[2] = (float)bce;
+    terms[3] = (float)rd;
+    terms[4] = (float)pf;
+    terms[5] = (float)I;
+    terms[6] = (float)P;
+    terms[7] = (float)T;
+  }
 }
 
-// rows per block of the whole-row forward: ~4096 pixels (4 float4 items per thread)
-static int loss_rows(int H, int W) { return std::max(1, std::min(H, 4096 / W)); }
-static bool loss_rows_ok(int H, int W) { return (W & 3) == 0 && H >= 2 && W >= 8; }
+// rows per block of the whole-row forward: at least ~4096 pixels (4 float4 items per thread), and
+// few enough blocks that the finalize stages every partial in LDS (<= LOSS_MAX_BLOCKS)
+static int loss_rows(int B, int H, int W) {
+  int r = std::max(1, 4096 / W);
+  while ((int64_t)B * cdiv(H, r) > LOSS_MAX_BLOCKS) r *= 2;
+  return std::min(r, H);
+}
+static bool loss_rows_ok(int B, int H, int W) {
+  return (W & 3) == 0 && H >= 2 && W >= 8 && B <= LOSS_MAX_BLOCKS;
+}
 
 struct LossBwdArgs {
   const float* p;
@@ -844,7 +845,7 @@ static int64_t loss_nblk(int B, int H, int W) {
   int tx, ty;
   loss_plan(H, W, tx, ty);
   int64_t n = (int64_t)B * tx * ty;
-  if (loss_rows_ok(H, W)) n = std::max<int64_t>(n, (int64_t)B * cdiv(H, loss_rows(H, W)));
+  if (loss_rows_ok(B, H, W)) n = std::max<int64_t>(n, (int64_t)B * cdiv(H, loss_rows(B, H, W)));
   return n;
 }
 
@@ -869,10 +870,10 @@ extern "C" int pis_loss_fwd(const float* p, const float* t, int B, int H, int W,
   const bool all = prm->flags & PIS_LOSS_ALL_TERMS;
   const bool rd = all || prm->rd_w > 0.f, pf = all || prm->pf_w > 0.f;
   hipStream_t s = (hipStream_t)stream;
-  if (loss_rows_ok(H, W) && tune_get(PIS_TUNE_LOSS_ROWS) != 0) {
+  if (loss_rows_ok(B, H, W) && tune_get(PIS_TUNE_LOSS_ROWS) != 0) {
     LossRowArgs a{};
     a.g = g;
-    a.rows = loss_rows(H, W);
+    a.rows = loss_rows(B, H, W);
     a.bands = (int)cdiv(H, a.rows);
     a.terms = out_terms; a.counts = counts; a.scores = scores;
     const dim3 grid(a.bands, B);
