@@ -361,6 +361,7 @@ def main():
     broadcast_parameters(model)
     if world > 1:
         GradBucketer(model)
+    torch.cuda.manual_seed(42 + rank)  # Dropout2d masks per rank (train() does the same)
     crit = DiceBCEPDELoss(**loss_kw)
     opt = AdamW(model.parameters(), lr=LR, weight_decay=1e-5, grad_scale=1.0 / world)
     x, t = make_batch(rank, device)

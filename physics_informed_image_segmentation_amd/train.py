@@ -459,6 +459,9 @@ def train(use_two_stage: bool = True, pde_weight: float = 1e-4, diffusion_coeff:
     broadcast_parameters(model)
     if world > 1:
         GradBucketer(model)
+        # every replica starts from rank 0's weights; Dropout2d masks (the device RNG) differ per
+        # rank, as its data shard does (rank 0 keeps the reference's seed)
+        torch.cuda.manual_seed(seed + rank)
     grad_scale = 1.0 / world
 
     def run(criterion, lr, epochs, name, csv_path):
