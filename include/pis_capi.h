@@ -82,9 +82,11 @@ int pis_version(void);
 #define PIS_TUNE_WINO_DZ2 16     /* pis_conv3x3_bwd_prep: 1 (default) one pass over dz for both transforms, 0 off */
 #define PIS_TUNE_WINO_VW 17      /* F(4x4) input / output transforms: 2 (default: half the registers, +2-11 % on the
                                     512^2-256^2 layers) or 4 channels per thread */
-#define PIS_TUNE_LOSS_ROWS 18     /* pis_loss_fwd with W % 4 == 0: 1 (default) whole-row bands (no column halo),
-                                    0 16x128 tiles; both followed by the one-block fixed-order finalize */
-#define PIS_TUNE_NKEYS 19
+#define PIS_TUNE_LOSS_ROWS 18     /* pis_loss_fwd with W % 4 == 0: 1 (default) whole-row bands, 0 16x128 tiles;
+                                    both followed by the one-block fixed-order finalize (deterministic) */
+#define PIS_TUNE_LOSS_ROWMUL 19  /* whole-row loss forward: rows per block multiplier (1 default: the most blocks
+                                    up to 2048; 2, 4: fewer blocks, more row batches per thread) */
+#define PIS_TUNE_NKEYS 20
 #define PIS_DEBUG_NOLOAD (1 << 16)
 int pis_tune(int key, int value);
 /* Tooling (tools/bench_gemm.py): time one batched NT GEMM kernel variant in isolation,
@@ -95,6 +97,13 @@ int pis_tune(int key, int value);
  * 5-9 need K % 32 == 0. */
 int pis_debug_gemm_nt(const float* A, const float* B, float* C, int M, int N, int K, int batch, int variant,
                       pis_stream_t stream);
+
+/* Scheduling aid: arm an event (hipEvent_t) that the next F(4x4,3x3) convolution launched on this
+ * thread (pis_conv3x3_fwd_ex / _dgrad_ex / _fwd_keep / _fwd_pool) records on its stream right after
+ * its 36 contractions, before the output transform; the slot then disarms. Lets a caller start
+ * MFMA-bound work on another stream while the HBM-bound output transform runs. Returns 1 when
+ * the previously armed event was never recorded (NULL disarms), else 0. */
+int pis_arm_gemm_event(void* event);
 
 /* Profiling hook: called on the launching thread right before (phase 0) and after (phase 1)
  * the enqueue of each heavy kernel ("conv3x3_halo", "wino_gemm", "wgrad3x3_halo",
@@ -221,6 +230,7 @@ typedef struct pis_loss_params {
  * counts: [B][3] = exact (I_hat, P_hat, T) of the thresholded prediction per sample.
  * scores: [B][2] = (Dice, IoU) per sample (src/metrics.py:67-70, src/evaluate.py:91-94). */
 #define PIS_LOSS_NTERMS 8
+/* ws: pis_loss_ws(B, H, W) bytes of device scratch (no state between calls). */
 size_t pis_loss_ws(int B, int H, int W);
 int pis_loss_fwd(const float* p, const float* t, int B, int H, int W, const pis_loss_params* prm,
                  float* out_terms, int* counts, float* scores, void* ws, size_t ws_bytes,

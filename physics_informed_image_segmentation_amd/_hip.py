@@ -34,6 +34,7 @@ LAUNCH_HOOK_T = ctypes.CFUNCTYPE(None, ctypes.c_char_p, c_int, c_void_p, ctypes.
 
 _SIGNATURES = {
     "pis_set_launch_hook": ([LAUNCH_HOOK_T, P], None),
+    "pis_arm_gemm_event": ([P], c_int),
     "pis_version": ([], c_int),
     "pis_last_error": ([], ctypes.c_char_p),
     "pis_tune": ([I, I], c_int),

@@ -15,7 +15,7 @@ void set_error(const char* fmt, ...) {
 }
 
 // kernel-variant knobs (defaults = the measured best on MI355X)
-static std::atomic<int> g_tune[PIS_TUNE_NKEYS] = {0, 16, 0, 1, 0, 1, 512, 0, 1, 2048, 3, 1, 0, 1, 1, 1, 1, 2, 1};
+static std::atomic<int> g_tune[PIS_TUNE_NKEYS] = {0, 16, 0, 1, 0, 1, 512, 0, 1, 2048, 3, 1, 0, 1, 1, 1, 1, 2, 1, 1};
 
 int tune_get(int key) { return (key > 0 && key < PIS_TUNE_NKEYS) ? g_tune[key].load() : 0; }
 
@@ -26,10 +26,27 @@ void launch_hook(const char* kernel, int phase, hipStream_t s, double flop) {
   const pis_launch_hook_t fn = g_hook.load(std::memory_order_relaxed);
   if (fn) fn(kernel, phase, (pis_stream_t)s, flop, g_hook_user.load(std::memory_order_relaxed));
 }
+
+// pis_arm_gemm_event: an event the NEXT F(4x4) contraction launched by this thread records on its
+// stream right after the GEMM (before the output transform), then the slot is disarmed
+static thread_local hipEvent_t g_gemm_event = nullptr;
+
+void gemm_done(hipStream_t s) {
+  if (g_gemm_event) {
+    (void)hipEventRecord(g_gemm_event, s);
+    g_gemm_event = nullptr;
+  }
+}
 }  // namespace pis
 
 extern "C" const char* pis_last_error(void) { return pis::g_last_error; }
 extern "C" int pis_version(void) { return 1; }
+
+extern "C" int pis_arm_gemm_event(void* event) {
+  const int pending = pis::g_gemm_event != nullptr;
+  pis::g_gemm_event = (hipEvent_t)event;
+  return pending;
+}
 
 extern "C" void pis_set_launch_hook(pis_launch_hook_t fn, void* user) {
   pis::g_hook_user.store(user);

@@ -22,6 +22,7 @@ int tune_get(int key);  // pis_tune() knob value (csrc/capi.hip)
 // Optional host callback around the heavy launches (pis_set_launch_hook): lets a
 // profiler record HIP events on the launch stream right before/after one kernel.
 void launch_hook(const char* kernel, int phase, hipStream_t s, double flop);
+void gemm_done(hipStream_t s);  // records the event armed by pis_arm_gemm_event, if any
 
 inline int launch_status(const char* what) {
   hipError_t e = hipGetLastError();

@@ -268,13 +268,16 @@ __global__ __launch_bounds__(256) void loss_finalize_kernel(LossArgs g, float* _
 
 // ---------------------------------------------------------------------------
 // Forward for W % 4 == 0 (the training shapes): a block owns `rows` whole image rows of one
-// sample (~4096 px); each thread streams float4 items with all loads of four items in flight
-// before their arithmetic (no LDS staging, no barrier): the up/down neighbour rows and the
-// left/right ghosts (reflect: column -1 is column 1, W is W-2) are re-reads of lines the block
-// itself fetches, served by L1/L2, so HBM sees p and t about once. A one-block finalize launch
-// reduces the per-block partials in a fixed order (double, four partials in flight per
-// thread, fixed butterflies): deterministic.
+// sample; its threads tile a row with float4 columns (TX = min(W/4, 256) threads a row) and
+// split the rows into RY = 256/TX contiguous segments. Each thread walks its segment DOWN its
+// column with a sliding window of three u rows in registers, so a row of u is loaded once per
+// thread (not three times): per U rows it issues U u-rows, U t-rows and the 2U left/right ghost
+// scalars (reflect: column -1 is column 1, W is W-2; re-reads of lines the block fetches, L1/L2
+// hits) before any arithmetic. No LDS staging, no integer division in the loop. A one-block
+// finalize launch reduces the per-block partials in a fixed order: deterministic.
 // ---------------------------------------------------------------------------
+constexpr int LOSS_ROW_BATCH = 2;  // rows per thread per batch of the whole-row forward
+
 struct LossRowArgs {
   LossArgs g;
   int rows;             // image rows per block
@@ -285,7 +288,7 @@ struct LossRowArgs {
 };
 
 template <bool RD, bool PF>
-__global__ __launch_bounds__(256) void loss_fwd_rows_kernel(LossRowArgs a) {
+__global__ __launch_bounds__(256, 5) void loss_fwd_rows_kernel(LossRowArgs a) {
   constexpr bool ST = RD || PF;
   const LossArgs& g = a.g;
   const int H = g.H, W = g.W, W4 = W >> 2;
@@ -293,78 +296,124 @@ __global__ __launch_bounds__(256) void loss_fwd_rows_kernel(LossRowArgs a) {
   const int y0 = band * a.rows, nr = min(a.rows, H - y0);
   const float* u = g.p + (size_t)b * H * W;
   const float* tt = g.t + (size_t)b * H * W;
-  const int items = nr * W4;  // float4 items of the block's rows
+  const int TX = min(W4, 256), RY = 256 / TX;
+  const int tx = threadIdx.x % TX, ty = threadIdx.x / TX;
+  const int seg = (nr + RY - 1) / RY;
+  const int ys = y0 + ty * seg, ye = min(ys + seg, y0 + nr);  // ys >= ye: an idle thread
   constexpr float kLn2 = 0.69314718055994531f, kClamp2 = -144.26950408889634f;  // -100 / ln 2
-  float s_it = 0.f, s_p = 0.f, s_t = 0.f, s_bce2 = 0.f, s_rd = 0.f, s_g2 = 0.f, s_q2 = 0.f;
+  // per-thread sums as pixel pairs (packed fp32 math: one v_pk_* instruction per two pixels)
+  f32x2 s_it = {0.f, 0.f}, s_p = s_it, s_t = s_it, s_bce2 = s_it, s_rd = s_it, s_g2 = s_it, s_q2 = s_it;
   int c_i = 0, c_p = 0, c_t = 0;
-  constexpr int U = 4;  // items per thread in flight
-  for (int k0 = threadIdx.x; k0 < items; k0 += U * 256) {
-    f32x4 tv[U], pv[U], uv[U], dv[U];
-    float lft[U], rgt[U];
-#pragma unroll
-    for (int j = 0; j < U; ++j) {  // every load of U items first, then the arithmetic
-      const int k = min(k0 + 256 * j, items - 1);  // tail items recompute the last one, discarded below
-      const int r = k / W4, xb = 4 * (k - r * W4), y = y0 + r;
-      const float* row = u + (size_t)y * W;
-      tv[j] = *(const f32x4*)(tt + (size_t)y * W + xb);
-      pv[j] = *(const f32x4*)(row + xb);
+  // Two rows per batch (LOSS_ROW_BATCH); the NEXT batch's loads are issued before this batch's
+  // arithmetic (software pipelining: each wave keeps a batch in flight while it computes). Every
+  // value is a named register: arrays indexed by a loop variable are promoted to LDS by the
+  // compiler before unrolling.
+  struct Batch {
+    f32x4 d0, d1;            // ST: rows y + 1, y + 2 (down neighbours; row H is H-2); else rows y, y + 1
+    f32x4 t0, t1;            // targets of rows y, y + 1
+    float l0, r0, l1, r1;    // left / right ghosts of rows y, y + 1 (reflect: column -1 is 1, W is W-2)
+  };
+  for (int xi = tx; xi < W4 && ty < RY && ys < ye; xi += TX) {
+    const int xb = 4 * xi;
+    const int xl = xb == 0 ? 1 : xb - 1, xr = xb + 4 == W ? W - 2 : xb + 4;
+    // 32-bit offsets from the block-uniform sample base (H W < 2^31); rows past the segment repeat
+    // its last row (discarded below), so the loads are branch-free
+    auto load = [&](Batch& bt, int y) {
+      const int ya = min(y, ye - 1), yb = min(y + 1, ye - 1);
+      bt.t0 = *(const f32x4*)(tt + (ya * W + xb));
+      bt.t1 = *(const f32x4*)(tt + (yb * W + xb));
       if constexpr (ST) {
-        uv[j] = *(const f32x4*)(u + (size_t)refl(y - 1, H) * W + xb);  // reflect: row -1 is row 1
-        dv[j] = *(const f32x4*)(u + (size_t)refl(y + 1, H) * W + xb);  // row H is row H-2
-        lft[j] = row[xb == 0 ? 1 : xb - 1];                             // column -1 is column 1
-        rgt[j] = row[xb + 4 == W ? W - 2 : xb + 4];                     // column W is column W-2
+        bt.d0 = *(const f32x4*)(u + (refl(min(ya + 1, H), H) * W + xb));
+        bt.d1 = *(const f32x4*)(u + (refl(min(yb + 1, H), H) * W + xb));
+        bt.l0 = u[ya * W + xl];
+        bt.r0 = u[ya * W + xr];
+        bt.l1 = u[yb * W + xl];
+        bt.r1 = u[yb * W + xr];
+      } else {
+        bt.d0 = *(const f32x4*)(u + (ya * W + xb));
+        bt.d1 = *(const f32x4*)(u + (yb * W + xb));
       }
+    };
+    f32x4 up, cur;  // ST: rows y - 1 and y (reflect: row -1 is row 1)
+    if constexpr (ST) {
+      up = *(const f32x4*)(u + (refl(ys - 1, H) * W + xb));
+      cur = *(const f32x4*)(u + (ys * W + xb));
     }
-#pragma unroll
-    for (int j = 0; j < U; ++j) {
-      if (k0 + 256 * j >= items) break;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const float p = pv[j][i], t = tv[j][i];
-        s_it = fmaf(p, t, s_it);
-        s_p += p;
-        s_t += t;
-        s_bce2 += (t - 1.f) * fmaxf(__builtin_amdgcn_logf(1.f - p), kClamp2) -
-                  t * fmaxf(__builtin_amdgcn_logf(p), kClamp2);
-        const bool pb = p > g.thr, tb = t > 0.5f;
-        c_p += pb;
-        c_t += tb;
-        c_i += pb && tb;
-        if constexpr (ST) {
-          const float ul = i == 0 ? lft[j] : pv[j][i - 1], ur = i == 3 ? rgt[j] : pv[j][i + 1];
-          const float uu = uv[j][i], ud = dv[j][i];
-          const float qq = fmaf(-p, p, p);  // p (1 - p)
-          if (RD) {
-            const float lap = (uu + ud) + (ul + ur) - 4.f * p;
-            const float rr = fmaf(g.D, lap, g.rx * qq * (p - g.a));
-            s_rd = fmaf(rr, rr, s_rd);
-          }
-          if (PF) {
-            const float gx = ur - ul, gy = ud - uu;  // 2x the central differences
-            s_g2 = fmaf(gx, gx, fmaf(gy, gy, s_g2));
-            s_q2 = fmaf(qq, qq, s_q2);
-          }
+    const f32x2 a2 = {g.a, g.a}, D2 = {g.D, g.D}, rx2 = {g.rx, g.rx};
+    // two pixels: p, t, and the up / down / left / right neighbours of u (packed fp32 math)
+    auto px2 = [&](f32x2 p, f32x2 t, f32x2 uu, f32x2 ud, f32x2 ul, f32x2 ur) {
+      s_it = __builtin_elementwise_fma(p, t, s_it);
+      s_p += p;
+      s_t += t;
+      // (t - 1) L1 - t L0 = t (L1 - L0) - L1 (log2 domain, clamped at -100 / ln 2)
+      const f32x2 l1 = {fmaxf(__builtin_amdgcn_logf(1.f - p.x), kClamp2), fmaxf(__builtin_amdgcn_logf(1.f - p.y), kClamp2)};
+      const f32x2 l0 = {fmaxf(__builtin_amdgcn_logf(p.x), kClamp2), fmaxf(__builtin_amdgcn_logf(p.y), kClamp2)};
+      s_bce2 = __builtin_elementwise_fma(t, l1 - l0, s_bce2) - l1;
+      // thresholded counters as wave ballots: one compare per pixel on the VALU, the counting on
+      // the scalar unit (exact; lanes past their segment's end are inactive and count 0)
+      const unsigned long long mp0 = __ballot(p.x > g.thr), mt0 = __ballot(t.x > 0.5f);
+      const unsigned long long mp1 = __ballot(p.y > g.thr), mt1 = __ballot(t.y > 0.5f);
+      c_p += __popcll(mp0) + __popcll(mp1);
+      c_t += __popcll(mt0) + __popcll(mt1);
+      c_i += __popcll(mp0 & mt0) + __popcll(mp1 & mt1);
+      if constexpr (ST) {
+        const f32x2 qq = __builtin_elementwise_fma(-p, p, p);  // p (1 - p)
+        if (RD) {
+          const f32x2 lap = __builtin_elementwise_fma(f32x2{-4.f, -4.f}, p, (uu + ud) + (ul + ur));
+          const f32x2 rr = __builtin_elementwise_fma(D2, lap, rx2 * qq * (p - a2));
+          s_rd = __builtin_elementwise_fma(rr, rr, s_rd);
+        }
+        if (PF) {
+          const f32x2 gx = ur - ul, gy = ud - uu;  // 2x the central differences
+          s_g2 = __builtin_elementwise_fma(gx, gx, __builtin_elementwise_fma(gy, gy, s_g2));
+          s_q2 = __builtin_elementwise_fma(qq, qq, s_q2);
         }
       }
+    };
+    // one row of 4 pixels as pairs (0, 1), (2, 3): c the row, uu / dd the rows above / below
+    auto row = [&](f32x4 c, f32x4 t, f32x4 uu, f32x4 dd, float l, float r) {
+      px2(f32x2{c.x, c.y}, f32x2{t.x, t.y}, f32x2{uu.x, uu.y}, f32x2{dd.x, dd.y}, f32x2{l, c.x}, f32x2{c.y, c.z});
+      px2(f32x2{c.z, c.w}, f32x2{t.z, t.w}, f32x2{uu.z, uu.w}, f32x2{dd.z, dd.w}, f32x2{c.y, c.z}, f32x2{c.w, r});
+    };
+    auto compute = [&](const Batch& bt, int y) {
+      if constexpr (ST) {
+        row(cur, bt.t0, up, bt.d0, bt.l0, bt.r0);
+        if (y + 1 < ye) row(bt.d0, bt.t1, cur, bt.d1, bt.l1, bt.r1);
+        up = bt.d0;
+        cur = bt.d1;
+      } else {
+        row(bt.d0, bt.t0, bt.d0, bt.d0, 0.f, 0.f);
+        if (y + 1 < ye) row(bt.d1, bt.t1, bt.d1, bt.d1, 0.f, 0.f);
+      }
+    };
+    // ping-pong buffers (no register copies, which would make every batch wait for the next)
+    Batch A, Bn;
+    load(A, ys);
+    for (int y = ys; y < ye; y += 4) {
+      load(Bn, y + 2);  // unconditional: branch-free, exact vmcnt waits
+      compute(A, y);
+      load(A, y + 4);
+      if (y + 2 < ye) compute(Bn, y + 2);
     }
   }
-  float v[6] = {s_it, s_p, s_t, s_bce2 * kLn2, s_rd, 0.125f * g.eps * s_g2 + s_q2 / g.eps};
-  int c[3] = {c_i, c_p, c_t};
+  // block partials: wave sums (fixed butterflies), then the 4 waves in order; explicit scalars
+  // (a per-thread array here is promoted to LDS by the compiler)
+  const float v0 = wave_sum(s_it[0] + s_it[1]), v1 = wave_sum(s_p[0] + s_p[1]), v2 = wave_sum(s_t[0] + s_t[1]);
+  const float v3 = wave_sum((s_bce2[0] + s_bce2[1]) * kLn2), v4 = wave_sum(s_rd[0] + s_rd[1]);
+  const float v5 = wave_sum(0.125f * g.eps * (s_g2[0] + s_g2[1]) + (s_q2[0] + s_q2[1]) / g.eps);
   __shared__ float fr[4][6];
   __shared__ int ir[4][3];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-#pragma unroll
-  for (int j = 0; j < 6; ++j) v[j] = wave_sum(v[j]);
-#pragma unroll
-  for (int j = 0; j < 3; ++j) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) c[j] += __shfl_xor(c[j], off, 64);
-  }
-  if (lane == 0) {
-#pragma unroll
-    for (int j = 0; j < 6; ++j) fr[wave][j] = v[j];
-#pragma unroll
-    for (int j = 0; j < 3; ++j) ir[wave][j] = c[j];
+  if (lane == 0) {  // c_*: already whole-wave counts (ballots)
+    fr[wave][0] = v0;
+    fr[wave][1] = v1;
+    fr[wave][2] = v2;
+    fr[wave][3] = v3;
+    fr[wave][4] = v4;
+    fr[wave][5] = v5;
+    ir[wave][0] = c_i;
+    ir[wave][1] = c_p;
+    ir[wave][2] = c_t;
   }
   __syncthreads();
   const int blk = b * a.bands + band;
@@ -376,91 +425,127 @@ __global__ __launch_bounds__(256) void loss_fwd_rows_kernel(LossRowArgs a) {
   }
 }
 
-// The fixed-order reduction of the row kernel's partials (one block of 1024 threads; the launch
-// boundary is the hand-off — an in-kernel last-arriver hand-off costs an agent-scope L2 write-back
-// per block, measured 2x slower at C2). Every partial is first copied to LDS with all loads in
-// flight (one memory round trip), then reduced from LDS: thread k sums blocks k, k + 1024, ... in
-// double, fixed butterflies; per-sample counters one wave per sample.
+// The fixed-order reduction of the row kernel's partials: a one-block launch (the launch boundary
+// is the hand-off; folding it into the forward's last block was measured slower both ways: a
+// same-address agent-scope ticket serialises ~2048 atomics, +20 us at C2; per-block flags polled
+// by the grid's last block, +4-7 us). Every load is issued before any arithmetic (one memory round
+// trip): the float partials straight into registers (thread k owns blocks k, k + 256, ...; summed
+// in double in that order, fixed butterflies), the per-block counters staged in LDS and summed per
+// sample by G lanes. Deterministic.
 constexpr int LOSS_MAX_BLOCKS = 2048;
 
-__global__ __launch_bounds__(1024) void loss_finalize_rows_kernel(LossRowArgs a) {
-  __shared__ float sf[LOSS_MAX_BLOCKS * 6];
-  __shared__ int si[LOSS_MAX_BLOCKS * 3];
-  const LossArgs& g = a.g;
-  const int nblk = g.B * a.bands, bps = a.bands;
-  for (int k = threadIdx.x; k < nblk * 6; k += 1024) sf[k] = g.fpart[k];
-  for (int k = threadIdx.x; k < nblk * 3; k += 1024) si[k] = g.ipart[k];
-  __syncthreads();
-  double s[6] = {0, 0, 0, 0, 0, 0};
-  for (int k = threadIdx.x; k < nblk; k += 1024)
-#pragma unroll
-    for (int j = 0; j < 6; ++j) s[j] += (double)sf[k * 6 + j];
-  __shared__ double red[16][6];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-#pragma unroll
-  for (int j = 0; j < 6; ++j) s[j] = wave_sum_d(s[j]);
-  if (lane == 0)
-#pragma unroll
-    for (int j = 0; j < 6; ++j) red[wave][j] = s[j];
-  for (int b = wave; b < g.B; b += 16) {
-    long long ci = 0, cp = 0, ct = 0;
-    for (int k = lane; k < bps; k += 64) {
-      const int blk = b * bps + k;
-      ci += si[blk * 3 + 0];
-      cp += si[blk * 3 + 1];
-      ct += si[blk * 3 + 2];
-    }
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-      ci += __shfl_xor(ci, off, 64);
-      cp += __shfl_xor(cp, off, 64);
-      ct += __shfl_xor(ct, off, 64);
-    }
-    if (lane == 0) {
-      if (a.counts) {
-        a.counts[b * 3 + 0] = (int)ci;
-        a.counts[b * 3 + 1] = (int)cp;
-        a.counts[b * 3 + 2] = (int)ct;
-      }
-      if (a.scores) {  // fp32 arithmetic exactly as the reference metric (src/metrics.py:67-70, evaluate.py:91-94)
-        const float fi = (float)ci, fp = (float)cp, ft = (float)ct, sm = g.smooth;
-        a.scores[b * 2 + 0] = (2.f * fi + sm) / (fp + ft + sm);
-        a.scores[b * 2 + 1] = (fi + sm) / (fp + ft - fi + sm);
-      }
-    }
+__device__ __forceinline__ void store_counts(const LossRowArgs& a, int b, int ci, int cp, int ct) {
+  if (a.counts) {
+    a.counts[b * 3 + 0] = ci;
+    a.counts[b * 3 + 1] = cp;
+    a.counts[b * 3 + 2] = ct;
   }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    double tot[6];
-#pragma unroll
-    for (int j = 0; j < 6; ++j) {
-      tot[j] = red[0][j];
-      for (int w = 1; w < 16; ++w) tot[j] += red[w][j];
-    }
-    const double n = (double)g.B * g.H * g.W;
-    const double I = tot[0], P = tot[1], T = tot[2];
-    const double dice = 1.0 - (2.0 * I + g.smooth) / (P + T + g.smooth);
-    const double bce = tot[3] / n, rd = tot[4] / n, pf = tot[5] / n;
-    double total = g.dice_w * dice + g.bce_w * bce;
-    if (g.rd_w > 0.f) total += g.rd_w * rd;
-    if (g.pf_w > 0.f) total += g.pf_w * pf;
-    float* terms = a.terms;
-    terms[0] = (float)total;
-    terms[1] = (float)dice;
-    terms[2] = (float)bce;
-    terms[3] = (float)rd;
-    terms[4] = (float)pf;
-    terms[5] = (float)I;
-    terms[6] = (float)P;
-    terms[7] = (float)T;
+  if (a.scores) {  // fp32 arithmetic exactly as the reference metric (src/metrics.py:67-70, evaluate.py:91-94)
+    const float fi = (float)ci, fp = (float)cp, ft = (float)ct, sm = a.g.smooth;
+    a.scores[b * 2 + 0] = (2.f * fi + sm) / (fp + ft + sm);
+    a.scores[b * 2 + 1] = (fi + sm) / (fp + ft - fi + sm);
   }
 }
 
-// rows per block of the whole-row forward: at least ~4096 pixels (4 float4 items per thread), and
-// few enough blocks that the finalize stages every partial in LDS (<= LOSS_MAX_BLOCKS)
+__device__ void finalize_rows_store(const LossArgs& g, const double* tot, float* terms);
+
+__global__ __launch_bounds__(256) void loss_finalize_rows_kernel(LossRowArgs a) {
+  const LossArgs& g = a.g;
+  const int nblk = g.B * a.bands, tid = threadIdx.x;
+  constexpr int PB = LOSS_MAX_BLOCKS / 256, PI = LOSS_MAX_BLOCKS * 3 / 256;
+  __shared__ double red[4][6];
+  __shared__ int si[LOSS_MAX_BLOCKS * 3];
+  float v[PB][6];
+  int vi[PI];
+#pragma unroll
+  for (int i = 0; i < PB; ++i) {
+    const int k = tid + 256 * i;
+#pragma unroll
+    for (int j = 0; j < 6; ++j) v[i][j] = k < nblk ? g.fpart[k * 6 + j] : 0.f;
+  }
+#pragma unroll
+  for (int i = 0; i < PI; ++i) {
+    const int k = tid + 256 * i;
+    vi[i] = k < nblk * 3 ? g.ipart[k] : 0;
+  }
+#pragma unroll
+  for (int i = 0; i < PI; ++i) si[tid + 256 * i] = vi[i];
+  double s[6];
+#pragma unroll
+  for (int j = 0; j < 6; ++j) {
+    s[j] = 0.0;
+#pragma unroll
+    for (int i = 0; i < PB; ++i) s[j] += (double)v[i][j];
+    s[j] = wave_sum_d(s[j]);
+  }
+  const int lane = tid & 63, wave = tid >> 6;
+  if (lane == 0)
+#pragma unroll
+    for (int j = 0; j < 6; ++j) red[wave][j] = s[j];
+  __syncthreads();
+  {  // G lanes (a power of two <= 64) per sample, uniform trip count so the butterflies run with
+     // every lane active
+    const int bps = a.bands;
+    int G = 1;
+    while (G < 64 && g.B * G * 2 <= 256) G *= 2;
+    const int grp = tid / G, gl = tid % G, ngrp = 256 / G;
+    const int iters = (g.B + ngrp - 1) / ngrp;
+    for (int it = 0; it < iters; ++it) {
+      const int b = grp + it * ngrp;
+      int ci = 0, cp = 0, ct = 0;
+      if (b < g.B)
+        for (int k = gl; k < bps; k += G) {
+          const int blk = b * bps + k;
+          ci += si[blk * 3 + 0];
+          cp += si[blk * 3 + 1];
+          ct += si[blk * 3 + 2];
+        }
+      for (int off = 1; off < G; off <<= 1) {
+        ci += __shfl_xor(ci, off, 64);
+        cp += __shfl_xor(cp, off, 64);
+        ct += __shfl_xor(ct, off, 64);
+      }
+      if (gl == 0 && b < g.B) store_counts(a, b, ci, cp, ct);
+    }
+  }
+  if (tid == 0) {
+    double tot[6];
+#pragma unroll
+    for (int j = 0; j < 6; ++j) tot[j] = ((red[0][j] + red[1][j]) + red[2][j]) + red[3][j];
+    finalize_rows_store(g, tot, a.terms);
+  }
+}
+
+__device__ void finalize_rows_store(const LossArgs& g, const double* tot, float* terms) {
+  const double n = (double)g.B * g.H * g.W;
+  const double I = tot[0], P = tot[1], T = tot[2];
+  const double dice = 1.0 - (2.0 * I + g.smooth) / (P + T + g.smooth);
+  const double bce = tot[3] / n, rd = tot[4] / n, pf = tot[5] / n;
+  double total = g.dice_w * dice + g.bce_w * bce;
+  if (g.rd_w > 0.f) total += g.rd_w * rd;
+  if (g.pf_w > 0.f) total += g.pf_w * pf;
+  terms[0] = (float)total;
+  terms[1] = (float)dice;
+  terms[2] = (float)bce;
+  terms[3] = (float)rd;
+  terms[4] = (float)pf;
+  terms[5] = (float)I;
+  terms[6] = (float)P;
+  terms[7] = (float)T;
+}
+
+
+// rows per block of the whole-row forward
+// about 4 blocks per CU: enough row batches per thread that the waves of a SIMD drift out of
+// phase (loads of one overlapping arithmetic of another); 2048 blocks (2 batches) measured 15 %
+// slower at B = 64
+constexpr int LOSS_TARGET_BLOCKS = 1024;
 static int loss_rows(int B, int H, int W) {
-  int r = std::max(1, 4096 / W);
-  while ((int64_t)B * cdiv(H, r) > LOSS_MAX_BLOCKS) r *= 2;
+  // a multiple of RY x LOSS_ROW_BATCH rows (RY row segments per block) so no thread pads its last
+  // batch; at least as many rows as keep the block count near the target
+  const int ry = 256 / std::min(std::max(W / 4, 1), 256), q = ry * LOSS_ROW_BATCH;
+  int r = (int)std::max<int64_t>(q, cdiv((int64_t)B * H, LOSS_TARGET_BLOCKS));
+  r = (int)cdiv(r, q) * q * std::max(1, tune_get(PIS_TUNE_LOSS_ROWMUL));
   return std::min(r, H);
 }
 static bool loss_rows_ok(int B, int H, int W) {
@@ -839,8 +924,8 @@ static void loss_plan(int H, int W, int& tiles_x, int& tiles_y) {
 
 using namespace pis;
 
-// workspace: [16 B reserved][fpart: nblk x 6 floats][ipart: nblk x 3 ints], nblk = the larger
-// of the two plans
+// workspace: [16 B reserved][fpart: nblk x 6 floats][ipart: nblk x 3 ints], nblk = the larger of
+// the two plans; no state is carried between calls
 static int64_t loss_nblk(int B, int H, int W) {
   int tx, ty;
   loss_plan(H, W, tx, ty);
@@ -877,14 +962,13 @@ extern "C" int pis_loss_fwd(const float* p, const float* t, int B, int H, int W,
     a.bands = (int)cdiv(H, a.rows);
     a.terms = out_terms; a.counts = counts; a.scores = scores;
     const dim3 grid(a.bands, B);
-    const size_t smem = 0;
-    if (rd && pf) hipLaunchKernelGGL((loss_fwd_rows_kernel<true, true>), grid, dim3(256), smem, s, a);
-    else if (rd) hipLaunchKernelGGL((loss_fwd_rows_kernel<true, false>), grid, dim3(256), smem, s, a);
-    else if (pf) hipLaunchKernelGGL((loss_fwd_rows_kernel<false, true>), grid, dim3(256), smem, s, a);
-    else hipLaunchKernelGGL((loss_fwd_rows_kernel<false, false>), grid, dim3(256), smem, s, a);
+    if (rd && pf) hipLaunchKernelGGL((loss_fwd_rows_kernel<true, true>), grid, dim3(256), 0, s, a);
+    else if (rd) hipLaunchKernelGGL((loss_fwd_rows_kernel<true, false>), grid, dim3(256), 0, s, a);
+    else if (pf) hipLaunchKernelGGL((loss_fwd_rows_kernel<false, true>), grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((loss_fwd_rows_kernel<false, false>), grid, dim3(256), 0, s, a);
     const int rc = launch_status("loss_fwd_rows");
     if (rc) return rc;
-    hipLaunchKernelGGL(loss_finalize_rows_kernel, dim3(1), dim3(1024), 0, s, a);
+    hipLaunchKernelGGL(loss_finalize_rows_kernel, dim3(1), dim3(256), 0, s, a);
     return launch_status("loss_finalize");
   }
   loss_plan(H, W, g.tiles_x, g.tiles_y);

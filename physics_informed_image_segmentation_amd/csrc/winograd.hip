@@ -1568,6 +1568,7 @@ int launch_wino3x3(const IGemmArgs& a, int B, void* ws, hipStream_t s, float* ke
     launch_hook("wino_gemm_out", 0, s, flop);
     rc = launch_wino_gemm_out(V, Up, a, B, T, s);
     launch_hook("wino_gemm_out", 1, s, flop);
+    gemm_done(s);
     return rc;
   }
   if (v_ready && m != 4) return set_error("launch_wino3x3: prepared transforms need F(4x4,3x3)"), PIS_ERR_ARG;
@@ -1631,6 +1632,7 @@ int launch_wino3x3(const IGemmArgs& a, int B, void* ws, hipStream_t s, float* ke
   }
   launch_hook("wino_gemm", 1, s, flop);
   if (rc) return rc;
+  gemm_done(s);
   if (m == 4)
     launch_wino4_output(Mt, a, B, T, N, s);
   else

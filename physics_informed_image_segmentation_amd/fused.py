@@ -47,7 +47,7 @@ def _workspace(B: int, H: int, W: int, dev: torch.device) -> torch.Tensor:
     ws = _WS.get(key)
     if ws is None:
         n = _hip.lib().pis_loss_ws(B, H, W)
-        ws = torch.empty((n + 3) // 4, dtype=torch.float32, device=dev)
+        ws = torch.zeros((n + 3) // 4, dtype=torch.float32, device=dev)  # zeroed once (pis_capi.h)
         _WS[key] = ws
     return ws
 

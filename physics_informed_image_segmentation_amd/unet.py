@@ -316,6 +316,10 @@ class UNetEngine:
     # transforms are HBM-bound while the weight-gradient GEMMs are MFMA-bound
     # (PIS_SIDE_STREAM=0 serialises them on the caller's stream, for A/B measurements)
     side_stream = os.environ.get("PIS_SIDE_STREAM", "1") != "0"
+    # where a prepared layer's weight gradient joins the side stream (tools/ab_streams.py): "prep"
+    # right after dz's transforms, "gemm" after the input gradient's contractions, "dgrad" after
+    # the whole input gradient
+    side_sync = os.environ.get("PIS_SIDE_SYNC", "prep")
 
     def __init__(self, model: UNet):
         self.m = model
@@ -608,16 +612,17 @@ class UNetEngine:
                 if prep:
                     nprep[0] += 1
                     wsw, wswb = self.ws3[j].data_ptr(), self.ws3_bytes
-            to_side()
-            call("pis_conv3x3_wgrad_keep", x.p, x.ld, dz.p, dz.ld, self._gptr(conv.weight), self._gptr(conv.bias),
-                 B, Hl, Wl, conv.in_channels, conv.out_channels, acc | (PIS_WINO_PREPARED if prep else 0), wsw, wswb,
-                 ptr(kept), sst)
-            if prep and side is not main:
-                ev = torch.cuda.Event()
-                ev.record(side)
-                self.ws3_free[(nprep[0] - 1) & 1] = ev
-            ready_on_side(conv.weight, conv.bias)
-            if dx is not None:
+            def wgrad():
+                call("pis_conv3x3_wgrad_keep", x.p, x.ld, dz.p, dz.ld, self._gptr(conv.weight),
+                     self._gptr(conv.bias), B, Hl, Wl, conv.in_channels, conv.out_channels,
+                     acc | (PIS_WINO_PREPARED if prep else 0), wsw, wswb, ptr(kept), sst)
+                if prep and side is not main:
+                    ev = torch.cuda.Event()
+                    ev.record(side)
+                    self.ws3_free[(nprep[0] - 1) & 1] = ev
+                ready_on_side(conv.weight, conv.bias)
+
+            def dgrad():
                 flags = (PIS_MASK if mask is not None else 0) | (PIS_SCALE if scale is not None else 0)
                 if prep:
                     wf, flags = conv.weight.data_ptr(), flags | PIS_WINO_PREPARED | PIS_W_UNFLIPPED
@@ -626,6 +631,26 @@ class UNetEngine:
                 call("pis_conv3x3_dgrad_ex", dz.p, dz.ld, wf,
                      mask.p if mask is not None else 0, mask.ld if mask is not None else 0, ptr(scale),
                      dx.p, dx.ld, B, Hl, Wl, conv.in_channels, conv.out_channels, flags, ws, wsb, st)
+
+            sync = self.side_sync if (prep and dx is not None and side is not main) else "prep"
+            if sync == "prep":  # the weight gradient starts as soon as dz's transforms exist
+                to_side()
+                wgrad()
+                if dx is not None:
+                    dgrad()
+                return
+            # the weight gradient (MFMA-bound) starts after the input gradient's contractions
+            # ("gemm": overlapping the HBM-bound output transform) or after the whole input
+            # gradient ("dgrad"); it only needs dz's transforms, which precede either point
+            ev = torch.cuda.Event()
+            ev.record(main)
+            if sync == "gemm":
+                lib.pis_arm_gemm_event(ev.cuda_event)
+            dgrad()
+            if sync != "gemm" or lib.pis_arm_gemm_event(None):
+                ev.record(main)
+            side.wait_event(ev)
+            wgrad()
 
         # head: sigmoid backward + 1x1 conv + ReLU backward of dec1.conv1
         d1 = _Buf(bf["d1_1"], c)

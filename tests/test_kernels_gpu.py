@@ -427,15 +427,16 @@ def test_fused_loss_vs_oracle(hip, shape, kw):
     np.testing.assert_allclose(scores.numpy(), np.stack([d, u], 1), rtol=1e-6)
 
 
-@pytest.mark.parametrize("shape", [(16, 512, 512), (3, 130, 68), (2, 2, 8), (1, 37, 1024), (5, 64, 4096)])
-def test_loss_fwd_row_bands_match_tile_path(hip, shape):
+@pytest.mark.parametrize("shape", [(16, 512, 512), (3, 130, 68), (2, 2, 8), (1, 37, 1024), (5, 64, 4096), (4, 5, 20), (64, 512, 512)])
+@pytest.mark.parametrize("terms", [(1e-4, 1e-4), (0.0, 0.0), (1e-4, 0.0), (0.0, 1e-4)])
+def test_loss_fwd_row_bands_match_tile_path(hip, shape, terms):
     """The whole-row forward (PIS_TUNE_LOSS_ROWS = 1) and the 16x128-tile forward give the same
     terms and exactly the same counters; repeated launches on one workspace are bitwise identical
     (fixed-order reductions)."""
     g = torch.Generator().manual_seed(12)
     p = 0.02 + 0.96 * torch.rand(shape, generator=g)
     t = (torch.rand(shape, generator=g) > 0.8).float()
-    kw = dict(rd_w=1e-4, pf_w=1e-4, D=5.0, a=0.5, eps=0.05)
+    kw = dict(rd_w=terms[0], pf_w=terms[1], D=5.0, a=0.5, eps=0.05)
     prev = hip.pis_tune(18, 0)
     try:
         ref = _loss_call(hip, p, t, kw)

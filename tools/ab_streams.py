@@ -3,6 +3,8 @@
   default   : main = torch's current stream, weight gradients on a side stream (priority 0)
   main_hi   : the whole step inside a high-priority stream, side stream at normal priority
   serial    : weight gradients serialised on the main stream (no side stream)
+  sync_gemm : a prepared layer's weight gradient waits for the input gradient's contractions
+  sync_dgrad: ... waits for the whole input gradient (PIS_SIDE_SYNC, unet.py conv_bwd)
 
     python tools/ab_streams.py [--rounds 4] [--steps 10]
 """
@@ -45,7 +47,9 @@ def main():
 
     def run(variant):
         eng = model.engine()
-        side = eng.side
+        side, sync = eng.side, eng.side_sync
+        if variant.startswith("sync_"):
+            eng.side_sync = variant[5:]
         if variant == "serial":
             eng.side = None
         ctx = torch.cuda.stream(hi_stream) if variant == "main_hi" else torch.cuda.stream(torch.cuda.current_stream())
@@ -57,16 +61,16 @@ def main():
                 step()
             torch.cuda.synchronize()
             dt = time.perf_counter() - t0
-        eng.side = side
+        eng.side, eng.side_sync = side, sync
         return dt / args.steps * 1e3
 
     res = {}
     for _ in range(args.rounds):
-        for v in ("default", "main_hi", "serial"):
+        for v in ("default", "main_hi", "serial", "sync_gemm", "sync_dgrad"):
             res.setdefault(v, []).append(run(v))
     for v, ms in res.items():
         ms.sort()
-        print(f"{v:8s} ms/step median {ms[len(ms) // 2]:.2f}  min {ms[0]:.2f}  -> {8e3 / ms[len(ms) // 2]:.1f} img/s",
+        print(f"{v:10s} ms/step median {ms[len(ms) // 2]:.2f}  min {ms[0]:.2f}  -> {8e3 / ms[len(ms) // 2]:.1f} img/s",
               flush=True)
 
 

@@ -1,6 +1,6 @@
 """Fused PDE-loss kernel micro-benchmark (C2: B=8, 512x512, Stage-II weights).
 
-Times pis_loss_fwd (tile kernel + finalize) and pis_loss_bwd with HIP events and
+Times pis_loss_fwd (one launch: whole-row bands, the last block reduces) and pis_loss_bwd with HIP events and
 prints algorithmic HBM GB/s: forward reads p and t (8 B/px), backward reads p, t
 and writes dL/dz (12 B/px).
 
@@ -25,8 +25,19 @@ def main():
     ap.add_argument("--reps", type=int, default=50)
     ap.add_argument("--rd", type=float, default=1e-4)
     ap.add_argument("--pf", type=float, default=1e-4)
+    ap.add_argument("--modes", default="", help="comma list of PIS_TUNE_LOSS_ROWS[:ROWMUL] values to time")
     args = ap.parse_args()
     lib = _hip.lib()
+    for mode in [m for m in args.modes.split(",") if m] or [None]:
+        if mode is not None:
+            rows, _, mul = mode.partition(":")
+            lib.pis_tune(18, int(rows))
+            lib.pis_tune(19, int(mul or 1))
+            print(f"-- PIS_TUNE_LOSS_ROWS = {rows}, ROWMUL = {mul or 1}", flush=True)
+        run(lib, args, fwd_only=mode is not None)
+
+
+def run(lib, args, fwd_only=False):
     B, H, W = args.B, args.H, args.W
     s = torch.cuda.current_stream().cuda_stream
     g = torch.Generator(device="cuda").manual_seed(0)
@@ -39,7 +50,10 @@ def main():
     nws = lib.pis_loss_ws(B, H, W)
     ws = torch.zeros(nws // 4 + 1, device="cuda")
     dst = torch.empty(B, H, W, device="cuda")
-    flush = torch.empty(512 * 1024 * 1024 // 4, device="cuda")  # 512 MB: evict L2 + MALL between reps
+    # 1 GiB READ between reps: evicts L2 + Infinity Cache with clean lines (a write-flush leaves
+    # ~256 MB of dirty lines whose write-back then competes with the timed kernel)
+    flush = torch.ones(256 << 20, device="cuda")
+    sink = torch.empty((), device="cuda")
 
     def fwd():
         lib.pis_loss_fwd(p.data_ptr(), t.data_ptr(), B, H, W, ctypes.byref(prm), terms.data_ptr(),
@@ -50,13 +64,13 @@ def main():
                          dst.data_ptr(), 2, s)
 
     npx = B * H * W
-    for name, fn, nbytes in (("loss_fwd+finalize", fwd, 8 * npx), ("loss_bwd", bwd, 12 * npx)):
+    for name, fn, nbytes in (("loss_fwd", fwd, 8 * npx), ("loss_bwd", bwd, 12 * npx))[:1 if fwd_only else 2]:
         for cold in (False, True):
             fn()
             ms = []
             for _ in range(args.reps):
                 if cold:
-                    flush.zero_()
+                    torch.sum(flush, dim=0, out=sink)
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
                 fn()

@@ -19,9 +19,11 @@ for x in "$@"; do
   case $x in
     ab) run ab_streams 300 python -u tools/ab_streams.py --rounds 4 --steps 10 ;;
     loss) run loss_b64 120 python -u tools/bench_loss.py --B 64; run loss_c2 120 python -u tools/bench_loss.py --B 8 ;;
+    lossmodes) run lossmodes_b64 120 python -u tools/bench_loss.py --B 64 --modes 0,1,2,1:2,1:4,2:2,2:4; run lossmodes_c2 120 python -u tools/bench_loss.py --B 8 --modes 0,1,2,1:2,2:2 ;;
     bench) run bench 300 python -u bench.py --no-cpu-baseline ;;
     gemm) run bench_gemm 300 python -u tools/bench_gemm.py --variants 6,8,9 --rounds 3 --check ;;
     lossprof) run lossprof 200 rocprofv3 --kernel-trace --stats -d "$OUT/lossprof" -o run --output-format csv -- python3 tools/bench_loss.py --B 64 --reps 20 ;;
+    lossprof8) run lossprof8 200 rocprofv3 --kernel-trace --stats -d "$OUT/lossprof8" -o run --output-format csv -- python3 tools/bench_loss.py --B 8 --reps 20 ;;
   esac
 done
 echo "== quick done"
