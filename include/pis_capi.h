@@ -86,7 +86,9 @@ int pis_version(void);
                                     both followed by the one-block fixed-order finalize (deterministic) */
 #define PIS_TUNE_LOSS_ROWMUL 19  /* whole-row loss forward: rows per block multiplier (1 default: the most blocks
                                     up to 2048; 2, 4: fewer blocks, more row batches per thread) */
-#define PIS_TUNE_NKEYS 20
+#define PIS_TUNE_SLAB_CHUNKS 20  /* thousands of partial slabs over <= 1024 columns (bias gradients): 1 (default)
+                                    two-pass chunked row reduction, 0 one column per block */
+#define PIS_TUNE_NKEYS 21
 #define PIS_DEBUG_NOLOAD (1 << 16)
 int pis_tune(int key, int value);
 /* Tooling (tools/bench_gemm.py): time one batched NT GEMM kernel variant in isolation,

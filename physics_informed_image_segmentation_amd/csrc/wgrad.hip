@@ -384,7 +384,52 @@ int reduce_slabs_pitched(const float* part, int splits, int64_t n, int64_t pitch
   return launch_status("reduce_slabs");
 }
 
+// Thousands of slabs over a few columns (the per-block bias partials of the dz transforms: 8192
+// slabs x 64 channels at 512^2): pass 1 lets block g sum a contiguous chunk of slabs with
+// coalesced row reads (n/4 float4 lanes per row, 256/(n/4) rows in flight) and writes its sum
+// over the FIRST slab of its own chunk (which only it reads); pass 2 is the pitched reduction of
+// those G rows. Both orders are fixed: deterministic. (One column per block across all slabs
+// fetched each 128-B line once per float4 column: 30-50 us per bias at 512^2.)
+__global__ __launch_bounds__(256) void reduce_rows_chunk_kernel(float* __restrict__ part, int splits, int n4,
+                                                                int chunk) {
+  const int R = 256 / n4, r = threadIdx.x / n4, c = threadIdx.x - r * n4;
+  const int s0 = blockIdx.x * chunk, s1 = min(splits, s0 + chunk);
+  const int64_t n = 4 * (int64_t)n4;
+  f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = a0, a2 = a0, a3 = a0;  // four chains: loads in flight
+  if (r < R) {
+    int k = s0 + r;
+    for (; k + 3 * R < s1; k += 4 * R) {
+      a0 += *reinterpret_cast<const f32x4*>(part + (int64_t)k * n + 4 * c);
+      a1 += *reinterpret_cast<const f32x4*>(part + (int64_t)(k + R) * n + 4 * c);
+      a2 += *reinterpret_cast<const f32x4*>(part + (int64_t)(k + 2 * R) * n + 4 * c);
+      a3 += *reinterpret_cast<const f32x4*>(part + (int64_t)(k + 3 * R) * n + 4 * c);
+    }
+    if (k < s1) a0 += *reinterpret_cast<const f32x4*>(part + (int64_t)k * n + 4 * c);
+    if (k + R < s1) a1 += *reinterpret_cast<const f32x4*>(part + (int64_t)(k + R) * n + 4 * c);
+    if (k + 2 * R < s1) a2 += *reinterpret_cast<const f32x4*>(part + (int64_t)(k + 2 * R) * n + 4 * c);
+  }
+  __shared__ f32x4 red[256];
+  red[threadIdx.x] = (a0 + a1) + (a2 + a3);
+  __syncthreads();  // every read of this chunk is done before its first slab is overwritten
+  if (r == 0) {
+    f32x4 t = red[c];
+    for (int q = 1; q < R; ++q) t += red[q * n4 + c];
+    *reinterpret_cast<f32x4*>(part + (int64_t)s0 * n + 4 * c) = t;
+  }
+}
+
+// NOTE: may overwrite part (every caller passes its own partial-slab scratch)
 int reduce_slabs(const float* part, int splits, int64_t n, float* dst, int accumulate, hipStream_t s) {
+  const bool v4 = (n % 4 == 0) && ((uintptr_t)part % 16 == 0) && ((uintptr_t)dst % 16 == 0);
+  if (v4 && splits >= 1024 && n <= 1024 && tune_get(PIS_TUNE_SLAB_CHUNKS) != 0) {
+    const int G = std::min(256, splits / 16);
+    const int chunk = (int)cdiv(splits, G), nblk = (int)cdiv(splits, chunk);
+    hipLaunchKernelGGL(reduce_rows_chunk_kernel, dim3(nblk), dim3(256), 0, s, const_cast<float*>(part), splits,
+                       (int)(n / 4), chunk);
+    const int rc = launch_status("reduce_rows_chunk");
+    if (rc) return rc;
+    return reduce_slabs_pitched(part, nblk, n, (int64_t)chunk * n, dst, accumulate, s);
+  }
   return reduce_slabs_pitched(part, splits, n, n, dst, accumulate, s);
 }
 

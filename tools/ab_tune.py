@@ -1,0 +1,74 @@
+"""A/B of pis_tune settings on the C2 training step, interleaved rounds in one process on one
+GPU (box-to-box variance is ~3 %; same-process interleaving is not).
+
+    python tools/ab_tune.py --variants "base;20=0;15=0,17=4" [--rounds 4] [--steps 10]
+
+Each variant is a comma list of KEY=VALUE (include/pis_capi.h PIS_TUNE_*); "base" = defaults.
+"""
+import argparse
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from physics_informed_image_segmentation_amd import AdamW, DiceBCEPDELoss, UNet, _hip  # noqa: E402
+from physics_informed_image_segmentation_amd.dataset import disc_sample  # noqa: E402
+
+
+def parse(v):
+    if v.strip() in ("", "base"):
+        return {}
+    return {int(k): int(x) for k, x in (kv.split("=") for kv in v.split(","))}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--variants", required=True)
+    ap.add_argument("--rounds", type=int, default=4)
+    ap.add_argument("--steps", type=int, default=10)
+    args = ap.parse_args()
+    lib = _hip.lib()
+    variants = [(v.strip(), parse(v)) for v in args.variants.split(";")]
+    keys = sorted({k for _, kv in variants for k in kv})
+    defaults = {k: lib.pis_tune(k, -1) for k in keys}
+    dev = torch.device("cuda")
+    g = torch.Generator().manual_seed(42)
+    imgs, masks = zip(*[disc_sample(512, 512, g) for _ in range(8)])
+    x, t = torch.stack(imgs).to(dev), torch.stack(masks).to(dev)
+    torch.manual_seed(42)
+    model = UNet(1, 1, 64).to(dev).train()
+    crit = DiceBCEPDELoss(pde_weight=1e-4, phase_field_weight=1e-4, diffusion_coeff=5.0, epsilon=0.05)
+    opt = AdamW(model.parameters(), lr=1e-5, weight_decay=1e-5)
+
+    def step():
+        opt.zero_grad()
+        crit(model(x), t).backward()
+        opt.step()
+
+    def run(kv):
+        for k in keys:
+            lib.pis_tune(k, kv.get(k, defaults[k]))
+        step()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) / args.steps * 1e3
+
+    res = {}
+    for _ in range(args.rounds):
+        for name, kv in variants:
+            res.setdefault(name, []).append(run(kv))
+    for k in keys:
+        lib.pis_tune(k, defaults[k])
+    for name, ms in res.items():
+        ms.sort()
+        med = ms[len(ms) // 2]
+        print(f"{name:16s} ms/step median {med:.2f}  min {ms[0]:.2f}  -> {8e3 / med:.1f} img/s", flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -29,7 +29,7 @@ def read(paths):
     for path in paths:
         for r in csv.DictReader(open(path)):
             name = r["Kernel_Name"]
-            if "pis::" not in name:
+            if "pis::" not in name and "_ZN3pis" not in name:  # some names arrive mangled
                 continue
             acc[name][r["Counter_Name"]].append(float(r["Counter_Value"]))
     return {k: {c: (sum(v) / len(v), len(v)) for c, v in cs.items()} for k, cs in acc.items()}
