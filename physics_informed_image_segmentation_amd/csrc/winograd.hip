@@ -1294,7 +1294,12 @@ template <int NWN, int NWT, int KC>
 __global__ __launch_bounds__(64 * NWN * NWT) void wino4_gemm_out_x6_kernel(const float* __restrict__ V,
                                                                           const __bf16* __restrict__ Up,
                                                                           IGemmArgs g, int B) {
-  constexpr int NT = 64 * NWN * NWT, TB = 16 * NWT, NN = 16 * NWN, KP = KC + 8;  // KP: LDS row pitch (bf16)
+  constexpr int NT = 64 * NWN * NWT, TB = 16 * NWT, NN = 16 * NWN, KP = KC;  // KP: LDS row pitch (bf16)
+  // unpadded rows, 16-B chunks XOR-swizzled by (row / 2) % 8: every ds_read_b128 lane group (16
+  // rows of one 16-row window, two adjacent chunks) hits 16 distinct slots of the 256-B bank row;
+  // without the 8-element padding a block needs 72 KB of LDS, so two blocks share a CU
+  static_assert(KC == 64, "the swizzle spans 8 chunks of 8 bf16");
+  auto sw = [](int row, int k) { return row * KP + ((((k >> 3) ^ ((row >> 1) & 7)) << 3) | (k & 7)); };
   constexpr int NV4 = TB * KC / 4, AL = (NV4 + NT - 1) / NT;  // float4 of V[xi] per thread
   constexpr bool VPART = NV4 % NT != 0;                         // (then NV4 < NT: some threads idle)
   constexpr int NU8 = 3 * NN * KC / 8, UL = NU8 / NT;          // 16-B chunks of the U[xi] planes per thread
@@ -1326,9 +1331,9 @@ __global__ __launch_bounds__(64 * NWN * NWT) void wino4_gemm_out_x6_kernel(const
       const int row = idx / (KC / 4), c = 4 * (idx % (KC / 4));
       u32x2 h, m, l;
       split3_x4(r[i], h, m, l);
-      *reinterpret_cast<u32x2*>(&sA[buf][0][row * KP + c]) = h;
-      *reinterpret_cast<u32x2*>(&sA[buf][1][row * KP + c]) = m;
-      *reinterpret_cast<u32x2*>(&sA[buf][2][row * KP + c]) = l;
+      *reinterpret_cast<u32x2*>(&sA[buf][0][sw(row, c)]) = h;
+      *reinterpret_cast<u32x2*>(&sA[buf][1][sw(row, c)]) = m;
+      *reinterpret_cast<u32x2*>(&sA[buf][2][sw(row, c)]) = l;
     }
   };
   u32x4 ur[2][UL];
@@ -1346,7 +1351,7 @@ __global__ __launch_bounds__(64 * NWN * NWT) void wino4_gemm_out_x6_kernel(const
       const int c = tid + i * NT;
       const int pl = c / (NN * KC / 8), rem = c % (NN * KC / 8);
       const int row = rem / (KC / 8), k = 8 * (rem % (KC / 8));
-      *reinterpret_cast<u32x4*>(&sU[buf][pl][row * KP + k]) = r[i];
+      *reinterpret_cast<u32x4*>(&sU[buf][pl][sw(row, k)]) = r[i];
     }
   };
   f32x4 y[4][4], rr[4];
@@ -1377,8 +1382,8 @@ __global__ __launch_bounds__(64 * NWN * NWT) void wino4_gemm_out_x6_kernel(const
         bf16x8g af[3], bf[3];
 #pragma unroll
         for (int p = 0; p < 3; ++p) {
-          af[p] = *reinterpret_cast<const bf16x8g*>(&sA[cur][p][(16 * wt + lr) * KP + k]);
-          bf[p] = *reinterpret_cast<const bf16x8g*>(&sU[cur][p][n * KP + k]);
+          af[p] = *reinterpret_cast<const bf16x8g*>(&sA[cur][p][sw(16 * wt + lr, k)]);
+          bf[p] = *reinterpret_cast<const bf16x8g*>(&sU[cur][p][sw(n, k)]);
         }
         // smallest partial products first
         acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[2], bf[0], acc, 0, 0, 0);
