@@ -1022,17 +1022,23 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_x6_kernel(
     }
 }
 
+__device__ __forceinline__ int x6w8_off(int row, int chunk) {  // bf16 element offset of a 16-B chunk
+  return row * 32 + 8 * (chunk ^ ((row >> 2) & 3));
+}
+
 // K-step 32 variant of gemm_nt_x6_kernel with ONE LDS buffer (48 KB at 128 x 128, so three
 // blocks still fit a CU): compute, barrier, store the next stage, barrier, issue the loads of
 // the stage after — a load has a whole 48-MFMA compute phase to land, and every 128-B line a
-// wave touches is consumed in the same stage. LDS rows padded to 40 bf16 (80 B: conflict-free
-// 16-B fragment reads).
+// wave touches is consumed in the same stage. LDS rows are 64 B (32 bf16) with the 16-B chunk
+// XOR-swizzled by row bits 2..3 (x6w8_off): conflict-free ds_read_b128 fragments AND ds_write_b64
+// staging (two rows = 128 contiguous bytes), and 48 KB per 128 x 128 block, so three blocks fit a
+// CU (80-B padded rows: 60 KB, two blocks, and 2-way conflicted staging stores).
 template <int BM, int BN, int OCC = 2>
 __global__ __launch_bounds__(256, OCC) void gemm_nt_x6_bk32_kernel(const float* __restrict__ A,
                                                                 const float* __restrict__ Bm, float* __restrict__ Cm,
                                                                 int M, int N, int K, int64_t bsA, int64_t bsB,
                                                                 int64_t bsC) {
-  constexpr int BK = 32, KP = 40;
+  constexpr int BK = 32, KP = 32;
   constexpr int TM = BM / 64, TN = BN / 64;
   constexpr int AL = BM * 8 / 256, BL = BN * 8 / 256;  // float4 loads per thread per stage
   __shared__ __attribute__((aligned(16))) __bf16 sA[3][BM * KP];
@@ -1068,7 +1074,7 @@ __global__ __launch_bounds__(256, OCC) void gemm_nt_x6_bk32_kernel(const float* 
     for (int i = 0; i < AL; ++i) {
       u32x2 h, m, l;
       split3_x4(ra[i], h, m, l);
-      const int o = ((tid + i * 256) / 8) * KP + q8;
+      const int row = (tid + i * 256) / 8, o = x6w8_off(row, q8 >> 3) + (q8 & 7);
       *reinterpret_cast<u32x2*>(&sA[0][o]) = h;
       *reinterpret_cast<u32x2*>(&sA[1][o]) = m;
       *reinterpret_cast<u32x2*>(&sA[2][o]) = l;
@@ -1077,7 +1083,7 @@ __global__ __launch_bounds__(256, OCC) void gemm_nt_x6_bk32_kernel(const float* 
     for (int i = 0; i < BL; ++i) {
       u32x2 h, m, l;
       split3_x4(rb[i], h, m, l);
-      const int o = ((tid + i * 256) / 8) * KP + q8;
+      const int row = (tid + i * 256) / 8, o = x6w8_off(row, q8 >> 3) + (q8 & 7);
       *reinterpret_cast<u32x2*>(&sB[0][o]) = h;
       *reinterpret_cast<u32x2*>(&sB[1][o]) = m;
       *reinterpret_cast<u32x2*>(&sB[2][o]) = l;
@@ -1103,10 +1109,10 @@ __global__ __launch_bounds__(256, OCC) void gemm_nt_x6_bk32_kernel(const float* 
       for (int p = 0; p < 3; ++p) {
 #pragma unroll
         for (int a = 0; a < TM; ++a)
-          af[p][a] = *reinterpret_cast<const bf16x8*>(&sA[p][(wm * (BM / 2) + a * 32 + li) * KP + 16 * ks + 8 * lh]);
+          af[p][a] = *reinterpret_cast<const bf16x8*>(&sA[p][x6w8_off(wm * (BM / 2) + a * 32 + li, 2 * ks + lh)]);
 #pragma unroll
         for (int b = 0; b < TN; ++b)
-          bf[p][b] = *reinterpret_cast<const bf16x8*>(&sB[p][(wn * (BN / 2) + b * 32 + li) * KP + 16 * ks + 8 * lh]);
+          bf[p][b] = *reinterpret_cast<const bf16x8*>(&sB[p][x6w8_off(wn * (BN / 2) + b * 32 + li, 2 * ks + lh)]);
       }
 #pragma unroll
       for (int a = 0; a < TM; ++a)
@@ -1148,9 +1154,6 @@ __global__ __launch_bounds__(256, OCC) void gemm_nt_x6_bk32_kernel(const float* 
 // load has a whole K-step of MFMAs (96 per SIMD) to land. LDS rows are 64 B (32 bf16) with the 16-B chunk XOR-swizzled by row bits
 // 2..3 (chunk ^= (row >> 2) & 3), so the 16 rows a ds_read_b128 lane group reads at one chunk
 // hit 16 distinct bank quads: 2 buffers x 3 planes x 384 rows x 64 B = 147 KB.
-__device__ __forceinline__ int x6w8_off(int row, int chunk) {  // bf16 element offset of a 16-B chunk
-  return row * 32 + 8 * (chunk ^ ((row >> 2) & 3));
-}
 
 template <int DBG = 0>
 __global__ __launch_bounds__(512, 1) void gemm_nt_x6_w8_kernel(const float* __restrict__ A,
