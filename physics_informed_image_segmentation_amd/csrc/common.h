@@ -74,6 +74,15 @@ __device__ __forceinline__ void split3_x4(f32x4 v, u32x2& h, u32x2& m, u32x2& l)
   l = u32x2{l0, l1};
 }
 
+// LDS element offset of (row, k) in a [row][16 k] bf16 plane: the two 16-B chunks of a row are
+// swapped on rows where bit 2 ^ bit 3 of the row is set, so the 16 rows a ds_read_b128 lane group
+// reads at one chunk hit 16 distinct slots of the 256-B bank row, and 8 consecutive rows written
+// by a ds_write_b128 group hit 8 distinct slots of the 128-B write bank row (unswizzled 32-B rows:
+// 2-way on both)
+__device__ __forceinline__ int wsw(int row, int k) {
+  return row * 16 + ((((k >> 3) ^ ((row >> 2) ^ (row >> 3))) & 1) << 3) + (k & 7);
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);

@@ -99,7 +99,7 @@ __global__ __launch_bounds__(256, 2) void convt_gemm_kernel(ConvtGemmArgs g) {
       for (int i = 0; i < AL; ++i) {
         u32x2 h, m, l;
         split3_x4(ra[i], h, m, l);
-        const int o = ((tid + i * 256) / 4) * BK + q4;
+        const int o = wsw((tid + i * 256) / 4, q4);  // swizzled rows: conflict-free fragment reads
         *reinterpret_cast<u32x2*>(pa + o) = h;
         *reinterpret_cast<u32x2*>(pa + BM * BK + o) = m;
         *reinterpret_cast<u32x2*>(pa + 2 * BM * BK + o) = l;
@@ -108,7 +108,7 @@ __global__ __launch_bounds__(256, 2) void convt_gemm_kernel(ConvtGemmArgs g) {
       for (int i = 0; i < BL; ++i) {
         u32x2 h, m, l;
         split3_x4(rb[i], h, m, l);
-        const int o = ((tid + i * 256) / 4) * BK + q4;
+        const int o = wsw((tid + i * 256) / 4, q4);
         *reinterpret_cast<u32x2*>(pb + o) = h;
         *reinterpret_cast<u32x2*>(pb + BN * BK + o) = m;
         *reinterpret_cast<u32x2*>(pb + 2 * BN * BK + o) = l;
@@ -142,10 +142,10 @@ __global__ __launch_bounds__(256, 2) void convt_gemm_kernel(ConvtGemmArgs g) {
       for (int p = 0; p < 3; ++p) {
 #pragma unroll
         for (int a = 0; a < 2; ++a)
-          af[p][a] = *reinterpret_cast<const cbf16x8*>(pa + p * BM * BK + (wm * 64 + a * 32 + li) * BK + 8 * lh);
+          af[p][a] = *reinterpret_cast<const cbf16x8*>(pa + p * BM * BK + wsw(wm * 64 + a * 32 + li, 8 * lh));
 #pragma unroll
         for (int b = 0; b < 2; ++b)
-          bf[p][b] = *reinterpret_cast<const cbf16x8*>(pb + p * BN * BK + (wn * 64 + b * 32 + li) * BK + 8 * lh);
+          bf[p][b] = *reinterpret_cast<const cbf16x8*>(pb + p * BN * BK + wsw(wn * 64 + b * 32 + li, 8 * lh));
       }
 #pragma unroll
       for (int a = 0; a < 2; ++a)

@@ -634,8 +634,8 @@ __global__ __launch_bounds__(256, 2) void wgrad_x6_kernel(WgradArgs g) {
 #pragma unroll
       for (int e = 0; e < EA; ++e) bsum += ra[e];
     }
-    wsplit_store<EA>(ra, &sA[buf][0][am * BK + ap], &sA[buf][1][am * BK + ap], &sA[buf][2][am * BK + ap]);
-    wsplit_store<EB>(rb, &sB[buf][0][bn * BK + bp], &sB[buf][1][bn * BK + bp], &sB[buf][2][bn * BK + bp]);
+    wsplit_store<EA>(ra, &sA[buf][0][wsw(am, ap)], &sA[buf][1][wsw(am, ap)], &sA[buf][2][wsw(am, ap)]);
+    wsplit_store<EB>(rb, &sB[buf][0][wsw(bn, bp)], &sB[buf][1][wsw(bn, bp)], &sB[buf][2][wsw(bn, bp)]);
   };
   f32x16 acc[TM][TN];
 #pragma unroll
@@ -658,10 +658,10 @@ __global__ __launch_bounds__(256, 2) void wgrad_x6_kernel(WgradArgs g) {
     for (int pl = 0; pl < 3; ++pl) {
 #pragma unroll
       for (int a = 0; a < TM; ++a)
-        af[pl][a] = *reinterpret_cast<const wbf16x8*>(&sA[cur][pl][(wm * (BM / 2) + a * 32 + li) * BK + 8 * lh]);
+        af[pl][a] = *reinterpret_cast<const wbf16x8*>(&sA[cur][pl][wsw(wm * (BM / 2) + a * 32 + li, 8 * lh)]);
 #pragma unroll
       for (int b = 0; b < TN; ++b)
-        bf[pl][b] = *reinterpret_cast<const wbf16x8*>(&sB[cur][pl][(wn * (BN / 2) + b * 32 + li) * BK + 8 * lh]);
+        bf[pl][b] = *reinterpret_cast<const wbf16x8*>(&sB[cur][pl][wsw(wn * (BN / 2) + b * 32 + li, 8 * lh)]);
     }
 #pragma unroll
     for (int a = 0; a < TM; ++a)
