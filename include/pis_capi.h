@@ -88,7 +88,11 @@ int pis_version(void);
                                     up to 2048; 2, 4: fewer blocks, more row batches per thread) */
 #define PIS_TUNE_SLAB_CHUNKS 20  /* thousands of partial slabs over <= 1024 columns (bias gradients): 1 (default)
                                     two-pass chunked row reduction, 0 one column per block */
-#define PIS_TUNE_NKEYS 21
+#define PIS_TUNE_WGRAD_PAIR 21   /* bf16x6 weight-gradient GEMM, 64-wide operand tiles: 0 (default) one 4-pixel run per
+                                    lane (2-way conflicted ds_write_b64), 1 lane pairs stage the two 8-B halves of one 16-B
+                                    chunk (conflict-free; the two 128-B pixel rows per load cost more: enc1.conv1 -4 %, up1
+                                    +9 %, step -0.4 %) */
+#define PIS_TUNE_NKEYS 22
 #define PIS_DEBUG_NOLOAD (1 << 16)
 int pis_tune(int key, int value);
 /* Tooling (tools/bench_gemm.py): time one batched NT GEMM kernel variant in isolation,

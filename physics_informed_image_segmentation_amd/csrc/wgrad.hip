@@ -34,6 +34,7 @@ struct WgradArgs {
   float* part_bias;                              // [splits][Mp] or NULL
   // batched launches (gridDim.y > 1, Winograd's 16 GEMMs): per-batch offsets; slab pitch
   int64_t bs_a, bs_b, bs_part, split_stride;     // split_stride 0 = Mp * Np
+  int pair;                                      // wgrad_x6: pair-lane staging of 4-pixel operands
 };
 
 // BKP pixels per stage: 32 MFMAs per wave between barriers for every tile shape
@@ -598,8 +599,15 @@ __global__ __launch_bounds__(256, 2) void wgrad_x6_kernel(WgradArgs g) {
   const int m0 = (tile / ntn) * BM, n0 = (tile % ntn) * BN;
   const int p_begin = split * g.pix_per_split;
   const int p_end = min(g.P, p_begin + g.pix_per_split);
-  const int am = tid % BM, ap = (tid / BM) * EA;  // this thread's column and pixel offset
-  const int bn = tid % BN, bp = (tid / BN) * EB;
+  // this thread's column and pixel offset. g.pair (pis_tune 21, off by default): with 4 pixels
+  // per thread (64-wide tiles) the two lanes of a pair take the two 8-B halves of one 16-B chunk
+  // of one row, so a ds_write_b64 lane group covers 8 rows x 16 B: with the row swizzle, 16
+  // distinct 8-B slots (one pixel group per lane: 2-way conflicts, but better-coalesced loads)
+  const bool pa = EA == 4 && g.pair, pb = EB == 4 && g.pair;
+  const int am = pa ? (tid >> 1) % BM : tid % BM;
+  const int ap = pa ? 8 * (tid / (2 * BM)) + 4 * (tid & 1) : (tid / BM) * EA;
+  const int bn = pb ? (tid >> 1) % BN : tid % BN;
+  const int bp = pb ? 8 * (tid / (2 * BN)) + 4 * (tid & 1) : (tid / BN) * EB;
   const bool do_bias = g.part_bias != nullptr && n0 == 0;
   // a_up2 (transposed-conv weight gradient): the tile's (i, j) tap of the 2x2 output block
   int a_dr = 0, a_ds = 0, a_c0 = m0;
@@ -693,10 +701,15 @@ __global__ __launch_bounds__(256, 2) void wgrad_x6_kernel(WgradArgs g) {
     float* red = reinterpret_cast<float*>(&sA[0][0][0]);
     red[tid] = bsum;
     __syncthreads();
-    if (tid < BM) {
+    if (tid < BM) {  // the threads whose column am is tid, in a fixed order
       float t = 0.f;
+      if (!pa) {
 #pragma unroll
-      for (int q = 0; q < 256 / BM; ++q) t += red[q * BM + tid];
+        for (int q = 0; q < 256 / BM; ++q) t += red[q * BM + tid];
+      } else {
+#pragma unroll
+        for (int q = 0; q < 256 / (2 * BM); ++q) t += red[q * 2 * BM + 2 * tid] + red[q * 2 * BM + 2 * tid + 1];
+      }
       g.part_bias[(size_t)split * g.Mp + m0 + tid] = t;
     }
   }
@@ -705,6 +718,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_x6_kernel(WgradArgs g) {
 static int run_wgrad(const WgradArgs& base, const WgradPlan& pl, hipStream_t s, int batches = 1) {
   WgradArgs a = base;
   a.pix_per_split = pl.pps;
+  a.pair = tune_get(PIS_TUNE_WGRAD_PAIR);
   const int tiles = (a.Mp / pl.bm) * (a.Np / pl.bn);
   const dim3 grid(tiles * pl.splits, batches);
   if (tune_get(PIS_TUNE_WGRAD_X6) != 0 && a.b_mode == B_PLAIN && pl.pps % 16 == 0 && (!a.a_up2 || a.W % 8 == 0)) {
