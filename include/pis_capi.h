@@ -84,8 +84,8 @@ int pis_version(void);
                                     512^2-256^2 layers) or 4 channels per thread */
 #define PIS_TUNE_LOSS_ROWS 18     /* pis_loss_fwd with W % 4 == 0: 1 (default) whole-row bands, 0 16x128 tiles;
                                     both followed by the one-block fixed-order finalize (deterministic) */
-#define PIS_TUNE_LOSS_ROWMUL 19  /* whole-row loss forward: rows per block multiplier (1 default: the most blocks
-                                    up to 2048; 2, 4: fewer blocks, more row batches per thread) */
+#define PIS_TUNE_LOSS_ROWMUL 19  /* whole-row loss forward: rows per block multiplier (1 default: about 1024 blocks;
+                                    2, 4: fewer blocks, more row batches per thread) */
 #define PIS_TUNE_SLAB_CHUNKS 20  /* thousands of partial slabs over <= 1024 columns (bias gradients): 1 (default)
                                     two-pass chunked row reduction, 0 one column per block */
 #define PIS_TUNE_WGRAD_PAIR 21   /* bf16x6 weight-gradient GEMM, 64-wide operand tiles: 0 (default) one 4-pixel run per

@@ -37,31 +37,40 @@ def main():
     g = torch.Generator().manual_seed(42)
     imgs, masks = zip(*[disc_sample(512, 512, g) for _ in range(8)])
     x, t = torch.stack(imgs).to(dev), torch.stack(masks).to(dev)
-    torch.manual_seed(42)
-    model = UNet(1, 1, 64).to(dev).train()
     crit = DiceBCEPDELoss(pde_weight=1e-4, phase_field_weight=1e-4, diffusion_coeff=5.0, epsilon=0.05)
-    opt = AdamW(model.parameters(), lr=1e-5, weight_decay=1e-5)
 
-    def step():
+    def setv(kv):
+        for k in keys:
+            lib.pis_tune(k, kv.get(k, defaults[k]))
+
+    # one model (and engine plan: workspaces depend on the knobs) per variant, same seed
+    models = {}
+    for name, kv in variants:
+        setv(kv)
+        torch.manual_seed(42)
+        m = UNet(1, 1, 64).to(dev).train()
+        models[name] = (m, AdamW(m.parameters(), lr=1e-5, weight_decay=1e-5))
+
+    def step(name):
+        model, opt = models[name]
         opt.zero_grad()
         crit(model(x), t).backward()
         opt.step()
 
-    def run(kv):
-        for k in keys:
-            lib.pis_tune(k, kv.get(k, defaults[k]))
-        step()
+    def run(name, kv):
+        setv(kv)
+        step(name)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(args.steps):
-            step()
+            step(name)
         torch.cuda.synchronize()
         return (time.perf_counter() - t0) / args.steps * 1e3
 
     res = {}
     for _ in range(args.rounds):
         for name, kv in variants:
-            res.setdefault(name, []).append(run(kv))
+            res.setdefault(name, []).append(run(name, kv))
     for k in keys:
         lib.pis_tune(k, defaults[k])
     for name, ms in res.items():
