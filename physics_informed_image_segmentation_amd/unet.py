@@ -563,6 +563,10 @@ class UNetEngine:
         sst = side.cuda_stream
         if side is not main:
             side.wait_stream(main)  # forward activations, kept transforms, a zeroed scratch arena
+        # the previous backward ended with main.wait_stream(side): every earlier use of the
+        # alternating weight-gradient workspaces is ordered before this point already (and a
+        # graph capture must not wait on events recorded outside it)
+        self.ws3_free = [None, None]
         gb = self._gbuf
 
         def to_side():
