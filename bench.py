@@ -460,7 +460,7 @@ def main():
             "step_tflops_direct_equiv": flops / (ms * 1e-3) / 1e12,
             # north-star HBM figure for the fused loss (live over the timed steps): the backward
             # runs inside the head backward kernel (its reduce_slabs follow-ups inside the
-            # events); the forward is one launch (its last block reduces the partials)
+            # events); the forward is the row kernel + its one-block finalize launch
             "roofline_loss": dict({
                 name.replace("pis_", "") + "_live": {
                     "bound": "hbm", "achieved": gbs, "peak": 8000.0, "unit": "GB/s", "frac": gbs / 8000.0,

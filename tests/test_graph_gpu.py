@@ -1,0 +1,54 @@
+"""The graph-replayed training step (physics_informed_image_segmentation_amd/graph.py) IS the
+eager step: same Dropout2d draws, same kernels, same order of every reduction — so the weights
+after N steps are bitwise equal to N eager steps of an identically seeded model."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _setup(dropout, H=64, B=4):
+    from physics_informed_image_segmentation_amd import AdamW, DiceBCEPDELoss, UNet
+    from physics_informed_image_segmentation_amd.dataset import disc_sample
+    g = torch.Generator().manual_seed(5)
+    imgs, masks = zip(*[disc_sample(H, H, g) for _ in range(B)])
+    x, t = torch.stack(imgs).cuda(), torch.stack(masks).cuda()
+    torch.manual_seed(42)
+    m = UNet(1, 1, 64, dropout=dropout).cuda().train()
+    opt = AdamW(m.parameters(), lr=1e-3, weight_decay=1e-5)
+    crit = DiceBCEPDELoss(pde_weight=1e-2, phase_field_weight=1e-2, diffusion_coeff=5.0, epsilon=0.05)
+    return m, opt, crit, x, t
+
+
+@pytest.mark.parametrize("dropout", [0.0, 0.2])
+def test_graph_steps_equal_eager_steps(hip, dropout):
+    from physics_informed_image_segmentation_amd.graph import StepGraph
+    n = 5
+    me, oe, crit, x, t = _setup(dropout)
+    torch.cuda.manual_seed(11)
+    losses_e = []
+    for _ in range(n):
+        oe.zero_grad(set_to_none=True)
+        loss = crit(me(x), t)
+        loss.backward()
+        oe.step()
+        losses_e.append(loss.item())
+    mg, og, crit, x, t = _setup(dropout)
+    torch.cuda.manual_seed(11)
+    sg = StepGraph(mg, crit, og, x, t, warmup=2)  # steps 1-2 eager, then capture
+    losses_g = [sg.step().item() for _ in range(n - 2)]
+    sg.close()
+    torch.cuda.synchronize()
+    assert losses_g == losses_e[2:]
+    for (k, p), q in zip(me.named_parameters(), mg.parameters()):
+        assert torch.equal(p, q), k
+
+
+def test_graph_step_takes_new_batches(hip):
+    from physics_informed_image_segmentation_amd.graph import StepGraph
+    m, o, crit, x, t = _setup(0.0)
+    sg = StepGraph(m, crit, o, x.clone(), t.clone(), warmup=1)
+    a = sg.step(x, t).item()
+    b = sg.step(torch.flip(x, dims=[-1]), torch.flip(t, dims=[-1])).item()
+    assert a != b
+    sg.close()
