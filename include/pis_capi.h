@@ -47,6 +47,9 @@ typedef void* pis_stream_t; /* hipStream_t */
                                 layer's dz transforms into the call's workspace          */
 #define PIS_W_UNFLIPPED 32   /* conv3x3 dgrad_ex with PIS_WINO_PREPARED: w_flip is the layer's ORIGINAL
                                 KRSC weight (the F(4x4) filter transform rotates it in place) */
+#define PIS_FILTER_READY 64  /* conv3x3 fwd_ex / fwd_keep / fwd_pool / dgrad_ex: the weight argument is
+                                the layer's filter transform from pis_conv3x3_filter (same shape and
+                                direction), so the call launches no filter transform of its own */
 
 const char* pis_last_error(void);
 int pis_version(void);
@@ -169,6 +172,17 @@ int pis_conv3x3_wgrad_keep(const float* x, int ldx, const float* dz, int ldz, fl
  * partials into ws_wgrad (for pis_conv3x3_wgrad_keep); both calls then pass PIS_WINO_PREPARED.
  * Returns 1 when done, 0 when this layer / workspace does not take that path (call without the
  * flag), < 0 on error. ws_wgrad must stay untouched until its pis_conv3x3_wgrad_keep ran. */
+/* The F(4x4,3x3) filter transform of a conv3x3 layer, ahead of its convolution call (so it can run
+ * on another stream, off the critical path). dgrad = 0: for the forward, w = KRSC [Cout][9][Cin];
+ * dgrad = 1: for the input gradient, w = the ORIGINAL KRSC weights (rotated in place, as
+ * PIS_W_UNFLIPPED). The output format is the one the call with these shapes will consume (fp32
+ * U[36][N][C] for the batched GEMMs, bf16x6 planes for the fused 64->64 contraction).
+ * pis_conv3x3_filter_bytes returns its size, 0 when that call would not take the F(4x4,3x3)
+ * GEMM path (then PIS_FILTER_READY must not be used). Pass the result as the weight argument
+ * with PIS_FILTER_READY (dgrad: with PIS_WINO_PREPARED | PIS_W_UNFLIPPED semantics kept). */
+size_t pis_conv3x3_filter_bytes(int B, int H, int W, int Cin, int Cout, int dgrad);
+int pis_conv3x3_filter(const float* w, int B, int H, int W, int Cin, int Cout, int dgrad, void* out,
+                       size_t out_bytes, pis_stream_t stream);
 int pis_conv3x3_bwd_prep(const float* dz, int ldz, int B, int H, int W, int Cin, int Cout, void* ws_dgrad,
                          size_t ws_dgrad_bytes, void* ws_wgrad, size_t ws_wgrad_bytes, pis_stream_t stream);
 size_t pis_conv3x3_wgrad_ws(int B, int H, int W, int Cin, int Cout);

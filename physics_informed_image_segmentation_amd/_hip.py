@@ -17,6 +17,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "_lib", "libpis.so")
 
 PIS_RELU, PIS_SCALE, PIS_MASK, PIS_ACCUMULATE, PIS_WINO_PREPARED, PIS_W_UNFLIPPED = 1, 2, 4, 8, 16, 32
+PIS_FILTER_READY = 64
 PIS_LOSS_ALL_TERMS, PIS_LOSS_CHAIN_SIGMOID, PIS_LOSS_NO_REACTION = 1, 2, 4
 LOSS_NTERMS = 8
 TERM_TOTAL, TERM_DICE, TERM_BCE, TERM_RD, TERM_PF, TERM_I, TERM_P, TERM_T = range(8)
@@ -40,6 +41,8 @@ _SIGNATURES = {
     "pis_tune": ([I, I], c_int),
     "pis_debug_gemm_nt": ([P, P, P, I, I, I, I, I, P], c_int),
     "pis_conv3x3_bwd_prep": ([P, I, I, I, I, I, I, P, Z, P, Z, P], c_int),
+    "pis_conv3x3_filter_bytes": ([I, I, I, I, I, I], c_size_t),
+    "pis_conv3x3_filter": ([P, I, I, I, I, I, I, P, Z, P], c_int),
     "pis_conv3x3_fwd_pool": ([P, I, P, P, P, P, I, I, I, I, I, I, I, P, Z, P, P, P], c_int),
     "pis_conv3x3_fwd": ([P, I, P, P, P, P, I, I, I, I, I, I, I, P], c_int),
     "pis_conv3x3_flip": ([P, P, I, I, P], c_int),

@@ -574,6 +574,10 @@ static int dispatch_conv3x3(const IGemmArgs& a, int B, void* ws, size_t ws_bytes
   if (ws && wino_ok(a) && (keep_v || wino_wanted_dims(a.H, a.W, a.Csrc, a.N)) &&
       ws_bytes >= wino_ws_bytes(B, a.H, a.W, a.Csrc, a.N))
     return launch_wino3x3(a, B, ws, s, keep_v, v_ready);
+  if (a.filter_ready) {
+    set_error("conv3x3: PIS_FILTER_READY but this call does not take the F(4x4,3x3) path");
+    return PIS_ERR_ARG;
+  }
   if (v_ready) {
     set_error("pis_conv3x3_dgrad_ex: PIS_WINO_PREPARED but this call does not take the Winograd path");
     return PIS_ERR_ARG;
@@ -620,6 +624,7 @@ extern "C" int pis_conv3x3_fwd_keep(const float* x, int ldx, const float* w_krsc
   a.Csrc = Cin; a.ntaps = 9; a.tap_mode = TAP_CONV3; a.wt = w_krsc; a.ldw = 9 * Cin; a.N = Cout;
   a.epi = EPI_NHWC; a.bias = bias; a.scale = scale; a.dst = y; a.ldd = ldy;
   a.flags = flags & (PIS_RELU | PIS_SCALE | PIS_ACCUMULATE);
+  a.filter_ready = (flags & PIS_FILTER_READY) != 0;
   return dispatch_conv3x3(a, B, ws, ws_bytes, (hipStream_t)stream, keep);
 }
 
@@ -639,6 +644,7 @@ extern "C" int pis_conv3x3_fwd_pool(const float* x, int ldx, const float* w_krsc
   a.Csrc = Cin; a.ntaps = 9; a.tap_mode = TAP_CONV3; a.wt = w_krsc; a.ldw = 9 * Cin; a.N = Cout;
   a.epi = EPI_NHWC; a.bias = bias; a.scale = scale; a.dst = y; a.ldd = ldy;
   a.flags = flags & (PIS_RELU | PIS_SCALE);
+  a.filter_ready = (flags & PIS_FILTER_READY) != 0;
   // the F(4x4,3x3) output epilogues pool the tile they just wrote; every other path pools after
   if (Cin > 1 && ws && wino_ok(a) && wino_tile(H, W) == 4 && (kept || wino_wanted_dims(H, W, Cin, Cout)) &&
       ws_bytes >= wino_ws_bytes(B, H, W, Cin, Cout)) {
@@ -659,6 +665,7 @@ extern "C" int pis_conv3x3_fwd_ex(const float* x, int ldx, const float* w_krsc, 
   PIS_CHECK_ARG(!(flags & PIS_SCALE) || scale, "pis_conv3x3_fwd: PIS_SCALE without scale");
   PIS_CHECK_ARG(ldy % 4 == 0 && Cout % 4 == 0, "pis_conv3x3_fwd: ldy/Cout must be multiples of 4");
   hipStream_t s = (hipStream_t)stream;
+  PIS_CHECK_ARG(!(flags & PIS_FILTER_READY) || Cin > 1, "pis_conv3x3_fwd: PIS_FILTER_READY with Cin == 1");
   if (Cin == 1 && Cout == 64 && W % 64 == 0) {
     hipLaunchKernelGGL(conv3x3_c1_row_kernel, dim3((unsigned)(B * H * (W / 64))), dim3(256), 0, s, x, ldx, w_krsc,
                        bias, scale, y, ldy, H, W, flags);
@@ -678,6 +685,7 @@ extern "C" int pis_conv3x3_fwd_ex(const float* x, int ldx, const float* w_krsc, 
   a.Csrc = Cin; a.ntaps = 9; a.tap_mode = TAP_CONV3; a.wt = w_krsc; a.ldw = 9 * Cin; a.N = Cout;
   a.epi = EPI_NHWC; a.bias = bias; a.scale = scale; a.dst = y; a.ldd = ldy;
   a.flags = flags & (PIS_RELU | PIS_SCALE | PIS_ACCUMULATE);
+  a.filter_ready = (flags & PIS_FILTER_READY) != 0;
   return dispatch_conv3x3(a, B, ws, ws_bytes, s);
 }
 
@@ -689,6 +697,40 @@ extern "C" int pis_conv3x3_flip(const float* w_krsc, float* w_flip, int Cin, int
   hipLaunchKernelGGL(conv3x3_flip_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, w_krsc,
                      w_flip, Cin, Cout);
   return launch_status("conv3x3_flip");
+}
+
+namespace pis {  // winograd.hip
+int wino_filter_format(int B, int H, int W, int C, int N, bool kept);
+int launch_wino4_filter_only(const float* w, int C, int N, int dgrad, int format, void* out, hipStream_t s);
+}  // namespace pis
+
+// the filter transform pis_conv3x3_{fwd_keep,fwd_pool,dgrad_ex} would compute (engine shapes:
+// kept forward transforms, prepared 32-aligned input gradients)
+static int filter_format(int B, int H, int W, int Cin, int Cout, int dgrad) {
+  if (B <= 0 || H <= 0 || W <= 0 || Cin % 4 || Cout % 4 || Cin < 4) return 0;
+  if (dgrad) {
+    if (Cin % 32 || Cout % 32 || !wino_wanted_dims(H, W, Cout, Cin)) return 0;
+    return wino_filter_format(B, H, W, Cout, Cin, false);
+  }
+  if (pis_conv3x3_keep_bytes(B, H, W, Cin, Cout) == 0 && !wino_wanted_dims(H, W, Cin, Cout)) return 0;
+  return wino_filter_format(B, H, W, Cin, Cout, pis_conv3x3_keep_bytes(B, H, W, Cin, Cout) > 0);
+}
+
+extern "C" size_t pis_conv3x3_filter_bytes(int B, int H, int W, int Cin, int Cout, int dgrad) {
+  const int f = filter_format(B, H, W, Cin, Cout, dgrad);
+  if (f == 0) return 0;
+  const size_t nc = (size_t)36 * Cin * Cout;
+  return f == 2 ? 3 * nc * sizeof(__bf16) : nc * sizeof(float);
+}
+
+extern "C" int pis_conv3x3_filter(const float* w, int B, int H, int W, int Cin, int Cout, int dgrad, void* out,
+                                  size_t out_bytes, pis_stream_t stream) {
+  const int f = filter_format(B, H, W, Cin, Cout, dgrad);
+  PIS_CHECK_ARG(w && out && f != 0, "pis_conv3x3_filter: no F(4x4,3x3) GEMM path for these shapes");
+  PIS_CHECK_ARG(out_bytes >= pis_conv3x3_filter_bytes(B, H, W, Cin, Cout, dgrad), "pis_conv3x3_filter: output too small");
+  // forward: contraction C = Cin, outputs N = Cout; input gradient: C = Cout, N = Cin
+  return dgrad ? launch_wino4_filter_only(w, Cout, Cin, 1, f, out, (hipStream_t)stream)
+               : launch_wino4_filter_only(w, Cin, Cout, 0, f, out, (hipStream_t)stream);
 }
 
 extern "C" int pis_conv3x3_dgrad(const float* dz, int ldz, const float* w_flip, const float* mask,
@@ -713,6 +755,7 @@ extern "C" int pis_conv3x3_dgrad_ex(const float* dz, int ldz, const float* w_fli
   a.epi = EPI_NHWC; a.mask = mask; a.ldm = ldm; a.scale = scale; a.dst = dx; a.ldd = lddx;
   a.flags = flags & (PIS_MASK | PIS_SCALE | PIS_ACCUMULATE);
   a.w_unflipped = (flags & PIS_W_UNFLIPPED) != 0;
+  a.filter_ready = (flags & PIS_FILTER_READY) != 0;
   PIS_CHECK_ARG(!a.w_unflipped || (flags & PIS_WINO_PREPARED),
                 "pis_conv3x3_dgrad_ex: PIS_W_UNFLIPPED needs the prepared F(4x4,3x3) path");
   return dispatch_conv3x3(a, B, ws, ws_bytes, (hipStream_t)stream, nullptr, (flags & PIS_WINO_PREPARED) != 0);

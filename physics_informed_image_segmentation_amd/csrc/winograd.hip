@@ -1554,6 +1554,8 @@ int launch_wino3x3(const IGemmArgs& a, int B, void* ws, hipStream_t s, float* ke
   float* Mt = V + (size_t)nxi * T * C;
   if (keep_v && m == 4) V = keep_v;
   const double flop = 2.0 * nxi * (double)T * N * C;
+  if (a.filter_ready && (m != 4 || (!keep_v && wino_fused_wanted(a.H, a.W, C, N))))
+    return set_error("launch_wino3x3: PIS_FILTER_READY needs the F(4x4,3x3) GEMM path"), PIS_ERR_ARG;
   if (m == 4 && !keep_v && wino_fused_wanted(a.H, a.W, C, N)) {
     launch_wino4_filter(a, N, C, U, 1, nullptr, s);
     int rc = launch_status("wino_filter");
@@ -1567,7 +1569,8 @@ int launch_wino3x3(const IGemmArgs& a, int B, void* ws, hipStream_t s, float* ke
   if (wino_gemm_out_wanted(m, T, C, N)) {
     // the pre-split filter planes (1.5x U's bytes) go where M would have been
     __bf16* Up = reinterpret_cast<__bf16*>(Mt);
-    launch_wino4_filter(a, N, C, U, 0, Up, s);
+    if (a.filter_ready) Up = const_cast<__bf16*>(reinterpret_cast<const __bf16*>(a.wt));
+    else launch_wino4_filter(a, N, C, U, 0, Up, s);
     if (!v_ready)
       launch_wino4_input(T, C, s, a.src, a.lds, B, a.H, a.W,
                          C, V);
@@ -1583,7 +1586,8 @@ int launch_wino3x3(const IGemmArgs& a, int B, void* ws, hipStream_t s, float* ke
   if (a.w_unflipped && (m != 4 || N % 32 || C % 32))
     return set_error("launch_wino3x3: unflipped weights need F(4x4,3x3) and 32-aligned channels"), PIS_ERR_ARG;
   if (m == 4) {
-    launch_wino4_filter(a, N, C, U, 0, nullptr, s);
+    if (a.filter_ready) U = const_cast<float*>(a.wt);
+    else launch_wino4_filter(a, N, C, U, 0, nullptr, s);
     if (!v_ready)
       launch_wino4_input(T, C, s, a.src, a.lds, B, a.H, a.W,
                          C, V);
@@ -1646,6 +1650,27 @@ int launch_wino3x3(const IGemmArgs& a, int B, void* ws, hipStream_t s, float* ke
   else
     hipLaunchKernelGGL(wino_output_kernel, dim3(grid_of(T * (N / 4))), dim3(256), 0, s, Mt, a, B);
   return launch_status("wino_output");
+}
+
+// the F(4x4,3x3) filter transform a conv call with these shapes consumes (pis_conv3x3_filter):
+// 1 fp32 U[36][N][C] for the batched GEMMs, 2 the bf16x6 planes of the fused 64 -> 64
+// contraction, 0 none (not the F(4x4,3x3) GEMM path). C = contraction channels, N = outputs.
+int wino_filter_format(int B, int H, int W, int C, int N, bool kept) {
+  if (wino_tile(H, W) != 4) return 0;
+  const int64_t T = (int64_t)B * (H / 4) * (W / 4);
+  if (!kept && wino_fused_wanted(H, W, C, N)) return 0;
+  if (wino_gemm_out_wanted(4, T, C, N)) return 2;
+  return 1;
+}
+
+int launch_wino4_filter_only(const float* w, int C, int N, int dgrad, int format, void* out, hipStream_t s) {
+  IGemmArgs a{};
+  a.wt = w; a.ldw = 9 * C; a.w_unflipped = dgrad;
+  if (dgrad && (N % 32 || C % 32)) return set_error("pis_conv3x3_filter: the input-gradient transform needs "
+                                                    "32-aligned channels"), PIS_ERR_ARG;
+  if (format == 2) launch_wino4_filter(a, N, C, nullptr, 0, reinterpret_cast<__bf16*>(out), s);
+  else launch_wino4_filter(a, N, C, reinterpret_cast<float*>(out), 0, nullptr, s);
+  return launch_status("wino_filter");
 }
 
 int launch_wino_input(const float* x, int ldx, int B, int H, int W, int C, float* V, hipStream_t s, int m) {

@@ -28,7 +28,8 @@ import torch
 import torch.nn as nn
 
 from . import _hip
-from ._hip import PIS_ACCUMULATE, PIS_MASK, PIS_RELU, PIS_SCALE, PIS_W_UNFLIPPED, PIS_WINO_PREPARED, call, ptr
+from ._hip import (PIS_ACCUMULATE, PIS_FILTER_READY, PIS_MASK, PIS_RELU, PIS_SCALE, PIS_W_UNFLIPPED, PIS_WINO_PREPARED,
+                   call, ptr)
 
 # block name -> dropout multiplier of UNet(dropout=d), src/unet.py:120-154
 _DROP_MULT = {"enc1": 0.0, "enc2": 0.5, "enc3": 1.0, "enc4": 1.0, "bottleneck": 1.0,
@@ -320,6 +321,12 @@ class UNetEngine:
     # right after dz's transforms, "gemm" after the input gradient's contractions, "dgrad" after
     # the whole input gradient
     side_sync = os.environ.get("PIS_SIDE_SYNC", "prep")
+    # PIS_FILTER_AHEAD=1: the F(4x4,3x3) filter transforms of a step (forward: the layers' weights;
+    # backward: their rotated input-gradient form) run on the side stream, idle during the forward,
+    # at its start, and the main stream's convs wait on one event each instead of transforming
+    # their own. Measured 1.5 % SLOWER at C2 (tools/ab_tune.py "base;fa=0": 31.48 vs 31.01 ms, and
+    # 31.39 vs 30.95 with the backward's transforms at the start of the backward): off by default
+    filter_ahead = os.environ.get("PIS_FILTER_AHEAD", "0") == "1"
 
     def __init__(self, model: UNet):
         self.m = model
@@ -395,6 +402,45 @@ class UNetEngine:
                 nb = lib.pis_conv3x3_keep_bytes(B, Hl, Wl, conv.in_channels, conv.out_channels)
                 if nb:
                     self.keep[id(conv)] = torch.empty((nb + 3) // 4, dtype=torch.float32, device=dev)
+        # per-layer filter transforms computed ahead on the side stream (forward order; the
+        # backward walks them in reverse): {id(conv): (conv, H, W, buffer)}
+        self.ffilt: Dict[int, tuple] = {}
+        self.bfilt: Dict[int, tuple] = {}
+        self.fev: Dict[int, torch.cuda.Event] = {}
+        self.bev: Dict[int, torch.cuda.Event] = {}
+        if self.side is not None and self.filter_ahead:
+            for name in BLOCK_ORDER:
+                blk = self.m.block(name)
+                lvl = 5 if name == "bottleneck" else int(name[-1])
+                Hl, Wl = H >> (lvl - 1), W >> (lvl - 1)
+                for conv in (blk.conv0, blk.conv1):
+                    if id(conv) not in self.keep:
+                        continue
+                    ci, co = conv.in_channels, conv.out_channels
+                    nb = lib.pis_conv3x3_filter_bytes(B, Hl, Wl, ci, co, 0)
+                    if nb:
+                        self.ffilt[id(conv)] = (conv, Hl, Wl, torch.empty((nb + 3) // 4, dtype=torch.float32,
+                                                                          device=dev))
+                    nb = lib.pis_conv3x3_filter_bytes(B, Hl, Wl, ci, co, 1)
+                    if nb and not (name == "enc1" and conv is blk.conv0):  # the first conv has no dgrad
+                        self.bfilt[id(conv)] = (conv, Hl, Wl, torch.empty((nb + 3) // 4, dtype=torch.float32,
+                                                                          device=dev))
+
+    def _filters_ahead(self, table, dgrad: int, order):
+        """Launch the filter transforms of `table` on the side stream (after everything the main
+        stream has enqueued: the weights are final), one event per layer."""
+        main, side = torch.cuda.current_stream(), self.side
+        side.wait_stream(main)
+        events = {}
+        with torch.cuda.stream(side):
+            for cid in order:
+                conv, Hl, Wl, buf = table[cid]
+                call("pis_conv3x3_filter", conv.weight.data_ptr(), self.B, Hl, Wl, conv.in_channels,
+                     conv.out_channels, dgrad, buf.data_ptr(), buf.numel() * 4, side.cuda_stream)
+                ev = torch.cuda.Event()
+                ev.record(side)
+                events[cid] = ev
+        return events
 
     def _gbuf(self, name: str, *shape) -> torch.Tensor:
         t = self.gbufs.get(name)
@@ -430,12 +476,17 @@ class UNetEngine:
     def _conv_fwd(self, conv: nn.Conv2d, x: _Buf, y: _Buf, B, H, W, scale, pool: Optional[torch.Tensor] = None):
         flags = PIS_RELU | (PIS_SCALE if scale is not None else 0)
         keep = self.keep.get(id(conv)) if self._keeping else None
+        wptr = conv.weight.data_ptr()
+        ready = self.ffilt.get(id(conv)) if keep is not None else None
+        if ready is not None and id(conv) in self.fev:
+            torch.cuda.current_stream().wait_event(self.fev.pop(id(conv)))
+            wptr, flags = ready[3].data_ptr(), flags | PIS_FILTER_READY
         if pool is not None:  # encoder conv1 + MaxPool2d in one call (pooled in the output epilogue)
-            call("pis_conv3x3_fwd_pool", x.p, x.ld, conv.weight.data_ptr(), conv.bias.data_ptr(), ptr(scale),
+            call("pis_conv3x3_fwd_pool", x.p, x.ld, wptr, conv.bias.data_ptr(), ptr(scale),
                  y.p, y.ld, B, H, W, conv.in_channels, conv.out_channels, flags, self.ws.data_ptr(), self.ws_bytes,
                  ptr(keep), pool.data_ptr(), self._stream())
             return
-        call("pis_conv3x3_fwd_keep", x.p, x.ld, conv.weight.data_ptr(), conv.bias.data_ptr(), ptr(scale),
+        call("pis_conv3x3_fwd_keep", x.p, x.ld, wptr, conv.bias.data_ptr(), ptr(scale),
              y.p, y.ld, B, H, W, conv.in_channels, conv.out_channels, flags, self.ws.data_ptr(), self.ws_bytes,
              ptr(keep), self._stream())
 
@@ -463,6 +514,14 @@ class UNetEngine:
         x = x.contiguous()
         bf = self.bufs
         self._keeping = keep  # only a forward the backward will use may overwrite the kept transforms
+        # the side stream is idle during the forward: it transforms every filter of the step there,
+        # the forward's in layer order, then the input gradients' (backward order)
+        self.fev, self.bev = {}, {}
+        if keep and self.side is not None:
+            if self.ffilt:
+                self.fev = self._filters_ahead(self.ffilt, 0, list(self.ffilt))
+            if self.bfilt:
+                self.bev = self._filters_ahead(self.bfilt, 1, list(reversed(list(self.bfilt))))
         self.x = x
         self.scales = scales
         src = _Buf(x, m.in_channels)
@@ -567,6 +626,8 @@ class UNetEngine:
         # alternating weight-gradient workspaces is ordered before this point already (and a
         # graph capture must not wait on events recorded outside it)
         self.ws3_free = [None, None]
+        if side is main:
+            self.bev = {}  # serialised A/B mode: each dgrad transforms its own filter
         gb = self._gbuf
 
         def to_side():
@@ -630,6 +691,9 @@ class UNetEngine:
                 flags = (PIS_MASK if mask is not None else 0) | (PIS_SCALE if scale is not None else 0)
                 if prep:
                     wf, flags = conv.weight.data_ptr(), flags | PIS_WINO_PREPARED | PIS_W_UNFLIPPED
+                    if id(conv) in self.bev:  # its rotated filter transform, computed ahead
+                        main.wait_event(self.bev.pop(id(conv)))
+                        wf, flags = self.bfilt[id(conv)][3].data_ptr(), flags | PIS_FILTER_READY
                 else:
                     wf = flipped(conv).data_ptr()
                 call("pis_conv3x3_dgrad_ex", dz.p, dz.ld, wf,

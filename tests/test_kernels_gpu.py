@@ -789,3 +789,70 @@ def test_pde_fields_and_their_gradients(hip, shape):
         ga = ud.grad.cpu().double()
         assert ((ga - gref).norm() / gref.norm()).item() < 1e-6, name
         assert (ga - gref).abs().max().item() <= 1e-5 * gref.abs().max().item(), name
+
+
+@pytest.mark.parametrize("H,cin,cout", [(64, 64, 64), (32, 128, 128), (32, 256, 128), (16, 512, 256)])
+def test_filter_ready_matches_inline_transform(hip, H, cin, cout):
+    """pis_conv3x3_filter + PIS_FILTER_READY (the engine's filter transforms computed ahead on the
+    side stream) gives bitwise the conv the call computes with its own filter transform: forward
+    with a kept input transform, and the prepared input gradient from the original weights."""
+    B = 2
+    s = torch.cuda.current_stream().cuda_stream
+    g = torch.Generator().manual_seed(21)
+    x = torch.randn(B, H, H, cin, generator=g).cuda()
+    dz = torch.randn(B, H, H, cout, generator=g).cuda()
+    w = (torch.randn(cout, 3, 3, cin, generator=g) * 0.05).cuda()
+    bias = torch.randn(cout, generator=g).cuda()
+    nws = hip.pis_conv3x3_ex_ws(B, H, H, cin, cout)
+    ws = torch.empty(nws // 4 + 1, device="cuda")
+    nk = hip.pis_conv3x3_keep_bytes(B, H, H, cin, cout)
+    assert nk > 0
+    ys, keeps = [], []
+    for ready in (False, True):
+        wptr, flags = w.data_ptr(), 1  # PIS_RELU
+        if ready:
+            nb = hip.pis_conv3x3_filter_bytes(B, H, H, cin, cout, 0)
+            assert nb > 0
+            U = torch.empty(nb // 4 + 1, device="cuda")
+            assert hip.pis_conv3x3_filter(w.data_ptr(), B, H, H, cin, cout, 0, U.data_ptr(), nb, s) == 0
+            wptr, flags = U.data_ptr(), flags | 64  # PIS_FILTER_READY
+        y = torch.empty(B, H, H, cout, device="cuda")
+        keep = torch.empty(nk // 4 + 1, device="cuda")
+        assert hip.pis_conv3x3_fwd_keep(x.data_ptr(), cin, wptr, bias.data_ptr(), 0, y.data_ptr(), cout, B, H, H,
+                                        cin, cout, flags, ws.data_ptr(), nws, keep.data_ptr(), s) == 0
+        ys.append(y)
+        keeps.append(keep)
+    torch.cuda.synchronize()
+    assert torch.equal(ys[0], ys[1])
+    assert torch.equal(keeps[0][:nk // 4], keeps[1][:nk // 4])  # (the +1 float is padding)
+    nw3 = hip.pis_conv3x3_wgrad_ws(B, H, H, cin, cout)
+    ws3 = torch.empty(nw3 // 4 + 1, device="cuda")
+    dxs = []
+    for ready in (False, True):
+        assert hip.pis_conv3x3_bwd_prep(dz.data_ptr(), cout, B, H, H, cin, cout, ws.data_ptr(), nws,
+                                        ws3.data_ptr(), nw3, s) == 1
+        wptr, flags = w.data_ptr(), 16 | 32  # PIS_WINO_PREPARED | PIS_W_UNFLIPPED
+        if ready:
+            nb = hip.pis_conv3x3_filter_bytes(B, H, H, cin, cout, 1)
+            assert nb > 0
+            Ub = torch.empty(nb // 4 + 1, device="cuda")
+            assert hip.pis_conv3x3_filter(w.data_ptr(), B, H, H, cin, cout, 1, Ub.data_ptr(), nb, s) == 0
+            wptr, flags = Ub.data_ptr(), flags | 64
+        dx = torch.empty(B, H, H, cin, device="cuda")
+        assert hip.pis_conv3x3_dgrad_ex(dz.data_ptr(), cout, wptr, 0, 0, 0, dx.data_ptr(), cin, B, H, H, cin, cout,
+                                        flags, ws.data_ptr(), nws, s) == 0
+        dxs.append(dx)
+    torch.cuda.synchronize()
+    assert torch.equal(dxs[0], dxs[1])
+
+
+def test_filter_ready_refused_off_the_winograd_path(hip):
+    """A conv that would not take the F(4x4,3x3) GEMM path reports 0 filter bytes and refuses
+    PIS_FILTER_READY loudly."""
+    assert hip.pis_conv3x3_filter_bytes(2, 16, 16, 1, 64, 0) == 0  # Cin = 1: direct kernels
+    x = torch.randn(1, 16, 16, 1, device="cuda")
+    y = torch.empty(1, 16, 16, 64, device="cuda")
+    w = torch.randn(64 * 9, device="cuda")
+    rc = hip.pis_conv3x3_fwd_ex(x.data_ptr(), 1, w.data_ptr(), 0, 0, y.data_ptr(), 64, 1, 16, 16, 1, 64, 64, 0, 0,
+                                torch.cuda.current_stream().cuda_stream)
+    assert rc != 0
