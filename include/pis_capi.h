@@ -183,6 +183,16 @@ int pis_conv3x3_wgrad_keep(const float* x, int ldx, const float* dz, int ldz, fl
 size_t pis_conv3x3_filter_bytes(int B, int H, int W, int Cin, int Cout, int dgrad);
 int pis_conv3x3_filter(const float* w, int B, int H, int W, int Cin, int Cout, int dgrad, void* out,
                        size_t out_bytes, pis_stream_t stream);
+/* Several layers' filter transforms (as pis_conv3x3_filter) in ONE launch: a layer's own grid is
+ * small and latency-bound, here all jobs' blocks run side by side. At most PIS_FILTER_MAX_JOBS. */
+typedef struct pis_filter_job {
+  const float* w;
+  void* out;
+  size_t out_bytes;
+  int B, H, W, Cin, Cout, dgrad;
+} pis_filter_job;
+#define PIS_FILTER_MAX_JOBS 40
+int pis_conv3x3_filters(const pis_filter_job* jobs, int n, pis_stream_t stream);
 int pis_conv3x3_bwd_prep(const float* dz, int ldz, int B, int H, int W, int Cin, int Cout, void* ws_dgrad,
                          size_t ws_dgrad_bytes, void* ws_wgrad, size_t ws_wgrad_bytes, pis_stream_t stream);
 size_t pis_conv3x3_wgrad_ws(int B, int H, int W, int Cin, int Cout);

@@ -23,6 +23,12 @@ LOSS_NTERMS = 8
 TERM_TOTAL, TERM_DICE, TERM_BCE, TERM_RD, TERM_PF, TERM_I, TERM_P, TERM_T = range(8)
 
 
+class FilterJob(ctypes.Structure):
+    """pis_filter_job (include/pis_capi.h): one layer's filter transform in pis_conv3x3_filters."""
+    _fields_ = [("w", c_void_p), ("out", c_void_p), ("out_bytes", c_size_t), ("B", c_int), ("H", c_int),
+                ("W", c_int), ("Cin", c_int), ("Cout", c_int), ("dgrad", c_int)]
+
+
 class LossParams(ctypes.Structure):
     _fields_ = [("dice_w", c_float), ("bce_w", c_float), ("rd_w", c_float), ("pf_w", c_float),
                 ("smooth", c_float), ("D", c_float), ("a", c_float), ("eps", c_float),
@@ -43,6 +49,7 @@ _SIGNATURES = {
     "pis_conv3x3_bwd_prep": ([P, I, I, I, I, I, I, P, Z, P, Z, P], c_int),
     "pis_conv3x3_filter_bytes": ([I, I, I, I, I, I], c_size_t),
     "pis_conv3x3_filter": ([P, I, I, I, I, I, I, P, Z, P], c_int),
+    "pis_conv3x3_filters": ([P, I, P], c_int),
     "pis_conv3x3_fwd_pool": ([P, I, P, P, P, P, I, I, I, I, I, I, I, P, Z, P, P, P], c_int),
     "pis_conv3x3_fwd": ([P, I, P, P, P, P, I, I, I, I, I, I, I, P], c_int),
     "pis_conv3x3_flip": ([P, P, I, I, P], c_int),

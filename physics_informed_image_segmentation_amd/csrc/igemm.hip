@@ -702,6 +702,8 @@ extern "C" int pis_conv3x3_flip(const float* w_krsc, float* w_flip, int Cin, int
 namespace pis {  // winograd.hip
 int wino_filter_format(int B, int H, int W, int C, int N, bool kept);
 int launch_wino4_filter_only(const float* w, int C, int N, int dgrad, int format, void* out, hipStream_t s);
+int launch_wino4_filter_batch(int n, const float* const* w, void* const* out, const int* C, const int* N,
+                              const int* dgrad, const int* format, hipStream_t s);
 }  // namespace pis
 
 // the filter transform pis_conv3x3_{fwd_keep,fwd_pool,dgrad_ex} would compute (engine shapes:
@@ -731,6 +733,24 @@ extern "C" int pis_conv3x3_filter(const float* w, int B, int H, int W, int Cin, 
   // forward: contraction C = Cin, outputs N = Cout; input gradient: C = Cout, N = Cin
   return dgrad ? launch_wino4_filter_only(w, Cout, Cin, 1, f, out, (hipStream_t)stream)
                : launch_wino4_filter_only(w, Cin, Cout, 0, f, out, (hipStream_t)stream);
+}
+
+extern "C" int pis_conv3x3_filters(const pis_filter_job* jobs, int n, pis_stream_t stream) {
+  PIS_CHECK_ARG(jobs && n >= 0 && n <= PIS_FILTER_MAX_JOBS, "pis_conv3x3_filters: bad arguments");
+  const float* w[PIS_FILTER_MAX_JOBS];
+  void* out[PIS_FILTER_MAX_JOBS];
+  int C[PIS_FILTER_MAX_JOBS], N[PIS_FILTER_MAX_JOBS], dg[PIS_FILTER_MAX_JOBS], fmt[PIS_FILTER_MAX_JOBS];
+  for (int k = 0; k < n; ++k) {
+    const pis_filter_job& j = jobs[k];
+    const int f = filter_format(j.B, j.H, j.W, j.Cin, j.Cout, j.dgrad);
+    PIS_CHECK_ARG(j.w && j.out && f != 0, "pis_conv3x3_filters: a job has no F(4x4,3x3) GEMM path");
+    PIS_CHECK_ARG(j.out_bytes >= pis_conv3x3_filter_bytes(j.B, j.H, j.W, j.Cin, j.Cout, j.dgrad),
+                  "pis_conv3x3_filters: a job's output is too small");
+    w[k] = j.w; out[k] = j.out; fmt[k] = f; dg[k] = j.dgrad ? 1 : 0;
+    C[k] = j.dgrad ? j.Cout : j.Cin;  // contraction channels
+    N[k] = j.dgrad ? j.Cin : j.Cout;  // output channels
+  }
+  return launch_wino4_filter_batch(n, w, out, C, N, dg, fmt, (hipStream_t)stream);
 }
 
 extern "C" int pis_conv3x3_dgrad(const float* dz, int ldz, const float* w_flip, const float* mask,

@@ -323,12 +323,12 @@ __device__ __forceinline__ void wino4_filter_item(const float (&g)[3][3], int64_
 }
 
 // w: KRSC weights [N][9][C] (row pitch ldw), already in the operand's orientation (the forward's
-// own weights, or pis_conv3x3_flip's copy for an input gradient).
-__global__ __launch_bounds__(256) void wino4_filter_kernel(const float* __restrict__ w, int ldw, int N, int C,
-                                                           float* __restrict__ U, int transposed = 0,
-                                                           __bf16* __restrict__ Up = nullptr) {
+// own weights, or pis_conv3x3_flip's copy for an input gradient). Block `bid` of `nblk`.
+__device__ __forceinline__ void wino4_filter_range(const float* __restrict__ w, int ldw, int N, int C,
+                                                   float* __restrict__ U, int transposed, __bf16* __restrict__ Up,
+                                                   int bid, int nblk) {
   const int64_t NC = (int64_t)N * C;
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < NC; e += (int64_t)gridDim.x * blockDim.x) {
+  for (int64_t e = (int64_t)bid * blockDim.x + threadIdx.x; e < NC; e += (int64_t)nblk * blockDim.x) {
     const int n = (int)(e / C), c = (int)(e - (int64_t)n * C);
     float g[3][3];
 #pragma unroll
@@ -337,17 +337,23 @@ __global__ __launch_bounds__(256) void wino4_filter_kernel(const float* __restri
   }
 }
 
+__global__ __launch_bounds__(256) void wino4_filter_kernel(const float* __restrict__ w, int ldw, int N, int C,
+                                                           float* __restrict__ U, int transposed = 0,
+                                                           __bf16* __restrict__ Up = nullptr) {
+  wino4_filter_range(w, ldw, N, C, U, transposed, Up, blockIdx.x, gridDim.x);
+}
+
 // The input-gradient filter transform straight from the layer's ORIGINAL KRSC weights [C][9][N]
 // (N = Cin, C = Cout; PIS_W_UNFLIPPED): g = the 180-degree-rotated, transposed filter, read in
 // place instead of from a pis_conv3x3_flip copy. N % 32 == 0, C % 32 == 0; a block owns
 // 32 n x 32 c; the 9 taps of that tile are read along n (128-B runs of the original [C][9][N]
 // weights) into LDS and each thread then transforms (n, c) pairs with c fastest, so the 36
 // output planes are written in runs along c as by wino4_filter_kernel.
-__global__ __launch_bounds__(256) void wino4_filter_rot_kernel(const float* __restrict__ w, int N, int C,
-                                                               float* __restrict__ U, int transposed,
-                                                               __bf16* __restrict__ Up) {
+__device__ __forceinline__ void wino4_filter_rot_tile(const float* __restrict__ w, int N, int C,
+                                                      float* __restrict__ U, int transposed,
+                                                      __bf16* __restrict__ Up, int tile) {
   __shared__ float sg[9][32][33];  // [tap][c][n], padded: the transform reads along c conflict-free
-  const int nb = N / 32, n0 = 32 * (blockIdx.x % nb), c0 = 32 * (blockIdx.x / nb);
+  const int nb = N / 32, n0 = 32 * (tile % nb), c0 = 32 * (tile / nb);
   const int tid = threadIdx.x, lx = tid & 31, ly = tid >> 5;
 #pragma unroll
   for (int t = 0; t < 9; ++t)
@@ -366,6 +372,38 @@ __global__ __launch_bounds__(256) void wino4_filter_rot_kernel(const float* __re
     for (int t = 0; t < 9; ++t) g[t / 3][t % 3] = sg[8 - t][c][nl];
     wino4_filter_item(g, (int64_t)n * C + c0 + c, n, c0 + c, N, NC, U, transposed, Up);
   }
+}
+
+__global__ __launch_bounds__(256) void wino4_filter_rot_kernel(const float* __restrict__ w, int N, int C,
+                                                               float* __restrict__ U, int transposed,
+                                                               __bf16* __restrict__ Up) {
+  wino4_filter_rot_tile(w, N, C, U, transposed, Up, blockIdx.x);
+}
+
+// Many layers' filter transforms in ONE launch (pis_conv3x3_filters): one layer's grid is a few
+// to a few hundred blocks, so each separate launch is latency-bound (13-47 us at C2); here every
+// job's blocks run side by side. Block b belongs to the job whose [start, start + blocks) holds it.
+struct FilterJobDev {
+  const float* w;
+  void* out;
+  int N, C, dgrad, planes, blocks;
+};
+constexpr int FILTER_MAX_JOBS = 40;
+struct FilterBatch {
+  FilterJobDev j[FILTER_MAX_JOBS];
+  int start[FILTER_MAX_JOBS + 1];
+  int n;
+};
+
+__global__ __launch_bounds__(256) void wino4_filter_batch_kernel(FilterBatch fb) {
+  int k = 0;
+  while (k + 1 < fb.n && (int)blockIdx.x >= fb.start[k + 1]) ++k;
+  const FilterJobDev& jb = fb.j[k];
+  const int lb = (int)blockIdx.x - fb.start[k];
+  float* U = jb.planes ? nullptr : reinterpret_cast<float*>(jb.out);
+  __bf16* Up = jb.planes ? reinterpret_cast<__bf16*>(jb.out) : nullptr;
+  if (jb.dgrad) wino4_filter_rot_tile(jb.w, jb.N, jb.C, U, 0, Up, lb);
+  else wino4_filter_range(jb.w, 9 * jb.C, jb.N, jb.C, U, 0, Up, lb, jb.blocks);
 }
 
 // V[xi][t][c] = (BT d BT^T)[xi], d = the 6x6 input patch at rows 4ty-1.., cols 4tx-1.. (zero padded)
@@ -1671,6 +1709,27 @@ int launch_wino4_filter_only(const float* w, int C, int N, int dgrad, int format
   if (format == 2) launch_wino4_filter(a, N, C, nullptr, 0, reinterpret_cast<__bf16*>(out), s);
   else launch_wino4_filter(a, N, C, reinterpret_cast<float*>(out), 0, nullptr, s);
   return launch_status("wino_filter");
+}
+
+// jobs: (w, out, contraction C, outputs N, dgrad, format) — validated by the caller
+int launch_wino4_filter_batch(int n, const float* const* w, void* const* out, const int* C, const int* N,
+                              const int* dgrad, const int* format, hipStream_t s) {
+  if (n <= 0) return PIS_OK;
+  if (n > FILTER_MAX_JOBS) return set_error("pis_conv3x3_filters: more than 40 jobs"), PIS_ERR_ARG;
+  FilterBatch fb{};
+  fb.n = n;
+  int total = 0;
+  for (int k = 0; k < n; ++k) {
+    if (dgrad[k] && (N[k] % 32 || C[k] % 32))
+      return set_error("pis_conv3x3_filters: an input-gradient transform needs 32-aligned channels"), PIS_ERR_ARG;
+    const int blocks = dgrad[k] ? (N[k] / 32) * (C[k] / 32) : grid_of((int64_t)N[k] * C[k]);
+    fb.j[k] = FilterJobDev{w[k], out[k], N[k], C[k], dgrad[k], format[k] == 2 ? 1 : 0, blocks};
+    fb.start[k] = total;
+    total += blocks;
+  }
+  fb.start[n] = total;
+  hipLaunchKernelGGL(wino4_filter_batch_kernel, dim3(total), dim3(256), 0, s, fb);
+  return launch_status("wino_filter_batch");
 }
 
 int launch_wino_input(const float* x, int ldx, int B, int H, int W, int C, float* V, hipStream_t s, int m) {

@@ -21,6 +21,7 @@ Memory layout (MI355X-first):
 """
 from __future__ import annotations
 
+import ctypes
 import os
 from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
@@ -324,9 +325,13 @@ class UNetEngine:
     # PIS_FILTER_AHEAD=1: the F(4x4,3x3) filter transforms of a step (forward: the layers' weights;
     # backward: their rotated input-gradient form) run on the side stream, idle during the forward,
     # at its start, and the main stream's convs wait on one event each instead of transforming
-    # their own. Measured 1.5 % SLOWER at C2 (tools/ab_tune.py "base;fa=0": 31.48 vs 31.01 ms, and
-    # 31.39 vs 30.95 with the backward's transforms at the start of the backward): off by default
-    filter_ahead = os.environ.get("PIS_FILTER_AHEAD", "0") == "1"
+    # their own. Measured 1.5 % SLOWER at C2 (tools/ab_tune.py: 31.48 vs 31.01 ms, and 31.39 vs
+    # 30.95 with the backward's transforms at the start of the backward).
+    # PIS_FILTER_AHEAD=2: every filter transform of the step (both directions) in ONE launch on the
+    # main stream at the start of the training forward (pis_conv3x3_filters) instead of 34 small,
+    # latency-bound launches: measured neutral at C2 (31.29 vs 31.27 ms). Default 0: each conv
+    # transforms its own filter.
+    filter_ahead = os.environ.get("PIS_FILTER_AHEAD", "0")
 
     def __init__(self, model: UNet):
         self.m = model
@@ -402,13 +407,15 @@ class UNetEngine:
                 nb = lib.pis_conv3x3_keep_bytes(B, Hl, Wl, conv.in_channels, conv.out_channels)
                 if nb:
                     self.keep[id(conv)] = torch.empty((nb + 3) // 4, dtype=torch.float32, device=dev)
-        # per-layer filter transforms computed ahead on the side stream (forward order; the
-        # backward walks them in reverse): {id(conv): (conv, H, W, buffer)}
+        # per-layer filter transforms computed ahead (forward order; the backward walks them in
+        # reverse): {id(conv): (conv, H, W, buffer)}
         self.ffilt: Dict[int, tuple] = {}
         self.bfilt: Dict[int, tuple] = {}
-        self.fev: Dict[int, torch.cuda.Event] = {}
-        self.bev: Dict[int, torch.cuda.Event] = {}
-        if self.side is not None and self.filter_ahead:
+        self.fev: Dict[int, Optional[torch.cuda.Event]] = {}  # filters computed for this forward
+        self.bev: Dict[int, Optional[torch.cuda.Event]] = {}  # ... for its backward (None: same stream)
+        self.filter_jobs = None
+        mode = str(self.filter_ahead)
+        if (mode == "1" and self.side is not None) or mode == "2":
             for name in BLOCK_ORDER:
                 blk = self.m.block(name)
                 lvl = 5 if name == "bottleneck" else int(name[-1])
@@ -425,6 +432,13 @@ class UNetEngine:
                     if nb and not (name == "enc1" and conv is blk.conv0):  # the first conv has no dgrad
                         self.bfilt[id(conv)] = (conv, Hl, Wl, torch.empty((nb + 3) // 4, dtype=torch.float32,
                                                                           device=dev))
+        if mode == "2" and (self.ffilt or self.bfilt):
+            jobs = [(t, 0) for t in self.ffilt.values()] + [(t, 1) for t in self.bfilt.values()]
+            arr = (_hip.FilterJob * len(jobs))()
+            for k, ((conv, Hl, Wl, buf), dg) in enumerate(jobs):
+                arr[k] = _hip.FilterJob(conv.weight.data_ptr(), buf.data_ptr(), buf.numel() * 4, B, Hl, Wl,
+                                        conv.in_channels, conv.out_channels, dg)
+            self.filter_jobs = arr
 
     def _filters_ahead(self, table, dgrad: int, order):
         """Launch the filter transforms of `table` on the side stream (after everything the main
@@ -477,10 +491,11 @@ class UNetEngine:
         flags = PIS_RELU | (PIS_SCALE if scale is not None else 0)
         keep = self.keep.get(id(conv)) if self._keeping else None
         wptr = conv.weight.data_ptr()
-        ready = self.ffilt.get(id(conv)) if keep is not None else None
-        if ready is not None and id(conv) in self.fev:
-            torch.cuda.current_stream().wait_event(self.fev.pop(id(conv)))
-            wptr, flags = ready[3].data_ptr(), flags | PIS_FILTER_READY
+        if keep is not None and id(conv) in self.fev:
+            ev = self.fev.pop(id(conv))
+            if ev is not None:
+                torch.cuda.current_stream().wait_event(ev)
+            wptr, flags = self.ffilt[id(conv)][3].data_ptr(), flags | PIS_FILTER_READY
         if pool is not None:  # encoder conv1 + MaxPool2d in one call (pooled in the output epilogue)
             call("pis_conv3x3_fwd_pool", x.p, x.ld, wptr, conv.bias.data_ptr(), ptr(scale),
                  y.p, y.ld, B, H, W, conv.in_channels, conv.out_channels, flags, self.ws.data_ptr(), self.ws_bytes,
@@ -517,7 +532,11 @@ class UNetEngine:
         # the side stream is idle during the forward: it transforms every filter of the step there,
         # the forward's in layer order, then the input gradients' (backward order)
         self.fev, self.bev = {}, {}
-        if keep and self.side is not None:
+        if keep and self.filter_jobs is not None:  # one launch, same stream: no events
+            call("pis_conv3x3_filters", ctypes.addressof(self.filter_jobs), len(self.filter_jobs), self._stream())
+            self.fev = dict.fromkeys(self.ffilt)
+            self.bev = dict.fromkeys(self.bfilt)
+        elif keep and self.side is not None:
             if self.ffilt:
                 self.fev = self._filters_ahead(self.ffilt, 0, list(self.ffilt))
             if self.bfilt:
@@ -626,7 +645,7 @@ class UNetEngine:
         # alternating weight-gradient workspaces is ordered before this point already (and a
         # graph capture must not wait on events recorded outside it)
         self.ws3_free = [None, None]
-        if side is main:
+        if side is main and self.filter_jobs is None:
             self.bev = {}  # serialised A/B mode: each dgrad transforms its own filter
         gb = self._gbuf
 
@@ -692,7 +711,9 @@ class UNetEngine:
                 if prep:
                     wf, flags = conv.weight.data_ptr(), flags | PIS_WINO_PREPARED | PIS_W_UNFLIPPED
                     if id(conv) in self.bev:  # its rotated filter transform, computed ahead
-                        main.wait_event(self.bev.pop(id(conv)))
+                        ev = self.bev.pop(id(conv))
+                        if ev is not None:
+                            main.wait_event(ev)
                         wf, flags = self.bfilt[id(conv)][3].data_ptr(), flags | PIS_FILTER_READY
                 else:
                     wf = flipped(conv).data_ptr()

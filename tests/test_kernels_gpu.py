@@ -1,5 +1,7 @@
 """Per-kernel parity through the C-ABI on the GPU, against stock fp32 PyTorch on
 the CPU (the ATen ops the reference calls) and the float64 numpy loss oracle."""
+import ctypes
+
 import numpy as np
 import pytest
 import torch
@@ -856,3 +858,28 @@ def test_filter_ready_refused_off_the_winograd_path(hip):
     rc = hip.pis_conv3x3_fwd_ex(x.data_ptr(), 1, w.data_ptr(), 0, 0, y.data_ptr(), 64, 1, 16, 16, 1, 64, 64, 0, 0,
                                 torch.cuda.current_stream().cuda_stream)
     assert rc != 0
+
+
+def test_batched_filter_transforms_match_single(hip):
+    """pis_conv3x3_filters (every layer's filter transform in one launch) writes bitwise what
+    pis_conv3x3_filter writes per layer, both directions and both formats."""
+    from physics_informed_image_segmentation_amd import _hip
+    s = torch.cuda.current_stream().cuda_stream
+    g = torch.Generator().manual_seed(4)
+    shapes = [(2, 64, 64, 64, 64, 0), (2, 64, 64, 64, 64, 1), (2, 32, 32, 128, 128, 0), (2, 32, 32, 256, 128, 1),
+              (2, 16, 16, 512, 256, 0), (2, 16, 16, 512, 256, 1)]
+    jobs = (_hip.FilterJob * len(shapes))()
+    keep = []
+    for k, (B, H, W, ci, co, dg) in enumerate(shapes):
+        w = (torch.randn(co, 3, 3, ci, generator=g) * 0.1).cuda()
+        nb = hip.pis_conv3x3_filter_bytes(B, H, W, ci, co, dg)
+        assert nb > 0
+        one = torch.empty(nb // 4 + 1, device="cuda")
+        bat = torch.empty(nb // 4 + 1, device="cuda")
+        assert hip.pis_conv3x3_filter(w.data_ptr(), B, H, W, ci, co, dg, one.data_ptr(), nb, s) == 0
+        jobs[k] = _hip.FilterJob(w.data_ptr(), bat.data_ptr(), nb, B, H, W, ci, co, dg)
+        keep.append((w, one, bat, nb))
+    assert hip.pis_conv3x3_filters(ctypes.addressof(jobs), len(shapes), s) == 0
+    torch.cuda.synchronize()
+    for w, one, bat, nb in keep:
+        assert torch.equal(one[:nb // 4], bat[:nb // 4])

@@ -4,7 +4,7 @@ GPU (box-to-box variance is ~3 %; same-process interleaving is not).
     python tools/ab_tune.py --variants "base;20=0;15=0,17=4" [--rounds 4] [--steps 10]
 
 Each variant is a comma list of KEY=VALUE (include/pis_capi.h PIS_TUNE_*); "base" = defaults;
-"fa=1" / "fa=0" plans that variant's engine with / without the filter transforms computed ahead.
+"fa=0|1|2" plans that variant's engine with PIS_FILTER_AHEAD = that value (unet.py).
 """
 import argparse
 import os
@@ -57,7 +57,7 @@ def main():
 
     def step(name):
         model, opt = models[name]
-        UNetEngine.filter_ahead = bool(dict(variants)[name].get("fa", fa_default))
+        UNetEngine.filter_ahead = str(dict(variants)[name].get("fa", fa_default))
         opt.zero_grad()
         crit(model(x), t).backward()
         opt.step()
