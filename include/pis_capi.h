@@ -81,7 +81,9 @@ int pis_version(void);
 #define PIS_TUNE_WGRAD_X6 14     /* Winograd and transposed-conv weight-gradient GEMMs: 1 (default) fp32-accurate
                                     bf16x6 on bf16 MFMA, 0 fp32 MFMA */
 #define PIS_TUNE_WINO_GEMM_OUT 15 /* F(4x4,3x3) 64 -> 64 channels: 1 (default) the 36 bf16x6 contractions fused with
-                                     the output transform (M stays on chip), 0 separate GEMM + output transform */
+                                     the output transform (M stays on chip; 4 groups of 32 tiles per block), 2 / 3 / 4
+                                     the same with 1 / 2 / 8 groups per block (bitwise equal), 0 separate GEMM +
+                                     output transform */
 #define PIS_TUNE_WINO_DZ2 16     /* pis_conv3x3_bwd_prep: 1 (default) one pass over dz for both transforms, 0 off */
 #define PIS_TUNE_WINO_VW 17      /* F(4x4) input / output transforms: 2 (default: half the registers, +2-11 % on the
                                     512^2-256^2 layers) or 4 channels per thread */

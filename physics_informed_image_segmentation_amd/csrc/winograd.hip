@@ -115,6 +115,23 @@ __device__ __forceinline__ fvec<VW> conv_epilogue4(const IGemmArgs& g, size_t pi
   return v;
 }
 
+// the same with the ReLU-backward mask already loaded (mk; ignored without PIS_MASK)
+__device__ __forceinline__ f32x4 conv_epilogue4m(const IGemmArgs& g, size_t pix, int n, f32x4 v, f32x4 sc4, f32x4 mk) {
+  if (g.flags & PIS_RELU) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = fmaxf(v[k], 0.f);
+  }
+  if (g.flags & PIS_MASK) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = mk[k] > 0.f ? v[k] : 0.f;
+  }
+  v *= sc4;
+  float* dst = g.dst + pix * g.ldd + n;
+  if (g.flags & PIS_ACCUMULATE) v += *reinterpret_cast<const f32x4*>(dst);
+  *reinterpret_cast<f32x4*>(dst) = v;
+  return v;
+}
+
 template <int VW = 4>
 __device__ __forceinline__ fvec<VW> max4(fvec<VW> a, fvec<VW> b, fvec<VW> c, fvec<VW> d) {
   fvec<VW> m;
@@ -1331,7 +1348,7 @@ constexpr size_t X6W8_SMEM = 2 * 3 * 384 * 32 * sizeof(__bf16);  // 147,456 B
 // epilogue (bias, ReLU, mask, keep-scale, accumulate).
 typedef __bf16 bf16x8g __attribute__((ext_vector_type(8)));
 
-template <int NWN, int NWT, int KC>
+template <int NWN, int NWT, int KC, int G = 1>
 __global__ __launch_bounds__(64 * NWN * NWT) void wino4_gemm_out_x6_kernel(const float* __restrict__ V,
                                                                           const __bf16* __restrict__ Up,
                                                                           IGemmArgs g, int B) {
@@ -1346,19 +1363,28 @@ __global__ __launch_bounds__(64 * NWN * NWT) void wino4_gemm_out_x6_kernel(const
   constexpr int NU8 = 3 * NN * KC / 8, UL = NU8 / NT;          // 16-B chunks of the U[xi] planes per thread
   static_assert((!VPART || NV4 < NT) && NU8 % NT == 0, "staging must tile the block");
   constexpr int RING = 6, KS = KC / 32;
-  __shared__ __attribute__((aligned(16))) __bf16 sA[2][3][TB * KP];
-  __shared__ __attribute__((aligned(16))) __bf16 sU[2][3][NN * KP];
+  // LDS: the double-buffered operand planes, and (aliased) the epilogue's staging of all four
+  // tile quarters of Y (139 KB: one block per CU either way, its registers allow no second)
+  constexpr int QT = 4 * NWT, EP = NN + 4, EQ = QT * 16 * EP;  // tiles per quarter; row pitch, floats
+  constexpr int OPS_BYTES = 2 * 3 * (TB + NN) * KP * 2, EPI_BYTES = 4 * EQ * 4;
+  static_assert(QT * 4 * (NN / 4) == NT, "one epilogue item per thread and quarter");
+  __shared__ __attribute__((aligned(16))) char smem[OPS_BYTES > EPI_BYTES ? OPS_BYTES : EPI_BYTES];
+  auto sA = reinterpret_cast<__bf16(*)[3][TB * KP]>(smem);
+  auto sU = reinterpret_cast<__bf16(*)[3][NN * KP]>(smem + 2 * 3 * TB * KP * 2);
+  float* E = reinterpret_cast<float*>(smem);
   const int N = g.N, TW = g.W / 4, TH = g.H / 4;
   const int64_t T = (int64_t)B * TH * TW;
-  const int64_t TK = T * KC, NK = (int64_t)N * KC;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  int64_t TK = T * KC, NK = (int64_t)N * KC;  // laundered per group with Ug (below)
+  int tid = threadIdx.x;  // laundered per group (below), like every tid-derived address
+  const int lane = tid & 63, wave = tid >> 6;
   const int wn = wave % NWN, wt = wave / NWN;
   const int lr = lane & 15, lq = lane >> 4;
-  const int64_t t0 = (int64_t)xcd_remap(blockIdx.x, gridDim.x) * TB;
   const int n = 16 * wn + lr;  // this lane's output channel
-  const float* vb = V + t0 * KC;
+  // G consecutive groups of TB tiles per block: the next group's first V and U loads are issued
+  // before this group's epilogue, so their latency hides behind its stores
+  const int64_t grp0 = (int64_t)blockIdx.x * G;
   f32x4 vr[RING][AL];
-  auto gload = [&](int xi, f32x4 (&r)[AL]) {
+  auto gload = [&](const float* vb, int xi, f32x4 (&r)[AL]) {
 #pragma unroll
     for (int i = 0; i < AL; ++i) {
       if (!VPART || tid + i * NT < NV4) r[i] = *reinterpret_cast<const f32x4*>(vb + xi * TK + 4 * (tid + i * NT));
@@ -1378,12 +1404,13 @@ __global__ __launch_bounds__(64 * NWN * NWT) void wino4_gemm_out_x6_kernel(const
     }
   };
   u32x4 ur[2][UL];
+  const __bf16* Ug = Up;  // laundered per group (below): keeps 36 x UL U addresses from being hoisted
   auto uload = [&](int xi, u32x4 (&r)[UL]) {
 #pragma unroll
     for (int i = 0; i < UL; ++i) {
       const int c = tid + i * NT;  // (plane, channel, 8-k chunk), k fastest: contiguous per plane
       const int pl = c / (NN * KC / 8), rem = c % (NN * KC / 8);
-      r[i] = *reinterpret_cast<const u32x4*>(Up + (pl * 36 + xi) * NK + 8 * rem);
+      r[i] = *reinterpret_cast<const u32x4*>(Ug + (pl * 36 + xi) * NK + 8 * rem);
     }
   };
   auto ustore = [&](int buf, const u32x4 (&r)[UL]) {
@@ -1395,114 +1422,140 @@ __global__ __launch_bounds__(64 * NWN * NWT) void wino4_gemm_out_x6_kernel(const
       *reinterpret_cast<u32x4*>(&sU[buf][pl][sw(row, k)]) = r[i];
     }
   };
-  f32x4 y[4][4], rr[4];
+  // a group's first stages: V[0..RING) and U[0..2) in flight, V[0] / U[0] in LDS buffer 0
+  auto prime = [&](const float* vb) {
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    rr[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int j = 0; j < 4; ++j) y[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  }
-#pragma unroll
-  for (int j = 0; j < RING; ++j) gload(j, vr[j]);
-  uload(0, ur[0]);
-  uload(1, ur[1]);
-  lstore(0, vr[0]);
-  ustore(0, ur[0]);
-  gload(RING, vr[0]);
-  uload(2, ur[0]);
-  __syncthreads();
-#pragma unroll
-  for (int a = 0; a < 6; ++a) {  // fully unrolled: the compiler keeps exact vmcnt counts across rows
-#pragma unroll
-    for (int b = 0; b < 6; ++b) {
-      const int xi = 6 * a + b, cur = b & 1;
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int s = 0; s < KS; ++s) {
-        const int k = 32 * s + 8 * lq;
-        bf16x8g af[3], bf[3];
-#pragma unroll
-        for (int p = 0; p < 3; ++p) {
-          af[p] = *reinterpret_cast<const bf16x8g*>(&sA[cur][p][sw(16 * wt + lr, k)]);
-          bf[p] = *reinterpret_cast<const bf16x8g*>(&sU[cur][p][sw(n, k)]);
-        }
-        // smallest partial products first
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[2], bf[0], acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[1], bf[1], acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0], bf[2], acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[1], bf[0], acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0], bf[1], acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0], bf[0], acc, 0, 0, 0);
-      }
-#pragma unroll
-      for (int j = 0; j < 4; ++j) axpy_c(rr[j], w4_at(j, b), acc);
-      // stage xi + 1 (V from its ring slot, U from the register pair), then refill both
-      const int vslot = (b + 1) % RING;
-      if (xi + 1 < 36) {
-        lstore(cur ^ 1, vr[vslot]);
-        ustore(cur ^ 1, ur[cur ^ 1]);
-      }
-      if (xi + 1 + RING < 36) gload(xi + 1 + RING, vr[vslot]);
-      if (xi + 3 < 36) uload(xi + 3, ur[cur ^ 1]);
-      __syncthreads();
-    }
-    // Y[i][j] += AT[i][a] R[j] (a is a runtime row index: coefficients selected from the table)
-    float at[4];
+    for (int j = 0; j < RING; ++j) gload(vb, j, vr[j]);
+  };
+  auto first_stage = [&](const float* vb) {
+    uload(0, ur[0]);
+    uload(1, ur[1]);
+    lstore(0, vr[0]);
+    ustore(0, ur[0]);
+    gload(vb, RING, vr[0]);
+    uload(2, ur[0]);
+    __syncthreads();
+  };
+  prime(V + grp0 * TB * KC);
+  first_stage(V + grp0 * TB * KC);
+#pragma unroll 1
+  for (int gi = 0; gi < G; ++gi) {
+    const int64_t t0 = (grp0 + gi) * TB;
+    const float* vb = V + t0 * KC;
+    asm volatile("" : "+s"(Ug), "+s"(TK), "+s"(NK), "+v"(tid));
+    f32x4 y[4][4], rr[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      float v = 0.f;
+      rr[i] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int q = 0; q < 6; ++q) v = a == q ? w4_at(i, q) : v;
-      at[i] = v;
+      for (int j = 0; j < 4; ++j) y[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int a = 0; a < 6; ++a) {  // fully unrolled: the compiler keeps exact vmcnt counts across rows
 #pragma unroll
-      for (int j = 0; j < 4; ++j) y[i][j] += at[i] * rr[j];
+      for (int b = 0; b < 6; ++b) {
+        const int xi = 6 * a + b, cur = b & 1;
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int j = 0; j < 4; ++j) rr[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  }
-  // epilogue, one tile quarter q at a time: the lanes' (channel n, tiles t0 + 16 wt + 4 lq + q)
-  // values go through LDS (the operand buffers are free now) so that every thread finishes
-  // 4 consecutive channels of one pixel with float4 accesses (conv_epilogue4)
-  constexpr int QT = 4 * NWT, EP = NN + 4;  // tiles per quarter; LDS row pitch (floats)
-  static_assert(QT * 16 * EP * 4 <= (int)sizeof(sU), "epilogue staging must fit in the U buffers");
-  float* E = reinterpret_cast<float*>(&sU[0][0][0]);
-  auto eaddr = [&](int idx) -> float* { return E + idx; };
+        for (int s = 0; s < KS; ++s) {
+          const int k = 32 * s + 8 * lq;
+          bf16x8g af[3], bf[3];
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
+          for (int p = 0; p < 3; ++p) {
+            af[p] = *reinterpret_cast<const bf16x8g*>(&sA[cur][p][sw(16 * wt + lr, k)]);
+            bf[p] = *reinterpret_cast<const bf16x8g*>(&sU[cur][p][sw(n, k)]);
+          }
+          // smallest partial products first
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[2], bf[0], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[1], bf[1], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0], bf[2], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[1], bf[0], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0], bf[1], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0], bf[0], acc, 0, 0, 0);
+        }
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j) axpy_c(rr[j], w4_at(j, b), acc);
+        // stage xi + 1 (V from its ring slot, U from the register pair), then refill both
+        const int vslot = (b + 1) % RING;
+        if (xi + 1 < 36) {
+          lstore(cur ^ 1, vr[vslot]);
+          ustore(cur ^ 1, ur[cur ^ 1]);
+        }
+        if (xi + 1 + RING < 36) gload(vb, xi + 1 + RING, vr[vslot]);
+        if (xi + 3 < 36) uload(xi + 3, ur[cur ^ 1]);
+        __syncthreads();
+      }
+      // Y[i][j] += AT[i][a] R[j] (a is a runtime row index: coefficients selected from the table)
+      float at[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) *eaddr(((4 * wt + lq) * 16 + 4 * i + j) * EP + n) = y[i][j][q];
-    __syncthreads();
-    // one 2x2 pixel quad x 4 channels per item (the max pool of the quad when g.pool is set)
-    for (int idx = tid; idx < QT * 4 * (NN / 4); idx += NT) {
-      const int c4 = idx % (NN / 4), pq = idx / (NN / 4);
-      const int tl = pq / 4, quad = pq % 4, qi = quad >> 1, qj = quad & 1;
+      for (int i = 0; i < 4; ++i) {
+        float v = 0.f;
+#pragma unroll
+        for (int q = 0; q < 6; ++q) v = a == q ? w4_at(i, q) : v;
+        at[i] = v;
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) y[i][j] += at[i] * rr[j];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) rr[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    const bool more = gi + 1 < G;
+    if (more) prime(vb + TB * KC);
+    // epilogue: the lanes' (channel n, tiles t0 + 16 wt + 4 lq + q) values of all four tile
+    // quarters q go through LDS so that every thread finishes 4 consecutive channels of one 2x2
+    // pixel quad per quarter with float4 accesses; its ReLU-mask loads for the four quads are
+    // issued together, before the barrier (one memory round trip per group, not four)
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) E[q * EQ + ((4 * wt + lq) * 16 + 4 * i + j) * EP + n] = y[i][j][q];
+    int et = tid;  // laundered: the epilogue's index math stays out of the group loop's registers
+    asm volatile("" : "+v"(et));
+    const int c4 = et % (NN / 4), pq = et / (NN / 4);
+    const int tl = pq / 4, quad = pq % 4, qi = quad >> 1, qj = quad & 1, nn = 4 * c4;
+    size_t pix0[4], pp[4];  // the quad's first pixel; its pooled pixel
+    int bq[4];
+    f32x4 mk[4][2][2];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
       const int64_t t = t0 + 16 * (tl / 4) + 4 * (tl % 4) + q;
       const int b = (int)(t / (TH * TW)), rem = (int)(t - (int64_t)b * TH * TW);
       const int ty = rem / TW, tx = rem - ty * TW;
-      const int nn = 4 * c4;
-      f32x4 bias4 = {0.f, 0.f, 0.f, 0.f}, sc4 = {1.f, 1.f, 1.f, 1.f};
-      if (g.bias) bias4 = *reinterpret_cast<const f32x4*>(g.bias + nn);
-      if (g.flags & PIS_SCALE) sc4 = *reinterpret_cast<const f32x4*>(g.scale + (size_t)b * N + nn);
+      bq[q] = b;
+      pix0[q] = ((size_t)b * g.H + 4 * ty + 2 * qi) * g.W + 4 * tx + 2 * qj;
+      pp[q] = ((size_t)b * (g.H / 2) + 2 * ty + qi) * (g.W / 2) + 2 * tx + qj;
+#pragma unroll
+      for (int di = 0; di < 2; ++di)
+#pragma unroll
+        for (int dj = 0; dj < 2; ++dj)
+          mk[q][di][dj] = (g.flags & PIS_MASK)
+                              ? *reinterpret_cast<const f32x4*>(g.mask + (pix0[q] + di * g.W + dj) * g.ldm + nn)
+                              : f32x4{1.f, 1.f, 1.f, 1.f};
+    }
+    __syncthreads();
+    f32x4 bias4 = {0.f, 0.f, 0.f, 0.f};
+    if (g.bias) bias4 = *reinterpret_cast<const f32x4*>(g.bias + nn);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      f32x4 sc4 = {1.f, 1.f, 1.f, 1.f};
+      if (g.flags & PIS_SCALE) sc4 = *reinterpret_cast<const f32x4*>(g.scale + (size_t)bq[q] * N + nn);
       f32x4 o[2][2];
 #pragma unroll
       for (int di = 0; di < 2; ++di)
 #pragma unroll
         for (int dj = 0; dj < 2; ++dj) {
           const int i = 2 * qi + di, j = 2 * qj + dj;
-          const f32x4 v = *reinterpret_cast<const f32x4*>(eaddr((tl * 16 + 4 * i + j) * EP + nn));
-          const size_t pix = ((size_t)b * g.H + 4 * ty + i) * g.W + 4 * tx + j;
-          o[di][dj] = conv_epilogue4(g, pix, nn, v + bias4, sc4);
+          const f32x4 v = *reinterpret_cast<const f32x4*>(&E[q * EQ + (tl * 16 + 4 * i + j) * EP + nn]);
+          o[di][dj] = conv_epilogue4m(g, pix0[q] + di * g.W + dj, nn, v + bias4, sc4, mk[q][di][dj]);
         }
-      if (g.pool) {
-        const size_t pp = ((size_t)b * (g.H / 2) + 2 * ty + qi) * (g.W / 2) + 2 * tx + qj;
-        *reinterpret_cast<f32x4*>(g.pool + pp * N + nn) = max4(o[0][0], o[0][1], o[1][0], o[1][1]);
-      }
+      if (g.pool) *reinterpret_cast<f32x4*>(g.pool + pp[q] * N + nn) = max4(o[0][0], o[0][1], o[1][0], o[1][1]);
     }
     __syncthreads();
+    if (more) first_stage(vb + TB * KC);
   }
 }
 
@@ -1549,8 +1602,20 @@ static bool wino_gemm_out_wanted(int m, int64_t T, int C, int N) {
 
 static int launch_wino_gemm_out(const float* V, const __bf16* Up, const IGemmArgs& a, int B, int64_t T,
                                 hipStream_t s) {
-  // 8 waves: 32 tiles x 64 channels per block
-  hipLaunchKernelGGL((wino4_gemm_out_x6_kernel<4, 2, 64>), dim3((int)(T / 32)), dim3(512), 0, s, V, Up, a, B);
+  // 8 waves: 32 tiles x 64 channels per block; G such groups per block where they divide
+  // (pis_tune key 15: 1 -> G = 4, 2 -> 1, 3 -> 2, 4 -> 8: experiments)
+  const int64_t groups = T / 32;
+  const int mode = tune_get(PIS_TUNE_WINO_GEMM_OUT);
+  const int G = mode == 2 ? 1 : mode == 3 ? 2 : mode == 4 ? 8 : 4;
+  const dim3 blk(512);
+  if (G == 8 && groups % 8 == 0)
+    hipLaunchKernelGGL((wino4_gemm_out_x6_kernel<4, 2, 64, 8>), dim3((int)(groups / 8)), blk, 0, s, V, Up, a, B);
+  else if (G == 4 && groups % 4 == 0)
+    hipLaunchKernelGGL((wino4_gemm_out_x6_kernel<4, 2, 64, 4>), dim3((int)(groups / 4)), blk, 0, s, V, Up, a, B);
+  else if (G == 2 && groups % 2 == 0)
+    hipLaunchKernelGGL((wino4_gemm_out_x6_kernel<4, 2, 64, 2>), dim3((int)(groups / 2)), blk, 0, s, V, Up, a, B);
+  else
+    hipLaunchKernelGGL((wino4_gemm_out_x6_kernel<4, 2, 64, 1>), dim3((int)groups), blk, 0, s, V, Up, a, B);
   return launch_status("wino_gemm_out");
 }
 

@@ -661,6 +661,54 @@ def test_convt_bf16x6_is_fp32_accurate(hip, Cin, Cout):
         assert e6 < 5e-6, errs
 
 
+@pytest.mark.parametrize("B,H,W", [(2, 32, 64), (1, 16, 128), (3, 32, 32)])
+def test_fused_64_groups_per_block_bitwise(hip, B, H, W):
+    """The fused 64->64 contraction + output transform takes G groups of 32 tiles per block
+    (pis_tune key 15: 1 -> G = 4 where the group count divides, 2 -> 1, 3 -> 2, 4 -> 8): every G
+    gives bit-for-bit the same forward (ReLU, keep-scale, fused max pool) and input gradient
+    (ReLU mask, keep-scale, accumulate), and G = 1 matches the float64 reference."""
+    Cin = Cout = 64
+    g = torch.Generator().manual_seed(31)
+    x = F.relu(torch.randn(B, Cin, H, W, generator=g))
+    w = torch.randn(Cout, Cin, 3, 3, generator=g) / (3 * Cin ** 0.5)
+    b = torch.randn(Cout, generator=g)
+    scale = (torch.rand(B, Cout, generator=g) > 0.2).float() / 0.8
+    dz = torch.randn(B, Cout, H, W, generator=g)
+    xd, wd, bd, sd, dzd = nhwc(x).cuda(), krsc(w).cuda(), b.cuda(), scale.cuda(), nhwc(dz).cuda()
+    nws = hip.pis_conv3x3_ex_ws(B, H, W, Cin, Cout)
+    ws = torch.empty(nws // 4 + 1, device="cuda")
+    wf = torch.empty(Cin * 9 * Cout, device="cuda")
+    assert hip.pis_conv3x3_flip(wd.data_ptr(), wf.data_ptr(), Cin, Cout, s()) == 0
+    prev = hip.pis_tune(15, -1)
+    out = {}
+    try:
+        for v in (2, 1, 3, 4):
+            hip.pis_tune(15, v)
+            y = torch.empty(B, H, W, Cout, device="cuda")
+            pool = torch.empty(B, H // 2, W // 2, Cout, device="cuda")
+            rc = hip.pis_conv3x3_fwd_pool(xd.data_ptr(), Cin, wd.data_ptr(), bd.data_ptr(), sd.data_ptr(),
+                                          y.data_ptr(), Cout, B, H, W, Cin, Cout, RELU | SCALE, ws.data_ptr(), nws,
+                                          0, pool.data_ptr(), s())
+            assert rc == 0, hip.pis_last_error()
+            dx = torch.full((B, H, W, Cin), 0.5, device="cuda")
+            rc = hip.pis_conv3x3_dgrad_ex(dzd.data_ptr(), Cout, wf.data_ptr(), xd.data_ptr(), Cin, sd.data_ptr(),
+                                          dx.data_ptr(), Cin, B, H, W, Cin, Cout, MASK | SCALE | ACC, ws.data_ptr(),
+                                          nws, s())
+            assert rc == 0, hip.pis_last_error()
+            torch.cuda.synchronize()
+            out[v] = (y.cpu(), pool.cpu(), dx.cpu())
+    finally:
+        hip.pis_tune(15, prev)
+    for v in (1, 3, 4):
+        for a, c in zip(out[2], out[v]):
+            assert torch.equal(a, c), v
+    y_ref = F.relu(F.conv2d(x.double(), w.double(), b.double(), padding=1)) * scale[:, :, None, None]
+    dx_ref = torch.nn.grad.conv2d_input(x.shape, w.double(), dz.double(), padding=1) * (x > 0) * scale[:, :, None, None]
+    assert rel_err(nchw(out[2][0]), y_ref) < 1e-6
+    assert rel_err(nchw(out[2][1]), F.max_pool2d(y_ref, 2)) < 1e-6
+    assert rel_err(nchw(out[2][2]) - 0.5, dx_ref) < 1e-6
+
+
 @pytest.mark.parametrize("B,H,W,Cin,Cout", [(2, 32, 64, 64, 64), (2, 16, 32, 128, 128), (1, 32, 32, 128, 64),
                                            (2, 16, 16, 256, 256)])
 def test_conv3x3_bwd_prep(hip, B, H, W, Cin, Cout):
