@@ -85,7 +85,7 @@ def conv_flops_per_image(H: int, W: int, c: int = 64) -> float:
 # of the Winograd 3x3 convs (forward + input gradient), launched as "wino_gemm" by the C-ABI
 # (csrc/winograd.hip) and named gemm_nt_kernel<128, 128> / <128, 64> by rocprofv3.
 DOMINANT = "wino_gemm"
-DOMINANT_KERNEL = "gemm_nt_kernel<"  # rocprofv3 name stem; gemm_nt_x6_kernel< on the bf16x6 pipe (key 10 = 3)
+DOMINANT_KERNEL = "gemm_nt_kernel<"  # rocprofv3 name stem on the fp32 pipe (key 10 = 2); gemm_nt_h3_ / gemm_nt_x6_ on fp16x3 / bf16x6
 
 
 def loss_call_bytes(name, a):
@@ -419,16 +419,20 @@ def main():
     _hip.set_launch_hook(None)
     eng.side = side
     _, iso_flop, iso_ms = iso.summary()
-    # the pipe the dominant kernel runs on: fp32-accurate GEMMs via bf16x6 (pis_tune key 10 = 3,
-    # the default) execute six bf16 MFMAs per fp32 multiply-add, so their roofline is the dense
-    # bf16 MFMA peak (~2.5 PFLOP/s, MI355X_MICROARCH.md / the task's dense figure) / 6 in
-    # fp32-equivalent FLOPs; the native fp32 MFMA path (key 10 = 2) peaks at 157.3 TFLOP/s
-    x6 = _hip.lib().pis_tune(10, -1) == 3
-    peak = 2500.0 / 6.0 if x6 else 157.3
-    pipe = ("bf16 MFMA, fp32-accurate bf16x6 split (6 bf16 products per fp32 multiply-add); achieved/peak in "
+    # the pipe the dominant kernel runs on. fp32-class GEMMs on the MFMA pipe: fp16x3 (pis_tune
+    # key 10 = 4, the default: per-K-step power-of-two tile scales, hi + lo fp16 split, three
+    # fp16 MFMAs per fp32 multiply-add) peaks at the dense fp16 MFMA rate (~2.5 PFLOP/s,
+    # MI355X_MICROARCH.md / the task's dense figure) / 3 in fp32-equivalent FLOPs; bf16x6 (key 10
+    # = 3: six bf16 MFMAs) at / 6; the native fp32 MFMA path (key 10 = 2) at 157.3 TFLOP/s
+    mode = _hip.lib().pis_tune(10, -1)
+    x6, h3 = mode == 3, mode == 4
+    peak = 2500.0 / 3.0 if h3 else 2500.0 / 6.0 if x6 else 157.3
+    pipe = ("fp16 MFMA, fp32-class fp16x3 split (per-K-step power-of-two tile scales, hi + lo fp16, 3 fp16 "
+            "products per fp32 multiply-add); achieved/peak in fp32-equivalent FLOPs" if h3 else
+            "bf16 MFMA, fp32-accurate bf16x6 split (6 bf16 products per fp32 multiply-add); achieved/peak in "
             "fp32-equivalent FLOPs" if x6 else "fp32 MFMA")
-    # bf16x6: gemm_nt_x6_bk32_kernel (K % 32 == 0, every C2 layer) or gemm_nt_x6_kernel
-    kname = "gemm_nt_x6_" if x6 else DOMINANT_KERNEL
+    # gemm_nt_h3_bk32_kernel / gemm_nt_x6_bk32_kernel (K % 32 == 0, every C2 layer)
+    kname = "gemm_nt_h3_" if h3 else "gemm_nt_x6_" if x6 else DOMINANT_KERNEL
     traffic, mfma_busy, busy_by_kernel = load_pmc(kname)
     loss_cold = loss_standalone(model.engine().u, t, loss_kw)
     if rank == 0:
@@ -441,11 +445,15 @@ def main():
             "vs_baseline": None, "dtype": "fp32", "data": "synthetic",
             "config": {"workload": workload,
                        "global_batch": B * world, "image_size": [H, W], "parallelism": f"dp{world}"},
-            "roofline": {"bound": "mfma", "kernel": ("gemm_nt_x6_bk32_kernel<128, 128|64>" if x6 else "gemm_nt_kernel<128, 128|64>")
+            "roofline": {"bound": "mfma", "kernel": ("gemm_nt_h3_bk32_kernel<128, 128|64>" if h3 else
+                                                     "gemm_nt_x6_bk32_kernel<128, 128|64>" if x6 else
+                                                     "gemm_nt_kernel<128, 128|64>")
                          + f" ({DOMINANT}: the 36 batched GEMMs of Winograd F(4x4,3x3) fwd/dgrad)",
                          "achieved": achieved, "peak": peak,
                          "unit": "TFLOP/s", "frac": achieved / peak, "traffic": traffic, "pipe": pipe,
                          "fp32_mfma_peak_frac": achieved / 157.3,
+                         # against the round-1/2 bf16x6 pipe roofline (2.5 PF / 6), for continuity
+                         "bf16x6_roofline_frac": achieved / (2500.0 / 6.0),
                          # rocprofv3 PMC (profiles/pmc_dominant.json): fraction of SIMD-cycles the
                          # matrix pipe was busy in this kernel, and in the step's other kernels
                          "mfma_busy_frac": mfma_busy, "mfma_busy_by_kernel": busy_by_kernel,

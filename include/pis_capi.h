@@ -68,8 +68,11 @@ int pis_version(void);
                                     2 Winograd whenever legal */
 #define PIS_TUNE_WINO_WGRAD_BLOCKS 9 /* target workgroups of the 16 batched Winograd weight-gradient GEMMs */
 #define PIS_TUNE_WINO_TILE 10    /* Winograd batched GEMM: 0 generic igemm, 1 lean NT GEMM 128x256 (N % 256 == 0), 2 lean NT GEMM
-                                    128x128|64 on fp32 MFMA, 3 (default) the same at fp32 accuracy on bf16 MFMA ("bf16x6":
-                                    exact 3-way bf16 split of each operand, the six partial products >= 2^-24) */
+                                    128x128|64 on fp32 MFMA, 3 the same at fp32 accuracy on bf16 MFMA ("bf16x6": exact
+                                    3-way bf16 split of each operand, the six partial products >= 2^-24), 4 (default)
+                                    "fp16x3" on fp16 MFMA: each K-step's operand tiles scaled by a power of two into
+                                    fp16 range, split into hi + lo fp16 (22 significant bits), the three products
+                                    above 2^-22 accumulated in fp32 (measured error below fp32 MFMA's and bf16x6's) */
 #define PIS_TUNE_WINO_F4 11      /* Winograd tile: 0 F(2x2,3x3) fwd/dgrad + F(3x3,2x2) wgrad; 1 (default) F(4x4,3x3) +
                                     F(3x3,4x4) when H % 4 == W % 4 == 0 */
 #define PIS_TUNE_WINO_FUSED 12   /* F(4x4,3x3) fwd/dgrad as ONE fused kernel (transforms in LDS/registers): 0/1 off

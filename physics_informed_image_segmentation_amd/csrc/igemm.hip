@@ -563,7 +563,7 @@ static bool wino_wanted_dims(int H, int W, int C, int N) {
   // F(2x2,3x3) needs >= 256 contraction channels and 128 outputs. With the bf16x6 GEMMs
   // (key 10 = 3) F(4x4,3x3) also wins at 64 -> 64 (enc1.conv1 fwd -13 %, dgrad -11 %).
   if (wino_tile(H, W) == 4)
-    return C >= 128 || N >= 128 || (tune_get(PIS_TUNE_WINO_TILE) == 3 && C >= 64 && N >= 64);
+    return C >= 128 || N >= 128 || (tune_get(PIS_TUNE_WINO_TILE) >= 3 && C >= 64 && N >= 64);
   return C >= 256 && N >= 128;
 }
 

@@ -1201,6 +1201,197 @@ __global__ __launch_bounds__(256, OCC) void gemm_nt_x6_bk32_kernel(const float* 
     }
 }
 
+// ---- experiment: fp16x3 (hi/lo fp16 split, 3 products) in the bk32 structure --------------
+// Unscaled (operands must sit in fp16's normal range): pis_debug_gemm_nt variants 10-12 only,
+// to price the split against bf16x6 (2 planes per operand: 2/3 of the LDS, half the MFMAs).
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void split2h_x4(f32x4 v, u32x2& h, u32x2& l) {
+  _Float16 hh[4], ll[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    hh[k] = (_Float16)v[k];
+    ll[k] = (_Float16)(v[k] - (float)hh[k]);
+  }
+  h = u32x2{__builtin_bit_cast(unsigned, f16x2_t{hh[0], hh[1]}), __builtin_bit_cast(unsigned, f16x2_t{hh[2], hh[3]})};
+  l = u32x2{__builtin_bit_cast(unsigned, f16x2_t{ll[0], ll[1]}), __builtin_bit_cast(unsigned, f16x2_t{ll[2], ll[3]})};
+}
+
+// 2^(13 - e) for m in [2^e, 2^(e+1)): m * scale lands in [2^13, 2^14), 4x under fp16's largest
+// finite value; 1 for a zero (or NaN) tile, 2^127 for a tile below 2^-114
+__device__ __forceinline__ float h3_scale(float m) {
+  if (!(m > 0.f)) return 1.f;
+  const int eb = (int)(__float_as_uint(m) >> 23);  // m >= 0: the biased exponent
+  const int sb = 267 - eb;                           // 127 + 13 - (eb - 127)
+  return __uint_as_float((unsigned)(sb > 254 ? 254 : sb) << 23);
+}
+
+// max over the wave of v >= 0 (DPP row shifts + row broadcasts: VALU only, no LDS round trip),
+// returned uniform
+template <int CTRL, int RMASK>
+__device__ __forceinline__ float dpp_f(float x) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, RMASK, 0xf, true));
+}
+__device__ __forceinline__ float wave_max_nonneg(float v) {
+  v = fmaxf(v, dpp_f<0x111, 0xf>(v));  // row_shr:1
+  v = fmaxf(v, dpp_f<0x112, 0xf>(v));  // row_shr:2
+  v = fmaxf(v, dpp_f<0x114, 0xf>(v));  // row_shr:4
+  v = fmaxf(v, dpp_f<0x118, 0xf>(v));  // row_shr:8: lane 15 of each row holds the row's max
+  v = fmaxf(v, dpp_f<0x142, 0xa>(v));  // row_bcast:15
+  v = fmaxf(v, dpp_f<0x143, 0xc>(v));  // row_bcast:31: lane 63 holds the wave's max
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
+
+template <int BM, int BN, int OCC = 3, bool SC = true>
+__global__ __launch_bounds__(256, OCC) void gemm_nt_h3_bk32_kernel(const float* __restrict__ A,
+                                                                const float* __restrict__ Bm, float* __restrict__ Cm,
+                                                                int M, int N, int K, int64_t bsA, int64_t bsB,
+                                                                int64_t bsC) {
+  constexpr int BK = 32, KP = 32;
+  constexpr int TM = BM / 64, TN = BN / 64;
+  constexpr int AL = BM * 8 / 256, BL = BN * 8 / 256;
+  __shared__ __attribute__((aligned(16))) _Float16 sA[2][BM * KP];
+  __shared__ __attribute__((aligned(16))) _Float16 sB[2][BN * KP];
+  __shared__ float smax[2][4];
+  A += blockIdx.y * bsA;
+  Bm += blockIdx.y * bsB;
+  Cm += blockIdx.y * bsC;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave & 1, wn = wave >> 1, li = lane & 31, lh = lane >> 5;
+  const int ntn = N / BN;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int m0 = (bid / ntn) * BM, n0 = (bid % ntn) * BN;
+  const int q8 = (tid & 7) * 4;
+  const bool full = m0 + BM <= M && K % BK == 0;
+  f32x4 ra[AL], rb[BL];
+  auto gload = [&](int k0) {
+    const int k = k0 + q8;
+#pragma unroll
+    for (int i = 0; i < AL; ++i) {
+      const int m = m0 + (tid + i * 256) / 8;
+      ra[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (full || (m < M && k < K)) ra[i] = *reinterpret_cast<const f32x4*>(A + (size_t)m * K + k);
+    }
+#pragma unroll
+    for (int i = 0; i < BL; ++i) {
+      const int n = n0 + (tid + i * 256) / 8;
+      rb[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (full || k < K) rb[i] = *reinterpret_cast<const f32x4*>(Bm + (size_t)n * K + k);
+    }
+  };
+  // the staged K-step's tile maxima -> smax (before the barrier that frees the LDS planes)
+  auto stage_max = [&]() {
+    float ma = 0.f, mb = 0.f;
+#pragma unroll
+    for (int i = 0; i < AL; ++i)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) ma = fmaxf(ma, fabsf(ra[i][k]));
+#pragma unroll
+    for (int i = 0; i < BL; ++i)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) mb = fmaxf(mb, fabsf(rb[i][k]));
+    ma = wave_max_nonneg(ma);
+    mb = wave_max_nonneg(mb);
+    if (lane == 0) {
+      smax[0][wave] = ma;
+      smax[1][wave] = mb;
+    }
+  };
+  float sa = 1.f, sb = 1.f;  // the current K-step's operand scales (powers of two)
+  auto lstore = [&]() {
+    if (SC) {
+      sa = h3_scale(fmaxf(fmaxf(smax[0][0], smax[0][1]), fmaxf(smax[0][2], smax[0][3])));
+      sb = h3_scale(fmaxf(fmaxf(smax[1][0], smax[1][1]), fmaxf(smax[1][2], smax[1][3])));
+    }
+#pragma unroll
+    for (int i = 0; i < AL; ++i) {
+      u32x2 h, l;
+      split2h_x4(SC ? ra[i] * sa : ra[i], h, l);
+      const int row = (tid + i * 256) / 8, o = x6w8_off(row, q8 >> 3) + (q8 & 7);
+      *reinterpret_cast<u32x2*>(&sA[0][o]) = h;
+      *reinterpret_cast<u32x2*>(&sA[1][o]) = l;
+    }
+#pragma unroll
+    for (int i = 0; i < BL; ++i) {
+      u32x2 h, l;
+      split2h_x4(SC ? rb[i] * sb : rb[i], h, l);
+      const int row = (tid + i * 256) / 8, o = x6w8_off(row, q8 >> 3) + (q8 & 7);
+      *reinterpret_cast<u32x2*>(&sB[0][o]) = h;
+      *reinterpret_cast<u32x2*>(&sB[1][o]) = l;
+    }
+  };
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int b = 0; b < TN; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+  const int KT = (K + BK - 1) / BK;
+  gload(0);
+  if (SC) {
+    stage_max();
+    __syncthreads();
+  }
+  lstore();
+  float s_acc = sa * sb;  // acc is kept in units of the current K-step's product scale
+  if (KT > 1) gload(BK);
+  __syncthreads();
+  for (int kt = 0; kt < KT; ++kt) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      f16x8 af[2][TM], bf[2][TN];
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+#pragma unroll
+        for (int a = 0; a < TM; ++a)
+          af[p][a] = *reinterpret_cast<const f16x8*>(&sA[p][x6w8_off(wm * (BM / 2) + a * 32 + li, 2 * ks + lh)]);
+#pragma unroll
+        for (int b = 0; b < TN; ++b)
+          bf[p][b] = *reinterpret_cast<const f16x8*>(&sB[p][x6w8_off(wn * (BN / 2) + b * 32 + li, 2 * ks + lh)]);
+      }
+#pragma unroll
+      for (int a = 0; a < TM; ++a)
+#pragma unroll
+        for (int b = 0; b < TN; ++b) {
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[1][a], bf[0][b], acc[a][b], 0, 0, 0);
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[0][a], bf[1][b], acc[a][b], 0, 0, 0);
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[0][a], bf[0][b], acc[a][b], 0, 0, 0);
+        }
+    }
+    if (kt + 1 < KT) {
+      if (SC) stage_max();
+      __syncthreads();
+      lstore();
+      __syncthreads();
+      if (kt + 2 < KT) gload((kt + 2) * BK);
+      if (SC) {  // re-express the partial sums in the new K-step's units (exact: powers of two)
+        const float s_new = sa * sb;
+        if (s_new != s_acc) {
+          const float r = s_new / s_acc;
+#pragma unroll
+          for (int a = 0; a < TM; ++a)
+#pragma unroll
+            for (int b = 0; b < TN; ++b) acc[a][b] *= r;
+          s_acc = s_new;
+        }
+      }
+    }
+  }
+  const float inv = SC ? 1.f / s_acc : 1.f;
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int b = 0; b < TN; ++b) {
+      const int n = n0 + wn * (BN / 2) + b * 32 + li;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm * (BM / 2) + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        if (m < M) Cm[(size_t)m * N + n] = acc[a][b][r] * inv;
+      }
+    }
+}
+
 // ---- 8-wave, 256 x 128, two-stage pipelined bf16x6 NT GEMM --------------------------------
 // One block per CU (8 waves = 2 per SIMD, wave tile 64 x 64 = 2 x 2 v_mfma_f32_32x32x16_bf16).
 // Per K-step of 32: step k is computed from one of two LDS plane buffers, then step k+1's fp32
@@ -1595,7 +1786,7 @@ static void launch_wino4_filter(const IGemmArgs& a, int N, int C, float* U, int 
 // 1.30 -> 1.13 ms; with 128 input or output channels (dec1.conv0, enc2.conv0) it is 2-8 % slower
 // than the separate GEMM + output transform, so those keep the 3-pass pipeline.
 static bool wino_gemm_out_wanted(int m, int64_t T, int C, int N) {
-  return m == 4 && tune_get(PIS_TUNE_WINO_GEMM_OUT) != 0 && tune_get(PIS_TUNE_WINO_TILE) == 3 && T % 32 == 0 &&
+  return m == 4 && tune_get(PIS_TUNE_WINO_GEMM_OUT) != 0 && tune_get(PIS_TUNE_WINO_TILE) >= 3 && T % 32 == 0 &&
          T >= 2 * (int64_t)C &&  // the filter planes fit in the M region
          N == 64 && C == 64;
 }
@@ -1708,7 +1899,19 @@ int launch_wino3x3(const IGemmArgs& a, int B, void* ws, hipStream_t s, float* ke
     hipLaunchKernelGGL((gemm_nt_kernel<128, 256>), grid, dim3(256), 0, s, V, U, Mt, (int)T, N, C, T * C,
                        (int64_t)N * C, T * N);
     rc = launch_status("wino_gemm");
-  } else if (v == 3 && N % 128 == 0) {
+  } else if (v == 4 && N % 64 == 0 && C % 32 == 0) {
+    // fp16x3 with per-K-step power-of-two tile scales (gemm_nt_h3_bk32_kernel)
+    if (N % 128 == 0) {
+      const dim3 grid((int)cdiv(T, 128) * (N / 128), nxi);
+      hipLaunchKernelGGL((gemm_nt_h3_bk32_kernel<128, 128, 3>), grid, dim3(256), 0, s, V, U, Mt, (int)T, N, C,
+                         T * C, (int64_t)N * C, T * N);
+    } else {
+      const dim3 grid((int)cdiv(T, 128) * (N / 64), nxi);
+      hipLaunchKernelGGL((gemm_nt_h3_bk32_kernel<128, 64, 4>), grid, dim3(256), 0, s, V, U, Mt, (int)T, N, C,
+                         T * C, (int64_t)N * C, T * N);
+    }
+    rc = launch_status("wino_gemm");
+  } else if (v >= 3 && N % 128 == 0) {
     // K-step 32 single-buffer variant where C allows: 2-9 % faster (tools/bench_gemm.py)
     const dim3 grid((int)cdiv(T, 128) * (N / 128), nxi);
     if (C % 32 == 0)
@@ -1718,7 +1921,7 @@ int launch_wino3x3(const IGemmArgs& a, int B, void* ws, hipStream_t s, float* ke
       hipLaunchKernelGGL((gemm_nt_x6_kernel<128, 128>), grid, dim3(256), 0, s, V, U, Mt, (int)T, N, C, T * C,
                          (int64_t)N * C, T * N);
     rc = launch_status("wino_gemm");
-  } else if (v == 3 && N % 64 == 0) {
+  } else if (v >= 3 && N % 64 == 0) {
     const dim3 grid((int)cdiv(T, 128) * (N / 64), nxi);
     if (C % 32 == 0)
       hipLaunchKernelGGL((gemm_nt_x6_bk32_kernel<128, 64, 3>), grid, dim3(256), 0, s, V, U, Mt, (int)T, N, C,
@@ -1847,7 +2050,7 @@ int launch_wino_wgrad_out(const float* M, int N, int C, float* dw, int accumulat
 // waves per SIMD, 7 its 128x64. Requires N % 128 == 0 (64 for 4), K % 16 == 0.
 extern "C" int pis_debug_gemm_nt(const float* A, const float* B, float* C, int M, int N, int K, int batch,
                                  int variant, pis_stream_t stream) {
-  const int bn = variant == 4 || variant == 7 ? 64 : 128;
+  const int bn = variant == 4 || variant == 7 || variant == 12 ? 64 : 128;
   PIS_CHECK_ARG(A && B && C && M > 0 && N > 0 && K > 0 && batch > 0 && K % (variant >= 5 ? 32 : 16) == 0 &&
                     N % bn == 0,
                 "pis_debug_gemm_nt: bad arguments");
@@ -1872,6 +2075,9 @@ extern "C" int pis_debug_gemm_nt(const float* A, const float* B, float* C, int M
     case 5: hipLaunchKernelGGL((gemm_nt_x6_bk32_kernel<128, 128>), grid, dim3(256), 0, s, A, B, C, M, N, K, sa, sb, sc); break;
     case 6: hipLaunchKernelGGL((gemm_nt_x6_bk32_kernel<128, 128, 3>), grid, dim3(256), 0, s, A, B, C, M, N, K, sa, sb, sc); break;
     case 7: hipLaunchKernelGGL((gemm_nt_x6_bk32_kernel<128, 64, 3>), grid, dim3(256), 0, s, A, B, C, M, N, K, sa, sb, sc); break;
+    case 10: hipLaunchKernelGGL((gemm_nt_h3_bk32_kernel<128, 128, 3, false>), grid, dim3(256), 0, s, A, B, C, M, N, K, sa, sb, sc); break;
+    case 11: hipLaunchKernelGGL((gemm_nt_h3_bk32_kernel<128, 128, 3>), grid, dim3(256), 0, s, A, B, C, M, N, K, sa, sb, sc); break;
+    case 12: hipLaunchKernelGGL((gemm_nt_h3_bk32_kernel<128, 64, 4>), grid, dim3(256), 0, s, A, B, C, M, N, K, sa, sb, sc); break;
     default: set_error("pis_debug_gemm_nt: unknown variant %d", variant); return PIS_ERR_ARG;
   }
   return launch_status("debug_gemm_nt");

@@ -105,7 +105,7 @@ def test_conv3x3_dgrad_wgrad(hip, B, H, W, Cin, Cout):
 
 # every non-default kernel variant behind pis_tune (include/pis_capi.h) stays exact too
 TUNE_VARIANTS = [(4, 1), (4, 2), (4, 3), (5, 0), (6, 2048), (3, 0), (7, 1), (8, 0), (8, 2), (10, 0), (10, 1),
-                 (11, 0), (12, 0), (12, 2), (13, 0), (13, 2), (10, 2), (14, 0), (15, 0), (16, 0), (17, 4)]
+                 (11, 0), (12, 0), (12, 2), (13, 0), (13, 2), (10, 2), (10, 3), (14, 0), (15, 0), (16, 0), (17, 4)]
 
 
 @pytest.mark.parametrize("key,value", TUNE_VARIANTS)
@@ -152,7 +152,7 @@ def test_conv3x3_ex_winograd(hip, B, H, W, Cin, Cout, mode):
         nws = hip.pis_conv3x3_ex_ws(B, H, W, Cin, Cout)
         f4 = hip.pis_tune(11, -1) != 0 and H % 4 == 0 and W % 4 == 0
         if f4:  # F(4x4,3x3) policy
-            wino_fwd = wino_dgrad = max(Cin, Cout) >= 128 or (hip.pis_tune(10, -1) == 3 and min(Cin, Cout) >= 64)
+            wino_fwd = wino_dgrad = max(Cin, Cout) >= 128 or (hip.pis_tune(10, -1) >= 3 and min(Cin, Cout) >= 64)
         else:  # F(2x2,3x3) policy
             wino_fwd = Cin >= 256 and Cout >= 128
             wino_dgrad = Cout >= 256 and Cin >= 128
@@ -556,9 +556,11 @@ def test_conv3x3_winograd_fused(hip, B, H, W, Cin, Cout):
 @pytest.mark.parametrize("Cin,Cout", [(256, 256), (512, 128), (128, 64)])
 def test_winograd_gemm_bf16x6_is_fp32_accurate(hip, Cin, Cout):
     """The bf16x6 Winograd GEMM (pis_tune(10, 3): each fp32 operand split exactly into three
-    bf16, the six partial products above 2^-24 on bf16 MFMA, fp32 accumulation) must be as
-    accurate as the native fp32 MFMA GEMM (pis_tune(10, 2)): same conv against a float64
-    reference, error no larger than fp32's (+25 % slack for rounding-order luck)."""
+    bf16, the six partial products above 2^-24 on bf16 MFMA, fp32 accumulation) and the fp16x3
+    one (pis_tune(10, 4): each K-step's operand tiles scaled by a power of two into fp16 range and
+    split into hi + lo fp16, three products on fp16 MFMA) must be as accurate as the native fp32
+    MFMA GEMM (pis_tune(10, 2)): same conv against a float64 reference, error no larger than
+    fp32's (+25 % slack for rounding-order luck)."""
     B, H, W = 2, 16, 32
     g = torch.Generator().manual_seed(31)
     x = F.relu(torch.randn(B, Cin, H, W, generator=g, dtype=torch.float64))
@@ -569,7 +571,7 @@ def test_winograd_gemm_bf16x6_is_fp32_accurate(hip, Cin, Cout):
     prev8 = hip.pis_tune(8, 2)
     errs = {}
     try:
-        for v in (2, 3):
+        for v in (2, 3, 4):
             prev = hip.pis_tune(10, v)
             nws = hip.pis_conv3x3_ex_ws(B, H, W, Cin, Cout)
             ws = torch.empty(nws // 4 + 1, device="cuda")
@@ -581,8 +583,41 @@ def test_winograd_gemm_bf16x6_is_fp32_accurate(hip, Cin, Cout):
             errs[v] = ((nchw(y.cpu()).double() - ref).norm() / ref.norm()).item()
     finally:
         hip.pis_tune(8, prev8)
-    assert errs[3] <= 1.25 * errs[2] + 1e-9, errs
-    assert errs[3] < 5e-6, errs
+    for v in (3, 4):
+        assert errs[v] <= 1.25 * errs[2] + 1e-9, errs
+        assert errs[v] < 5e-6, errs
+
+
+def test_winograd_gemm_fp16x3_scales_any_magnitude(hip):
+    """fp16x3's per-K-step power-of-two scales keep gradient-sized (1e-12) and large (1e6)
+    operands exactly as accurate as unit ones (the scales are powers of two: the same fp16
+    digits, no underflow or overflow), and every one as accurate as the native fp32 MFMA GEMM."""
+    B, H, W, Cin, Cout = 2, 16, 32, 256, 128
+    g = torch.Generator().manual_seed(32)
+    x0 = torch.randn(B, Cin, H, W, generator=g, dtype=torch.float64)
+    w = torch.randn(Cout, Cin, 3, 3, generator=g, dtype=torch.float64) / (3 * Cin ** 0.5)
+    wd = krsc(w.float()).cuda()
+    prev8 = hip.pis_tune(8, 2)
+    errs = {}
+    try:
+        for v in (2, 4):
+            prev10 = hip.pis_tune(10, v)
+            for scale in (1.0, 1e-12, 1e-6, 1e6):
+                x = x0 * scale
+                ref = F.conv2d(x, w, padding=1)
+                nws = hip.pis_conv3x3_ex_ws(B, H, W, Cin, Cout)
+                ws = torch.empty(nws // 4 + 1, device="cuda")
+                y = torch.empty(B, H, W, Cout, device="cuda")
+                assert hip.pis_conv3x3_fwd_ex(nhwc(x.float()).cuda().data_ptr(), Cin, wd.data_ptr(), 0, 0,
+                                              y.data_ptr(), Cout, B, H, W, Cin, Cout, 0, ws.data_ptr(), nws, s()) == 0
+                torch.cuda.synchronize()
+                errs[v, scale] = ((nchw(y.cpu()).double() - ref).norm() / ref.norm()).item()
+            hip.pis_tune(10, prev10)
+    finally:
+        hip.pis_tune(8, prev8)
+    for scale in (1e-12, 1e-6, 1e6):
+        assert errs[4, scale] <= 1.05 * errs[4, 1.0] + 1e-9, errs
+        assert errs[4, scale] <= 1.25 * errs[2, scale] + 1e-9, errs
 
 
 @pytest.mark.parametrize("Cin,Cout", [(256, 256), (512, 128), (64, 128), (128, 64)])

@@ -236,7 +236,7 @@ def test_train_epoch_keys_and_validate(hip):
 
 def test_full_size_forward_and_loss_c2_shape(hip):
     """BASELINE config C2's image size (512 x 512) through the whole HIP forward (Winograd
-    F(4x4) with bf16x6 GEMMs on every >= 64-channel conv, the fused contraction + output
+    F(4x4) with fp16x3 GEMMs on every >= 64-channel conv, the bf16x6 fused contraction + output
     transform at 64 -> 64, max-pool in the encoder epilogues) and the fused Stage-II
     loss, against the fp32 oracle on the CPU: logits/probabilities and every loss term within
     the north-star 1e-4 relative tolerance. One image keeps the CPU side to a few seconds."""

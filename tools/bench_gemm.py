@@ -29,14 +29,26 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--check", action="store_true", help="compare variant outputs with torch fp64")
+    ap.add_argument("--dist", default="randn",
+                    help="operand values: randn | tiny (A x 1e-9, B x 1e-3: gradient-like) | "
+                         "wide (A rows x 10^U(-5,0), B x 1e4)")
+    ap.add_argument("--shapes", default="", help="comma-separated shape names (default: all)")
     args = ap.parse_args()
     lib = _hip.lib()
     s = torch.cuda.current_stream().cuda_stream
     variants = [int(v) for v in args.variants.split(",")]
     for name, H, C, N in SHAPES:
+        if args.shapes and name not in args.shapes.split(","):
+            continue
         T = 8 * H * H // 16
         A = torch.randn(36, T, C, device="cuda")
         Bm = torch.randn(36, N, C, device="cuda")
+        if args.dist == "tiny":
+            A *= 1e-9
+            Bm *= 1e-3
+        elif args.dist == "wide":
+            A *= 10.0 ** (-5 * torch.rand(36, T, 1, device="cuda"))
+            Bm *= 1e4
         Cm = torch.empty(36, T, N, device="cuda")
         bptr = {}
         flop = 2.0 * 36 * T * N * C

@@ -37,5 +37,5 @@ step rocprof_stats 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --
 step pmc_fetch 120 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline
 step pmc_write 120 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline
 step pmc_mfma 120 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_BF16 SQ_INSTS_VALU_MFMA_MOPS_F32 GRBM_GUI_ACTIVE -d "$OUT/pmc_mfma" -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline
-python3 tools/pmc_summary.py "$OUT/pmc.json" gemm_nt_x6_ $(find "$OUT"/pmc_fetch "$OUT"/pmc_write "$OUT"/pmc_mfma -name '*counter_collection.csv') > "$OUT/pmc_summary.txt" 2>&1
+python3 tools/pmc_summary.py "$OUT/pmc.json" gemm_nt_h3_ $(find "$OUT"/pmc_fetch "$OUT"/pmc_write "$OUT"/pmc_mfma -name '*counter_collection.csv') > "$OUT/pmc_summary.txt" 2>&1
 echo "== done"
