@@ -1201,20 +1201,20 @@ __global__ __launch_bounds__(256, OCC) void gemm_nt_x6_bk32_kernel(const float* 
     }
 }
 
-// ---- experiment: fp16x3 (hi/lo fp16 split, 3 products) in the bk32 structure --------------
-// Unscaled (operands must sit in fp16's normal range): pis_debug_gemm_nt variants 10-12 only,
-// to price the split against bf16x6 (2 planes per operand: 2/3 of the LDS, half the MFMAs).
+// ---- fp16x3: hi/lo fp16 split, 3 products, in the bk32 structure ---------------
+// 2 planes per operand (2/3 of bf16x6's LDS) and half its MFMAs; each K-step's tiles scaled by
+// a power of two into fp16 range (SC; the unscaled form is pis_debug_gemm_nt variant 10 only).
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x2_t __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ void split2h_x4(f32x4 v, u32x2& h, u32x2& l) {
-  _Float16 hh[4], ll[4];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    hh[k] = (_Float16)v[k];
-    ll[k] = (_Float16)(v[k] - (float)hh[k]);
-  }
-  h = u32x2{__builtin_bit_cast(unsigned, f16x2_t{hh[0], hh[1]}), __builtin_bit_cast(unsigned, f16x2_t{hh[2], hh[3]})};
-  l = u32x2{__builtin_bit_cast(unsigned, f16x2_t{ll[0], ll[1]}), __builtin_bit_cast(unsigned, f16x2_t{ll[2], ll[3]})};
+  // packed: v_cvt_pk_f16_f32 (hi), v_cvt_f32_f16 x2 + v_pk_add_f32 (residual), v_cvt_pk_f16_f32 (lo)
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  const f2 a = {v[0], v[1]}, b = {v[2], v[3]};
+  const f16x2_t ha = __builtin_convertvector(a, f16x2_t), hb = __builtin_convertvector(b, f16x2_t);
+  const f16x2_t la = __builtin_convertvector(a - __builtin_convertvector(ha, f2), f16x2_t);
+  const f16x2_t lb = __builtin_convertvector(b - __builtin_convertvector(hb, f2), f16x2_t);
+  h = u32x2{__builtin_bit_cast(unsigned, ha), __builtin_bit_cast(unsigned, hb)};
+  l = u32x2{__builtin_bit_cast(unsigned, la), __builtin_bit_cast(unsigned, lb)};
 }
 
 // 2^(13 - e) for m in [2^e, 2^(e+1)): m * scale lands in [2^13, 2^14), 4x under fp16's largest
@@ -1242,6 +1242,12 @@ __device__ __forceinline__ float wave_max_nonneg(float v) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
 }
 
+// Scales per WAVE and K-step: the 8 threads that stage one 32-k row of a tile belong to one wave
+// (row = tid / 8 + 32 i), so each wave scales the rows it stages by the power of two of its own
+// maximum (no block-wide exchange: no extra barrier), and publishes it in LDS with the planes.
+// In the 32 x 32 MFMA output a lane holds column n = li (B row staged by wave (li / 8) % 4) and
+// rows r -> (r & 3) + 8 (r >> 2) + 4 lh (A rows staged by wave r >> 2): accumulator register r
+// is in units sA[r >> 2] * sB[(li / 8) % 4], and is re-expressed when a K-step's scales differ.
 template <int BM, int BN, int OCC = 3, bool SC = true>
 __global__ __launch_bounds__(256, OCC) void gemm_nt_h3_bk32_kernel(const float* __restrict__ A,
                                                                 const float* __restrict__ Bm, float* __restrict__ Cm,
@@ -1250,9 +1256,10 @@ __global__ __launch_bounds__(256, OCC) void gemm_nt_h3_bk32_kernel(const float* 
   constexpr int BK = 32, KP = 32;
   constexpr int TM = BM / 64, TN = BN / 64;
   constexpr int AL = BM * 8 / 256, BL = BN * 8 / 256;
+  static_assert(BM % 128 == 0 && BN % 64 == 0, "row r's staging wave must be r / 8 % 4");
   __shared__ __attribute__((aligned(16))) _Float16 sA[2][BM * KP];
   __shared__ __attribute__((aligned(16))) _Float16 sB[2][BN * KP];
-  __shared__ float smax[2][4];
+  __shared__ __attribute__((aligned(16))) float sscale[2][4];  // [A|B][staging wave]
   A += blockIdx.y * bsA;
   Bm += blockIdx.y * bsB;
   Cm += blockIdx.y * bsC;
@@ -1279,29 +1286,30 @@ __global__ __launch_bounds__(256, OCC) void gemm_nt_h3_bk32_kernel(const float* 
       if (full || k < K) rb[i] = *reinterpret_cast<const f32x4*>(Bm + (size_t)n * K + k);
     }
   };
-  // the staged K-step's tile maxima -> smax (before the barrier that frees the LDS planes)
-  auto stage_max = [&]() {
-    float ma = 0.f, mb = 0.f;
-#pragma unroll
-    for (int i = 0; i < AL; ++i)
-#pragma unroll
-      for (int k = 0; k < 4; ++k) ma = fmaxf(ma, fabsf(ra[i][k]));
-#pragma unroll
-    for (int i = 0; i < BL; ++i)
-#pragma unroll
-      for (int k = 0; k < 4; ++k) mb = fmaxf(mb, fabsf(rb[i][k]));
-    ma = wave_max_nonneg(ma);
-    mb = wave_max_nonneg(mb);
-    if (lane == 0) {
-      smax[0][wave] = ma;
-      smax[1][wave] = mb;
-    }
+  // the wave's current scales: kept while its tile max stays in [2^7, 2^15) after scaling (fp16
+  // digits for everything above 2^-10 of the max, 2x headroom), so accumulators are rarely rescaled
+  float sa = 0.f, sb = 0.f;
+  auto keep_or_new = [](float cur, float m) {
+    const float v = m * cur;
+    return (v >= 128.f && v < 32768.f) ? cur : h3_scale(m);
   };
-  float sa = 1.f, sb = 1.f;  // the current K-step's operand scales (powers of two)
   auto lstore = [&]() {
     if (SC) {
-      sa = h3_scale(fmaxf(fmaxf(smax[0][0], smax[0][1]), fmaxf(smax[0][2], smax[0][3])));
-      sb = h3_scale(fmaxf(fmaxf(smax[1][0], smax[1][1]), fmaxf(smax[1][2], smax[1][3])));
+      float ma = 0.f, mb = 0.f;
+#pragma unroll
+      for (int i = 0; i < AL; ++i)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) ma = fmaxf(ma, fabsf(ra[i][k]));
+#pragma unroll
+      for (int i = 0; i < BL; ++i)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) mb = fmaxf(mb, fabsf(rb[i][k]));
+      sa = keep_or_new(sa, wave_max_nonneg(ma));
+      sb = keep_or_new(sb, wave_max_nonneg(mb));
+      if (lane == 0) {
+        sscale[0][wave] = sa;
+        sscale[1][wave] = sb;
+      }
     }
 #pragma unroll
     for (int i = 0; i < AL; ++i) {
@@ -1329,15 +1337,33 @@ __global__ __launch_bounds__(256, OCC) void gemm_nt_h3_bk32_kernel(const float* 
       for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
   const int KT = (K + BK - 1) / BK;
   gload(0);
-  if (SC) {
-    stage_max();
-    __syncthreads();
-  }
   lstore();
-  float s_acc = sa * sb;  // acc is kept in units of the current K-step's product scale
   if (KT > 1) gload(BK);
   __syncthreads();
+  f32x4 ua = {1.f, 1.f, 1.f, 1.f};  // units of the accumulators: A scale per row group r >> 2,
+  float ub = 1.f;                   // B scale of this lane's column
   for (int kt = 0; kt < KT; ++kt) {
+    if (SC) {  // this K-step's scales; re-express the partial sums in them (exact: powers of two)
+      const f32x4 na = *reinterpret_cast<const f32x4*>(&sscale[0][0]);
+      const float nb = sscale[1][(li >> 3) & 3];
+      if (kt == 0) {
+        ua = na;
+        ub = nb;
+      } else if (na[0] != ua[0] || na[1] != ua[1] || na[2] != ua[2] || na[3] != ua[3] || nb != ub) {
+        const float rb_ = nb / ub;
+        float f[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) f[q] = na[q] / ua[q] * rb_;
+#pragma unroll
+        for (int a = 0; a < TM; ++a)
+#pragma unroll
+          for (int b = 0; b < TN; ++b)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[a][b][r] *= f[r >> 2];
+        ua = na;
+        ub = nb;
+      }
+    }
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       f16x8 af[2][TM], bf[2][TN];
@@ -1360,25 +1386,15 @@ __global__ __launch_bounds__(256, OCC) void gemm_nt_h3_bk32_kernel(const float* 
         }
     }
     if (kt + 1 < KT) {
-      if (SC) stage_max();
       __syncthreads();
       lstore();
       __syncthreads();
       if (kt + 2 < KT) gload((kt + 2) * BK);
-      if (SC) {  // re-express the partial sums in the new K-step's units (exact: powers of two)
-        const float s_new = sa * sb;
-        if (s_new != s_acc) {
-          const float r = s_new / s_acc;
-#pragma unroll
-          for (int a = 0; a < TM; ++a)
-#pragma unroll
-            for (int b = 0; b < TN; ++b) acc[a][b] *= r;
-          s_acc = s_new;
-        }
-      }
     }
   }
-  const float inv = SC ? 1.f / s_acc : 1.f;
+  float inv[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) inv[q] = SC ? 1.f / (ua[q] * ub) : 1.f;
 #pragma unroll
   for (int a = 0; a < TM; ++a)
 #pragma unroll
@@ -1387,7 +1403,7 @@ __global__ __launch_bounds__(256, OCC) void gemm_nt_h3_bk32_kernel(const float* 
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int m = m0 + wm * (BM / 2) + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-        if (m < M) Cm[(size_t)m * N + n] = acc[a][b][r] * inv;
+        if (m < M) Cm[(size_t)m * N + n] = acc[a][b][r] * inv[r >> 2];
       }
     }
 }
