@@ -82,7 +82,8 @@ int pis_version(void);
                                     Cin, Cout % 16 == 0 — 1 (default) fp32-accurate bf16x6 on bf16 MFMA, 2 on fp32
                                     MFMA; 0 generic implicit GEMM */
 #define PIS_TUNE_WGRAD_X6 14     /* Winograd and transposed-conv weight-gradient GEMMs: 1 (default) fp32-accurate
-                                    bf16x6 on bf16 MFMA, 0 fp32 MFMA */
+                                    bf16x6 on bf16 MFMA, 2 fp16x3 (as key 10 = 4; measured -1 % on the step: the
+                                    512^2 layers are HBM-bound), 0 fp32 MFMA */
 #define PIS_TUNE_WINO_GEMM_OUT 15 /* F(4x4,3x3) 64 -> 64 channels: 1 (default) the 36 bf16x6 contractions fused with
                                      the output transform (M stays on chip; 4 groups of 32 tiles per block), 2 / 3 / 4
                                      the same with 1 / 2 / 8 groups per block (bitwise equal), 0 separate GEMM +

@@ -74,6 +74,54 @@ __device__ __forceinline__ void split3_x4(f32x4 v, u32x2& h, u32x2& m, u32x2& l)
   l = u32x2{l0, l1};
 }
 
+// ---- fp16x3: x = (hi + lo) / s with hi = fp16(x s), lo = fp16(x s - hi), s a power
+// of two per wave and K-step; the three products lo*hi, hi*lo, hi*hi on fp16 MFMA
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void split2h_x4(f32x4 v, u32x2& h, u32x2& l) {
+  // packed: v_cvt_pk_f16_f32 (hi), v_cvt_f32_f16 x2 + v_pk_add_f32 (residual), v_cvt_pk_f16_f32 (lo)
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  const f2 a = {v[0], v[1]}, b = {v[2], v[3]};
+  const f16x2_t ha = __builtin_convertvector(a, f16x2_t), hb = __builtin_convertvector(b, f16x2_t);
+  const f16x2_t la = __builtin_convertvector(a - __builtin_convertvector(ha, f2), f16x2_t);
+  const f16x2_t lb = __builtin_convertvector(b - __builtin_convertvector(hb, f2), f16x2_t);
+  h = u32x2{__builtin_bit_cast(unsigned, ha), __builtin_bit_cast(unsigned, hb)};
+  l = u32x2{__builtin_bit_cast(unsigned, la), __builtin_bit_cast(unsigned, lb)};
+}
+
+// 2^(13 - e) for m in [2^e, 2^(e+1)): m * scale lands in [2^13, 2^14), 4x under fp16's largest
+// finite value; 1 for a zero (or NaN) tile, 2^127 for a tile below 2^-114
+__device__ __forceinline__ float h3_scale(float m) {
+  if (!(m > 0.f)) return 1.f;
+  const int eb = (int)(__float_as_uint(m) >> 23);  // m >= 0: the biased exponent
+  const int sb = 267 - eb;                           // 127 + 13 - (eb - 127)
+  return __uint_as_float((unsigned)(sb > 254 ? 254 : sb) << 23);
+}
+
+// max over the wave of v >= 0 (DPP row shifts + row broadcasts: VALU only, no LDS round trip),
+// returned uniform
+// the scale for a tile of max m given the current scale: kept while m * cur stays in [2^7, 2^15)
+// (fp16 digits for everything above 2^-10 of the max, 2x headroom), so accumulators are rarely
+// rescaled; else re-chosen (h3_scale). cur = 0 always re-chooses.
+__device__ __forceinline__ float h3_keep(float cur, float m) {
+  const float v = m * cur;
+  return (v >= 128.f && v < 32768.f) ? cur : h3_scale(m);
+}
+
+template <int CTRL, int RMASK>
+__device__ __forceinline__ float dpp_f(float x) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, RMASK, 0xf, true));
+}
+__device__ __forceinline__ float wave_max_nonneg(float v) {
+  v = fmaxf(v, dpp_f<0x111, 0xf>(v));  // row_shr:1
+  v = fmaxf(v, dpp_f<0x112, 0xf>(v));  // row_shr:2
+  v = fmaxf(v, dpp_f<0x114, 0xf>(v));  // row_shr:4
+  v = fmaxf(v, dpp_f<0x118, 0xf>(v));  // row_shr:8: lane 15 of each row holds the row's max
+  v = fmaxf(v, dpp_f<0x142, 0xa>(v));  // row_bcast:15
+  v = fmaxf(v, dpp_f<0x143, 0xc>(v));  // row_bcast:31: lane 63 holds the wave's max
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
+
 // LDS element offset of (row, k) in a [row][16 k] bf16 plane: the two 16-B chunks of a row are
 // swapped on rows where bit 2 ^ bit 3 of the row is set, so the 16 rows a ds_read_b128 lane group
 // reads at one chunk hit 16 distinct slots of the 256-B bank row, and 8 consecutive rows written

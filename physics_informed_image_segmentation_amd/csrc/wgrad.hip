@@ -715,12 +715,202 @@ __global__ __launch_bounds__(256, 2) void wgrad_x6_kernel(WgradArgs g) {
   }
 }
 
+// The same contraction in fp16x3 (common.h): hi/lo fp16 planes, three fp16 MFMA
+// products, per-wave per-K-step power-of-two scales. The TPR = 16 / E threads that stage one
+// row's 16 pixels of a K-step are consecutive lanes of ONE wave (row = tid / TPR), so a row is
+// scaled uniformly; row m of the tile was staged by wave m / (64 / TPR). Accumulator register r
+// of block (a, b) is in units sA[wave of its row] * sB[wave of its column].
+template <int BM, int BN>
+__global__ __launch_bounds__(256, 2) void wgrad_h3_kernel(WgradArgs g) {
+  if (blockIdx.y) {
+    g.a += blockIdx.y * g.bs_a;
+    g.b += blockIdx.y * g.bs_b;
+    g.part += blockIdx.y * g.bs_part;
+  }
+  constexpr int BK = 16;
+  constexpr int TM = BM / 64, TN = BN / 64;
+  constexpr int EA = BM * BK / 256, EB = BN * BK / 256;  // pixels per thread per stage (8 or 4)
+  constexpr int TPA = BK / EA, TPB = BK / EB;            // threads per row
+  constexpr int RWA = 64 / TPA, RWB = 64 / TPB;          // rows staged per wave
+  __shared__ __attribute__((aligned(16))) _Float16 sA[2][2][BM * BK];  // [buf][hi|lo][m][k]
+  __shared__ __attribute__((aligned(16))) _Float16 sB[2][2][BN * BK];
+  __shared__ __attribute__((aligned(16))) float sscale[2][2][4];      // [buf][A|B][staging wave]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave & 1, wn = wave >> 1, li = lane & 31, lh = lane >> 5;
+  const int ntm = g.Mp / BM, ntn = g.Np / BN;
+  const int tiles = ntm * ntn;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = bid / tiles;
+  const int tile = bid - split * tiles;
+  const int m0 = (tile / ntn) * BM, n0 = (tile % ntn) * BN;
+  const int p_begin = split * g.pix_per_split;
+  const int p_end = min(g.P, p_begin + g.pix_per_split);
+  const int am = tid / TPA, ap = (tid % TPA) * EA;
+  const int bn = tid / TPB, bp = (tid % TPB) * EB;
+  const bool do_bias = g.part_bias != nullptr && n0 == 0;
+  int a_dr = 0, a_ds = 0, a_c0 = m0;
+  if (g.a_up2) { const int ij = m0 / g.Ca; a_dr = ij >> 1; a_ds = ij & 1; a_c0 = m0 - ij * g.Ca; }
+  const int HW = g.H * g.W;
+  float ra[EA], rb[EB];
+  float bsum = 0.f;
+  auto gload = [&](int p0) {
+    size_t pix0 = p0 + ap;
+    int pstep = 1;
+    if (g.a_up2) {
+      const int p = p0 + ap;
+      const int bb = p / HW, rem = p - bb * HW, h = rem / g.W, w = rem - h * g.W;
+      pix0 = ((size_t)bb * 2 * g.H + 2 * h + a_dr) * (2 * g.W) + 2 * w + a_ds;
+      pstep = 2;
+    }
+#pragma unroll
+    for (int e = 0; e < EA; ++e) {
+      const int p = p0 + ap + e;
+      ra[e] = p < p_end ? g.a[(pix0 + (size_t)pstep * e) * g.lda + a_c0 + am] : 0.f;
+    }
+#pragma unroll
+    for (int e = 0; e < EB; ++e) {
+      const int p = p0 + bp + e;
+      rb[e] = p < p_end ? g.b[(size_t)p * g.ldb + n0 + bn] : 0.f;
+    }
+  };
+  float sa = 0.f, sb = 0.f;  // this wave's current scales (h3_keep)
+  auto store_row = [&](const float* v, int E, float sc, _Float16* hp, _Float16* lp) {
+    u32x2 h0, l0;
+    split2h_x4(f32x4{v[0], v[1], v[2], v[3]} * sc, h0, l0);
+    if (E == 8) {
+      u32x2 h1, l1;
+      split2h_x4(f32x4{v[4], v[5], v[6], v[7]} * sc, h1, l1);
+      *reinterpret_cast<u32x4*>(hp) = u32x4{h0[0], h0[1], h1[0], h1[1]};
+      *reinterpret_cast<u32x4*>(lp) = u32x4{l0[0], l0[1], l1[0], l1[1]};
+    } else {
+      *reinterpret_cast<u32x2*>(hp) = h0;
+      *reinterpret_cast<u32x2*>(lp) = l0;
+    }
+  };
+  auto lstore = [&](int buf) {
+    float ma = 0.f, mb = 0.f;
+#pragma unroll
+    for (int e = 0; e < EA; ++e) {
+      if (do_bias) bsum += ra[e];
+      ma = fmaxf(ma, fabsf(ra[e]));
+    }
+#pragma unroll
+    for (int e = 0; e < EB; ++e) mb = fmaxf(mb, fabsf(rb[e]));
+    sa = h3_keep(sa, wave_max_nonneg(ma));
+    sb = h3_keep(sb, wave_max_nonneg(mb));
+    if (lane == 0) {
+      sscale[buf][0][wave] = sa;
+      sscale[buf][1][wave] = sb;
+    }
+    store_row(ra, EA, sa, &sA[buf][0][wsw(am, ap)], &sA[buf][1][wsw(am, ap)]);
+    store_row(rb, EB, sb, &sB[buf][0][wsw(bn, bp)], &sB[buf][1][wsw(bn, bp)]);
+  };
+  // staging wave of this lane's accumulator rows (per a, r) and columns (per b)
+  auto wave_a = [&](int a, int r) { return (wm * (BM / 2) + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh) / RWA; };
+  auto wave_b = [&](int b) { return (wn * (BN / 2) + b * 32 + li) / RWB; };
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int b = 0; b < TN; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+  f32x4 ua = {1.f, 1.f, 1.f, 1.f}, ub = {1.f, 1.f, 1.f, 1.f};  // accumulator units per staging wave
+  const int nst = (p_end - p_begin + BK - 1) / BK;
+  if (nst > 0) {
+    gload(p_begin);
+    lstore(0);
+  }
+  __syncthreads();
+  for (int st = 0; st < nst; ++st) {
+    const int cur = st & 1;
+    if (st + 1 < nst) gload(p_begin + (st + 1) * BK);
+    {  // this K-step's scales; re-express the partial sums in them (exact: powers of two)
+      const f32x4 na = *reinterpret_cast<const f32x4*>(&sscale[cur][0][0]);
+      const f32x4 nb = *reinterpret_cast<const f32x4*>(&sscale[cur][1][0]);
+      if (st == 0) {
+        ua = na;
+        ub = nb;
+      } else if (na[0] != ua[0] || na[1] != ua[1] || na[2] != ua[2] || na[3] != ua[3] || nb[0] != ub[0] ||
+                 nb[1] != ub[1] || nb[2] != ub[2] || nb[3] != ub[3]) {
+        float fa[4], fb[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          fa[q] = na[q] / ua[q];
+          fb[q] = nb[q] / ub[q];
+        }
+#pragma unroll
+        for (int a = 0; a < TM; ++a)
+#pragma unroll
+          for (int b = 0; b < TN; ++b) {
+            const float f = fb[wave_b(b)];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[a][b][r] *= fa[wave_a(a, r)] * f;
+          }
+        ua = na;
+        ub = nb;
+      }
+    }
+    f16x8 af[2][TM], bf[2][TN];
+#pragma unroll
+    for (int pl = 0; pl < 2; ++pl) {
+#pragma unroll
+      for (int a = 0; a < TM; ++a)
+        af[pl][a] = *reinterpret_cast<const f16x8*>(&sA[cur][pl][wsw(wm * (BM / 2) + a * 32 + li, 8 * lh)]);
+#pragma unroll
+      for (int b = 0; b < TN; ++b)
+        bf[pl][b] = *reinterpret_cast<const f16x8*>(&sB[cur][pl][wsw(wn * (BN / 2) + b * 32 + li, 8 * lh)]);
+    }
+#pragma unroll
+    for (int a = 0; a < TM; ++a)
+#pragma unroll
+      for (int b = 0; b < TN; ++b) {
+        acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[1][a], bf[0][b], acc[a][b], 0, 0, 0);
+        acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[0][a], bf[1][b], acc[a][b], 0, 0, 0);
+        acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[0][a], bf[0][b], acc[a][b], 0, 0, 0);
+      }
+    if (st + 1 < nst) lstore(cur ^ 1);
+    __syncthreads();
+  }
+  float* out = g.part + (size_t)split * (g.split_stride ? g.split_stride : (int64_t)g.Mp * g.Np);
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int b = 0; b < TN; ++b) {
+      const int n = n0 + wn * (BN / 2) + b * 32 + li;
+      const float ib = 1.f / ub[wave_b(b)];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm * (BM / 2) + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        out[(size_t)m * g.Np + n] = acc[a][b][r] * (ib / ua[wave_a(a, r)]);
+      }
+    }
+  if (do_bias) {  // column sums of A: TPA partial sums per column (consecutive threads), fixed order
+    float* red = reinterpret_cast<float*>(&sA[0][0][0]);
+    red[tid] = bsum;
+    __syncthreads();
+    if (tid < BM) {
+      float t = 0.f;
+#pragma unroll
+      for (int q = 0; q < TPA; ++q) t += red[tid * TPA + q];
+      g.part_bias[(size_t)split * g.Mp + m0 + tid] = t;
+    }
+  }
+}
+
 static int run_wgrad(const WgradArgs& base, const WgradPlan& pl, hipStream_t s, int batches = 1) {
   WgradArgs a = base;
   a.pix_per_split = pl.pps;
   a.pair = tune_get(PIS_TUNE_WGRAD_PAIR);
   const int tiles = (a.Mp / pl.bm) * (a.Np / pl.bn);
   const dim3 grid(tiles * pl.splits, batches);
+  if (tune_get(PIS_TUNE_WGRAD_X6) == 2 && a.b_mode == B_PLAIN && pl.pps % 16 == 0 && (!a.a_up2 || a.W % 8 == 0)) {
+    if (pl.bm == 128 && pl.bn == 128) hipLaunchKernelGGL((wgrad_h3_kernel<128, 128>), grid, dim3(256), 0, s, a);
+    else if (pl.bm == 128) hipLaunchKernelGGL((wgrad_h3_kernel<128, 64>), grid, dim3(256), 0, s, a);
+    else if (pl.bn == 128) hipLaunchKernelGGL((wgrad_h3_kernel<64, 128>), grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((wgrad_h3_kernel<64, 64>), grid, dim3(256), 0, s, a);
+    return launch_status("wgrad_h3");
+  }
   if (tune_get(PIS_TUNE_WGRAD_X6) != 0 && a.b_mode == B_PLAIN && pl.pps % 16 == 0 && (!a.a_up2 || a.W % 8 == 0)) {
     if (pl.bm == 128 && pl.bn == 128) hipLaunchKernelGGL((wgrad_x6_kernel<128, 128>), grid, dim3(256), 0, s, a);
     else if (pl.bm == 128) hipLaunchKernelGGL((wgrad_x6_kernel<128, 64>), grid, dim3(256), 0, s, a);

@@ -1204,44 +1204,6 @@ __global__ __launch_bounds__(256, OCC) void gemm_nt_x6_bk32_kernel(const float* 
 // ---- fp16x3: hi/lo fp16 split, 3 products, in the bk32 structure ---------------
 // 2 planes per operand (2/3 of bf16x6's LDS) and half its MFMAs; each K-step's tiles scaled by
 // a power of two into fp16 range (SC; the unscaled form is pis_debug_gemm_nt variant 10 only).
-typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
-typedef _Float16 f16x2_t __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ void split2h_x4(f32x4 v, u32x2& h, u32x2& l) {
-  // packed: v_cvt_pk_f16_f32 (hi), v_cvt_f32_f16 x2 + v_pk_add_f32 (residual), v_cvt_pk_f16_f32 (lo)
-  typedef float f2 __attribute__((ext_vector_type(2)));
-  const f2 a = {v[0], v[1]}, b = {v[2], v[3]};
-  const f16x2_t ha = __builtin_convertvector(a, f16x2_t), hb = __builtin_convertvector(b, f16x2_t);
-  const f16x2_t la = __builtin_convertvector(a - __builtin_convertvector(ha, f2), f16x2_t);
-  const f16x2_t lb = __builtin_convertvector(b - __builtin_convertvector(hb, f2), f16x2_t);
-  h = u32x2{__builtin_bit_cast(unsigned, ha), __builtin_bit_cast(unsigned, hb)};
-  l = u32x2{__builtin_bit_cast(unsigned, la), __builtin_bit_cast(unsigned, lb)};
-}
-
-// 2^(13 - e) for m in [2^e, 2^(e+1)): m * scale lands in [2^13, 2^14), 4x under fp16's largest
-// finite value; 1 for a zero (or NaN) tile, 2^127 for a tile below 2^-114
-__device__ __forceinline__ float h3_scale(float m) {
-  if (!(m > 0.f)) return 1.f;
-  const int eb = (int)(__float_as_uint(m) >> 23);  // m >= 0: the biased exponent
-  const int sb = 267 - eb;                           // 127 + 13 - (eb - 127)
-  return __uint_as_float((unsigned)(sb > 254 ? 254 : sb) << 23);
-}
-
-// max over the wave of v >= 0 (DPP row shifts + row broadcasts: VALU only, no LDS round trip),
-// returned uniform
-template <int CTRL, int RMASK>
-__device__ __forceinline__ float dpp_f(float x) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, RMASK, 0xf, true));
-}
-__device__ __forceinline__ float wave_max_nonneg(float v) {
-  v = fmaxf(v, dpp_f<0x111, 0xf>(v));  // row_shr:1
-  v = fmaxf(v, dpp_f<0x112, 0xf>(v));  // row_shr:2
-  v = fmaxf(v, dpp_f<0x114, 0xf>(v));  // row_shr:4
-  v = fmaxf(v, dpp_f<0x118, 0xf>(v));  // row_shr:8: lane 15 of each row holds the row's max
-  v = fmaxf(v, dpp_f<0x142, 0xa>(v));  // row_bcast:15
-  v = fmaxf(v, dpp_f<0x143, 0xc>(v));  // row_bcast:31: lane 63 holds the wave's max
-  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
-}
-
 // Scales per WAVE and K-step: the 8 threads that stage one 32-k row of a tile belong to one wave
 // (row = tid / 8 + 32 i), so each wave scales the rows it stages by the power of two of its own
 // maximum (no block-wide exchange: no extra barrier), and publishes it in LDS with the planes.
@@ -1286,13 +1248,7 @@ __global__ __launch_bounds__(256, OCC) void gemm_nt_h3_bk32_kernel(const float* 
       if (full || k < K) rb[i] = *reinterpret_cast<const f32x4*>(Bm + (size_t)n * K + k);
     }
   };
-  // the wave's current scales: kept while its tile max stays in [2^7, 2^15) after scaling (fp16
-  // digits for everything above 2^-10 of the max, 2x headroom), so accumulators are rarely rescaled
-  float sa = 0.f, sb = 0.f;
-  auto keep_or_new = [](float cur, float m) {
-    const float v = m * cur;
-    return (v >= 128.f && v < 32768.f) ? cur : h3_scale(m);
-  };
+  float sa = 0.f, sb = 0.f;  // the wave's current scales (h3_keep)
   auto lstore = [&]() {
     if (SC) {
       float ma = 0.f, mb = 0.f;
@@ -1304,8 +1260,8 @@ __global__ __launch_bounds__(256, OCC) void gemm_nt_h3_bk32_kernel(const float* 
       for (int i = 0; i < BL; ++i)
 #pragma unroll
         for (int k = 0; k < 4; ++k) mb = fmaxf(mb, fabsf(rb[i][k]));
-      sa = keep_or_new(sa, wave_max_nonneg(ma));
-      sb = keep_or_new(sb, wave_max_nonneg(mb));
+      sa = h3_keep(sa, wave_max_nonneg(ma));
+      sb = h3_keep(sb, wave_max_nonneg(mb));
       if (lane == 0) {
         sscale[0][wave] = sa;
         sscale[1][wave] = sb;

@@ -105,7 +105,7 @@ def test_conv3x3_dgrad_wgrad(hip, B, H, W, Cin, Cout):
 
 # every non-default kernel variant behind pis_tune (include/pis_capi.h) stays exact too
 TUNE_VARIANTS = [(4, 1), (4, 2), (4, 3), (5, 0), (6, 2048), (3, 0), (7, 1), (8, 0), (8, 2), (10, 0), (10, 1),
-                 (11, 0), (12, 0), (12, 2), (13, 0), (13, 2), (10, 2), (10, 3), (14, 0), (15, 0), (16, 0), (17, 4)]
+                 (11, 0), (12, 0), (12, 2), (13, 0), (13, 2), (10, 2), (10, 3), (14, 0), (14, 2), (15, 0), (16, 0), (17, 4)]
 
 
 @pytest.mark.parametrize("key,value", TUNE_VARIANTS)
@@ -622,9 +622,9 @@ def test_winograd_gemm_fp16x3_scales_any_magnitude(hip):
 
 @pytest.mark.parametrize("Cin,Cout", [(256, 256), (512, 128), (64, 128), (128, 64)])
 def test_winograd_wgrad_bf16x6_is_fp32_accurate(hip, Cin, Cout):
-    """The bf16x6 weight-gradient GEMM (pis_tune(14, 1), default) against the fp32 MFMA one
-    (pis_tune(14, 0)): dW and db of the same conv against a float64 reference, error no larger
-    than fp32's (+25 % slack)."""
+    """The bf16x6 (pis_tune(14, 1)) and fp16x3 (pis_tune(14, 2)) weight-gradient GEMMs against
+    the fp32 MFMA one (pis_tune(14, 0)): dW and db of the same conv against a float64 reference,
+    error no larger than fp32's (+25 % slack); fp16x3 again with dz scaled to gradient size."""
     B, H, W = 2, 16, 32
     g = torch.Generator().manual_seed(37)
     x = F.relu(torch.randn(B, Cin, H, W, generator=g, dtype=torch.float64))
@@ -633,8 +633,10 @@ def test_winograd_wgrad_bf16x6_is_fp32_accurate(hip, Cin, Cout):
     db_ref = dz.sum(dim=(0, 2, 3))
     xd, dzd = nhwc(x.float()).cuda(), nhwc(dz.float()).cuda()
     errs = {}
-    for v in (0, 1):
-        prev = hip.pis_tune(14, v)
+    for v in (0, 1, 2, "2tiny"):
+        sc = 1e-9 if v == "2tiny" else 1.0
+        dzd = nhwc((dz * sc).float()).cuda()
+        prev = hip.pis_tune(14, 2 if v == "2tiny" else v)
         try:
             nws = hip.pis_conv3x3_wgrad_ws(B, H, W, Cin, Cout)
             ws = torch.empty(nws // 4 + 1, device="cuda")
@@ -646,11 +648,12 @@ def test_winograd_wgrad_bf16x6_is_fp32_accurate(hip, Cin, Cout):
             torch.cuda.synchronize()
         finally:
             hip.pis_tune(14, prev)
-        dwc = dw.cpu().permute(0, 3, 1, 2).double()
+        dwc = dw.cpu().permute(0, 3, 1, 2).double() / sc
         errs[v] = ((dwc - dw_ref).norm() / dw_ref.norm()).item()
-        assert rel_err(db.cpu().double(), db_ref) < 1e-5
-    assert errs[1] <= 1.25 * errs[0] + 1e-9, errs
-    assert errs[1] < 5e-6, errs
+        assert rel_err(db.cpu().double() / sc, db_ref) < 1e-5
+    for v in (1, 2, "2tiny"):
+        assert errs[v] <= 1.25 * errs[0] + 1e-9, errs
+        assert errs[v] < 5e-6, errs
 
 
 @pytest.mark.parametrize("Cin,Cout", [(128, 64), (512, 256)])
@@ -670,7 +673,7 @@ def test_convt_bf16x6_is_fp32_accurate(hip, Cin, Cout):
     wc = torch.empty(Cin * 4 * Cout, device="cuda")
     assert hip.pis_convt2x2_prep(w_ijoc.data_ptr(), wc.data_ptr(), Cin, Cout, s()) == 0
     errs = {}
-    for name, (v13, v14) in {"x6": (1, 1), "f32": (2, 0)}.items():
+    for name, (v13, v14) in {"x6": (1, 1), "h3": (1, 2), "f32": (2, 0)}.items():
         p13, p14 = hip.pis_tune(13, v13), hip.pis_tune(14, v14)
         try:
             yd = torch.empty(B, 2 * H, 2 * W, Cout, device="cuda")
@@ -691,9 +694,10 @@ def test_convt_bf16x6_is_fp32_accurate(hip, Cin, Cout):
             hip.pis_tune(14, p14)
         errs[name] = [rel_err(nchw(yd.cpu()), y.detach()), rel_err(nchw(dx.cpu()), x.grad),
                       rel_err(dw.cpu().permute(3, 2, 0, 1), w.grad), rel_err(db.cpu(), b.grad)]
-    for e6, e32 in zip(errs["x6"], errs["f32"]):
-        assert e6 <= 1.25 * e32 + 1e-9, errs
-        assert e6 < 5e-6, errs
+    for v in ("x6", "h3"):
+        for e6, e32 in zip(errs[v], errs["f32"]):
+            assert e6 <= 1.25 * e32 + 1e-9, errs
+            assert e6 < 5e-6, errs
 
 
 @pytest.mark.parametrize("B,H,W", [(2, 32, 64), (1, 16, 128), (3, 32, 32)])
