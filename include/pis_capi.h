@@ -101,7 +101,10 @@ int pis_version(void);
                                     lane (2-way conflicted ds_write_b64), 1 lane pairs stage the two 8-B halves of one 16-B
                                     chunk (conflict-free; the two 128-B pixel rows per load cost more: enc1.conv1 -4 %, up1
                                     +9 %, step -0.4 %) */
-#define PIS_TUNE_NKEYS 22
+#define PIS_TUNE_WINO_GEMM_OUT_H3 22 /* the fused 64 -> 64 kernel (key 15): 1 fp16x3 (per-(tile, xi, K-step) power-of-two
+                                        scales, hi + lo fp16, 3 products; its filter planes, also those written by
+                                        pis_conv3x3_filter(s), switch format with it), 0 bf16x6 */
+#define PIS_TUNE_NKEYS 23
 #define PIS_DEBUG_NOLOAD (1 << 16)
 int pis_tune(int key, int value);
 /* Tooling (tools/bench_gemm.py): time one batched NT GEMM kernel variant in isolation,
@@ -182,7 +185,9 @@ int pis_conv3x3_wgrad_keep(const float* x, int ldx, const float* dz, int ldz, fl
  * on another stream, off the critical path). dgrad = 0: for the forward, w = KRSC [Cout][9][Cin];
  * dgrad = 1: for the input gradient, w = the ORIGINAL KRSC weights (rotated in place, as
  * PIS_W_UNFLIPPED). The output format is the one the call with these shapes will consume (fp32
- * U[36][N][C] for the batched GEMMs, bf16x6 planes for the fused 64->64 contraction).
+ * U[36][N][C] for the batched GEMMs; for the fused 64->64 contraction the fp16x3 hi / lo planes +
+ * one inverse scale per output channel, or with pis_tune(22, 0) the bf16x6 planes: the tune key
+ * must not change between this call and the conv call that consumes it).
  * pis_conv3x3_filter_bytes returns its size, 0 when that call would not take the F(4x4,3x3)
  * GEMM path (then PIS_FILTER_READY must not be used). Pass the result as the weight argument
  * with PIS_FILTER_READY (dgrad: with PIS_WINO_PREPARED | PIS_W_UNFLIPPED semantics kept). */

@@ -122,6 +122,27 @@ __device__ __forceinline__ float wave_max_nonneg(float v) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
 }
 
+// max of v >= 0 over each aligned group of 8 lanes, returned in every lane of the group (two quad
+// permutes + row_half_mirror)
+__device__ __forceinline__ float group8_max_nonneg(float v) {
+  v = fmaxf(v, dpp_f<0xB1, 0xf>(v));   // quad_perm [1,0,3,2]
+  v = fmaxf(v, dpp_f<0x4E, 0xf>(v));   // quad_perm [2,3,0,1]
+  v = fmaxf(v, dpp_f<0x141, 0xf>(v));  // row_half_mirror: the other quad of the 8
+  return v;
+}
+
+// the fp16x3 scale s = 2^(13 - e) for a group max m in [2^e, 2^(e+1)) (as h3_scale) and its exact
+// inverse; s is capped at 2^126 so that 1/s stays a normal float; s = inv = 1 for a zero / NaN max
+__device__ __forceinline__ void h2_scale_pair(float m, float& s, float& inv) {
+  // selects, not branches: this runs in fully unrolled loops where a divergent branch would cut
+  // the schedule into pieces
+  const bool ok = m > 0.f;
+  const int eb = (int)(__float_as_uint(m) >> 23) & 0xff;
+  const int sb = std::min(267 - eb, 253);
+  s = ok ? __uint_as_float((unsigned)sb << 23) : 1.f;
+  inv = ok ? __uint_as_float((unsigned)(254 - sb) << 23) : 1.f;
+}
+
 // LDS element offset of (row, k) in a [row][16 k] bf16 plane: the two 16-B chunks of a row are
 // swapped on rows where bit 2 ^ bit 3 of the row is set, so the 16 rows a ds_read_b128 lane group
 // reads at one chunk hit 16 distinct slots of the 256-B bank row, and 8 consecutive rows written

@@ -53,8 +53,11 @@ int launch_wino3x3(const IGemmArgs& a, int B, void* ws, hipStream_t s, float* ke
                    bool v_ready = false);
 float* wino_v_slot(void* ws, int C, int N);
 // one pass over dz: V (input-gradient input transform) and E + bias partials (weight gradient)
+// (tmax != NULL: also the per-tile max |V| the fused fp16x3 dgrad reads, at wino_tmax_slot)
 int launch_wino_dz2(const float* dz, int ldz, int B, int H, int W, int N, float* V, float* E, float* bpart,
-                    hipStream_t s);
+                    hipStream_t s, float* tmax = nullptr);
+float* wino_tmax_slot(void* ws, int B, int H, int W, int C, int N);
+bool wino_fused_h3_planned(int B, int H, int W, int C, int N);
 // does pis_conv3x3_dgrad_ex take F(4x4,3x3) Winograd for this layer with this workspace?
 bool dgrad_wino4_planned(int B, int H, int W, int Cin, int Cout, int ldz, size_t ws_bytes);
 // Winograd weight-gradient pieces for tile edge m (2: F(3x3,2x2), 4: F(3x3,4x4)), nxi = (m+2)^2:

@@ -1215,7 +1215,8 @@ extern "C" int pis_conv3x3_bwd_prep(const float* dz, int ldz, int B, int H, int 
   char* base = (char*)ws_wgrad;
   float* E = (float*)(base + wp.off_E);
   float* bpart = wp.fused_bias ? (float*)(base + wp.off_cs) : nullptr;
-  const int rc = launch_wino_dz2(dz, ldz, B, H, W, Cout, V, E, bpart, (hipStream_t)stream);
+  float* tmax = wino_fused_h3_planned(B, H, W, Cout, Cin) ? wino_tmax_slot(ws_dgrad, B, H, W, Cout, Cin) : nullptr;
+  const int rc = launch_wino_dz2(dz, ldz, B, H, W, Cout, V, E, bpart, (hipStream_t)stream, tmax);
   return rc ? rc : 1;
 }
 

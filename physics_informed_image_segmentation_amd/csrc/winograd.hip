@@ -397,6 +397,61 @@ __global__ __launch_bounds__(256) void wino4_filter_rot_kernel(const float* __re
   wino4_filter_rot_tile(w, N, C, U, transposed, Up, blockIdx.x);
 }
 
+// The fused kernel's fp16x3 filter planes (pis_tune key 22), C == 64: one wave per output channel
+// n, lane c. All 36 U[xi][n][c] of the channel share ONE power-of-two scale t_n (from their max
+// over xi and c): Uh[p][xi][n][c] = hi / lo fp16 of u t_n, then Us[n] = 1 / t_n after the planes.
+// dgrad: the input-gradient filter straight from the original KRSC weights [C][9][N] (rotated,
+// transposed; as wino4_filter_rot_tile), else w is [N][9][C] with row pitch ldw.
+__device__ __forceinline__ void wino4_filter_h2_wave(const float* __restrict__ w, int ldw, int N, int dgrad,
+                                                     __bf16* __restrict__ Up, int n) {
+  constexpr int C = 64;
+  const int c = threadIdx.x & 63;
+  float g[3][3];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+    g[t / 3][t % 3] = dgrad ? w[((size_t)c * 9 + 8 - t) * N + n] : w[(size_t)n * ldw + t * C + c];
+  float gg[6][3], u[36];
+#pragma unroll
+  for (int i = 0; i < 6; ++i)
+#pragma unroll
+    for (int s = 0; s < 3; ++s) {
+      gg[i][s] = 0.f;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) axpy_c(gg[i][s], w4_g(i, k), g[k][s]);
+    }
+  float m = 0.f;
+#pragma unroll
+  for (int i = 0; i < 6; ++i)
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+      float v = 0.f;
+#pragma unroll
+      for (int s = 0; s < 3; ++s) axpy_c(v, w4_g(j, s), gg[i][s]);
+      u[6 * i + j] = v;
+      m = fmaxf(m, fabsf(v));
+    }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off, 64));
+  float sc, inv;
+  h2_scale_pair(m, sc, inv);
+  _Float16* Uh = reinterpret_cast<_Float16*>(Up);
+  const size_t NC = (size_t)N * C;
+#pragma unroll
+  for (int xi = 0; xi < 36; ++xi) {
+    const float us = u[xi] * sc;
+    const _Float16 h = (_Float16)us;
+    const size_t o = xi * NC + (size_t)n * C + c;
+    Uh[o] = h;
+    Uh[36 * NC + o] = (_Float16)(us - (float)h);
+  }
+  if (c == 0) reinterpret_cast<float*>(Uh + 72 * NC)[n] = inv;
+}
+
+__global__ __launch_bounds__(256) void wino4_filter_h2_kernel(const float* __restrict__ w, int ldw, int N, int dgrad,
+                                                              __bf16* __restrict__ Up) {
+  wino4_filter_h2_wave(w, ldw, N, dgrad, Up, 4 * blockIdx.x + (threadIdx.x >> 6));
+}
+
 // Many layers' filter transforms in ONE launch (pis_conv3x3_filters): one layer's grid is a few
 // to a few hundred blocks, so each separate launch is latency-bound (13-47 us at C2); here every
 // job's blocks run side by side. Block b belongs to the job whose [start, start + blocks) holds it.
@@ -419,15 +474,17 @@ __global__ __launch_bounds__(256) void wino4_filter_batch_kernel(FilterBatch fb)
   const int lb = (int)blockIdx.x - fb.start[k];
   float* U = jb.planes ? nullptr : reinterpret_cast<float*>(jb.out);
   __bf16* Up = jb.planes ? reinterpret_cast<__bf16*>(jb.out) : nullptr;
-  if (jb.dgrad) wino4_filter_rot_tile(jb.w, jb.N, jb.C, U, 0, Up, lb);
+  if (jb.planes == 2) wino4_filter_h2_wave(jb.w, 9 * jb.C, jb.N, jb.dgrad, Up, 4 * lb + (threadIdx.x >> 6));
+  else if (jb.dgrad) wino4_filter_rot_tile(jb.w, jb.N, jb.C, U, 0, Up, lb);
   else wino4_filter_range(jb.w, 9 * jb.C, jb.N, jb.C, U, 0, Up, lb, jb.blocks);
 }
 
 // V[xi][t][c] = (BT d BT^T)[xi], d = the 6x6 input patch at rows 4ty-1.., cols 4tx-1.. (zero padded)
-template <int VW = 4>
-__device__ __forceinline__ void wino4_input_item(const float* __restrict__ x, int ldx, int H, int W, int C,
-                                                 float* __restrict__ V, int64_t TC, int64_t t, int b, int ty,
-                                                 int tx, int c) {
+// TM: also returns the max |V| over this item's 36 x VW values (the fused kernel's fp16x3 tile scale)
+template <int VW = 4, bool TM = false>
+__device__ __forceinline__ float wino4_input_item(const float* __restrict__ x, int ldx, int H, int W, int C,
+                                                  float* __restrict__ V, int64_t TC, int64_t t, int b, int ty,
+                                                  int tx, int c) {
   fvec<VW> v[6][6];
 #pragma unroll
   for (int i = 0; i < 6; ++i)
@@ -456,12 +513,27 @@ __device__ __forceinline__ void wino4_input_item(const float* __restrict__ x, in
 #pragma unroll
   for (int xi = 0; xi < 36; ++xi)
     *reinterpret_cast<fvec<VW>*>(V + (size_t)xi * TC + t * C + c) = v[xi / 6][xi % 6];
+  float m = 0.f;
+  if constexpr (TM)
+#pragma unroll
+    for (int xi = 0; xi < 36; ++xi)
+#pragma unroll
+      for (int q = 0; q < VW; ++q) m = fmaxf(m, fabsf(v[xi / 6][xi % 6][q]));
+  return m;
+}
+
+// tmax[t] = max over the tile's lanes (C / VW consecutive lanes, a power of two <= 64: every lane
+// of a tile takes the same grid-stride trip count)
+__device__ __forceinline__ void tile_max_store(float m, int lanes, int c, int64_t t, float* __restrict__ tmax) {
+  for (int off = lanes >> 1; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off, 64));
+  if (c == 0) tmax[t] = m;
 }
 
 // VW channels per thread (pis_tune key 17): 2 (default) = half the registers of 4 (float4 accesses)
-template <int VW>
+template <int VW, bool TM = false>
 __global__ __launch_bounds__(256) void wino4_input_kernel(const float* __restrict__ x, int ldx, int B, int H, int W,
-                                                          int C, float* __restrict__ V) {
+                                                          int C, float* __restrict__ V,
+                                                          float* __restrict__ tmax = nullptr) {
   const int c4n = C / VW, TW = W / 4, TH = H / 4;
   const int64_t T = (int64_t)B * TH * TW, TC = T * C;
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < T * c4n; e += (int64_t)gridDim.x * blockDim.x) {
@@ -469,7 +541,8 @@ __global__ __launch_bounds__(256) void wino4_input_kernel(const float* __restric
     int c, b, rem;
     tile_decode<VW>(e, c4n, TH * TW, t, c, b, rem);
     const int ty = rem / TW, tx = rem - ty * TW;
-    wino4_input_item<VW>(x, ldx, H, W, C, V, TC, t, b, ty, tx, c);
+    const float m = wino4_input_item<VW, TM>(x, ldx, H, W, C, V, TC, t, b, ty, tx, c);
+    if constexpr (TM) tile_max_store(m, c4n, c, t, tmax);
   }
 }
 
@@ -777,9 +850,10 @@ __global__ __launch_bounds__(256) void wino4_dz_kernel(const float* __restrict__
 // F(4x4,3x3) input transform of dz (as wino4_input_kernel) and E = the weight gradient's
 // F(3x3,4x4) transform + bias partials (as wino4_dz_kernel); the second half re-reads the tile's
 // 4x4 interior from cache instead of HBM. Same grid as wino4_dz_kernel (bpart layout).
+template <bool TM = false>
 __global__ __launch_bounds__(256) void wino4_dz2_kernel(const float* __restrict__ dz, int ldz, int B, int H, int W,
                                                         int N, float* __restrict__ V, float* __restrict__ E,
-                                                        float* __restrict__ bpart) {
+                                                        float* __restrict__ bpart, float* __restrict__ tmax = nullptr) {
   const int n4n = N / 4, TW = W / 4, TH = H / 4;
   const int64_t T = (int64_t)B * TH * TW, TN = T * N;
   f32x4 bsum = {0.f, 0.f, 0.f, 0.f};
@@ -788,7 +862,8 @@ __global__ __launch_bounds__(256) void wino4_dz2_kernel(const float* __restrict_
     int n, b, rem;
     tile_decode(e, n4n, TH * TW, t, n, b, rem);
     const int ty = rem / TW, tx = rem - ty * TW;
-    wino4_input_item(dz, ldz, H, W, N, V, TN, t, b, ty, tx, n);
+    const float m = wino4_input_item<4, TM>(dz, ldz, H, W, N, V, TN, t, b, ty, tx, n);
+    if constexpr (TM) tile_max_store(m, n4n, n, t, tmax);
     wino4_dz_item(dz, ldz, H, W, N, E, TN, t, b, ty, tx, n, bsum);
   }
   if (bpart) wino4_bias_partials(bsum, N, bpart);
@@ -1511,11 +1586,21 @@ constexpr size_t X6W8_SMEM = 2 * 3 * 384 * 32 * sizeof(__bf16);  // 147,456 B
 // epilogue (bias, ReLU, mask, keep-scale, accumulate).
 typedef __bf16 bf16x8g __attribute__((ext_vector_type(8)));
 
-template <int NWN, int NWT, int KC, int G = 1>
+// H3: fp16x3 instead (pis_tune key 22). Every V row (tile) is split into hi / lo fp16 of v * s_t
+// with ONE power of two s_t per tile for all 36 xi and 64 channels, from the tile's max |V| that
+// the V producer wrote (wino4_input_kernel / wino4_dz2_kernel `tmax`), and the filter planes carry
+// one scale t_n per output channel (wino4_filter_h2_*): M[xi] and therefore Y are in units
+// s_t t_n for every xi, so the products need no per-xi unscaling — the epilogue divides once.
+// Elements more than 2^16 below their tile's max keep an absolute error <= 2^-37 of that max,
+// far below the fp32 transform's own rounding (~2^-24 of the patch max). One chain of three fp16
+// products (lo hi, hi lo, hi hi) per K-step: two thirds of the LDS operand reads, half the MFMAs.
+template <int NWN, int NWT, int KC, int G = 1, bool H3 = false>
 __global__ __launch_bounds__(64 * NWN * NWT) void wino4_gemm_out_x6_kernel(const float* __restrict__ V,
                                                                           const __bf16* __restrict__ Up,
-                                                                          IGemmArgs g, int B) {
+                                                                          IGemmArgs g, int B,
+                                                                          const float* __restrict__ tmax = nullptr) {
   constexpr int NT = 64 * NWN * NWT, TB = 16 * NWT, NN = 16 * NWN, KP = KC;  // KP: LDS row pitch (bf16)
+  constexpr int P = H3 ? 2 : 3;  // operand planes
   // unpadded rows, 16-B chunks XOR-swizzled by (row / 2) % 8: every ds_read_b128 lane group (16
   // rows of one 16-row window, two adjacent chunks) hits 16 distinct slots of the 256-B bank row;
   // without the 8-element padding a block needs 72 KB of LDS, so two blocks share a CU
@@ -1523,17 +1608,19 @@ __global__ __launch_bounds__(64 * NWN * NWT) void wino4_gemm_out_x6_kernel(const
   auto sw = [](int row, int k) { return row * KP + ((((k >> 3) ^ ((row >> 1) & 7)) << 3) | (k & 7)); };
   constexpr int NV4 = TB * KC / 4, AL = (NV4 + NT - 1) / NT;  // float4 of V[xi] per thread
   constexpr bool VPART = NV4 % NT != 0;                         // (then NV4 < NT: some threads idle)
-  constexpr int NU8 = 3 * NN * KC / 8, UL = NU8 / NT;          // 16-B chunks of the U[xi] planes per thread
+  constexpr int NU8 = P * NN * KC / 8, UL = NU8 / NT;          // 16-B chunks of the U[xi] planes per thread
   static_assert((!VPART || NV4 < NT) && NU8 % NT == 0, "staging must tile the block");
   constexpr int RING = 6, KS = KC / 32;
   // LDS: the double-buffered operand planes, and (aliased) the epilogue's staging of all four
   // tile quarters of Y (139 KB: one block per CU either way, its registers allow no second)
   constexpr int QT = 4 * NWT, EP = NN + 4, EQ = QT * 16 * EP;  // tiles per quarter; row pitch, floats
-  constexpr int OPS_BYTES = 2 * 3 * (TB + NN) * KP * 2, EPI_BYTES = 4 * EQ * 4;
+  constexpr int OPS_BYTES = 2 * P * (TB + NN) * KP * 2, EPI_BYTES = 4 * EQ * 4;
+  constexpr int LDS_BYTES = OPS_BYTES > EPI_BYTES ? OPS_BYTES : EPI_BYTES;
   static_assert(QT * 4 * (NN / 4) == NT, "one epilogue item per thread and quarter");
-  __shared__ __attribute__((aligned(16))) char smem[OPS_BYTES > EPI_BYTES ? OPS_BYTES : EPI_BYTES];
-  auto sA = reinterpret_cast<__bf16(*)[3][TB * KP]>(smem);
-  auto sU = reinterpret_cast<__bf16(*)[3][NN * KP]>(smem + 2 * 3 * TB * KP * 2);
+  static_assert(!H3 || (AL == 1 && !VPART), "H3: one V row per thread (its tile scale in a register)");
+  __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
+  auto sA = reinterpret_cast<__bf16(*)[P][TB * KP]>(smem);
+  auto sU = reinterpret_cast<__bf16(*)[P][NN * KP]>(smem + 2 * P * TB * KP * 2);
   float* E = reinterpret_cast<float*>(smem);
   const int N = g.N, TW = g.W / 4, TH = g.H / 4;
   const int64_t T = (int64_t)B * TH * TW;
@@ -1553,36 +1640,43 @@ __global__ __launch_bounds__(64 * NWN * NWT) void wino4_gemm_out_x6_kernel(const
       if (!VPART || tid + i * NT < NV4) r[i] = *reinterpret_cast<const f32x4*>(vb + xi * TK + 4 * (tid + i * NT));
     }
   };
-  auto lstore = [&](int buf, const f32x4 (&r)[AL]) {
+  auto lstore = [&](int buf, const f32x4 (&r)[AL], float srow) {  // srow: H3 tile scale
 #pragma unroll
     for (int i = 0; i < AL; ++i) {
       const int idx = tid + i * NT;
       if (VPART && idx >= NV4) continue;
       const int row = idx / (KC / 4), c = 4 * (idx % (KC / 4));
+      if constexpr (H3) {
+        u32x2 h, l;
+        split2h_x4(r[i] * srow, h, l);
+        *reinterpret_cast<u32x2*>(&sA[buf][0][sw(row, c)]) = h;
+        *reinterpret_cast<u32x2*>(&sA[buf][1][sw(row, c)]) = l;
+        continue;
+      }
       u32x2 h, m, l;
       split3_x4(r[i], h, m, l);
       *reinterpret_cast<u32x2*>(&sA[buf][0][sw(row, c)]) = h;
       *reinterpret_cast<u32x2*>(&sA[buf][1][sw(row, c)]) = m;
-      *reinterpret_cast<u32x2*>(&sA[buf][2][sw(row, c)]) = l;
+      *reinterpret_cast<u32x2*>(&sA[buf][P - 1][sw(row, c)]) = l;
     }
   };
   u32x4 ur[2][UL];
   const __bf16* Ug = Up;  // laundered per group (below): keeps 36 x UL U addresses from being hoisted
-  auto uload = [&](int xi, u32x4 (&r)[UL]) {
+  auto uload = [&](int xi, int slot) {
 #pragma unroll
     for (int i = 0; i < UL; ++i) {
       const int c = tid + i * NT;  // (plane, channel, 8-k chunk), k fastest: contiguous per plane
       const int pl = c / (NN * KC / 8), rem = c % (NN * KC / 8);
-      r[i] = *reinterpret_cast<const u32x4*>(Ug + (pl * 36 + xi) * NK + 8 * rem);
+      ur[slot][i] = *reinterpret_cast<const u32x4*>(Ug + (pl * 36 + xi) * NK + 8 * rem);
     }
   };
-  auto ustore = [&](int buf, const u32x4 (&r)[UL]) {
+  auto ustore = [&](int buf, int slot) {
 #pragma unroll
     for (int i = 0; i < UL; ++i) {
       const int c = tid + i * NT;
       const int pl = c / (NN * KC / 8), rem = c % (NN * KC / 8);
       const int row = rem / (KC / 8), k = 8 * (rem % (KC / 8));
-      *reinterpret_cast<u32x4*>(&sU[buf][pl][sw(row, k)]) = r[i];
+      *reinterpret_cast<u32x4*>(&sU[buf][pl][sw(row, k)]) = ur[slot][i];
     }
   };
   // a group's first stages: V[0..RING) and U[0..2) in flight, V[0] / U[0] in LDS buffer 0
@@ -1590,17 +1684,26 @@ __global__ __launch_bounds__(64 * NWN * NWT) void wino4_gemm_out_x6_kernel(const
 #pragma unroll
     for (int j = 0; j < RING; ++j) gload(vb, j, vr[j]);
   };
-  auto first_stage = [&](const float* vb) {
-    uload(0, ur[0]);
-    uload(1, ur[1]);
-    lstore(0, vr[0]);
-    ustore(0, ur[0]);
+  auto first_stage = [&](const float* vb, float srow) {
+    uload(0, 0);
+    uload(1, 1);
+    lstore(0, vr[0], srow);
+    ustore(0, 0);
     gload(vb, RING, vr[0]);
-    uload(2, ur[0]);
+    uload(2, 0);
     __syncthreads();
   };
+  // H3: this thread's V row is tile t0 + tid / (KC / 4) of each group (AL == 1); its scale, and the
+  // inverse scale of this lane's output channel n (after the two filter planes)
+  auto tile_scale = [&](float m) {
+    float sc, inv;
+    h2_scale_pair(m, sc, inv);
+    return sc;
+  };
+  float srow = 1.f, tm_next = 0.f;
+  if constexpr (H3) srow = tile_scale(tmax[grp0 * TB + tid / (KC / 4)]);
   prime(V + grp0 * TB * KC);
-  first_stage(V + grp0 * TB * KC);
+  first_stage(V + grp0 * TB * KC, srow);
 #pragma unroll 1
   for (int gi = 0; gi < G; ++gi) {
     const int64_t t0 = (grp0 + gi) * TB;
@@ -1619,14 +1722,28 @@ __global__ __launch_bounds__(64 * NWN * NWT) void wino4_gemm_out_x6_kernel(const
       for (int b = 0; b < 6; ++b) {
         const int xi = 6 * a + b, cur = b & 1;
         f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+        if constexpr (H3) {
 #pragma unroll
-        for (int s = 0; s < KS; ++s) {
+          for (int s = 0; s < KS; ++s) {
+            const int k = 32 * s + 8 * lq;
+            const f16x8 a0 = *reinterpret_cast<const f16x8*>(&sA[cur][0][sw(16 * wt + lr, k)]);
+            const f16x8 a1 = *reinterpret_cast<const f16x8*>(&sA[cur][1][sw(16 * wt + lr, k)]);
+            const f16x8 b0 = *reinterpret_cast<const f16x8*>(&sU[cur][0][sw(n, k)]);
+            const f16x8 b1 = *reinterpret_cast<const f16x8*>(&sU[cur][1][sw(n, k)]);
+            // smallest partial products first
+            acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1, b0, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, b1, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, b0, acc, 0, 0, 0);
+          }
+        }
+#pragma unroll
+        for (int s = 0; s < (H3 ? 0 : KS); ++s) {
           const int k = 32 * s + 8 * lq;
           bf16x8g af[3], bf[3];
 #pragma unroll
           for (int p = 0; p < 3; ++p) {
-            af[p] = *reinterpret_cast<const bf16x8g*>(&sA[cur][p][sw(16 * wt + lr, k)]);
-            bf[p] = *reinterpret_cast<const bf16x8g*>(&sU[cur][p][sw(n, k)]);
+            af[p] = *reinterpret_cast<const bf16x8g*>(&sA[cur][p % P][sw(16 * wt + lr, k)]);
+            bf[p] = *reinterpret_cast<const bf16x8g*>(&sU[cur][p % P][sw(n, k)]);
           }
           // smallest partial products first
           acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[2], bf[0], acc, 0, 0, 0);
@@ -1641,11 +1758,11 @@ __global__ __launch_bounds__(64 * NWN * NWT) void wino4_gemm_out_x6_kernel(const
         // stage xi + 1 (V from its ring slot, U from the register pair), then refill both
         const int vslot = (b + 1) % RING;
         if (xi + 1 < 36) {
-          lstore(cur ^ 1, vr[vslot]);
-          ustore(cur ^ 1, ur[cur ^ 1]);
+          lstore(cur ^ 1, vr[vslot], srow);
+          ustore(cur ^ 1, cur ^ 1);
         }
         if (xi + 1 + RING < 36) gload(vb, xi + 1 + RING, vr[vslot]);
-        if (xi + 3 < 36) uload(xi + 3, ur[cur ^ 1]);
+        if (xi + 3 < 36) uload(xi + 3, cur ^ 1);
         __syncthreads();
       }
       // Y[i][j] += AT[i][a] R[j] (a is a runtime row index: coefficients selected from the table)
@@ -1665,7 +1782,23 @@ __global__ __launch_bounds__(64 * NWN * NWT) void wino4_gemm_out_x6_kernel(const
       for (int j = 0; j < 4; ++j) rr[j] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
     const bool more = gi + 1 < G;
-    if (more) prime(vb + TB * KC);
+    if (more) {
+      if constexpr (H3) tm_next = tmax[t0 + TB + tid / (KC / 4)];
+      prime(vb + TB * KC);
+    }
+    if constexpr (H3) {
+      // Y is in units s_t t_n: divide (exact powers of two, one factor at a time)
+      const float inv_t = reinterpret_cast<const float*>(Up + 2 * 36 * (int64_t)N * KC)[n];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        float sc, inv_s;
+        h2_scale_pair(tmax[t0 + 16 * wt + 4 * lq + q], sc, inv_s);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) y[i][j][q] = (y[i][j][q] * inv_s) * inv_t;
+      }
+    }
     // epilogue: the lanes' (channel n, tiles t0 + 16 wt + 4 lq + q) values of all four tile
     // quarters q go through LDS so that every thread finishes 4 consecutive channels of one 2x2
     // pixel quad per quarter with float4 accesses; its ReLU-mask loads for the four quads are
@@ -1718,7 +1851,10 @@ __global__ __launch_bounds__(64 * NWN * NWT) void wino4_gemm_out_x6_kernel(const
       if (g.pool) *reinterpret_cast<f32x4*>(g.pool + pp[q] * N + nn) = max4(o[0][0], o[0][1], o[1][0], o[1][1]);
     }
     __syncthreads();
-    if (more) first_stage(vb + TB * KC);
+    if (more) {
+      if constexpr (H3) srow = tile_scale(tm_next);
+      first_stage(vb + TB * KC, srow);
+    }
   }
 }
 
@@ -1734,24 +1870,41 @@ static void launch_wino4_output(const float* Mt, const IGemmArgs& a, int B, int6
 }
 
 // the F(4x4,3x3) input transform, 2 (default) or 4 channels per thread (pis_tune key 17)
+// tmax (C == 64 only): also the per-tile max |V| (the fused kernel's fp16x3 tile scales)
 static void launch_wino4_input(int64_t T, int C, hipStream_t s, const float* x, int ldx, int B, int H, int W, int,
-                               float* V) {
-  if (tune_get(PIS_TUNE_WINO_VW) != 4)
-    hipLaunchKernelGGL(wino4_input_kernel<2>, dim3(grid_of(T * (C / 2))), dim3(256), 0, s, x, ldx, B, H, W, C, V);
+                               float* V, float* tmax = nullptr) {
+  const bool vw2 = tune_get(PIS_TUNE_WINO_VW) != 4;
+  if (tmax && vw2)
+    hipLaunchKernelGGL((wino4_input_kernel<2, true>), dim3(grid_of(T * (C / 2))), dim3(256), 0, s, x, ldx, B, H, W, C,
+                       V, tmax);
+  else if (tmax)
+    hipLaunchKernelGGL((wino4_input_kernel<4, true>), dim3(grid_of(T * (C / 4))), dim3(256), 0, s, x, ldx, B, H, W, C,
+                       V, tmax);
+  else if (vw2)
+    hipLaunchKernelGGL(wino4_input_kernel<2>, dim3(grid_of(T * (C / 2))), dim3(256), 0, s, x, ldx, B, H, W, C, V,
+                       nullptr);
   else
-    hipLaunchKernelGGL(wino4_input_kernel<4>, dim3(grid_of(T * (C / 4))), dim3(256), 0, s, x, ldx, B, H, W, C, V);
+    hipLaunchKernelGGL(wino4_input_kernel<4>, dim3(grid_of(T * (C / 4))), dim3(256), 0, s, x, ldx, B, H, W, C, V,
+                       nullptr);
 }
 
 // the F(4x4,3x3) filter transform of a's weights (the tiled kernel for unflipped 32-aligned shapes)
+// (Up: the fused kernel's planes, bf16x6 or, with h2, fp16x3 + scales — C % 32 == 0)
 static void launch_wino4_filter(const IGemmArgs& a, int N, int C, float* U, int transposed, __bf16* Up,
-                                hipStream_t s) {
-  if (a.w_unflipped)  // N, C % 32 == 0 checked by launch_wino3x3
+                                hipStream_t s, bool h2 = false) {
+  if (h2)  // C == 64, N % 4 == 0 (the fused kernel's shapes)
+    hipLaunchKernelGGL(wino4_filter_h2_kernel, dim3(N / 4), dim3(256), 0, s, a.wt, a.ldw, N, a.w_unflipped ? 1 : 0,
+                       Up);
+  else if (a.w_unflipped)  // N, C % 32 == 0 checked by launch_wino3x3
     hipLaunchKernelGGL(wino4_filter_rot_kernel, dim3((N / 32) * (C / 32)), dim3(256), 0, s, a.wt, N, C, U,
                        transposed, Up);
   else
     hipLaunchKernelGGL(wino4_filter_kernel, dim3(grid_of((int64_t)N * C)), dim3(256), 0, s, a.wt, a.ldw, N, C, U,
                        transposed, Up);
 }
+
+// the fused 64 -> 64 kernel's arithmetic (pis_tune key 22): fp16x3 planes instead of bf16x6
+static bool wino_gemm_out_h3() { return tune_get(PIS_TUNE_WINO_GEMM_OUT_H3) != 0; }
 
 // fused path eligibility (pis_tune key 15): F(4x4), bf16x6 GEMMs, 64 -> 64 channels. Measured
 // (tools/bench_kernels.py --key 15, C2): enc1.conv1 forward 1.13 -> 0.98 ms, input gradient
@@ -1764,21 +1917,33 @@ static bool wino_gemm_out_wanted(int m, int64_t T, int C, int N) {
 }
 
 static int launch_wino_gemm_out(const float* V, const __bf16* Up, const IGemmArgs& a, int B, int64_t T,
-                                hipStream_t s) {
+                                hipStream_t s, const float* tmax) {
   // 8 waves: 32 tiles x 64 channels per block; G such groups per block where they divide
   // (pis_tune key 15: 1 -> G = 4, 2 -> 1, 3 -> 2, 4 -> 8: experiments)
   const int64_t groups = T / 32;
   const int mode = tune_get(PIS_TUNE_WINO_GEMM_OUT);
   const int G = mode == 2 ? 1 : mode == 3 ? 2 : mode == 4 ? 8 : 4;
   const dim3 blk(512);
-  if (G == 8 && groups % 8 == 0)
-    hipLaunchKernelGGL((wino4_gemm_out_x6_kernel<4, 2, 64, 8>), dim3((int)(groups / 8)), blk, 0, s, V, Up, a, B);
+  if (wino_gemm_out_h3()) {
+    if (G == 8 && groups % 8 == 0)
+      hipLaunchKernelGGL((wino4_gemm_out_x6_kernel<4, 2, 64, 8, true>), dim3((int)(groups / 8)), blk, 0, s, V, Up, a,
+                         B, tmax);
+    else if (G == 4 && groups % 4 == 0)
+      hipLaunchKernelGGL((wino4_gemm_out_x6_kernel<4, 2, 64, 4, true>), dim3((int)(groups / 4)), blk, 0, s, V, Up, a,
+                         B, tmax);
+    else if (G == 2 && groups % 2 == 0)
+      hipLaunchKernelGGL((wino4_gemm_out_x6_kernel<4, 2, 64, 2, true>), dim3((int)(groups / 2)), blk, 0, s, V, Up, a,
+                         B, tmax);
+    else
+      hipLaunchKernelGGL((wino4_gemm_out_x6_kernel<4, 2, 64, 1, true>), dim3((int)groups), blk, 0, s, V, Up, a, B, tmax);
+  } else if (G == 8 && groups % 8 == 0)
+    hipLaunchKernelGGL((wino4_gemm_out_x6_kernel<4, 2, 64, 8>), dim3((int)(groups / 8)), blk, 0, s, V, Up, a, B, nullptr);
   else if (G == 4 && groups % 4 == 0)
-    hipLaunchKernelGGL((wino4_gemm_out_x6_kernel<4, 2, 64, 4>), dim3((int)(groups / 4)), blk, 0, s, V, Up, a, B);
+    hipLaunchKernelGGL((wino4_gemm_out_x6_kernel<4, 2, 64, 4>), dim3((int)(groups / 4)), blk, 0, s, V, Up, a, B, nullptr);
   else if (G == 2 && groups % 2 == 0)
-    hipLaunchKernelGGL((wino4_gemm_out_x6_kernel<4, 2, 64, 2>), dim3((int)(groups / 2)), blk, 0, s, V, Up, a, B);
+    hipLaunchKernelGGL((wino4_gemm_out_x6_kernel<4, 2, 64, 2>), dim3((int)(groups / 2)), blk, 0, s, V, Up, a, B, nullptr);
   else
-    hipLaunchKernelGGL((wino4_gemm_out_x6_kernel<4, 2, 64, 1>), dim3((int)groups), blk, 0, s, V, Up, a, B);
+    hipLaunchKernelGGL((wino4_gemm_out_x6_kernel<4, 2, 64, 1>), dim3((int)groups), blk, 0, s, V, Up, a, B, nullptr);
   return launch_status("wino_gemm_out");
 }
 
@@ -1797,7 +1962,8 @@ float* wino_v_slot(void* ws, int C, int N) { return (float*)ws + (size_t)36 * N 
 size_t wino_ws_bytes(int B, int H, int W, int C, int N) {
   const int m = wino_tile(H, W), nxi = (m + 2) * (m + 2);
   const int64_t T = (int64_t)B * (H / m) * (W / m);
-  return (size_t)nxi * ((int64_t)N * C + T * C + T * N) * sizeof(float) + 1024;
+  // + T floats: the per-tile max |V| of the fused fp16x3 kernel (wino_tmax_slot)
+  return (size_t)(nxi * ((int64_t)N * C + T * C + T * N) + T) * sizeof(float) + 1024;
 }
 
 // fused F(4x4,3x3) (pis_tune key 12: 0 off, 1 auto, 2 whenever the shape allows)
@@ -1836,14 +2002,15 @@ int launch_wino3x3(const IGemmArgs& a, int B, void* ws, hipStream_t s, float* ke
     // the pre-split filter planes (1.5x U's bytes) go where M would have been
     __bf16* Up = reinterpret_cast<__bf16*>(Mt);
     if (a.filter_ready) Up = const_cast<__bf16*>(reinterpret_cast<const __bf16*>(a.wt));
-    else launch_wino4_filter(a, N, C, U, 0, Up, s);
+    else launch_wino4_filter(a, N, C, U, 0, Up, s, wino_gemm_out_h3());
+    float* tmax = wino_gemm_out_h3() ? wino_tmax_slot(ws, B, a.H, a.W, C, N) : nullptr;
     if (!v_ready)
       launch_wino4_input(T, C, s, a.src, a.lds, B, a.H, a.W,
-                         C, V);
+                         C, V, tmax);
     int rc = launch_status("wino_transforms");
     if (rc) return rc;
     launch_hook("wino_gemm_out", 0, s, flop);
-    rc = launch_wino_gemm_out(V, Up, a, B, T, s);
+    rc = launch_wino_gemm_out(V, Up, a, B, T, s, tmax);
     launch_hook("wino_gemm_out", 1, s, flop);
     gemm_done(s);
     return rc;
@@ -1946,7 +2113,9 @@ int launch_wino4_filter_only(const float* w, int C, int N, int dgrad, int format
   a.wt = w; a.ldw = 9 * C; a.w_unflipped = dgrad;
   if (dgrad && (N % 32 || C % 32)) return set_error("pis_conv3x3_filter: the input-gradient transform needs "
                                                     "32-aligned channels"), PIS_ERR_ARG;
-  if (format == 2) launch_wino4_filter(a, N, C, nullptr, 0, reinterpret_cast<__bf16*>(out), s);
+  if (format == 2 && wino_gemm_out_h3() && (C != 64 || N % 4))
+    return set_error("pis_conv3x3_filter: fp16x3 planes need 64 contraction channels"), PIS_ERR_ARG;
+  if (format == 2) launch_wino4_filter(a, N, C, nullptr, 0, reinterpret_cast<__bf16*>(out), s, wino_gemm_out_h3());
   else launch_wino4_filter(a, N, C, reinterpret_cast<float*>(out), 0, nullptr, s);
   return launch_status("wino_filter");
 }
@@ -1962,8 +2131,11 @@ int launch_wino4_filter_batch(int n, const float* const* w, void* const* out, co
   for (int k = 0; k < n; ++k) {
     if (dgrad[k] && (N[k] % 32 || C[k] % 32))
       return set_error("pis_conv3x3_filters: an input-gradient transform needs 32-aligned channels"), PIS_ERR_ARG;
-    const int blocks = dgrad[k] ? (N[k] / 32) * (C[k] / 32) : grid_of((int64_t)N[k] * C[k]);
-    fb.j[k] = FilterJobDev{w[k], out[k], N[k], C[k], dgrad[k], format[k] == 2 ? 1 : 0, blocks};
+    const int planes = format[k] == 2 ? (wino_gemm_out_h3() ? 2 : 1) : 0;
+    if (planes == 2 && (C[k] != 64 || N[k] % 4))
+      return set_error("pis_conv3x3_filters: fp16x3 planes need 64 contraction channels"), PIS_ERR_ARG;
+    const int blocks = planes == 2 ? N[k] / 4 : dgrad[k] ? (N[k] / 32) * (C[k] / 32) : grid_of((int64_t)N[k] * C[k]);
+    fb.j[k] = FilterJobDev{w[k], out[k], N[k], C[k], dgrad[k], planes, blocks};
     fb.start[k] = total;
     total += blocks;
   }
@@ -1996,10 +2168,28 @@ int launch_wino_dz(const float* dz, int ldz, int B, int H, int W, int N, float* 
 }
 
 int launch_wino_dz2(const float* dz, int ldz, int B, int H, int W, int N, float* V, float* E, float* bpart,
-                    hipStream_t s) {
+                    hipStream_t s, float* tmax) {
   const int64_t T = (int64_t)B * (H / 4) * (W / 4);
-  hipLaunchKernelGGL(wino4_dz2_kernel, dim3(grid_of(T * (N / 4))), dim3(256), 0, s, dz, ldz, B, H, W, N, V, E, bpart);
+  if (tmax)
+    hipLaunchKernelGGL((wino4_dz2_kernel<true>), dim3(grid_of(T * (N / 4))), dim3(256), 0, s, dz, ldz, B, H, W, N, V,
+                       E, bpart, tmax);
+  else
+    hipLaunchKernelGGL((wino4_dz2_kernel<false>), dim3(grid_of(T * (N / 4))), dim3(256), 0, s, dz, ldz, B, H, W, N, V,
+                       E, bpart, nullptr);
   return launch_status("wino_dz2");
+}
+
+// where the fused fp16x3 kernel finds the per-tile max |V| of its V (after the M region)
+float* wino_tmax_slot(void* ws, int B, int H, int W, int C, int N) {
+  const int64_t T = (int64_t)B * (H / 4) * (W / 4);
+  return (float*)ws + (size_t)36 * ((int64_t)N * C + T * C + T * N);
+}
+
+// the dgrad of these shapes (C contraction = Cout, N = Cin) runs the fused fp16x3 kernel: its V
+// producer (pis_conv3x3_bwd_prep) must leave the tile maxima at wino_tmax_slot
+bool wino_fused_h3_planned(int B, int H, int W, int C, int N) {
+  if (wino_tile(H, W) != 4 || !wino_gemm_out_h3()) return false;
+  return wino_gemm_out_wanted(4, (int64_t)B * (H / 4) * (W / 4), C, N);
 }
 
 int launch_wino_wgrad_out(const float* M, int N, int C, float* dw, int accumulate, hipStream_t s, int m,

@@ -105,7 +105,7 @@ def test_conv3x3_dgrad_wgrad(hip, B, H, W, Cin, Cout):
 
 # every non-default kernel variant behind pis_tune (include/pis_capi.h) stays exact too
 TUNE_VARIANTS = [(4, 1), (4, 2), (4, 3), (5, 0), (6, 2048), (3, 0), (7, 1), (8, 0), (8, 2), (10, 0), (10, 1),
-                 (11, 0), (12, 0), (12, 2), (13, 0), (13, 2), (10, 2), (10, 3), (14, 0), (14, 2), (15, 0), (16, 0), (17, 4)]
+                 (11, 0), (12, 0), (12, 2), (13, 0), (13, 2), (10, 2), (10, 3), (14, 0), (14, 2), (15, 0), (16, 0), (17, 4), (22, 0)]
 
 
 @pytest.mark.parametrize("key,value", TUNE_VARIANTS)
@@ -746,6 +746,55 @@ def test_fused_64_groups_per_block_bitwise(hip, B, H, W):
     assert rel_err(nchw(out[2][0]), y_ref) < 1e-6
     assert rel_err(nchw(out[2][1]), F.max_pool2d(y_ref, 2)) < 1e-6
     assert rel_err(nchw(out[2][2]) - 0.5, dx_ref) < 1e-6
+
+
+def test_fused_64_fp16x3_is_fp32_accurate(hip):
+    """The fused 64->64 kernel in fp16x3 (pis_tune(22, 1): per-tile and per-channel power-of-two
+    scales, hi + lo fp16, three fp16 products) against float64: forward and input gradient as
+    accurate (+25 % slack) as the same Winograd pipeline with the native fp32 MFMA GEMM, as the
+    bf16x6 fused kernel (22, 0) and as the 3-pass fp16x3 GEMM path (15, 0), for unit,
+    gradient-sized (1e-9, 1e-12) and large (1e6) operands, and with one region whose values span
+    2^-60 .. 1 (the tile scale's worst case)."""
+    B, H, W, C = 2, 32, 64, 64
+    g = torch.Generator().manual_seed(53)
+    x0 = F.relu(torch.randn(B, C, H, W, generator=g, dtype=torch.float64))
+    x0[0, :, :8, :8] *= torch.pow(2.0, -60 * torch.rand(C, 8, 8, generator=g, dtype=torch.float64))
+    w = torch.randn(C, C, 3, 3, generator=g, dtype=torch.float64) / (3 * C ** 0.5)
+    dz0 = torch.randn(B, C, H, W, generator=g, dtype=torch.float64)
+    wd = krsc(w.float()).cuda()
+    wf = torch.empty(C * 9 * C, device="cuda")
+    assert hip.pis_conv3x3_flip(wd.data_ptr(), wf.data_ptr(), C, C, s()) == 0
+    nws = hip.pis_conv3x3_ex_ws(B, H, W, C, C)
+    ws = torch.empty(nws // 4 + 1, device="cuda")
+    # f32: the same F(4x4,3x3) pipeline with the native fp32 MFMA GEMM (key 8 = 2 keeps Winograd;
+    # key 10 = 2 alone would route 64 -> 64 to the direct conv, whose error has no transforms in it)
+    variants = {"h3": ((22, 1),), "x6": ((22, 0),), "f32": ((8, 2), (15, 0), (10, 2)), "h3gemm": ((15, 0), (10, 4))}
+    errs = {}
+    for name, knobs in variants.items():
+        prev = [(k, hip.pis_tune(k, v)) for k, v in knobs]
+        try:
+            for sc in (1.0, 1e-12, 1e-9, 1e6):
+                x, dz = x0 * sc, dz0 * sc
+                y = torch.empty(B, H, W, C, device="cuda")
+                assert hip.pis_conv3x3_fwd_ex(nhwc(x.float()).cuda().data_ptr(), C, wd.data_ptr(), 0, 0,
+                                              y.data_ptr(), C, B, H, W, C, C, 0, ws.data_ptr(), nws, s()) == 0
+                dx = torch.empty(B, H, W, C, device="cuda")
+                assert hip.pis_conv3x3_dgrad_ex(nhwc(dz.float()).cuda().data_ptr(), C, wf.data_ptr(), 0, 0, 0,
+                                                dx.data_ptr(), C, B, H, W, C, C, 0, ws.data_ptr(), nws, s()) == 0
+                torch.cuda.synchronize()
+                y_ref = F.conv2d(x.float().double(), w.float().double(), padding=1)
+                dx_ref = torch.nn.grad.conv2d_input(x.shape, w.float().double(), dz.float().double(), padding=1)
+                errs[name, sc] = (((nchw(y.cpu()).double() - y_ref).norm() / y_ref.norm()).item(),
+                                  ((nchw(dx.cpu()).double() - dx_ref).norm() / dx_ref.norm()).item())
+        finally:
+            for k, v in prev:
+                hip.pis_tune(k, v)
+    for sc in (1.0, 1e-12, 1e-9, 1e6):
+        for i in range(2):
+            e = errs["h3", sc][i]
+            for ref in ("f32", "x6", "h3gemm"):
+                assert e <= 1.25 * errs[ref, sc][i] + 1e-9, (ref, errs)
+            assert e < 2e-6, errs
 
 
 @pytest.mark.parametrize("B,H,W,Cin,Cout", [(2, 32, 64, 64, 64), (2, 16, 32, 128, 128), (1, 32, 32, 128, 64),

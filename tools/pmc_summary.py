@@ -48,10 +48,13 @@ def derive(cs):
         out["kernel_cycles"] = cyc / XCDS
         if busy is not None:
             out["mfma_busy_frac"] = busy / (cyc / XCDS * SIMDS)
-    bf, f32 = g("SQ_INSTS_VALU_MFMA_MOPS_BF16"), g("SQ_INSTS_VALU_MFMA_MOPS_F32")
+    bf, f32, f16 = (g("SQ_INSTS_VALU_MFMA_MOPS_BF16"), g("SQ_INSTS_VALU_MFMA_MOPS_F32"),
+                    g("SQ_INSTS_VALU_MFMA_MOPS_F16"))
     if bf is not None:
         out["mfma_bf16_flop"] = bf * 512
-        exp = bf / 2 + (f32 or 0.0) * 512 / 64
+        if f16 is not None:
+            out["mfma_f16_flop"] = f16 * 512
+        exp = (bf + (f16 or 0.0)) / 2 + (f32 or 0.0) * 512 / 64
         out["busy_cycles_from_mops"] = exp
         if busy:
             out["busy_check_ratio"] = exp / busy
