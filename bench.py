@@ -81,6 +81,42 @@ def conv_flops_per_image(H: int, W: int, c: int = 64) -> float:
     return 2.0 * macs * 3 - 2.0 * first
 
 
+def wino_gemm_launches(H: int, W: int, B: int, c: int = 64):
+    """(T, C, N) of every batched Winograd GEMM launch ("wino_gemm") of one training step: the
+    forward and input gradient of each F(4x4,3x3) 3x3 conv (T = B H W / 16 tiles, contraction C,
+    N outputs), in no particular order — the 64 -> 64 convs run the fused contraction + output
+    transform kernel instead, and enc1.conv0 (Cin = 1) the VALU row kernels (csrc/winograd.hip
+    wino_gemm_out_wanted, csrc/igemm.hip wino_wanted_dims)."""
+    convs = []
+    for l in range(1, 5):
+        cl = c << (l - 1)
+        hl, wl = H >> (l - 1), W >> (l - 1)
+        if l > 1:
+            convs.append((hl, wl, cl // 2, cl))          # enc conv0
+        convs += [(hl, wl, cl, cl), (hl, wl, 2 * cl, cl), (hl, wl, cl, cl)]  # enc conv1, dec conv0, conv1
+    convs += [(H >> 4, W >> 4, 8 * c, 8 * c)] * 2        # bottleneck
+    out = []
+    for hl, wl, ci, co in convs:
+        if ci == co == 64:
+            continue
+        T = B * (hl // 4) * (wl // 4)
+        out += [(T, ci, co), (T, co, ci)]
+    return out
+
+
+def gemm_attainable(launches, pipe_peak_tflops: float, hbm_gbs: float = 8000.0):
+    """Per launch the roofline time max(FLOP / pipe peak, algorithmic bytes / HBM peak), the
+    algorithmic bytes being V read + U read + M written once (36 fp32 planes each). Returns
+    (FLOP, bytes, roofline seconds, FLOP-only seconds, bytes-only seconds), summed."""
+    fl = by = tmin = tf = tb = 0.0
+    for T, C, N in launches:
+        f, b = 2.0 * 36 * T * C * N, 4.0 * 36 * (T * C + N * C + T * N)
+        fl, by = fl + f, by + b
+        tf, tb = tf + f / (pipe_peak_tflops * 1e12), tb + b / (hbm_gbs * 1e9)
+        tmin += max(f / (pipe_peak_tflops * 1e12), b / (hbm_gbs * 1e9))
+    return fl, by, tmin, tf, tb
+
+
 # The dominant kernel of the step (profiles/r1_*_kernel_stats.csv): the batched fp32 MFMA GEMM
 # of the Winograd 3x3 convs (forward + input gradient), launched as "wino_gemm" by the C-ABI
 # (csrc/winograd.hip) and named gemm_nt_kernel<128, 128> / <128, 64> by rocprofv3.
@@ -434,6 +470,25 @@ def main():
     # gemm_nt_h3_bk32_kernel / gemm_nt_x6_bk32_kernel (K % 32 == 0, every C2 layer)
     kname = "gemm_nt_h3_" if h3 else "gemm_nt_x6_" if x6 else DOMINANT_KERNEL
     traffic, mfma_busy, busy_by_kernel = load_pmc(kname)
+    # the same launches against BOTH bounds (per launch max of FLOP / pipe peak and algorithmic
+    # bytes / 8 TB/s): only valid when the shape list reproduces the launches the hook timed
+    gl = wino_gemm_launches(H, W, B)
+    g_fl, g_by, g_tmin, g_tf, g_tb = gemm_attainable(gl, peak)
+    hbm_view = None
+    if len(gl) == n_launch and abs(g_fl / len(gl) - flop_per_launch) <= 1e-6 * flop_per_launch:
+        bpl = g_by / len(gl)
+        hbm_view = {
+            "bytes_per_launch": bpl, "unit": "GB/s", "peak": 8000.0,
+            "achieved": bpl / (ms_per_launch * 1e-3) / 1e9, "frac": bpl / (ms_per_launch * 1e-3) / 8e12,
+            "isolated_frac": bpl / (iso_ms * 1e-3) / 8e12,
+            "step_bytes_s": g_tb, "step_flop_s": g_tf,
+            "attainable_frac": g_tmin / (n_launch * ms_per_launch * 1e-3),
+            "attainable_frac_isolated": g_tmin / (n_launch * iso_ms * 1e-3),
+            "hbm_bound_launches": sum(1 for T, C, N in gl if 4.0 * 36 * (T * C + N * C + T * N) / 8e12 >
+                                      2.0 * 36 * T * C * N / (peak * 1e12)),
+            "note": "algorithmic bytes = V read + U read + M written once (4 B x 36 planes); attainable = "
+                    "sum over the step's launches of max(FLOP / pipe peak, bytes / 8 TB/s) / their measured "
+                    "time: the C2 GEMMs are mostly HBM-bound (the 36 fp32 M planes)"}
     loss_cold = loss_standalone(model.engine().u, t, loss_kw)
     if rank == 0:
         flops = conv_flops_per_image(H, W) * B
@@ -457,6 +512,7 @@ def main():
                          # rocprofv3 PMC (profiles/pmc_dominant.json): fraction of SIMD-cycles the
                          # matrix pipe was busy in this kernel, and in the step's other kernels
                          "mfma_busy_frac": mfma_busy, "mfma_busy_by_kernel": busy_by_kernel,
+                         "hbm_view": hbm_view,
                          "launches_per_step": n_launch, "avg_launch_ms": ms_per_launch,
                          "flop_per_launch": flop_per_launch,
                          "measured": "live over the timed steps; the input-gradient launches share the GPU "

@@ -81,8 +81,9 @@ int pis_version(void);
 #define PIS_TUNE_CONVT_GEMM 13   /* transposed conv fwd/dgrad: lean NT GEMM with gather/scatter addressing when
                                     Cin, Cout % 16 == 0 — 1 (default) fp32-accurate bf16x6 on bf16 MFMA, 2 on fp32
                                     MFMA; 0 generic implicit GEMM */
-#define PIS_TUNE_WGRAD_X6 14     /* Winograd and transposed-conv weight-gradient GEMMs: 1 (default) fp32-accurate
-                                    bf16x6 on bf16 MFMA, 2 fp16x3 (as key 10 = 4; measured -1 % on the step: the
+#define PIS_TUNE_WGRAD_X6 14     /* Winograd and transposed-conv weight-gradient GEMMs: 3 (default) fp16x3 where the
+                                    layer has >= 256 input channels, bf16x6 elsewhere; 1 fp32-accurate bf16x6 on
+                                    bf16 MFMA everywhere, 2 fp16x3 (as key 10 = 4) everywhere (-1 % on the step: the
                                     512^2 layers are HBM-bound), 0 fp32 MFMA */
 #define PIS_TUNE_WINO_GEMM_OUT 15 /* F(4x4,3x3) 64 -> 64 channels: 1 (default) the 36 bf16x6 contractions fused with
                                      the output transform (M stays on chip; 4 groups of 32 tiles per block), 2 / 3 / 4
@@ -104,7 +105,12 @@ int pis_version(void);
 #define PIS_TUNE_WINO_GEMM_OUT_H3 22 /* the fused 64 -> 64 kernel (key 15): 1 fp16x3 (per-(tile, xi, K-step) power-of-two
                                         scales, hi + lo fp16, 3 products; its filter planes, also those written by
                                         pis_conv3x3_filter(s), switch format with it), 0 bf16x6 */
-#define PIS_TUNE_NKEYS 23
+#define PIS_TUNE_WINO_H3_PRE 23  /* the batched fp16x3 Winograd GEMM (key 10 = 4) with C, N % 64 == 0: 0 (default)
+                                    per-wave, per-K-step scales inside the GEMM; 1 one power-of-two scale per A row
+                                    (tile) and per B row (output channel) for the whole contraction, from maxima the
+                                    input / dz / filter transforms write (no in-loop scales; measured slower: GEMM
+                                    +10 %, input transform +11 %, step -1.7 %, profiles/r2_q65_*, r2_q66_*) */
+#define PIS_TUNE_NKEYS 24
 #define PIS_DEBUG_NOLOAD (1 << 16)
 int pis_tune(int key, int value);
 /* Tooling (tools/bench_gemm.py): time one batched NT GEMM kernel variant in isolation,
@@ -185,7 +191,8 @@ int pis_conv3x3_wgrad_keep(const float* x, int ldx, const float* dz, int ldz, fl
  * on another stream, off the critical path). dgrad = 0: for the forward, w = KRSC [Cout][9][Cin];
  * dgrad = 1: for the input gradient, w = the ORIGINAL KRSC weights (rotated in place, as
  * PIS_W_UNFLIPPED). The output format is the one the call with these shapes will consume (fp32
- * U[36][N][C] for the batched GEMMs; for the fused 64->64 contraction the fp16x3 hi / lo planes +
+ * U[36][N][C] for the batched GEMMs (followed, with pis_tune(23, 1) and C, N % 64 == 0, by its
+ * per-(output, 32-channel chunk) maxima umax[N][C / 32]); for the fused 64->64 contraction the fp16x3 hi / lo planes +
  * one inverse scale per output channel, or with pis_tune(22, 0) the bf16x6 planes: the tune key
  * must not change between this call and the conv call that consumes it).
  * pis_conv3x3_filter_bytes returns its size, 0 when that call would not take the F(4x4,3x3)

@@ -904,14 +904,19 @@ static int run_wgrad(const WgradArgs& base, const WgradPlan& pl, hipStream_t s, 
   a.pair = tune_get(PIS_TUNE_WGRAD_PAIR);
   const int tiles = (a.Mp / pl.bm) * (a.Np / pl.bn);
   const dim3 grid(tiles * pl.splits, batches);
-  if (tune_get(PIS_TUNE_WGRAD_X6) == 2 && a.b_mode == B_PLAIN && pl.pps % 16 == 0 && (!a.a_up2 || a.W % 8 == 0)) {
+  // key 14 = 3 (auto): fp16x3 where the contraction's output has >= 256 columns (Cin): measured
+  // per layer (profiles/r2_q53_wgrad_fp16x3.txt) it wins on exactly those (-1..-10 %) and loses on
+  // the HBM-bound 64 / 128-channel layers (+1..+9 %)
+  const int x6 = tune_get(PIS_TUNE_WGRAD_X6);
+  if ((x6 == 2 || (x6 == 3 && a.Np >= 256)) && a.b_mode == B_PLAIN && pl.pps % 16 == 0 &&
+      (!a.a_up2 || a.W % 8 == 0)) {
     if (pl.bm == 128 && pl.bn == 128) hipLaunchKernelGGL((wgrad_h3_kernel<128, 128>), grid, dim3(256), 0, s, a);
     else if (pl.bm == 128) hipLaunchKernelGGL((wgrad_h3_kernel<128, 64>), grid, dim3(256), 0, s, a);
     else if (pl.bn == 128) hipLaunchKernelGGL((wgrad_h3_kernel<64, 128>), grid, dim3(256), 0, s, a);
     else hipLaunchKernelGGL((wgrad_h3_kernel<64, 64>), grid, dim3(256), 0, s, a);
     return launch_status("wgrad_h3");
   }
-  if (tune_get(PIS_TUNE_WGRAD_X6) != 0 && a.b_mode == B_PLAIN && pl.pps % 16 == 0 && (!a.a_up2 || a.W % 8 == 0)) {
+  if (x6 != 0 && a.b_mode == B_PLAIN && pl.pps % 16 == 0 && (!a.a_up2 || a.W % 8 == 0)) {
     if (pl.bm == 128 && pl.bn == 128) hipLaunchKernelGGL((wgrad_x6_kernel<128, 128>), grid, dim3(256), 0, s, a);
     else if (pl.bm == 128) hipLaunchKernelGGL((wgrad_x6_kernel<128, 64>), grid, dim3(256), 0, s, a);
     else if (pl.bn == 128) hipLaunchKernelGGL((wgrad_x6_kernel<64, 128>), grid, dim3(256), 0, s, a);

@@ -307,8 +307,9 @@ __device__ __forceinline__ void tile_decode(int64_t e, int c4n, int tpi, int64_t
 // (the fused GEMM + output-transform kernel reads its B fragments straight from them).
 __device__ __forceinline__ void wino4_filter_item(const float (&g)[3][3], int64_t e, int n, int c, int N,
                                                   int64_t NC, float* __restrict__ U, int transposed,
-                                                  __bf16* __restrict__ Up) {
+                                                  __bf16* __restrict__ Up, float* __restrict__ umax = nullptr) {
   float gg[6][3];  // G g
+  float um = 0.f;
 #pragma unroll
   for (int i = 0; i < 6; ++i)
 #pragma unroll
@@ -336,28 +337,37 @@ __device__ __forceinline__ void wino4_filter_item(const float (&g)[3][3], int64_
       }
       // [xi][n][c] for the batched GEMMs; [xi][c][n] for the fused kernel's B operand
       U[(size_t)(i * 6 + j) * NC + (transposed ? (int64_t)c * N + n : e)] = u;
+      um = fmaxf(um, fabsf(u));
     }
+  // umax[n][c / 32] = max |U| over xi and the 32-channel chunk (the fp16x3 GEMM's per-row filter
+  // scales): the callers give a chunk's 32 (n, c) items to an aligned half-wave, all active
+  if (umax) {
+#pragma unroll
+    for (int off = 16; off > 0; off >>= 1) um = fmaxf(um, __shfl_xor(um, off, 32));
+    if ((c & 31) == 0) umax[e >> 5] = um;
+  }
 }
 
 // w: KRSC weights [N][9][C] (row pitch ldw), already in the operand's orientation (the forward's
 // own weights, or pis_conv3x3_flip's copy for an input gradient). Block `bid` of `nblk`.
 __device__ __forceinline__ void wino4_filter_range(const float* __restrict__ w, int ldw, int N, int C,
                                                    float* __restrict__ U, int transposed, __bf16* __restrict__ Up,
-                                                   int bid, int nblk) {
+                                                   int bid, int nblk, float* __restrict__ umax = nullptr) {
   const int64_t NC = (int64_t)N * C;
   for (int64_t e = (int64_t)bid * blockDim.x + threadIdx.x; e < NC; e += (int64_t)nblk * blockDim.x) {
     const int n = (int)(e / C), c = (int)(e - (int64_t)n * C);
     float g[3][3];
 #pragma unroll
     for (int t = 0; t < 9; ++t) g[t / 3][t % 3] = w[(size_t)n * ldw + t * C + c];
-    wino4_filter_item(g, e, n, c, N, NC, U, transposed, Up);
+    wino4_filter_item(g, e, n, c, N, NC, U, transposed, Up, umax);
   }
 }
 
 __global__ __launch_bounds__(256) void wino4_filter_kernel(const float* __restrict__ w, int ldw, int N, int C,
                                                            float* __restrict__ U, int transposed = 0,
-                                                           __bf16* __restrict__ Up = nullptr) {
-  wino4_filter_range(w, ldw, N, C, U, transposed, Up, blockIdx.x, gridDim.x);
+                                                           __bf16* __restrict__ Up = nullptr,
+                                                           float* __restrict__ umax = nullptr) {
+  wino4_filter_range(w, ldw, N, C, U, transposed, Up, blockIdx.x, gridDim.x, umax);
 }
 
 // The input-gradient filter transform straight from the layer's ORIGINAL KRSC weights [C][9][N]
@@ -368,7 +378,8 @@ __global__ __launch_bounds__(256) void wino4_filter_kernel(const float* __restri
 // output planes are written in runs along c as by wino4_filter_kernel.
 __device__ __forceinline__ void wino4_filter_rot_tile(const float* __restrict__ w, int N, int C,
                                                       float* __restrict__ U, int transposed,
-                                                      __bf16* __restrict__ Up, int tile) {
+                                                      __bf16* __restrict__ Up, int tile,
+                                                      float* __restrict__ umax = nullptr) {
   __shared__ float sg[9][32][33];  // [tap][c][n], padded: the transform reads along c conflict-free
   const int nb = N / 32, n0 = 32 * (tile % nb), c0 = 32 * (tile / nb);
   const int tid = threadIdx.x, lx = tid & 31, ly = tid >> 5;
@@ -387,14 +398,15 @@ __device__ __forceinline__ void wino4_filter_rot_tile(const float* __restrict__ 
     float g[3][3];
 #pragma unroll
     for (int t = 0; t < 9; ++t) g[t / 3][t % 3] = sg[8 - t][c][nl];
-    wino4_filter_item(g, (int64_t)n * C + c0 + c, n, c0 + c, N, NC, U, transposed, Up);
+    wino4_filter_item(g, (int64_t)n * C + c0 + c, n, c0 + c, N, NC, U, transposed, Up, umax);
   }
 }
 
 __global__ __launch_bounds__(256) void wino4_filter_rot_kernel(const float* __restrict__ w, int N, int C,
                                                                float* __restrict__ U, int transposed,
-                                                               __bf16* __restrict__ Up) {
-  wino4_filter_rot_tile(w, N, C, U, transposed, Up, blockIdx.x);
+                                                               __bf16* __restrict__ Up,
+                                                               float* __restrict__ umax = nullptr) {
+  wino4_filter_rot_tile(w, N, C, U, transposed, Up, blockIdx.x, umax);
 }
 
 // The fused kernel's fp16x3 filter planes (pis_tune key 22), C == 64: one wave per output channel
@@ -458,6 +470,7 @@ __global__ __launch_bounds__(256) void wino4_filter_h2_kernel(const float* __res
 struct FilterJobDev {
   const float* w;
   void* out;
+  float* umax;  // fp32 format: the per-(n, 32-channel chunk) maxima after U, or NULL
   int N, C, dgrad, planes, blocks;
 };
 constexpr int FILTER_MAX_JOBS = 40;
@@ -475,8 +488,8 @@ __global__ __launch_bounds__(256) void wino4_filter_batch_kernel(FilterBatch fb)
   float* U = jb.planes ? nullptr : reinterpret_cast<float*>(jb.out);
   __bf16* Up = jb.planes ? reinterpret_cast<__bf16*>(jb.out) : nullptr;
   if (jb.planes == 2) wino4_filter_h2_wave(jb.w, 9 * jb.C, jb.N, jb.dgrad, Up, 4 * lb + (threadIdx.x >> 6));
-  else if (jb.dgrad) wino4_filter_rot_tile(jb.w, jb.N, jb.C, U, 0, Up, lb);
-  else wino4_filter_range(jb.w, 9 * jb.C, jb.N, jb.C, U, 0, Up, lb, jb.blocks);
+  else if (jb.dgrad) wino4_filter_rot_tile(jb.w, jb.N, jb.C, U, 0, Up, lb, jb.umax);
+  else wino4_filter_range(jb.w, 9 * jb.C, jb.N, jb.C, U, 0, Up, lb, jb.blocks, jb.umax);
 }
 
 // V[xi][t][c] = (BT d BT^T)[xi], d = the 6x6 input patch at rows 4ty-1.., cols 4tx-1.. (zero padded)
@@ -522,11 +535,14 @@ __device__ __forceinline__ float wino4_input_item(const float* __restrict__ x, i
   return m;
 }
 
-// tmax[t] = max over the tile's lanes (C / VW consecutive lanes, a power of two <= 64: every lane
-// of a tile takes the same grid-stride trip count)
-__device__ __forceinline__ void tile_max_store(float m, int lanes, int c, int64_t t, float* __restrict__ tmax) {
-  for (int off = lanes >> 1; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off, 64));
-  if (c == 0) tmax[t] = m;
+// tmax[t][c / 64] = max |V| over the tile's 64-channel chunk: 64 / VW consecutive lanes (C % 64 ==
+// 0, so a chunk's lanes are an aligned group of one wave and take the same grid-stride trip count).
+// The fp16x3 consumers take one power-of-two scale per tile (row) from the max over its chunks.
+template <int VW>
+__device__ __forceinline__ void tile_max_store(float m, int C, int c, int64_t t, float* __restrict__ tmax) {
+#pragma unroll
+  for (int off = 32 / VW; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off, 64));
+  if ((c & 63) == 0) tmax[t * (C >> 6) + (c >> 6)] = m;
 }
 
 // VW channels per thread (pis_tune key 17): 2 (default) = half the registers of 4 (float4 accesses)
@@ -542,7 +558,7 @@ __global__ __launch_bounds__(256) void wino4_input_kernel(const float* __restric
     tile_decode<VW>(e, c4n, TH * TW, t, c, b, rem);
     const int ty = rem / TW, tx = rem - ty * TW;
     const float m = wino4_input_item<VW, TM>(x, ldx, H, W, C, V, TC, t, b, ty, tx, c);
-    if constexpr (TM) tile_max_store(m, c4n, c, t, tmax);
+    if constexpr (TM) tile_max_store<VW>(m, C, c, t, tmax);
   }
 }
 
@@ -863,7 +879,7 @@ __global__ __launch_bounds__(256) void wino4_dz2_kernel(const float* __restrict_
     tile_decode(e, n4n, TH * TW, t, n, b, rem);
     const int ty = rem / TW, tx = rem - ty * TW;
     const float m = wino4_input_item<4, TM>(dz, ldz, H, W, N, V, TN, t, b, ty, tx, n);
-    if constexpr (TM) tile_max_store(m, n4n, n, t, tmax);
+    if constexpr (TM) tile_max_store<4>(m, N, n, t, tmax);
     wino4_dz_item(dz, ldz, H, W, N, E, TN, t, b, ty, tx, n, bsum);
   }
   if (bpart) wino4_bias_partials(bsum, N, bpart);
@@ -1285,18 +1301,29 @@ __global__ __launch_bounds__(256, OCC) void gemm_nt_x6_bk32_kernel(const float* 
 // In the 32 x 32 MFMA output a lane holds column n = li (B row staged by wave (li / 8) % 4) and
 // rows r -> (r & 3) + 8 (r >> 2) + 4 lh (A rows staged by wave r >> 2): accumulator register r
 // is in units sA[r >> 2] * sB[(li / 8) % 4], and is re-expressed when a K-step's scales differ.
-template <int BM, int BN, int OCC = 3, bool SC = true>
+//
+// PRE (pis_tune key 23, opt-in: measured 10 % slower than the wave scales, its producers' maxima
+// another 11 % on the input transform; profiles/r2_q65_*): no in-loop scales at all. Every A row (a
+// tile) and every B row (an output channel) gets ONE power-of-two scale for the whole contraction
+// from maxima its producers wrote — amax[m][K / 64] by the input / dz transforms (over all 36 xi
+// of the tile and each 64-channel chunk), umax[n][K / 32] by the filter transform (over all xi
+// and each 32-channel chunk) — so the accumulators are in units s_m t_n throughout and the
+// epilogue divides once: no wave maxima, no scale exchange, no rescaling of partial sums.
+template <int BM, int BN, int OCC = 3, bool SC = true, bool PRE = false>
 __global__ __launch_bounds__(256, OCC) void gemm_nt_h3_bk32_kernel(const float* __restrict__ A,
                                                                 const float* __restrict__ Bm, float* __restrict__ Cm,
                                                                 int M, int N, int K, int64_t bsA, int64_t bsB,
-                                                                int64_t bsC) {
+                                                                int64_t bsC, const float* __restrict__ amax,
+                                                                const float* __restrict__ umax) {
   constexpr int BK = 32, KP = 32;
+  constexpr bool WS = SC && !PRE;  // per-wave, per-K-step scales
   constexpr int TM = BM / 64, TN = BN / 64;
   constexpr int AL = BM * 8 / 256, BL = BN * 8 / 256;
   static_assert(BM % 128 == 0 && BN % 64 == 0, "row r's staging wave must be r / 8 % 4");
   __shared__ __attribute__((aligned(16))) _Float16 sA[2][BM * KP];
   __shared__ __attribute__((aligned(16))) _Float16 sB[2][BN * KP];
   __shared__ __attribute__((aligned(16))) float sscale[2][4];  // [A|B][staging wave]
+  __shared__ float sinv[PRE ? BM + BN : 1];                    // PRE: 1 / scale of each A, B row
   A += blockIdx.y * bsA;
   Bm += blockIdx.y * bsB;
   Cm += blockIdx.y * bsC;
@@ -1306,6 +1333,34 @@ __global__ __launch_bounds__(256, OCC) void gemm_nt_h3_bk32_kernel(const float* 
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int m0 = (bid / ntn) * BM, n0 = (bid % ntn) * BN;
   const int q8 = (tid & 7) * 4;
+  // PRE: the staged rows' scales as biased exponent bytes (AL, BL <= 4: one register each)
+  static_assert(!PRE || (AL <= 4 && BL <= 4), "one exponent byte per staged row");
+  unsigned pae = 0, pbe = 0;
+  if constexpr (PRE) {
+    // the 8 threads staging a row (an aligned group of 8 lanes) split its chunk maxima
+    const int j8 = tid & 7, ka = K >> 6, kb = K >> 5;
+#pragma unroll
+    for (int i = 0; i < AL; ++i) {
+      const int r = (tid + i * 256) / 8, m = m0 + r;
+      float mx = 0.f;
+      if (m < M)
+        for (int j = j8; j < ka; j += 8) mx = fmaxf(mx, amax[(size_t)m * ka + j]);
+      float sc, inv;
+      h2_scale_pair(group8_max_nonneg(mx), sc, inv);
+      pae |= (__float_as_uint(sc) >> 23) << (8 * i);
+      if (j8 == 0) sinv[r] = inv;
+    }
+#pragma unroll
+    for (int i = 0; i < BL; ++i) {
+      const int r = (tid + i * 256) / 8, n = n0 + r;
+      float mx = 0.f;
+      for (int j = j8; j < kb; j += 8) mx = fmaxf(mx, umax[(size_t)n * kb + j]);
+      float sc, inv;
+      h2_scale_pair(group8_max_nonneg(mx), sc, inv);
+      pbe |= (__float_as_uint(sc) >> 23) << (8 * i);
+      if (j8 == 0) sinv[BM + r] = inv;
+    }
+  }
   const bool full = m0 + BM <= M && K % BK == 0;
   f32x4 ra[AL], rb[BL];
   auto gload = [&](int k0) {
@@ -1325,7 +1380,10 @@ __global__ __launch_bounds__(256, OCC) void gemm_nt_h3_bk32_kernel(const float* 
   };
   float sa = 0.f, sb = 0.f;  // the wave's current scales (h3_keep)
   auto lstore = [&]() {
-    if (SC) {
+    // PRE: re-read the packed exponents every K-step: hoisted out of the loop, the compiler keeps
+    // 8 broadcast scale pairs live (16 VGPRs) and spills them
+    if (PRE) asm volatile("" : "+v"(pae), "+v"(pbe));
+    if (WS) {
       float ma = 0.f, mb = 0.f;
 #pragma unroll
       for (int i = 0; i < AL; ++i)
@@ -1345,7 +1403,7 @@ __global__ __launch_bounds__(256, OCC) void gemm_nt_h3_bk32_kernel(const float* 
 #pragma unroll
     for (int i = 0; i < AL; ++i) {
       u32x2 h, l;
-      split2h_x4(SC ? ra[i] * sa : ra[i], h, l);
+      split2h_x4(PRE ? ra[i] * __uint_as_float(((pae >> (8 * i)) & 0xffu) << 23) : WS ? ra[i] * sa : ra[i], h, l);
       const int row = (tid + i * 256) / 8, o = x6w8_off(row, q8 >> 3) + (q8 & 7);
       *reinterpret_cast<u32x2*>(&sA[0][o]) = h;
       *reinterpret_cast<u32x2*>(&sA[1][o]) = l;
@@ -1353,7 +1411,7 @@ __global__ __launch_bounds__(256, OCC) void gemm_nt_h3_bk32_kernel(const float* 
 #pragma unroll
     for (int i = 0; i < BL; ++i) {
       u32x2 h, l;
-      split2h_x4(SC ? rb[i] * sb : rb[i], h, l);
+      split2h_x4(PRE ? rb[i] * __uint_as_float(((pbe >> (8 * i)) & 0xffu) << 23) : WS ? rb[i] * sb : rb[i], h, l);
       const int row = (tid + i * 256) / 8, o = x6w8_off(row, q8 >> 3) + (q8 & 7);
       *reinterpret_cast<u32x2*>(&sB[0][o]) = h;
       *reinterpret_cast<u32x2*>(&sB[1][o]) = l;
@@ -1374,7 +1432,7 @@ __global__ __launch_bounds__(256, OCC) void gemm_nt_h3_bk32_kernel(const float* 
   f32x4 ua = {1.f, 1.f, 1.f, 1.f};  // units of the accumulators: A scale per row group r >> 2,
   float ub = 1.f;                   // B scale of this lane's column
   for (int kt = 0; kt < KT; ++kt) {
-    if (SC) {  // this K-step's scales; re-express the partial sums in them (exact: powers of two)
+    if (WS) {  // this K-step's scales; re-express the partial sums in them (exact: powers of two)
       const f32x4 na = *reinterpret_cast<const f32x4*>(&sscale[0][0]);
       const float nb = sscale[1][(li >> 3) & 3];
       if (kt == 0) {
@@ -1425,16 +1483,18 @@ __global__ __launch_bounds__(256, OCC) void gemm_nt_h3_bk32_kernel(const float* 
   }
   float inv[4];
 #pragma unroll
-  for (int q = 0; q < 4; ++q) inv[q] = SC ? 1.f / (ua[q] * ub) : 1.f;
+  for (int q = 0; q < 4; ++q) inv[q] = WS ? 1.f / (ua[q] * ub) : 1.f;
 #pragma unroll
   for (int a = 0; a < TM; ++a)
 #pragma unroll
     for (int b = 0; b < TN; ++b) {
-      const int n = n0 + wn * (BN / 2) + b * 32 + li;
+      const int nl = wn * (BN / 2) + b * 32 + li, n = n0 + nl;
+      const float ib = PRE ? sinv[BM + nl] : 1.f;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int m = m0 + wm * (BM / 2) + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-        if (m < M) Cm[(size_t)m * N + n] = acc[a][b][r] * inv[r >> 2];
+        const int ml = wm * (BM / 2) + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh, m = m0 + ml;
+        // PRE: exact powers of two, one at a time (no product of two inverses can underflow)
+        if (m < M) Cm[(size_t)m * N + n] = PRE ? (acc[a][b][r] * sinv[ml]) * ib : acc[a][b][r] * inv[r >> 2];
       }
     }
 }
@@ -1870,7 +1930,7 @@ static void launch_wino4_output(const float* Mt, const IGemmArgs& a, int B, int6
 }
 
 // the F(4x4,3x3) input transform, 2 (default) or 4 channels per thread (pis_tune key 17)
-// tmax (C == 64 only): also the per-tile max |V| (the fused kernel's fp16x3 tile scales)
+// tmax (C % 64 == 0): also the per-tile, per-64-channel-chunk max |V| (the fp16x3 tile scales)
 static void launch_wino4_input(int64_t T, int C, hipStream_t s, const float* x, int ldx, int B, int H, int W, int,
                                float* V, float* tmax = nullptr) {
   const bool vw2 = tune_get(PIS_TUNE_WINO_VW) != 4;
@@ -1891,17 +1951,25 @@ static void launch_wino4_input(int64_t T, int C, hipStream_t s, const float* x, 
 // the F(4x4,3x3) filter transform of a's weights (the tiled kernel for unflipped 32-aligned shapes)
 // (Up: the fused kernel's planes, bf16x6 or, with h2, fp16x3 + scales — C % 32 == 0)
 static void launch_wino4_filter(const IGemmArgs& a, int N, int C, float* U, int transposed, __bf16* Up,
-                                hipStream_t s, bool h2 = false) {
+                                hipStream_t s, bool h2 = false, float* umax = nullptr) {
   if (h2)  // C == 64, N % 4 == 0 (the fused kernel's shapes)
     hipLaunchKernelGGL(wino4_filter_h2_kernel, dim3(N / 4), dim3(256), 0, s, a.wt, a.ldw, N, a.w_unflipped ? 1 : 0,
                        Up);
   else if (a.w_unflipped)  // N, C % 32 == 0 checked by launch_wino3x3
     hipLaunchKernelGGL(wino4_filter_rot_kernel, dim3((N / 32) * (C / 32)), dim3(256), 0, s, a.wt, N, C, U,
-                       transposed, Up);
+                       transposed, Up, umax);
   else
     hipLaunchKernelGGL(wino4_filter_kernel, dim3(grid_of((int64_t)N * C)), dim3(256), 0, s, a.wt, a.ldw, N, C, U,
-                       transposed, Up);
+                       transposed, Up, umax);
 }
+
+// the batched fp16x3 GEMM with producer-written row scales (pis_tune key 23; gemm_nt_h3_bk32_kernel
+// PRE): the input / dz transform leaves per-(tile, 64-channel) maxima, the filter transform
+// per-(channel, 32-channel) maxima, in the workspace after M (wino_tmax_slot / wino_umax_slot)
+static bool h3_prescaled(int C, int N) {
+  return tune_get(PIS_TUNE_WINO_TILE) == 4 && tune_get(PIS_TUNE_WINO_H3_PRE) != 0 && C % 64 == 0 && N % 64 == 0;
+}
+bool wino_h3_prescaled(int C, int N) { return h3_prescaled(C, N); }
 
 // the fused 64 -> 64 kernel's arithmetic (pis_tune key 22): fp16x3 planes instead of bf16x6
 static bool wino_gemm_out_h3() { return tune_get(PIS_TUNE_WINO_GEMM_OUT_H3) != 0; }
@@ -1962,8 +2030,10 @@ float* wino_v_slot(void* ws, int C, int N) { return (float*)ws + (size_t)36 * N 
 size_t wino_ws_bytes(int B, int H, int W, int C, int N) {
   const int m = wino_tile(H, W), nxi = (m + 2) * (m + 2);
   const int64_t T = (int64_t)B * (H / m) * (W / m);
-  // + T floats: the per-tile max |V| of the fused fp16x3 kernel (wino_tmax_slot)
-  return (size_t)(nxi * ((int64_t)N * C + T * C + T * N) + T) * sizeof(float) + 1024;
+  // + the fp16x3 row maxima after M: per (tile, 64-channel chunk) of V (wino_tmax_slot), per
+  // (channel, 32-channel chunk) of U (wino_umax_slot)
+  const int64_t extra = T * ((C + 63) / 64) + 8 + (int64_t)N * ((C + 31) / 32);
+  return (size_t)(nxi * ((int64_t)N * C + T * C + T * N) + extra) * sizeof(float) + 1024;
 }
 
 // fused F(4x4,3x3) (pis_tune key 12: 0 off, 1 auto, 2 whenever the shape allows)
@@ -2018,12 +2088,19 @@ int launch_wino3x3(const IGemmArgs& a, int B, void* ws, hipStream_t s, float* ke
   if (v_ready && m != 4) return set_error("launch_wino3x3: prepared transforms need F(4x4,3x3)"), PIS_ERR_ARG;
   if (a.w_unflipped && (m != 4 || N % 32 || C % 32))
     return set_error("launch_wino3x3: unflipped weights need F(4x4,3x3) and 32-aligned channels"), PIS_ERR_ARG;
+  const bool pre = m == 4 && h3_prescaled(C, N);
+  float* tmax = pre ? wino_tmax_slot(ws, B, a.H, a.W, C, N) : nullptr;
+  float* umax = pre ? wino_umax_slot(ws, B, a.H, a.W, C, N) : nullptr;
   if (m == 4) {
-    if (a.filter_ready) U = const_cast<float*>(a.wt);
-    else launch_wino4_filter(a, N, C, U, 0, nullptr, s);
+    if (a.filter_ready) {
+      U = const_cast<float*>(a.wt);
+      if (pre) umax = U + (size_t)36 * N * C;  // pis_conv3x3_filter writes them after U
+    } else {
+      launch_wino4_filter(a, N, C, U, 0, nullptr, s, false, umax);
+    }
     if (!v_ready)
       launch_wino4_input(T, C, s, a.src, a.lds, B, a.H, a.W,
-                         C, V);
+                         C, V, tmax);
   } else {
     hipLaunchKernelGGL(wino_filter_kernel, dim3(grid_of((int64_t)N * C)), dim3(256), 0, s, a.wt, a.ldw, N, C, U);
     hipLaunchKernelGGL(wino_input_kernel, dim3(grid_of(T * (C / 4))), dim3(256), 0, s, a.src, a.lds, B, a.H, a.W,
@@ -2042,12 +2119,20 @@ int launch_wino3x3(const IGemmArgs& a, int B, void* ws, hipStream_t s, float* ke
     // fp16x3 with per-K-step power-of-two tile scales (gemm_nt_h3_bk32_kernel)
     if (N % 128 == 0) {
       const dim3 grid((int)cdiv(T, 128) * (N / 128), nxi);
-      hipLaunchKernelGGL((gemm_nt_h3_bk32_kernel<128, 128, 3>), grid, dim3(256), 0, s, V, U, Mt, (int)T, N, C,
-                         T * C, (int64_t)N * C, T * N);
+      if (pre)
+        hipLaunchKernelGGL((gemm_nt_h3_bk32_kernel<128, 128, 3, true, true>), grid, dim3(256), 0, s, V, U, Mt,
+                           (int)T, N, C, T * C, (int64_t)N * C, T * N, tmax, umax);
+      else
+        hipLaunchKernelGGL((gemm_nt_h3_bk32_kernel<128, 128, 3>), grid, dim3(256), 0, s, V, U, Mt, (int)T, N, C,
+                           T * C, (int64_t)N * C, T * N, nullptr, nullptr);
     } else {
       const dim3 grid((int)cdiv(T, 128) * (N / 64), nxi);
-      hipLaunchKernelGGL((gemm_nt_h3_bk32_kernel<128, 64, 4>), grid, dim3(256), 0, s, V, U, Mt, (int)T, N, C,
-                         T * C, (int64_t)N * C, T * N);
+      if (pre)
+        hipLaunchKernelGGL((gemm_nt_h3_bk32_kernel<128, 64, 4, true, true>), grid, dim3(256), 0, s, V, U, Mt,
+                           (int)T, N, C, T * C, (int64_t)N * C, T * N, tmax, umax);
+      else
+        hipLaunchKernelGGL((gemm_nt_h3_bk32_kernel<128, 64, 4>), grid, dim3(256), 0, s, V, U, Mt, (int)T, N, C,
+                           T * C, (int64_t)N * C, T * N, nullptr, nullptr);
     }
     rc = launch_status("wino_gemm");
   } else if (v >= 3 && N % 128 == 0) {
@@ -2116,7 +2201,9 @@ int launch_wino4_filter_only(const float* w, int C, int N, int dgrad, int format
   if (format == 2 && wino_gemm_out_h3() && (C != 64 || N % 4))
     return set_error("pis_conv3x3_filter: fp16x3 planes need 64 contraction channels"), PIS_ERR_ARG;
   if (format == 2) launch_wino4_filter(a, N, C, nullptr, 0, reinterpret_cast<__bf16*>(out), s, wino_gemm_out_h3());
-  else launch_wino4_filter(a, N, C, reinterpret_cast<float*>(out), 0, nullptr, s);
+  else  // + the row maxima after U when the consuming GEMM is the prescaled fp16x3 one
+    launch_wino4_filter(a, N, C, reinterpret_cast<float*>(out), 0, nullptr, s, false,
+                        h3_prescaled(C, N) ? reinterpret_cast<float*>(out) + (size_t)36 * N * C : nullptr);
   return launch_status("wino_filter");
 }
 
@@ -2135,7 +2222,9 @@ int launch_wino4_filter_batch(int n, const float* const* w, void* const* out, co
     if (planes == 2 && (C[k] != 64 || N[k] % 4))
       return set_error("pis_conv3x3_filters: fp16x3 planes need 64 contraction channels"), PIS_ERR_ARG;
     const int blocks = planes == 2 ? N[k] / 4 : dgrad[k] ? (N[k] / 32) * (C[k] / 32) : grid_of((int64_t)N[k] * C[k]);
-    fb.j[k] = FilterJobDev{w[k], out[k], N[k], C[k], dgrad[k], planes, blocks};
+    float* umax = planes == 0 && h3_prescaled(C[k], N[k]) ? reinterpret_cast<float*>(out[k]) + (size_t)36 * N[k] * C[k]
+                                                          : nullptr;
+    fb.j[k] = FilterJobDev{w[k], out[k], umax, N[k], C[k], dgrad[k], planes, blocks};
     fb.start[k] = total;
     total += blocks;
   }
@@ -2179,17 +2268,25 @@ int launch_wino_dz2(const float* dz, int ldz, int B, int H, int W, int N, float*
   return launch_status("wino_dz2");
 }
 
-// where the fused fp16x3 kernel finds the per-tile max |V| of its V (after the M region)
+// where the fp16x3 consumers find the per-(tile, 64-channel chunk) max |V| of their V (after M)
 float* wino_tmax_slot(void* ws, int B, int H, int W, int C, int N) {
   const int64_t T = (int64_t)B * (H / 4) * (W / 4);
   return (float*)ws + (size_t)36 * ((int64_t)N * C + T * C + T * N);
 }
 
-// the dgrad of these shapes (C contraction = Cout, N = Cin) runs the fused fp16x3 kernel: its V
-// producer (pis_conv3x3_bwd_prep) must leave the tile maxima at wino_tmax_slot
+// ... and the per-(channel, 32-channel chunk) max |U| of the batched GEMMs' filter
+float* wino_umax_slot(void* ws, int B, int H, int W, int C, int N) {
+  const int64_t T = (int64_t)B * (H / 4) * (W / 4);
+  return wino_tmax_slot(ws, B, H, W, C, N) + ((T * ((C + 63) / 64) + 7) & ~(int64_t)7);
+}
+
+// the dgrad of these shapes (C contraction = Cout, N = Cin) reads tile maxima (the fused fp16x3
+// kernel or the prescaled fp16x3 GEMM): its V producer (pis_conv3x3_bwd_prep) must write them
 bool wino_fused_h3_planned(int B, int H, int W, int C, int N) {
-  if (wino_tile(H, W) != 4 || !wino_gemm_out_h3()) return false;
-  return wino_gemm_out_wanted(4, (int64_t)B * (H / 4) * (W / 4), C, N);
+  if (wino_tile(H, W) != 4) return false;
+  const int64_t T = (int64_t)B * (H / 4) * (W / 4);
+  if (wino_gemm_out_wanted(4, T, C, N)) return wino_gemm_out_h3();
+  return h3_prescaled(C, N);
 }
 
 int launch_wino_wgrad_out(const float* M, int N, int C, float* dw, int accumulate, hipStream_t s, int m,
@@ -2237,9 +2334,9 @@ extern "C" int pis_debug_gemm_nt(const float* A, const float* B, float* C, int M
     case 5: hipLaunchKernelGGL((gemm_nt_x6_bk32_kernel<128, 128>), grid, dim3(256), 0, s, A, B, C, M, N, K, sa, sb, sc); break;
     case 6: hipLaunchKernelGGL((gemm_nt_x6_bk32_kernel<128, 128, 3>), grid, dim3(256), 0, s, A, B, C, M, N, K, sa, sb, sc); break;
     case 7: hipLaunchKernelGGL((gemm_nt_x6_bk32_kernel<128, 64, 3>), grid, dim3(256), 0, s, A, B, C, M, N, K, sa, sb, sc); break;
-    case 10: hipLaunchKernelGGL((gemm_nt_h3_bk32_kernel<128, 128, 3, false>), grid, dim3(256), 0, s, A, B, C, M, N, K, sa, sb, sc); break;
-    case 11: hipLaunchKernelGGL((gemm_nt_h3_bk32_kernel<128, 128, 3>), grid, dim3(256), 0, s, A, B, C, M, N, K, sa, sb, sc); break;
-    case 12: hipLaunchKernelGGL((gemm_nt_h3_bk32_kernel<128, 64, 4>), grid, dim3(256), 0, s, A, B, C, M, N, K, sa, sb, sc); break;
+    case 10: hipLaunchKernelGGL((gemm_nt_h3_bk32_kernel<128, 128, 3, false>), grid, dim3(256), 0, s, A, B, C, M, N, K, sa, sb, sc, nullptr, nullptr); break;
+    case 11: hipLaunchKernelGGL((gemm_nt_h3_bk32_kernel<128, 128, 3>), grid, dim3(256), 0, s, A, B, C, M, N, K, sa, sb, sc, nullptr, nullptr); break;
+    case 12: hipLaunchKernelGGL((gemm_nt_h3_bk32_kernel<128, 64, 4>), grid, dim3(256), 0, s, A, B, C, M, N, K, sa, sb, sc, nullptr, nullptr); break;
     default: set_error("pis_debug_gemm_nt: unknown variant %d", variant); return PIS_ERR_ARG;
   }
   return launch_status("debug_gemm_nt");
