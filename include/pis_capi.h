@@ -79,8 +79,9 @@ int pis_version(void);
                                     (auto: measured slower than the 3-pass pipeline on every layer that keeps V),
                                     2 whenever H % 16 == W % 64 == N % 16 == 0 */
 #define PIS_TUNE_CONVT_GEMM 13   /* transposed conv fwd/dgrad: lean NT GEMM with gather/scatter addressing when
-                                    Cin, Cout % 16 == 0 — 1 (default) fp32-accurate bf16x6 on bf16 MFMA, 2 on fp32
-                                    MFMA; 0 generic implicit GEMM */
+                                    Cin, Cout % 16 == 0 — 3 (default) fp32-class fp16x3 on fp16 MFMA (per-wave,
+                                    per-K-step power-of-two scales), 1 bf16x6 on bf16 MFMA, 2 on fp32 MFMA; 0 generic
+                                    implicit GEMM */
 #define PIS_TUNE_WGRAD_X6 14     /* Winograd and transposed-conv weight-gradient GEMMs: 3 (default) fp16x3 where the
                                     layer has >= 256 input channels, bf16x6 elsewhere; 1 fp32-accurate bf16x6 on
                                     bf16 MFMA everywhere, 2 fp16x3 (as key 10 = 4) everywhere (-1 % on the step: the

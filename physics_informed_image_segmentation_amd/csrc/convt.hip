@@ -12,8 +12,9 @@
 //            Bt = w_cijo rows (pis_convt2x2_prep); the epilogue applies the ReLU mask of the
 //            convT input and optionally accumulates.
 // Block tile 128 x 128, 4 waves of 64 x 64 (2 x 2 32x32 MFMA tiles), K-step 16 through a
-// register-staged LDS double buffer; XCD-aware tile order. pis_tune key 13: 1 (default) bf16x6
-// on bf16 MFMA (fp32-accurate), 2 native fp32 MFMA, 0 off (implicit-GEMM fallback).
+// register-staged LDS double buffer; XCD-aware tile order. pis_tune key 13: 3 (default) fp16x3 on
+// fp16 MFMA (fp32-class, -3..-18 % per layer vs bf16x6, profiles/r2_q68_*), 1 bf16x6 on bf16 MFMA
+// (fp32-accurate), 2 native fp32 MFMA, 0 off (implicit-GEMM fallback).
 #include "igemm.h"
 
 namespace pis {
@@ -36,16 +37,22 @@ struct ConvtGemmArgs {
 
 typedef __bf16 cbf16x8 __attribute__((ext_vector_type(8)));
 
-// X6: the operands are split into hi/mid/lo bf16 planes at LDS staging and every fp32
-// multiply-add becomes six bf16 MFMA partial products (fp32 accuracy, see gemm_nt_x6_kernel)
-template <int MODE, bool X6>  // MODE 0 forward, 1 input gradient
+// AR (arithmetic): 0 native fp32 MFMA; 1 X6: the operands are split into hi/mid/lo bf16 planes at
+// LDS staging and every fp32 multiply-add becomes six bf16 MFMA partial products (fp32 accuracy,
+// see gemm_nt_x6_kernel); 2 H3: fp16x3 (common.h) — hi/lo fp16 planes of the operands scaled by a
+// power of two per wave and K-step (h3_keep), three fp16 products, accumulators re-expressed when
+// a K-step's scales change (as wgrad_h3_kernel). Row r of a 128-row tile is staged by wave
+// (r / 16) % 4 (threads tid / 4 and 64 + tid / 4).
+template <int MODE, int AR>  // MODE 0 forward, 1 input gradient
 __global__ __launch_bounds__(256, 2) void convt_gemm_kernel(ConvtGemmArgs g) {
+  constexpr bool X6 = AR == 1, H3 = AR == 2;
   constexpr int BM = 128, BN = 128, BK = 16, ROW = BK + 4;
   constexpr int AL = BM * 4 / 256, BL = BN * 4 / 256;
   // LDS image per buffer: fp32 [row][ROW], or (X6) bf16 [hi|mid|lo][row][16] in the same floats
   constexpr int SA = X6 ? 3 * BM * BK / 2 : BM * ROW, SB = X6 ? 3 * BN * BK / 2 : BN * ROW;
   __shared__ __attribute__((aligned(16))) float sA[2][SA];
   __shared__ __attribute__((aligned(16))) float sB[2][SB];
+  __shared__ __attribute__((aligned(16))) float sscale[2][2][4];  // H3: [buf][A|B][staging wave]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave & 1, wn = wave >> 1, li = lane & 31, lh = lane >> 5;
   const int ntn = (g.N + BN - 1) / BN;
@@ -91,8 +98,43 @@ __global__ __launch_bounds__(256, 2) void convt_gemm_kernel(ConvtGemmArgs g) {
       if (n < g.N) rb[i] = *reinterpret_cast<const f32x4*>(g.bt + (size_t)n * g.K + k0 + q4);
     }
   };
+  float sa = 0.f, sb = 0.f;  // H3: this wave's current scales
   auto lstore = [&](int buf) {
-    if constexpr (X6) {
+    if constexpr (H3) {
+      float ma = 0.f, mb = 0.f;
+#pragma unroll
+      for (int i = 0; i < AL; ++i)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) ma = fmaxf(ma, fabsf(ra[i][k]));
+#pragma unroll
+      for (int i = 0; i < BL; ++i)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) mb = fmaxf(mb, fabsf(rb[i][k]));
+      sa = h3_keep(sa, wave_max_nonneg(ma));
+      sb = h3_keep(sb, wave_max_nonneg(mb));
+      if (lane == 0) {
+        sscale[buf][0][wave] = sa;
+        sscale[buf][1][wave] = sb;
+      }
+      _Float16* pa = reinterpret_cast<_Float16*>(sA[buf]);
+      _Float16* pb = reinterpret_cast<_Float16*>(sB[buf]);
+#pragma unroll
+      for (int i = 0; i < AL; ++i) {
+        u32x2 h, l;
+        split2h_x4(ra[i] * sa, h, l);
+        const int o = wsw((tid + i * 256) / 4, q4);
+        *reinterpret_cast<u32x2*>(pa + o) = h;
+        *reinterpret_cast<u32x2*>(pa + BM * BK + o) = l;
+      }
+#pragma unroll
+      for (int i = 0; i < BL; ++i) {
+        u32x2 h, l;
+        split2h_x4(rb[i] * sb, h, l);
+        const int o = wsw((tid + i * 256) / 4, q4);
+        *reinterpret_cast<u32x2*>(pb + o) = h;
+        *reinterpret_cast<u32x2*>(pb + BN * BK + o) = l;
+      }
+    } else if constexpr (X6) {
       __bf16* pa = reinterpret_cast<__bf16*>(sA[buf]);
       __bf16* pb = reinterpret_cast<__bf16*>(sB[buf]);
 #pragma unroll
@@ -127,6 +169,11 @@ __global__ __launch_bounds__(256, 2) void convt_gemm_kernel(ConvtGemmArgs g) {
     for (int b = 0; b < 2; ++b)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+  // H3: staging wave of this lane's accumulator rows (per a, r) and columns (per b); the
+  // accumulators' units per staging wave
+  auto wave_a = [&](int a, int r) { return ((wm * 64 + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh) >> 4) & 3; };
+  auto wave_b = [&](int b) { return ((wn * 64 + b * 32 + li) >> 4) & 3; };
+  f32x4 ua = {1.f, 1.f, 1.f, 1.f}, ub = {1.f, 1.f, 1.f, 1.f};
   const int KT = g.K / BK;
   gload(0);
   lstore(0);
@@ -134,7 +181,53 @@ __global__ __launch_bounds__(256, 2) void convt_gemm_kernel(ConvtGemmArgs g) {
   for (int kt = 0; kt < KT; ++kt) {
     const int cur = kt & 1;
     if (kt + 1 < KT) gload((kt + 1) * BK);
-    if constexpr (X6) {
+    if constexpr (H3) {
+      // this K-step's scales; re-express the partial sums in them (exact: powers of two)
+      const f32x4 na = *reinterpret_cast<const f32x4*>(&sscale[cur][0][0]);
+      const f32x4 nb = *reinterpret_cast<const f32x4*>(&sscale[cur][1][0]);
+      if (kt == 0) {
+        ua = na;
+        ub = nb;
+      } else if (na[0] != ua[0] || na[1] != ua[1] || na[2] != ua[2] || na[3] != ua[3] || nb[0] != ub[0] ||
+                 nb[1] != ub[1] || nb[2] != ub[2] || nb[3] != ub[3]) {
+        float fa[4], fb[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          fa[q] = na[q] / ua[q];
+          fb[q] = nb[q] / ub[q];
+        }
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+          for (int b = 0; b < 2; ++b) {
+            const float f = fb[wave_b(b)];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[a][b][r] *= fa[wave_a(a, r)] * f;
+          }
+        ua = na;
+        ub = nb;
+      }
+      const _Float16* pa = reinterpret_cast<const _Float16*>(sA[cur]);
+      const _Float16* pb = reinterpret_cast<const _Float16*>(sB[cur]);
+      f16x8 af[2][2], bf[2][2];  // lane: row li, k = 8 lh .. 8 lh + 7
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+          af[p][a] = *reinterpret_cast<const f16x8*>(pa + p * BM * BK + wsw(wm * 64 + a * 32 + li, 8 * lh));
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+          bf[p][b] = *reinterpret_cast<const f16x8*>(pb + p * BN * BK + wsw(wn * 64 + b * 32 + li, 8 * lh));
+      }
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {  // smallest partial products first
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[1][a], bf[0][b], acc[a][b], 0, 0, 0);
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[0][a], bf[1][b], acc[a][b], 0, 0, 0);
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[0][a], bf[0][b], acc[a][b], 0, 0, 0);
+        }
+    } else if constexpr (X6) {
       const __bf16* pa = reinterpret_cast<const __bf16*>(sA[cur]);
       const __bf16* pb = reinterpret_cast<const __bf16*>(sB[cur]);
       cbf16x8 af[3][2], bf[3][2];  // lane: row li, k = 8 lh .. 8 lh + 7
@@ -209,6 +302,7 @@ __global__ __launch_bounds__(256, 2) void convt_gemm_kernel(ConvtGemmArgs g) {
         const int m = m0 + wm * 64 + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
         if (m >= g.M) continue;
         float v = acc[a][b][r];
+        if constexpr (H3) v = v * (1.f / ua[wave_a(a, r)]) * (1.f / ub[wave_b(b)]);  // exact powers of two
         if (MODE == 0) {
           size_t pix;
           if (rowconst) {
@@ -240,11 +334,13 @@ int launch_convt_gemm(int mode, const float* a, int lda, const float* bt, int B,
   g.K = mode == 0 ? cin : 4 * cout;
   g.bias = bias; g.mask = mask; g.ldm = ldm; g.dst = dst; g.ldd = ldd; g.flags = flags;
   const int grid = (int)(cdiv(g.M, 128) * cdiv(g.N, 128));
-  const bool x6 = tune_get(PIS_TUNE_CONVT_GEMM) == 1;
-  if (mode == 0 && x6) hipLaunchKernelGGL((convt_gemm_kernel<0, true>), dim3(grid), dim3(256), 0, s, g);
-  else if (mode == 0) hipLaunchKernelGGL((convt_gemm_kernel<0, false>), dim3(grid), dim3(256), 0, s, g);
-  else if (x6) hipLaunchKernelGGL((convt_gemm_kernel<1, true>), dim3(grid), dim3(256), 0, s, g);
-  else hipLaunchKernelGGL((convt_gemm_kernel<1, false>), dim3(grid), dim3(256), 0, s, g);
+  const int v = tune_get(PIS_TUNE_CONVT_GEMM), ar = v == 1 ? 1 : v == 3 ? 2 : 0;  // 2 = fp32 MFMA
+  if (mode == 0 && ar == 2) hipLaunchKernelGGL((convt_gemm_kernel<0, 2>), dim3(grid), dim3(256), 0, s, g);
+  else if (mode == 0 && ar == 1) hipLaunchKernelGGL((convt_gemm_kernel<0, 1>), dim3(grid), dim3(256), 0, s, g);
+  else if (mode == 0) hipLaunchKernelGGL((convt_gemm_kernel<0, 0>), dim3(grid), dim3(256), 0, s, g);
+  else if (ar == 2) hipLaunchKernelGGL((convt_gemm_kernel<1, 2>), dim3(grid), dim3(256), 0, s, g);
+  else if (ar == 1) hipLaunchKernelGGL((convt_gemm_kernel<1, 1>), dim3(grid), dim3(256), 0, s, g);
+  else hipLaunchKernelGGL((convt_gemm_kernel<1, 0>), dim3(grid), dim3(256), 0, s, g);
   return launch_status(mode == 0 ? "convt_gemm_fwd" : "convt_gemm_dgrad");
 }
 
