@@ -111,7 +111,11 @@ int pis_version(void);
                                     (tile) and per B row (output channel) for the whole contraction, from maxima the
                                     input / dz / filter transforms write (no in-loop scales; measured slower: GEMM
                                     +10 %, input transform +11 %, step -1.7 %, profiles/r2_q65_*, r2_q66_*) */
-#define PIS_TUNE_NKEYS 24
+#define PIS_TUNE_WINO_PERSIST 24 /* batched fp16x3 Winograd GEMM (key 10 = 4), N % 128 == 0: a persistent kernel (blocks walk
+                                    the tiles as one stream of K-steps) for contractions of C <= 32 x value channels;
+                                    0 (default) never — per layer within +-1 %, the step +0.4 % slower with one shared
+                                    model (profiles/r2_q70_*, r2_q72_*) */
+#define PIS_TUNE_NKEYS 25
 #define PIS_DEBUG_NOLOAD (1 << 16)
 int pis_tune(int key, int value);
 /* Tooling (tools/bench_gemm.py): time one batched NT GEMM kernel variant in isolation,

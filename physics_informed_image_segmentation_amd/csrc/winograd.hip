@@ -1508,6 +1508,183 @@ __global__ __launch_bounds__(256, OCC) void gemm_nt_h3_bk32_kernel(const float* 
 // 2..3 (chunk ^= (row >> 2) & 3), so the 16 rows a ds_read_b128 lane group reads at one chunk
 // hit 16 distinct bank quads: 2 buffers x 3 planes x 384 rows x 64 B = 147 KB.
 
+// The same fp16x3 GEMM as a PERSISTENT kernel (pis_tune key 24): for the short-K, HBM-bound
+// Winograd launches (K = 64..256: 2-8 K-steps per 128 x 128 tile) a block's start-up — its first
+// two K-steps' loads — and its epilogue stores are exposed once per tile. Here each block walks
+// tiles u = block, block + grid, ... of the flattened (xi, m-tile, n-tile) space as ONE stream
+// of K-steps: the loads of step s + 2 (possibly the next tile's first) are in flight while step s
+// computes and while a finished tile's M is stored. Per-wave per-K-step scales as above; a tile's
+// first K-step re-bases the accumulator units.
+template <int BM, int BN, int OCC = 3>
+__global__ __launch_bounds__(256, OCC) void gemm_nt_h3_persist_kernel(const float* __restrict__ A,
+                                                                   const float* __restrict__ Bm,
+                                                                   float* __restrict__ Cm, int M, int N, int K,
+                                                                   int64_t bsA, int64_t bsB, int64_t bsC,
+                                                                   int batches) {
+  constexpr int BK = 32, KP = 32;
+  constexpr int TM = BM / 64, TN = BN / 64;
+  constexpr int AL = BM * 8 / 256, BL = BN * 8 / 256;
+  static_assert(BM % 128 == 0 && BN % 64 == 0, "row r's staging wave must be r / 8 % 4");
+  __shared__ __attribute__((aligned(16))) _Float16 sA[2][BM * KP];
+  __shared__ __attribute__((aligned(16))) _Float16 sB[2][BN * KP];
+  __shared__ __attribute__((aligned(16))) float sscale[2][4];  // [A|B][staging wave]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave & 1, wn = wave >> 1, li = lane & 31, lh = lane >> 5;
+  const int ntn = N / BN, ntm = (M + BM - 1) / BM, per_b = ntm * ntn;
+  const int ntiles = per_b * batches;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x), G = gridDim.x;
+  const int KT = K / BK;  // K % BK == 0 (launcher)
+  const int my_tiles = bid < ntiles ? (ntiles - bid + G - 1) / G : 0;
+  const int nsteps = my_tiles * KT;
+  const int q8 = (tid & 7) * 4;
+  // tile u -> batch, m0, n0 (block-uniform: scalar arithmetic)
+  auto tile_of = [&](int i, int& bt, int& m0, int& n0) {
+    const int u = bid + i * G;
+    bt = u / per_b;
+    const int rem = u - bt * per_b;
+    m0 = (rem / ntn) * BM;
+    n0 = (rem % ntn) * BN;
+  };
+  f32x4 ra[AL], rb[BL];
+  auto gload = [&](int st) {
+    int bt, m0, n0;
+    tile_of(st / KT, bt, m0, n0);
+    const int k = (st % KT) * BK + q8;
+    const float* Ab = A + bt * bsA;
+    const float* Bb = Bm + bt * bsB;
+#pragma unroll
+    for (int i = 0; i < AL; ++i) {
+      const int m = m0 + (tid + i * 256) / 8;
+      ra[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (m < M) ra[i] = *reinterpret_cast<const f32x4*>(Ab + (size_t)m * K + k);
+    }
+#pragma unroll
+    for (int i = 0; i < BL; ++i) {
+      const int n = n0 + (tid + i * 256) / 8;
+      rb[i] = *reinterpret_cast<const f32x4*>(Bb + (size_t)n * K + k);
+    }
+  };
+  float sa = 0.f, sb = 0.f;
+  auto lstore = [&](bool first) {  // first: the tile's first K-step (scales re-chosen)
+    float ma = 0.f, mb = 0.f;
+#pragma unroll
+    for (int i = 0; i < AL; ++i)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) ma = fmaxf(ma, fabsf(ra[i][k]));
+#pragma unroll
+    for (int i = 0; i < BL; ++i)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) mb = fmaxf(mb, fabsf(rb[i][k]));
+    sa = h3_keep(first ? 0.f : sa, wave_max_nonneg(ma));
+    sb = h3_keep(first ? 0.f : sb, wave_max_nonneg(mb));
+    if (lane == 0) {
+      sscale[0][wave] = sa;
+      sscale[1][wave] = sb;
+    }
+#pragma unroll
+    for (int i = 0; i < AL; ++i) {
+      u32x2 h, l;
+      split2h_x4(ra[i] * sa, h, l);
+      const int row = (tid + i * 256) / 8, o = x6w8_off(row, q8 >> 3) + (q8 & 7);
+      *reinterpret_cast<u32x2*>(&sA[0][o]) = h;
+      *reinterpret_cast<u32x2*>(&sA[1][o]) = l;
+    }
+#pragma unroll
+    for (int i = 0; i < BL; ++i) {
+      u32x2 h, l;
+      split2h_x4(rb[i] * sb, h, l);
+      const int row = (tid + i * 256) / 8, o = x6w8_off(row, q8 >> 3) + (q8 & 7);
+      *reinterpret_cast<u32x2*>(&sB[0][o]) = h;
+      *reinterpret_cast<u32x2*>(&sB[1][o]) = l;
+    }
+  };
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int b = 0; b < TN; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+  if (nsteps == 0) return;  // block-uniform: no barrier is skipped by part of a block
+  gload(0);
+  lstore(true);
+  if (nsteps > 1) gload(1);
+  __syncthreads();
+  f32x4 ua = {1.f, 1.f, 1.f, 1.f};
+  float ub = 1.f;
+  for (int st = 0; st < nsteps; ++st) {
+    const int kt = st % KT;
+    {
+      const f32x4 na = *reinterpret_cast<const f32x4*>(&sscale[0][0]);
+      const float nb = sscale[1][(li >> 3) & 3];
+      if (kt == 0) {
+        ua = na;
+        ub = nb;
+      } else if (na[0] != ua[0] || na[1] != ua[1] || na[2] != ua[2] || na[3] != ua[3] || nb != ub) {
+        const float rb_ = nb / ub;
+        float f[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) f[q] = na[q] / ua[q] * rb_;
+#pragma unroll
+        for (int a = 0; a < TM; ++a)
+#pragma unroll
+          for (int b = 0; b < TN; ++b)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[a][b][r] *= f[r >> 2];
+        ua = na;
+        ub = nb;
+      }
+    }
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      f16x8 af[2][TM], bf[2][TN];
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+#pragma unroll
+        for (int a = 0; a < TM; ++a)
+          af[p][a] = *reinterpret_cast<const f16x8*>(&sA[p][x6w8_off(wm * (BM / 2) + a * 32 + li, 2 * ks + lh)]);
+#pragma unroll
+        for (int b = 0; b < TN; ++b)
+          bf[p][b] = *reinterpret_cast<const f16x8*>(&sB[p][x6w8_off(wn * (BN / 2) + b * 32 + li, 2 * ks + lh)]);
+      }
+#pragma unroll
+      for (int a = 0; a < TM; ++a)
+#pragma unroll
+        for (int b = 0; b < TN; ++b) {
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[1][a], bf[0][b], acc[a][b], 0, 0, 0);
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[0][a], bf[1][b], acc[a][b], 0, 0, 0);
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[0][a], bf[0][b], acc[a][b], 0, 0, 0);
+        }
+    }
+    if (kt == KT - 1) {  // tile done: store it (the next steps' loads are already in flight)
+      int bt, m0, n0;
+      tile_of(st / KT, bt, m0, n0);
+      float* Cb = Cm + bt * bsC;
+      float inv[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) inv[q] = 1.f / (ua[q] * ub);
+#pragma unroll
+      for (int a = 0; a < TM; ++a)
+#pragma unroll
+        for (int b = 0; b < TN; ++b) {
+          const int n = n0 + wn * (BN / 2) + b * 32 + li;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int m = m0 + wm * (BM / 2) + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+            if (m < M) Cb[(size_t)m * N + n] = acc[a][b][r] * inv[r >> 2];
+            acc[a][b][r] = 0.f;
+          }
+        }
+    }
+    if (st + 1 < nsteps) {
+      __syncthreads();
+      lstore((st + 1) % KT == 0);
+      __syncthreads();
+      if (st + 2 < nsteps) gload(st + 2);
+    }
+  }
+}
+
 template <int DBG = 0>
 __global__ __launch_bounds__(512, 1) void gemm_nt_x6_w8_kernel(const float* __restrict__ A,
                                                                const float* __restrict__ Bm, float* __restrict__ Cm,
@@ -2117,7 +2294,14 @@ int launch_wino3x3(const IGemmArgs& a, int B, void* ws, hipStream_t s, float* ke
     rc = launch_status("wino_gemm");
   } else if (v == 4 && N % 64 == 0 && C % 32 == 0) {
     // fp16x3 with per-K-step power-of-two tile scales (gemm_nt_h3_bk32_kernel)
-    if (N % 128 == 0) {
+    const int pk = tune_get(PIS_TUNE_WINO_PERSIST);
+    if (!pre && pk > 0 && C <= 32 * pk && N % 128 == 0) {
+      // persistent: a few resident waves of blocks walk every tile (short-K launches)
+      const int64_t tiles = cdiv(T, 128) * (N / 128) * nxi;
+      const int grid = (int)std::min<int64_t>(tiles, 256 * 3 * 2);
+      hipLaunchKernelGGL((gemm_nt_h3_persist_kernel<128, 128, 3>), dim3(grid), dim3(256), 0, s, V, U, Mt, (int)T,
+                         N, C, T * C, (int64_t)N * C, T * N, nxi);
+    } else if (N % 128 == 0) {
       const dim3 grid((int)cdiv(T, 128) * (N / 128), nxi);
       if (pre)
         hipLaunchKernelGGL((gemm_nt_h3_bk32_kernel<128, 128, 3, true, true>), grid, dim3(256), 0, s, V, U, Mt,

@@ -1,7 +1,7 @@
 """A/B of pis_tune settings on the C2 training step, interleaved rounds in one process on one
 GPU (box-to-box variance is ~3 %; same-process interleaving is not).
 
-    python tools/ab_tune.py --variants "base;20=0;15=0,17=4" [--rounds 4] [--steps 10]
+    python tools/ab_tune.py --variants "base;20=0;15=0,17=4" [--rounds 4] [--steps 10] [--shared]
 
 Each variant is a comma list of KEY=VALUE (include/pis_capi.h PIS_TUNE_*); "base" = defaults;
 "fa=0|1|2" plans that variant's engine with PIS_FILTER_AHEAD = that value (unet.py).
@@ -29,6 +29,9 @@ def main():
     ap.add_argument("--variants", required=True)
     ap.add_argument("--rounds", type=int, default=4)
     ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--shared", action="store_true",
+                    help="one model (planned with the defaults) for every variant: for knobs that do not change "
+                         "the engine's plan; removes the 2-3 %% placement effect of separately allocated models")
     args = ap.parse_args()
     lib = _hip.lib()
     variants = [(v.strip(), parse(v)) for v in args.variants.split(";")]
@@ -47,7 +50,10 @@ def main():
     # one model (and engine plan: workspaces depend on the knobs) per variant, same seed
     models = {}
     for name, kv in variants:
-        setv(kv)
+        if args.shared and models:
+            models[name] = next(iter(models.values()))
+            continue
+        setv({} if args.shared else kv)
         torch.manual_seed(42)
         m = UNet(1, 1, 64).to(dev).train()
         models[name] = (m, AdamW(m.parameters(), lr=1e-5, weight_decay=1e-5))
