@@ -115,7 +115,9 @@ int pis_version(void);
                                     the tiles as one stream of K-steps) for contractions of C <= 32 x value channels;
                                     0 (default) never — per layer within +-1 %, the step +0.4 % slower with one shared
                                     model (profiles/r2_q70_*, r2_q72_*) */
-#define PIS_TUNE_NKEYS 25
+#define PIS_TUNE_FUSED_STAGGER 25 /* fused 64 -> 64 kernel in fp16x3 (key 22): 1 the SIMD-partner waves fold one xi late
+                                     (stagger; bit-for-bit the same), 0 (default) all waves in lockstep */
+#define PIS_TUNE_NKEYS 26
 #define PIS_DEBUG_NOLOAD (1 << 16)
 int pis_tune(int key, int value);
 /* Tooling (tools/bench_gemm.py): time one batched NT GEMM kernel variant in isolation,

@@ -1831,7 +1831,11 @@ typedef __bf16 bf16x8g __attribute__((ext_vector_type(8)));
 // Elements more than 2^16 below their tile's max keep an absolute error <= 2^-37 of that max,
 // far below the fp32 transform's own rounding (~2^-24 of the patch max). One chain of three fp16
 // products (lo hi, hi lo, hi hi) per K-step: two thirds of the LDS operand reads, half the MFMAs.
-template <int NWN, int NWT, int KC, int G = 1, bool H3 = false>
+// STG (pis_tune key 25): the second half of the waves (wt = 1: the SIMD partners of waves 0-3)
+// fold each xi's product one xi late, keeping it in registers across the barrier (a stagger,
+// MI355X_MICROARCH.md 'Two waves that run the SAME program with one barrier per block'): the
+// partners' MFMA and fold phases no longer coincide. Bit-for-bit the same sums in the same order.
+template <int NWN, int NWT, int KC, int G = 1, bool H3 = false, bool STG = false>
 __global__ __launch_bounds__(64 * NWN * NWT) void wino4_gemm_out_x6_kernel(const float* __restrict__ V,
                                                                           const __bf16* __restrict__ Up,
                                                                           IGemmArgs g, int B,
@@ -1946,13 +1950,31 @@ __global__ __launch_bounds__(64 * NWN * NWT) void wino4_gemm_out_x6_kernel(const
     const int64_t t0 = (grp0 + gi) * TB;
     const float* vb = V + t0 * KC;
     asm volatile("" : "+s"(Ug), "+s"(TK), "+s"(NK), "+v"(tid));
-    f32x4 y[4][4], rr[4];
+    f32x4 y[4][4], rr[4], accp = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       rr[i] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int j = 0; j < 4; ++j) y[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
+    const bool late = STG && wt == 1;  // wave-uniform
+    // Y[i][j] += AT[i][ra] R[j], then R = 0 (ra: the grid row whose six products R holds)
+    auto rowend = [&](int ra) {
+      float at[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float v = 0.f;
+#pragma unroll
+        for (int q = 0; q < 6; ++q) v = ra == q ? w4_at(i, q) : v;
+        at[i] = v;
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) y[i][j] += at[i] * rr[j];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) rr[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    };
 #pragma unroll
     for (int a = 0; a < 6; ++a) {  // fully unrolled: the compiler keeps exact vmcnt counts across rows
 #pragma unroll
@@ -1990,8 +2012,17 @@ __global__ __launch_bounds__(64 * NWN * NWT) void wino4_gemm_out_x6_kernel(const
           acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0], bf[1], acc, 0, 0, 0);
           acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0], bf[0], acc, 0, 0, 0);
         }
+        if (!late) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) axpy_c(rr[j], w4_at(j, b), acc);
+          for (int j = 0; j < 4; ++j) axpy_c(rr[j], w4_at(j, b), acc);
+        } else {  // fold the previous xi's product (column b - 1, or the previous row's last)
+          if (xi > 0) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) axpy_c(rr[j], w4_at(j, (b + 5) % 6), accp);
+            if (b == 0) rowend(a - 1);
+          }
+          accp = acc;
+        }
         // stage xi + 1 (V from its ring slot, U from the register pair), then refill both
         const int vslot = (b + 1) % RING;
         if (xi + 1 < 36) {
@@ -2003,20 +2034,12 @@ __global__ __launch_bounds__(64 * NWN * NWT) void wino4_gemm_out_x6_kernel(const
         __syncthreads();
       }
       // Y[i][j] += AT[i][a] R[j] (a is a runtime row index: coefficients selected from the table)
-      float at[4];
+      if (!late) rowend(a);
+    }
+    if (late) {  // the last product
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        float v = 0.f;
-#pragma unroll
-        for (int q = 0; q < 6; ++q) v = a == q ? w4_at(i, q) : v;
-        at[i] = v;
-      }
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) y[i][j] += at[i] * rr[j];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) rr[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < 4; ++j) axpy_c(rr[j], w4_at(j, 5), accp);
+      rowend(5);
     }
     const bool more = gi + 1 < G;
     if (more) {
@@ -2169,7 +2192,10 @@ static int launch_wino_gemm_out(const float* V, const __bf16* Up, const IGemmArg
   const int mode = tune_get(PIS_TUNE_WINO_GEMM_OUT);
   const int G = mode == 2 ? 1 : mode == 3 ? 2 : mode == 4 ? 8 : 4;
   const dim3 blk(512);
-  if (wino_gemm_out_h3()) {
+  if (wino_gemm_out_h3() && tune_get(PIS_TUNE_FUSED_STAGGER) != 0 && groups % 4 == 0) {
+    hipLaunchKernelGGL((wino4_gemm_out_x6_kernel<4, 2, 64, 4, true, true>), dim3((int)(groups / 4)), blk, 0, s, V, Up,
+                       a, B, tmax);
+  } else if (wino_gemm_out_h3()) {
     if (G == 8 && groups % 8 == 0)
       hipLaunchKernelGGL((wino4_gemm_out_x6_kernel<4, 2, 64, 8, true>), dim3((int)(groups / 8)), blk, 0, s, V, Up, a,
                          B, tmax);

@@ -105,7 +105,7 @@ def test_conv3x3_dgrad_wgrad(hip, B, H, W, Cin, Cout):
 
 # every non-default kernel variant behind pis_tune (include/pis_capi.h) stays exact too
 TUNE_VARIANTS = [(4, 1), (4, 2), (4, 3), (5, 0), (6, 2048), (3, 0), (7, 1), (8, 0), (8, 2), (10, 0), (10, 1),
-                 (11, 0), (12, 0), (12, 2), (13, 0), (13, 1), (13, 2), (10, 2), (10, 3), (14, 0), (14, 1), (14, 2), (15, 0), (16, 0), (17, 4), (22, 0), (23, 1), (24, 32)]
+                 (11, 0), (12, 0), (12, 2), (13, 0), (13, 1), (13, 2), (10, 2), (10, 3), (14, 0), (14, 1), (14, 2), (15, 0), (16, 0), (17, 4), (22, 0), (23, 1), (24, 32), (25, 1)]
 
 
 @pytest.mark.parametrize("key,value", TUNE_VARIANTS)
@@ -704,8 +704,8 @@ def test_convt_bf16x6_is_fp32_accurate(hip, Cin, Cout):
 @pytest.mark.parametrize("B,H,W", [(2, 32, 64), (1, 16, 128), (3, 32, 32)])
 def test_fused_64_groups_per_block_bitwise(hip, B, H, W):
     """The fused 64->64 contraction + output transform takes G groups of 32 tiles per block
-    (pis_tune key 15: 1 -> G = 4 where the group count divides, 2 -> 1, 3 -> 2, 4 -> 8): every G
-    gives bit-for-bit the same forward (ReLU, keep-scale, fused max pool) and input gradient
+    (pis_tune key 15: 1 -> G = 4 where the group count divides, 2 -> 1, 3 -> 2, 4 -> 8), with and
+    without the staggered fold (key 25): every variant gives bit-for-bit the same forward (ReLU, keep-scale, fused max pool) and input gradient
     (ReLU mask, keep-scale, accumulate), and G = 1 matches the float64 reference."""
     Cin = Cout = 64
     g = torch.Generator().manual_seed(31)
@@ -719,11 +719,12 @@ def test_fused_64_groups_per_block_bitwise(hip, B, H, W):
     ws = torch.empty(nws // 4 + 1, device="cuda")
     wf = torch.empty(Cin * 9 * Cout, device="cuda")
     assert hip.pis_conv3x3_flip(wd.data_ptr(), wf.data_ptr(), Cin, Cout, s()) == 0
-    prev = hip.pis_tune(15, -1)
+    prev, prev25 = hip.pis_tune(15, -1), hip.pis_tune(25, -1)
     out = {}
     try:
-        for v in (2, 1, 3, 4):
-            hip.pis_tune(15, v)
+        for v in (2, 1, 3, 4, "stagger"):
+            hip.pis_tune(15, 1 if v == "stagger" else v)
+            hip.pis_tune(25, 1 if v == "stagger" else 0)
             y = torch.empty(B, H, W, Cout, device="cuda")
             pool = torch.empty(B, H // 2, W // 2, Cout, device="cuda")
             rc = hip.pis_conv3x3_fwd_pool(xd.data_ptr(), Cin, wd.data_ptr(), bd.data_ptr(), sd.data_ptr(),
@@ -739,7 +740,8 @@ def test_fused_64_groups_per_block_bitwise(hip, B, H, W):
             out[v] = (y.cpu(), pool.cpu(), dx.cpu())
     finally:
         hip.pis_tune(15, prev)
-    for v in (1, 3, 4):
+        hip.pis_tune(25, prev25)
+    for v in (1, 3, 4, "stagger"):
         for a, c in zip(out[2], out[v]):
             assert torch.equal(a, c), v
     y_ref = F.relu(F.conv2d(x.double(), w.double(), b.double(), padding=1)) * scale[:, :, None, None]
