@@ -117,7 +117,10 @@ int pis_version(void);
                                     model (profiles/r2_q70_*, r2_q72_*) */
 #define PIS_TUNE_FUSED_STAGGER 25 /* fused 64 -> 64 kernel in fp16x3 (key 22): 1 the SIMD-partner waves fold one xi late
                                      (stagger; bit-for-bit the same), 0 (default) all waves in lockstep */
-#define PIS_TUNE_NKEYS 26
+#define PIS_TUNE_FUSED_WIDE 26   /* 1 (default): the fused contraction + output transform (key 15) also for 64 -> 128
+                                    channels (two 64-channel blocks per tile group, V read twice from L2, M never
+                                    written: enc2.conv0 forward -21 %, dec1.conv0 input gradient -20 %); 0: 64 -> 64 only */
+#define PIS_TUNE_NKEYS 27
 #define PIS_DEBUG_NOLOAD (1 << 16)
 int pis_tune(int key, int value);
 /* Tooling (tools/bench_gemm.py): time one batched NT GEMM kernel variant in isolation,

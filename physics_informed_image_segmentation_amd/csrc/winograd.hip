@@ -1870,10 +1870,24 @@ __global__ __launch_bounds__(64 * NWN * NWT) void wino4_gemm_out_x6_kernel(const
   const int lane = tid & 63, wave = tid >> 6;
   const int wn = wave % NWN, wt = wave / NWN;
   const int lr = lane & 15, lq = lane >> 4;
-  const int n = 16 * wn + lr;  // this lane's output channel
+  const int n = 16 * wn + lr;  // this lane's output channel within the block's NN
+  // N > NN (pis_tune key 26): nblk blocks share a tile group, one NN-channel slice each, dealt
+  // so that they sit 8 apart in dispatch order (one XCD, back to back: V comes from its L2)
+  const int nblk = N / NN;
+  int gblk = blockIdx.x, nb = 0;
+  if (nblk > 1) {
+    if ((gridDim.x / nblk) % 8 == 0) {
+      gblk = (blockIdx.x / (8 * nblk)) * 8 + blockIdx.x % 8;
+      nb = (blockIdx.x / 8) % nblk;
+    } else {
+      gblk = blockIdx.x / nblk;
+      nb = blockIdx.x % nblk;
+    }
+  }
+  const int n0 = nb * NN;
   // G consecutive groups of TB tiles per block: the next group's first V and U loads are issued
   // before this group's epilogue, so their latency hides behind its stores
-  const int64_t grp0 = (int64_t)blockIdx.x * G;
+  const int64_t grp0 = (int64_t)gblk * G;
   f32x4 vr[RING][AL];
   auto gload = [&](const float* vb, int xi, f32x4 (&r)[AL]) {
 #pragma unroll
@@ -1908,7 +1922,7 @@ __global__ __launch_bounds__(64 * NWN * NWT) void wino4_gemm_out_x6_kernel(const
     for (int i = 0; i < UL; ++i) {
       const int c = tid + i * NT;  // (plane, channel, 8-k chunk), k fastest: contiguous per plane
       const int pl = c / (NN * KC / 8), rem = c % (NN * KC / 8);
-      ur[slot][i] = *reinterpret_cast<const u32x4*>(Ug + (pl * 36 + xi) * NK + 8 * rem);
+      ur[slot][i] = *reinterpret_cast<const u32x4*>(Ug + (pl * 36 + xi) * NK + n0 * KC + 8 * rem);
     }
   };
   auto ustore = [&](int buf, int slot) {
@@ -2048,7 +2062,7 @@ __global__ __launch_bounds__(64 * NWN * NWT) void wino4_gemm_out_x6_kernel(const
     }
     if constexpr (H3) {
       // Y is in units s_t t_n: divide (exact powers of two, one factor at a time)
-      const float inv_t = reinterpret_cast<const float*>(Up + 2 * 36 * (int64_t)N * KC)[n];
+      const float inv_t = reinterpret_cast<const float*>(Up + 2 * 36 * (int64_t)N * KC)[n0 + n];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         float sc, inv_s;
@@ -2072,7 +2086,7 @@ __global__ __launch_bounds__(64 * NWN * NWT) void wino4_gemm_out_x6_kernel(const
     int et = tid;  // laundered: the epilogue's index math stays out of the group loop's registers
     asm volatile("" : "+v"(et));
     const int c4 = et % (NN / 4), pq = et / (NN / 4);
-    const int tl = pq / 4, quad = pq % 4, qi = quad >> 1, qj = quad & 1, nn = 4 * c4;
+    const int tl = pq / 4, quad = pq % 4, qi = quad >> 1, qj = quad & 1, nl = 4 * c4, nn = n0 + nl;
     size_t pix0[4], pp[4];  // the quad's first pixel; its pooled pixel
     int bq[4];
     f32x4 mk[4][2][2];
@@ -2105,7 +2119,7 @@ __global__ __launch_bounds__(64 * NWN * NWT) void wino4_gemm_out_x6_kernel(const
 #pragma unroll
         for (int dj = 0; dj < 2; ++dj) {
           const int i = 2 * qi + di, j = 2 * qj + dj;
-          const f32x4 v = *reinterpret_cast<const f32x4*>(&E[q * EQ + (tl * 16 + 4 * i + j) * EP + nn]);
+          const f32x4 v = *reinterpret_cast<const f32x4*>(&E[q * EQ + (tl * 16 + 4 * i + j) * EP + nl]);
           o[di][dj] = conv_epilogue4m(g, pix0[q] + di * g.W + dj, nn, v + bias4, sc4, mk[q][di][dj]);
         }
       if (g.pool) *reinterpret_cast<f32x4*>(g.pool + pp[q] * N + nn) = max4(o[0][0], o[0][1], o[1][0], o[1][1]);
@@ -2179,9 +2193,11 @@ static bool wino_gemm_out_h3() { return tune_get(PIS_TUNE_WINO_GEMM_OUT_H3) != 0
 // 1.30 -> 1.13 ms; with 128 input or output channels (dec1.conv0, enc2.conv0) it is 2-8 % slower
 // than the separate GEMM + output transform, so those keep the 3-pass pipeline.
 static bool wino_gemm_out_wanted(int m, int64_t T, int C, int N) {
+  // N = 128 (64-channel contractions into 128 outputs: enc2.conv0 forward, dec1.conv0 input
+  // gradient) with pis_tune key 26: two blocks per tile group, V read twice (from L2), M never
   return m == 4 && tune_get(PIS_TUNE_WINO_GEMM_OUT) != 0 && tune_get(PIS_TUNE_WINO_TILE) >= 3 && T % 32 == 0 &&
          T >= 2 * (int64_t)C &&  // the filter planes fit in the M region
-         N == 64 && C == 64;
+         C == 64 && (N == 64 || (N == 128 && tune_get(PIS_TUNE_FUSED_WIDE) != 0));
 }
 
 static int launch_wino_gemm_out(const float* V, const __bf16* Up, const IGemmArgs& a, int B, int64_t T,
@@ -2189,32 +2205,33 @@ static int launch_wino_gemm_out(const float* V, const __bf16* Up, const IGemmArg
   // 8 waves: 32 tiles x 64 channels per block; G such groups per block where they divide
   // (pis_tune key 15: 1 -> G = 4, 2 -> 1, 3 -> 2, 4 -> 8: experiments)
   const int64_t groups = T / 32;
+  const int nblk = a.N / 64;  // 64-channel slices (pis_tune key 26: N = 128 too)
   const int mode = tune_get(PIS_TUNE_WINO_GEMM_OUT);
   const int G = mode == 2 ? 1 : mode == 3 ? 2 : mode == 4 ? 8 : 4;
   const dim3 blk(512);
   if (wino_gemm_out_h3() && tune_get(PIS_TUNE_FUSED_STAGGER) != 0 && groups % 4 == 0) {
-    hipLaunchKernelGGL((wino4_gemm_out_x6_kernel<4, 2, 64, 4, true, true>), dim3((int)(groups / 4)), blk, 0, s, V, Up,
+    hipLaunchKernelGGL((wino4_gemm_out_x6_kernel<4, 2, 64, 4, true, true>), dim3((int)(groups / 4) * nblk), blk, 0, s, V, Up,
                        a, B, tmax);
   } else if (wino_gemm_out_h3()) {
     if (G == 8 && groups % 8 == 0)
-      hipLaunchKernelGGL((wino4_gemm_out_x6_kernel<4, 2, 64, 8, true>), dim3((int)(groups / 8)), blk, 0, s, V, Up, a,
+      hipLaunchKernelGGL((wino4_gemm_out_x6_kernel<4, 2, 64, 8, true>), dim3((int)(groups / 8) * nblk), blk, 0, s, V, Up, a,
                          B, tmax);
     else if (G == 4 && groups % 4 == 0)
-      hipLaunchKernelGGL((wino4_gemm_out_x6_kernel<4, 2, 64, 4, true>), dim3((int)(groups / 4)), blk, 0, s, V, Up, a,
+      hipLaunchKernelGGL((wino4_gemm_out_x6_kernel<4, 2, 64, 4, true>), dim3((int)(groups / 4) * nblk), blk, 0, s, V, Up, a,
                          B, tmax);
     else if (G == 2 && groups % 2 == 0)
-      hipLaunchKernelGGL((wino4_gemm_out_x6_kernel<4, 2, 64, 2, true>), dim3((int)(groups / 2)), blk, 0, s, V, Up, a,
+      hipLaunchKernelGGL((wino4_gemm_out_x6_kernel<4, 2, 64, 2, true>), dim3((int)(groups / 2) * nblk), blk, 0, s, V, Up, a,
                          B, tmax);
     else
-      hipLaunchKernelGGL((wino4_gemm_out_x6_kernel<4, 2, 64, 1, true>), dim3((int)groups), blk, 0, s, V, Up, a, B, tmax);
+      hipLaunchKernelGGL((wino4_gemm_out_x6_kernel<4, 2, 64, 1, true>), dim3((int)groups * nblk), blk, 0, s, V, Up, a, B, tmax);
   } else if (G == 8 && groups % 8 == 0)
-    hipLaunchKernelGGL((wino4_gemm_out_x6_kernel<4, 2, 64, 8>), dim3((int)(groups / 8)), blk, 0, s, V, Up, a, B, nullptr);
+    hipLaunchKernelGGL((wino4_gemm_out_x6_kernel<4, 2, 64, 8>), dim3((int)(groups / 8) * nblk), blk, 0, s, V, Up, a, B, nullptr);
   else if (G == 4 && groups % 4 == 0)
-    hipLaunchKernelGGL((wino4_gemm_out_x6_kernel<4, 2, 64, 4>), dim3((int)(groups / 4)), blk, 0, s, V, Up, a, B, nullptr);
+    hipLaunchKernelGGL((wino4_gemm_out_x6_kernel<4, 2, 64, 4>), dim3((int)(groups / 4) * nblk), blk, 0, s, V, Up, a, B, nullptr);
   else if (G == 2 && groups % 2 == 0)
-    hipLaunchKernelGGL((wino4_gemm_out_x6_kernel<4, 2, 64, 2>), dim3((int)(groups / 2)), blk, 0, s, V, Up, a, B, nullptr);
+    hipLaunchKernelGGL((wino4_gemm_out_x6_kernel<4, 2, 64, 2>), dim3((int)(groups / 2) * nblk), blk, 0, s, V, Up, a, B, nullptr);
   else
-    hipLaunchKernelGGL((wino4_gemm_out_x6_kernel<4, 2, 64, 1>), dim3((int)groups), blk, 0, s, V, Up, a, B, nullptr);
+    hipLaunchKernelGGL((wino4_gemm_out_x6_kernel<4, 2, 64, 1>), dim3((int)groups * nblk), blk, 0, s, V, Up, a, B, nullptr);
   return launch_status("wino_gemm_out");
 }
 

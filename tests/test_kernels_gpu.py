@@ -105,7 +105,7 @@ def test_conv3x3_dgrad_wgrad(hip, B, H, W, Cin, Cout):
 
 # every non-default kernel variant behind pis_tune (include/pis_capi.h) stays exact too
 TUNE_VARIANTS = [(4, 1), (4, 2), (4, 3), (5, 0), (6, 2048), (3, 0), (7, 1), (8, 0), (8, 2), (10, 0), (10, 1),
-                 (11, 0), (12, 0), (12, 2), (13, 0), (13, 1), (13, 2), (10, 2), (10, 3), (14, 0), (14, 1), (14, 2), (15, 0), (16, 0), (17, 4), (22, 0), (23, 1), (24, 32), (25, 1)]
+                 (11, 0), (12, 0), (12, 2), (13, 0), (13, 1), (13, 2), (10, 2), (10, 3), (14, 0), (14, 1), (14, 2), (15, 0), (16, 0), (17, 4), (22, 0), (23, 1), (24, 32), (25, 1), (26, 0)]
 
 
 @pytest.mark.parametrize("key,value", TUNE_VARIANTS)
@@ -119,7 +119,8 @@ def test_conv3x3_tuned_variants(hip, key, value):
         test_conv3x3_c1_wgrad(hip)
         for shape in [(2, 8, 12, 128, 64), (1, 16, 32, 256, 128)]:
             test_convt2x2(hip, *shape)
-        for shape in [(2, 8, 8, 256, 256, 2), (1, 6, 10, 132, 64, 2)]:
+        for shape in [(2, 8, 8, 256, 256, 2), (1, 6, 10, 132, 64, 2), (2, 32, 64, 64, 128, 1),
+                      (2, 32, 64, 128, 64, 1)]:
             test_conv3x3_ex_winograd(hip, *shape)
     finally:
         hip.pis_tune(key, prev)
@@ -801,7 +802,7 @@ def test_fused_64_fp16x3_is_fp32_accurate(hip):
 
 
 @pytest.mark.parametrize("B,H,W,Cin,Cout", [(2, 32, 64, 64, 64), (2, 16, 32, 128, 128), (1, 32, 32, 128, 64),
-                                           (2, 16, 16, 256, 256)])
+                                           (2, 16, 16, 256, 256), (2, 32, 64, 128, 64)])
 def test_conv3x3_bwd_prep(hip, B, H, W, Cin, Cout):
     """pis_conv3x3_bwd_prep: one pass over dz writes both backward transforms; the dgrad_ex and
     wgrad_keep calls that then pass PIS_WINO_PREPARED give the same results as without it (and
