@@ -120,7 +120,11 @@ int pis_version(void);
 #define PIS_TUNE_FUSED_WIDE 26   /* 1 (default): the fused contraction + output transform (key 15) also for 64 -> 128
                                     channels (two 64-channel blocks per tile group, V read twice from L2, M never
                                     written: enc2.conv0 forward -21 %, dec1.conv0 input gradient -20 %); 0: 64 -> 64 only */
-#define PIS_TUNE_NKEYS 27
+#define PIS_TUNE_FUSED_K128 27   /* 1 (default): the fused contraction + output transform also for 128-channel
+                                    contractions (128 -> 64, and 128 -> 128 with key 26; the SIMD-partner waves always
+                                    staggered: dec1.conv0 forward -11 %, enc2.conv0 input gradient -15 %);
+                                    0: 64-channel contractions only */
+#define PIS_TUNE_NKEYS 28
 #define PIS_DEBUG_NOLOAD (1 << 16)
 int pis_tune(int key, int value);
 /* Tooling (tools/bench_gemm.py): time one batched NT GEMM kernel variant in isolation,

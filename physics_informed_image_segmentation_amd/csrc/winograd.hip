@@ -409,20 +409,19 @@ __global__ __launch_bounds__(256) void wino4_filter_rot_kernel(const float* __re
   wino4_filter_rot_tile(w, N, C, U, transposed, Up, blockIdx.x, umax);
 }
 
-// The fused kernel's fp16x3 filter planes (pis_tune key 22), C == 64: one wave per output channel
-// n, lane c. All 36 U[xi][n][c] of the channel share ONE power-of-two scale t_n (from their max
-// over xi and c): Uh[p][xi][n][c] = hi / lo fp16 of u t_n, then Us[n] = 1 / t_n after the planes.
-// dgrad: the input-gradient filter straight from the original KRSC weights [C][9][N] (rotated,
-// transposed; as wino4_filter_rot_tile), else w is [N][9][C] with row pitch ldw.
-__device__ __forceinline__ void wino4_filter_h2_wave(const float* __restrict__ w, int ldw, int N, int dgrad,
-                                                     __bf16* __restrict__ Up, int n) {
-  constexpr int C = 64;
-  const int c = threadIdx.x & 63;
+// The fused kernel's fp16x3 filter planes (pis_tune key 22), C % 64 == 0: one wave per output
+// channel n, lane c (+ 64 j). All 36 C U[xi][n][c] of the channel share ONE power-of-two scale t_n
+// (from their max over xi and c; a first pass finds it, the second recomputes and writes):
+// Uh[p][xi][n][c] = hi / lo fp16 of u t_n, then Us[n] = 1 / t_n after the planes. dgrad: the
+// input-gradient filter straight from the original KRSC weights [C][9][N] (rotated, transposed;
+// as wino4_filter_rot_tile), else w is [N][9][C] with row pitch ldw.
+__device__ __forceinline__ void wino4_filter_h2_u(const float* __restrict__ w, int ldw, int N, int C, int dgrad,
+                                                  int n, int c, float (&u)[36]) {
   float g[3][3];
 #pragma unroll
   for (int t = 0; t < 9; ++t)
     g[t / 3][t % 3] = dgrad ? w[((size_t)c * 9 + 8 - t) * N + n] : w[(size_t)n * ldw + t * C + c];
-  float gg[6][3], u[36];
+  float gg[6][3];
 #pragma unroll
   for (int i = 0; i < 6; ++i)
 #pragma unroll
@@ -431,7 +430,6 @@ __device__ __forceinline__ void wino4_filter_h2_wave(const float* __restrict__ w
 #pragma unroll
       for (int k = 0; k < 3; ++k) axpy_c(gg[i][s], w4_g(i, k), g[k][s]);
     }
-  float m = 0.f;
 #pragma unroll
   for (int i = 0; i < 6; ++i)
 #pragma unroll
@@ -440,28 +438,42 @@ __device__ __forceinline__ void wino4_filter_h2_wave(const float* __restrict__ w
 #pragma unroll
       for (int s = 0; s < 3; ++s) axpy_c(v, w4_g(j, s), gg[i][s]);
       u[6 * i + j] = v;
-      m = fmaxf(m, fabsf(v));
     }
+}
+
+__device__ __forceinline__ void wino4_filter_h2_wave(const float* __restrict__ w, int ldw, int N, int C, int dgrad,
+                                                     __bf16* __restrict__ Up, int n) {
+  const int lane = threadIdx.x & 63;
+  float u[36];
+  float m = 0.f;
+  for (int c = lane; c < C; c += 64) {
+    wino4_filter_h2_u(w, ldw, N, C, dgrad, n, c, u);
+#pragma unroll
+    for (int xi = 0; xi < 36; ++xi) m = fmaxf(m, fabsf(u[xi]));
+  }
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off, 64));
   float sc, inv;
   h2_scale_pair(m, sc, inv);
   _Float16* Uh = reinterpret_cast<_Float16*>(Up);
   const size_t NC = (size_t)N * C;
+  for (int c = lane; c < C; c += 64) {
+    wino4_filter_h2_u(w, ldw, N, C, dgrad, n, c, u);
 #pragma unroll
-  for (int xi = 0; xi < 36; ++xi) {
-    const float us = u[xi] * sc;
-    const _Float16 h = (_Float16)us;
-    const size_t o = xi * NC + (size_t)n * C + c;
-    Uh[o] = h;
-    Uh[36 * NC + o] = (_Float16)(us - (float)h);
+    for (int xi = 0; xi < 36; ++xi) {
+      const float us = u[xi] * sc;
+      const _Float16 h = (_Float16)us;
+      const size_t o = xi * NC + (size_t)n * C + c;
+      Uh[o] = h;
+      Uh[36 * NC + o] = (_Float16)(us - (float)h);
+    }
   }
-  if (c == 0) reinterpret_cast<float*>(Uh + 72 * NC)[n] = inv;
+  if (lane == 0) reinterpret_cast<float*>(Uh + 72 * NC)[n] = inv;
 }
 
-__global__ __launch_bounds__(256) void wino4_filter_h2_kernel(const float* __restrict__ w, int ldw, int N, int dgrad,
-                                                              __bf16* __restrict__ Up) {
-  wino4_filter_h2_wave(w, ldw, N, dgrad, Up, 4 * blockIdx.x + (threadIdx.x >> 6));
+__global__ __launch_bounds__(256) void wino4_filter_h2_kernel(const float* __restrict__ w, int ldw, int N, int C,
+                                                              int dgrad, __bf16* __restrict__ Up) {
+  wino4_filter_h2_wave(w, ldw, N, C, dgrad, Up, 4 * blockIdx.x + (threadIdx.x >> 6));
 }
 
 // Many layers' filter transforms in ONE launch (pis_conv3x3_filters): one layer's grid is a few
@@ -487,7 +499,7 @@ __global__ __launch_bounds__(256) void wino4_filter_batch_kernel(FilterBatch fb)
   const int lb = (int)blockIdx.x - fb.start[k];
   float* U = jb.planes ? nullptr : reinterpret_cast<float*>(jb.out);
   __bf16* Up = jb.planes ? reinterpret_cast<__bf16*>(jb.out) : nullptr;
-  if (jb.planes == 2) wino4_filter_h2_wave(jb.w, 9 * jb.C, jb.N, jb.dgrad, Up, 4 * lb + (threadIdx.x >> 6));
+  if (jb.planes == 2) wino4_filter_h2_wave(jb.w, 9 * jb.C, jb.N, jb.C, jb.dgrad, Up, 4 * lb + (threadIdx.x >> 6));
   else if (jb.dgrad) wino4_filter_rot_tile(jb.w, jb.N, jb.C, U, 0, Up, lb, jb.umax);
   else wino4_filter_range(jb.w, 9 * jb.C, jb.N, jb.C, U, 0, Up, lb, jb.blocks, jb.umax);
 }
@@ -1845,20 +1857,25 @@ __global__ __launch_bounds__(64 * NWN * NWT) void wino4_gemm_out_x6_kernel(const
   // unpadded rows, 16-B chunks XOR-swizzled by (row / 2) % 8: every ds_read_b128 lane group (16
   // rows of one 16-row window, two adjacent chunks) hits 16 distinct slots of the 256-B bank row;
   // without the 8-element padding a block needs 72 KB of LDS, so two blocks share a CU
-  static_assert(KC == 64, "the swizzle spans 8 chunks of 8 bf16");
-  auto sw = [](int row, int k) { return row * KP + ((((k >> 3) ^ ((row >> 1) & 7)) << 3) | (k & 7)); };
+  // KC = 128 (128-channel contractions): 256-B rows span a whole bank row, so the 16-B chunk is
+  // XOR-swizzled by the row's low 4 bits (16 rows of one ds_read_b128 lane group: 16 slots)
+  static_assert(KC == 64 || KC == 128, "the swizzle spans 8 or 16 chunks of 8 bf16");
+  auto sw = [](int row, int k) {
+    const int x = KC == 64 ? (row >> 1) & 7 : row & 15;
+    return row * KP + ((((k >> 3) ^ x) << 3) | (k & 7));
+  };
   constexpr int NV4 = TB * KC / 4, AL = (NV4 + NT - 1) / NT;  // float4 of V[xi] per thread
   constexpr bool VPART = NV4 % NT != 0;                         // (then NV4 < NT: some threads idle)
   constexpr int NU8 = P * NN * KC / 8, UL = NU8 / NT;          // 16-B chunks of the U[xi] planes per thread
   static_assert((!VPART || NV4 < NT) && NU8 % NT == 0, "staging must tile the block");
-  constexpr int RING = 6, KS = KC / 32;
+  constexpr int RING = KC == 64 ? 6 : 3, KS = KC / 32;  // V stages in flight (same bytes either way)
   // LDS: the double-buffered operand planes, and (aliased) the epilogue's staging of all four
   // tile quarters of Y (139 KB: one block per CU either way, its registers allow no second)
   constexpr int QT = 4 * NWT, EP = NN + 4, EQ = QT * 16 * EP;  // tiles per quarter; row pitch, floats
   constexpr int OPS_BYTES = 2 * P * (TB + NN) * KP * 2, EPI_BYTES = 4 * EQ * 4;
   constexpr int LDS_BYTES = OPS_BYTES > EPI_BYTES ? OPS_BYTES : EPI_BYTES;
   static_assert(QT * 4 * (NN / 4) == NT, "one epilogue item per thread and quarter");
-  static_assert(!H3 || (AL == 1 && !VPART), "H3: one V row per thread (its tile scale in a register)");
+  static_assert(!H3 || (AL <= 2 && !VPART), "H3: at most two V rows per thread (their tile scales in registers)");
   __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
   auto sA = reinterpret_cast<__bf16(*)[P][TB * KP]>(smem);
   auto sU = reinterpret_cast<__bf16(*)[P][NN * KP]>(smem + 2 * P * TB * KP * 2);
@@ -1895,7 +1912,7 @@ __global__ __launch_bounds__(64 * NWN * NWT) void wino4_gemm_out_x6_kernel(const
       if (!VPART || tid + i * NT < NV4) r[i] = *reinterpret_cast<const f32x4*>(vb + xi * TK + 4 * (tid + i * NT));
     }
   };
-  auto lstore = [&](int buf, const f32x4 (&r)[AL], float srow) {  // srow: H3 tile scale
+  auto lstore = [&](int buf, const f32x4 (&r)[AL], f32x2 srow) {  // srow: H3 tile scales of the rows
 #pragma unroll
     for (int i = 0; i < AL; ++i) {
       const int idx = tid + i * NT;
@@ -1903,7 +1920,7 @@ __global__ __launch_bounds__(64 * NWN * NWT) void wino4_gemm_out_x6_kernel(const
       const int row = idx / (KC / 4), c = 4 * (idx % (KC / 4));
       if constexpr (H3) {
         u32x2 h, l;
-        split2h_x4(r[i] * srow, h, l);
+        split2h_x4(r[i] * srow[i], h, l);
         *reinterpret_cast<u32x2*>(&sA[buf][0][sw(row, c)]) = h;
         *reinterpret_cast<u32x2*>(&sA[buf][1][sw(row, c)]) = l;
         continue;
@@ -1939,7 +1956,7 @@ __global__ __launch_bounds__(64 * NWN * NWT) void wino4_gemm_out_x6_kernel(const
 #pragma unroll
     for (int j = 0; j < RING; ++j) gload(vb, j, vr[j]);
   };
-  auto first_stage = [&](const float* vb, float srow) {
+  auto first_stage = [&](const float* vb, f32x2 srow) {
     uload(0, 0);
     uload(1, 1);
     lstore(0, vr[0], srow);
@@ -1955,8 +1972,23 @@ __global__ __launch_bounds__(64 * NWN * NWT) void wino4_gemm_out_x6_kernel(const
     h2_scale_pair(m, sc, inv);
     return sc;
   };
-  float srow = 1.f, tm_next = 0.f;
-  if constexpr (H3) srow = tile_scale(tmax[grp0 * TB + tid / (KC / 4)]);
+  // a tile's max |V| over its KC / 64 channel chunks (tmax[t][KC / 64])
+  auto tmx = [&](int64_t t) {
+    float m = tmax[t * (KC / 64)];
+#pragma unroll
+    for (int j = 1; j < KC / 64; ++j) m = fmaxf(m, tmax[t * (KC / 64) + j]);
+    return m;
+  };
+  // the tile maxima of this thread's staged rows (row = (tid + i NT) / (KC / 4)) in group t0
+  auto row_max = [&](int64_t t0) {
+    f32x2 m = {0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < AL; ++i) m[i] = tmx(t0 + (tid + i * NT) / (KC / 4));
+    return m;
+  };
+  auto row_scale = [&](f32x2 m) { return f32x2{tile_scale(m[0]), tile_scale(m[1])}; };
+  f32x2 srow = {1.f, 1.f}, tm_next = {0.f, 0.f};
+  if constexpr (H3) srow = row_scale(row_max(grp0 * TB));
   prime(V + grp0 * TB * KC);
   first_stage(V + grp0 * TB * KC, srow);
 #pragma unroll 1
@@ -2057,7 +2089,7 @@ __global__ __launch_bounds__(64 * NWN * NWT) void wino4_gemm_out_x6_kernel(const
     }
     const bool more = gi + 1 < G;
     if (more) {
-      if constexpr (H3) tm_next = tmax[t0 + TB + tid / (KC / 4)];
+      if constexpr (H3) tm_next = row_max(t0 + TB);
       prime(vb + TB * KC);
     }
     if constexpr (H3) {
@@ -2066,7 +2098,7 @@ __global__ __launch_bounds__(64 * NWN * NWT) void wino4_gemm_out_x6_kernel(const
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         float sc, inv_s;
-        h2_scale_pair(tmax[t0 + 16 * wt + 4 * lq + q], sc, inv_s);
+        h2_scale_pair(tmx(t0 + 16 * wt + 4 * lq + q), sc, inv_s);
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -2126,7 +2158,7 @@ __global__ __launch_bounds__(64 * NWN * NWT) void wino4_gemm_out_x6_kernel(const
     }
     __syncthreads();
     if (more) {
-      if constexpr (H3) srow = tile_scale(tm_next);
+      if constexpr (H3) srow = row_scale(tm_next);
       first_stage(vb + TB * KC, srow);
     }
   }
@@ -2166,8 +2198,8 @@ static void launch_wino4_input(int64_t T, int C, hipStream_t s, const float* x, 
 // (Up: the fused kernel's planes, bf16x6 or, with h2, fp16x3 + scales — C % 32 == 0)
 static void launch_wino4_filter(const IGemmArgs& a, int N, int C, float* U, int transposed, __bf16* Up,
                                 hipStream_t s, bool h2 = false, float* umax = nullptr) {
-  if (h2)  // C == 64, N % 4 == 0 (the fused kernel's shapes)
-    hipLaunchKernelGGL(wino4_filter_h2_kernel, dim3(N / 4), dim3(256), 0, s, a.wt, a.ldw, N, a.w_unflipped ? 1 : 0,
+  if (h2)  // C % 64 == 0, N % 4 == 0 (the fused kernel's shapes)
+    hipLaunchKernelGGL(wino4_filter_h2_kernel, dim3(N / 4), dim3(256), 0, s, a.wt, a.ldw, N, C, a.w_unflipped ? 1 : 0,
                        Up);
   else if (a.w_unflipped)  // N, C % 32 == 0 checked by launch_wino3x3
     hipLaunchKernelGGL(wino4_filter_rot_kernel, dim3((N / 32) * (C / 32)), dim3(256), 0, s, a.wt, N, C, U,
@@ -2197,7 +2229,8 @@ static bool wino_gemm_out_wanted(int m, int64_t T, int C, int N) {
   // gradient) with pis_tune key 26: two blocks per tile group, V read twice (from L2), M never
   return m == 4 && tune_get(PIS_TUNE_WINO_GEMM_OUT) != 0 && tune_get(PIS_TUNE_WINO_TILE) >= 3 && T % 32 == 0 &&
          T >= 2 * (int64_t)C &&  // the filter planes fit in the M region
-         C == 64 && (N == 64 || (N == 128 && tune_get(PIS_TUNE_FUSED_WIDE) != 0));
+         (C == 64 || (C == 128 && tune_get(PIS_TUNE_FUSED_K128) != 0)) &&
+         (N == 64 || (N == 128 && tune_get(PIS_TUNE_FUSED_WIDE) != 0));
 }
 
 static int launch_wino_gemm_out(const float* V, const __bf16* Up, const IGemmArgs& a, int B, int64_t T,
@@ -2209,29 +2242,56 @@ static int launch_wino_gemm_out(const float* V, const __bf16* Up, const IGemmArg
   const int mode = tune_get(PIS_TUNE_WINO_GEMM_OUT);
   const int G = mode == 2 ? 1 : mode == 3 ? 2 : mode == 4 ? 8 : 4;
   const dim3 blk(512);
-  if (wino_gemm_out_h3() && tune_get(PIS_TUNE_FUSED_STAGGER) != 0 && groups % 4 == 0) {
-    hipLaunchKernelGGL((wino4_gemm_out_x6_kernel<4, 2, 64, 4, true, true>), dim3((int)(groups / 4) * nblk), blk, 0, s, V, Up,
-                       a, B, tmax);
-  } else if (wino_gemm_out_h3()) {
-    if (G == 8 && groups % 8 == 0)
-      hipLaunchKernelGGL((wino4_gemm_out_x6_kernel<4, 2, 64, 8, true>), dim3((int)(groups / 8) * nblk), blk, 0, s, V, Up, a,
-                         B, tmax);
+  if (a.Csrc == 128) {
+    // KC = 128 always staggered where it can be: that form fits 250 VGPRs, the lockstep one spills
+    if (wino_gemm_out_h3() && groups % 4 == 0) {
+      hipLaunchKernelGGL((wino4_gemm_out_x6_kernel<4, 2, 128, 4, true, true>), dim3((int)(groups / 4) * nblk), blk, 0, s, V, Up,
+                         a, B, tmax);
+    } else if (wino_gemm_out_h3()) {
+      if (G == 8 && groups % 8 == 0)
+        hipLaunchKernelGGL((wino4_gemm_out_x6_kernel<4, 2, 128, 8, true>), dim3((int)(groups / 8) * nblk), blk, 0, s, V, Up, a,
+                           B, tmax);
+      else if (G == 4 && groups % 4 == 0)
+        hipLaunchKernelGGL((wino4_gemm_out_x6_kernel<4, 2, 128, 4, true>), dim3((int)(groups / 4) * nblk), blk, 0, s, V, Up, a,
+                           B, tmax);
+      else if (G == 2 && groups % 2 == 0)
+        hipLaunchKernelGGL((wino4_gemm_out_x6_kernel<4, 2, 128, 2, true>), dim3((int)(groups / 2) * nblk), blk, 0, s, V, Up, a,
+                           B, tmax);
+      else
+        hipLaunchKernelGGL((wino4_gemm_out_x6_kernel<4, 2, 128, 1, true>), dim3((int)groups * nblk), blk, 0, s, V, Up, a, B, tmax);
+    } else if (G == 8 && groups % 8 == 0)
+      hipLaunchKernelGGL((wino4_gemm_out_x6_kernel<4, 2, 128, 8>), dim3((int)(groups / 8) * nblk), blk, 0, s, V, Up, a, B, nullptr);
     else if (G == 4 && groups % 4 == 0)
-      hipLaunchKernelGGL((wino4_gemm_out_x6_kernel<4, 2, 64, 4, true>), dim3((int)(groups / 4) * nblk), blk, 0, s, V, Up, a,
-                         B, tmax);
+      hipLaunchKernelGGL((wino4_gemm_out_x6_kernel<4, 2, 128, 4>), dim3((int)(groups / 4) * nblk), blk, 0, s, V, Up, a, B, nullptr);
     else if (G == 2 && groups % 2 == 0)
-      hipLaunchKernelGGL((wino4_gemm_out_x6_kernel<4, 2, 64, 2, true>), dim3((int)(groups / 2) * nblk), blk, 0, s, V, Up, a,
-                         B, tmax);
+      hipLaunchKernelGGL((wino4_gemm_out_x6_kernel<4, 2, 128, 2>), dim3((int)(groups / 2) * nblk), blk, 0, s, V, Up, a, B, nullptr);
     else
-      hipLaunchKernelGGL((wino4_gemm_out_x6_kernel<4, 2, 64, 1, true>), dim3((int)groups * nblk), blk, 0, s, V, Up, a, B, tmax);
-  } else if (G == 8 && groups % 8 == 0)
-    hipLaunchKernelGGL((wino4_gemm_out_x6_kernel<4, 2, 64, 8>), dim3((int)(groups / 8) * nblk), blk, 0, s, V, Up, a, B, nullptr);
-  else if (G == 4 && groups % 4 == 0)
-    hipLaunchKernelGGL((wino4_gemm_out_x6_kernel<4, 2, 64, 4>), dim3((int)(groups / 4) * nblk), blk, 0, s, V, Up, a, B, nullptr);
-  else if (G == 2 && groups % 2 == 0)
-    hipLaunchKernelGGL((wino4_gemm_out_x6_kernel<4, 2, 64, 2>), dim3((int)(groups / 2) * nblk), blk, 0, s, V, Up, a, B, nullptr);
-  else
-    hipLaunchKernelGGL((wino4_gemm_out_x6_kernel<4, 2, 64, 1>), dim3((int)groups * nblk), blk, 0, s, V, Up, a, B, nullptr);
+      hipLaunchKernelGGL((wino4_gemm_out_x6_kernel<4, 2, 128, 1>), dim3((int)groups * nblk), blk, 0, s, V, Up, a, B, nullptr);
+  } else {
+  if (wino_gemm_out_h3() && tune_get(PIS_TUNE_FUSED_STAGGER) != 0 && groups % 4 == 0) {
+      hipLaunchKernelGGL((wino4_gemm_out_x6_kernel<4, 2, 64, 4, true, true>), dim3((int)(groups / 4) * nblk), blk, 0, s, V, Up,
+                         a, B, tmax);
+    } else if (wino_gemm_out_h3()) {
+      if (G == 8 && groups % 8 == 0)
+        hipLaunchKernelGGL((wino4_gemm_out_x6_kernel<4, 2, 64, 8, true>), dim3((int)(groups / 8) * nblk), blk, 0, s, V, Up, a,
+                           B, tmax);
+      else if (G == 4 && groups % 4 == 0)
+        hipLaunchKernelGGL((wino4_gemm_out_x6_kernel<4, 2, 64, 4, true>), dim3((int)(groups / 4) * nblk), blk, 0, s, V, Up, a,
+                           B, tmax);
+      else if (G == 2 && groups % 2 == 0)
+        hipLaunchKernelGGL((wino4_gemm_out_x6_kernel<4, 2, 64, 2, true>), dim3((int)(groups / 2) * nblk), blk, 0, s, V, Up, a,
+                           B, tmax);
+      else
+        hipLaunchKernelGGL((wino4_gemm_out_x6_kernel<4, 2, 64, 1, true>), dim3((int)groups * nblk), blk, 0, s, V, Up, a, B, tmax);
+    } else if (G == 8 && groups % 8 == 0)
+      hipLaunchKernelGGL((wino4_gemm_out_x6_kernel<4, 2, 64, 8>), dim3((int)(groups / 8) * nblk), blk, 0, s, V, Up, a, B, nullptr);
+    else if (G == 4 && groups % 4 == 0)
+      hipLaunchKernelGGL((wino4_gemm_out_x6_kernel<4, 2, 64, 4>), dim3((int)(groups / 4) * nblk), blk, 0, s, V, Up, a, B, nullptr);
+    else if (G == 2 && groups % 2 == 0)
+      hipLaunchKernelGGL((wino4_gemm_out_x6_kernel<4, 2, 64, 2>), dim3((int)(groups / 2) * nblk), blk, 0, s, V, Up, a, B, nullptr);
+    else
+      hipLaunchKernelGGL((wino4_gemm_out_x6_kernel<4, 2, 64, 1>), dim3((int)groups * nblk), blk, 0, s, V, Up, a, B, nullptr);
+  }
   return launch_status("wino_gemm_out");
 }
 
@@ -2425,8 +2485,8 @@ int launch_wino4_filter_only(const float* w, int C, int N, int dgrad, int format
   a.wt = w; a.ldw = 9 * C; a.w_unflipped = dgrad;
   if (dgrad && (N % 32 || C % 32)) return set_error("pis_conv3x3_filter: the input-gradient transform needs "
                                                     "32-aligned channels"), PIS_ERR_ARG;
-  if (format == 2 && wino_gemm_out_h3() && (C != 64 || N % 4))
-    return set_error("pis_conv3x3_filter: fp16x3 planes need 64 contraction channels"), PIS_ERR_ARG;
+  if (format == 2 && wino_gemm_out_h3() && (C % 64 || N % 4))
+    return set_error("pis_conv3x3_filter: fp16x3 planes need 64 x k contraction channels"), PIS_ERR_ARG;
   if (format == 2) launch_wino4_filter(a, N, C, nullptr, 0, reinterpret_cast<__bf16*>(out), s, wino_gemm_out_h3());
   else  // + the row maxima after U when the consuming GEMM is the prescaled fp16x3 one
     launch_wino4_filter(a, N, C, reinterpret_cast<float*>(out), 0, nullptr, s, false,
@@ -2446,8 +2506,8 @@ int launch_wino4_filter_batch(int n, const float* const* w, void* const* out, co
     if (dgrad[k] && (N[k] % 32 || C[k] % 32))
       return set_error("pis_conv3x3_filters: an input-gradient transform needs 32-aligned channels"), PIS_ERR_ARG;
     const int planes = format[k] == 2 ? (wino_gemm_out_h3() ? 2 : 1) : 0;
-    if (planes == 2 && (C[k] != 64 || N[k] % 4))
-      return set_error("pis_conv3x3_filters: fp16x3 planes need 64 contraction channels"), PIS_ERR_ARG;
+    if (planes == 2 && (C[k] % 64 || N[k] % 4))
+      return set_error("pis_conv3x3_filters: fp16x3 planes need 64 x k contraction channels"), PIS_ERR_ARG;
     const int blocks = planes == 2 ? N[k] / 4 : dgrad[k] ? (N[k] / 32) * (C[k] / 32) : grid_of((int64_t)N[k] * C[k]);
     float* umax = planes == 0 && h3_prescaled(C[k], N[k]) ? reinterpret_cast<float*>(out[k]) + (size_t)36 * N[k] * C[k]
                                                           : nullptr;

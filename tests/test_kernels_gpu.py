@@ -105,7 +105,7 @@ def test_conv3x3_dgrad_wgrad(hip, B, H, W, Cin, Cout):
 
 # every non-default kernel variant behind pis_tune (include/pis_capi.h) stays exact too
 TUNE_VARIANTS = [(4, 1), (4, 2), (4, 3), (5, 0), (6, 2048), (3, 0), (7, 1), (8, 0), (8, 2), (10, 0), (10, 1),
-                 (11, 0), (12, 0), (12, 2), (13, 0), (13, 1), (13, 2), (10, 2), (10, 3), (14, 0), (14, 1), (14, 2), (15, 0), (16, 0), (17, 4), (22, 0), (23, 1), (24, 32), (25, 1), (26, 0)]
+                 (11, 0), (12, 0), (12, 2), (13, 0), (13, 1), (13, 2), (10, 2), (10, 3), (14, 0), (14, 1), (14, 2), (15, 0), (16, 0), (17, 4), (22, 0), (23, 1), (24, 32), (25, 1), (26, 0), (27, 0)]
 
 
 @pytest.mark.parametrize("key,value", TUNE_VARIANTS)
@@ -120,7 +120,7 @@ def test_conv3x3_tuned_variants(hip, key, value):
         for shape in [(2, 8, 12, 128, 64), (1, 16, 32, 256, 128)]:
             test_convt2x2(hip, *shape)
         for shape in [(2, 8, 8, 256, 256, 2), (1, 6, 10, 132, 64, 2), (2, 32, 64, 64, 128, 1),
-                      (2, 32, 64, 128, 64, 1)]:
+                      (2, 32, 64, 128, 64, 1), (2, 32, 64, 128, 128, 1)]:
             test_conv3x3_ex_winograd(hip, *shape)
     finally:
         hip.pis_tune(key, prev)
@@ -752,14 +752,16 @@ def test_fused_64_groups_per_block_bitwise(hip, B, H, W):
     assert rel_err(nchw(out[2][2]) - 0.5, dx_ref) < 1e-6
 
 
-def test_fused_64_fp16x3_is_fp32_accurate(hip):
-    """The fused 64->64 kernel in fp16x3 (pis_tune(22, 1): per-tile and per-channel power-of-two
+@pytest.mark.parametrize("C", [64, 128])
+def test_fused_64_fp16x3_is_fp32_accurate(hip, C):
+    """The fused kernel (C -> C channels: 64-channel contractions, and 128-channel ones with two
+    64-channel output blocks, keys 26 / 27) in fp16x3 (pis_tune(22, 1): per-tile and per-channel power-of-two
     scales, hi + lo fp16, three fp16 products) against float64: forward and input gradient as
     accurate (+25 % slack) as the same Winograd pipeline with the native fp32 MFMA GEMM, as the
     bf16x6 fused kernel (22, 0) and as the 3-pass fp16x3 GEMM path (15, 0), for unit,
     gradient-sized (1e-9, 1e-12) and large (1e6) operands, and with one region whose values span
     2^-60 .. 1 (the tile scale's worst case)."""
-    B, H, W, C = 2, 32, 64, 64
+    B, H, W = 2, 32, 64
     g = torch.Generator().manual_seed(53)
     x0 = F.relu(torch.randn(B, C, H, W, generator=g, dtype=torch.float64))
     x0[0, :, :8, :8] *= torch.pow(2.0, -60 * torch.rand(C, 8, 8, generator=g, dtype=torch.float64))
@@ -802,7 +804,7 @@ def test_fused_64_fp16x3_is_fp32_accurate(hip):
 
 
 @pytest.mark.parametrize("B,H,W,Cin,Cout", [(2, 32, 64, 64, 64), (2, 16, 32, 128, 128), (1, 32, 32, 128, 64),
-                                           (2, 16, 16, 256, 256), (2, 32, 64, 128, 64)])
+                                           (2, 16, 16, 256, 256), (2, 32, 64, 128, 64), (2, 32, 64, 128, 128)])
 def test_conv3x3_bwd_prep(hip, B, H, W, Cin, Cout):
     """pis_conv3x3_bwd_prep: one pass over dz writes both backward transforms; the dgrad_ex and
     wgrad_keep calls that then pass PIS_WINO_PREPARED give the same results as without it (and
