@@ -117,9 +117,10 @@ int pis_version(void);
                                     model (profiles/r2_q70_*, r2_q72_*) */
 #define PIS_TUNE_FUSED_STAGGER 25 /* fused 64 -> 64 kernel in fp16x3 (key 22): 1 the SIMD-partner waves fold one xi late
                                      (stagger; bit-for-bit the same), 0 (default) all waves in lockstep */
-#define PIS_TUNE_FUSED_WIDE 26   /* 1 (default): the fused contraction + output transform (key 15) also for 64 -> 128
-                                    channels (two 64-channel blocks per tile group, V read twice from L2, M never
-                                    written: enc2.conv0 forward -21 %, dec1.conv0 input gradient -20 %); 0: 64 -> 64 only */
+#define PIS_TUNE_FUSED_WIDE 26   /* v: the fused contraction + output transform (key 15) for up to 64 x 2^v output
+                                    channels (N / 64 blocks per tile group, V re-read from L2, M never written):
+                                    2 (default, N <= 256; enc3.conv0 forward -9 %), 1 (N <= 128: enc2.conv0 forward
+                                    -21 %, dec1.conv0 input gradient -20 %), 0: 64 outputs only */
 #define PIS_TUNE_FUSED_K128 27   /* 1 (default): the fused contraction + output transform also for 128-channel
                                     contractions (128 -> 64, and 128 -> 128 with key 26; the SIMD-partner waves always
                                     staggered: dec1.conv0 forward -11 %, enc2.conv0 input gradient -15 %);

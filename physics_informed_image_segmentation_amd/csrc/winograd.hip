@@ -2230,7 +2230,7 @@ static bool wino_gemm_out_wanted(int m, int64_t T, int C, int N) {
   return m == 4 && tune_get(PIS_TUNE_WINO_GEMM_OUT) != 0 && tune_get(PIS_TUNE_WINO_TILE) >= 3 && T % 32 == 0 &&
          T >= 2 * (int64_t)C &&  // the filter planes fit in the M region
          (C == 64 || (C == 128 && tune_get(PIS_TUNE_FUSED_K128) != 0)) &&
-         (N == 64 || (N == 128 && tune_get(PIS_TUNE_FUSED_WIDE) != 0));
+         (N == 64 || (N % 64 == 0 && N <= 64 * (1 << tune_get(PIS_TUNE_FUSED_WIDE))));
 }
 
 static int launch_wino_gemm_out(const float* V, const __bf16* Up, const IGemmArgs& a, int B, int64_t T,
