@@ -83,7 +83,13 @@ class StepGraph:
         return self.loss
 
     def close(self):
-        """Back to the model's own dropout draws (the graph and its buffers are released)."""
+        """Back to the model's own dropout draws (the graph and its buffers are released).
+        Synchronises first and releases the graph at once, so its executable (and the events and
+        streams its capture referenced) are never torn down by a later garbage collection while
+        other work is in flight."""
+        torch.cuda.synchronize()
         if self.blocks:
             self.model.set_dropout_scales(None)
-        self.graph = None
+        graph, self.graph = self.graph, None
+        del graph
+        torch.cuda.synchronize()

@@ -1,6 +1,8 @@
 """The graph-replayed training step (physics_informed_image_segmentation_amd/graph.py) IS the
 eager step: same Dropout2d draws, same kernels, same order of every reduction — so the weights
 after N steps are bitwise equal to N eager steps of an identically seeded model."""
+import gc
+
 import pytest
 import torch
 
@@ -39,9 +41,14 @@ def test_graph_steps_equal_eager_steps(hip, dropout):
     losses_g = [sg.step().item() for _ in range(n - 2)]
     sg.close()
     torch.cuda.synchronize()
-    assert losses_g == losses_e[2:]
-    for (k, p), q in zip(me.named_parameters(), mg.parameters()):
-        assert torch.equal(p, q), k
+    ok = losses_g == losses_e[2:]
+    diff = [k for (k, p), q in zip(me.named_parameters(), mg.parameters()) if not torch.equal(p, q)]
+    # release both models' engines (streams, events) here, not in a later test's garbage collection
+    del sg, me, mg, oe, og
+    gc.collect()
+    torch.cuda.synchronize()
+    assert ok, (losses_g, losses_e[2:])
+    assert not diff, diff
 
 
 def test_graph_step_takes_new_batches(hip):
@@ -52,3 +59,6 @@ def test_graph_step_takes_new_batches(hip):
     b = sg.step(torch.flip(x, dims=[-1]), torch.flip(t, dims=[-1])).item()
     assert a != b
     sg.close()
+    del sg, m, o
+    gc.collect()
+    torch.cuda.synchronize()
