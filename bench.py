@@ -84,8 +84,8 @@ def conv_flops_per_image(H: int, W: int, c: int = 64) -> float:
 def wino_gemm_launches(H: int, W: int, B: int, c: int = 64):
     """(T, C, N) of every batched Winograd GEMM launch ("wino_gemm") of one training step: the
     forward and input gradient of each F(4x4,3x3) 3x3 conv (T = B H W / 16 tiles, contraction C,
-    N outputs), in no particular order — the 64 -> 64 convs run the fused contraction + output
-    transform kernel instead, and enc1.conv0 (Cin = 1) the VALU row kernels (csrc/winograd.hip
+    N outputs), in no particular order — the 64 / 128-channel contractions into <= 256 outputs run
+    the fused contraction + output transform kernel instead (fused_wanted), and enc1.conv0 (Cin = 1) the VALU row kernels (csrc/winograd.hip
     wino_gemm_out_wanted, csrc/igemm.hip wino_wanted_dims)."""
     convs = []
     for l in range(1, 5):
@@ -97,11 +97,59 @@ def wino_gemm_launches(H: int, W: int, B: int, c: int = 64):
     convs += [(H >> 4, W >> 4, 8 * c, 8 * c)] * 2        # bottleneck
     out = []
     for hl, wl, ci, co in convs:
-        if ci == co == 64:
-            continue
         T = B * (hl // 4) * (wl // 4)
-        out += [(T, ci, co), (T, co, ci)]
+        out += [(T, C, N) for C, N in ((ci, co), (co, ci)) if not fused_wanted(T, C, N)]
     return out
+
+
+def fused_launches(H: int, W: int, B: int, c: int = 64):
+    """(T, C, N, dgrad) of every launch of the fused contraction + output transform
+    ("wino_gemm_out") in one training step (the complement of wino_gemm_launches)."""
+    convs = []
+    for l in range(1, 5):
+        cl = c << (l - 1)
+        hl, wl = H >> (l - 1), W >> (l - 1)
+        if l > 1:
+            convs.append((hl, wl, cl // 2, cl))
+        convs += [(hl, wl, cl, cl), (hl, wl, 2 * cl, cl), (hl, wl, cl, cl)]
+    convs += [(H >> 4, W >> 4, 8 * c, 8 * c)] * 2
+    out = []
+    for hl, wl, ci, co in convs:
+        T = B * (hl // 4) * (wl // 4)
+        out += [(T, C, N, dg) for C, N, dg in ((ci, co, 0), (co, ci, 1)) if fused_wanted(T, C, N)]
+    return out
+
+
+def fused_bytes(T: int, C: int, N: int, dgrad: int) -> float:
+    """Algorithmic HBM bytes of one fused launch: V read (36 fp32 planes of C channels per tile),
+    the filter planes read once (fp16x3: 4 B per element), the 4x4 output tile written (16 pixels
+    x N fp32 per tile) and, for an input gradient, the ReLU mask of its input read; the pooled
+    copy, keep-scales and accumulation reads are not counted."""
+    return 4.0 * (36 * T * C + 36 * N * C + 16 * T * N * (2 if dgrad else 1))
+
+
+def pmc_bytes(substr: str):
+    """Launch-weighted HBM bytes per launch of the kernels whose name contains substr, from the
+    committed rocprofv3 --pmc summary (profiles/pmc_dominant.json), or None."""
+    path = os.path.join(HERE, "profiles", "pmc_dominant.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        ks = json.load(f).get("kernels", {})
+    sel = [(v["hbm_bytes_per_launch"], v["launches"]) for k, v in ks.items()
+           if substr in k and "hbm_bytes_per_launch" in v]
+    n = sum(c for _, c in sel)
+    return sum(b * c for b, c in sel) / n if n else None
+
+
+def fused_wanted(T: int, C: int, N: int) -> bool:
+    """csrc/winograd.hip wino_gemm_out_wanted: the launches the fused contraction + output
+    transform takes instead of the batched GEMM (pis_tune keys 10, 15, 26, 27 as set now)."""
+    from physics_informed_image_segmentation_amd import _hip
+    tune = _hip.lib().pis_tune
+    if tune(15, -1) == 0 or tune(10, -1) < 3 or T % 32 or T < 2 * C:
+        return False
+    return (C == 64 or (C == 128 and tune(27, -1) != 0)) and (N == 64 or (N % 64 == 0 and N <= 64 << tune(26, -1)))
 
 
 def gemm_attainable(launches, pipe_peak_tflops: float, hbm_gbs: float = 8000.0):
@@ -158,6 +206,8 @@ class KernelTimer:
 
     def summary(self):
         torch.cuda.synchronize()
+        if not self.records:
+            return 0, 0.0, 0.0
         ms = [e0.elapsed_time(e1) for e0, e1, _ in self.records]
         fl = [f for _, _, f in self.records]
         return len(ms), sum(fl) / len(fl), sum(ms) / len(ms)
@@ -421,8 +471,8 @@ def main():
     # launch stream right around each of its launches (pis_set_launch_hook), and around the
     # fused-loss C-ABI calls (host-side enqueue only; the GPU stays the bottleneck)
     from physics_informed_image_segmentation_amd import _hip
-    ktimer, ltimer = KernelTimer(), LossCallTimer()
-    _hip.set_launch_hook(ktimer)
+    ktimer, ftimer, ltimer = KernelTimer(), KernelTimer("wino_gemm_out"), LossCallTimer()
+    _hip.set_launch_hook(lambda *a: (ktimer(*a), ftimer(*a)))
     _hip.set_tracer(ltimer)
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -443,18 +493,21 @@ def main():
     _hip.set_launch_hook(None)
     n_launch, flop_per_launch, ms_per_launch = ktimer.summary()
     n_launch //= args.steps
+    nf_launch, f_flop, f_ms = ftimer.summary()
+    nf_launch //= args.steps
     loss_t = ltimer.summary()
     achieved = flop_per_launch / (ms_per_launch * 1e-3) / 1e12
     # the same kernel with the weight gradients serialised on one stream (no concurrent
     # kernel sharing the CUs): one extra instrumented step after the timed region
     eng = model.engine()
     side, eng.side = eng.side, None
-    iso = KernelTimer()
-    _hip.set_launch_hook(iso)
+    iso, fiso = KernelTimer(), KernelTimer("wino_gemm_out")
+    _hip.set_launch_hook(lambda *a: (iso(*a), fiso(*a)))
     step()
     _hip.set_launch_hook(None)
     eng.side = side
     _, iso_flop, iso_ms = iso.summary()
+    _, _, fiso_ms = fiso.summary()
     # the pipe the dominant kernel runs on. fp32-class GEMMs on the MFMA pipe: fp16x3 (pis_tune
     # key 10 = 4, the default: per-K-step power-of-two tile scales, hi + lo fp16 split, three
     # fp16 MFMAs per fp32 multiply-add) peaks at the dense fp16 MFMA rate (~2.5 PFLOP/s,
@@ -488,7 +541,24 @@ def main():
                                       2.0 * 36 * T * C * N / (peak * 1e12)),
             "note": "algorithmic bytes = V read + U read + M written once (4 B x 36 planes); attainable = "
                     "sum over the step's launches of max(FLOP / pipe peak, bytes / 8 TB/s) / their measured "
-                    "time: the C2 GEMMs are mostly HBM-bound (the 36 fp32 M planes)"}
+                    "time: the GEMMs are mostly HBM-bound (the 36 fp32 M planes)"}
+    # the fused contraction + output transform (wino4_gemm_out_x6_kernel): HBM-bound by design
+    fl_ = fused_launches(H, W, B)
+    fused_roof = None
+    if nf_launch and len(fl_) == nf_launch:
+        fb = sum(fused_bytes(*u) for u in fl_) / nf_launch
+        fused_roof = {
+            "bound": "hbm", "kernel": "wino4_gemm_out_x6_kernel<4, 2, 64|128, 4, fp16x3> (wino_gemm_out: the 36 "
+                                      "F(4x4,3x3) contractions fused with the output transform, 64 / 128-channel "
+                                      "contractions into <= 256 outputs)",
+            "achieved": fb / (f_ms * 1e-3) / 1e9, "peak": 8000.0, "unit": "GB/s",
+            "frac": fb / (f_ms * 1e-3) / 8e12, "traffic": pmc_bytes("wino4_gemm_out"),
+            "bytes_per_launch": fb, "launches_per_step": nf_launch, "avg_launch_ms": f_ms,
+            "flop_per_launch": f_flop, "mfma_tflops": f_flop / (f_ms * 1e-3) / 1e12,
+            "bytes": "V read + filter planes read once + output written (+ the input gradient's ReLU mask read)",
+            "measured": "live over the timed steps",
+            "isolated": {"frac": fb / (fiso_ms * 1e-3) / 8e12 if fiso_ms else None, "avg_launch_ms": fiso_ms,
+                         "measured": "one extra step, weight gradients serialised"}}
     loss_cold = loss_standalone(model.engine().u, t, loss_kw)
     if rank == 0:
         flops = conv_flops_per_image(H, W) * B
@@ -500,7 +570,8 @@ def main():
             "vs_baseline": None, "dtype": "fp32", "data": "synthetic",
             "config": {"workload": workload,
                        "global_batch": B * world, "image_size": [H, W], "parallelism": f"dp{world}"},
-            "roofline": {"bound": "mfma", "kernel": ("gemm_nt_h3_bk32_kernel<128, 128|64>" if h3 else
+            "roofline": None,
+            "roofline_gemm": {"bound": "mfma", "kernel": ("gemm_nt_h3_bk32_kernel<128, 128|64>" if h3 else
                                                      "gemm_nt_x6_bk32_kernel<128, 128|64>" if x6 else
                                                      "gemm_nt_kernel<128, 128|64>")
                          + f" ({DOMINANT}: the 36 batched GEMMs of Winograd F(4x4,3x3) fwd/dgrad)",
@@ -520,6 +591,7 @@ def main():
                          "isolated": {"achieved": iso_flop / (iso_ms * 1e-3) / 1e12,
                                       "frac": iso_flop / (iso_ms * 1e-3) / 1e12 / peak, "avg_launch_ms": iso_ms,
                                       "measured": "one extra step, weight gradients serialised"}},
+            "roofline_fused": fused_roof,
             # direct-convolution FLOPs of the step / step time (Winograd executes fewer)
             "step_tflops_direct_equiv": flops / (ms * 1e-3) / 1e12,
             # north-star HBM figure for the fused loss (live over the timed steps): the backward
@@ -535,6 +607,14 @@ def main():
                 for name, (t, nb, gbs) in loss_t.items()}, **loss_cold),
             "final_loss": float(loss.item()),
         }
+        # the dominant kernel (most GPU time per step) carries the contract's "roofline"; the
+        # other of the two conv kernels stays beside it
+        g_ms, f_ms_step = n_launch * ms_per_launch, (nf_launch * f_ms if fused_roof else 0.0)
+        out["roofline_gemm"]["ms_per_step"] = g_ms
+        if fused_roof:
+            fused_roof["ms_per_step"] = f_ms_step
+        out["roofline"] = fused_roof if fused_roof and f_ms_step > g_ms else out["roofline_gemm"]
+        out["roofline_dominant"] = "roofline_fused" if out["roofline"] is fused_roof else "roofline_gemm"
         if world == 1 and not args.no_cpu_baseline and args.config == "c2":
             out["cpu_baseline"] = cpu_baseline()
         print(json.dumps(out))
