@@ -1868,7 +1868,9 @@ __global__ __launch_bounds__(64 * NWN * NWT) void wino4_gemm_out_x6_kernel(const
   constexpr bool VPART = NV4 % NT != 0;                         // (then NV4 < NT: some threads idle)
   constexpr int NU8 = P * NN * KC / 8, UL = NU8 / NT;          // 16-B chunks of the U[xi] planes per thread
   static_assert((!VPART || NV4 < NT) && NU8 % NT == 0, "staging must tile the block");
-  constexpr int RING = KC == 64 ? 6 : 3, KS = KC / 32;  // V stages in flight (same bytes either way)
+  // V stages in flight: 6 x 8 KB (KC = 64) or 3 x 16 KB (KC = 128); 10 stages in the staggered
+  // KC = 64 form (it has the registers) measured 2 % slower (profiles/r2_q82_*)
+  constexpr int RING = KC == 64 ? 6 : 3, KS = KC / 32;
   // LDS: the double-buffered operand planes, and (aliased) the epilogue's staging of all four
   // tile quarters of Y (139 KB: one block per CU either way, its registers allow no second)
   constexpr int QT = 4 * NWT, EP = NN + 4, EQ = QT * 16 * EP;  // tiles per quarter; row pitch, floats
@@ -2070,7 +2072,7 @@ __global__ __launch_bounds__(64 * NWN * NWT) void wino4_gemm_out_x6_kernel(const
           accp = acc;
         }
         // stage xi + 1 (V from its ring slot, U from the register pair), then refill both
-        const int vslot = (b + 1) % RING;
+        const int vslot = (xi + 1) % RING;
         if (xi + 1 < 36) {
           lstore(cur ^ 1, vr[vslot], srow);
           ustore(cur ^ 1, cur ^ 1);
