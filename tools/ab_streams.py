@@ -2,6 +2,8 @@
 (cdna_hip_programming.md §5.4 rule 24):
   default   : main = torch's current stream, weight gradients on a side stream (priority 0)
   main_hi   : the whole step inside a high-priority stream, side stream at normal priority
+  side_hi   : the weight-gradient side stream at high priority (its blocks dispatch first whenever a
+              CU frees up: the fused contraction kernels fill every CU's registers and LDS)
   serial    : weight gradients serialised on the main stream (no side stream)
   sync_gemm : a prepared layer's weight gradient waits for the input gradient's contractions
   sync_dgrad: ... waits for the whole input gradient (PIS_SIDE_SYNC, unet.py conv_bwd)
@@ -35,6 +37,7 @@ def main():
     opt = AdamW(model.parameters(), lr=1e-5, weight_decay=1e-5)
     lo, hi = torch.cuda.Stream.priority_range() if hasattr(torch.cuda.Stream, "priority_range") else (0, -1)
     hi_stream = torch.cuda.Stream(priority=hi)
+    side_hi = torch.cuda.Stream(priority=hi)
     print(f"stream priority range (low, high) = ({lo}, {hi})", flush=True)
 
     def step():
@@ -52,6 +55,8 @@ def main():
             eng.side_sync = variant[5:]
         if variant == "serial":
             eng.side = None
+        if variant == "side_hi":
+            eng.side = side_hi
         ctx = torch.cuda.stream(hi_stream) if variant == "main_hi" else torch.cuda.stream(torch.cuda.current_stream())
         with ctx:
             step()
@@ -66,7 +71,7 @@ def main():
 
     res = {}
     for _ in range(args.rounds):
-        for v in ("default", "main_hi", "serial", "sync_gemm", "sync_dgrad"):
+        for v in ("default", "side_hi", "main_hi", "serial", "sync_gemm", "sync_dgrad"):
             res.setdefault(v, []).append(run(v))
     for v, ms in res.items():
         ms.sort()
