@@ -1941,7 +1941,9 @@ __global__ __launch_bounds__(64 * NWN * NWT) void wino4_gemm_out_x6_kernel(const
     for (int i = 0; i < UL; ++i) {
       const int c = tid + i * NT;  // (plane, channel, 8-k chunk), k fastest: contiguous per plane
       const int pl = c / (NN * KC / 8), rem = c % (NN * KC / 8);
-      ur[slot][i] = *reinterpret_cast<const u32x4*>(Ug + (pl * 36 + xi) * NK + n0 * KC + 8 * rem);
+      // an explicit global-address-space load: the laundered pointer would otherwise become a FLAT
+      // load, which also counts in lgkmcnt and makes every LDS wait wait for this L2 round trip
+      ur[slot][i] = *(const __attribute__((address_space(1))) u32x4*)(Ug + (pl * 36 + xi) * NK + n0 * KC + 8 * rem);
     }
   };
   auto ustore = [&](int buf, int slot) {
