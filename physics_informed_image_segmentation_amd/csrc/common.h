@@ -122,6 +122,14 @@ __device__ __forceinline__ float wave_max_nonneg(float v) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
 }
 
+// 16-byte load from a wave-uniform base (SGPRs) at an unsigned 32-bit per-lane byte offset, as a
+// raw buffer load: the address needs no per-lane 64-bit arithmetic (offsets below 2 GiB)
+__device__ __forceinline__ u32x4 buf_load16(const void* base, uint32_t off) {
+  const __amdgpu_buffer_rsrc_t r =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, 0x7fffffff, 0x00020000);
+  return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
+
 // max of v >= 0 over each aligned group of 8 lanes, returned in every lane of the group (two quad
 // permutes + row_half_mirror)
 __device__ __forceinline__ float group8_max_nonneg(float v) {

@@ -1911,7 +1911,10 @@ __global__ __launch_bounds__(64 * NWN * NWT) void wino4_gemm_out_x6_kernel(const
   auto gload = [&](const float* vb, int xi, f32x4 (&r)[AL]) {
 #pragma unroll
     for (int i = 0; i < AL; ++i) {
-      if (!VPART || tid + i * NT < NV4) r[i] = *reinterpret_cast<const f32x4*>(vb + xi * TK + 4 * (tid + i * NT));
+      // wave-uniform base + unsigned 32-bit per-thread byte offset (a buffer load): no per-load
+      // 64-bit VALU address arithmetic
+      if (!VPART || tid + i * NT < NV4)
+        r[i] = __builtin_bit_cast(f32x4, buf_load16(vb + xi * TK, 16u * (uint32_t)(tid + i * NT)));
     }
   };
   auto lstore = [&](int buf, const f32x4 (&r)[AL], f32x2 srow) {  // srow: H3 tile scales of the rows
@@ -1941,9 +1944,9 @@ __global__ __launch_bounds__(64 * NWN * NWT) void wino4_gemm_out_x6_kernel(const
     for (int i = 0; i < UL; ++i) {
       const int c = tid + i * NT;  // (plane, channel, 8-k chunk), k fastest: contiguous per plane
       const int pl = c / (NN * KC / 8), rem = c % (NN * KC / 8);
-      // an explicit global-address-space load: the laundered pointer would otherwise become a FLAT
-      // load, which also counts in lgkmcnt and makes every LDS wait wait for this L2 round trip
-      ur[slot][i] = *(const __attribute__((address_space(1))) u32x4*)(Ug + (pl * 36 + xi) * NK + n0 * KC + 8 * rem);
+      // (a buffer load from a uniform base, like gload: global, not FLAT, so it stays out of lgkmcnt
+      // and LDS waits do not wait for its L2 round trip)
+      ur[slot][i] = buf_load16(Ug + xi * NK + n0 * KC, 2u * ((uint32_t)pl * 36u * (uint32_t)NK + 8u * (uint32_t)rem));
     }
   };
   auto ustore = [&](int buf, int slot) {
@@ -1999,7 +2002,10 @@ __global__ __launch_bounds__(64 * NWN * NWT) void wino4_gemm_out_x6_kernel(const
   for (int gi = 0; gi < G; ++gi) {
     const int64_t t0 = (grp0 + gi) * TB;
     const float* vb = V + t0 * KC;
-    asm volatile("" : "+s"(Ug), "+s"(TK), "+s"(NK), "+v"(tid));
+    // two statements: an asm whose outputs include a VGPR is divergent as a whole, and the buffer
+    // loads need Ug / TK / NK wave-uniform
+    asm volatile("" : "+s"(Ug), "+s"(TK), "+s"(NK));
+    asm volatile("" : "+v"(tid));
     f32x4 y[4][4], rr[4], accp = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
