@@ -125,7 +125,10 @@ int pis_version(void);
                                     contractions (128 -> 64, and 128 -> 128 with key 26; the SIMD-partner waves always
                                     staggered: dec1.conv0 forward -11 %, enc2.conv0 input gradient -15 %);
                                     0: 64-channel contractions only */
-#define PIS_TUNE_NKEYS 28
+#define PIS_TUNE_FUSED_PAIR 28   /* fused kernel, 64-channel contractions in fp16x3 (key 22), lockstep form: 1 two xi per
+                                    barrier (four LDS operand buffers; the two products' MFMA chains interleave),
+                                    0 one xi per barrier; bit-for-bit the same sums */
+#define PIS_TUNE_NKEYS 29
 #define PIS_DEBUG_NOLOAD (1 << 16)
 int pis_tune(int key, int value);
 /* Tooling (tools/bench_gemm.py): time one batched NT GEMM kernel variant in isolation,

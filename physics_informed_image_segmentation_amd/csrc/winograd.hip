@@ -1847,7 +1847,10 @@ typedef __bf16 bf16x8g __attribute__((ext_vector_type(8)));
 // fold each xi's product one xi late, keeping it in registers across the barrier (a stagger,
 // MI355X_MICROARCH.md 'Two waves that run the SAME program with one barrier per block'): the
 // partners' MFMA and fold phases no longer coincide. Bit-for-bit the same sums in the same order.
-template <int NWN, int NWT, int KC, int G = 1, bool H3 = false, bool STG = false>
+// PR (pis_tune key 28; KC = 64, lockstep only): two xi per barrier. Four LDS operand buffers (xi & 3;
+// still inside the epilogue's 139 KB), xi + 2 and xi + 3 staged after xi + 1's fold, so the two
+// products' independent MFMA chains and folds can interleave and half the barriers go. Same sums.
+template <int NWN, int NWT, int KC, int G = 1, bool H3 = false, bool STG = false, bool PR = false>
 __global__ __launch_bounds__(64 * NWN * NWT) void wino4_gemm_out_x6_kernel(const float* __restrict__ V,
                                                                           const __bf16* __restrict__ Up,
                                                                           IGemmArgs g, int B,
@@ -1874,13 +1877,15 @@ __global__ __launch_bounds__(64 * NWN * NWT) void wino4_gemm_out_x6_kernel(const
   // LDS: the double-buffered operand planes, and (aliased) the epilogue's staging of all four
   // tile quarters of Y (139 KB: one block per CU either way, its registers allow no second)
   constexpr int QT = 4 * NWT, EP = NN + 4, EQ = QT * 16 * EP;  // tiles per quarter; row pitch, floats
-  constexpr int OPS_BYTES = 2 * P * (TB + NN) * KP * 2, EPI_BYTES = 4 * EQ * 4;
+  static_assert(!PR || (KC == 64 && !STG), "paired stages: the lockstep 64-channel form");
+  constexpr int NB = PR ? 4 : 2;  // LDS operand buffers
+  constexpr int OPS_BYTES = NB * P * (TB + NN) * KP * 2, EPI_BYTES = 4 * EQ * 4;
   constexpr int LDS_BYTES = OPS_BYTES > EPI_BYTES ? OPS_BYTES : EPI_BYTES;
   static_assert(QT * 4 * (NN / 4) == NT, "one epilogue item per thread and quarter");
   static_assert(!H3 || (AL <= 2 && !VPART), "H3: at most two V rows per thread (their tile scales in registers)");
   __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
   auto sA = reinterpret_cast<__bf16(*)[P][TB * KP]>(smem);
-  auto sU = reinterpret_cast<__bf16(*)[P][NN * KP]>(smem + 2 * P * TB * KP * 2);
+  auto sU = reinterpret_cast<__bf16(*)[P][NN * KP]>(smem + NB * P * TB * KP * 2);
   float* E = reinterpret_cast<float*>(smem);
   const int N = g.N, TW = g.W / 4, TH = g.H / 4;
   const int64_t T = (int64_t)B * TH * TW;
@@ -1969,6 +1974,12 @@ __global__ __launch_bounds__(64 * NWN * NWT) void wino4_gemm_out_x6_kernel(const
     lstore(0, vr[0], srow);
     ustore(0, 0);
     gload(vb, RING, vr[0]);
+    if constexpr (PR) {  // xi = 1 too; U[2], U[3] in flight
+      lstore(1, vr[1], srow);
+      ustore(1, 1);
+      gload(vb, RING + 1, vr[1]);
+      uload(3, 1);
+    }
     uload(2, 0);
     __syncthreads();
   };
@@ -2035,7 +2046,7 @@ __global__ __launch_bounds__(64 * NWN * NWT) void wino4_gemm_out_x6_kernel(const
     for (int a = 0; a < 6; ++a) {  // fully unrolled: the compiler keeps exact vmcnt counts across rows
 #pragma unroll
       for (int b = 0; b < 6; ++b) {
-        const int xi = 6 * a + b, cur = b & 1;
+        const int xi = 6 * a + b, cur = PR ? (xi & 3) : (b & 1);
         f32x4 acc = {0.f, 0.f, 0.f, 0.f};
         if constexpr (H3) {
 #pragma unroll
@@ -2079,6 +2090,23 @@ __global__ __launch_bounds__(64 * NWN * NWT) void wino4_gemm_out_x6_kernel(const
           }
           accp = acc;
         }
+        if constexpr (PR) {
+          // after the pair's second product: stage xi + 1, xi + 2 (U of xi in register slot xi & 1),
+          // refill their V ring slots and load U two xi ahead
+          if (xi & 1) {
+#pragma unroll
+            for (int d = 1; d <= 2; ++d) {
+              const int xs = xi + d, vslot = xs % RING;
+              if (xs < 36) {
+                lstore(xs & 3, vr[vslot], srow);
+                ustore(xs & 3, xs & 1);
+              }
+              if (xs + RING < 36) gload(vb, xs + RING, vr[vslot]);
+              if (xs + 2 < 36) uload(xs + 2, xs & 1);
+            }
+            __syncthreads();
+          }
+        } else {
         // stage xi + 1 (V from its ring slot, U from the register pair), then refill both
         const int vslot = (xi + 1) % RING;
         if (xi + 1 < 36) {
@@ -2088,6 +2116,7 @@ __global__ __launch_bounds__(64 * NWN * NWT) void wino4_gemm_out_x6_kernel(const
         if (xi + 1 + RING < 36) gload(vb, xi + 1 + RING, vr[vslot]);
         if (xi + 3 < 36) uload(xi + 3, cur ^ 1);
         __syncthreads();
+        }
       }
       // Y[i][j] += AT[i][a] R[j] (a is a runtime row index: coefficients selected from the table)
       if (!late) rowend(a);
@@ -2281,6 +2310,9 @@ static int launch_wino_gemm_out(const float* V, const __bf16* Up, const IGemmArg
   if (wino_gemm_out_h3() && tune_get(PIS_TUNE_FUSED_STAGGER) != 0 && groups % 4 == 0) {
       hipLaunchKernelGGL((wino4_gemm_out_x6_kernel<4, 2, 64, 4, true, true>), dim3((int)(groups / 4) * nblk), blk, 0, s, V, Up,
                          a, B, tmax);
+    } else if (wino_gemm_out_h3() && tune_get(PIS_TUNE_FUSED_PAIR) != 0 && groups % 4 == 0) {
+      hipLaunchKernelGGL((wino4_gemm_out_x6_kernel<4, 2, 64, 4, true, false, true>), dim3((int)(groups / 4) * nblk), blk, 0, s,
+                         V, Up, a, B, tmax);
     } else if (wino_gemm_out_h3()) {
       if (G == 8 && groups % 8 == 0)
         hipLaunchKernelGGL((wino4_gemm_out_x6_kernel<4, 2, 64, 8, true>), dim3((int)(groups / 8) * nblk), blk, 0, s, V, Up, a,

@@ -706,7 +706,7 @@ def test_convt_bf16x6_is_fp32_accurate(hip, Cin, Cout):
 def test_fused_64_groups_per_block_bitwise(hip, B, H, W):
     """The fused 64->64 contraction + output transform takes G groups of 32 tiles per block
     (pis_tune key 15: 1 -> G = 4 where the group count divides, 2 -> 1, 3 -> 2, 4 -> 8), with and
-    without the staggered fold (key 25): every variant gives bit-for-bit the same forward (ReLU, keep-scale, fused max pool) and input gradient
+    without the staggered fold (key 25), and with two xi per barrier (key 28): every variant gives bit-for-bit the same forward (ReLU, keep-scale, fused max pool) and input gradient
     (ReLU mask, keep-scale, accumulate), and G = 1 matches the float64 reference."""
     Cin = Cout = 64
     g = torch.Generator().manual_seed(31)
@@ -720,12 +720,13 @@ def test_fused_64_groups_per_block_bitwise(hip, B, H, W):
     ws = torch.empty(nws // 4 + 1, device="cuda")
     wf = torch.empty(Cin * 9 * Cout, device="cuda")
     assert hip.pis_conv3x3_flip(wd.data_ptr(), wf.data_ptr(), Cin, Cout, s()) == 0
-    prev, prev25 = hip.pis_tune(15, -1), hip.pis_tune(25, -1)
+    prev, prev25, prev28 = hip.pis_tune(15, -1), hip.pis_tune(25, -1), hip.pis_tune(28, -1)
     out = {}
     try:
-        for v in (2, 1, 3, 4, "stagger"):
-            hip.pis_tune(15, 1 if v == "stagger" else v)
+        for v in (2, 1, 3, 4, "stagger", "pair"):
+            hip.pis_tune(15, 1 if v in ("stagger", "pair") else v)
             hip.pis_tune(25, 1 if v == "stagger" else 0)
+            hip.pis_tune(28, 1 if v == "pair" else 0)
             y = torch.empty(B, H, W, Cout, device="cuda")
             pool = torch.empty(B, H // 2, W // 2, Cout, device="cuda")
             rc = hip.pis_conv3x3_fwd_pool(xd.data_ptr(), Cin, wd.data_ptr(), bd.data_ptr(), sd.data_ptr(),
@@ -742,7 +743,8 @@ def test_fused_64_groups_per_block_bitwise(hip, B, H, W):
     finally:
         hip.pis_tune(15, prev)
         hip.pis_tune(25, prev25)
-    for v in (1, 3, 4, "stagger"):
+        hip.pis_tune(28, prev28)
+    for v in (1, 3, 4, "stagger", "pair"):
         for a, c in zip(out[2], out[v]):
             assert torch.equal(a, c), v
     y_ref = F.relu(F.conv2d(x.double(), w.double(), b.double(), padding=1)) * scale[:, :, None, None]
