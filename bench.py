@@ -567,7 +567,7 @@ def main():
                        else f"training images/sec ({H}x{W}, {args.config})"),
             "value": imgs_per_s, "unit": "images/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "fp32", "data": "synthetic",
+            "vs_baseline": None, "dtype": "fp32 (fp16x3/bf16x6 split MFMA, Winograd)", "data": "synthetic",
             "config": {"workload": workload,
                        "global_batch": B * world, "image_size": [H, W], "parallelism": f"dp{world}"},
             "roofline": None,

@@ -147,6 +147,16 @@ int pis_debug_gemm_nt(const float* A, const float* B, float* C, int M, int N, in
  * the previously armed event was never recorded (NULL disarms), else 0. */
 int pis_arm_gemm_event(void* event);
 
+/* Owned HIP streams (hipStreamNonBlocking, the given priority: 0 normal, -1 high). torch's
+ * torch.cuda.Stream() hands out a fixed round-robin pool, so a stream that took part in a HIP graph
+ * capture is later handed to unrelated code; the engine's weight-gradient stream and the capture
+ * stream of a graphed step are owned instead (wrapped with torch.cuda.ExternalStream) and destroyed
+ * with their owner. pis_stream_capture_status: hipStreamCaptureStatus (0 none, 1 active,
+ * 2 invalidated) or a negative error. */
+int pis_stream_create(int priority, pis_stream_t* out);
+int pis_stream_destroy(pis_stream_t stream);
+int pis_stream_capture_status(pis_stream_t stream);
+
 /* Profiling hook: called on the launching thread right before (phase 0) and after (phase 1)
  * the enqueue of each heavy kernel ("conv3x3_halo", "wino_gemm", "wgrad3x3_halo",
  * "wino_wgrad_gemm"), with its stream and the MFMA FLOPs it executes, so a profiler can

@@ -42,6 +42,9 @@ LAUNCH_HOOK_T = ctypes.CFUNCTYPE(None, ctypes.c_char_p, c_int, c_void_p, ctypes.
 _SIGNATURES = {
     "pis_set_launch_hook": ([LAUNCH_HOOK_T, P], None),
     "pis_arm_gemm_event": ([P], c_int),
+    "pis_stream_create": ([I, ctypes.POINTER(c_void_p)], c_int),
+    "pis_stream_destroy": ([P], c_int),
+    "pis_stream_capture_status": ([P], c_int),
     "pis_version": ([], c_int),
     "pis_last_error": ([], ctypes.c_char_p),
     "pis_tune": ([I, I], c_int),
@@ -162,6 +165,58 @@ def call(name: str, *args) -> None:
     tok = tr.begin(name, args)
     check(getattr(lib(), name)(*args), name)
     tr.end(tok)
+
+
+_stream_graveyard = []  # owned streams released while a capture was running: destroyed later
+
+
+def _capturing() -> bool:
+    try:
+        return torch.cuda.is_current_stream_capturing()
+    except Exception:
+        return False
+
+
+def _bury() -> None:
+    """Destroy the owned streams whose release had to wait for a capture to end."""
+    while _stream_graveyard and not _capturing():
+        h = _stream_graveyard.pop()
+        lib().pis_stream_destroy(h)
+
+
+class OwnedStream:
+    """A HIP stream this process owns (pis_stream_create), usable as a torch stream
+    (``.stream`` is a torch.cuda.ExternalStream) and destroyed by ``close()`` — after its work
+    drains — instead of returning to torch's round-robin stream pool, where a stream that took
+    part in a graph capture would later be handed to unrelated code. Released during a capture
+    (synchronising is illegal then), it is destroyed after the capture instead."""
+
+    def __init__(self, device=None, priority: int = 0):
+        _bury()
+        raw = c_void_p()
+        check(lib().pis_stream_create(priority, ctypes.byref(raw)), "pis_stream_create")
+        self.handle = raw.value
+        self.stream = torch.cuda.ExternalStream(self.handle, device=device)
+
+    def capture_status(self) -> int:
+        return lib().pis_stream_capture_status(self.handle)
+
+    def close(self) -> None:
+        h, self.handle = self.handle, None
+        if not h:
+            return
+        if _capturing():
+            _stream_graveyard.append(h)
+            return
+        self.stream.synchronize()
+        check(lib().pis_stream_destroy(h), "pis_stream_destroy")
+        _bury()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # interpreter shutdown: the runtime may already be gone
+            pass
 
 
 def require_cuda(t: torch.Tensor, what: str) -> None:

@@ -48,6 +48,38 @@ extern "C" int pis_arm_gemm_event(void* event) {
   return pending;
 }
 
+extern "C" int pis_stream_create(int priority, pis_stream_t* out) {
+  PIS_CHECK_ARG(out != nullptr, "pis_stream_create: out is NULL");
+  hipStream_t s = nullptr;
+  const hipError_t e = hipStreamCreateWithPriority(&s, hipStreamNonBlocking, priority);
+  if (e != hipSuccess) {
+    pis::set_error("pis_stream_create: %s", hipGetErrorString(e));
+    return PIS_ERR_LAUNCH;
+  }
+  *out = (pis_stream_t)s;
+  return PIS_OK;
+}
+
+extern "C" int pis_stream_destroy(pis_stream_t stream) {
+  PIS_CHECK_ARG(stream != nullptr, "pis_stream_destroy: NULL stream");
+  const hipError_t e = hipStreamDestroy((hipStream_t)stream);
+  if (e != hipSuccess) {
+    pis::set_error("pis_stream_destroy: %s", hipGetErrorString(e));
+    return PIS_ERR_LAUNCH;
+  }
+  return PIS_OK;
+}
+
+extern "C" int pis_stream_capture_status(pis_stream_t stream) {
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  const hipError_t e = hipStreamIsCapturing((hipStream_t)stream, &st);
+  if (e != hipSuccess) {
+    pis::set_error("pis_stream_capture_status: %s", hipGetErrorString(e));
+    return PIS_ERR_LAUNCH;
+  }
+  return (int)st;
+}
+
 extern "C" void pis_set_launch_hook(pis_launch_hook_t fn, void* user) {
   pis::g_hook_user.store(user);
   pis::g_hook.store(fn);

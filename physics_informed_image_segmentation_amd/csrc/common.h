@@ -102,10 +102,21 @@ __device__ __forceinline__ float h3_scale(float m) {
 // returned uniform
 // the scale for a tile of max m given the current scale: kept while m * cur stays in [2^7, 2^15)
 // (fp16 digits for everything above 2^-10 of the max, 2x headroom), so accumulators are rarely
-// rescaled; else re-chosen (h3_scale). cur = 0 always re-chooses.
-__device__ __forceinline__ float h3_keep(float cur, float m) {
+// rescaled; else re-chosen (h3_scale). cur = 0 always re-chooses; an all-zero K-step keeps cur.
+// smin (per wave, +inf before the first K-step) is the smallest scale used so far, i.e. the one
+// of the largest operands the accumulators hold: a scale may rise at most 2^32 above it. The
+// accumulators are re-expressed in every new scale, so without the cap a K-step of operands
+// 2^100 below the earlier ones would multiply partial sums of ~2^26 by ~2^200 (inf, for good);
+// with it they stay below K 2^90, and the capped K-step's operands — at most 2^-32 of the sum
+// already accumulated — keep fp16 digits down to 2^-46 of it.
+__device__ __forceinline__ float h3_keep(float cur, float m, float& smin) {
+  if (!(m > 0.f)) return cur > 0.f ? cur : 1.f;
   const float v = m * cur;
-  return (v >= 128.f && v < 32768.f) ? cur : h3_scale(m);
+  // wave-uniform: kept in SGPRs (the GEMMs run at their VGPR limit)
+  const float s = __int_as_float(__builtin_amdgcn_readfirstlane(
+      __float_as_int(fminf((v >= 128.f && v < 32768.f) ? cur : h3_scale(m), smin * 0x1p32f))));
+  smin = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(fminf(smin, s))));
+  return s;
 }
 
 template <int CTRL, int RMASK>

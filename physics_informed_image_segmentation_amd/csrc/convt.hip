@@ -99,6 +99,7 @@ __global__ __launch_bounds__(256, 2) void convt_gemm_kernel(ConvtGemmArgs g) {
     }
   };
   float sa = 0.f, sb = 0.f;  // H3: this wave's current scales
+  float sa_min = __builtin_inff(), sb_min = __builtin_inff();  // ... and the smallest so far
   auto lstore = [&](int buf) {
     if constexpr (H3) {
       float ma = 0.f, mb = 0.f;
@@ -110,8 +111,8 @@ __global__ __launch_bounds__(256, 2) void convt_gemm_kernel(ConvtGemmArgs g) {
       for (int i = 0; i < BL; ++i)
 #pragma unroll
         for (int k = 0; k < 4; ++k) mb = fmaxf(mb, fabsf(rb[i][k]));
-      sa = h3_keep(sa, wave_max_nonneg(ma));
-      sb = h3_keep(sb, wave_max_nonneg(mb));
+      sa = h3_keep(sa, wave_max_nonneg(ma), sa_min);
+      sb = h3_keep(sb, wave_max_nonneg(mb), sb_min);
       if (lane == 0) {
         sscale[buf][0][wave] = sa;
         sscale[buf][1][wave] = sb;

@@ -774,6 +774,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_h3_kernel(WgradArgs g) {
     }
   };
   float sa = 0.f, sb = 0.f;  // this wave's current scales (h3_keep)
+  float sa_min = __builtin_inff(), sb_min = __builtin_inff();  // ... and the smallest so far
   auto store_row = [&](const float* v, int E, float sc, _Float16* hp, _Float16* lp) {
     u32x2 h0, l0;
     split2h_x4(f32x4{v[0], v[1], v[2], v[3]} * sc, h0, l0);
@@ -796,8 +797,8 @@ __global__ __launch_bounds__(256, 2) void wgrad_h3_kernel(WgradArgs g) {
     }
 #pragma unroll
     for (int e = 0; e < EB; ++e) mb = fmaxf(mb, fabsf(rb[e]));
-    sa = h3_keep(sa, wave_max_nonneg(ma));
-    sb = h3_keep(sb, wave_max_nonneg(mb));
+    sa = h3_keep(sa, wave_max_nonneg(ma), sa_min);
+    sb = h3_keep(sb, wave_max_nonneg(mb), sb_min);
     if (lane == 0) {
       sscale[buf][0][wave] = sa;
       sscale[buf][1][wave] = sb;
@@ -906,9 +907,13 @@ static int run_wgrad(const WgradArgs& base, const WgradPlan& pl, hipStream_t s, 
   const dim3 grid(tiles * pl.splits, batches);
   // key 14 = 3 (auto): fp16x3 where the contraction's output has >= 256 columns (Cin): measured
   // per layer (profiles/r2_q53_wgrad_fp16x3.txt) it wins on exactly those (-1..-10 %) and loses on
-  // the HBM-bound 64 / 128-channel layers (+1..+9 %)
+  // the HBM-bound 64 / 128-channel layers (+1..+9 %). The split GEMMs take plain B operands only,
+  // where Np IS the input-channel count (Winograd: Cin; convT: Cin); the direct path's B_CONV3
+  // operand (Np = 9 Cin) never reaches them, it runs the fp32 MFMA kernel below
   const int x6 = tune_get(PIS_TUNE_WGRAD_X6);
-  if ((x6 == 2 || (x6 == 3 && a.Np >= 256)) && a.b_mode == B_PLAIN && pl.pps % 16 == 0 &&
+  const bool plain = a.b_mode == B_PLAIN;
+  const int cin = plain ? a.Np : a.Cb;
+  if ((x6 == 2 || (x6 == 3 && cin >= 256)) && plain && pl.pps % 16 == 0 &&
       (!a.a_up2 || a.W % 8 == 0)) {
     if (pl.bm == 128 && pl.bn == 128) hipLaunchKernelGGL((wgrad_h3_kernel<128, 128>), grid, dim3(256), 0, s, a);
     else if (pl.bm == 128) hipLaunchKernelGGL((wgrad_h3_kernel<128, 64>), grid, dim3(256), 0, s, a);
@@ -1222,6 +1227,8 @@ extern "C" int pis_conv3x3_bwd_prep(const float* dz, int ldz, int B, int H, int 
   float* bpart = wp.fused_bias ? (float*)(base + wp.off_cs) : nullptr;
   float* tmax = wino_fused_h3_planned(B, H, W, Cout, Cin) ? wino_tmax_slot(ws_dgrad, B, H, W, Cout, Cin) : nullptr;
   const int rc = launch_wino_dz2(dz, ldz, B, H, W, Cout, V, E, bpart, (hipStream_t)stream, tmax);
+  // the dgrad_ex that consumes this V checks that it decides the same tile-maxima format
+  if (!rc) wino_prep_record(ws_dgrad, B, H, W, Cout, Cin, tmax != nullptr);
   return rc ? rc : 1;
 }
 

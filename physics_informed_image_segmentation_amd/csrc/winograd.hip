@@ -1391,6 +1391,7 @@ __global__ __launch_bounds__(256, OCC) void gemm_nt_h3_bk32_kernel(const float* 
     }
   };
   float sa = 0.f, sb = 0.f;  // the wave's current scales (h3_keep)
+  float sa_min = __builtin_inff(), sb_min = __builtin_inff();  // ... and the smallest so far
   auto lstore = [&]() {
     // PRE: re-read the packed exponents every K-step: hoisted out of the loop, the compiler keeps
     // 8 broadcast scale pairs live (16 VGPRs) and spills them
@@ -1405,8 +1406,8 @@ __global__ __launch_bounds__(256, OCC) void gemm_nt_h3_bk32_kernel(const float* 
       for (int i = 0; i < BL; ++i)
 #pragma unroll
         for (int k = 0; k < 4; ++k) mb = fmaxf(mb, fabsf(rb[i][k]));
-      sa = h3_keep(sa, wave_max_nonneg(ma));
-      sb = h3_keep(sb, wave_max_nonneg(mb));
+      sa = h3_keep(sa, wave_max_nonneg(ma), sa_min);
+      sb = h3_keep(sb, wave_max_nonneg(mb), sb_min);
       if (lane == 0) {
         sscale[0][wave] = sa;
         sscale[1][wave] = sb;
@@ -1576,7 +1577,7 @@ __global__ __launch_bounds__(256, OCC) void gemm_nt_h3_persist_kernel(const floa
       rb[i] = *reinterpret_cast<const f32x4*>(Bb + (size_t)n * K + k);
     }
   };
-  float sa = 0.f, sb = 0.f;
+  float sa = 0.f, sb = 0.f, sa_min = 0.f, sb_min = 0.f;
   auto lstore = [&](bool first) {  // first: the tile's first K-step (scales re-chosen)
     float ma = 0.f, mb = 0.f;
 #pragma unroll
@@ -1587,8 +1588,9 @@ __global__ __launch_bounds__(256, OCC) void gemm_nt_h3_persist_kernel(const floa
     for (int i = 0; i < BL; ++i)
 #pragma unroll
       for (int k = 0; k < 4; ++k) mb = fmaxf(mb, fabsf(rb[i][k]));
-    sa = h3_keep(first ? 0.f : sa, wave_max_nonneg(ma));
-    sb = h3_keep(first ? 0.f : sb, wave_max_nonneg(mb));
+    if (first) sa_min = sb_min = __builtin_inff();
+    sa = h3_keep(first ? 0.f : sa, wave_max_nonneg(ma), sa_min);
+    sb = h3_keep(first ? 0.f : sb, wave_max_nonneg(mb), sb_min);
     if (lane == 0) {
       sscale[0][wave] = sa;
       sscale[1][wave] = sb;
@@ -2368,6 +2370,8 @@ static bool wino_fused_wanted(int H, int W, int C, int N) {
   return mode == 2;
 }
 
+static int wino_prep_check(const void* ws, int B, int H, int W, int C, int N);
+
 // a describes the direct conv (src/lds = input, wt/ldw = KRSC weights, N outputs, epilogue)
 int launch_wino3x3(const IGemmArgs& a, int B, void* ws, hipStream_t s, float* keep_v, bool v_ready) {
   const int C = a.Csrc, N = a.N;
@@ -2377,6 +2381,10 @@ int launch_wino3x3(const IGemmArgs& a, int B, void* ws, hipStream_t s, float* ke
   float* V = U + (size_t)nxi * N * C;
   float* Mt = V + (size_t)nxi * T * C;
   if (keep_v && m == 4) V = keep_v;
+  if (v_ready && m == 4) {
+    const int rc = wino_prep_check(ws, B, a.H, a.W, C, N);
+    if (rc) return rc;
+  }
   const double flop = 2.0 * nxi * (double)T * N * C;
   if (a.filter_ready && (m != 4 || (!keep_v && wino_fused_wanted(a.H, a.W, C, N))))
     return set_error("launch_wino3x3: PIS_FILTER_READY needs the F(4x4,3x3) GEMM path"), PIS_ERR_ARG;
@@ -2595,6 +2603,40 @@ int launch_wino_dz2(const float* dz, int ldz, int B, int H, int W, int N, float*
     hipLaunchKernelGGL((wino4_dz2_kernel<false>), dim3(grid_of(T * (N / 4))), dim3(256), 0, s, dz, ldz, B, H, W, N, V,
                        E, bpart, nullptr);
   return launch_status("wino_dz2");
+}
+
+// pis_conv3x3_bwd_prep decides whether its V carries tile maxima (wino_fused_h3_planned) from the
+// tune state at ITS call; the dgrad_ex that consumes the V decides again at its own. A changed
+// knob in between would make the fused fp16x3 kernel read stale or unwritten scales, so every prep
+// is recorded (workspace, shape, decision) and a prepared dgrad must find a matching record.
+namespace {
+struct PrepRecord {
+  const void* ws;
+  int B, H, W, C, N;
+  bool tmax;
+};
+thread_local PrepRecord g_prep[16];
+thread_local int g_prep_next = 0;
+}  // namespace
+
+void wino_prep_record(const void* ws, int B, int H, int W, int C, int N, bool tmax) {
+  for (auto& r : g_prep)
+    if (r.ws == ws) r.ws = nullptr;  // the workspace's previous content is gone
+  g_prep[g_prep_next] = PrepRecord{ws, B, H, W, C, N, tmax};
+  g_prep_next = (g_prep_next + 1) % 16;
+}
+
+static int wino_prep_check(const void* ws, int B, int H, int W, int C, int N) {
+  for (const auto& r : g_prep)
+    if (r.ws == ws && r.B == B && r.H == H && r.W == W && r.C == C && r.N == N) {
+      if (r.tmax != wino_fused_h3_planned(B, H, W, C, N))
+        return set_error("PIS_WINO_PREPARED: pis_conv3x3_bwd_prep wrote %s tile maxima but this call's kernel "
+                         "choice needs %s (a pis_tune knob changed in between)",
+                         r.tmax ? "" : "no", r.tmax ? "none" : "them"),
+               PIS_ERR_ARG;
+      return PIS_OK;
+    }
+  return set_error("PIS_WINO_PREPARED: no pis_conv3x3_bwd_prep of this shape into this workspace"), PIS_ERR_ARG;
 }
 
 // where the fp16x3 consumers find the per-(tile, 64-channel chunk) max |V| of their V (after M)

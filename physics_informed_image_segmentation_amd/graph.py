@@ -20,7 +20,9 @@ from __future__ import annotations
 from typing import Optional
 
 import torch
+import torch.distributed as dist
 
+from . import _hip
 from .unet import BLOCK_ORDER, UNet
 
 
@@ -28,11 +30,26 @@ class StepGraph:
     """``StepGraph(model, criterion, optimizer, x, target)``: runs ``warmup`` eager steps (they
     are real training steps), captures the next step's forward + backward, and then each
     ``step()`` is one full training step; ``step(x, target)`` copies a new batch of the same
-    shape into the captured input buffers first. Returns the loss tensor (device)."""
+    shape into the captured input buffers first. Returns the loss of that step (a fresh device
+    tensor: the captured one is overwritten by the next replay).
+
+    Lifetime. A captured graph references everything its capture touched: the engine's
+    activation / workspace buffers, its weight-gradient stream, the capture stream and the HIP
+    events through which the two streams' edges were recorded. The StepGraph owns all of them —
+    the engine, the events (``UNetEngine.capture_events``) and two streams of its own
+    (``_hip.OwnedStream``: torch's ``torch.cuda.Stream()`` hands out a round-robin pool, so a
+    pooled capture stream would later be given to unrelated code) — and releases them in
+    ``close()`` only after the device is idle and the graph is destroyed, in that order.
+    ``close()`` also runs when the StepGraph is garbage collected without it."""
 
     def __init__(self, model: UNet, criterion, optimizer, x: torch.Tensor, target: torch.Tensor, warmup: int = 2):
         if not x.is_cuda:
             raise RuntimeError("StepGraph needs the model and batch on the GPU")
+        if model.grad_ready_hook is not None or (dist.is_available() and dist.is_initialized()
+                                                 and dist.get_world_size() > 1):
+            raise RuntimeError("StepGraph captures a single-process step: data-parallel all-reduces "
+                               "(GradBucketer) cannot be replayed from a graph")
+        self.graph = None
         self.model, self.criterion, self.opt = model, criterion, optimizer
         self.x, self.t = x, target
         B = x.shape[0]
@@ -44,13 +61,16 @@ class StepGraph:
                 raise ValueError("StepGraph: dropout p >= 1")
             model.set_dropout_scales(self.scales)
         cur = torch.cuda.current_stream()
-        side = torch.cuda.Stream()
+        self._stream = _hip.OwnedStream(device=x.device)
+        side = self._stream.stream
         side.wait_stream(cur)
         with torch.cuda.stream(side):
             for _ in range(max(1, warmup)):  # plans the engine, allocates every persistent buffer
                 self._eager()
         cur.wait_stream(side)
         torch.cuda.synchronize()
+        self.engine = model.engine()
+        self.engine.capture_events = []
         self.graph = torch.cuda.CUDAGraph()
         optimizer.zero_grad(set_to_none=True)
         # captured on the warm-up stream: autograd's AccumulateGrad nodes remember the stream they
@@ -59,6 +79,12 @@ class StepGraph:
         with torch.cuda.graph(self.graph, stream=side):
             self.loss = criterion(model(self.x), self.t)
             self.loss.backward()
+        # the events the capture recorded through, including the engine's workspace fences
+        self._events = list(self.engine.capture_events) + [e for e in self.engine.ws3_free if e is not None]
+        self.engine.capture_events = []
+        self.engine.ws3_free = [None, None]
+        # the gradient buffers the replays write: AdamW must see exactly these
+        self._grads = [(p, p.grad.data_ptr()) for p in model.parameters() if p.grad is not None]
 
     def _refill(self):
         for n, p, _ in self.blocks:
@@ -73,23 +99,41 @@ class StepGraph:
         return loss
 
     def step(self, x: Optional[torch.Tensor] = None, target: Optional[torch.Tensor] = None) -> torch.Tensor:
+        if self.graph is None:
+            raise RuntimeError("StepGraph.step after close()")
         if x is not None:
             self.x.copy_(x)
         if target is not None:
             self.t.copy_(target)
+        for p, ptr in self._grads:  # e.g. zero_grad(set_to_none=True) between steps would detach them
+            if p.grad is None or p.grad.data_ptr() != ptr:
+                raise RuntimeError("StepGraph: a parameter's .grad no longer views the captured gradient "
+                                   "buffer (do not zero_grad / replace grads between graph steps)")
         self._refill()
         self.graph.replay()
         self.opt.step()
-        return self.loss
+        return self.loss.clone()
 
     def close(self):
-        """Back to the model's own dropout draws (the graph and its buffers are released).
-        Synchronises first and releases the graph at once, so its executable (and the events and
-        streams its capture referenced) are never torn down by a later garbage collection while
-        other work is in flight."""
+        """Back to the model's own dropout draws; the graph, then the events, the engine reference
+        and the owned capture stream are released, each only once the device is idle."""
+        if self.graph is None and getattr(self, "_stream", None) is None:
+            return
         torch.cuda.synchronize()
         if self.blocks:
             self.model.set_dropout_scales(None)
         graph, self.graph = self.graph, None
         del graph
         torch.cuda.synchronize()
+        self._events = []
+        self.engine = None
+        stream, self._stream = getattr(self, "_stream", None), None
+        if stream is not None:
+            stream.close()
+
+    def __del__(self):
+        try:
+            if getattr(self, "graph", None) is not None or getattr(self, "_stream", None) is not None:
+                self.close()
+        except Exception:  # interpreter shutdown
+            pass

@@ -159,6 +159,10 @@ class _BoundaryF1Async:
         from concurrent.futures import ThreadPoolExecutor
         n = workers or max(1, min(8, len(os.sched_getaffinity(0)) - 1))
         self.pool = ThreadPoolExecutor(max_workers=n)
+        # backpressure: at most this many steps in flight; beyond it the oldest is waited for and
+        # folded into the running sum (bounded pinned memory when scoring is slower than the GPU)
+        self.max_inflight = 2 * n
+        self.total = 0.0
         self.cuda = torch.device(device).type == "cuda"  # host tensors (tests): no streams
         self.copy = torch.cuda.Stream(device=device) if self.cuda else None
         self.fence: Optional[torch.cuda.Event] = None
@@ -177,7 +181,12 @@ class _BoundaryF1Async:
         return (torch.empty(shape, dtype=torch.float32, pin_memory=True),
                 torch.empty(shape, dtype=torch.float32, pin_memory=True))
 
+    def _drain(self, keep: int) -> None:
+        while len(self.futures) > keep:
+            self.total += self.futures.pop(0).result()[0]
+
     def submit(self, outputs: torch.Tensor, masks: torch.Tensor):
+        self._drain(self.max_inflight - 1)
         B, H, W = outputs.shape[0], outputs.shape[-2], outputs.shape[-1]
         if not self.cuda:
             hp = outputs.detach().reshape(B, H, W).float().clone()
@@ -210,8 +219,8 @@ class _BoundaryF1Async:
 
     def collect(self) -> float:
         """Sum of the per-sample scores submitted so far (waits for the host threads)."""
-        tot = sum(f.result()[0] for f in self.futures)
-        self.futures = []
+        self._drain(0)
+        tot, self.total = self.total, 0.0
         return tot
 
     def close(self):

@@ -342,6 +342,10 @@ class UNetEngine:
         self._offsets = {id(mod._parameters[pn]): (o, n) for mod, pn, _, _, o, n in model._entries}
         self.last_grad_mode = None
         self.pending_head = None  # dL/du tensor whose head backward already ran fused with the loss
+        # HIP events created while a graph capture runs: the captured graph's cross-stream edges
+        # were recorded through them, so they are kept (and handed to the StepGraph that owns the
+        # graph) instead of being destroyed mid-capture when the local reference goes
+        self.capture_events: List[torch.cuda.Event] = []
 
     # ---- planning -----------------------------------------------------------
     def _plan(self, B: int, H: int, W: int, dev: torch.device):
@@ -384,7 +388,10 @@ class UNetEngine:
         self.ws_bytes = self.ws.numel() * 4
         # weight gradients run on a second stream beside the input-gradient chain (backward)
         self.ws2 = torch.empty_like(self.ws) if self.side_stream else self.ws
-        self.side = torch.cuda.Stream(device=dev) if self.side_stream else None
+        # an owned stream, not one of torch's pooled ones: it takes part in any graph capture of
+        # the step (graph.StepGraph), and is destroyed with the engine rather than handed on
+        self._side_owner = _hip.OwnedStream(device=dev) if self.side_stream else None
+        self.side = self._side_owner.stream if self.side_stream else None
         # pis_conv3x3_bwd_prep writes a layer's weight-gradient dz transform from the MAIN stream
         # while the side stream may still read the previous layer's: two alternating workspaces
         # for those weight gradients, each reused only after the side stream has finished with it
@@ -451,10 +458,16 @@ class UNetEngine:
                 conv, Hl, Wl, buf = table[cid]
                 call("pis_conv3x3_filter", conv.weight.data_ptr(), self.B, Hl, Wl, conv.in_channels,
                      conv.out_channels, dgrad, buf.data_ptr(), buf.numel() * 4, side.cuda_stream)
-                ev = torch.cuda.Event()
+                ev = self._event()
                 ev.record(side)
                 events[cid] = ev
         return events
+
+    def _event(self) -> torch.cuda.Event:
+        ev = torch.cuda.Event()
+        if torch.cuda.is_current_stream_capturing():
+            self.capture_events.append(ev)
+        return ev
 
     def _gbuf(self, name: str, *shape) -> torch.Tensor:
         t = self.gbufs.get(name)
@@ -652,7 +665,7 @@ class UNetEngine:
         def to_side():
             """Order the side stream after everything enqueued on the main stream so far."""
             if side is not main:
-                ev = torch.cuda.Event()
+                ev = self._event()
                 ev.record(main)
                 side.wait_event(ev)
 
@@ -701,7 +714,7 @@ class UNetEngine:
                      self._gptr(conv.bias), B, Hl, Wl, conv.in_channels, conv.out_channels,
                      acc | (PIS_WINO_PREPARED if prep else 0), wsw, wswb, ptr(kept), sst)
                 if prep and side is not main:
-                    ev = torch.cuda.Event()
+                    ev = self._event()
                     ev.record(side)
                     self.ws3_free[(nprep[0] - 1) & 1] = ev
                 ready_on_side(conv.weight, conv.bias)
@@ -731,7 +744,7 @@ class UNetEngine:
             # the weight gradient (MFMA-bound) starts after the input gradient's contractions
             # ("gemm": overlapping the HBM-bound output transform) or after the whole input
             # gradient ("dgrad"); it only needs dz's transforms, which precede either point
-            ev = torch.cuda.Event()
+            ev = self._event()
             ev.record(main)
             if sync == "gemm":
                 lib.pis_arm_gemm_event(ev.cuda_event)

@@ -2,6 +2,7 @@
 one-line JSON contract (metric, whole-job value, roofline with the dominant kernel, cpu_baseline)."""
 import importlib.util
 import json
+import math
 import os
 import subprocess
 import sys
@@ -36,6 +37,8 @@ def test_bench_json_contract():
         assert k in d, k
     assert d["n_gpus"] == 1 and d["steps"] == 2 and d["scaling"] == "weak" and d["higher_is_better"] is True
     assert abs(d["value"] - 8 * 1000.0 / d["ms_per_step"]) < 1e-6 * d["value"]  # B = 8 images per step
+    assert d["dtype"].startswith("fp32")
+    assert math.isfinite(d["final_loss"]) and 0.0 < d["final_loss"] < 10.0  # the timed steps trained
     # "roofline" is the dominant one of the two conv kernels (the most GPU time per step); both are
     # reported, each against its own bound, with per-launch shapes matching the hook's launch counts
     assert d["roofline"] is d[d["roofline_dominant"]] or d["roofline"] == d[d["roofline_dominant"]]

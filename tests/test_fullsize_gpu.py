@@ -4,6 +4,11 @@
   every parameter gradient. This exercises the large-grid code paths the small tests cannot:
   split-K slab counts proportional to the grid, the slab reduction trees, the two alternating
   weight-gradient workspaces and the side-stream ordering.
+* C2 itself (B = 8, 512 x 512, Stage II, injected Dropout2d): the batch BASELINE's metric is
+  quoted on. Split counts, slab-reduction regimes and the chunked two-pass bias reduction of the
+  weight gradients scale with B H W (csrc/wgrad.hip), so B = 8 reaches code paths B = 1 never
+  does. Forward, every loss term, the per-sample Dice / IoU counters, every parameter gradient and
+  one AdamW step (src/train.py:108-167).
 * C5 shape (1024 x 1024, lambda_RD = 1e-3, lambda_PF = 0) at the ends of the S2 sweep, D = 0.5
   and D = 100 (run_ablation.py:176-188): the same checks.
 * L_RD at C2 (src/pde.py:124-145): D Lap(u) + f(u) of a near-constant random-init u cancels,
@@ -27,16 +32,16 @@ def rel(a, b):
     return ((a - b).norm() / max(b.norm().item(), 1e-30)).item()
 
 
-def _run(H, W, loss_kws, seed):
+def _run(H, W, loss_kws, seed, B=1, keep_net=False):
     """One HIP training step per loss config (same weights, same dropout masks) and the float64
     oracle on the first run's decisions (one forward, one backward per config)."""
     from physics_informed_image_segmentation_amd import DiceBCEPDELoss, UNet
-    img, mask = rt.synthetic_batch(1, H, W, seed=seed)
+    img, mask = rt.synthetic_batch(B, H, W, seed=seed)
     torch.manual_seed(seed)
     ref = rt.UNetRef(1, 1, 64).train()
     torch.manual_seed(seed)
     net = UNet(1, 1, 64).cuda().train()
-    scales = rt.make_drop_scales(ref, 1, torch.Generator().manual_seed(seed))
+    scales = rt.make_drop_scales(ref, B, torch.Generator().manual_seed(seed))
     net.set_dropout_scales(scales)
     hip_runs = []
     decisions = None
@@ -50,7 +55,8 @@ def _run(H, W, loss_kws, seed):
         if decisions is None:
             decisions = net.activation_decisions()
         hip_runs.append((u.detach().cpu(), net.last_logits.detach().cpu(), crit.last["terms"].cpu(),
-                         {n: p.grad.detach().cpu().clone() for n, p in net.named_parameters()}))
+                         {n: p.grad.detach().cpu().clone() for n, p in net.named_parameters()},
+                         crit.last["counts"].cpu()))
     ref64 = rt.UNetRef().double().train()
     ref64.load_state_dict(ref.state_dict())
     record = {}
@@ -64,11 +70,13 @@ def _run(H, W, loss_kws, seed):
         t64["loss"].backward(retain_graph=True)
         truth.append(({k: float(v) for k, v in t64.items()},
                       {n: q.grad.detach().clone() for n, q in ref64.named_parameters()}))
+    if keep_net:
+        return img, mask, ref, scales, hip_runs, p64, z64, flips, truth, net
     return img, mask, ref, scales, hip_runs, p64, z64, flips, truth
 
 
 def _check_step(hip_run, p64, z64, truth, flips, npx, skip_terms=()):
-    u, z, terms, grads = hip_run
+    u, z, terms, grads, _ = hip_run
     t64, g64 = truth
     assert rel(z, z64) < TOL and rel(u, p64) < TOL
     for i, k in enumerate(("loss", "dice_loss", "bce_loss", "pde_loss", "phase_field_loss")):
@@ -108,3 +116,48 @@ def test_c5_train_step_d_sweep_ends(hip):
         rd64, rd_hip = tr[0]["pde_loss"], run[2][3].item()
         print(f"L_RD at C5, D={kw['D']}: fp64 {rd64:.9e}  HIP {rd_hip:.9e}  fp32 oracle {rd32:.9e}")
         assert abs(rd_hip - rd64) <= max(10.0 * abs(rd32 - rd64), TOL * abs(rd64)), kw
+
+
+def test_c2_batch8_train_step(hip):
+    """BASELINE configs[1] exactly: B = 8, 512 x 512, Stage II (lambda_RD = lambda_PF = 1e-4, D = 5,
+    a = 0.5, eps = 0.05), train mode with injected Dropout2d masks. Logits, probabilities, every
+    loss term (L_RD bounded by the fp32 oracle's own error), every parameter gradient against
+    float64 on the HIP decisions, the per-sample Dice / IoU counters (src/metrics.py:57-71,
+    src/evaluate.py:81-95) and one AdamW step over the arena (src/train.py:722-726, lr 1e-5)."""
+    from physics_informed_image_segmentation_amd import AdamW
+    kw = dict(rd_w=1e-4, pf_w=1e-4, D=5.0, a=0.5, eps=0.05)
+    B = 8
+    img, mask, ref, scales, runs, p64, z64, flips, truth, net = _run(512, 512, [kw], seed=42, B=B, keep_net=True)
+    _check_step(runs[0], p64, z64, truth[0], flips, B * 512 * 512, skip_terms=("pde_loss",))
+    u, z, terms, grads, counts = runs[0]
+    with torch.no_grad():
+        p32 = ref(img, scales)
+    rd32 = rt.rd_loss(p32.double(), 5.0, 0.5).item()
+    rd64, rd_hip = truth[0][0]["pde_loss"], terms[3].item()
+    print(f"L_RD at C2 B=8: fp64 {rd64:.9e}  HIP {rd_hip:.9e}  fp32 oracle {rd32:.9e}")
+    assert abs(rd_hip - rd64) <= max(10.0 * abs(rd32 - rd64), TOL * abs(rd64))
+    # metric counters: exact integers of thresholding the HIP probabilities themselves ...
+    pb, tb = (u > 0.5).reshape(B, -1), mask.reshape(B, -1) > 0.5
+    inter = (pb & tb).sum(1)
+    assert torch.equal(counts[:, 0].long(), inter) and torch.equal(counts[:, 1].long(), pb.sum(1))
+    assert torch.equal(counts[:, 2].long(), tb.sum(1))
+    # ... and the reference's Dice / IoU on its own fp32 probabilities to 1e-4 (a pixel within
+    # fp32 rounding of the 0.5 threshold may flip: the counts may differ by a few)
+    d_hip = (2.0 * inter + 1e-6) / (pb.sum(1) + tb.sum(1) + 1e-6)
+    assert torch.allclose(d_hip.double(), rt.dice_score_batch(p32, mask).double(), rtol=1e-4, atol=1e-6)
+    iou_hip = (inter + 1e-6) / (pb.sum(1) + tb.sum(1) - inter + 1e-6)
+    assert torch.allclose(iou_hip.double(), rt.iou_batch(p32, mask).double(), rtol=1e-4, atol=1e-6)
+    # one AdamW step at C2's Stage-II learning rate over the 20.5 M-parameter arena, against
+    # torch.optim.AdamW fed the same gradients (src/train.py:722-726)
+    opt = AdamW(net.parameters(), lr=1e-5, weight_decay=1e-5)
+    w0 = {n: p.detach().cpu().clone() for n, p in net.named_parameters()}
+    opt.step()
+    torch.cuda.synchronize()
+    cpu = rt.UNetRef(1, 1, 64)
+    cpu.load_state_dict(w0)
+    for n, q in cpu.named_parameters():
+        q.grad = grads[n].clone()
+    rt.make_adamw(cpu, lr=1e-5, weight_decay=1e-5).step()
+    worst = max((((p.detach().cpu() - q.detach()).norm() / q.detach().norm()).item(), n)
+                for (n, p), q in zip(net.named_parameters(), cpu.parameters()))
+    assert worst[0] < 1e-6, worst

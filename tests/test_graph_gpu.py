@@ -62,3 +62,60 @@ def test_graph_step_takes_new_batches(hip):
     del sg, m, o
     gc.collect()
     torch.cuda.synchronize()
+
+
+def test_graph_dropped_without_close(hip):
+    """StepGraph lifetime (graph.py): dropped WITHOUT close() and garbage collected, it releases
+    the graph, then the capture's events, its engine reference and its owned capture stream; no
+    stream the capture used is left in capture state; eager steps then run on the same model
+    (whose engine and weight-gradient stream it no longer holds) and on a new model."""
+    from physics_informed_image_segmentation_amd.graph import StepGraph
+    m, o, crit, x, t = _setup(0.2)
+    sg = StepGraph(m, crit, o, x, t, warmup=1)
+    l1 = sg.step()
+    l2 = sg.step()
+    assert l1.data_ptr() != l2.data_ptr()  # each step returns its own loss tensor
+    cap, side = sg._stream, m.engine()._side_owner
+    assert cap.capture_status() == 0 and side.capture_status() == 0
+    assert len(sg._events) > 0  # the capture's cross-stream events are owned by the StepGraph
+    del sg
+    gc.collect()
+    assert cap.handle is None  # closed (its stream destroyed) by the collector
+    assert side.capture_status() == 0
+    for _ in range(2):  # the same model, eagerly
+        o.zero_grad(set_to_none=True)
+        loss = crit(m(x), t)
+        loss.backward()
+        o.step()
+    assert torch.isfinite(loss).item()
+    m2, o2, crit2, x2, t2 = _setup(0.2)
+    o2.zero_grad(set_to_none=True)
+    crit2(m2(x2), t2).backward()
+    o2.step()
+    torch.cuda.synchronize()
+    assert all(torch.isfinite(p).all().item() for p in m2.parameters())
+
+
+def test_graph_refuses_data_parallel_and_detached_grads(hip):
+    """A StepGraph refuses a model with a data-parallel gradient hook (its all-reduces cannot be
+    replayed), and a step raises when the parameters' .grad were replaced after the capture."""
+    from physics_informed_image_segmentation_amd.graph import StepGraph
+    m, o, crit, x, t = _setup(0.0)
+
+    class Hook:
+        def on_ready(self, lo, hi):
+            pass
+
+        def finish(self):
+            pass
+
+    m.grad_ready_hook = Hook()
+    with pytest.raises(RuntimeError, match="data-parallel"):
+        StepGraph(m, crit, o, x, t, warmup=1)
+    m.grad_ready_hook = None
+    sg = StepGraph(m, crit, o, x, t, warmup=1)
+    sg.step()
+    o.zero_grad(set_to_none=True)
+    with pytest.raises(RuntimeError, match="captured gradient"):
+        sg.step()
+    sg.close()

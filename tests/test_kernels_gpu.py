@@ -657,6 +657,46 @@ def test_winograd_wgrad_bf16x6_is_fp32_accurate(hip, Cin, Cout):
         assert errs[v] < 5e-6, errs
 
 
+@pytest.mark.parametrize("Cin,Cout", [(64, 64), (256, 128)])
+def test_wgrad_fp16x3_mixed_magnitude_samples(hip, Cin, Cout):
+    """fp16x3 weight-gradient GEMM (pis_tune(14, 2)) over a batch whose first sample's dz is ~1
+    and whose second sample's is ~1e-30 (then the reverse): the contraction runs over pixels, so
+    one wave's scale jumps by ~2^100 between K-steps. The rise is capped at 2^32 above the largest
+    operands already accumulated (common.h h3_keep), so the partial sums are re-expressed without
+    overflow: dW and db finite and as accurate as the native fp32 MFMA path against float64."""
+    B, H, W = 2, 16, 32
+    g = torch.Generator().manual_seed(59)
+    x = F.relu(torch.randn(B, Cin, H, W, generator=g, dtype=torch.float64))
+    for order in ((1.0, 1e-30), (1e-30, 1.0)):
+        dz = torch.randn(B, Cout, H, W, generator=g, dtype=torch.float64)
+        dz[0] *= order[0]
+        dz[1] *= order[1]
+        dz = dz.float().double()  # the exact fp32 inputs
+        dw_ref = torch.nn.grad.conv2d_weight(x.float().double(), (Cout, Cin, 3, 3), dz, padding=1)
+        db_ref = dz.sum(dim=(0, 2, 3))
+        xd, dzd = nhwc(x.float()).cuda(), nhwc(dz.float()).cuda()
+        errs = {}
+        for v in (0, 2):
+            prev = hip.pis_tune(14, v)
+            try:
+                nws = hip.pis_conv3x3_wgrad_ws(B, H, W, Cin, Cout)
+                ws = torch.empty(nws // 4 + 1, device="cuda")
+                dw = torch.empty(Cout, 3, 3, Cin, device="cuda")
+                db = torch.empty(Cout, device="cuda")
+                rc = hip.pis_conv3x3_wgrad(xd.data_ptr(), Cin, dzd.data_ptr(), Cout, dw.data_ptr(), db.data_ptr(),
+                                           B, H, W, Cin, Cout, 0, ws.data_ptr(), nws, s())
+                assert rc == 0, hip.pis_last_error()
+                torch.cuda.synchronize()
+            finally:
+                hip.pis_tune(14, prev)
+            dwc = dw.cpu().permute(0, 3, 1, 2).double()
+            assert torch.isfinite(dwc).all() and torch.isfinite(db.cpu()).all(), (order, v)
+            errs[v] = ((dwc - dw_ref).norm() / dw_ref.norm()).item()
+            assert rel_err(db.cpu().double(), db_ref) < 1e-5, (order, v)
+        assert errs[2] <= 1.25 * errs[0] + 1e-9, (order, errs)
+        assert errs[2] < 5e-6, (order, errs)
+
+
 @pytest.mark.parametrize("Cin,Cout", [(128, 64), (512, 256)])
 def test_convt_bf16x6_is_fp32_accurate(hip, Cin, Cout):
     """Transposed conv forward / input gradient (key 13: 1 bf16x6, 3 fp16x3 vs 2 fp32 MFMA) and
