@@ -150,8 +150,9 @@ int pis_arm_gemm_event(void* event);
 /* Owned HIP streams (hipStreamNonBlocking, the given priority: 0 normal, -1 high). torch's
  * torch.cuda.Stream() hands out a fixed round-robin pool, so a stream that took part in a HIP graph
  * capture is later handed to unrelated code; the engine's weight-gradient stream and the capture
- * stream of a graphed step are owned instead (wrapped with torch.cuda.ExternalStream) and destroyed
- * with their owner. pis_stream_capture_status: hipStreamCaptureStatus (0 none, 1 active,
+ * stream of a graphed step are owned instead (wrapped with torch.cuda.ExternalStream) and recycled
+ * among owners (the Python side never destroys one: PyTorch keeps raw stream handles in autograd
+ * nodes and allocator blocks). pis_stream_capture_status: hipStreamCaptureStatus (0 none, 1 active,
  * 2 invalidated) or a negative error. */
 int pis_stream_create(int priority, pis_stream_t* out);
 int pis_stream_destroy(pis_stream_t stream);

@@ -167,50 +167,50 @@ def call(name: str, *args) -> None:
     tr.end(tok)
 
 
-_stream_graveyard = []  # owned streams released while a capture was running: destroyed later
-
-
-def _capturing() -> bool:
-    try:
-        return torch.cuda.is_current_stream_capturing()
-    except Exception:
-        return False
-
-
-def _bury() -> None:
-    """Destroy the owned streams whose release had to wait for a capture to end."""
-    while _stream_graveyard and not _capturing():
-        h = _stream_graveyard.pop()
-        lib().pis_stream_destroy(h)
+_free_streams = []  # owned streams no longer in use: handed to the next OwnedStream, never destroyed
 
 
 class OwnedStream:
     """A HIP stream this process owns (pis_stream_create), usable as a torch stream
-    (``.stream`` is a torch.cuda.ExternalStream) and destroyed by ``close()`` — after its work
-    drains — instead of returning to torch's round-robin stream pool, where a stream that took
-    part in a graph capture would later be handed to unrelated code. Released during a capture
-    (synchronising is illegal then), it is destroyed after the capture instead."""
+    (``.stream`` is a torch.cuda.ExternalStream). torch's ``torch.cuda.Stream()`` hands out a
+    fixed round-robin pool, so a stream that took part in a graph capture would later be given to
+    unrelated code; an owned stream is recycled only into other OwnedStreams (``close()`` returns
+    it to a free list after its work drains). It is never destroyed: PyTorch keeps raw stream
+    handles beyond the objects that used them — autograd's AccumulateGrad nodes record the stream
+    of the forward that created them and sync with it in every later backward, and the caching
+    allocator tags blocks with their allocation stream — so a destroyed stream would leave those
+    handles dangling (tests/test_graph_gpu.py::test_graph_dropped_without_close reproduced exactly
+    that: a segfault in the next eager backward of the graphed model)."""
 
     def __init__(self, device=None, priority: int = 0):
-        _bury()
-        raw = c_void_p()
-        check(lib().pis_stream_create(priority, ctypes.byref(raw)), "pis_stream_create")
-        self.handle = raw.value
+        self.handle = None
+        for i, (h, p) in enumerate(_free_streams):
+            if p == priority:
+                self.handle = _free_streams.pop(i)[0]
+                break
+        if self.handle is None:
+            raw = c_void_p()
+            check(lib().pis_stream_create(priority, ctypes.byref(raw)), "pis_stream_create")
+            self.handle = raw.value
+        self.priority = priority
         self.stream = torch.cuda.ExternalStream(self.handle, device=device)
 
     def capture_status(self) -> int:
         return lib().pis_stream_capture_status(self.handle)
 
     def close(self) -> None:
+        """Return the stream to the free list once its queued work is done (no sync inside a capture:
+        the work is then waited for by whoever takes the stream next, in stream order)."""
         h, self.handle = self.handle, None
         if not h:
             return
-        if _capturing():
-            _stream_graveyard.append(h)
-            return
-        self.stream.synchronize()
-        check(lib().pis_stream_destroy(h), "pis_stream_destroy")
-        _bury()
+        try:
+            capturing = torch.cuda.is_current_stream_capturing()
+        except Exception:
+            capturing = False
+        if not capturing:
+            self.stream.synchronize()
+        _free_streams.append((h, self.priority))
 
     def __del__(self):
         try:

@@ -35,12 +35,15 @@ class StepGraph:
 
     Lifetime. A captured graph references everything its capture touched: the engine's
     activation / workspace buffers, its weight-gradient stream, the capture stream and the HIP
-    events through which the two streams' edges were recorded. The StepGraph owns all of them —
-    the engine, the events (``UNetEngine.capture_events``) and two streams of its own
-    (``_hip.OwnedStream``: torch's ``torch.cuda.Stream()`` hands out a round-robin pool, so a
-    pooled capture stream would later be given to unrelated code) — and releases them in
-    ``close()`` only after the device is idle and the graph is destroyed, in that order.
-    ``close()`` also runs when the StepGraph is garbage collected without it."""
+    events through which the two streams' edges were recorded; the captured loss's autograd graph
+    holds the parameters' AccumulateGrad nodes, which recorded the capture stream and sync with it
+    in every later backward of the model while they live. The StepGraph owns all of them — the
+    engine, the events (``UNetEngine.capture_events``), the loss (``step()`` hands out detached
+    copies, so no caller keeps that autograd graph alive) and the capture stream
+    (``_hip.OwnedStream``, recycled only into other owned streams, never destroyed) — and releases
+    them in ``close()`` only after the device is idle: the graph, the loss and its autograd graph,
+    the events, the engine, then the stream. ``close()`` also runs when the StepGraph is garbage
+    collected without it."""
 
     def __init__(self, model: UNet, criterion, optimizer, x: torch.Tensor, target: torch.Tensor, warmup: int = 2):
         if not x.is_cuda:
@@ -112,7 +115,7 @@ class StepGraph:
         self._refill()
         self.graph.replay()
         self.opt.step()
-        return self.loss.clone()
+        return self.loss.detach().clone()
 
     def close(self):
         """Back to the model's own dropout draws; the graph, then the events, the engine reference
@@ -124,6 +127,7 @@ class StepGraph:
             self.model.set_dropout_scales(None)
         graph, self.graph = self.graph, None
         del graph
+        self.loss = None  # its autograd graph (AccumulateGrad nodes on the capture stream) with it
         torch.cuda.synchronize()
         self._events = []
         self.engine = None

@@ -180,7 +180,7 @@ def _per_param(holder, flat):
             for nm, (_, _, shape, kind, o, n) in zip(names, holder._entries)}
 
 
-@pytest.mark.parametrize("bucket_bytes", [16 << 20, 1024])
+@pytest.mark.parametrize("bucket_bytes", [16 << 20, 4])
 def test_two_rank_train_mode_matches_oracle(hip, bucket_bytes):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -192,8 +192,8 @@ def test_two_rank_train_mode_matches_oracle(hip, bucket_bytes):
     for p in procs:
         p.join(timeout=120)
     assert all(p.exitcode == 0 for p in procs)
-    if bucket_bytes == 1024:
-        assert res[0][2] > 40  # (nearly) one bucket per parameter tensor
+    if bucket_bytes == 4:
+        assert res[0][2] == 46  # one bucket per parameter tensor: out_conv's closes on the main stream
     for step in range(2):
         w = res[0][0][step][0]
         assert (w == res[1][0][step][0]).all(), "replicas diverged"  # bitwise-identical replicas

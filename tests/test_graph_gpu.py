@@ -66,9 +66,11 @@ def test_graph_step_takes_new_batches(hip):
 
 def test_graph_dropped_without_close(hip):
     """StepGraph lifetime (graph.py): dropped WITHOUT close() and garbage collected, it releases
-    the graph, then the capture's events, its engine reference and its owned capture stream; no
-    stream the capture used is left in capture state; eager steps then run on the same model
-    (whose engine and weight-gradient stream it no longer holds) and on a new model."""
+    the graph, the captured loss with its autograd graph, the capture's events, its engine
+    reference and its owned capture stream (recycled, not destroyed); no stream the capture used
+    is left in capture state; eager steps then run on the same model and on a new model.
+    (Destroying the capture stream here segfaulted the next eager backward: the parameters'
+    AccumulateGrad nodes, kept alive by a loss tensor the caller still held, had recorded it.)"""
     from physics_informed_image_segmentation_amd.graph import StepGraph
     m, o, crit, x, t = _setup(0.2)
     sg = StepGraph(m, crit, o, x, t, warmup=1)
@@ -78,9 +80,12 @@ def test_graph_dropped_without_close(hip):
     cap, side = sg._stream, m.engine()._side_owner
     assert cap.capture_status() == 0 and side.capture_status() == 0
     assert len(sg._events) > 0  # the capture's cross-stream events are owned by the StepGraph
-    del sg
+    cap_handle = cap.handle
+    del sg, l1, l2
     gc.collect()
-    assert cap.handle is None  # closed (its stream destroyed) by the collector
+    from physics_informed_image_segmentation_amd import _hip as hipmod
+    assert cap.handle is None  # closed by the collector ...
+    assert any(h == cap_handle for h, _ in hipmod._free_streams)  # ... and recycled, never destroyed
     assert side.capture_status() == 0
     for _ in range(2):  # the same model, eagerly
         o.zero_grad(set_to_none=True)
