@@ -128,7 +128,10 @@ int pis_version(void);
 #define PIS_TUNE_FUSED_PAIR 28   /* fused kernel, 64-channel contractions in fp16x3 (key 22), lockstep form: 1 two xi per
                                     barrier (four LDS operand buffers; the two products' MFMA chains interleave),
                                     0 one xi per barrier; bit-for-bit the same sums */
-#define PIS_TUNE_NKEYS 29
+#define PIS_TUNE_DIRECT_H3 29   /* direct 3x3 conv in fp16x3 (csrc/direct.hip; forward and input gradient): 0 off,
+                                   1 auto (the shallow layers: <= 128 channels on both sides, H >= 256),
+                                   2 every shape it covers (H % 8, W % 32, C % 16, N % 64 == 0) */
+#define PIS_TUNE_NKEYS 30
 #define PIS_DEBUG_NOLOAD (1 << 16)
 int pis_tune(int key, int value);
 /* Tooling (tools/bench_gemm.py): time one batched NT GEMM kernel variant in isolation,
@@ -240,6 +243,10 @@ typedef struct pis_filter_job {
 } pis_filter_job;
 #define PIS_FILTER_MAX_JOBS 40
 int pis_conv3x3_filters(const pis_filter_job* jobs, int n, pis_stream_t stream);
+/* 1 when pis_conv3x3_dgrad_ex of these shapes (and workspace) runs the direct fp16x3 kernel
+ * (pis_tune key 29), which accepts PIS_W_UNFLIPPED (the original weights) without
+ * PIS_WINO_PREPARED; 0 otherwise. */
+int pis_conv3x3_dgrad_direct(int B, int H, int W, int Cin, int Cout, int ldz, size_t ws_bytes);
 int pis_conv3x3_bwd_prep(const float* dz, int ldz, int B, int H, int W, int Cin, int Cout, void* ws_dgrad,
                          size_t ws_dgrad_bytes, void* ws_wgrad, size_t ws_wgrad_bytes, pis_stream_t stream);
 size_t pis_conv3x3_wgrad_ws(int B, int H, int W, int Cin, int Cout);

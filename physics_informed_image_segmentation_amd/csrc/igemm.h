@@ -76,6 +76,14 @@ int wino_dz_blocks(int B, int H, int W, int N, int m);
 int launch_wino_wgrad_out(const float* M, int N, int C, float* dw, int accumulate, hipStream_t s, int m,
                           int nsplit = 1, int64_t sstride = 0);
 
+// direct 3x3 conv in fp16x3 (direct.hip): shapes it covers, its workspace (split weights), the
+// launch (dgrad_orig: an input gradient whose a.wt holds the ORIGINAL KRSC weights)
+bool direct_h3_shape_ok(int H, int W, int C, int N, int ldx);
+size_t direct_h3_ws_bytes(int C, int N);
+int launch_direct_h3(const IGemmArgs& a, int B, void* ws, size_t ws_bytes, hipStream_t s, bool dgrad_orig);
+// pis_tune key 29's policy for a contraction of C channels into N outputs on an H x W grid
+bool direct_h3_wanted(int H, int W, int C, int N, int ldx);
+
 // transposed-conv GEMMs (convt.hip): 0 = launched, 1 = shape not covered, < 0 = error
 int launch_convt_gemm(int mode, const float* a, int lda, const float* bt, int B, int h, int w, int cin, int cout,
                       const float* bias, const float* mask, int ldm, float* dst, int ldd, int flags,

@@ -569,6 +569,14 @@ static bool wino_wanted_dims(int H, int W, int C, int N) {
 
 static int dispatch_conv3x3(const IGemmArgs& a, int B, void* ws, size_t ws_bytes, hipStream_t s,
                             float* keep_v = nullptr, bool v_ready = false) {
+  // the direct fp16x3 kernel (pis_tune key 29) where its policy takes the layer; a kept forward
+  // transform is then still owed to the layer's Winograd weight gradient
+  if (ws && !a.filter_ready && !v_ready && a.tap_mode == TAP_CONV3 && a.epi == EPI_NHWC &&
+      direct_h3_wanted(a.H, a.W, a.Csrc, a.N, a.lds) && ws_bytes >= direct_h3_ws_bytes(a.Csrc, a.N)) {
+    int rc = launch_direct_h3(a, B, ws, ws_bytes, s, a.w_unflipped != 0);
+    if (!rc && keep_v) rc = launch_wino_input(a.src, a.lds, B, a.H, a.W, a.Csrc, keep_v, s, 4);
+    return rc;
+  }
   // a kept transform is computed either way: then Winograd wins even where the plain policy
   // prefers the direct kernel (64 -> 64 at 512^2: +2 % forward, -27 % weight gradient)
   if (ws && wino_ok(a) && (keep_v || wino_wanted_dims(a.H, a.W, a.Csrc, a.N)) &&
@@ -592,6 +600,8 @@ size_t wino_wgrad_keep_bytes(int B, int H, int W, int Cin, int Cout);  // wgrad.
 
 extern "C" size_t pis_conv3x3_ex_ws(int B, int H, int W, int Cin, int Cout) {
   size_t need = 0;
+  if (direct_h3_wanted(H, W, Cin, Cout, 4)) need = std::max(need, direct_h3_ws_bytes(Cin, Cout));
+  if (direct_h3_wanted(H, W, Cout, Cin, 4)) need = std::max(need, direct_h3_ws_bytes(Cout, Cin));
   const bool keepable = Cin % 4 == 0 && wino_tile(H, W) == 4 && wino_wgrad_keep_bytes(B, H, W, Cin, Cout) > 0;
   if (keepable || wino_wanted_dims(H, W, Cin, Cout)) need = std::max(need, wino_ws_bytes(B, H, W, Cin, Cout));  // fwd
   if (wino_wanted_dims(H, W, Cout, Cin)) need = std::max(need, wino_ws_bytes(B, H, W, Cout, Cin));  // dgrad
@@ -645,7 +655,13 @@ extern "C" int pis_conv3x3_fwd_pool(const float* x, int ldx, const float* w_krsc
   a.epi = EPI_NHWC; a.bias = bias; a.scale = scale; a.dst = y; a.ldd = ldy;
   a.flags = flags & (PIS_RELU | PIS_SCALE);
   a.filter_ready = (flags & PIS_FILTER_READY) != 0;
-  // the F(4x4,3x3) output epilogues pool the tile they just wrote; every other path pools after
+  // the direct fp16x3 kernel and the F(4x4,3x3) output epilogues pool the tile they just wrote;
+  // every other path pools after
+  if (Cin > 1 && ws && !a.filter_ready && direct_h3_wanted(H, W, Cin, Cout, ldx) &&
+      ws_bytes >= direct_h3_ws_bytes(Cin, Cout)) {
+    a.pool = pool;
+    return dispatch_conv3x3(a, B, ws, ws_bytes, (hipStream_t)stream, kept ? keep : nullptr);
+  }
   if (Cin > 1 && ws && wino_ok(a) && wino_tile(H, W) == 4 && (kept || wino_wanted_dims(H, W, Cin, Cout)) &&
       ws_bytes >= wino_ws_bytes(B, H, W, Cin, Cout)) {
     a.pool = pool;
@@ -781,8 +797,9 @@ extern "C" int pis_conv3x3_dgrad_ex(const float* dz, int ldz, const float* w_fli
   a.flags = flags & (PIS_MASK | PIS_SCALE | PIS_ACCUMULATE);
   a.w_unflipped = (flags & PIS_W_UNFLIPPED) != 0;
   a.filter_ready = (flags & PIS_FILTER_READY) != 0;
-  PIS_CHECK_ARG(!a.w_unflipped || (flags & PIS_WINO_PREPARED),
-                "pis_conv3x3_dgrad_ex: PIS_W_UNFLIPPED needs the prepared F(4x4,3x3) path");
+  PIS_CHECK_ARG(!a.w_unflipped || (flags & PIS_WINO_PREPARED) ||
+                    (ws && direct_h3_wanted(H, W, Cout, Cin, ldz) && ws_bytes >= direct_h3_ws_bytes(Cout, Cin)),
+                "pis_conv3x3_dgrad_ex: PIS_W_UNFLIPPED needs the prepared F(4x4,3x3) path or the direct one");
   return dispatch_conv3x3(a, B, ws, ws_bytes, (hipStream_t)stream, nullptr, (flags & PIS_WINO_PREPARED) != 0);
 }
 
@@ -791,7 +808,13 @@ bool pis::dgrad_wino4_planned(int B, int H, int W, int Cin, int Cout, int ldz, s
   a.H = H; a.W = W; a.Csrc = Cout; a.N = Cin; a.lds = ldz; a.ldd = 4; a.ldm = 4;
   a.tap_mode = TAP_CONV3; a.epi = EPI_NHWC;
   return wino_ok(a) && wino_tile(H, W) == 4 && wino_wanted_dims(H, W, Cout, Cin) &&
-         ws_bytes >= wino_ws_bytes(B, H, W, Cout, Cin);
+         ws_bytes >= wino_ws_bytes(B, H, W, Cout, Cin) && !direct_h3_wanted(H, W, Cout, Cin, ldz);
+}
+
+// does pis_conv3x3_dgrad_ex take the direct fp16x3 kernel (which reads the original weights
+// with PIS_W_UNFLIPPED, no flipped copy)?
+extern "C" int pis_conv3x3_dgrad_direct(int B, int H, int W, int Cin, int Cout, int ldz, size_t ws_bytes) {
+  return B > 0 && direct_h3_wanted(H, W, Cout, Cin, ldz) && ws_bytes >= direct_h3_ws_bytes(Cout, Cin);
 }
 
 extern "C" int pis_convt2x2_fwd(const float* x, int ldx, const float* w_ijoc, const float* bias,

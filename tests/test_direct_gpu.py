@@ -1,0 +1,173 @@
+"""The direct 3x3 convolution in fp16x3 (csrc/direct.hip, pis_tune key 29): the forward of
+src/unet.py:29,38's nn.Conv2d (bias, ReLU, Dropout2d keep-scale, the encoder's fused 2x2 max
+pool) and its input gradient (ReLU mask of the conv's input, keep-scale, accumulate; flipped or
+original weights) against float64, as accurate as the native fp32 MFMA direct kernel (key 8 = 0)
+for unit, gradient-sized and large operands and for a region spanning 2^-60 .. 1."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+RELU, SCALE, MASK, ACC, UNFLIPPED = 1, 2, 4, 8, 32
+
+
+def nhwc(t):
+    return t.permute(0, 2, 3, 1).contiguous()
+
+
+def nchw(t):
+    return t.permute(0, 3, 1, 2).contiguous()
+
+
+def krsc(w):
+    return w.permute(0, 2, 3, 1).contiguous()
+
+
+def rel(a, b):
+    a, b = a.double().cpu(), b.double().cpu()
+    return ((a - b).norm() / max(b.norm().item(), 1e-300)).item()
+
+
+def s():
+    return torch.cuda.current_stream().cuda_stream
+
+
+class Knobs:
+    def __init__(self, hip, **kv):
+        self.hip, self.kv, self.prev = hip, kv, {}
+
+    def __enter__(self):
+        for k, v in self.kv.items():
+            self.prev[k] = self.hip.pis_tune(int(k[1:]), v)
+
+    def __exit__(self, *a):
+        for k, v in self.prev.items():
+            self.hip.pis_tune(int(k[1:]), v)
+
+
+DIRECT = dict(k29=2)
+NATIVE = dict(k29=0, k8=0)  # the fp32-MFMA direct halo kernel
+
+
+def _fwd(hip, x, w, b, scale, flags, pool=False, ldx_extra=0):
+    B, Cin, H, W = x.shape
+    Cout = w.shape[0]
+    ldx = Cin + ldx_extra
+    xb = torch.zeros(B, H, W, ldx, device="cuda")
+    xb[..., :Cin] = nhwc(x.float()).cuda()
+    nws = max(hip.pis_conv3x3_ex_ws(B, H, W, Cin, Cout), 4)
+    ws = torch.empty(nws // 4 + 1, device="cuda")
+    y = torch.empty(B, H, W, Cout, device="cuda")
+    wd = krsc(w.float()).cuda()
+    bd = b.float().cuda() if b is not None else None
+    sd = scale.float().cuda() if scale is not None else None
+    if pool:
+        pl = torch.empty(B, H // 2, W // 2, Cout, device="cuda")
+        rc = hip.pis_conv3x3_fwd_pool(xb.data_ptr(), ldx, wd.data_ptr(), bd.data_ptr() if bd is not None else 0,
+                                      sd.data_ptr() if sd is not None else 0, y.data_ptr(), Cout, B, H, W, Cin, Cout,
+                                      flags, ws.data_ptr(), nws, 0, pl.data_ptr(), s())
+    else:
+        rc = hip.pis_conv3x3_fwd_ex(xb.data_ptr(), ldx, wd.data_ptr(), bd.data_ptr() if bd is not None else 0,
+                                    sd.data_ptr() if sd is not None else 0, y.data_ptr(), Cout, B, H, W, Cin, Cout,
+                                    flags, ws.data_ptr(), nws, s())
+    assert rc == 0, hip.pis_last_error()
+    torch.cuda.synchronize()
+    return (nchw(y.cpu()), nchw(pl.cpu())) if pool else nchw(y.cpu())
+
+
+@pytest.mark.parametrize("B,H,W,Cin,Cout", [(2, 16, 64, 64, 64), (1, 8, 32, 128, 64), (2, 16, 32, 64, 128),
+                                           (1, 16, 32, 256, 128)])
+def test_direct_fwd_is_fp32_accurate(hip, B, H, W, Cin, Cout):
+    g = torch.Generator().manual_seed(61)
+    x0 = F.relu(torch.randn(B, Cin, H, W, generator=g, dtype=torch.float64))
+    x0[0, :, :8, :8] *= torch.pow(2.0, -60 * torch.rand(Cin, 8, 8, generator=g, dtype=torch.float64))
+    w = (torch.randn(Cout, Cin, 3, 3, generator=g, dtype=torch.float64) / (3 * Cin ** 0.5)).float().double()
+    b = torch.randn(Cout, generator=g, dtype=torch.float64).float().double()
+    scale = ((torch.rand(B, Cout, generator=g) > 0.2).double() / 0.8).float().double()
+    errs = {}
+    for sc in (1.0, 1e-12, 1e6):
+        x = (x0 * sc).float().double()
+        ref = F.relu(F.conv2d(x, w, b * sc, padding=1)) * scale[:, :, None, None]
+        for name, knobs in (("direct", DIRECT), ("native", NATIVE)):
+            with Knobs(hip, **knobs):
+                y = _fwd(hip, x, w, b * sc, scale, RELU | SCALE)
+            errs[name, sc] = rel(y, ref)
+    for sc in (1.0, 1e-12, 1e6):
+        assert errs["direct", sc] <= 1.25 * errs["native", sc] + 1e-9, errs
+        assert errs["direct", sc] < 2e-6, errs
+
+
+def test_direct_fwd_pool_and_row_pitch(hip):
+    """Encoder conv1 + MaxPool2d(2, 2) in one call (pooled in the epilogue), the input read from a
+    channel slice of a wider buffer (the concat layout), against float64."""
+    B, H, W, Cin, Cout = 2, 16, 64, 64, 128
+    g = torch.Generator().manual_seed(62)
+    x = F.relu(torch.randn(B, Cin, H, W, generator=g, dtype=torch.float64)).float().double()
+    w = (torch.randn(Cout, Cin, 3, 3, generator=g, dtype=torch.float64) / (3 * Cin ** 0.5)).float().double()
+    b = torch.randn(Cout, generator=g, dtype=torch.float64).float().double()
+    with Knobs(hip, **DIRECT):
+        y, pl = _fwd(hip, x, w, b, None, RELU, pool=True, ldx_extra=64)
+    ref = F.relu(F.conv2d(x, w, b, padding=1))
+    assert rel(y, ref) < 2e-6
+    assert torch.equal(pl, F.max_pool2d(y, 2))  # the pool of exactly the values written
+
+
+@pytest.mark.parametrize("B,H,W,Cin,Cout", [(2, 16, 64, 64, 64), (1, 8, 32, 128, 64), (2, 16, 32, 64, 128)])
+@pytest.mark.parametrize("unflipped", [False, True])
+def test_direct_dgrad_is_fp32_accurate(hip, B, H, W, Cin, Cout, unflipped):
+    """dx = conv_input(dz, w) * (x > 0) * keep-scale (+ dx), from a flipped copy of the weights or
+    from the original ones (PIS_W_UNFLIPPED), for gradient-sized and unit dz."""
+    g = torch.Generator().manual_seed(63)
+    x = F.relu(torch.randn(B, Cin, H, W, generator=g, dtype=torch.float64)).float().double()
+    w = (torch.randn(Cout, Cin, 3, 3, generator=g, dtype=torch.float64) / (3 * Cin ** 0.5)).float().double()
+    scale = ((torch.rand(B, Cin, generator=g) > 0.2).double() / 0.8).float().double()
+    dz0 = torch.randn(B, Cout, H, W, generator=g, dtype=torch.float64)
+    xd = nhwc(x.float()).cuda()
+    wd = krsc(w.float()).cuda()
+    wf = torch.empty(Cin * 9 * Cout, device="cuda")
+    assert hip.pis_conv3x3_flip(wd.data_ptr(), wf.data_ptr(), Cin, Cout, s()) == 0
+    sd = scale.float().cuda()
+    errs = {}
+    for sc in (1.0, 1e-9):
+        dz = (dz0 * sc).float().double()
+        ref = torch.nn.grad.conv2d_input(x.shape, w, dz, padding=1) * (x > 0) * scale[:, :, None, None] + 0.5
+        for name, knobs in (("direct", DIRECT), ("native", NATIVE)):
+            with Knobs(hip, **knobs):
+                nws = max(hip.pis_conv3x3_ex_ws(B, H, W, Cin, Cout), 4)
+                ws = torch.empty(nws // 4 + 1, device="cuda")
+                direct = hip.pis_conv3x3_dgrad_direct(B, H, W, Cin, Cout, Cout, nws)
+                assert direct == (name == "direct")
+                use_orig = unflipped and name == "direct"
+                dx = torch.full((B, H, W, Cin), 0.5, device="cuda")
+                rc = hip.pis_conv3x3_dgrad_ex(nhwc(dz.float()).cuda().data_ptr(), Cout,
+                                              (wd if use_orig else wf).data_ptr(), xd.data_ptr(), Cin, sd.data_ptr(),
+                                              dx.data_ptr(), Cin, B, H, W, Cin, Cout,
+                                              MASK | SCALE | ACC | (UNFLIPPED if use_orig else 0), ws.data_ptr(), nws,
+                                              s())
+                assert rc == 0, hip.pis_last_error()
+                torch.cuda.synchronize()
+            errs[name, sc] = rel(nchw(dx.cpu()) - 0.5, ref - 0.5)
+    for sc in (1.0, 1e-9):
+        assert errs["direct", sc] <= 1.25 * errs["native", sc] + 1e-9, errs
+        assert errs["direct", sc] < 2e-6, errs
+
+
+def test_direct_mixed_magnitude_chunks(hip):
+    """The input's scale is chosen per block and 16-channel chunk: channels 0-15 ~1, 16-31 ~1e-30,
+    32-47 ~1e20 — the partial sums are re-expressed at each chunk (rises capped, common.h
+    h3_keep) without overflow, and the result is as accurate as the fp32 MFMA kernel's."""
+    B, H, W, Cin, Cout = 1, 8, 32, 64, 64
+    g = torch.Generator().manual_seed(64)
+    x = torch.randn(B, Cin, H, W, generator=g, dtype=torch.float64)
+    x[:, 16:32] *= 1e-30
+    x[:, 32:48] *= 1e20
+    x = x.float().double()
+    w = (torch.randn(Cout, Cin, 3, 3, generator=g, dtype=torch.float64) / 24).float().double()
+    ref = F.conv2d(x, w, padding=1)
+    out = {}
+    for name, knobs in (("direct", DIRECT), ("native", NATIVE)):
+        with Knobs(hip, **knobs):
+            out[name] = _fwd(hip, x, w, None, None, 0)
+    assert torch.isfinite(out["direct"]).all()
+    assert rel(out["direct"], ref) <= 1.25 * rel(out["native"], ref) + 1e-9
