@@ -223,17 +223,24 @@ __global__ __launch_bounds__(256, 2) void conv3x3_h3_kernel(DirectArgs g) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int row = r0 + 2 * wave + i;
+      const size_t pix0 = ((size_t)b * g.H + row) * g.W + c0 + 4 * lh;
+      // every load of the block first (mask, accumulate source), then the stores: y may alias
+      // them as far as the compiler knows, so interleaved they would serialise on each load
+      float mk[16], old[16];
 #pragma unroll
       for (int reg = 0; reg < 16; ++reg) {
-        const int col = c0 + (reg & 3) + 8 * (reg >> 2) + 4 * lh;
-        const size_t pix = ((size_t)b * g.H + row) * g.W + col;
+        const size_t pix = pix0 + (reg & 3) + 8 * (reg >> 2);
+        mk[reg] = (g.flags & PIS_MASK) ? g.mask[pix * g.ldm + n] : 1.f;
+        old[reg] = (g.flags & PIS_ACCUMULATE) ? g.y[pix * g.ldy + n] : 0.f;
+      }
+#pragma unroll
+      for (int reg = 0; reg < 16; ++reg) {
+        const size_t pix = pix0 + (reg & 3) + 8 * (reg >> 2);
         float v = (acc[i][j][reg] * inv_s) * wi + bias;
         if (g.flags & PIS_RELU) v = fmaxf(v, 0.f);
-        if ((g.flags & PIS_MASK) && !(g.mask[pix * g.ldm + n] > 0.f)) v = 0.f;
-        v *= sc;
-        float* dst = g.y + pix * g.ldy + n;
-        if (g.flags & PIS_ACCUMULATE) v += *dst;
-        *dst = v;
+        if (!(mk[reg] > 0.f)) v = 0.f;
+        v = v * sc + old[reg];
+        g.y[pix * g.ldy + n] = v;
         if constexpr (POOL) {
           if (reg & 1) pm[i][reg >> 1] = fmaxf(pm[i][reg >> 1], v);
           else pm[i][reg >> 1] = v;
@@ -294,6 +301,265 @@ int launch_direct_h3(const IGemmArgs& a, int B, void* ws, size_t ws_bytes, hipSt
     hipLaunchKernelGGL(conv3x3_h3_kernel<false>, dim3(blocks), dim3(256), 0, s, g);
   launch_hook("direct_h3", 1, s, flop);
   return launch_status("conv3x3_h3");
+}
+
+
+// =============================================================================================
+// Weight gradient of the direct conv (src/unet.py:29,38's backward w.r.t. the conv's weight and
+// bias): dW[n][r][s][c] = sum_p dz[p][n] x[p + (r-1, s-1)][c], db[n] = sum_p dz[p][n], in fp16x3.
+// GEMM view: rows n (64 per block), columns (tap, c) (9 x 64 per block), contraction over pixels.
+// A block walks pixel tiles of 4 rows x 32 columns (split-K: tiles split, split + splits, ...):
+// per tile the dz tile (128 px x 64 n) and the x halo (6 x 34 px x 64 c), each in hi / lo fp16
+// planes with one power-of-two scale per tile and operand (block-wide max, h3_keep), are staged
+// in LDS as [pixel][channel] rows, and the MFMA operands — k = 8 consecutive pixels of one channel
+// per lane — come out of them by transposed reads (ds_read_b64_tr_b16: 4 pixels x 16 channels per
+// 16-lane group), the tap shift being a per-lane row address. Wave w: n-half w >> 1, c-half w & 1,
+// all 9 taps (9 accumulator tiles of 32 x 32). One block per CU (85 KB LDS, ~290 registers per
+// lane), the next tile's global loads in flight during this tile's 216 MFMAs per wave. Partial
+// sums per block go to fp32 slabs [split][Cout][9][Cin] (reduce_slabs: fixed order, deterministic)
+// and the bias partials to [split][Cout].
+// LDS rows are 128 B (64 fp16); the 16-B chunk index is XORed with bit 1 of the row, shifted to
+// bit 2: a transposed read's 32-lane half (4 consecutive rows x 64 B) then hits 64 distinct banks.
+// =============================================================================================
+
+struct DirectWArgs {
+  const float* x;
+  int ldx;
+  const float* dz;
+  int ldz;
+  float* part;       // [splits][Cout][9][Cin]
+  float* part_bias;  // [splits][Cout] or NULL
+  int B, H, W, Cin, Cout, splits;
+};
+
+constexpr int WT_H = 4, WT_W = 32, WT_P = WT_H * WT_W, WH_H = WT_H + 2, WH_W = WT_W + 2, WH_P = WH_H * WH_W;
+constexpr int WZ_HALFS = WT_P * 64, WX_HALFS = WH_P * 64;                 // per plane
+constexpr int WZ_ITEMS = WT_P * 8, WX_ITEMS = WH_P * 8;                   // 8-channel groups
+constexpr int WZ_PER_T = WZ_ITEMS / 256, WX_PER_T = (WX_ITEMS + 255) / 256;  // 4, 7
+constexpr int WLDS_BYTES = 2 * (WZ_HALFS + WX_HALFS) * 2;
+
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+
+// element offset of channel group (16-B chunk) ch of row `row` in a [row][64] fp16 image
+__device__ __forceinline__ int wsw64(int row, int ch) { return row * 64 + 8 * (ch ^ (((row >> 1) & 1) << 2)); }
+
+// 4 consecutive fp16 of one row (8-B aligned) read transposed across the 16-lane group
+__device__ __forceinline__ s16x4 tr_read(const _Float16* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(p));
+}
+
+__global__ __launch_bounds__(256, 1) void conv3x3_wgrad_h3_kernel(DirectWArgs g) {
+  __shared__ __attribute__((aligned(16))) char smem[WLDS_BYTES + 64];
+  _Float16* sz = reinterpret_cast<_Float16*>(smem);                        // [plane][128][64]
+  _Float16* sx = reinterpret_cast<_Float16*>(smem + 2 * WZ_HALFS * 2);     // [plane][204][64]
+  float* red = reinterpret_cast<float*>(smem + WLDS_BYTES);                // [2][4] wave maxima
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wi = wave >> 1, wj = wave & 1;  // n-half, c-half
+  const int ncb = g.Cin / 64, pairs = (g.Cout / 64) * ncb;
+  const int pair = blockIdx.x % pairs, split = blockIdx.x / pairs;
+  const int n0 = (pair / ncb) * 64, c0 = (pair % ncb) * 64;
+  const int tw_n = g.W / WT_W, per_img = (g.H / WT_H) * tw_n, ntile = g.B * per_img;
+  const bool do_bias = g.part_bias != nullptr && c0 == 0;
+
+  f32x4 zr[WZ_PER_T][2], xr[WX_PER_T][2];
+  auto gload = [&](int t) {
+    const int b = t / per_img, rem = t - b * per_img, pr0 = (rem / tw_n) * WT_H, pc0 = (rem % tw_n) * WT_W;
+    const size_t img = (size_t)b * g.H * g.W;
+#pragma unroll
+    for (int j = 0; j < WZ_PER_T; ++j) {
+      const int i = tid + 256 * j, px = i >> 3, cg = i & 7;
+      const float* p = g.dz + (img + (size_t)(pr0 + (px >> 5)) * g.W + pc0 + (px & 31)) * g.ldz + n0 + 8 * cg;
+      zr[j][0] = *reinterpret_cast<const f32x4*>(p);
+      zr[j][1] = *reinterpret_cast<const f32x4*>(p + 4);
+    }
+#pragma unroll
+    for (int j = 0; j < WX_PER_T; ++j) {
+      const int i = tid + 256 * j, q = i >> 3, cg = i & 7;
+      xr[j][0] = xr[j][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (i < WX_ITEMS) {
+        const int qr = q / WH_W, qc = q - qr * WH_W, row = pr0 - 1 + qr, col = pc0 - 1 + qc;
+        if (row >= 0 && row < g.H && col >= 0 && col < g.W) {
+          const float* p = g.x + (img + (size_t)row * g.W + col) * g.ldx + c0 + 8 * cg;
+          xr[j][0] = *reinterpret_cast<const f32x4*>(p);
+          xr[j][1] = *reinterpret_cast<const f32x4*>(p + 4);
+        }
+      }
+    }
+  };
+
+  f32x16 acc[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+  float bs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // bias partials: channels n0 + 8 (tid & 7) + e
+  float sz_cur = 0.f, sx_cur = 0.f, sz_min = __builtin_inff(), sx_min = __builtin_inff();
+
+  // lane roles in the transposed reads: 16-lane group gq, its row q and 8-B column slot p
+  const int gq = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+  const int kh = gq >> 1;  // k half (pixels 8 kh ..)
+  const int cgA = 4 * wi + 2 * (gq & 1) + (p >> 1), cgB = 4 * wj + 2 * (gq & 1) + (p >> 1);
+
+  int t = split;
+  if (t < ntile) gload(t);
+#pragma unroll 1
+  for (; t < ntile; t += g.splits) {
+    // 1. block maxima of the staged operands
+    float mz = 0.f, mx = 0.f;
+#pragma unroll
+    for (int j = 0; j < WZ_PER_T; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) mz = fmaxf(mz, fmaxf(fabsf(zr[j][0][e]), fabsf(zr[j][1][e])));
+#pragma unroll
+    for (int j = 0; j < WX_PER_T; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) mx = fmaxf(mx, fmaxf(fabsf(xr[j][0][e]), fabsf(xr[j][1][e])));
+    mz = wave_max_nonneg(mz);
+    mx = wave_max_nonneg(mx);
+    if (lane == 0) {
+      red[wave] = mz;
+      red[4 + wave] = mx;
+    }
+    if (do_bias) {
+#pragma unroll
+      for (int j = 0; j < WZ_PER_T; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          bs[e] += zr[j][0][e];
+          bs[4 + e] += zr[j][1][e];
+        }
+    }
+    __syncthreads();
+    // 2. this tile's scales; the partial sums re-expressed in them; split into LDS
+    mz = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    mx = fmaxf(fmaxf(red[4], red[5]), fmaxf(red[6], red[7]));
+    const float sz_new = h3_keep(sz_cur, mz, sz_min), sx_new = h3_keep(sx_cur, mx, sx_min);
+    if (sz_cur > 0.f && (sz_new != sz_cur || sx_new != sx_cur)) {
+      const float f = (sz_new / sz_cur) * (sx_new / sx_cur);
+#pragma unroll
+      for (int k = 0; k < 9; ++k) acc[k] *= f;
+    }
+    sz_cur = sz_new;
+    sx_cur = sx_new;
+#pragma unroll
+    for (int j = 0; j < WZ_PER_T; ++j) {
+      const int i = tid + 256 * j, px = i >> 3, cg = i & 7;
+      u32x2 h0, l0, h1, l1;
+      split2h_x4(zr[j][0] * sz_cur, h0, l0);
+      split2h_x4(zr[j][1] * sz_cur, h1, l1);
+      *reinterpret_cast<u32x4*>(&sz[wsw64(px, cg)]) = u32x4{h0[0], h0[1], h1[0], h1[1]};
+      *reinterpret_cast<u32x4*>(&sz[WZ_HALFS + wsw64(px, cg)]) = u32x4{l0[0], l0[1], l1[0], l1[1]};
+    }
+#pragma unroll
+    for (int j = 0; j < WX_PER_T; ++j) {
+      const int i = tid + 256 * j, qq = i >> 3, cg = i & 7;
+      if (i < WX_ITEMS) {
+        u32x2 h0, l0, h1, l1;
+        split2h_x4(xr[j][0] * sx_cur, h0, l0);
+        split2h_x4(xr[j][1] * sx_cur, h1, l1);
+        *reinterpret_cast<u32x4*>(&sx[wsw64(qq, cg)]) = u32x4{h0[0], h0[1], h1[0], h1[1]};
+        *reinterpret_cast<u32x4*>(&sx[WX_HALFS + wsw64(qq, cg)]) = u32x4{l0[0], l0[1], l1[0], l1[1]};
+      }
+    }
+    __syncthreads();
+    // 3. the next tile's loads fly during this tile's MFMAs
+    if (t + g.splits < ntile) gload(t + g.splits);
+#pragma unroll 1
+    for (int ks = 0; ks < 8; ++ks) {  // 16-pixel K-steps: tile row ks >> 1, columns 16 (ks & 1) ..
+      const int rr = ks >> 1, cc0 = 16 * (ks & 1);
+      // A = dz^T (rows n, k pixels): pixels 16 ks + 8 kh + q (+ 4) of the tile, channels of cgA
+      f16x8 a[2];
+#pragma unroll
+      for (int pl = 0; pl < 2; ++pl) {
+        const _Float16* base = sz + pl * WZ_HALFS;
+        const int px = 16 * ks + 8 * kh + q;
+        const s16x4 lo4 = tr_read(base + wsw64(px, cgA) + 4 * (p & 1));
+        const s16x4 hi4 = tr_read(base + wsw64(px + 4, cgA) + 4 * (p & 1));
+        a[pl] = __builtin_bit_cast(f16x8, __builtin_shufflevector(lo4, hi4, 0, 1, 2, 3, 4, 5, 6, 7));
+      }
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) {
+        const int r = tap / 3, s = tap % 3;
+        // B = x (k pixels, columns c): halo pixel (rr + r, cc0 + 8 kh + q (+ 4) + s), channels of cgB
+        f16x8 bb[2];
+        const int hp = (rr + r) * WH_W + cc0 + 8 * kh + q + s;
+#pragma unroll
+        for (int pl = 0; pl < 2; ++pl) {
+          const _Float16* base = sx + pl * WX_HALFS;
+          const s16x4 lo4 = tr_read(base + wsw64(hp, cgB) + 4 * (p & 1));
+          const s16x4 hi4 = tr_read(base + wsw64(hp + 4, cgB) + 4 * (p & 1));
+          bb[pl] = __builtin_bit_cast(f16x8, __builtin_shufflevector(lo4, hi4, 0, 1, 2, 3, 4, 5, 6, 7));
+        }
+        acc[tap] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[1], bb[0], acc[tap], 0, 0, 0);
+        acc[tap] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[0], bb[1], acc[tap], 0, 0, 0);
+        acc[tap] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[0], bb[0], acc[tap], 0, 0, 0);
+      }
+    }
+    __syncthreads();
+  }
+
+  // partial sums / (sz sx) -> slab [split][Cout][9][Cin]: lane column c0 + 32 wj + (lane & 31),
+  // rows n0 + 32 wi + (reg & 3) + 8 (reg >> 2) + 4 (lane >> 5)
+  const float inv = (sz_cur > 0.f) ? (1.f / sz_cur) * (1.f / sx_cur) : 0.f;
+  float* slab = g.part + (size_t)split * g.Cout * 9 * g.Cin;
+  const int c = c0 + 32 * wj + (lane & 31);
+#pragma unroll
+  for (int tap = 0; tap < 9; ++tap)
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+      const int n = n0 + 32 * wi + (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5);
+      slab[((size_t)n * 9 + tap) * g.Cin + c] = acc[tap][reg] * inv;
+    }
+  if (do_bias) {  // fixed-order reduction over the 32 threads of each channel group
+    float* rb = reinterpret_cast<float*>(smem);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) rb[tid * 8 + e] = bs[e];
+    __syncthreads();
+    if (tid < 64) {
+      const int cg = tid >> 3, e = tid & 7;
+      float sum = 0.f;
+      for (int k = 0; k < 32; ++k) sum += rb[(8 * k + cg) * 8 + e];
+      g.part_bias[(size_t)split * g.Cout + n0 + tid] = sum;
+    }
+  }
+}
+
+bool direct_w_wanted(int B, int H, int W, int Cin, int Cout, int ldx, int ldz) {
+  return B > 0 && H % WT_H == 0 && W % WT_W == 0 && Cin % 64 == 0 && Cout % 64 == 0 && ldz % 4 == 0 &&
+         direct_h3_wanted(H, W, Cin, Cout, ldx);
+}
+
+static int direct_w_splits(int B, int H, int W, int Cin, int Cout) {
+  const int pairs = (Cout / 64) * (Cin / 64);
+  const int ntile = B * (H / WT_H) * (W / WT_W);
+  return std::max(1, std::min(ntile, 256 / std::max(1, std::min(pairs, 256))));
+}
+
+size_t direct_w_ws_bytes(int B, int H, int W, int Cin, int Cout) {
+  const int sp = direct_w_splits(B, H, W, Cin, Cout);
+  return (size_t)sp * Cout * 9 * Cin * sizeof(float) + (size_t)sp * Cout * sizeof(float) + 512;
+}
+
+int reduce_slabs(const float* part, int splits, int64_t n, float* dst, int accumulate, hipStream_t s);
+
+int launch_direct_wgrad(const float* x, int ldx, const float* dz, int ldz, float* dw, float* db, int B, int H, int W,
+                        int Cin, int Cout, int acc, void* ws, size_t ws_bytes, hipStream_t s) {
+  if (ws_bytes < direct_w_ws_bytes(B, H, W, Cin, Cout)) return set_error("direct wgrad: workspace too small"), PIS_ERR_ARG;
+  DirectWArgs g{};
+  g.x = x; g.ldx = ldx; g.dz = dz; g.ldz = ldz;
+  g.B = B; g.H = H; g.W = W; g.Cin = Cin; g.Cout = Cout;
+  g.splits = direct_w_splits(B, H, W, Cin, Cout);
+  g.part = reinterpret_cast<float*>(ws);
+  g.part_bias = db ? g.part + (size_t)g.splits * Cout * 9 * Cin : nullptr;
+  const int pairs = (Cout / 64) * (Cin / 64);
+  const double flop = 2.0 * 9 * (double)B * H * W * Cin * Cout;
+  launch_hook("direct_wgrad_h3", 0, s, flop);
+  hipLaunchKernelGGL(conv3x3_wgrad_h3_kernel, dim3(g.splits * pairs), dim3(256), 0, s, g);
+  launch_hook("direct_wgrad_h3", 1, s, flop);
+  int rc = launch_status("conv3x3_wgrad_h3");
+  if (!rc) rc = reduce_slabs(g.part, g.splits, (int64_t)Cout * 9 * Cin, dw, acc, s);
+  if (!rc && db) rc = reduce_slabs(g.part_bias, g.splits, Cout, db, acc, s);
+  return rc;
 }
 
 }  // namespace pis

@@ -83,6 +83,11 @@ size_t direct_h3_ws_bytes(int C, int N);
 int launch_direct_h3(const IGemmArgs& a, int B, void* ws, size_t ws_bytes, hipStream_t s, bool dgrad_orig);
 // pis_tune key 29's policy for a contraction of C channels into N outputs on an H x W grid
 bool direct_h3_wanted(int H, int W, int C, int N, int ldx);
+// ... and for the layer's weight gradient (the direct fp16x3 wgrad kernel): its workspace, launch
+bool direct_w_wanted(int B, int H, int W, int Cin, int Cout, int ldx, int ldz);
+size_t direct_w_ws_bytes(int B, int H, int W, int Cin, int Cout);
+int launch_direct_wgrad(const float* x, int ldx, const float* dz, int ldz, float* dw, float* db, int B, int H, int W,
+                        int Cin, int Cout, int acc, void* ws, size_t ws_bytes, hipStream_t s);
 
 // transposed-conv GEMMs (convt.hip): 0 = launched, 1 = shape not covered, < 0 = error
 int launch_convt_gemm(int mode, const float* a, int lda, const float* bt, int B, int h, int w, int cin, int cout,

@@ -1131,6 +1131,7 @@ static WinoWgradPlan wino_wgrad_plan(int B, int H, int W, int Cin, int Cout) {
 // bytes of the forward's F(4x4,3x3) input transform the weight gradient can take over
 // (pis_conv3x3_keep_bytes): the same B^T on the same 6x6 patches
 size_t wino_wgrad_keep_bytes(int B, int H, int W, int Cin, int Cout) {
+  if (direct_w_wanted(B, H, W, Cin, Cout, 4, 4)) return 0;  // the direct weight gradient reads x itself
   const WinoWgradPlan p = wino_wgrad_plan(B, H, W, Cin, Cout);
   return (p.use && p.m == 4) ? (size_t)p.nxi * p.T * Cin * sizeof(float) : 0;
 }
@@ -1176,6 +1177,7 @@ static int wino_wgrad(const float* x, int ldx, const float* dz, int ldz, float* 
 }
 
 extern "C" size_t pis_conv3x3_wgrad_ws(int B, int H, int W, int Cin, int Cout) {
+  if (direct_w_wanted(B, H, W, Cin, Cout, 4, 4)) return direct_w_ws_bytes(B, H, W, Cin, Cout);
   const WinoWgradPlan wp = wino_wgrad_plan(B, H, W, Cin, Cout);
   if (wp.use) return wp.total;
   const HaloPlan hp = halo_plan(B, H, W, Cin, Cout);
@@ -1204,7 +1206,7 @@ extern "C" int pis_conv3x3_wgrad_keep(const float* x, int ldx, const float* dz, 
   const bool prepared = flags & PIS_WINO_PREPARED;
   PIS_CHECK_ARG(!prepared || (keep && wp.use && wp.m == 4),
                 "pis_conv3x3_wgrad_keep: PIS_WINO_PREPARED needs the kept-transform F(3x3,4x4) path");
-  if (!keep || !(wp.use && wp.m == 4))
+  if (!keep || !(wp.use && wp.m == 4) || (!prepared && direct_w_wanted(B, H, W, Cin, Cout, ldx, ldz)))
     return pis_conv3x3_wgrad(x, ldx, dz, ldz, dw_krsc, db, B, H, W, Cin, Cout, flags, ws, ws_bytes, stream);
   PIS_CHECK_ARG(x && dz && dw_krsc && ldz % 4 == 0, "pis_conv3x3_wgrad_keep: bad arguments");
   PIS_CHECK_ARG(ws && ws_bytes >= wp.total, "pis_conv3x3_wgrad_keep: workspace too small");
@@ -1216,6 +1218,7 @@ extern "C" int pis_conv3x3_bwd_prep(const float* dz, int ldz, int B, int H, int 
                                     void* ws_dgrad, size_t ws_dgrad_bytes, void* ws_wgrad, size_t ws_wgrad_bytes,
                                     pis_stream_t stream) {
   PIS_CHECK_ARG(dz && B > 0 && H > 0 && W > 0 && Cin > 0 && Cout > 0, "pis_conv3x3_bwd_prep: bad arguments");
+  if (direct_w_wanted(B, H, W, Cin, Cout, 4, ldz)) return 0;  // direct kernels read dz themselves
   const WinoWgradPlan wp = wino_wgrad_plan(B, H, W, Cin, Cout);
   if (tune_get(PIS_TUNE_WINO_DZ2) == 0 || !ws_dgrad || !ws_wgrad || !(wp.use && wp.m == 4) ||
       Cin % 64 || Cout % 64 ||  // pis_conv3x3_wgrad_keep's channel contract
@@ -1244,6 +1247,8 @@ extern "C" int pis_conv3x3_wgrad(const float* x, int ldx, const float* dz, int l
   PIS_CHECK_ARG((Cin == 1 || ldx % 4 == 0) && ldz % 4 == 0, "pis_conv3x3_wgrad: ld must be multiples of 4");
   hipStream_t s = (hipStream_t)stream;
   const int acc = flags & PIS_ACCUMULATE;
+  if (direct_w_wanted(B, H, W, Cin, Cout, ldx, ldz) && ws_bytes >= direct_w_ws_bytes(B, H, W, Cin, Cout))
+    return launch_direct_wgrad(x, ldx, dz, ldz, dw_krsc, db, B, H, W, Cin, Cout, acc, ws, ws_bytes, s);
   const WinoWgradPlan wp = wino_wgrad_plan(B, H, W, Cin, Cout);
   if (wp.use && ldx % 4 == 0 && ws_bytes >= wp.total)
     return wino_wgrad(x, ldx, dz, ldz, dw_krsc, db, B, H, W, Cin, Cout, acc, wp, ws, s);

@@ -728,6 +728,8 @@ class UNetEngine:
                         if ev is not None:
                             main.wait_event(ev)
                         wf, flags = self.bfilt[id(conv)][3].data_ptr(), flags | PIS_FILTER_READY
+                elif lib.pis_conv3x3_dgrad_direct(B, Hl, Wl, conv.in_channels, conv.out_channels, dz.ld, wsb):
+                    wf, flags = conv.weight.data_ptr(), flags | PIS_W_UNFLIPPED  # the direct kernel splits it
                 else:
                     wf = flipped(conv).data_ptr()
                 call("pis_conv3x3_dgrad_ex", dz.p, dz.ld, wf,

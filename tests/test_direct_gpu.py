@@ -131,7 +131,8 @@ def test_direct_dgrad_is_fp32_accurate(hip, B, H, W, Cin, Cout, unflipped):
     errs = {}
     for sc in (1.0, 1e-9):
         dz = (dz0 * sc).float().double()
-        ref = torch.nn.grad.conv2d_input(x.shape, w, dz, padding=1) * (x > 0) * scale[:, :, None, None] + 0.5
+        base = 0.5 * sc  # the accumulated-into gradient, of the same magnitude
+        ref = torch.nn.grad.conv2d_input(x.shape, w, dz, padding=1) * (x > 0) * scale[:, :, None, None] + base
         for name, knobs in (("direct", DIRECT), ("native", NATIVE)):
             with Knobs(hip, **knobs):
                 nws = max(hip.pis_conv3x3_ex_ws(B, H, W, Cin, Cout), 4)
@@ -139,7 +140,7 @@ def test_direct_dgrad_is_fp32_accurate(hip, B, H, W, Cin, Cout, unflipped):
                 direct = hip.pis_conv3x3_dgrad_direct(B, H, W, Cin, Cout, Cout, nws)
                 assert direct == (name == "direct")
                 use_orig = unflipped and name == "direct"
-                dx = torch.full((B, H, W, Cin), 0.5, device="cuda")
+                dx = torch.full((B, H, W, Cin), base, device="cuda")
                 rc = hip.pis_conv3x3_dgrad_ex(nhwc(dz.float()).cuda().data_ptr(), Cout,
                                               (wd if use_orig else wf).data_ptr(), xd.data_ptr(), Cin, sd.data_ptr(),
                                               dx.data_ptr(), Cin, B, H, W, Cin, Cout,
@@ -147,7 +148,8 @@ def test_direct_dgrad_is_fp32_accurate(hip, B, H, W, Cin, Cout, unflipped):
                                               s())
                 assert rc == 0, hip.pis_last_error()
                 torch.cuda.synchronize()
-            errs[name, sc] = rel(nchw(dx.cpu()) - 0.5, ref - 0.5)
+            errs[name, sc] = rel(nchw(dx.cpu()).double() - torch.tensor(base, dtype=torch.float32).double(),
+                                 ref - torch.tensor(base, dtype=torch.float32).double())
     for sc in (1.0, 1e-9):
         assert errs["direct", sc] <= 1.25 * errs["native", sc] + 1e-9, errs
         assert errs["direct", sc] < 2e-6, errs
@@ -171,3 +173,94 @@ def test_direct_mixed_magnitude_chunks(hip):
             out[name] = _fwd(hip, x, w, None, None, 0)
     assert torch.isfinite(out["direct"]).all()
     assert rel(out["direct"], ref) <= 1.25 * rel(out["native"], ref) + 1e-9
+
+
+@pytest.mark.parametrize("B,H,W,Cin,Cout", [(2, 16, 64, 64, 64), (1, 8, 32, 128, 64), (2, 16, 32, 64, 128),
+                                           (1, 16, 32, 128, 128)])
+def test_direct_wgrad_is_fp32_accurate(hip, B, H, W, Cin, Cout):
+    """dW = sum_p dz[p] x[p + tap] and db = sum_p dz[p] (direct fp16x3 weight gradient, split-K slabs
+    reduced in fixed order) against float64: as accurate as the fp32 MFMA weight gradient
+    (keys 29 = 0, 14 = 0), for unit and gradient-sized dz, a batch whose second sample's dz is
+    1e-30 of the first's (the per-tile scale jumps), and accumulation into existing gradients."""
+    g = torch.Generator().manual_seed(65)
+    x = F.relu(torch.randn(B, Cin, H, W, generator=g, dtype=torch.float64)).float().double()
+    dz0 = torch.randn(B, Cout, H, W, generator=g, dtype=torch.float64)
+    cases = {"unit": dz0, "tiny": dz0 * 1e-9}
+    if B > 1:
+        mixed = dz0.clone()
+        mixed[1] *= 1e-30
+        cases["mixed"] = mixed
+    xd = nhwc(x.float()).cuda()
+    for case, dz in cases.items():
+        dz = dz.float().double()
+        dw_ref = torch.nn.grad.conv2d_weight(x, (Cout, Cin, 3, 3), dz, padding=1)
+        db_ref = dz.sum(dim=(0, 2, 3))
+        errs = {}
+        for name, knobs in (("direct", DIRECT), ("native", dict(k29=0, k14=0))):
+            with Knobs(hip, **knobs):
+                nws = hip.pis_conv3x3_wgrad_ws(B, H, W, Cin, Cout)
+                ws = torch.empty(nws // 4 + 1, device="cuda")
+                dw = torch.full((Cout, 3, 3, Cin), 0.25, device="cuda")
+                db = torch.full((Cout,), 0.25, device="cuda")
+                rc = hip.pis_conv3x3_wgrad(xd.data_ptr(), Cin, nhwc(dz.float()).cuda().data_ptr(), Cout, dw.data_ptr(),
+                                           db.data_ptr(), B, H, W, Cin, Cout, ACC, ws.data_ptr(), nws, s())
+                assert rc == 0, hip.pis_last_error()
+                torch.cuda.synchronize()
+            dwc = dw.cpu().double().permute(0, 3, 1, 2) - 0.25
+            assert torch.isfinite(dwc).all(), (case, name)
+            errs[name] = (rel(dwc, dw_ref), rel(db.cpu().double() - 0.25, db_ref))
+        if case == "unit":  # accumulation onto 0.25 is exact to fp32 only at unit scale
+            assert errs["direct"][0] <= 1.25 * errs["native"][0] + 1e-9, (case, errs)
+            assert errs["direct"][0] < 5e-6 and errs["direct"][1] < 1e-5, (case, errs)
+
+
+@pytest.mark.parametrize("B,H,W,Cin,Cout", [(2, 16, 64, 64, 64), (2, 16, 32, 128, 128)])
+def test_direct_wgrad_scales_any_magnitude(hip, B, H, W, Cin, Cout):
+    """Without accumulation: gradient-sized (1e-9), tiny (1e-30) and large (1e6) dz and a batch
+    mixing 1 and 1e-30 per sample — finite and within 1.25x of the fp32 MFMA path's error."""
+    g = torch.Generator().manual_seed(66)
+    x = F.relu(torch.randn(B, Cin, H, W, generator=g, dtype=torch.float64)).float().double()
+    dz0 = torch.randn(B, Cout, H, W, generator=g, dtype=torch.float64)
+    xd = nhwc(x.float()).cuda()
+    mixed = dz0.clone()
+    mixed[1] *= 1e-30
+    for case, dz in {"1e-9": dz0 * 1e-9, "1e-30": dz0 * 1e-30, "1e6": dz0 * 1e6, "mixed": mixed}.items():
+        dz = dz.float().double()
+        dw_ref = torch.nn.grad.conv2d_weight(x, (Cout, Cin, 3, 3), dz, padding=1)
+        errs = {}
+        for name, knobs in (("direct", DIRECT), ("native", dict(k29=0, k14=0))):
+            with Knobs(hip, **knobs):
+                nws = hip.pis_conv3x3_wgrad_ws(B, H, W, Cin, Cout)
+                ws = torch.empty(nws // 4 + 1, device="cuda")
+                dw = torch.empty(Cout, 3, 3, Cin, device="cuda")
+                rc = hip.pis_conv3x3_wgrad(xd.data_ptr(), Cin, nhwc(dz.float()).cuda().data_ptr(), Cout, dw.data_ptr(),
+                                           0, B, H, W, Cin, Cout, 0, ws.data_ptr(), nws, s())
+                assert rc == 0, hip.pis_last_error()
+                torch.cuda.synchronize()
+            dwc = dw.cpu().double().permute(0, 3, 1, 2)
+            assert torch.isfinite(dwc).all(), (case, name)
+            errs[name] = rel(dwc, dw_ref)
+        assert errs["direct"] <= 1.25 * errs["native"] + 1e-9, (case, errs)
+        assert errs["direct"] < 5e-6, (case, errs)
+
+
+@pytest.mark.parametrize("loss_kw", [dict(), dict(rd_w=1e-2, pf_w=1e-2, D=5.0, a=0.5, eps=0.05)])
+def test_train_step_with_direct_convs(hip, loss_kw):
+    """The whole training step with every eligible conv on the direct kernels (key 29 = 2: forward
+    with the fused pool, input gradients from the original weights, weight gradients): outputs,
+    loss terms and every parameter gradient against the float64 oracle on the HIP decisions at
+    the north-star 1e-4 (tests/test_unet_gpu.py's check)."""
+    import importlib
+    tu = importlib.import_module("test_unet_gpu")
+    with Knobs(hip, k29=2):
+        net, ref, u, crit, p_ref, terms, ref64 = tu._step_pair(2, 64, 64, loss_kw)
+    assert tu.rel(u, p_ref) < 1e-4
+    got = crit.last["terms"].cpu()
+    for i, k in enumerate(("loss", "dice_loss", "bce_loss", "pde_loss", "phase_field_loss")):
+        if k in terms:
+            assert got[i].item() == pytest.approx(terms[k].item(), rel=1e-4), k
+    flips = {k: v for k, v in ref64.flips.items() if v[0]}
+    assert sum(n for n, _ in flips.values()) <= 8 and all(m <= 1e-5 for _, m in flips.values()), flips
+    worst = sorted(((tu.rel(p.grad, q.grad), n) for (n, p), q in zip(net.named_parameters(), ref64.parameters())),
+                   reverse=True)
+    assert worst[0][0] < 1e-4, worst[:5]
