@@ -211,48 +211,69 @@ __global__ __launch_bounds__(256, 2) void conv3x3_h3_kernel(DirectArgs g) {
   }
 
   // epilogue: lane (li, lh) holds, for output channel n0 + 32 j + li, image row r0 + 2 wave + i and
-  // column c0 + (reg & 3) + 8 (reg >> 2) + 4 lh (the 32x32x16 C/D map)
+  // column c0 + (reg & 3) + 8 (reg >> 2) + 4 lh (the 32x32x16 C/D map). Each image row goes through
+  // the wave's own 8 KB of LDS ([32 px][64 ch], conflict-free both ways) so that every lane then
+  // finishes 4 consecutive channels of 8 pixels with 16-B accesses: its mask / accumulate loads
+  // are issued together (one memory round trip per row) and a pixel's 64 channels are one 256-B
+  // store.
   const float inv_s = 1.f / s_cur;  // exact: a power of two
+  float* E = reinterpret_cast<float*>(smem) + wave * (32 * 64);  // free since the loop's last barrier
+  const int ch4 = 4 * (lane & 15);
+  const f32x4 wi4 = *reinterpret_cast<const f32x4*>(g.winv + n0 + ch4);
+  const f32x4 bias4 = g.bias ? *reinterpret_cast<const f32x4*>(g.bias + n0 + ch4) : f32x4{0.f, 0.f, 0.f, 0.f};
+  const f32x4 sc4 = (g.flags & PIS_SCALE) ? *reinterpret_cast<const f32x4*>(g.scale + (size_t)b * g.N + n0 + ch4)
+                                          : f32x4{1.f, 1.f, 1.f, 1.f};
+  float pm[2][2][8];  // POOL: per j, row i, column pair: the lane's pooled candidates
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int n = n0 + 32 * j + li;
-    const float wi = g.winv[n];
-    const float bias = g.bias ? g.bias[n] : 0.f;
-    const float sc = (g.flags & PIS_SCALE) ? g.scale[(size_t)b * g.N + n] : 1.f;
-    float pm[2][8];  // POOL: this lane's column-pair maxima of row 2w + i
+  for (int i = 0; i < 2; ++i) {
+    const int row = r0 + 2 * wave + i;
+    const size_t pix0 = ((size_t)b * g.H + row) * g.W + c0;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int row = r0 + 2 * wave + i;
-      const size_t pix0 = ((size_t)b * g.H + row) * g.W + c0 + 4 * lh;
-      // every load of the block first (mask, accumulate source), then the stores: y may alias
-      // them as far as the compiler knows, so interleaved they would serialise on each load
-      float mk[16], old[16];
-#pragma unroll
-      for (int reg = 0; reg < 16; ++reg) {
-        const size_t pix = pix0 + (reg & 3) + 8 * (reg >> 2);
-        mk[reg] = (g.flags & PIS_MASK) ? g.mask[pix * g.ldm + n] : 1.f;
-        old[reg] = (g.flags & PIS_ACCUMULATE) ? g.y[pix * g.ldy + n] : 0.f;
-      }
+    for (int j = 0; j < 2; ++j) {
 #pragma unroll
       for (int reg = 0; reg < 16; ++reg) {
-        const size_t pix = pix0 + (reg & 3) + 8 * (reg >> 2);
-        float v = (acc[i][j][reg] * inv_s) * wi + bias;
-        if (g.flags & PIS_RELU) v = fmaxf(v, 0.f);
-        if (!(mk[reg] > 0.f)) v = 0.f;
-        v = v * sc + old[reg];
-        g.y[pix * g.ldy + n] = v;
-        if constexpr (POOL) {
-          if (reg & 1) pm[i][reg >> 1] = fmaxf(pm[i][reg >> 1], v);
-          else pm[i][reg >> 1] = v;
+        const int px = (reg & 3) + 8 * (reg >> 2) + 4 * lh;
+        E[px * 64 + 32 * j + li] = acc[i][j][reg];
+        if constexpr (POOL) {  // the pooled values: y = ReLU(acc / (s t) + bias) (encoder conv1: no scale)
+          const int n = n0 + 32 * j + li;
+          const float v = fmaxf((acc[i][j][reg] * inv_s) * g.winv[n] + (g.bias ? g.bias[n] : 0.f), 0.f);
+          pm[j][i][reg >> 1] = (reg & 1) ? fmaxf(pm[j][i][reg >> 1], v) : v;
         }
       }
     }
-    if constexpr (POOL) {
-      const int prow = (r0 >> 1) + wave;
+    f32x4 mk[8], old[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const size_t pix = pix0 + (lane >> 4) + 4 * k;
+      mk[k] = (g.flags & PIS_MASK) ? *reinterpret_cast<const f32x4*>(g.mask + pix * g.ldm + n0 + ch4)
+                                   : f32x4{1.f, 1.f, 1.f, 1.f};
+      old[k] = (g.flags & PIS_ACCUMULATE) ? *reinterpret_cast<const f32x4*>(g.y + pix * g.ldy + n0 + ch4)
+                                          : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int px = (lane >> 4) + 4 * k;
+      const f32x4 a = *reinterpret_cast<const f32x4*>(&E[px * 64 + ch4]);
+      f32x4 v;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float t = (a[e] * inv_s) * wi4[e] + bias4[e];
+        if (g.flags & PIS_RELU) t = fmaxf(t, 0.f);
+        if (!(mk[k][e] > 0.f)) t = 0.f;
+        v[e] = t * sc4[e] + old[k][e];
+      }
+      *reinterpret_cast<f32x4*>(g.y + (pix0 + px) * g.ldy + n0 + ch4) = v;
+    }
+  }
+  if constexpr (POOL) {
+    const int prow = (r0 >> 1) + wave;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int n = n0 + 32 * j + li;
 #pragma unroll
       for (int q = 0; q < 8; ++q) {  // column pair q: columns 2 (q & 1) + 8 (q >> 1) + 4 lh, +1
         const int pcol = (c0 >> 1) + (q & 1) + 4 * (q >> 1) + 2 * lh;
-        g.pool[(((size_t)b * (g.H >> 1) + prow) * (g.W >> 1) + pcol) * g.N + n] = fmaxf(pm[0][q], pm[1][q]);
+        g.pool[(((size_t)b * (g.H >> 1) + prow) * (g.W >> 1) + pcol) * g.N + n] = fmaxf(pm[j][0][q], pm[j][1][q]);
       }
     }
   }
@@ -279,6 +300,11 @@ int launch_direct_h3(const IGemmArgs& a, int B, void* ws, size_t ws_bytes, hipSt
   const int C = a.Csrc, N = a.N;
   if (!direct_h3_shape_ok(a.H, a.W, C, N, a.lds) || ws_bytes < direct_h3_ws_bytes(C, N))
     return set_error("direct conv: shape or workspace not supported"), PIS_ERR_ARG;
+  auto a16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+  if (!a16(a.src) || !a16(a.dst) || a.ldd % 4 || ((a.flags & PIS_MASK) && (!a16(a.mask) || a.ldm % 4)) ||
+      (a.pool && !a16(a.pool)) || ((a.flags & PIS_SCALE) && !a16(a.scale)) || (a.bias && !a16(a.bias)))
+    return set_error("direct conv: input, output, mask, scale, bias and pool must be 16-byte aligned with "
+                     "channel strides % 4 == 0"), PIS_ERR_ARG;
   _Float16* wp = reinterpret_cast<_Float16*>(ws);
   float* winv = reinterpret_cast<float*>(reinterpret_cast<char*>(ws) + (size_t)9 * C * N * 2 * sizeof(_Float16));
   // forward (or a flipped copy [Cin'=N][3][3][C] read as KRSC): out N, contraction C
