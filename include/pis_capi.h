@@ -130,7 +130,8 @@ int pis_version(void);
                                     0 one xi per barrier; bit-for-bit the same sums */
 #define PIS_TUNE_DIRECT_H3 29   /* direct 3x3 conv in fp16x3 (csrc/direct.hip; forward and input gradient): 0 off,
                                    1 auto (the shallow layers: <= 128 channels on both sides, H >= 256),
-                                   2 every shape it covers (H % 8, W % 32, C % 16, N % 64 == 0) */
+                                   2 every shape it covers (H % 8, W % 32, C % 16, N % 64 == 0),
+                                   3 auto + the 128 <-> 256-channel layers at 256^2 and 128^2 */
 #define PIS_TUNE_NKEYS 30
 #define PIS_DEBUG_NOLOAD (1 << 16)
 int pis_tune(int key, int value);

@@ -286,7 +286,10 @@ bool direct_h3_shape_ok(int H, int W, int C, int N, int ldx) {
 bool direct_h3_wanted(int H, int W, int C, int N, int ldx) {
   const int mode = tune_get(PIS_TUNE_DIRECT_H3);
   if (mode == 0 || !direct_h3_shape_ok(H, W, C, N, ldx)) return false;
-  return mode == 2 || (C <= 128 && N <= 128 && H >= 256);
+  const int lo = std::min(C, N), hi = std::max(C, N);
+  if (mode == 3)  // + dec2.conv0 (256 <-> 128 at 256^2) and enc3.conv0 (128 <-> 256 at 128^2)
+    return (H >= 256 && hi <= 256) || (H >= 128 && hi <= 256 && lo <= 128);
+  return mode == 2 || (hi <= 128 && H >= 256);
 }
 
 size_t direct_h3_ws_bytes(int C, int N) {

@@ -21,6 +21,9 @@ for x in "$@"; do
     loss) run loss_b64 120 python -u tools/bench_loss.py --B 64; run loss_c2 120 python -u tools/bench_loss.py --B 8 ;;
     lossmodes) run lossmodes_b64 120 python -u tools/bench_loss.py --B 64 --modes 0,1,2,1:2,1:4,2:2,2:4; run lossmodes_c2 120 python -u tools/bench_loss.py --B 8 --modes 0,1,2,1:2,2:2 ;;
     bench) run bench 300 python -u bench.py --no-cpu-baseline ;;
+    bench29b) run bench_k29_1 300 python -u bench.py --no-cpu-baseline --steps 20 --tune 29=1 && run bench_k29_3 300 python -u bench.py --no-cpu-baseline --steps 20 --tune 29=3 && run bench_k29_1b 300 python -u bench.py --no-cpu-baseline --steps 20 --tune 29=1 ;;
+    prof29) run prof29 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof29" -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --tune 29=1 ;;
+    directw3) run direct_wgrad3 300 python -u tools/bench_kernels.py --key 29 --variants 0,2 --ops wgrad --rounds 3 --layers enc3.conv0,dec2.conv0,enc1.conv1 ;;
     bench29) run bench_k29_0 300 python -u bench.py --no-cpu-baseline --steps 20 && run bench_k29_1 300 python -u bench.py --no-cpu-baseline --steps 20 --tune 29=1 ;;
     direct) run direct_kernels 300 python -u tools/bench_kernels.py --key 29 --variants 0,2 --ops fwd,dgrad --rounds 3 --layers enc1.conv1,dec1.conv0,enc2.conv0,enc2.conv1,dec2.conv0,enc3.conv0,enc3.conv1 ;;
     directw) run direct_wgrad 300 python -u tools/bench_kernels.py --key 29 --variants 0,2 --ops wgrad --rounds 3 --layers enc1.conv1,dec1.conv0,enc2.conv0,enc2.conv1,dec2.conv0 ;;
