@@ -132,7 +132,9 @@ int pis_version(void);
                                    1 auto (the shallow layers: <= 128 channels on both sides, H >= 256),
                                    2 every shape it covers (H % 8, W % 32, C % 16, N % 64 == 0),
                                    3 auto + the 128 <-> 256-channel layers at 256^2 and 128^2 */
-#define PIS_TUNE_NKEYS 30
+#define PIS_TUNE_DIRECT_WG 30   /* direct fp16x3 weight gradient (key 29): 0 one LDS buffer, 4-row pixel tiles;
+                                   1 two buffers, 2-row tiles, the next tile's split interleaved with this one's MFMAs */
+#define PIS_TUNE_NKEYS 31
 #define PIS_DEBUG_NOLOAD (1 << 16)
 int pis_tune(int key, int value);
 /* Tooling (tools/bench_gemm.py): time one batched NT GEMM kernel variant in isolation,

@@ -48,8 +48,12 @@ def main():
     ap.add_argument("--ops", default="fwd,dgrad,wgrad")
     ap.add_argument("--noload", action="store_true", help="also time each variant without global loads")
     ap.add_argument("--convt", action="store_true", help="time the transposed convs instead")
+    ap.add_argument("--tune", action="append", default=[], metavar="KEY=VALUE", help="fixed knobs for every variant")
     args = ap.parse_args()
     lib = _hip.lib()
+    for kv in args.tune:
+        k, v = kv.split("=")
+        lib.pis_tune(int(k), int(v))
     variants = [int(v) for v in args.variants.split(",")]
     default = lib.pis_tune(args.key, -1)
     s = torch.cuda.current_stream().cuda_stream
