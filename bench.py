@@ -244,7 +244,8 @@ class LossCallTimer:
 
 
 # kernels whose MFMA-busy fraction the bench line quotes: the GEMM-shaped ones and the fused loss
-BUSY_REPORTED = ("gemm_nt", "wgrad_x6", "wino4_gemm_out", "convt_gemm", "loss_fwd", "head_loss_bwd", "loss_bwd")
+BUSY_REPORTED = ("gemm_nt", "wgrad_x6", "wgrad_h3", "wino4_gemm_out", "convt_gemm", "conv3x3_h3", "conv3x3_wgrad_h3",
+                 "loss_fwd", "head_loss_bwd", "loss_bwd")
 
 
 def load_pmc(kernel=DOMINANT_KERNEL):
@@ -472,7 +473,8 @@ def main():
     # fused-loss C-ABI calls (host-side enqueue only; the GPU stays the bottleneck)
     from physics_informed_image_segmentation_amd import _hip
     ktimer, ftimer, ltimer = KernelTimer(), KernelTimer("wino_gemm_out"), LossCallTimer()
-    _hip.set_launch_hook(lambda *a: (ktimer(*a), ftimer(*a)))
+    dtimer, wtimer = KernelTimer("direct_h3"), KernelTimer("direct_wgrad_h3")
+    _hip.set_launch_hook(lambda *a: (ktimer(*a), ftimer(*a), dtimer(*a), wtimer(*a)))
     _hip.set_tracer(ltimer)
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -495,6 +497,7 @@ def main():
     n_launch //= args.steps
     nf_launch, f_flop, f_ms = ftimer.summary()
     nf_launch //= args.steps
+    direct_live = {k: tm.summary() for k, tm in (("direct_h3", dtimer), ("direct_wgrad_h3", wtimer))}
     loss_t = ltimer.summary()
     achieved = flop_per_launch / (ms_per_launch * 1e-3) / 1e12
     # the same kernel with the weight gradients serialised on one stream (no concurrent
@@ -502,12 +505,14 @@ def main():
     eng = model.engine()
     side, eng.side = eng.side, None
     iso, fiso = KernelTimer(), KernelTimer("wino_gemm_out")
-    _hip.set_launch_hook(lambda *a: (iso(*a), fiso(*a)))
+    diso, wiso = KernelTimer("direct_h3"), KernelTimer("direct_wgrad_h3")
+    _hip.set_launch_hook(lambda *a: (iso(*a), fiso(*a), diso(*a), wiso(*a)))
     step()
     _hip.set_launch_hook(None)
     eng.side = side
     _, iso_flop, iso_ms = iso.summary()
     _, _, fiso_ms = fiso.summary()
+    direct_iso = {"direct_h3": diso.summary(), "direct_wgrad_h3": wiso.summary()}
     # the pipe the dominant kernel runs on. fp32-class GEMMs on the MFMA pipe: fp16x3 (pis_tune
     # key 10 = 4, the default: per-K-step power-of-two tile scales, hi + lo fp16 split, three
     # fp16 MFMAs per fp32 multiply-add) peaks at the dense fp16 MFMA rate (~2.5 PFLOP/s,
@@ -559,6 +564,35 @@ def main():
             "measured": "live over the timed steps",
             "isolated": {"frac": fb / (fiso_ms * 1e-3) / 8e12 if fiso_ms else None, "avg_launch_ms": fiso_ms,
                          "measured": "one extra step, weight gradients serialised"}}
+    # the direct fp16x3 3x3 convolutions (csrc/direct.hip, the shallow layers): MFMA-bound, priced
+    # in fp32-equivalent FLOPs (2 x 9 x pixels x C x N per launch) against the fp16x3 pipe
+    h3_peak = 2500.0 / 3.0
+    direct_roofs = {}
+    for key, name, kern in (("direct_h3", "roofline_direct", "conv3x3_h3_kernel<POOL> (forward with the fused max "
+                                                                "pool / input gradient, 8 x 32 px x 64 ch per block)"),
+                            ("direct_wgrad_h3", "roofline_direct_wgrad", "conv3x3_wgrad_h3_kernel (weight gradient, "
+                                                                         "split-K slabs)")):
+        n_d, fl_d, ms_d = direct_live[key]
+        if not n_d:
+            continue
+        n_d //= args.steps
+        _, ifl_d, ims_d = direct_iso[key]
+        stem = "conv3x3_h3_kernel" if key == "direct_h3" else "conv3x3_wgrad_h3_kernel"
+        busy = None
+        if busy_by_kernel is not None:
+            hits = [v for k, v in busy_by_kernel.items() if stem in k]
+            busy = sum(hits) / len(hits) if hits else None
+        direct_roofs[name] = {
+            "bound": "mfma", "kernel": kern, "achieved": fl_d / (ms_d * 1e-3) / 1e12, "peak": h3_peak,
+            "unit": "TFLOP/s", "frac": fl_d / (ms_d * 1e-3) / 1e12 / h3_peak, "traffic": pmc_bytes(stem),
+            "pipe": "fp16 MFMA, fp32-class fp16x3 split (3 fp16 products per fp32 multiply-add); fp32-equivalent "
+                    "FLOPs of the direct convolution",
+            "mfma_busy_frac": busy, "launches_per_step": n_d, "avg_launch_ms": ms_d, "flop_per_launch": fl_d,
+            "ms_per_step": n_d * ms_d, "algorithmic_bytes_per_launch": None,
+            "measured": "live over the timed steps (HIP events on the launch stream)",
+            "isolated": {"achieved": ifl_d / (ims_d * 1e-3) / 1e12 if ims_d else None,
+                         "frac": ifl_d / (ims_d * 1e-3) / 1e12 / h3_peak if ims_d else None, "avg_launch_ms": ims_d,
+                         "measured": "one extra step, weight gradients serialised"}}
     loss_cold = loss_standalone(model.engine().u, t, loss_kw)
     if rank == 0:
         flops = conv_flops_per_image(H, W) * B
@@ -567,7 +601,7 @@ def main():
                        else f"training images/sec ({H}x{W}, {args.config})"),
             "value": imgs_per_s, "unit": "images/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "fp32 (fp16x3/bf16x6 split MFMA, Winograd)", "data": "synthetic",
+            "vs_baseline": None, "dtype": "fp32 (fp16x3/bf16x6 split MFMA; direct + Winograd convs)", "data": "synthetic",
             "config": {"workload": workload,
                        "global_batch": B * world, "image_size": [H, W], "parallelism": f"dp{world}"},
             "roofline": None,
@@ -613,8 +647,11 @@ def main():
         out["roofline_gemm"]["ms_per_step"] = g_ms
         if fused_roof:
             fused_roof["ms_per_step"] = f_ms_step
-        out["roofline"] = fused_roof if fused_roof and f_ms_step > g_ms else out["roofline_gemm"]
-        out["roofline_dominant"] = "roofline_fused" if out["roofline"] is fused_roof else "roofline_gemm"
+        out.update(direct_roofs)
+        cands = {"roofline_gemm": g_ms, **({"roofline_fused": f_ms_step} if fused_roof else {}),
+                 **{k: v["ms_per_step"] for k, v in direct_roofs.items()}}
+        out["roofline_dominant"] = max(cands, key=cands.get)
+        out["roofline"] = out[out["roofline_dominant"]]
         if world == 1 and not args.no_cpu_baseline and args.config == "c2":
             out["cpu_baseline"] = cpu_baseline()
         print(json.dumps(out))

@@ -128,8 +128,9 @@ int pis_version(void);
 #define PIS_TUNE_FUSED_PAIR 28   /* fused kernel, 64-channel contractions in fp16x3 (key 22), lockstep form: 1 two xi per
                                     barrier (four LDS operand buffers; the two products' MFMA chains interleave),
                                     0 one xi per barrier; bit-for-bit the same sums */
-#define PIS_TUNE_DIRECT_H3 29   /* direct 3x3 conv in fp16x3 (csrc/direct.hip; forward and input gradient): 0 off,
-                                   1 auto (the shallow layers: <= 128 channels on both sides, H >= 256),
+#define PIS_TUNE_DIRECT_H3 29   /* direct 3x3 conv in fp16x3 (csrc/direct.hip; forward, input and weight gradient):
+                                   0 off (Winograd / halo kernels), 1 (default) auto: the shallow layers (<= 128
+                                   channels on both sides, H >= 256),
                                    2 every shape it covers (H % 8, W % 32, C % 16, N % 64 == 0),
                                    3 auto + the 128 <-> 256-channel layers at 256^2 and 128^2 */
 #define PIS_TUNE_DIRECT_WG 30   /* direct fp16x3 weight gradient (key 29): 0 one LDS buffer, 4-row pixel tiles;
