@@ -50,6 +50,10 @@ constexpr int DX_ITEMS = 2 * DH_P;               // 8-channel halves of halo pix
 constexpr int DX_PER_T = (DX_ITEMS + 255) / 256; // 3
 constexpr int DW_PER_T = DW_BYTES / 16 / 256;    // 9
 
+__device__ __forceinline__ f32x4 vmax4(f32x4 a, f32x4 b) {
+  return f32x4{fmaxf(a[0], b[0]), fmaxf(a[1], b[1]), fmaxf(a[2], b[2]), fmaxf(a[3], b[3])};
+}
+
 __device__ __forceinline__ int dsw(int row, int half) { return row * DKC + 8 * (half ^ ((row >> 3) & 1)); }
 
 // weights -> [chunk][slice][tap][plane][64][16] fp16 (rows swizzled as dsw), per output scale.
@@ -95,33 +99,40 @@ __global__ __launch_bounds__(256, 2) void conv3x3_h3_kernel(DirectArgs g) {
   float* red = reinterpret_cast<float*>(smem + DX_BYTES + DW_BYTES);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, li = lane & 31, lh = lane >> 5;
   const int tw_n = g.W / DT_W, th_n = g.H / DT_H, per_img = tw_n * th_n, ntile = g.B * per_img;
-  const int ns = g.N / 64;
-  // the ns output slices of one pixel tile are dealt 8 apart (same XCD, back to back): the second
-  // reads the input tile from L2
-  const int bid = blockIdx.x;
-  int gt, slice;
-  if (ntile % 8 == 0) {
-    gt = (bid / (8 * ns)) * 8 + bid % 8;
-    slice = (bid / 8) % ns;
-  } else {
-    gt = bid / ns;
-    slice = bid % ns;
-  }
-  const int b = gt / per_img, rem = gt - b * per_img, r0 = (rem / tw_n) * DT_H, c0 = (rem % tw_n) * DT_W;
-  const int n0 = slice * 64;
-  const float* xb = g.x + (size_t)b * g.H * g.W * g.ldx;
+  const int ns = g.N / 64, total = ntile * ns, G = gridDim.x;
   const int nk = g.C / DKC;
+  // persistent: the block walks work items blockIdx.x, + G, ... (G % 8 == 0: every item of a block
+  // stays on its XCD), and the next item's first chunk is loaded during this item's last MFMAs, so
+  // a block pays the load latency of its first chunk once, not once per tile. An item = (pixel
+  // tile, 64-output slice); the ns slices of one tile are dealt 8 apart (same XCD, back to back:
+  // the second reads the input tile from L2)
+  struct Item {
+    int b, r0, c0, n0;
+  };
+  auto item = [&](int v) {
+    int gt, slice;
+    if (ntile % 8 == 0) {
+      gt = (v / (8 * ns)) * 8 + v % 8;
+      slice = (v / 8) % ns;
+    } else {
+      gt = v / ns;
+      slice = v % ns;
+    }
+    const int b = gt / per_img, rem = gt - b * per_img;
+    return Item{b, (rem / tw_n) * DT_H, (rem % tw_n) * DT_W, slice * 64};
+  };
 
   f32x4 xr[DX_PER_T][2];
   u32x4 wr[DW_PER_T];
-  auto gload = [&](int k) {
+  auto gload = [&](const Item& it, int k) {
+    const float* xb = g.x + (size_t)it.b * g.H * g.W * g.ldx;
 #pragma unroll
     for (int j = 0; j < DX_PER_T; ++j) {
       const int i = tid + 256 * j;
       xr[j][0] = xr[j][1] = f32x4{0.f, 0.f, 0.f, 0.f};
       if (i < DX_ITEMS) {
         const int q = i >> 1, h = i & 1, qr = q / DH_W, qc = q - qr * DH_W;
-        const int row = r0 - 1 + qr, col = c0 - 1 + qc;
+        const int row = it.r0 - 1 + qr, col = it.c0 - 1 + qc;
         if (row >= 0 && row < g.H && col >= 0 && col < g.W) {
           const float* p = xb + ((size_t)row * g.W + col) * g.ldx + k * DKC + 8 * h;
           xr[j][0] = *reinterpret_cast<const f32x4*>(p);
@@ -129,11 +140,16 @@ __global__ __launch_bounds__(256, 2) void conv3x3_h3_kernel(DirectArgs g) {
         }
       }
     }
-    const u32x4* wsrc = reinterpret_cast<const u32x4*>(g.wp + ((size_t)k * ns + slice) * DW_HALFS);
+    const u32x4* wsrc = reinterpret_cast<const u32x4*>(g.wp + ((size_t)k * ns + (it.n0 >> 6)) * DW_HALFS);
 #pragma unroll
     for (int j = 0; j < DW_PER_T; ++j) wr[j] = wsrc[tid + 256 * j];
   };
 
+  if (blockIdx.x < total) gload(item(blockIdx.x), 0);
+#pragma unroll 1
+  for (int v = blockIdx.x; v < total; v += G) {
+  const Item it = item(v);
+  const int b = it.b, r0 = it.r0, c0 = it.c0, n0 = it.n0;
   f32x16 acc[2][2];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -143,7 +159,6 @@ __global__ __launch_bounds__(256, 2) void conv3x3_h3_kernel(DirectArgs g) {
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
   float s_cur = 0.f, s_min = __builtin_inff();
 
-  gload(0);
 #pragma unroll 1
   for (int k = 0; k < nk; ++k) {
     // 1. this chunk's weights into LDS; the halo's block-wide max
@@ -181,8 +196,9 @@ __global__ __launch_bounds__(256, 2) void conv3x3_h3_kernel(DirectArgs g) {
       }
     }
     __syncthreads();
-    // 3. the next chunk's loads fly during this chunk's MFMAs
-    if (k + 1 < nk) gload(k + 1);
+    // 3. the next chunk's loads (or the next item's first) fly during this chunk's MFMAs
+    if (k + 1 < nk) gload(it, k + 1);
+    else if (v + G < total) gload(item(v + G), 0);
 #pragma unroll
     for (int tap = 0; tap < 9; ++tap) {
       const int r = tap / 3, s = tap % 3;
@@ -218,64 +234,60 @@ __global__ __launch_bounds__(256, 2) void conv3x3_h3_kernel(DirectArgs g) {
   // store.
   const float inv_s = 1.f / s_cur;  // exact: a power of two
   float* E = reinterpret_cast<float*>(smem) + wave * (32 * 64);  // free since the loop's last barrier
+  // float4 phase: lane (l & 15) owns channels n0 + ch4 .. + 3; pixel pair m = (l >> 4) + 4 k of the
+  // row (columns 2m, 2m + 1: the 2x2 pool window's columns stay in one lane)
   const int ch4 = 4 * (lane & 15);
   const f32x4 wi4 = *reinterpret_cast<const f32x4*>(g.winv + n0 + ch4);
   const f32x4 bias4 = g.bias ? *reinterpret_cast<const f32x4*>(g.bias + n0 + ch4) : f32x4{0.f, 0.f, 0.f, 0.f};
   const f32x4 sc4 = (g.flags & PIS_SCALE) ? *reinterpret_cast<const f32x4*>(g.scale + (size_t)b * g.N + n0 + ch4)
                                           : f32x4{1.f, 1.f, 1.f, 1.f};
-  float pm[2][2][8];  // POOL: per j, row i, column pair: the lane's pooled candidates
+  f32x4 prow0[4];  // POOL: row 2w's column-pair maxima
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int row = r0 + 2 * wave + i;
     const size_t pix0 = ((size_t)b * g.H + row) * g.W + c0;
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
+    for (int j = 0; j < 2; ++j)
 #pragma unroll
-      for (int reg = 0; reg < 16; ++reg) {
-        const int px = (reg & 3) + 8 * (reg >> 2) + 4 * lh;
-        E[px * 64 + 32 * j + li] = acc[i][j][reg];
-        if constexpr (POOL) {  // the pooled values: y = ReLU(acc / (s t) + bias) (encoder conv1: no scale)
-          const int n = n0 + 32 * j + li;
-          const float v = fmaxf((acc[i][j][reg] * inv_s) * g.winv[n] + (g.bias ? g.bias[n] : 0.f), 0.f);
-          pm[j][i][reg >> 1] = (reg & 1) ? fmaxf(pm[j][i][reg >> 1], v) : v;
-        }
-      }
-    }
+      for (int reg = 0; reg < 16; ++reg) E[((reg & 3) + 8 * (reg >> 2) + 4 * lh) * 64 + 32 * j + li] = acc[i][j][reg];
     f32x4 mk[8], old[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      const size_t pix = pix0 + (lane >> 4) + 4 * k;
+      const size_t pix = pix0 + 2 * ((lane >> 4) + 4 * (k >> 1)) + (k & 1);
       mk[k] = (g.flags & PIS_MASK) ? *reinterpret_cast<const f32x4*>(g.mask + pix * g.ldm + n0 + ch4)
                                    : f32x4{1.f, 1.f, 1.f, 1.f};
       old[k] = (g.flags & PIS_ACCUMULATE) ? *reinterpret_cast<const f32x4*>(g.y + pix * g.ldy + n0 + ch4)
                                           : f32x4{0.f, 0.f, 0.f, 0.f};
     }
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const int px = (lane >> 4) + 4 * k;
-      const f32x4 a = *reinterpret_cast<const f32x4*>(&E[px * 64 + ch4]);
-      f32x4 v;
+    for (int kp = 0; kp < 4; ++kp) {
+      const int m = (lane >> 4) + 4 * kp;
+      f32x4 v[2];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        float t = (a[e] * inv_s) * wi4[e] + bias4[e];
-        if (g.flags & PIS_RELU) t = fmaxf(t, 0.f);
-        if (!(mk[k][e] > 0.f)) t = 0.f;
-        v[e] = t * sc4[e] + old[k][e];
+      for (int d = 0; d < 2; ++d) {
+        const int k = 2 * kp + d;
+        const f32x4 a = *reinterpret_cast<const f32x4*>(&E[(2 * m + d) * 64 + ch4]);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float t = (a[e] * inv_s) * wi4[e] + bias4[e];
+          if (g.flags & PIS_RELU) t = fmaxf(t, 0.f);
+          if (!(mk[k][e] > 0.f)) t = 0.f;
+          v[d][e] = t * sc4[e] + old[k][e];
+        }
+        *reinterpret_cast<f32x4*>(g.y + (pix0 + 2 * m + d) * g.ldy + n0 + ch4) = v[d];
       }
-      *reinterpret_cast<f32x4*>(g.y + (pix0 + px) * g.ldy + n0 + ch4) = v;
+      if constexpr (POOL) {
+        const f32x4 cm = vmax4(v[0], v[1]);
+        if (i == 0) {
+          prow0[kp] = cm;
+        } else {
+          const size_t pp = ((size_t)b * (g.H >> 1) + (r0 >> 1) + wave) * (g.W >> 1) + (c0 >> 1) + m;
+          *reinterpret_cast<f32x4*>(g.pool + pp * g.N + n0 + ch4) = vmax4(prow0[kp], cm);
+        }
+      }
     }
   }
-  if constexpr (POOL) {
-    const int prow = (r0 >> 1) + wave;
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int n = n0 + 32 * j + li;
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {  // column pair q: columns 2 (q & 1) + 8 (q >> 1) + 4 lh, +1
-        const int pcol = (c0 >> 1) + (q & 1) + 4 * (q >> 1) + 2 * lh;
-        g.pool[(((size_t)b * (g.H >> 1) + prow) * (g.W >> 1) + pcol) * g.N + n] = fmaxf(pm[j][0][q], pm[j][1][q]);
-      }
-    }
+  __syncthreads();  // the next item's staging overwrites the epilogue's LDS
   }
 }
 
@@ -321,7 +333,10 @@ int launch_direct_h3(const IGemmArgs& a, int B, void* ws, size_t ws_bytes, hipSt
   g.x = a.src; g.ldx = a.lds; g.wp = wp; g.winv = winv; g.bias = a.bias; g.scale = a.scale;
   g.mask = a.mask; g.ldm = a.ldm; g.y = a.dst; g.ldy = a.ldd; g.pool = a.pool;
   g.B = B; g.H = a.H; g.W = a.W; g.C = C; g.N = N; g.flags = a.flags;
-  const int blocks = B * (a.H / DT_H) * (a.W / DT_W) * (N / 64);
+  // persistent grid (pis_tune key 31 = k: k blocks per CU walk the items; 0: one block per item)
+  const int items = B * (a.H / DT_H) * (a.W / DT_W) * (N / 64);
+  const int per_cu = tune_get(PIS_TUNE_DIRECT_GRID);
+  const int blocks = per_cu > 0 ? std::min(items, 256 * per_cu) : items;
   const double flop = 2.0 * 9 * (double)B * a.H * a.W * C * N;
   launch_hook("direct_h3", 0, s, flop);
   if (a.pool)
