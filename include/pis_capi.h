@@ -135,10 +135,7 @@ int pis_version(void);
                                    3 auto + the 128 <-> 256-channel layers at 256^2 and 128^2 */
 #define PIS_TUNE_DIRECT_WG 30   /* direct fp16x3 weight gradient (key 29): 0 one LDS buffer, 4-row pixel tiles;
                                    1 two buffers, 2-row tiles, the next tile's split interleaved with this one's MFMAs */
-#define PIS_TUNE_DIRECT_GRID 31  /* direct fp16x3 forward / input gradient: k > 0 a persistent grid of 256 k blocks that
-                                   walk the (pixel tile, 64-output slice) items, prefetching the next item's first
-                                   chunk during the current one's MFMAs; 0 one block per item */
-#define PIS_TUNE_NKEYS 32
+#define PIS_TUNE_NKEYS 31
 #define PIS_DEBUG_NOLOAD (1 << 16)
 int pis_tune(int key, int value);
 /* Tooling (tools/bench_gemm.py): time one batched NT GEMM kernel variant in isolation,

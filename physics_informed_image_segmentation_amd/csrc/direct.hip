@@ -99,40 +99,34 @@ __global__ __launch_bounds__(256, 2) void conv3x3_h3_kernel(DirectArgs g) {
   float* red = reinterpret_cast<float*>(smem + DX_BYTES + DW_BYTES);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, li = lane & 31, lh = lane >> 5;
   const int tw_n = g.W / DT_W, th_n = g.H / DT_H, per_img = tw_n * th_n, ntile = g.B * per_img;
-  const int ns = g.N / 64, total = ntile * ns, G = gridDim.x;
+  const int ns = g.N / 64;
   const int nk = g.C / DKC;
-  // persistent: the block walks work items blockIdx.x, + G, ... (G % 8 == 0: every item of a block
-  // stays on its XCD), and the next item's first chunk is loaded during this item's last MFMAs, so
-  // a block pays the load latency of its first chunk once, not once per tile. An item = (pixel
-  // tile, 64-output slice); the ns slices of one tile are dealt 8 apart (same XCD, back to back:
-  // the second reads the input tile from L2)
-  struct Item {
-    int b, r0, c0, n0;
-  };
-  auto item = [&](int v) {
-    int gt, slice;
-    if (ntile % 8 == 0) {
-      gt = (v / (8 * ns)) * 8 + v % 8;
-      slice = (v / 8) % ns;
-    } else {
-      gt = v / ns;
-      slice = v % ns;
-    }
-    const int b = gt / per_img, rem = gt - b * per_img;
-    return Item{b, (rem / tw_n) * DT_H, (rem % tw_n) * DT_W, slice * 64};
-  };
+  // block = (pixel tile, 64-output slice); the ns slices of one tile are dealt 8 apart (same XCD,
+  // back to back: the second reads the input tile from L2). (A persistent grid walking the items,
+  // prefetching the next item's first chunk during this one's MFMAs, measured 0.5-5 % slower per
+  // layer and on the step: profiles/r3_q7_direct_grid.txt — co-resident blocks already hide it.)
+  int gt, slice;
+  if (ntile % 8 == 0) {
+    gt = (blockIdx.x / (8 * ns)) * 8 + blockIdx.x % 8;
+    slice = (blockIdx.x / 8) % ns;
+  } else {
+    gt = blockIdx.x / ns;
+    slice = blockIdx.x % ns;
+  }
+  const int b = gt / per_img, rem = gt - b * per_img, r0 = (rem / tw_n) * DT_H, c0 = (rem % tw_n) * DT_W;
+  const int n0 = slice * 64;
+  const float* xb = g.x + (size_t)b * g.H * g.W * g.ldx;
 
   f32x4 xr[DX_PER_T][2];
   u32x4 wr[DW_PER_T];
-  auto gload = [&](const Item& it, int k) {
-    const float* xb = g.x + (size_t)it.b * g.H * g.W * g.ldx;
+  auto gload = [&](int k) {
 #pragma unroll
     for (int j = 0; j < DX_PER_T; ++j) {
       const int i = tid + 256 * j;
       xr[j][0] = xr[j][1] = f32x4{0.f, 0.f, 0.f, 0.f};
       if (i < DX_ITEMS) {
         const int q = i >> 1, h = i & 1, qr = q / DH_W, qc = q - qr * DH_W;
-        const int row = it.r0 - 1 + qr, col = it.c0 - 1 + qc;
+        const int row = r0 - 1 + qr, col = c0 - 1 + qc;
         if (row >= 0 && row < g.H && col >= 0 && col < g.W) {
           const float* p = xb + ((size_t)row * g.W + col) * g.ldx + k * DKC + 8 * h;
           xr[j][0] = *reinterpret_cast<const f32x4*>(p);
@@ -140,16 +134,11 @@ __global__ __launch_bounds__(256, 2) void conv3x3_h3_kernel(DirectArgs g) {
         }
       }
     }
-    const u32x4* wsrc = reinterpret_cast<const u32x4*>(g.wp + ((size_t)k * ns + (it.n0 >> 6)) * DW_HALFS);
+    const u32x4* wsrc = reinterpret_cast<const u32x4*>(g.wp + ((size_t)k * ns + slice) * DW_HALFS);
 #pragma unroll
     for (int j = 0; j < DW_PER_T; ++j) wr[j] = wsrc[tid + 256 * j];
   };
 
-  if (blockIdx.x < total) gload(item(blockIdx.x), 0);
-#pragma unroll 1
-  for (int v = blockIdx.x; v < total; v += G) {
-  const Item it = item(v);
-  const int b = it.b, r0 = it.r0, c0 = it.c0, n0 = it.n0;
   f32x16 acc[2][2];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -159,6 +148,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_h3_kernel(DirectArgs g) {
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
   float s_cur = 0.f, s_min = __builtin_inff();
 
+  gload(0);
 #pragma unroll 1
   for (int k = 0; k < nk; ++k) {
     // 1. this chunk's weights into LDS; the halo's block-wide max
@@ -196,9 +186,8 @@ __global__ __launch_bounds__(256, 2) void conv3x3_h3_kernel(DirectArgs g) {
       }
     }
     __syncthreads();
-    // 3. the next chunk's loads (or the next item's first) fly during this chunk's MFMAs
-    if (k + 1 < nk) gload(it, k + 1);
-    else if (v + G < total) gload(item(v + G), 0);
+    // 3. the next chunk's loads fly during this chunk's MFMAs
+    if (k + 1 < nk) gload(k + 1);
 #pragma unroll
     for (int tap = 0; tap < 9; ++tap) {
       const int r = tap / 3, s = tap % 3;
@@ -287,8 +276,6 @@ __global__ __launch_bounds__(256, 2) void conv3x3_h3_kernel(DirectArgs g) {
       }
     }
   }
-  __syncthreads();  // the next item's staging overwrites the epilogue's LDS
-  }
 }
 
 bool direct_h3_shape_ok(int H, int W, int C, int N, int ldx) {
@@ -333,10 +320,7 @@ int launch_direct_h3(const IGemmArgs& a, int B, void* ws, size_t ws_bytes, hipSt
   g.x = a.src; g.ldx = a.lds; g.wp = wp; g.winv = winv; g.bias = a.bias; g.scale = a.scale;
   g.mask = a.mask; g.ldm = a.ldm; g.y = a.dst; g.ldy = a.ldd; g.pool = a.pool;
   g.B = B; g.H = a.H; g.W = a.W; g.C = C; g.N = N; g.flags = a.flags;
-  // persistent grid (pis_tune key 31 = k: k blocks per CU walk the items; 0: one block per item)
-  const int items = B * (a.H / DT_H) * (a.W / DT_W) * (N / 64);
-  const int per_cu = tune_get(PIS_TUNE_DIRECT_GRID);
-  const int blocks = per_cu > 0 ? std::min(items, 256 * per_cu) : items;
+  const int blocks = B * (a.H / DT_H) * (a.W / DT_W) * (N / 64);
   const double flop = 2.0 * 9 * (double)B * a.H * a.W * C * N;
   launch_hook("direct_h3", 0, s, flop);
   if (a.pool)
