@@ -288,6 +288,10 @@ bool direct_h3_wanted(int H, int W, int C, int N, int ldx) {
   const int lo = std::min(C, N), hi = std::max(C, N);
   if (mode == 3)  // + dec2.conv0 (256 <-> 128 at 256^2) and enc3.conv0 (128 <-> 256 at 128^2)
     return (H >= 256 && hi <= 256) || (H >= 128 && hi <= 256 && lo <= 128);
+  if (mode == 4)  // + every <= 256-channel layer at 128^2 (enc3, dec3.conv1)
+    return H >= 128 && hi <= 256;
+  if (mode == 5)  // + every layer at 128^2 and above
+    return H >= 128;
   return mode == 2 || (hi <= 128 && H >= 256);
 }
 
