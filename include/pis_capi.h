@@ -132,7 +132,9 @@ int pis_version(void);
                                    0 off (Winograd / halo kernels), 1 (default) auto: the shallow layers (<= 128
                                    channels on both sides, H >= 256),
                                    2 every shape it covers (H % 8, W % 32, C % 16, N % 64 == 0),
-                                   3 auto + the 128 <-> 256-channel layers at 256^2 and 128^2 */
+                                   3 auto + the 128 <-> 256-channel layers at 256^2 and 128^2, 4 H >= 128 and
+                                   <= 256 channels, 5 H >= 128 (3/4/5 measured slower on the C2 step:
+                                   profiles/r3_q8_direct_policy.txt) */
 #define PIS_TUNE_DIRECT_WG 30   /* direct fp16x3 weight gradient (key 29): 0 one LDS buffer, 4-row pixel tiles;
                                    1 two buffers, 2-row tiles, the next tile's split interleaved with this one's MFMAs */
 #define PIS_TUNE_NKEYS 31
