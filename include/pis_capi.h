@@ -137,7 +137,10 @@ int pis_version(void);
                                    profiles/r3_q8_direct_policy.txt) */
 #define PIS_TUNE_DIRECT_WG 30   /* direct fp16x3 weight gradient (key 29): 0 one LDS buffer, 4-row pixel tiles;
                                    1 two buffers, 2-row tiles, the next tile's split interleaved with this one's MFMAs */
-#define PIS_TUNE_NKEYS 31
+#define PIS_TUNE_WGRAD_T 31      /* fp16x3 weight-gradient GEMM (key 14) on plain 128 x 128 tiles (the Winograd weight
+                                    gradient): 1 operands staged as stored (float4 rows, transposed LDS reads, 32-pixel
+                                    K-steps, block-wide scales), 0 the column-staged wgrad_h3_kernel */
+#define PIS_TUNE_NKEYS 32
 #define PIS_DEBUG_NOLOAD (1 << 16)
 int pis_tune(int key, int value);
 /* Tooling (tools/bench_gemm.py): time one batched NT GEMM kernel variant in isolation,

@@ -44,6 +44,19 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
 }
 
+// The same over a 2-D grid of gridDim.y independent batches of gridDim.x blocks: the dispatcher
+// deals the flattened ids (x fastest) round-robin over the XCDs, so remapping the flattened id
+// gives each XCD runs of consecutive (batch, block) pairs — whole tile groups of one batch that
+// share operand rows in that XCD's L2 — instead of an eighth of every batch's blocks
+struct Remap2 {
+  int batch, bid;
+};
+__device__ __forceinline__ Remap2 xcd_remap2() {
+  const int gx = gridDim.x;
+  const int l = xcd_remap(blockIdx.y * gx + blockIdx.x, gx * gridDim.y);
+  return Remap2{l / gx, l % gx};
+}
+
 // ---- bf16x6: exact 3-way bf16 split of fp32 operands ------------------------
 // hi = bf16(x), mid = bf16(x - hi), lo = bf16(x - hi - mid); both subtractions are exact, and
 // hi + mid + lo == x (24 significant bits). Two values per step: one v_cvt_pk_bf16_f32 per level,
@@ -117,6 +130,14 @@ __device__ __forceinline__ float h3_keep(float cur, float m, float& smin) {
       __float_as_int(fminf((v >= 128.f && v < 32768.f) ? cur : h3_scale(m), smin * 0x1p32f))));
   smin = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(fminf(smin, s))));
   return s;
+}
+
+// 4 consecutive fp16 of one LDS row (8-B aligned) read transposed across the 16-lane group
+// (ds_read_b64_tr_b16): lane (4 q + p) of the group addresses row q, columns 4 p .. 4 p + 3 of a
+// 4 x 16 block; lane j of the group receives column j, rows 0..3
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ s16x4 tr_read(const _Float16* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(p));
 }
 
 template <int CTRL, int RMASK>

@@ -370,15 +370,8 @@ constexpr int WZ_ITEMS = WT_P * 8, WX_ITEMS = WH_P * 8;                   // 8-c
 constexpr int WZ_PER_T = WZ_ITEMS / 256, WX_PER_T = (WX_ITEMS + 255) / 256;  // 4, 7
 constexpr int WLDS_BYTES = 2 * (WZ_HALFS + WX_HALFS) * 2;
 
-typedef short s16x4 __attribute__((ext_vector_type(4)));
-
 // element offset of channel group (16-B chunk) ch of row `row` in a [row][64] fp16 image
 __device__ __forceinline__ int wsw64(int row, int ch) { return row * 64 + 8 * (ch ^ (((row >> 1) & 1) << 2)); }
-
-// 4 consecutive fp16 of one row (8-B aligned) read transposed across the 16-lane group
-__device__ __forceinline__ s16x4 tr_read(const _Float16* p) {
-  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(p));
-}
 
 __global__ __launch_bounds__(256, 1) void conv3x3_wgrad_h3_kernel(DirectWArgs g) {
   __shared__ __attribute__((aligned(16))) char smem[WLDS_BYTES + 64];

@@ -40,10 +40,11 @@ struct WgradArgs {
 // BKP pixels per stage: 32 MFMAs per wave between barriers for every tile shape
 template <int BM, int BN, int BKP>
 __global__ __launch_bounds__(256) void wgrad_f32_kernel(WgradArgs g) {
-  if (blockIdx.y) {
-    g.a += blockIdx.y * g.bs_a;
-    g.b += blockIdx.y * g.bs_b;
-    g.part += blockIdx.y * g.bs_part;
+  const Remap2 rm = xcd_remap2();
+  if (rm.batch) {
+    g.a += rm.batch * g.bs_a;
+    g.b += rm.batch * g.bs_b;
+    g.part += rm.batch * g.bs_part;
   }
   constexpr int TM = BM / 64, TN = BN / 64;   // 32x32 tiles per wave
   constexpr int AL = BKP * BM / 4 / 256, BL = BKP * BN / 4 / 256;
@@ -54,7 +55,7 @@ __global__ __launch_bounds__(256) void wgrad_f32_kernel(WgradArgs g) {
   const int wm = wave & 1, wn = wave >> 1;
   const int ntm = g.Mp / BM, ntn = g.Np / BN;
   const int tiles = ntm * ntn;
-  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int bid = rm.bid;
   const int split = bid / tiles;
   const int tile = bid - split * tiles;
   const int tm = tile / ntn, tn = tile % ntn;
@@ -579,10 +580,11 @@ __device__ __forceinline__ void wsplit_store(const float (&v)[E], __bf16* p0, __
 
 template <int BM, int BN>
 __global__ __launch_bounds__(256, 2) void wgrad_x6_kernel(WgradArgs g) {
-  if (blockIdx.y) {
-    g.a += blockIdx.y * g.bs_a;
-    g.b += blockIdx.y * g.bs_b;
-    g.part += blockIdx.y * g.bs_part;
+  const Remap2 rm = xcd_remap2();
+  if (rm.batch) {
+    g.a += rm.batch * g.bs_a;
+    g.b += rm.batch * g.bs_b;
+    g.part += rm.batch * g.bs_part;
   }
   constexpr int BK = 16;
   constexpr int TM = BM / 64, TN = BN / 64;
@@ -593,7 +595,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_x6_kernel(WgradArgs g) {
   const int wm = wave & 1, wn = wave >> 1, li = lane & 31, lh = lane >> 5;
   const int ntm = g.Mp / BM, ntn = g.Np / BN;
   const int tiles = ntm * ntn;
-  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int bid = rm.bid;
   const int split = bid / tiles;
   const int tile = bid - split * tiles;
   const int m0 = (tile / ntn) * BM, n0 = (tile % ntn) * BN;
@@ -722,10 +724,11 @@ __global__ __launch_bounds__(256, 2) void wgrad_x6_kernel(WgradArgs g) {
 // of block (a, b) is in units sA[wave of its row] * sB[wave of its column].
 template <int BM, int BN>
 __global__ __launch_bounds__(256, 2) void wgrad_h3_kernel(WgradArgs g) {
-  if (blockIdx.y) {
-    g.a += blockIdx.y * g.bs_a;
-    g.b += blockIdx.y * g.bs_b;
-    g.part += blockIdx.y * g.bs_part;
+  const Remap2 rm = xcd_remap2();
+  if (rm.batch) {
+    g.a += rm.batch * g.bs_a;
+    g.b += rm.batch * g.bs_b;
+    g.part += rm.batch * g.bs_part;
   }
   constexpr int BK = 16;
   constexpr int TM = BM / 64, TN = BN / 64;
@@ -739,7 +742,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_h3_kernel(WgradArgs g) {
   const int wm = wave & 1, wn = wave >> 1, li = lane & 31, lh = lane >> 5;
   const int ntm = g.Mp / BM, ntn = g.Np / BN;
   const int tiles = ntm * ntn;
-  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int bid = rm.bid;
   const int split = bid / tiles;
   const int tile = bid - split * tiles;
   const int m0 = (tile / ntn) * BM, n0 = (tile % ntn) * BN;
@@ -899,6 +902,198 @@ __global__ __launch_bounds__(256, 2) void wgrad_h3_kernel(WgradArgs g) {
   }
 }
 
+// The Winograd weight-gradient contraction in fp16x3 with the operands staged as they lie in
+// memory (pis_tune key 31 = 1): a K-step is 32 pixel rows x 128 columns of A (E[t][Cout]) and of
+// B (V[t][Cin]), loaded as float4s along the rows (512 contiguous bytes per 32 lanes), split into
+// hi / lo fp16 planes [pixel][column] with ONE power-of-two scale per operand per K-step (the
+// block-wide max, h3_keep), and the MFMA fragments (8 consecutive pixels of one column per lane)
+// come out by transposed reads (ds_read_b64_tr_b16). Compared with wgrad_h3_kernel: 4x fewer
+// global load instructions, twice the K per barrier, and the raw operands of K-step st + 2 in
+// flight while K-step st multiplies (two register sets); the next K-step's split runs in this
+// K-step's MFMA stream. Wave (wm, wn): rows 64 wm .., columns 64 wn .. of the 128 x 128 tile.
+// LDS rows are 256 B; the 16-B chunk index is XORed with 4 (row & 3), so a transposed read's
+// 32-lane half (4 rows x 4 chunks) meets 64 distinct banks and a row store (32 lanes) too.
+constexpr int WT_BK = 32;                        // pixels per K-step
+constexpr int WT_PLANE = WT_BK * 128;            // fp16 per plane
+constexpr int WT_BUF = 4 * WT_PLANE;             // A hi, A lo, B hi, B lo
+
+__device__ __forceinline__ int wtsw(int row, int chunk) { return row * 128 + 8 * (chunk ^ ((row & 3) << 2)); }
+
+__global__ __launch_bounds__(256, 2) void wgrad_h3t_kernel(WgradArgs g) {
+  const Remap2 rm = xcd_remap2();
+  if (rm.batch) {
+    g.a += rm.batch * g.bs_a;
+    g.b += rm.batch * g.bs_b;
+    g.part += rm.batch * g.bs_part;
+  }
+  __shared__ __attribute__((aligned(16))) _Float16 smem[2 * WT_BUF];
+  __shared__ float red[2][2][4];  // [K-step parity][A|B][wave] maxima
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave & 1, wn = wave >> 1, li = lane & 31, lh = lane >> 5;
+  const int ntn = g.Np / 128;
+  const int tiles = (g.Mp / 128) * ntn;
+  const int bid = rm.bid;
+  const int split = bid / tiles;
+  const int tile = bid - split * tiles;
+  const int m0 = (tile / ntn) * 128, n0 = (tile % ntn) * 128;
+  const int p_begin = split * g.pix_per_split;
+  const int p_end = min(g.P, p_begin + g.pix_per_split);
+  const int nst = max(0, (p_end - p_begin + WT_BK - 1) / WT_BK);
+  // staging: item i = tid + 256 j -> pixel row i >> 5, float4 column (i & 31)
+  const int srow = tid >> 5, sc4 = tid & 31;
+  const float* ga = g.a + m0 + 4 * sc4;
+  const float* gb = g.b + n0 + 4 * sc4;
+
+  f32x4 ra[2][4], rb[2][4];
+  auto gload = [&](f32x4 (&xa)[4], f32x4 (&xb)[4], int st) __attribute__((always_inline)) {
+    const int p0 = p_begin + st * WT_BK;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      // rows past the split's end: a valid row loaded, zeros kept (no divergent branch)
+      const int p = p0 + srow + 8 * j;
+      const bool ok = p < p_end;
+      const size_t pc = ok ? p : p_begin;
+      const f32x4 va = *reinterpret_cast<const f32x4*>(ga + pc * g.lda);
+      const f32x4 vb = *reinterpret_cast<const f32x4*>(gb + pc * g.ldb);
+      xa[j] = ok ? va : f32x4{0.f, 0.f, 0.f, 0.f};
+      xb[j] = ok ? vb : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  auto publish = [&](const f32x4 (&xa)[4], const f32x4 (&xb)[4], int par) __attribute__((always_inline)) {
+    float ma = 0.f, mb = 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        ma = fmaxf(ma, fabsf(xa[j][e]));
+        mb = fmaxf(mb, fabsf(xb[j][e]));
+      }
+    ma = wave_max_nonneg(ma);
+    mb = wave_max_nonneg(mb);
+    if (lane == 0) {
+      red[par][0][wave] = ma;
+      red[par][1][wave] = mb;
+    }
+  };
+  float sa_last = 0.f, sb_last = 0.f, sa_min = __builtin_inff(), sb_min = __builtin_inff();
+  auto split_store = [&](const f32x4 (&xa)[4], const f32x4 (&xb)[4], int par, float& sa, float& sb) __attribute__((always_inline)) {
+    const float ma = fmaxf(fmaxf(red[par][0][0], red[par][0][1]), fmaxf(red[par][0][2], red[par][0][3]));
+    const float mb = fmaxf(fmaxf(red[par][1][0], red[par][1][1]), fmaxf(red[par][1][2], red[par][1][3]));
+    sa = sa_last = h3_keep(sa_last, ma, sa_min);
+    sb = sb_last = h3_keep(sb_last, mb, sb_min);
+    _Float16* buf = smem + par * WT_BUF;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int off = wtsw(srow + 8 * j, sc4 >> 1) + 4 * (sc4 & 1);
+      u32x2 h, l;
+      split2h_x4(xa[j] * sa, h, l);
+      *reinterpret_cast<u32x2*>(buf + off) = h;
+      *reinterpret_cast<u32x2*>(buf + WT_PLANE + off) = l;
+      split2h_x4(xb[j] * sb, h, l);
+      *reinterpret_cast<u32x2*>(buf + 2 * WT_PLANE + off) = h;
+      *reinterpret_cast<u32x2*>(buf + 3 * WT_PLANE + off) = l;
+    }
+  };
+
+  // transposed-read lane roles: 16-lane group gq, its row q and 8-B slot p
+  const int gq = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
+  const int kh = gq >> 1, chk = 2 * (gq & 1) + (pp >> 1), slot = 4 * (pp & 1);
+  auto frag = [&](const _Float16* plane, int ks, int col0) __attribute__((always_inline)) {
+    const int row = 16 * ks + 8 * kh + q, ch = col0 / 8 + chk;
+    const s16x4 lo4 = tr_read(plane + wtsw(row, ch) + slot);
+    const s16x4 hi4 = tr_read(plane + wtsw(row + 4, ch) + slot);
+    return __builtin_bit_cast(f16x8, __builtin_shufflevector(lo4, hi4, 0, 1, 2, 3, 4, 5, 6, 7));
+  };
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+  float units = 0.f;  // scale product the partial sums are expressed in (0: none yet)
+  float s_a[2] = {0.f, 0.f}, s_b[2] = {0.f, 0.f};  // per buffer parity: the staged K-step's scales
+
+  if (nst > 0) {
+    gload(ra[0], rb[0], 0);
+    if (nst > 1) gload(ra[1], rb[1], 1);
+    publish(ra[0], rb[0], 0);
+    __syncthreads();
+    split_store(ra[0], rb[0], 0, s_a[0], s_b[0]);
+    if (nst > 2) gload(ra[0], rb[0], 2);
+  }
+  auto kstep = [&](int st, auto par_c) __attribute__((always_inline)) {
+    constexpr int cur = decltype(par_c)::value, nxt = cur ^ 1;
+    if (st + 1 < nst) publish(ra[nxt], rb[nxt], nxt);
+    __syncthreads();  // buffer cur staged; buffer nxt's readers (K-step st - 1) done
+    const _Float16* buf = smem + cur * WT_BUF;
+    f16x8 af[2][2], bf[2][2];
+#pragma unroll
+    for (int pl = 0; pl < 2; ++pl)
+#pragma unroll
+      for (int a = 0; a < 2; ++a) {
+        af[pl][a] = frag(buf + pl * WT_PLANE, 0, 64 * wm + 32 * a);
+        bf[pl][a] = frag(buf + (2 + pl) * WT_PLANE, 0, 64 * wn + 32 * a);
+      }
+    if (st + 1 < nst) {
+      split_store(ra[nxt], rb[nxt], nxt, s_a[nxt], s_b[nxt]);
+      if (st + 3 < nst) gload(ra[nxt], rb[nxt], st + 3);
+    }
+    {  // the partial sums in this K-step's units (exact: powers of two)
+      const float u = s_a[cur] * s_b[cur];
+      if (u != units) {
+        if (units != 0.f) {
+          const float f = u / units;
+#pragma unroll
+          for (int a = 0; a < 2; ++a)
+#pragma unroll
+            for (int b = 0; b < 2; ++b) acc[a][b] *= f;
+        }
+        units = u;
+      }
+    }
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      if (ks) {
+#pragma unroll
+        for (int pl = 0; pl < 2; ++pl)
+#pragma unroll
+          for (int a = 0; a < 2; ++a) {
+            af[pl][a] = frag(buf + pl * WT_PLANE, 1, 64 * wm + 32 * a);
+            bf[pl][a] = frag(buf + (2 + pl) * WT_PLANE, 1, 64 * wn + 32 * a);
+          }
+      }
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[1][a], bf[0][b], acc[a][b], 0, 0, 0);
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[0][a], bf[1][b], acc[a][b], 0, 0, 0);
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[0][a], bf[0][b], acc[a][b], 0, 0, 0);
+        }
+    }
+  };
+#pragma unroll 1
+  for (int st = 0; st < nst; st += 2) {
+    kstep(st, std::integral_constant<int, 0>{});
+    if (st + 1 < nst) kstep(st + 1, std::integral_constant<int, 1>{});
+  }
+  float* out = g.part + (size_t)split * (g.split_stride ? g.split_stride : (int64_t)g.Mp * g.Np);
+  const float inv = units != 0.f ? 1.f / units : 0.f;
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const int n = n0 + 64 * wn + 32 * b + li;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + 64 * wm + 32 * a + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        out[(size_t)m * g.Np + n] = acc[a][b][r] * inv;
+      }
+    }
+}
+
 static int run_wgrad(const WgradArgs& base, const WgradPlan& pl, hipStream_t s, int batches = 1) {
   WgradArgs a = base;
   a.pix_per_split = pl.pps;
@@ -915,6 +1110,13 @@ static int run_wgrad(const WgradArgs& base, const WgradPlan& pl, hipStream_t s, 
   const int cin = plain ? a.Np : a.Cb;
   if ((x6 == 2 || (x6 == 3 && cin >= 256)) && plain && pl.pps % 16 == 0 &&
       (!a.a_up2 || a.W % 8 == 0)) {
+    // key 31: the row-staged kernel for plain 128 x 128 tiles (float4 rows: 16-B aligned)
+    if (tune_get(PIS_TUNE_WGRAD_T) != 0 && pl.bm == 128 && pl.bn == 128 && !a.a_up2 && !a.part_bias &&
+        pl.pps % WT_BK == 0 && a.lda % 4 == 0 && a.ldb % 4 == 0 && a.bs_a % 4 == 0 && a.bs_b % 4 == 0 &&
+        ((uintptr_t)a.a & 15) == 0 && ((uintptr_t)a.b & 15) == 0) {
+      hipLaunchKernelGGL(wgrad_h3t_kernel, grid, dim3(256), 0, s, a);
+      return launch_status("wgrad_h3t");
+    }
     if (pl.bm == 128 && pl.bn == 128) hipLaunchKernelGGL((wgrad_h3_kernel<128, 128>), grid, dim3(256), 0, s, a);
     else if (pl.bm == 128) hipLaunchKernelGGL((wgrad_h3_kernel<128, 64>), grid, dim3(256), 0, s, a);
     else if (pl.bn == 128) hipLaunchKernelGGL((wgrad_h3_kernel<64, 128>), grid, dim3(256), 0, s, a);

@@ -955,13 +955,14 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const float* __restrict
   constexpr int AL = BM * CPR / 256, BL = BN * CPR / 256;  // float4 loads per thread per stage
   __shared__ __attribute__((aligned(16))) float sA[2][BM * ROW];
   __shared__ __attribute__((aligned(16))) float sB[2][BN * ROW];
-  A += blockIdx.y * bsA;
-  Bm += blockIdx.y * bsB;
-  Cm += blockIdx.y * bsC;
+  const Remap2 rm = xcd_remap2();
+  A += rm.batch * bsA;
+  Bm += rm.batch * bsB;
+  Cm += rm.batch * bsC;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave & 1, wn = wave >> 1, li = lane & 31, lh = lane >> 5;
   const int ntn = N / BN;
-  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int bid = rm.bid;
   const int m0 = (bid / ntn) * BM, n0 = (bid % ntn) * BN;
   const int q4 = (tid % CPR) * 4;
   f32x4 ra[AL], rb[BL];
@@ -1055,13 +1056,14 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_x6_kernel(
   constexpr int AL = BM * 4 / 256, BL = BN * 4 / 256;  // float4 loads per thread per stage
   __shared__ __attribute__((aligned(16))) __bf16 sA[2][3][BM * BK];  // [buf][hi|mid|lo][row][k]
   __shared__ __attribute__((aligned(16))) __bf16 sB[2][3][BN * BK];
-  A += blockIdx.y * bsA;
-  Bm += blockIdx.y * bsB;
-  Cm += blockIdx.y * bsC;
+  const Remap2 rm = xcd_remap2();
+  A += rm.batch * bsA;
+  Bm += rm.batch * bsB;
+  Cm += rm.batch * bsC;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave & 1, wn = wave >> 1, li = lane & 31, lh = lane >> 5;
   const int ntn = N / BN;
-  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int bid = rm.bid;
   const int m0 = (bid / ntn) * BM, n0 = (bid % ntn) * BN;
   const int q4 = (tid & 3) * 4;
   const bool full = m0 + BM <= M && K % BK == 0;
@@ -1201,13 +1203,14 @@ __global__ __launch_bounds__(256, OCC) void gemm_nt_x6_bk32_kernel(const float* 
   constexpr int AL = BM * 8 / 256, BL = BN * 8 / 256;  // float4 loads per thread per stage
   __shared__ __attribute__((aligned(16))) __bf16 sA[3][BM * KP];
   __shared__ __attribute__((aligned(16))) __bf16 sB[3][BN * KP];
-  A += blockIdx.y * bsA;
-  Bm += blockIdx.y * bsB;
-  Cm += blockIdx.y * bsC;
+  const Remap2 rm = xcd_remap2();
+  A += rm.batch * bsA;
+  Bm += rm.batch * bsB;
+  Cm += rm.batch * bsC;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave & 1, wn = wave >> 1, li = lane & 31, lh = lane >> 5;
   const int ntn = N / BN;
-  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int bid = rm.bid;
   const int m0 = (bid / ntn) * BM, n0 = (bid % ntn) * BN;
   const int q8 = (tid & 7) * 4;
   const bool full = m0 + BM <= M && K % BK == 0;
@@ -1336,13 +1339,14 @@ __global__ __launch_bounds__(256, OCC) void gemm_nt_h3_bk32_kernel(const float* 
   __shared__ __attribute__((aligned(16))) _Float16 sB[2][BN * KP];
   __shared__ __attribute__((aligned(16))) float sscale[2][4];  // [A|B][staging wave]
   __shared__ float sinv[PRE ? BM + BN : 1];                    // PRE: 1 / scale of each A, B row
-  A += blockIdx.y * bsA;
-  Bm += blockIdx.y * bsB;
-  Cm += blockIdx.y * bsC;
+  const Remap2 rm = xcd_remap2();
+  A += rm.batch * bsA;
+  Bm += rm.batch * bsB;
+  Cm += rm.batch * bsC;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave & 1, wn = wave >> 1, li = lane & 31, lh = lane >> 5;
   const int ntn = N / BN;
-  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int bid = rm.bid;
   const int m0 = (bid / ntn) * BM, n0 = (bid % ntn) * BN;
   const int q8 = (tid & 7) * 4;
   // PRE: the staged rows' scales as biased exponent bytes (AL, BL <= 4: one register each)
@@ -1709,13 +1713,14 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_x6_w8_kernel(const float* __re
   extern __shared__ __attribute__((aligned(16))) __bf16 smem_x6w8[];
   __bf16* const buf0 = smem_x6w8;
   __bf16* const buf1 = smem_x6w8 + 3 * ROWS * 32;
-  A += blockIdx.y * bsA;
-  Bm += blockIdx.y * bsB;
-  Cm += blockIdx.y * bsC;
+  const Remap2 rm = xcd_remap2();
+  A += rm.batch * bsA;
+  Bm += rm.batch * bsB;
+  Cm += rm.batch * bsC;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave & 3, wn = wave >> 2, li = lane & 31, lh = lane >> 5;
   const int ntn = N / BN;
-  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int bid = rm.bid;
   const int m0 = (bid / ntn) * BM, n0 = (bid % ntn) * BN;
   const int q8 = (tid & 7) * 4;  // k offset of this thread's float4 within the 32-wide step
   const bool full = m0 + BM <= M;

@@ -697,6 +697,46 @@ def test_wgrad_fp16x3_mixed_magnitude_samples(hip, Cin, Cout):
         assert errs[2] < 5e-6, (order, errs)
 
 
+@pytest.mark.parametrize("B,H,W,Cin,Cout", [(2, 64, 64, 256, 256), (2, 36, 36, 512, 128), (1, 12, 20, 128, 256)])
+@pytest.mark.parametrize("mags", [(1.0, 1.0), (1.0, 1e-30), (1e-30, 1.0), (1e-9, 1e-9)])
+def test_wgrad_rowstaged_fp16x3(hip, B, H, W, Cin, Cout, mags):
+    """The row-staged fp16x3 Winograd weight-gradient GEMM (pis_tune(31, 1): float4 row loads,
+    transposed LDS reads, 32-pixel K-steps, block-wide scales, two register sets in flight) against
+    float64, next to the column-staged fp16x3 kernel (31 = 0) and the fp32 MFMA path (14 = 0):
+    K-step counts from 1 to 16 per split with ragged tails (T = 162, 15), and per-sample dz
+    magnitudes 1e30 apart in both orders (the scale jumps inside one accumulation chain)."""
+    g = torch.Generator().manual_seed(71)
+    x = F.relu(torch.randn(B, Cin, H, W, generator=g, dtype=torch.float64)).float().double()
+    dz = torch.randn(B, Cout, H, W, generator=g, dtype=torch.float64)
+    for i in range(B):
+        dz[i] *= mags[i % 2]
+    dz = dz.float().double()
+    dw_ref = torch.nn.grad.conv2d_weight(x, (Cout, Cin, 3, 3), dz, padding=1)
+    db_ref = dz.sum(dim=(0, 2, 3))
+    xd, dzd = nhwc(x.float()).cuda(), nhwc(dz.float()).cuda()
+    errs = {}
+    for name, knobs in (("f32", {14: 0}), ("h3col", {14: 2, 31: 0}), ("h3row", {14: 2, 31: 1})):
+        prev = {k: hip.pis_tune(k, v) for k, v in knobs.items()}
+        try:
+            nws = hip.pis_conv3x3_wgrad_ws(B, H, W, Cin, Cout)
+            ws = torch.empty(nws // 4 + 1, device="cuda")
+            dw = torch.empty(Cout, 3, 3, Cin, device="cuda")
+            db = torch.empty(Cout, device="cuda")
+            rc = hip.pis_conv3x3_wgrad(xd.data_ptr(), Cin, dzd.data_ptr(), Cout, dw.data_ptr(), db.data_ptr(),
+                                       B, H, W, Cin, Cout, 0, ws.data_ptr(), nws, s())
+            assert rc == 0, hip.pis_last_error()
+            torch.cuda.synchronize()
+        finally:
+            for k, v in prev.items():
+                hip.pis_tune(k, v)
+        dwc = dw.cpu().permute(0, 3, 1, 2).double()
+        assert torch.isfinite(dwc).all(), name
+        errs[name] = ((dwc - dw_ref).norm() / dw_ref.norm()).item()
+        assert rel_err(db.cpu().double(), db_ref) < 1e-5, name
+    assert errs["h3row"] <= 1.25 * errs["f32"] + 1e-9, errs
+    assert errs["h3row"] < 5e-6, errs
+
+
 @pytest.mark.parametrize("Cin,Cout", [(128, 64), (512, 256)])
 def test_convt_bf16x6_is_fp32_accurate(hip, Cin, Cout):
     """Transposed conv forward / input gradient (key 13: 1 bf16x6, 3 fp16x3 vs 2 fp32 MFMA) and

@@ -29,6 +29,10 @@ for x in "$@"; do
     dstall) run dstall 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_VALU_MFMA_BUSY_CYCLES -d "$OUT/dstall" -o run --output-format csv -- python3 tools/bench_kernels.py --key 29 --variants 2 --ops fwd,dgrad,wgrad --rounds 1 --layers enc1.conv1,enc2.conv1 && run dstall2 120 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_INSTS_VALU_MFMA_MOPS_F16 SQ_INSTS_SALU SQ_WAIT_INST_LDS -d "$OUT/dstall2" -o run --output-format csv -- python3 tools/bench_kernels.py --key 29 --variants 2 --ops fwd,dgrad,wgrad --rounds 1 --layers enc1.conv1,enc2.conv1 ;;
     grid31) run grid31 300 python -u tools/bench_kernels.py --key 31 --variants 0,2,4 --ops fwd,dgrad --rounds 3 --layers enc1.conv1,dec1.conv0,enc2.conv1,enc2.conv0 ;;
     bench31) run bench_g0 300 python -u bench.py --no-cpu-baseline --steps 20 --tune 31=0 && run bench_g2 300 python -u bench.py --no-cpu-baseline --steps 20 --tune 31=2 && run bench_g4 300 python -u bench.py --no-cpu-baseline --steps 20 --tune 31=4 && run bench_g0b 300 python -u bench.py --no-cpu-baseline --steps 20 --tune 31=0 ;;
+    wgt) run wgrad_t 300 python -u tools/bench_kernels.py --key 31 --variants 0,1 --ops wgrad --rounds 3 --layers dec2.conv0,enc3.conv1,dec3.conv0,enc4.conv0,enc4.conv1,dec4.conv0,bottleneck ;;
+    benchwt) for v in 0 1 0 1; do run bench_wt$v 300 python -u bench.py --no-cpu-baseline --steps 20 --tune 31=$v || exit 1; done ;;
+    wgtpmc) run wgtpmc 120 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_INSTS_VALU SQ_LDS_BANK_CONFLICT SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY -d "$OUT/wgtpmc" -o run --output-format csv -- python3 tools/bench_kernels.py --key 31 --variants 0,1 --ops wgrad --rounds 1 --layers enc3.conv1,enc4.conv1,bottleneck ;;
+    wgthbm) run wgthbm1 120 rocprofv3 --pmc FETCH_SIZE GRBM_GUI_ACTIVE -d "$OUT/wgthbm1" -o run --output-format csv -- python3 tools/bench_kernels.py --key 31 --variants 0,1 --ops wgrad --rounds 1 --layers enc3.conv1,enc4.conv1,dec4.conv0 && run wgthbm2 120 rocprofv3 --pmc WRITE_SIZE -d "$OUT/wgthbm2" -o run --output-format csv -- python3 tools/bench_kernels.py --key 31 --variants 0,1 --ops wgrad --rounds 1 --layers enc3.conv1,enc4.conv1,dec4.conv0 && run wgtkt 120 rocprofv3 --kernel-trace --stats -d "$OUT/wgtkt" -o run --output-format csv -- python3 tools/bench_kernels.py --key 31 --variants 0,1 --ops wgrad --rounds 1 --layers enc3.conv1,enc4.conv1,dec4.conv0 ;;
     pol) for v in 1 3 4 5 1; do run bench_p$v 300 python -u bench.py --no-cpu-baseline --steps 20 --tune 29=$v || exit 1; done ;;
     bench29) run bench_k29_0 300 python -u bench.py --no-cpu-baseline --steps 20 && run bench_k29_1 300 python -u bench.py --no-cpu-baseline --steps 20 --tune 29=1 ;;
     direct) run direct_kernels 300 python -u tools/bench_kernels.py --key 29 --variants 0,2 --ops fwd,dgrad --rounds 3 --layers enc1.conv1,dec1.conv0,enc2.conv0,enc2.conv1,dec2.conv0,enc3.conv0,enc3.conv1 ;;
