@@ -75,9 +75,8 @@ int pis_version(void);
                                     above 2^-22 accumulated in fp32 (measured error below fp32 MFMA's and bf16x6's) */
 #define PIS_TUNE_WINO_F4 11      /* Winograd tile: 0 F(2x2,3x3) fwd/dgrad + F(3x3,2x2) wgrad; 1 (default) F(4x4,3x3) +
                                     F(3x3,4x4) when H % 4 == W % 4 == 0 */
-#define PIS_TUNE_WINO_FUSED 12   /* F(4x4,3x3) fwd/dgrad as ONE fused kernel (transforms in LDS/registers): 0/1 off
-                                    (auto: measured slower than the 3-pass pipeline on every layer that keeps V),
-                                    2 whenever H % 16 == W % 64 == N % 16 == 0 */
+#define PIS_TUNE_WINO_FUSED 12   /* retired (round 3): the one-kernel F(4x4,3x3) was slower than the 3-pass pipeline
+                                    on every layer; the key is accepted and ignored */
 #define PIS_TUNE_CONVT_GEMM 13   /* transposed conv fwd/dgrad: lean NT GEMM with gather/scatter addressing when
                                     Cin, Cout % 16 == 0 — 3 (default) fp32-class fp16x3 on fp16 MFMA (per-wave,
                                     per-K-step power-of-two scales), 1 bf16x6 on bf16 MFMA, 2 on fp32 MFMA; 0 generic
@@ -106,15 +105,10 @@ int pis_version(void);
 #define PIS_TUNE_WINO_GEMM_OUT_H3 22 /* the fused 64 -> 64 kernel (key 15): 1 fp16x3 (per-(tile, xi, K-step) power-of-two
                                         scales, hi + lo fp16, 3 products; its filter planes, also those written by
                                         pis_conv3x3_filter(s), switch format with it), 0 bf16x6 */
-#define PIS_TUNE_WINO_H3_PRE 23  /* the batched fp16x3 Winograd GEMM (key 10 = 4) with C, N % 64 == 0: 0 (default)
-                                    per-wave, per-K-step scales inside the GEMM; 1 one power-of-two scale per A row
-                                    (tile) and per B row (output channel) for the whole contraction, from maxima the
-                                    input / dz / filter transforms write (no in-loop scales; measured slower: GEMM
-                                    +10 %, input transform +11 %, step -1.7 %, profiles/r2_q65_*, r2_q66_*) */
-#define PIS_TUNE_WINO_PERSIST 24 /* batched fp16x3 Winograd GEMM (key 10 = 4), N % 128 == 0: a persistent kernel (blocks walk
-                                    the tiles as one stream of K-steps) for contractions of C <= 32 x value channels;
-                                    0 (default) never — per layer within +-1 %, the step +0.4 % slower with one shared
-                                    model (profiles/r2_q70_*, r2_q72_*) */
+#define PIS_TUNE_WINO_H3_PRE 23  /* retired (round 3): producer-written row scales for the batched fp16x3 GEMM measured
+                                    slower (GEMM +10 %, input transform +11 %, profiles/r2_q65_*); ignored */
+#define PIS_TUNE_WINO_PERSIST 24 /* retired (round 3): the persistent batched GEMM was within +-1 % per layer and
+                                    +0.4 % on the step (profiles/r2_q70_*, r2_q72_*); ignored */
 #define PIS_TUNE_FUSED_STAGGER 25 /* fused 64 -> 64 kernel in fp16x3 (key 22): 1 the SIMD-partner waves fold one xi late
                                      (stagger; bit-for-bit the same), 0 (default) all waves in lockstep */
 #define PIS_TUNE_FUSED_WIDE 26   /* v: the fused contraction + output transform (key 15) for up to 64 x 2^v output
@@ -125,9 +119,7 @@ int pis_version(void);
                                     contractions (128 -> 64, and 128 -> 128 with key 26; the SIMD-partner waves always
                                     staggered: dec1.conv0 forward -11 %, enc2.conv0 input gradient -15 %);
                                     0: 64-channel contractions only */
-#define PIS_TUNE_FUSED_PAIR 28   /* fused kernel, 64-channel contractions in fp16x3 (key 22), lockstep form: 1 two xi per
-                                    barrier (four LDS operand buffers; the two products' MFMA chains interleave),
-                                    0 one xi per barrier; bit-for-bit the same sums */
+#define PIS_TUNE_FUSED_PAIR 28   /* retired (round 3): two xi per barrier in the fused kernel was not faster; ignored */
 #define PIS_TUNE_DIRECT_H3 29   /* direct 3x3 conv in fp16x3 (csrc/direct.hip; forward, input and weight gradient):
                                    0 off (Winograd / halo kernels), 1 (default) auto: the shallow layers (<= 128
                                    channels on both sides, H >= 256),
@@ -135,8 +127,8 @@ int pis_version(void);
                                    3 auto + the 128 <-> 256-channel layers at 256^2 and 128^2, 4 H >= 128 and
                                    <= 256 channels, 5 H >= 128 (3/4/5 measured slower on the C2 step:
                                    profiles/r3_q8_direct_policy.txt) */
-#define PIS_TUNE_DIRECT_WG 30   /* direct fp16x3 weight gradient (key 29): 0 one LDS buffer, 4-row pixel tiles;
-                                   1 two buffers, 2-row tiles, the next tile's split interleaved with this one's MFMAs */
+#define PIS_TUNE_DIRECT_WG 30    /* retired (round 3): the double-buffered direct weight gradient (2-row tiles, 512
+                                    registers per lane) measured slower than the single-buffer kernel; ignored */
 #define PIS_TUNE_WGRAD_T 31      /* fp16x3 weight-gradient GEMM (key 14) on plain 128 x 128 tiles (the Winograd weight
                                     gradient): 1 operands staged as stored (float4 rows, transposed LDS reads, 32-pixel
                                     K-steps, block-wide scales), 0 the column-staged wgrad_h3_kernel */
@@ -146,9 +138,9 @@ int pis_tune(int key, int value);
 /* Tooling (tools/bench_gemm.py): time one batched NT GEMM kernel variant in isolation,
  * C[b] = A[b] . B[b]^T row-major fp32 — 0 bf16x6 128x128 (the Winograd GEMM), 1/2 its
  * no-global-load / no-split timing twins (wrong results), 3 fp32 MFMA, 4 bf16x6 128x64, 5/6 the
- * K-step-32 single-LDS-buffer bf16x6 128x128 (2 / 3 waves per SIMD; 6 is the Winograd default), 7
- * its 128x64, 8 the 8-wave 256x128 two-stage pipelined bf16x6 kernel (9: its no-global-load twin).
- * 5-9 need K % 32 == 0. */
+ * K-step-32 single-LDS-buffer bf16x6 128x128 (2 / 3 waves per SIMD), 7 its 128x64, 10 / 11 the
+ * fp16x3 128x128 GEMM unscaled / with per-K-step scales (11 is the Winograd default), 12 its 128x64.
+ * 5-12 need K % 32 == 0. */
 int pis_debug_gemm_nt(const float* A, const float* B, float* C, int M, int N, int K, int batch, int variant,
                       pis_stream_t stream);
 

@@ -549,219 +549,6 @@ __global__ __launch_bounds__(256, 1) void conv3x3_wgrad_h3_kernel(DirectWArgs g)
   }
 }
 
-// The same weight gradient, software-pipelined (pis_tune key 30 = 1): 2-row pixel tiles (64 px, 4
-// K-steps; the 4 x 34 x 64 halo) in TWO LDS buffers (100 KB), one barrier per tile. In iteration t the
-// block runs tile t's MFMAs from buffer t & 1 while it splits tile t + 1 (loaded into registers
-// during iteration t - 1) into buffer (t + 1) & 1, interleaved K-step by K-step, and issues tile
-// t + 2's global loads: the staging VALU and LDS writes fill the gaps of the MFMA stream instead of
-// running between barriers. Tile t + 1's scales come from block maxima published before the
-// barrier (a second, double-indexed reduction slot), so they are known when its split starts;
-// the partial sums are re-expressed in tile t + 1's units before its first MFMA.
-constexpr int W2_H = 2, W2_P = W2_H * WT_W, W2_HH = W2_H + 2, W2_HP = W2_HH * WH_W;      // 64 px, 136 halo px
-constexpr int W2Z_HALFS = W2_P * 64, W2X_HALFS = W2_HP * 64;
-constexpr int W2Z_PER_T = W2_P * 8 / 256, W2X_ITEMS = W2_HP * 8, W2X_PER_T = (W2X_ITEMS + 255) / 256;  // 2, 5
-constexpr int W2_BUF_HALFS = 2 * (W2Z_HALFS + W2X_HALFS);  // one buffer: hi / lo planes of both operands
-constexpr int W2_LDS_BYTES = 2 * W2_BUF_HALFS * 2;
-
-__global__ __launch_bounds__(256, 1) void conv3x3_wgrad_h3db_kernel(DirectWArgs g) {
-  __shared__ __attribute__((aligned(16))) char smem[W2_LDS_BYTES + 2 * 8 * 4];
-  _Float16* lds = reinterpret_cast<_Float16*>(smem);
-  float* red = reinterpret_cast<float*>(smem + W2_LDS_BYTES);  // [2 tiles][dz 4 | x 4] wave maxima
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wi = wave >> 1, wj = wave & 1;
-  const int ncb = g.Cin / 64, pairs = (g.Cout / 64) * ncb;
-  const int pair = blockIdx.x % pairs, split = blockIdx.x / pairs;
-  const int n0 = (pair / ncb) * 64, c0 = (pair % ncb) * 64;
-  const int tw_n = g.W / WT_W, per_img = (g.H / W2_H) * tw_n, ntile = g.B * per_img;
-  const bool do_bias = g.part_bias != nullptr && c0 == 0;
-  auto zbuf = [&](int buf) { return lds + buf * W2_BUF_HALFS; };                 // [plane][64 px][64]
-  auto xbuf = [&](int buf) { return lds + buf * W2_BUF_HALFS + 2 * W2Z_HALFS; };  // [plane][136 px][64]
-
-  f32x4 zr[W2Z_PER_T][2], xr[W2X_PER_T][2];
-  auto gload = [&](int t) {
-    const int b = t / per_img, rem = t - b * per_img, pr0 = (rem / tw_n) * W2_H, pc0 = (rem % tw_n) * WT_W;
-    const size_t img = (size_t)b * g.H * g.W;
-#pragma unroll
-    for (int j = 0; j < W2Z_PER_T; ++j) {
-      const int i = tid + 256 * j, px = i >> 3, cg = i & 7;
-      const float* p = g.dz + (img + (size_t)(pr0 + (px >> 5)) * g.W + pc0 + (px & 31)) * g.ldz + n0 + 8 * cg;
-      zr[j][0] = *reinterpret_cast<const f32x4*>(p);
-      zr[j][1] = *reinterpret_cast<const f32x4*>(p + 4);
-    }
-#pragma unroll
-    for (int j = 0; j < W2X_PER_T; ++j) {
-      const int i = tid + 256 * j, q = i >> 3, cg = i & 7;
-      xr[j][0] = xr[j][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (i < W2X_ITEMS) {
-        const int qr = q / WH_W, qc = q - qr * WH_W, row = pr0 - 1 + qr, col = pc0 - 1 + qc;
-        if (row >= 0 && row < g.H && col >= 0 && col < g.W) {
-          const float* p = g.x + (img + (size_t)row * g.W + col) * g.ldx + c0 + 8 * cg;
-          xr[j][0] = *reinterpret_cast<const f32x4*>(p);
-          xr[j][1] = *reinterpret_cast<const f32x4*>(p + 4);
-        }
-      }
-    }
-  };
-  // the registers' wave maxima -> red[slot]; bias partials from the raw dz
-  float bs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  auto publish = [&](int slot) {
-    float mz = 0.f, mx = 0.f;
-#pragma unroll
-    for (int j = 0; j < W2Z_PER_T; ++j)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        mz = fmaxf(mz, fmaxf(fabsf(zr[j][0][e]), fabsf(zr[j][1][e])));
-        if (do_bias) {
-          bs[e] += zr[j][0][e];
-          bs[4 + e] += zr[j][1][e];
-        }
-      }
-#pragma unroll
-    for (int j = 0; j < W2X_PER_T; ++j)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) mx = fmaxf(mx, fmaxf(fabsf(xr[j][0][e]), fabsf(xr[j][1][e])));
-    mz = wave_max_nonneg(mz);
-    mx = wave_max_nonneg(mx);
-    if (lane == 0) {
-      red[8 * slot + wave] = mz;
-      red[8 * slot + 4 + wave] = mx;
-    }
-  };
-  // part `part` (of 4) of the split of the registers into buffer buf with scales sz, sx
-  auto stage = [&](int buf, int part, float sz, float sx) {
-    _Float16* zb = zbuf(buf);
-    _Float16* xb = xbuf(buf);
-    if (part < W2Z_PER_T) {
-      const int i = tid + 256 * part, px = i >> 3, cg = i & 7;
-      u32x2 h0, l0, h1, l1;
-      split2h_x4(zr[part][0] * sz, h0, l0);
-      split2h_x4(zr[part][1] * sz, h1, l1);
-      *reinterpret_cast<u32x4*>(&zb[wsw64(px, cg)]) = u32x4{h0[0], h0[1], h1[0], h1[1]};
-      *reinterpret_cast<u32x4*>(&zb[W2Z_HALFS + wsw64(px, cg)]) = u32x4{l0[0], l0[1], l1[0], l1[1]};
-    }
-#pragma unroll
-    for (int j = part; j < W2X_PER_T; j += 4) {
-      const int i = tid + 256 * j, q = i >> 3, cg = i & 7;
-      if (i < W2X_ITEMS) {
-        u32x2 h0, l0, h1, l1;
-        split2h_x4(xr[j][0] * sx, h0, l0);
-        split2h_x4(xr[j][1] * sx, h1, l1);
-        *reinterpret_cast<u32x4*>(&xb[wsw64(q, cg)]) = u32x4{h0[0], h0[1], h1[0], h1[1]};
-        *reinterpret_cast<u32x4*>(&xb[W2X_HALFS + wsw64(q, cg)]) = u32x4{l0[0], l0[1], l1[0], l1[1]};
-      }
-    }
-  };
-
-  f32x16 acc[9];
-#pragma unroll
-  for (int t = 0; t < 9; ++t)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
-  float sz_cur = 0.f, sx_cur = 0.f, sz_min = __builtin_inff(), sx_min = __builtin_inff();
-  const int gq = lane >> 4, q = (lane & 15) >> 2, p = lane & 3, kh = gq >> 1;
-  const int cgA = 4 * wi + 2 * (gq & 1) + (p >> 1), cgB = 4 * wj + 2 * (gq & 1) + (p >> 1);
-
-  // prologue: tile `split` into buffer 0 (its scales), tile split + splits into registers
-  int t = split;
-  if (t < ntile) {
-    gload(t);
-    publish(0);
-    __syncthreads();
-    const float mz = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
-    const float mx = fmaxf(fmaxf(red[4], red[5]), fmaxf(red[6], red[7]));
-    sz_cur = h3_keep(0.f, mz, sz_min);
-    sx_cur = h3_keep(0.f, mx, sx_min);
-#pragma unroll
-    for (int part = 0; part < 4; ++part) stage(0, part, sz_cur, sx_cur);
-    if (t + g.splits < ntile) gload(t + g.splits);
-  }
-  int it = 0;
-#pragma unroll 1
-  for (; t < ntile; t += g.splits, ++it) {
-    const int cur = it & 1;
-    const bool more = t + g.splits < ntile;
-    if (more) publish(cur ^ 1);  // tile t + 1's maxima (its data is in the registers)
-    __syncthreads();             // buffer cur complete; red[cur ^ 1] visible; buffer cur ^ 1 free
-    float sz_nx = sz_cur, sx_nx = sx_cur;
-    if (more) {
-      const float mz = fmaxf(fmaxf(red[8 * (cur ^ 1)], red[8 * (cur ^ 1) + 1]),
-                             fmaxf(red[8 * (cur ^ 1) + 2], red[8 * (cur ^ 1) + 3]));
-      const float mx = fmaxf(fmaxf(red[8 * (cur ^ 1) + 4], red[8 * (cur ^ 1) + 5]),
-                             fmaxf(red[8 * (cur ^ 1) + 6], red[8 * (cur ^ 1) + 7]));
-      sz_nx = h3_keep(sz_cur, mz, sz_min);
-      sx_nx = h3_keep(sx_cur, mx, sx_min);
-    }
-    const _Float16* zb = zbuf(cur);
-    const _Float16* xb = xbuf(cur);
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {  // K-steps: tile row ks >> 1, columns 16 (ks & 1) ..
-      const int rr = ks >> 1, cc0 = 16 * (ks & 1);
-      f16x8 a[2];
-#pragma unroll
-      for (int pl = 0; pl < 2; ++pl) {
-        const _Float16* base = zb + pl * W2Z_HALFS;
-        const int px = 16 * ks + 8 * kh + q;
-        const s16x4 lo4 = tr_read(base + wsw64(px, cgA) + 4 * (p & 1));
-        const s16x4 hi4 = tr_read(base + wsw64(px + 4, cgA) + 4 * (p & 1));
-        a[pl] = __builtin_bit_cast(f16x8, __builtin_shufflevector(lo4, hi4, 0, 1, 2, 3, 4, 5, 6, 7));
-      }
-#pragma unroll
-      for (int tap = 0; tap < 9; ++tap) {
-        const int r = tap / 3, s = tap % 3;
-        f16x8 bb[2];
-        const int hp = (rr + r) * WH_W + cc0 + 8 * kh + q + s;
-#pragma unroll
-        for (int pl = 0; pl < 2; ++pl) {
-          const _Float16* base = xb + pl * W2X_HALFS;
-          const s16x4 lo4 = tr_read(base + wsw64(hp, cgB) + 4 * (p & 1));
-          const s16x4 hi4 = tr_read(base + wsw64(hp + 4, cgB) + 4 * (p & 1));
-          bb[pl] = __builtin_bit_cast(f16x8, __builtin_shufflevector(lo4, hi4, 0, 1, 2, 3, 4, 5, 6, 7));
-        }
-        acc[tap] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[1], bb[0], acc[tap], 0, 0, 0);
-        acc[tap] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[0], bb[1], acc[tap], 0, 0, 0);
-        acc[tap] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[0], bb[0], acc[tap], 0, 0, 0);
-      }
-      if (more) stage(cur ^ 1, ks, sz_nx, sx_nx);  // tile t + 1, a quarter per K-step
-    }
-    if (more) {
-      if (t + 2 * g.splits < ntile) gload(t + 2 * g.splits);
-      if (sz_nx != sz_cur || sx_nx != sx_cur) {  // tile t + 1's units for everything accumulated so far
-        const float f = (sz_nx / sz_cur) * (sx_nx / sx_cur);
-#pragma unroll
-        for (int k = 0; k < 9; ++k) acc[k] *= f;
-      }
-      sz_cur = sz_nx;
-      sx_cur = sx_nx;
-    }
-  }
-  __syncthreads();
-
-  const float inv = (sz_cur > 0.f) ? (1.f / sz_cur) * (1.f / sx_cur) : 0.f;
-  float* slab = g.part + (size_t)split * g.Cout * 9 * g.Cin;
-  const int c = c0 + 32 * wj + (lane & 31);
-#pragma unroll
-  for (int tap = 0; tap < 9; ++tap)
-#pragma unroll
-    for (int reg = 0; reg < 16; ++reg) {
-      const int n = n0 + 32 * wi + (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5);
-      slab[((size_t)n * 9 + tap) * g.Cin + c] = acc[tap][reg] * inv;
-    }
-  if (do_bias) {
-    float* rb = reinterpret_cast<float*>(smem);
-#pragma unroll
-    for (int e = 0; e < 8; ++e) rb[tid * 8 + e] = bs[e];
-    __syncthreads();
-    if (tid < 64) {
-      const int cg = tid >> 3, e = tid & 7;
-      float sum = 0.f;
-      for (int k = 0; k < 32; ++k) sum += rb[(8 * k + cg) * 8 + e];
-      g.part_bias[(size_t)split * g.Cout + n0 + tid] = sum;
-    }
-  }
-}
-
-static bool direct_w_db() { return tune_get(PIS_TUNE_DIRECT_WG) == 1; }
-
 bool direct_w_wanted(int B, int H, int W, int Cin, int Cout, int ldx, int ldz) {
   return B > 0 && H % WT_H == 0 && W % WT_W == 0 && Cin % 64 == 0 && Cout % 64 == 0 && ldz % 4 == 0 &&
          direct_h3_wanted(H, W, Cin, Cout, ldx);
@@ -769,7 +556,7 @@ bool direct_w_wanted(int B, int H, int W, int Cin, int Cout, int ldx, int ldz) {
 
 static int direct_w_splits(int B, int H, int W, int Cin, int Cout) {
   const int pairs = (Cout / 64) * (Cin / 64);
-  const int ntile = B * (H / (direct_w_db() ? W2_H : WT_H)) * (W / WT_W);
+  const int ntile = B * (H / WT_H) * (W / WT_W);
   return std::max(1, std::min(ntile, 256 / std::max(1, std::min(pairs, 256))));
 }
 
@@ -792,10 +579,7 @@ int launch_direct_wgrad(const float* x, int ldx, const float* dz, int ldz, float
   const int pairs = (Cout / 64) * (Cin / 64);
   const double flop = 2.0 * 9 * (double)B * H * W * Cin * Cout;
   launch_hook("direct_wgrad_h3", 0, s, flop);
-  if (direct_w_db())
-    hipLaunchKernelGGL(conv3x3_wgrad_h3db_kernel, dim3(g.splits * pairs), dim3(256), 0, s, g);
-  else
-    hipLaunchKernelGGL(conv3x3_wgrad_h3_kernel, dim3(g.splits * pairs), dim3(256), 0, s, g);
+  hipLaunchKernelGGL(conv3x3_wgrad_h3_kernel, dim3(g.splits * pairs), dim3(256), 0, s, g);
   launch_hook("direct_wgrad_h3", 1, s, flop);
   int rc = launch_status("conv3x3_wgrad_h3");
   if (!rc) rc = reduce_slabs(g.part, g.splits, (int64_t)Cout * 9 * Cin, dw, acc, s);

@@ -57,11 +57,9 @@ float* wino_v_slot(void* ws, int C, int N);
 int launch_wino_dz2(const float* dz, int ldz, int B, int H, int W, int N, float* V, float* E, float* bpart,
                     hipStream_t s, float* tmax = nullptr);
 float* wino_tmax_slot(void* ws, int B, int H, int W, int C, int N);
-float* wino_umax_slot(void* ws, int B, int H, int W, int C, int N);
 bool wino_fused_h3_planned(int B, int H, int W, int C, int N);
 // pis_conv3x3_bwd_prep's record of the V it wrote into ws (checked by the prepared dgrad)
 void wino_prep_record(const void* ws, int B, int H, int W, int C, int N, bool tmax);
-bool wino_h3_prescaled(int C, int N);  // the batched fp16x3 GEMM reads producer-written row maxima
 // does pis_conv3x3_dgrad_ex take F(4x4,3x3) Winograd for this layer with this workspace?
 bool dgrad_wino4_planned(int B, int H, int W, int Cin, int Cout, int ldz, size_t ws_bytes);
 // Winograd weight-gradient pieces for tile edge m (2: F(3x3,2x2), 4: F(3x3,4x4)), nxi = (m+2)^2:

@@ -741,8 +741,6 @@ extern "C" size_t pis_conv3x3_filter_bytes(int B, int H, int W, int Cin, int Cou
   const int C = dgrad ? Cout : Cin, N = dgrad ? Cin : Cout;  // contraction, outputs
   if (f == 2 && tune_get(PIS_TUNE_WINO_GEMM_OUT_H3) != 0)  // fp16x3: hi / lo planes + one scale per output
     return 2 * nc * sizeof(_Float16) + (size_t)N * sizeof(float);
-  if (f == 1 && wino_h3_prescaled(C, N))  // U + its per-(output, 32-channel chunk) maxima
-    return nc * sizeof(float) + (size_t)N * (C / 32) * sizeof(float);
   return f == 2 ? 3 * nc * sizeof(__bf16) : nc * sizeof(float);
 }
 

@@ -307,9 +307,8 @@ __device__ __forceinline__ void tile_decode(int64_t e, int c4n, int tpi, int64_t
 // (the fused GEMM + output-transform kernel reads its B fragments straight from them).
 __device__ __forceinline__ void wino4_filter_item(const float (&g)[3][3], int64_t e, int n, int c, int N,
                                                   int64_t NC, float* __restrict__ U, int transposed,
-                                                  __bf16* __restrict__ Up, float* __restrict__ umax = nullptr) {
+                                                  __bf16* __restrict__ Up) {
   float gg[6][3];  // G g
-  float um = 0.f;
 #pragma unroll
   for (int i = 0; i < 6; ++i)
 #pragma unroll
@@ -337,37 +336,28 @@ __device__ __forceinline__ void wino4_filter_item(const float (&g)[3][3], int64_
       }
       // [xi][n][c] for the batched GEMMs; [xi][c][n] for the fused kernel's B operand
       U[(size_t)(i * 6 + j) * NC + (transposed ? (int64_t)c * N + n : e)] = u;
-      um = fmaxf(um, fabsf(u));
     }
-  // umax[n][c / 32] = max |U| over xi and the 32-channel chunk (the fp16x3 GEMM's per-row filter
-  // scales): the callers give a chunk's 32 (n, c) items to an aligned half-wave, all active
-  if (umax) {
-#pragma unroll
-    for (int off = 16; off > 0; off >>= 1) um = fmaxf(um, __shfl_xor(um, off, 32));
-    if ((c & 31) == 0) umax[e >> 5] = um;
-  }
 }
 
 // w: KRSC weights [N][9][C] (row pitch ldw), already in the operand's orientation (the forward's
 // own weights, or pis_conv3x3_flip's copy for an input gradient). Block `bid` of `nblk`.
 __device__ __forceinline__ void wino4_filter_range(const float* __restrict__ w, int ldw, int N, int C,
                                                    float* __restrict__ U, int transposed, __bf16* __restrict__ Up,
-                                                   int bid, int nblk, float* __restrict__ umax = nullptr) {
+                                                   int bid, int nblk) {
   const int64_t NC = (int64_t)N * C;
   for (int64_t e = (int64_t)bid * blockDim.x + threadIdx.x; e < NC; e += (int64_t)nblk * blockDim.x) {
     const int n = (int)(e / C), c = (int)(e - (int64_t)n * C);
     float g[3][3];
 #pragma unroll
     for (int t = 0; t < 9; ++t) g[t / 3][t % 3] = w[(size_t)n * ldw + t * C + c];
-    wino4_filter_item(g, e, n, c, N, NC, U, transposed, Up, umax);
+    wino4_filter_item(g, e, n, c, N, NC, U, transposed, Up);
   }
 }
 
 __global__ __launch_bounds__(256) void wino4_filter_kernel(const float* __restrict__ w, int ldw, int N, int C,
                                                            float* __restrict__ U, int transposed = 0,
-                                                           __bf16* __restrict__ Up = nullptr,
-                                                           float* __restrict__ umax = nullptr) {
-  wino4_filter_range(w, ldw, N, C, U, transposed, Up, blockIdx.x, gridDim.x, umax);
+                                                           __bf16* __restrict__ Up = nullptr) {
+  wino4_filter_range(w, ldw, N, C, U, transposed, Up, blockIdx.x, gridDim.x);
 }
 
 // The input-gradient filter transform straight from the layer's ORIGINAL KRSC weights [C][9][N]
@@ -378,8 +368,7 @@ __global__ __launch_bounds__(256) void wino4_filter_kernel(const float* __restri
 // output planes are written in runs along c as by wino4_filter_kernel.
 __device__ __forceinline__ void wino4_filter_rot_tile(const float* __restrict__ w, int N, int C,
                                                       float* __restrict__ U, int transposed,
-                                                      __bf16* __restrict__ Up, int tile,
-                                                      float* __restrict__ umax = nullptr) {
+                                                      __bf16* __restrict__ Up, int tile) {
   __shared__ float sg[9][32][33];  // [tap][c][n], padded: the transform reads along c conflict-free
   const int nb = N / 32, n0 = 32 * (tile % nb), c0 = 32 * (tile / nb);
   const int tid = threadIdx.x, lx = tid & 31, ly = tid >> 5;
@@ -398,15 +387,14 @@ __device__ __forceinline__ void wino4_filter_rot_tile(const float* __restrict__ 
     float g[3][3];
 #pragma unroll
     for (int t = 0; t < 9; ++t) g[t / 3][t % 3] = sg[8 - t][c][nl];
-    wino4_filter_item(g, (int64_t)n * C + c0 + c, n, c0 + c, N, NC, U, transposed, Up, umax);
+    wino4_filter_item(g, (int64_t)n * C + c0 + c, n, c0 + c, N, NC, U, transposed, Up);
   }
 }
 
 __global__ __launch_bounds__(256) void wino4_filter_rot_kernel(const float* __restrict__ w, int N, int C,
                                                                float* __restrict__ U, int transposed,
-                                                               __bf16* __restrict__ Up,
-                                                               float* __restrict__ umax = nullptr) {
-  wino4_filter_rot_tile(w, N, C, U, transposed, Up, blockIdx.x, umax);
+                                                               __bf16* __restrict__ Up) {
+  wino4_filter_rot_tile(w, N, C, U, transposed, Up, blockIdx.x);
 }
 
 // The fused kernel's fp16x3 filter planes (pis_tune key 22), C % 64 == 0: one wave per output
@@ -482,7 +470,6 @@ __global__ __launch_bounds__(256) void wino4_filter_h2_kernel(const float* __res
 struct FilterJobDev {
   const float* w;
   void* out;
-  float* umax;  // fp32 format: the per-(n, 32-channel chunk) maxima after U, or NULL
   int N, C, dgrad, planes, blocks;
 };
 constexpr int FILTER_MAX_JOBS = 40;
@@ -500,8 +487,8 @@ __global__ __launch_bounds__(256) void wino4_filter_batch_kernel(FilterBatch fb)
   float* U = jb.planes ? nullptr : reinterpret_cast<float*>(jb.out);
   __bf16* Up = jb.planes ? reinterpret_cast<__bf16*>(jb.out) : nullptr;
   if (jb.planes == 2) wino4_filter_h2_wave(jb.w, 9 * jb.C, jb.N, jb.C, jb.dgrad, Up, 4 * lb + (threadIdx.x >> 6));
-  else if (jb.dgrad) wino4_filter_rot_tile(jb.w, jb.N, jb.C, U, 0, Up, lb, jb.umax);
-  else wino4_filter_range(jb.w, 9 * jb.C, jb.N, jb.C, U, 0, Up, lb, jb.blocks, jb.umax);
+  else if (jb.dgrad) wino4_filter_rot_tile(jb.w, jb.N, jb.C, U, 0, Up, lb);
+  else wino4_filter_range(jb.w, 9 * jb.C, jb.N, jb.C, U, 0, Up, lb, jb.blocks);
 }
 
 // V[xi][t][c] = (BT d BT^T)[xi], d = the 6x6 input patch at rows 4ty-1.., cols 4tx-1.. (zero padded)
@@ -625,167 +612,6 @@ __global__ __launch_bounds__(256) void wino4_output_kernel(const float* __restri
               max4<VW>(o[2 * qi][2 * qj], o[2 * qi][2 * qj + 1], o[2 * qi + 1][2 * qj], o[2 * qi + 1][2 * qj + 1]);
         }
     }
-  }
-}
-
-// ---- fused F(4x4,3x3): transforms + the 36 contractions + output transform in one kernel ----
-// For channel counts where the non-fused pipeline is bound by the V / M round trips through
-// HBM. A block owns 4 x 16 output tiles (16 x 64 pixels) x 16 output channels; wave w owns
-// tile row w. Input channels are walked 4 at a time:
-//   * the 18 x 66 x 4 input patch and the 36 x 4 x 16 slice of Ut (= G g G^T, [xi][c][n]) are
-//     double-buffered in LDS (one barrier per step; the next step's global loads are in flight
-//     while the current one computes);
-//   * lane l transforms ITS OWN (tile l & 15, channel l >> 4) patch: V = BT d BT^T stays in
-//     registers and V[xi] is exactly lane l's A operand of v_mfma_f32_16x16x4_f32 (A[row l&15]
-//     [k l>>4]); each wave issues 36 MFMAs per step into 36 independent accumulators;
-//   * the C/D map (row 4 (l >> 4) + r, col l & 15) leaves all 36 xi of 4 (tile, channel) pairs
-//     in one lane: Y = AT M AT^T and the conv epilogue run in registers.
-// V and M never leave the CU. Needs H % 16 == 0, W % 64 == 0, N % 16 == 0, C % 4 == 0.
-constexpr int WF_TR = 4, WF_TC = 16, WF_NB = 16, WF_KC = 4;
-constexpr int WF_PR = 4 * WF_TR + 2, WF_PC = 4 * WF_TC + 2;  // 18 x 66 input patch
-constexpr int WF_PS = 5;                                      // LDS floats per patch pixel (4 + 1 pad)
-constexpr int WF_PBUF = WF_PR * WF_PC * WF_PS;                // 5940 floats
-constexpr int WF_UBUF = 36 * WF_KC * WF_NB;                   // 2304 floats
-
-__global__ __launch_bounds__(256, 2) void wino4_fused_kernel(const float* __restrict__ Ut, IGemmArgs g, int B) {
-  __shared__ __attribute__((aligned(16))) float sP[2][WF_PBUF];  // [row][col][k (+pad)]
-  __shared__ __attribute__((aligned(16))) float sU[2][WF_UBUF];  // [xi][k][n]
-  const int H = g.H, W = g.W, C = g.Csrc, N = g.N;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int nbn = N / WF_NB, bx = W / (4 * WF_TC), by = H / (4 * WF_TR);
-  const int bid = xcd_remap(blockIdx.x, gridDim.x);
-  const int nb = bid % nbn;
-  int rest = bid / nbn;
-  const int bxi = rest % bx;
-  rest /= bx;
-  const int byi = rest % by, b = rest / by;
-  const int y0 = byi * 4 * WF_TR - 1, x0 = bxi * 4 * WF_TC - 1, n0 = nb * WF_NB;
-  const float* src = g.src + (size_t)b * H * W * g.lds;
-
-  constexpr int PPIX = WF_PR * WF_PC;                  // 1188 pixels
-  constexpr int PL = (PPIX + 255) / 256;               // 5
-  constexpr int UQ = WF_UBUF / 4;                      // 576 float4
-  constexpr int UL = (UQ + 255) / 256;                 // 3
-  f32x4 rp[PL], ru[UL];
-  auto gload = [&](int c0) {
-#pragma unroll
-    for (int i = 0; i < PL; ++i) {
-      const int px = tid + 256 * i;
-      rp[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (px < PPIX) {
-        const int yy = y0 + px / WF_PC, xx = x0 + px % WF_PC;
-        if (yy >= 0 && yy < H && xx >= 0 && xx < W)
-          rp[i] = *reinterpret_cast<const f32x4*>(src + ((size_t)yy * W + xx) * g.lds + c0);
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < UL; ++i) {
-      const int q = tid + 256 * i;
-      if (q < UQ) {
-        const int xk = q / (WF_NB / 4), n4 = q % (WF_NB / 4);  // xk = xi * 4 + k
-        ru[i] = *reinterpret_cast<const f32x4*>(Ut + ((size_t)(xk >> 2) * C + c0 + (xk & 3)) * N + n0 + 4 * n4);
-      }
-    }
-  };
-  auto lstore = [&](int buf) {
-#pragma unroll
-    for (int i = 0; i < PL; ++i) {
-      const int px = tid + 256 * i;
-      if (px < PPIX) {
-        float* d = &sP[buf][px * WF_PS];
-        d[0] = rp[i][0];
-        d[1] = rp[i][1];
-        d[2] = rp[i][2];
-        d[3] = rp[i][3];
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < UL; ++i) {
-      const int q = tid + 256 * i;
-      if (q < UQ) *reinterpret_cast<f32x4*>(&sU[buf][q * 4]) = ru[i];
-    }
-  };
-
-  f32x4 acc[36];
-#pragma unroll
-  for (int xi = 0; xi < 36; ++xi) acc[xi] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int tc = lane & 15, tk = lane >> 4;
-
-  const int nks = C / WF_KC;
-  gload(0);
-  lstore(0);
-  for (int ks = 0; ks < nks; ++ks) {
-    const int buf = ks & 1;
-    __syncthreads();
-    if (ks + 1 < nks) gload((ks + 1) * WF_KC);
-    const float* P = &sP[buf][((4 * wave) * WF_PC + 4 * tc) * WF_PS + tk];
-    const float* Ub = &sU[buf][tk * WF_NB + tc];
-    float r[6][6];  // r[a][j] = (d BT^T)[a][j]
-#pragma unroll
-    for (int a = 0; a < 6; ++a) {
-      float d[6];
-#pragma unroll
-      for (int bb = 0; bb < 6; ++bb) d[bb] = P[(a * WF_PC + bb) * WF_PS];
-#pragma unroll
-      for (int j = 0; j < 6; ++j) {
-        r[a][j] = 0.f;
-#pragma unroll
-        for (int bb = 0; bb < 6; ++bb) axpy_c(r[a][j], w4_bt(j, bb), d[bb]);
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < 6; ++i) {
-      float ub[6];
-#pragma unroll
-      for (int j = 0; j < 6; ++j) ub[j] = Ub[(i * 6 + j) * WF_KC * WF_NB];
-#pragma unroll
-      for (int j = 0; j < 6; ++j) {
-        float v = 0.f;
-#pragma unroll
-        for (int a = 0; a < 6; ++a) axpy_c(v, w4_bt(i, a), r[a][j]);
-        acc[i * 6 + j] = __builtin_amdgcn_mfma_f32_16x16x4f32(v, ub[j], acc[i * 6 + j], 0, 0, 0);
-      }
-    }
-    if (ks + 1 < nks) lstore(buf ^ 1);
-  }
-
-  // output transform + epilogue: lane holds M[xi] of tiles (row wave, col 4 (lane >> 4) + r), channel n
-  const int n = n0 + (lane & 15);
-  const float bias = g.bias ? g.bias[n] : 0.f;
-  const float sc = (g.flags & PIS_SCALE) ? g.scale[(size_t)b * N + n] : 1.f;
-  const int oy = byi * 4 * WF_TR + 4 * wave;
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int ox = bxi * 4 * WF_TC + 4 * (4 * (lane >> 4) + r);
-    float y[4][4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) y[i][j] = 0.f;
-#pragma unroll
-    for (int k = 0; k < 6; ++k) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        float q = 0.f;
-#pragma unroll
-        for (int l = 0; l < 6; ++l) axpy_c(q, w4_at(j, l), acc[k * 6 + l][r]);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) axpy_c(y[i][j], w4_at(i, k), q);
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const size_t pix = ((size_t)b * H + oy + i) * W + ox + j;
-        float v = y[i][j] + bias;
-        if (g.flags & PIS_RELU) v = fmaxf(v, 0.f);
-        if (g.flags & PIS_MASK) v = g.mask[pix * g.ldm + n] > 0.f ? v : 0.f;
-        v *= sc;
-        float* dst = g.dst + pix * g.ldd + n;
-        if (g.flags & PIS_ACCUMULATE) v += *dst;
-        *dst = v;
-      }
   }
 }
 
@@ -1317,28 +1143,19 @@ __global__ __launch_bounds__(256, OCC) void gemm_nt_x6_bk32_kernel(const float* 
 // rows r -> (r & 3) + 8 (r >> 2) + 4 lh (A rows staged by wave r >> 2): accumulator register r
 // is in units sA[r >> 2] * sB[(li / 8) % 4], and is re-expressed when a K-step's scales differ.
 //
-// PRE (pis_tune key 23, opt-in: measured 10 % slower than the wave scales, its producers' maxima
-// another 11 % on the input transform; profiles/r2_q65_*): no in-loop scales at all. Every A row (a
-// tile) and every B row (an output channel) gets ONE power-of-two scale for the whole contraction
-// from maxima its producers wrote — amax[m][K / 64] by the input / dz transforms (over all 36 xi
-// of the tile and each 64-channel chunk), umax[n][K / 32] by the filter transform (over all xi
-// and each 32-channel chunk) — so the accumulators are in units s_m t_n throughout and the
-// epilogue divides once: no wave maxima, no scale exchange, no rescaling of partial sums.
-template <int BM, int BN, int OCC = 3, bool SC = true, bool PRE = false>
+template <int BM, int BN, int OCC = 3, bool SC = true>
 __global__ __launch_bounds__(256, OCC) void gemm_nt_h3_bk32_kernel(const float* __restrict__ A,
                                                                 const float* __restrict__ Bm, float* __restrict__ Cm,
                                                                 int M, int N, int K, int64_t bsA, int64_t bsB,
-                                                                int64_t bsC, const float* __restrict__ amax,
-                                                                const float* __restrict__ umax) {
+                                                                int64_t bsC) {
   constexpr int BK = 32, KP = 32;
-  constexpr bool WS = SC && !PRE;  // per-wave, per-K-step scales
+  constexpr bool WS = SC;  // per-wave, per-K-step scales
   constexpr int TM = BM / 64, TN = BN / 64;
   constexpr int AL = BM * 8 / 256, BL = BN * 8 / 256;
   static_assert(BM % 128 == 0 && BN % 64 == 0, "row r's staging wave must be r / 8 % 4");
   __shared__ __attribute__((aligned(16))) _Float16 sA[2][BM * KP];
   __shared__ __attribute__((aligned(16))) _Float16 sB[2][BN * KP];
   __shared__ __attribute__((aligned(16))) float sscale[2][4];  // [A|B][staging wave]
-  __shared__ float sinv[PRE ? BM + BN : 1];                    // PRE: 1 / scale of each A, B row
   const Remap2 rm = xcd_remap2();
   A += rm.batch * bsA;
   Bm += rm.batch * bsB;
@@ -1349,34 +1166,6 @@ __global__ __launch_bounds__(256, OCC) void gemm_nt_h3_bk32_kernel(const float* 
   const int bid = rm.bid;
   const int m0 = (bid / ntn) * BM, n0 = (bid % ntn) * BN;
   const int q8 = (tid & 7) * 4;
-  // PRE: the staged rows' scales as biased exponent bytes (AL, BL <= 4: one register each)
-  static_assert(!PRE || (AL <= 4 && BL <= 4), "one exponent byte per staged row");
-  unsigned pae = 0, pbe = 0;
-  if constexpr (PRE) {
-    // the 8 threads staging a row (an aligned group of 8 lanes) split its chunk maxima
-    const int j8 = tid & 7, ka = K >> 6, kb = K >> 5;
-#pragma unroll
-    for (int i = 0; i < AL; ++i) {
-      const int r = (tid + i * 256) / 8, m = m0 + r;
-      float mx = 0.f;
-      if (m < M)
-        for (int j = j8; j < ka; j += 8) mx = fmaxf(mx, amax[(size_t)m * ka + j]);
-      float sc, inv;
-      h2_scale_pair(group8_max_nonneg(mx), sc, inv);
-      pae |= (__float_as_uint(sc) >> 23) << (8 * i);
-      if (j8 == 0) sinv[r] = inv;
-    }
-#pragma unroll
-    for (int i = 0; i < BL; ++i) {
-      const int r = (tid + i * 256) / 8, n = n0 + r;
-      float mx = 0.f;
-      for (int j = j8; j < kb; j += 8) mx = fmaxf(mx, umax[(size_t)n * kb + j]);
-      float sc, inv;
-      h2_scale_pair(group8_max_nonneg(mx), sc, inv);
-      pbe |= (__float_as_uint(sc) >> 23) << (8 * i);
-      if (j8 == 0) sinv[BM + r] = inv;
-    }
-  }
   const bool full = m0 + BM <= M && K % BK == 0;
   f32x4 ra[AL], rb[BL];
   auto gload = [&](int k0) {
@@ -1397,9 +1186,6 @@ __global__ __launch_bounds__(256, OCC) void gemm_nt_h3_bk32_kernel(const float* 
   float sa = 0.f, sb = 0.f;  // the wave's current scales (h3_keep)
   float sa_min = __builtin_inff(), sb_min = __builtin_inff();  // ... and the smallest so far
   auto lstore = [&]() {
-    // PRE: re-read the packed exponents every K-step: hoisted out of the loop, the compiler keeps
-    // 8 broadcast scale pairs live (16 VGPRs) and spills them
-    if (PRE) asm volatile("" : "+v"(pae), "+v"(pbe));
     if (WS) {
       float ma = 0.f, mb = 0.f;
 #pragma unroll
@@ -1420,7 +1206,7 @@ __global__ __launch_bounds__(256, OCC) void gemm_nt_h3_bk32_kernel(const float* 
 #pragma unroll
     for (int i = 0; i < AL; ++i) {
       u32x2 h, l;
-      split2h_x4(PRE ? ra[i] * __uint_as_float(((pae >> (8 * i)) & 0xffu) << 23) : WS ? ra[i] * sa : ra[i], h, l);
+      split2h_x4(WS ? ra[i] * sa : ra[i], h, l);
       const int row = (tid + i * 256) / 8, o = x6w8_off(row, q8 >> 3) + (q8 & 7);
       *reinterpret_cast<u32x2*>(&sA[0][o]) = h;
       *reinterpret_cast<u32x2*>(&sA[1][o]) = l;
@@ -1428,7 +1214,7 @@ __global__ __launch_bounds__(256, OCC) void gemm_nt_h3_bk32_kernel(const float* 
 #pragma unroll
     for (int i = 0; i < BL; ++i) {
       u32x2 h, l;
-      split2h_x4(PRE ? rb[i] * __uint_as_float(((pbe >> (8 * i)) & 0xffu) << 23) : WS ? rb[i] * sb : rb[i], h, l);
+      split2h_x4(WS ? rb[i] * sb : rb[i], h, l);
       const int row = (tid + i * 256) / 8, o = x6w8_off(row, q8 >> 3) + (q8 & 7);
       *reinterpret_cast<u32x2*>(&sB[0][o]) = h;
       *reinterpret_cast<u32x2*>(&sB[1][o]) = l;
@@ -1506,327 +1292,13 @@ __global__ __launch_bounds__(256, OCC) void gemm_nt_h3_bk32_kernel(const float* 
 #pragma unroll
     for (int b = 0; b < TN; ++b) {
       const int nl = wn * (BN / 2) + b * 32 + li, n = n0 + nl;
-      const float ib = PRE ? sinv[BM + nl] : 1.f;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int ml = wm * (BM / 2) + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh, m = m0 + ml;
-        // PRE: exact powers of two, one at a time (no product of two inverses can underflow)
-        if (m < M) Cm[(size_t)m * N + n] = PRE ? (acc[a][b][r] * sinv[ml]) * ib : acc[a][b][r] * inv[r >> 2];
+        if (m < M) Cm[(size_t)m * N + n] = acc[a][b][r] * inv[r >> 2];
       }
     }
 }
-
-// ---- 8-wave, 256 x 128, two-stage pipelined bf16x6 NT GEMM --------------------------------
-// One block per CU (8 waves = 2 per SIMD, wave tile 64 x 64 = 2 x 2 v_mfma_f32_32x32x16_bf16).
-// Per K-step of 32: step k is computed from one of two LDS plane buffers, then step k+1's fp32
-// registers (loaded one K-step earlier) are split into hi/mid/lo planes in the other buffer and
-// the loads of step k+2 are issued into the same registers: ONE barrier per K-step, a global
-// load has a whole K-step of MFMAs (96 per SIMD) to land. LDS rows are 64 B (32 bf16) with the 16-B chunk XOR-swizzled by row bits
-// 2..3 (chunk ^= (row >> 2) & 3), so the 16 rows a ds_read_b128 lane group reads at one chunk
-// hit 16 distinct bank quads: 2 buffers x 3 planes x 384 rows x 64 B = 147 KB.
-
-// The same fp16x3 GEMM as a PERSISTENT kernel (pis_tune key 24): for the short-K, HBM-bound
-// Winograd launches (K = 64..256: 2-8 K-steps per 128 x 128 tile) a block's start-up — its first
-// two K-steps' loads — and its epilogue stores are exposed once per tile. Here each block walks
-// tiles u = block, block + grid, ... of the flattened (xi, m-tile, n-tile) space as ONE stream
-// of K-steps: the loads of step s + 2 (possibly the next tile's first) are in flight while step s
-// computes and while a finished tile's M is stored. Per-wave per-K-step scales as above; a tile's
-// first K-step re-bases the accumulator units.
-template <int BM, int BN, int OCC = 3>
-__global__ __launch_bounds__(256, OCC) void gemm_nt_h3_persist_kernel(const float* __restrict__ A,
-                                                                   const float* __restrict__ Bm,
-                                                                   float* __restrict__ Cm, int M, int N, int K,
-                                                                   int64_t bsA, int64_t bsB, int64_t bsC,
-                                                                   int batches) {
-  constexpr int BK = 32, KP = 32;
-  constexpr int TM = BM / 64, TN = BN / 64;
-  constexpr int AL = BM * 8 / 256, BL = BN * 8 / 256;
-  static_assert(BM % 128 == 0 && BN % 64 == 0, "row r's staging wave must be r / 8 % 4");
-  __shared__ __attribute__((aligned(16))) _Float16 sA[2][BM * KP];
-  __shared__ __attribute__((aligned(16))) _Float16 sB[2][BN * KP];
-  __shared__ __attribute__((aligned(16))) float sscale[2][4];  // [A|B][staging wave]
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave & 1, wn = wave >> 1, li = lane & 31, lh = lane >> 5;
-  const int ntn = N / BN, ntm = (M + BM - 1) / BM, per_b = ntm * ntn;
-  const int ntiles = per_b * batches;
-  const int bid = xcd_remap(blockIdx.x, gridDim.x), G = gridDim.x;
-  const int KT = K / BK;  // K % BK == 0 (launcher)
-  const int my_tiles = bid < ntiles ? (ntiles - bid + G - 1) / G : 0;
-  const int nsteps = my_tiles * KT;
-  const int q8 = (tid & 7) * 4;
-  // tile u -> batch, m0, n0 (block-uniform: scalar arithmetic)
-  auto tile_of = [&](int i, int& bt, int& m0, int& n0) {
-    const int u = bid + i * G;
-    bt = u / per_b;
-    const int rem = u - bt * per_b;
-    m0 = (rem / ntn) * BM;
-    n0 = (rem % ntn) * BN;
-  };
-  f32x4 ra[AL], rb[BL];
-  auto gload = [&](int st) {
-    int bt, m0, n0;
-    tile_of(st / KT, bt, m0, n0);
-    const int k = (st % KT) * BK + q8;
-    const float* Ab = A + bt * bsA;
-    const float* Bb = Bm + bt * bsB;
-#pragma unroll
-    for (int i = 0; i < AL; ++i) {
-      const int m = m0 + (tid + i * 256) / 8;
-      ra[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (m < M) ra[i] = *reinterpret_cast<const f32x4*>(Ab + (size_t)m * K + k);
-    }
-#pragma unroll
-    for (int i = 0; i < BL; ++i) {
-      const int n = n0 + (tid + i * 256) / 8;
-      rb[i] = *reinterpret_cast<const f32x4*>(Bb + (size_t)n * K + k);
-    }
-  };
-  float sa = 0.f, sb = 0.f, sa_min = 0.f, sb_min = 0.f;
-  auto lstore = [&](bool first) {  // first: the tile's first K-step (scales re-chosen)
-    float ma = 0.f, mb = 0.f;
-#pragma unroll
-    for (int i = 0; i < AL; ++i)
-#pragma unroll
-      for (int k = 0; k < 4; ++k) ma = fmaxf(ma, fabsf(ra[i][k]));
-#pragma unroll
-    for (int i = 0; i < BL; ++i)
-#pragma unroll
-      for (int k = 0; k < 4; ++k) mb = fmaxf(mb, fabsf(rb[i][k]));
-    if (first) sa_min = sb_min = __builtin_inff();
-    sa = h3_keep(first ? 0.f : sa, wave_max_nonneg(ma), sa_min);
-    sb = h3_keep(first ? 0.f : sb, wave_max_nonneg(mb), sb_min);
-    if (lane == 0) {
-      sscale[0][wave] = sa;
-      sscale[1][wave] = sb;
-    }
-#pragma unroll
-    for (int i = 0; i < AL; ++i) {
-      u32x2 h, l;
-      split2h_x4(ra[i] * sa, h, l);
-      const int row = (tid + i * 256) / 8, o = x6w8_off(row, q8 >> 3) + (q8 & 7);
-      *reinterpret_cast<u32x2*>(&sA[0][o]) = h;
-      *reinterpret_cast<u32x2*>(&sA[1][o]) = l;
-    }
-#pragma unroll
-    for (int i = 0; i < BL; ++i) {
-      u32x2 h, l;
-      split2h_x4(rb[i] * sb, h, l);
-      const int row = (tid + i * 256) / 8, o = x6w8_off(row, q8 >> 3) + (q8 & 7);
-      *reinterpret_cast<u32x2*>(&sB[0][o]) = h;
-      *reinterpret_cast<u32x2*>(&sB[1][o]) = l;
-    }
-  };
-  f32x16 acc[TM][TN];
-#pragma unroll
-  for (int a = 0; a < TM; ++a)
-#pragma unroll
-    for (int b = 0; b < TN; ++b)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
-  if (nsteps == 0) return;  // block-uniform: no barrier is skipped by part of a block
-  gload(0);
-  lstore(true);
-  if (nsteps > 1) gload(1);
-  __syncthreads();
-  f32x4 ua = {1.f, 1.f, 1.f, 1.f};
-  float ub = 1.f;
-  for (int st = 0; st < nsteps; ++st) {
-    const int kt = st % KT;
-    {
-      const f32x4 na = *reinterpret_cast<const f32x4*>(&sscale[0][0]);
-      const float nb = sscale[1][(li >> 3) & 3];
-      if (kt == 0) {
-        ua = na;
-        ub = nb;
-      } else if (na[0] != ua[0] || na[1] != ua[1] || na[2] != ua[2] || na[3] != ua[3] || nb != ub) {
-        const float rb_ = nb / ub;
-        float f[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) f[q] = na[q] / ua[q] * rb_;
-#pragma unroll
-        for (int a = 0; a < TM; ++a)
-#pragma unroll
-          for (int b = 0; b < TN; ++b)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc[a][b][r] *= f[r >> 2];
-        ua = na;
-        ub = nb;
-      }
-    }
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      f16x8 af[2][TM], bf[2][TN];
-#pragma unroll
-      for (int p = 0; p < 2; ++p) {
-#pragma unroll
-        for (int a = 0; a < TM; ++a)
-          af[p][a] = *reinterpret_cast<const f16x8*>(&sA[p][x6w8_off(wm * (BM / 2) + a * 32 + li, 2 * ks + lh)]);
-#pragma unroll
-        for (int b = 0; b < TN; ++b)
-          bf[p][b] = *reinterpret_cast<const f16x8*>(&sB[p][x6w8_off(wn * (BN / 2) + b * 32 + li, 2 * ks + lh)]);
-      }
-#pragma unroll
-      for (int a = 0; a < TM; ++a)
-#pragma unroll
-        for (int b = 0; b < TN; ++b) {
-          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[1][a], bf[0][b], acc[a][b], 0, 0, 0);
-          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[0][a], bf[1][b], acc[a][b], 0, 0, 0);
-          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[0][a], bf[0][b], acc[a][b], 0, 0, 0);
-        }
-    }
-    if (kt == KT - 1) {  // tile done: store it (the next steps' loads are already in flight)
-      int bt, m0, n0;
-      tile_of(st / KT, bt, m0, n0);
-      float* Cb = Cm + bt * bsC;
-      float inv[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) inv[q] = 1.f / (ua[q] * ub);
-#pragma unroll
-      for (int a = 0; a < TM; ++a)
-#pragma unroll
-        for (int b = 0; b < TN; ++b) {
-          const int n = n0 + wn * (BN / 2) + b * 32 + li;
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int m = m0 + wm * (BM / 2) + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-            if (m < M) Cb[(size_t)m * N + n] = acc[a][b][r] * inv[r >> 2];
-            acc[a][b][r] = 0.f;
-          }
-        }
-    }
-    if (st + 1 < nsteps) {
-      __syncthreads();
-      lstore((st + 1) % KT == 0);
-      __syncthreads();
-      if (st + 2 < nsteps) gload(st + 2);
-    }
-  }
-}
-
-template <int DBG = 0>
-__global__ __launch_bounds__(512, 1) void gemm_nt_x6_w8_kernel(const float* __restrict__ A,
-                                                               const float* __restrict__ Bm, float* __restrict__ Cm,
-                                                               int M, int N, int K, int64_t bsA, int64_t bsB,
-                                                               int64_t bsC) {
-  constexpr int BM = 256, BN = 128, BK = 32, ROWS = BM + BN;
-  constexpr int AL = BM * BK / 4 / 512, BL = BN * BK / 4 / 512;  // float4 loads per thread per stage: 4, 2
-  extern __shared__ __attribute__((aligned(16))) __bf16 smem_x6w8[];
-  __bf16* const buf0 = smem_x6w8;
-  __bf16* const buf1 = smem_x6w8 + 3 * ROWS * 32;
-  const Remap2 rm = xcd_remap2();
-  A += rm.batch * bsA;
-  Bm += rm.batch * bsB;
-  Cm += rm.batch * bsC;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave & 3, wn = wave >> 2, li = lane & 31, lh = lane >> 5;
-  const int ntn = N / BN;
-  const int bid = rm.bid;
-  const int m0 = (bid / ntn) * BM, n0 = (bid % ntn) * BN;
-  const int q8 = (tid & 7) * 4;  // k offset of this thread's float4 within the 32-wide step
-  const bool full = m0 + BM <= M;
-  struct Regs {
-    f32x4 a[AL], b[BL];
-  };
-  auto gload = [&](int k0, Regs& r) {
-    const int k = k0 + q8;
-#pragma unroll
-    for (int i = 0; i < AL; ++i) {
-      const int m = m0 + (tid + i * 512) / 8;
-      if (DBG == 1) {
-        r.a[i] = f32x4{(float)k0, 1.f, 2.f, 3.f};
-        continue;
-      }
-      r.a[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (full || m < M) r.a[i] = *reinterpret_cast<const f32x4*>(A + (size_t)m * K + k);
-    }
-#pragma unroll
-    for (int i = 0; i < BL; ++i) {
-      if (DBG == 1) {
-        r.b[i] = f32x4{(float)k0, 1.f, 2.f, 3.f};
-        continue;
-      }
-      r.b[i] = *reinterpret_cast<const f32x4*>(Bm + (size_t)(n0 + (tid + i * 512) / 8) * K + k);
-    }
-  };
-  auto lstore = [&](__bf16* buf, const Regs& r) {
-    const int chunk = q8 >> 3, half = (q8 >> 2) & 1;
-#pragma unroll
-    for (int i = 0; i < AL + BL; ++i) {
-      const int row = i < AL ? (tid + i * 512) / 8 : BM + (tid + (i - AL) * 512) / 8;
-      u32x2 h, m, l;
-      split3_x4(i < AL ? r.a[i] : r.b[i - AL], h, m, l);
-      const int o = x6w8_off(row, chunk) + 4 * half;
-      *reinterpret_cast<u32x2*>(buf + o) = h;
-      *reinterpret_cast<u32x2*>(buf + ROWS * 32 + o) = m;
-      *reinterpret_cast<u32x2*>(buf + 2 * ROWS * 32 + o) = l;
-    }
-  };
-  f32x16 acc[2][2];
-#pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int b = 0; b < 2; ++b)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
-  auto compute = [&](const __bf16* buf) {
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const int chunk = 2 * ks + lh;
-      bf16x8 af[3][2], bf[3][2];
-#pragma unroll
-      for (int p = 0; p < 3; ++p) {
-#pragma unroll
-        for (int a = 0; a < 2; ++a)
-          af[p][a] = *reinterpret_cast<const bf16x8*>(buf + p * ROWS * 32 + x6w8_off(wm * 64 + a * 32 + li, chunk));
-#pragma unroll
-        for (int b = 0; b < 2; ++b)
-          bf[p][b] = *reinterpret_cast<const bf16x8*>(buf + p * ROWS * 32 +
-                                                      x6w8_off(BM + wn * 64 + b * 32 + li, chunk));
-      }
-#pragma unroll
-      for (int a = 0; a < 2; ++a)
-#pragma unroll
-        for (int b = 0; b < 2; ++b) {  // smallest partial products first
-          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[2][a], bf[0][b], acc[a][b], 0, 0, 0);
-          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1][a], bf[1][b], acc[a][b], 0, 0, 0);
-          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0][a], bf[2][b], acc[a][b], 0, 0, 0);
-          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1][a], bf[0][b], acc[a][b], 0, 0, 0);
-          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0][a], bf[1][b], acc[a][b], 0, 0, 0);
-          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0][a], bf[0][b], acc[a][b], 0, 0, 0);
-        }
-    }
-  };
-  const int KT = K / BK;
-  Regs r;
-  gload(0, r);
-  lstore(buf0, r);
-  if (KT > 1) gload(BK, r);
-  __syncthreads();
-  // the loads of step k+2 are issued right after step k+1's registers are split into LDS, and land
-  // during step k+1's MFMAs (a runtime buffer select: the 2-step unrolled form spills at 256 VGPRs)
-  for (int kt = 0; kt < KT; ++kt) {
-    const __bf16* cur = (kt & 1) ? buf1 : buf0;
-    __bf16* nxt = (kt & 1) ? buf0 : buf1;
-    compute(cur);
-    if (kt + 1 < KT) {
-      lstore(nxt, r);
-      if (kt + 2 < KT) gload((kt + 2) * BK, r);
-    }
-    __syncthreads();
-  }
-#pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int b = 0; b < 2; ++b) {
-      const int n = n0 + wn * 64 + b * 32 + li;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = m0 + wm * 64 + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-        if (full || m < M) Cm[(size_t)m * N + n] = acc[a][b][r];
-      }
-    }
-}
-constexpr size_t X6W8_SMEM = 2 * 3 * 384 * 32 * sizeof(__bf16);  // 147,456 B
 
 // ---- F(4x4,3x3) contraction fused with the output transform (bf16x6) --------------------
 // For the shallow, HBM-bound layers: the 36 products M[xi] = V[xi] U[xi]^T never go to HBM.
@@ -1854,10 +1326,7 @@ typedef __bf16 bf16x8g __attribute__((ext_vector_type(8)));
 // fold each xi's product one xi late, keeping it in registers across the barrier (a stagger,
 // MI355X_MICROARCH.md 'Two waves that run the SAME program with one barrier per block'): the
 // partners' MFMA and fold phases no longer coincide. Bit-for-bit the same sums in the same order.
-// PR (pis_tune key 28; KC = 64, lockstep only): two xi per barrier. Four LDS operand buffers (xi & 3;
-// still inside the epilogue's 139 KB), xi + 2 and xi + 3 staged after xi + 1's fold, so the two
-// products' independent MFMA chains and folds can interleave and half the barriers go. Same sums.
-template <int NWN, int NWT, int KC, int G = 1, bool H3 = false, bool STG = false, bool PR = false>
+template <int NWN, int NWT, int KC, int G = 1, bool H3 = false, bool STG = false>
 __global__ __launch_bounds__(64 * NWN * NWT) void wino4_gemm_out_x6_kernel(const float* __restrict__ V,
                                                                           const __bf16* __restrict__ Up,
                                                                           IGemmArgs g, int B,
@@ -1884,8 +1353,7 @@ __global__ __launch_bounds__(64 * NWN * NWT) void wino4_gemm_out_x6_kernel(const
   // LDS: the double-buffered operand planes, and (aliased) the epilogue's staging of all four
   // tile quarters of Y (139 KB: one block per CU either way, its registers allow no second)
   constexpr int QT = 4 * NWT, EP = NN + 4, EQ = QT * 16 * EP;  // tiles per quarter; row pitch, floats
-  static_assert(!PR || (KC == 64 && !STG), "paired stages: the lockstep 64-channel form");
-  constexpr int NB = PR ? 4 : 2;  // LDS operand buffers
+  constexpr int NB = 2;  // LDS operand buffers
   constexpr int OPS_BYTES = NB * P * (TB + NN) * KP * 2, EPI_BYTES = 4 * EQ * 4;
   constexpr int LDS_BYTES = OPS_BYTES > EPI_BYTES ? OPS_BYTES : EPI_BYTES;
   static_assert(QT * 4 * (NN / 4) == NT, "one epilogue item per thread and quarter");
@@ -1981,12 +1449,6 @@ __global__ __launch_bounds__(64 * NWN * NWT) void wino4_gemm_out_x6_kernel(const
     lstore(0, vr[0], srow);
     ustore(0, 0);
     gload(vb, RING, vr[0]);
-    if constexpr (PR) {  // xi = 1 too; U[2], U[3] in flight
-      lstore(1, vr[1], srow);
-      ustore(1, 1);
-      gload(vb, RING + 1, vr[1]);
-      uload(3, 1);
-    }
     uload(2, 0);
     __syncthreads();
   };
@@ -2053,7 +1515,7 @@ __global__ __launch_bounds__(64 * NWN * NWT) void wino4_gemm_out_x6_kernel(const
     for (int a = 0; a < 6; ++a) {  // fully unrolled: the compiler keeps exact vmcnt counts across rows
 #pragma unroll
       for (int b = 0; b < 6; ++b) {
-        const int xi = 6 * a + b, cur = PR ? (xi & 3) : (b & 1);
+        const int xi = 6 * a + b, cur = b & 1;
         f32x4 acc = {0.f, 0.f, 0.f, 0.f};
         if constexpr (H3) {
 #pragma unroll
@@ -2097,23 +1559,6 @@ __global__ __launch_bounds__(64 * NWN * NWT) void wino4_gemm_out_x6_kernel(const
           }
           accp = acc;
         }
-        if constexpr (PR) {
-          // after the pair's second product: stage xi + 1, xi + 2 (U of xi in register slot xi & 1),
-          // refill their V ring slots and load U two xi ahead
-          if (xi & 1) {
-#pragma unroll
-            for (int d = 1; d <= 2; ++d) {
-              const int xs = xi + d, vslot = xs % RING;
-              if (xs < 36) {
-                lstore(xs & 3, vr[vslot], srow);
-                ustore(xs & 3, xs & 1);
-              }
-              if (xs + RING < 36) gload(vb, xs + RING, vr[vslot]);
-              if (xs + 2 < 36) uload(xs + 2, xs & 1);
-            }
-            __syncthreads();
-          }
-        } else {
         // stage xi + 1 (V from its ring slot, U from the register pair), then refill both
         const int vslot = (xi + 1) % RING;
         if (xi + 1 < 36) {
@@ -2123,7 +1568,6 @@ __global__ __launch_bounds__(64 * NWN * NWT) void wino4_gemm_out_x6_kernel(const
         if (xi + 1 + RING < 36) gload(vb, xi + 1 + RING, vr[vslot]);
         if (xi + 3 < 36) uload(xi + 3, cur ^ 1);
         __syncthreads();
-        }
       }
       // Y[i][j] += AT[i][a] R[j] (a is a runtime row index: coefficients selected from the table)
       if (!late) rowend(a);
@@ -2243,25 +1687,17 @@ static void launch_wino4_input(int64_t T, int C, hipStream_t s, const float* x, 
 // the F(4x4,3x3) filter transform of a's weights (the tiled kernel for unflipped 32-aligned shapes)
 // (Up: the fused kernel's planes, bf16x6 or, with h2, fp16x3 + scales — C % 32 == 0)
 static void launch_wino4_filter(const IGemmArgs& a, int N, int C, float* U, int transposed, __bf16* Up,
-                                hipStream_t s, bool h2 = false, float* umax = nullptr) {
+                                hipStream_t s, bool h2 = false) {
   if (h2)  // C % 64 == 0, N % 4 == 0 (the fused kernel's shapes)
     hipLaunchKernelGGL(wino4_filter_h2_kernel, dim3(N / 4), dim3(256), 0, s, a.wt, a.ldw, N, C, a.w_unflipped ? 1 : 0,
                        Up);
   else if (a.w_unflipped)  // N, C % 32 == 0 checked by launch_wino3x3
     hipLaunchKernelGGL(wino4_filter_rot_kernel, dim3((N / 32) * (C / 32)), dim3(256), 0, s, a.wt, N, C, U,
-                       transposed, Up, umax);
+                       transposed, Up);
   else
     hipLaunchKernelGGL(wino4_filter_kernel, dim3(grid_of((int64_t)N * C)), dim3(256), 0, s, a.wt, a.ldw, N, C, U,
-                       transposed, Up, umax);
+                       transposed, Up);
 }
-
-// the batched fp16x3 GEMM with producer-written row scales (pis_tune key 23; gemm_nt_h3_bk32_kernel
-// PRE): the input / dz transform leaves per-(tile, 64-channel) maxima, the filter transform
-// per-(channel, 32-channel) maxima, in the workspace after M (wino_tmax_slot / wino_umax_slot)
-static bool h3_prescaled(int C, int N) {
-  return tune_get(PIS_TUNE_WINO_TILE) == 4 && tune_get(PIS_TUNE_WINO_H3_PRE) != 0 && C % 64 == 0 && N % 64 == 0;
-}
-bool wino_h3_prescaled(int C, int N) { return h3_prescaled(C, N); }
 
 // the fused 64 -> 64 kernel's arithmetic (pis_tune key 22): fp16x3 planes instead of bf16x6
 static bool wino_gemm_out_h3() { return tune_get(PIS_TUNE_WINO_GEMM_OUT_H3) != 0; }
@@ -2317,9 +1753,6 @@ static int launch_wino_gemm_out(const float* V, const __bf16* Up, const IGemmArg
   if (wino_gemm_out_h3() && tune_get(PIS_TUNE_FUSED_STAGGER) != 0 && groups % 4 == 0) {
       hipLaunchKernelGGL((wino4_gemm_out_x6_kernel<4, 2, 64, 4, true, true>), dim3((int)(groups / 4) * nblk), blk, 0, s, V, Up,
                          a, B, tmax);
-    } else if (wino_gemm_out_h3() && tune_get(PIS_TUNE_FUSED_PAIR) != 0 && groups % 4 == 0) {
-      hipLaunchKernelGGL((wino4_gemm_out_x6_kernel<4, 2, 64, 4, true, false, true>), dim3((int)(groups / 4) * nblk), blk, 0, s,
-                         V, Up, a, B, tmax);
     } else if (wino_gemm_out_h3()) {
       if (G == 8 && groups % 8 == 0)
         hipLaunchKernelGGL((wino4_gemm_out_x6_kernel<4, 2, 64, 8, true>), dim3((int)(groups / 8) * nblk), blk, 0, s, V, Up, a,
@@ -2359,20 +1792,9 @@ float* wino_v_slot(void* ws, int C, int N) { return (float*)ws + (size_t)36 * N 
 size_t wino_ws_bytes(int B, int H, int W, int C, int N) {
   const int m = wino_tile(H, W), nxi = (m + 2) * (m + 2);
   const int64_t T = (int64_t)B * (H / m) * (W / m);
-  // + the fp16x3 row maxima after M: per (tile, 64-channel chunk) of V (wino_tmax_slot), per
-  // (channel, 32-channel chunk) of U (wino_umax_slot)
-  const int64_t extra = T * ((C + 63) / 64) + 8 + (int64_t)N * ((C + 31) / 32);
+  // + the fp16x3 tile maxima after M: per (tile, 64-channel chunk) of V (wino_tmax_slot)
+  const int64_t extra = T * ((C + 63) / 64) + 8;
   return (size_t)(nxi * ((int64_t)N * C + T * C + T * N) + extra) * sizeof(float) + 1024;
-}
-
-// fused F(4x4,3x3) (pis_tune key 12: 0 off, 1 auto, 2 whenever the shape allows)
-static bool wino_fused_wanted(int H, int W, int C, int N) {
-  const int mode = tune_get(PIS_TUNE_WINO_FUSED);
-  if (mode == 0 || H % (4 * WF_TR) || W % (4 * WF_TC) || N % WF_NB || C % WF_KC) return false;
-  // measured (tools/bench_kernels.py --key 12 --variants 0,2, B=8): faster only for dec1.conv0 fwd
-  // (-8 %) and enc2.conv0 fwd (-7 %) — the 4-channel steps re-fetch each input line 8x from
-  // L2/MALL — so auto uses it nowhere yet; 2 forces it (tests, experiments)
-  return mode == 2;
 }
 
 static int wino_prep_check(const void* ws, int B, int H, int W, int C, int N);
@@ -2391,18 +1813,8 @@ int launch_wino3x3(const IGemmArgs& a, int B, void* ws, hipStream_t s, float* ke
     if (rc) return rc;
   }
   const double flop = 2.0 * nxi * (double)T * N * C;
-  if (a.filter_ready && (m != 4 || (!keep_v && wino_fused_wanted(a.H, a.W, C, N))))
+  if (a.filter_ready && m != 4)
     return set_error("launch_wino3x3: PIS_FILTER_READY needs the F(4x4,3x3) GEMM path"), PIS_ERR_ARG;
-  if (m == 4 && !keep_v && wino_fused_wanted(a.H, a.W, C, N)) {
-    launch_wino4_filter(a, N, C, U, 1, nullptr, s);
-    int rc = launch_status("wino_filter");
-    if (rc) return rc;
-    const int blocks = B * (a.H / (4 * WF_TR)) * (a.W / (4 * WF_TC)) * (N / WF_NB);
-    launch_hook("wino_fused", 0, s, flop);
-    hipLaunchKernelGGL(wino4_fused_kernel, dim3(blocks), dim3(256), 0, s, U, a, B);
-    launch_hook("wino_fused", 1, s, flop);
-    return launch_status("wino_fused");
-  }
   if (wino_gemm_out_wanted(m, T, C, N)) {
     // the pre-split filter planes (1.5x U's bytes) go where M would have been
     __bf16* Up = reinterpret_cast<__bf16*>(Mt);
@@ -2423,19 +1835,10 @@ int launch_wino3x3(const IGemmArgs& a, int B, void* ws, hipStream_t s, float* ke
   if (v_ready && m != 4) return set_error("launch_wino3x3: prepared transforms need F(4x4,3x3)"), PIS_ERR_ARG;
   if (a.w_unflipped && (m != 4 || N % 32 || C % 32))
     return set_error("launch_wino3x3: unflipped weights need F(4x4,3x3) and 32-aligned channels"), PIS_ERR_ARG;
-  const bool pre = m == 4 && h3_prescaled(C, N);
-  float* tmax = pre ? wino_tmax_slot(ws, B, a.H, a.W, C, N) : nullptr;
-  float* umax = pre ? wino_umax_slot(ws, B, a.H, a.W, C, N) : nullptr;
   if (m == 4) {
-    if (a.filter_ready) {
-      U = const_cast<float*>(a.wt);
-      if (pre) umax = U + (size_t)36 * N * C;  // pis_conv3x3_filter writes them after U
-    } else {
-      launch_wino4_filter(a, N, C, U, 0, nullptr, s, false, umax);
-    }
-    if (!v_ready)
-      launch_wino4_input(T, C, s, a.src, a.lds, B, a.H, a.W,
-                         C, V, tmax);
+    if (a.filter_ready) U = const_cast<float*>(a.wt);
+    else launch_wino4_filter(a, N, C, U, 0, nullptr, s);
+    if (!v_ready) launch_wino4_input(T, C, s, a.src, a.lds, B, a.H, a.W, C, V, nullptr);
   } else {
     hipLaunchKernelGGL(wino_filter_kernel, dim3(grid_of((int64_t)N * C)), dim3(256), 0, s, a.wt, a.ldw, N, C, U);
     hipLaunchKernelGGL(wino_input_kernel, dim3(grid_of(T * (C / 4))), dim3(256), 0, s, a.src, a.lds, B, a.H, a.W,
@@ -2452,29 +1855,14 @@ int launch_wino3x3(const IGemmArgs& a, int B, void* ws, hipStream_t s, float* ke
     rc = launch_status("wino_gemm");
   } else if (v == 4 && N % 64 == 0 && C % 32 == 0) {
     // fp16x3 with per-K-step power-of-two tile scales (gemm_nt_h3_bk32_kernel)
-    const int pk = tune_get(PIS_TUNE_WINO_PERSIST);
-    if (!pre && pk > 0 && C <= 32 * pk && N % 128 == 0) {
-      // persistent: a few resident waves of blocks walk every tile (short-K launches)
-      const int64_t tiles = cdiv(T, 128) * (N / 128) * nxi;
-      const int grid = (int)std::min<int64_t>(tiles, 256 * 3 * 2);
-      hipLaunchKernelGGL((gemm_nt_h3_persist_kernel<128, 128, 3>), dim3(grid), dim3(256), 0, s, V, U, Mt, (int)T,
-                         N, C, T * C, (int64_t)N * C, T * N, nxi);
-    } else if (N % 128 == 0) {
+    if (N % 128 == 0) {
       const dim3 grid((int)cdiv(T, 128) * (N / 128), nxi);
-      if (pre)
-        hipLaunchKernelGGL((gemm_nt_h3_bk32_kernel<128, 128, 3, true, true>), grid, dim3(256), 0, s, V, U, Mt,
-                           (int)T, N, C, T * C, (int64_t)N * C, T * N, tmax, umax);
-      else
-        hipLaunchKernelGGL((gemm_nt_h3_bk32_kernel<128, 128, 3>), grid, dim3(256), 0, s, V, U, Mt, (int)T, N, C,
-                           T * C, (int64_t)N * C, T * N, nullptr, nullptr);
+      hipLaunchKernelGGL((gemm_nt_h3_bk32_kernel<128, 128, 3>), grid, dim3(256), 0, s, V, U, Mt, (int)T, N, C,
+                         T * C, (int64_t)N * C, T * N);
     } else {
       const dim3 grid((int)cdiv(T, 128) * (N / 64), nxi);
-      if (pre)
-        hipLaunchKernelGGL((gemm_nt_h3_bk32_kernel<128, 64, 4, true, true>), grid, dim3(256), 0, s, V, U, Mt,
-                           (int)T, N, C, T * C, (int64_t)N * C, T * N, tmax, umax);
-      else
-        hipLaunchKernelGGL((gemm_nt_h3_bk32_kernel<128, 64, 4>), grid, dim3(256), 0, s, V, U, Mt, (int)T, N, C,
-                           T * C, (int64_t)N * C, T * N, nullptr, nullptr);
+      hipLaunchKernelGGL((gemm_nt_h3_bk32_kernel<128, 64, 4>), grid, dim3(256), 0, s, V, U, Mt, (int)T, N, C,
+                         T * C, (int64_t)N * C, T * N);
     }
     rc = launch_status("wino_gemm");
   } else if (v >= 3 && N % 128 == 0) {
@@ -2530,7 +1918,6 @@ int launch_wino3x3(const IGemmArgs& a, int B, void* ws, hipStream_t s, float* ke
 int wino_filter_format(int B, int H, int W, int C, int N, bool kept) {
   if (wino_tile(H, W) != 4) return 0;
   const int64_t T = (int64_t)B * (H / 4) * (W / 4);
-  if (!kept && wino_fused_wanted(H, W, C, N)) return 0;
   if (wino_gemm_out_wanted(4, T, C, N)) return 2;
   return 1;
 }
@@ -2543,9 +1930,7 @@ int launch_wino4_filter_only(const float* w, int C, int N, int dgrad, int format
   if (format == 2 && wino_gemm_out_h3() && (C % 64 || N % 4))
     return set_error("pis_conv3x3_filter: fp16x3 planes need 64 x k contraction channels"), PIS_ERR_ARG;
   if (format == 2) launch_wino4_filter(a, N, C, nullptr, 0, reinterpret_cast<__bf16*>(out), s, wino_gemm_out_h3());
-  else  // + the row maxima after U when the consuming GEMM is the prescaled fp16x3 one
-    launch_wino4_filter(a, N, C, reinterpret_cast<float*>(out), 0, nullptr, s, false,
-                        h3_prescaled(C, N) ? reinterpret_cast<float*>(out) + (size_t)36 * N * C : nullptr);
+  else launch_wino4_filter(a, N, C, reinterpret_cast<float*>(out), 0, nullptr, s);
   return launch_status("wino_filter");
 }
 
@@ -2564,9 +1949,7 @@ int launch_wino4_filter_batch(int n, const float* const* w, void* const* out, co
     if (planes == 2 && (C[k] % 64 || N[k] % 4))
       return set_error("pis_conv3x3_filters: fp16x3 planes need 64 x k contraction channels"), PIS_ERR_ARG;
     const int blocks = planes == 2 ? N[k] / 4 : dgrad[k] ? (N[k] / 32) * (C[k] / 32) : grid_of((int64_t)N[k] * C[k]);
-    float* umax = planes == 0 && h3_prescaled(C[k], N[k]) ? reinterpret_cast<float*>(out[k]) + (size_t)36 * N[k] * C[k]
-                                                          : nullptr;
-    fb.j[k] = FilterJobDev{w[k], out[k], umax, N[k], C[k], dgrad[k], planes, blocks};
+    fb.j[k] = FilterJobDev{w[k], out[k], N[k], C[k], dgrad[k], planes, blocks};
     fb.start[k] = total;
     total += blocks;
   }
@@ -2650,19 +2033,12 @@ float* wino_tmax_slot(void* ws, int B, int H, int W, int C, int N) {
   return (float*)ws + (size_t)36 * ((int64_t)N * C + T * C + T * N);
 }
 
-// ... and the per-(channel, 32-channel chunk) max |U| of the batched GEMMs' filter
-float* wino_umax_slot(void* ws, int B, int H, int W, int C, int N) {
-  const int64_t T = (int64_t)B * (H / 4) * (W / 4);
-  return wino_tmax_slot(ws, B, H, W, C, N) + ((T * ((C + 63) / 64) + 7) & ~(int64_t)7);
-}
-
 // the dgrad of these shapes (C contraction = Cout, N = Cin) reads tile maxima (the fused fp16x3
-// kernel or the prescaled fp16x3 GEMM): its V producer (pis_conv3x3_bwd_prep) must write them
+// kernel): its V producer (pis_conv3x3_bwd_prep) must write them
 bool wino_fused_h3_planned(int B, int H, int W, int C, int N) {
   if (wino_tile(H, W) != 4) return false;
   const int64_t T = (int64_t)B * (H / 4) * (W / 4);
-  if (wino_gemm_out_wanted(4, T, C, N)) return wino_gemm_out_h3();
-  return h3_prescaled(C, N);
+  return wino_gemm_out_wanted(4, T, C, N) && wino_gemm_out_h3();
 }
 
 int launch_wino_wgrad_out(const float* M, int N, int C, float* dw, int accumulate, hipStream_t s, int m,
@@ -2682,7 +2058,8 @@ int launch_wino_wgrad_out(const float* M, int N, int C, float* dw, int accumulat
 // C[b] (M x N) = A[b] (M x K) . B[b]^T (N x K), batch b over gridDim.y, all row-major fp32.
 // variant: 0 bf16x6 128x128, 1 its no-global-load timing twin, 2 its no-split timing twin,
 // 3 fp32 MFMA 128x128, 4 bf16x6 128x64, 5/6 the K-step-32 single-buffer bf16x6 128x128 at 2 / 3
-// waves per SIMD, 7 its 128x64. Requires N % 128 == 0 (64 for 4), K % 16 == 0.
+// waves per SIMD, 7 its 128x64, 10/11 the fp16x3 128x128 unscaled / scaled, 12 its 128x64.
+// Requires N % 128 == 0 (64 for 4, 7, 12), K % 16 == 0 (32 from variant 5).
 extern "C" int pis_debug_gemm_nt(const float* A, const float* B, float* C, int M, int N, int K, int batch,
                                  int variant, pis_stream_t stream) {
   const int bn = variant == 4 || variant == 7 || variant == 12 ? 64 : 128;
@@ -2690,15 +2067,6 @@ extern "C" int pis_debug_gemm_nt(const float* A, const float* B, float* C, int M
                     N % bn == 0,
                 "pis_debug_gemm_nt: bad arguments");
   hipStream_t s = (hipStream_t)stream;
-  if (variant == 8 || variant == 9) {  // the 8-wave 256 x 128 pipelined bf16x6 kernel (9: no global loads)
-    const dim3 g8((int)cdiv(M, 256) * (N / 128), batch);
-    const int64_t sa = (int64_t)M * K, sb = (int64_t)N * K, sc = (int64_t)M * N;
-    if (variant == 8)
-      hipLaunchKernelGGL(gemm_nt_x6_w8_kernel<0>, g8, dim3(512), X6W8_SMEM, s, A, B, C, M, N, K, sa, sb, sc);
-    else
-      hipLaunchKernelGGL(gemm_nt_x6_w8_kernel<1>, g8, dim3(512), X6W8_SMEM, s, A, B, C, M, N, K, sa, sb, sc);
-    return launch_status("debug_gemm_nt");
-  }
   const dim3 grid((int)cdiv(M, 128) * (N / bn), batch);
   const int64_t sa = (int64_t)M * K, sb = (int64_t)N * K, sc = (int64_t)M * N;
   switch (variant) {
@@ -2710,9 +2078,9 @@ extern "C" int pis_debug_gemm_nt(const float* A, const float* B, float* C, int M
     case 5: hipLaunchKernelGGL((gemm_nt_x6_bk32_kernel<128, 128>), grid, dim3(256), 0, s, A, B, C, M, N, K, sa, sb, sc); break;
     case 6: hipLaunchKernelGGL((gemm_nt_x6_bk32_kernel<128, 128, 3>), grid, dim3(256), 0, s, A, B, C, M, N, K, sa, sb, sc); break;
     case 7: hipLaunchKernelGGL((gemm_nt_x6_bk32_kernel<128, 64, 3>), grid, dim3(256), 0, s, A, B, C, M, N, K, sa, sb, sc); break;
-    case 10: hipLaunchKernelGGL((gemm_nt_h3_bk32_kernel<128, 128, 3, false>), grid, dim3(256), 0, s, A, B, C, M, N, K, sa, sb, sc, nullptr, nullptr); break;
-    case 11: hipLaunchKernelGGL((gemm_nt_h3_bk32_kernel<128, 128, 3>), grid, dim3(256), 0, s, A, B, C, M, N, K, sa, sb, sc, nullptr, nullptr); break;
-    case 12: hipLaunchKernelGGL((gemm_nt_h3_bk32_kernel<128, 64, 4>), grid, dim3(256), 0, s, A, B, C, M, N, K, sa, sb, sc, nullptr, nullptr); break;
+    case 10: hipLaunchKernelGGL((gemm_nt_h3_bk32_kernel<128, 128, 3, false>), grid, dim3(256), 0, s, A, B, C, M, N, K, sa, sb, sc); break;
+    case 11: hipLaunchKernelGGL((gemm_nt_h3_bk32_kernel<128, 128, 3>), grid, dim3(256), 0, s, A, B, C, M, N, K, sa, sb, sc); break;
+    case 12: hipLaunchKernelGGL((gemm_nt_h3_bk32_kernel<128, 64, 4>), grid, dim3(256), 0, s, A, B, C, M, N, K, sa, sb, sc); break;
     default: set_error("pis_debug_gemm_nt: unknown variant %d", variant); return PIS_ERR_ARG;
   }
   return launch_status("debug_gemm_nt");

@@ -177,8 +177,7 @@ def test_direct_mixed_magnitude_chunks(hip):
 
 @pytest.mark.parametrize("B,H,W,Cin,Cout", [(2, 16, 64, 64, 64), (1, 8, 32, 128, 64), (2, 16, 32, 64, 128),
                                            (1, 16, 32, 128, 128)])
-@pytest.mark.parametrize("pipelined", [0, 1])
-def test_direct_wgrad_is_fp32_accurate(hip, B, H, W, Cin, Cout, pipelined):
+def test_direct_wgrad_is_fp32_accurate(hip, B, H, W, Cin, Cout):
     """dW = sum_p dz[p] x[p + tap] and db = sum_p dz[p] (direct fp16x3 weight gradient, split-K slabs
     reduced in fixed order) against float64: as accurate as the fp32 MFMA weight gradient
     (keys 29 = 0, 14 = 0), for unit and gradient-sized dz, a batch whose second sample's dz is
@@ -197,7 +196,7 @@ def test_direct_wgrad_is_fp32_accurate(hip, B, H, W, Cin, Cout, pipelined):
         dw_ref = torch.nn.grad.conv2d_weight(x, (Cout, Cin, 3, 3), dz, padding=1)
         db_ref = dz.sum(dim=(0, 2, 3))
         errs = {}
-        for name, knobs in (("direct", dict(DIRECT, k30=pipelined)), ("native", dict(k29=0, k14=0))):
+        for name, knobs in (("direct", DIRECT), ("native", dict(k29=0, k14=0))):
             with Knobs(hip, **knobs):
                 nws = hip.pis_conv3x3_wgrad_ws(B, H, W, Cin, Cout)
                 ws = torch.empty(nws // 4 + 1, device="cuda")
@@ -216,8 +215,7 @@ def test_direct_wgrad_is_fp32_accurate(hip, B, H, W, Cin, Cout, pipelined):
 
 
 @pytest.mark.parametrize("B,H,W,Cin,Cout", [(2, 16, 64, 64, 64), (2, 16, 32, 128, 128)])
-@pytest.mark.parametrize("pipelined", [0, 1])
-def test_direct_wgrad_scales_any_magnitude(hip, B, H, W, Cin, Cout, pipelined):
+def test_direct_wgrad_scales_any_magnitude(hip, B, H, W, Cin, Cout):
     """Without accumulation: gradient-sized (1e-9), tiny (1e-30) and large (1e6) dz and a batch
     mixing 1 and 1e-30 per sample — finite and within 1.25x of the fp32 MFMA path's error."""
     g = torch.Generator().manual_seed(66)
@@ -230,7 +228,7 @@ def test_direct_wgrad_scales_any_magnitude(hip, B, H, W, Cin, Cout, pipelined):
         dz = dz.float().double()
         dw_ref = torch.nn.grad.conv2d_weight(x, (Cout, Cin, 3, 3), dz, padding=1)
         errs = {}
-        for name, knobs in (("direct", dict(DIRECT, k30=pipelined)), ("native", dict(k29=0, k14=0))):
+        for name, knobs in (("direct", DIRECT), ("native", dict(k29=0, k14=0))):
             with Knobs(hip, **knobs):
                 nws = hip.pis_conv3x3_wgrad_ws(B, H, W, Cin, Cout)
                 ws = torch.empty(nws // 4 + 1, device="cuda")

@@ -105,7 +105,7 @@ def test_conv3x3_dgrad_wgrad(hip, B, H, W, Cin, Cout):
 
 # every non-default kernel variant behind pis_tune (include/pis_capi.h) stays exact too
 TUNE_VARIANTS = [(4, 1), (4, 2), (4, 3), (5, 0), (6, 2048), (3, 0), (7, 1), (8, 0), (8, 2), (10, 0), (10, 1),
-                 (11, 0), (12, 0), (12, 2), (13, 0), (13, 1), (13, 2), (10, 2), (10, 3), (14, 0), (14, 1), (14, 2), (15, 0), (16, 0), (17, 4), (22, 0), (23, 1), (24, 32), (25, 1), (26, 0), (26, 1), (27, 0)]
+                 (11, 0), (13, 0), (13, 1), (13, 2), (10, 2), (10, 3), (14, 0), (14, 1), (14, 2), (15, 0), (16, 0), (17, 4), (22, 0), (25, 1), (26, 0), (26, 1), (27, 0), (31, 0)]
 
 
 @pytest.mark.parametrize("key,value", TUNE_VARIANTS)
@@ -541,19 +541,6 @@ def test_conv3x3_kept_transform(hip, B, H, W, Cin, Cout, small_ws):
     assert rel_err(db.cpu(), dz.sum(dim=(0, 2, 3))) < 1e-5
 
 
-@pytest.mark.parametrize("B,H,W,Cin,Cout", [(2, 32, 64, 128, 64), (1, 16, 32, 256, 128), (1, 16, 128, 64, 64),
-                                           (2, 48, 64, 64, 128), (1, 32, 64, 512, 16)])
-def test_conv3x3_winograd_fused(hip, B, H, W, Cin, Cout):
-    """pis_tune(12, 2): Winograd F(4x4,3x3) fwd / dgrad as the one fused kernel (transforms in
-    LDS and registers) wherever H % 16 == W % 64 == 0 and the output channels are a multiple
-    of 16; every epilogue (bias, ReLU, mask, keep-scale, accumulate) through it."""
-    prev = hip.pis_tune(12, 2)
-    try:
-        test_conv3x3_ex_winograd(hip, B, H, W, Cin, Cout, 2)
-    finally:
-        hip.pis_tune(12, prev)
-
-
 @pytest.mark.parametrize("Cin,Cout", [(256, 256), (512, 128), (128, 64)])
 def test_winograd_gemm_bf16x6_is_fp32_accurate(hip, Cin, Cout):
     """The bf16x6 Winograd GEMM (pis_tune(10, 3): each fp32 operand split exactly into three
@@ -786,8 +773,9 @@ def test_convt_bf16x6_is_fp32_accurate(hip, Cin, Cout):
 def test_fused_64_groups_per_block_bitwise(hip, B, H, W):
     """The fused 64->64 contraction + output transform takes G groups of 32 tiles per block
     (pis_tune key 15: 1 -> G = 4 where the group count divides, 2 -> 1, 3 -> 2, 4 -> 8), with and
-    without the staggered fold (key 25), and with two xi per barrier (key 28): every variant gives bit-for-bit the same forward (ReLU, keep-scale, fused max pool) and input gradient
-    (ReLU mask, keep-scale, accumulate), and G = 1 matches the float64 reference."""
+    without the staggered fold (key 25): every variant gives bit-for-bit the same forward (ReLU,
+    keep-scale, fused max pool) and input gradient (ReLU mask, keep-scale, accumulate), and G = 1
+    matches the float64 reference."""
     Cin = Cout = 64
     g = torch.Generator().manual_seed(31)
     x = F.relu(torch.randn(B, Cin, H, W, generator=g))
@@ -800,13 +788,12 @@ def test_fused_64_groups_per_block_bitwise(hip, B, H, W):
     ws = torch.empty(nws // 4 + 1, device="cuda")
     wf = torch.empty(Cin * 9 * Cout, device="cuda")
     assert hip.pis_conv3x3_flip(wd.data_ptr(), wf.data_ptr(), Cin, Cout, s()) == 0
-    prev, prev25, prev28 = hip.pis_tune(15, -1), hip.pis_tune(25, -1), hip.pis_tune(28, -1)
+    prev, prev25 = hip.pis_tune(15, -1), hip.pis_tune(25, -1)
     out = {}
     try:
-        for v in (2, 1, 3, 4, "stagger", "pair"):
-            hip.pis_tune(15, 1 if v in ("stagger", "pair") else v)
+        for v in (2, 1, 3, 4, "stagger"):
+            hip.pis_tune(15, 1 if v == "stagger" else v)
             hip.pis_tune(25, 1 if v == "stagger" else 0)
-            hip.pis_tune(28, 1 if v == "pair" else 0)
             y = torch.empty(B, H, W, Cout, device="cuda")
             pool = torch.empty(B, H // 2, W // 2, Cout, device="cuda")
             rc = hip.pis_conv3x3_fwd_pool(xd.data_ptr(), Cin, wd.data_ptr(), bd.data_ptr(), sd.data_ptr(),
@@ -823,8 +810,7 @@ def test_fused_64_groups_per_block_bitwise(hip, B, H, W):
     finally:
         hip.pis_tune(15, prev)
         hip.pis_tune(25, prev25)
-        hip.pis_tune(28, prev28)
-    for v in (1, 3, 4, "stagger", "pair"):
+    for v in (1, 3, 4, "stagger"):
         for a, c in zip(out[2], out[v]):
             assert torch.equal(a, c), v
     y_ref = F.relu(F.conv2d(x.double(), w.double(), b.double(), padding=1)) * scale[:, :, None, None]

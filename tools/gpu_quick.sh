@@ -24,11 +24,7 @@ for x in "$@"; do
     bench29b) run bench_k29_1 300 python -u bench.py --no-cpu-baseline --steps 20 --tune 29=1 && run bench_k29_3 300 python -u bench.py --no-cpu-baseline --steps 20 --tune 29=3 && run bench_k29_1b 300 python -u bench.py --no-cpu-baseline --steps 20 --tune 29=1 ;;
     prof29) run prof29 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof29" -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --tune 29=1 ;;
     directw3) run direct_wgrad3 300 python -u tools/bench_kernels.py --key 29 --variants 0,2 --ops wgrad --rounds 3 --layers enc3.conv0,dec2.conv0,enc1.conv1 ;;
-    wg30) run wgrad_k30 300 python -u tools/bench_kernels.py --key 30 --variants 0,1 --ops wgrad --rounds 3 --tune 29=2 --layers enc1.conv1,dec1.conv0,enc2.conv1,enc2.conv0,dec2.conv0,enc3.conv0 ;;
-    bench30) run bench_a 300 python -u bench.py --no-cpu-baseline --steps 20 --tune 29=1 && run bench_b 300 python -u bench.py --no-cpu-baseline --steps 20 --tune 29=1 --tune 30=1 && run bench_c 300 python -u bench.py --no-cpu-baseline --steps 20 --tune 29=3 --tune 30=1 && run bench_d 300 python -u bench.py --no-cpu-baseline --steps 20 --tune 29=1 ;;
     dstall) run dstall 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_VALU_MFMA_BUSY_CYCLES -d "$OUT/dstall" -o run --output-format csv -- python3 tools/bench_kernels.py --key 29 --variants 2 --ops fwd,dgrad,wgrad --rounds 1 --layers enc1.conv1,enc2.conv1 && run dstall2 120 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_INSTS_VALU_MFMA_MOPS_F16 SQ_INSTS_SALU SQ_WAIT_INST_LDS -d "$OUT/dstall2" -o run --output-format csv -- python3 tools/bench_kernels.py --key 29 --variants 2 --ops fwd,dgrad,wgrad --rounds 1 --layers enc1.conv1,enc2.conv1 ;;
-    grid31) run grid31 300 python -u tools/bench_kernels.py --key 31 --variants 0,2,4 --ops fwd,dgrad --rounds 3 --layers enc1.conv1,dec1.conv0,enc2.conv1,enc2.conv0 ;;
-    bench31) run bench_g0 300 python -u bench.py --no-cpu-baseline --steps 20 --tune 31=0 && run bench_g2 300 python -u bench.py --no-cpu-baseline --steps 20 --tune 31=2 && run bench_g4 300 python -u bench.py --no-cpu-baseline --steps 20 --tune 31=4 && run bench_g0b 300 python -u bench.py --no-cpu-baseline --steps 20 --tune 31=0 ;;
     wgt) run wgrad_t 300 python -u tools/bench_kernels.py --key 31 --variants 0,1 --ops wgrad --rounds 3 --layers dec2.conv0,enc3.conv1,dec3.conv0,enc4.conv0,enc4.conv1,dec4.conv0,bottleneck ;;
     benchwt) for v in 0 1 0 1; do run bench_wt$v 300 python -u bench.py --no-cpu-baseline --steps 20 --tune 31=$v || exit 1; done ;;
     wgtpmc) run wgtpmc 120 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_INSTS_VALU SQ_LDS_BANK_CONFLICT SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY -d "$OUT/wgtpmc" -o run --output-format csv -- python3 tools/bench_kernels.py --key 31 --variants 0,1 --ops wgrad --rounds 1 --layers enc3.conv1,enc4.conv1,bottleneck ;;
@@ -38,7 +34,7 @@ for x in "$@"; do
     direct) run direct_kernels 300 python -u tools/bench_kernels.py --key 29 --variants 0,2 --ops fwd,dgrad --rounds 3 --layers enc1.conv1,dec1.conv0,enc2.conv0,enc2.conv1,dec2.conv0,enc3.conv0,enc3.conv1 ;;
     directw) run direct_wgrad 300 python -u tools/bench_kernels.py --key 29 --variants 0,2 --ops wgrad --rounds 3 --layers enc1.conv1,dec1.conv0,enc2.conv0,enc2.conv1,dec2.conv0 ;;
     directprof) run directprof 200 rocprofv3 --kernel-trace --stats -d "$OUT/directprof" -o run --output-format csv -- python3 tools/bench_kernels.py --key 29 --variants 0,2 --ops fwd,dgrad --rounds 1 --layers enc1.conv1,dec1.conv0,enc2.conv1 ;;
-    gemm) run bench_gemm 300 python -u tools/bench_gemm.py --variants 6,8,9 --rounds 3 --check ;;
+    gemm) run bench_gemm 300 python -u tools/bench_gemm.py --variants 6,11,12 --rounds 3 --check ;;
     lossprof) run lossprof 200 rocprofv3 --kernel-trace --stats -d "$OUT/lossprof" -o run --output-format csv -- python3 tools/bench_loss.py --B 64 --reps 20 ;;
     lossprof8) run lossprof8 200 rocprofv3 --kernel-trace --stats -d "$OUT/lossprof8" -o run --output-format csv -- python3 tools/bench_loss.py --B 8 --reps 20 ;;
   esac
