@@ -349,8 +349,7 @@ def loss_standalone(u: torch.Tensor, t: torch.Tensor, loss_kw: dict, reps: int =
         "bwd": (lambda: lib.pis_loss_bwd(u.data_ptr(), t.data_ptr(), Bn, Hn, Wn, ctypes.byref(prm), terms.data_ptr(),
                                          0, dz.data_ptr(), 2, st), 12.0),
     }
-    out = {}
-    for name, (fn, bpp) in calls.items():
+    def cold_ms(fn):
         ts = []
         for _ in range(reps):
             torch.sum(flush, dim=0, out=sink)  # a READ: evicts with clean lines (no write-back tail)
@@ -361,12 +360,31 @@ def loss_standalone(u: torch.Tensor, t: torch.Tensor, loss_kw: dict, reps: int =
             e1.record()
             ts.append((e0, e1))
         torch.cuda.synchronize()
-        ms = statistics.median(a.elapsed_time(b) for a, b in ts)
+        return statistics.median(a.elapsed_time(b) for a, b in ts)
+
+    # the floor at this size: ONE bandwidth-probe launch moving the same bytes (read p, t: forward;
+    # + write one float per pixel: backward) under the same protocol, best over its grid sizes
+    part = torch.empty(16384, device=u.device)
+    probe = {
+        "fwd": lambda grid: lib.pis_debug_stream_probe(u.data_ptr(), t.data_ptr(), 0, u.numel(), part.data_ptr(),
+                                                       grid, st),
+        "bwd": lambda grid: lib.pis_debug_stream_probe(u.data_ptr(), t.data_ptr(), dz.data_ptr(), u.numel(), 0,
+                                                       grid, st),
+    }
+    out = {}
+    for name, (fn, bpp) in calls.items():
+        ms = cold_ms(fn)
         nbytes = bpp * u.numel()
         gbs = nbytes / (ms * 1e-3) / 1e9
-        out[f"pis_loss_{name}_cold"] = {"bound": "hbm", "achieved": gbs, "peak": 8000.0, "unit": "GB/s",
-                                        "frac": gbs / 8000.0, "bytes_per_call": nbytes, "avg_call_ms": ms,
-                                        "measured": f"standalone, median of {reps}, 1 GiB read between calls"}
+        floor = min((cold_ms(lambda g=g: probe[name](g)), g) for g in (256, 512, 1024, 2048, 4096))
+        fgbs = nbytes / (floor[0] * 1e-3) / 1e9
+        out[f"pis_loss_{name}_cold"] = {
+            "bound": "hbm", "achieved": gbs, "peak": 8000.0, "unit": "GB/s", "frac": gbs / 8000.0,
+            "bytes_per_call": nbytes, "avg_call_ms": ms,
+            "measured": f"standalone, median of {reps}, 1 GiB read between calls",
+            "floor": {"kernel": "stream_probe_kernel (one float4 grid-stride launch, the same bytes)", "grid": floor[1],
+                      "avg_call_ms": floor[0], "achieved": fgbs, "frac": fgbs / 8000.0,
+                      "loss_over_floor": ms / floor[0]}}
     return out
 
 

@@ -78,9 +78,11 @@ int pis_version(void);
 #define PIS_TUNE_WINO_FUSED 12   /* retired (round 3): the one-kernel F(4x4,3x3) was slower than the 3-pass pipeline
                                     on every layer; the key is accepted and ignored */
 #define PIS_TUNE_CONVT_GEMM 13   /* transposed conv fwd/dgrad: lean NT GEMM with gather/scatter addressing when
-                                    Cin, Cout % 16 == 0 — 3 (default) fp32-class fp16x3 on fp16 MFMA (per-wave,
-                                    per-K-step power-of-two scales), 1 bf16x6 on bf16 MFMA, 2 on fp32 MFMA; 0 generic
-                                    implicit GEMM */
+                                    Cin, Cout % 16 == 0 — 4 (default) fp16x3, K-step 32 with the loads two K-steps
+                                    ahead, epilogue through LDS (16-B pixel stores), and the weight gradient on the
+                                    row-staged split-K kernel where Cin >= 256 (needs M, N % 128, w % 32; else 3);
+                                    3 fp32-class fp16x3 on fp16 MFMA, K-step 16 (per-wave, per-K-step power-of-two
+                                    scales), 1 bf16x6 on bf16 MFMA, 2 on fp32 MFMA; 0 generic implicit GEMM */
 #define PIS_TUNE_WGRAD_X6 14     /* Winograd and transposed-conv weight-gradient GEMMs: 3 (default) fp16x3 where the
                                     layer has >= 256 input channels, bf16x6 elsewhere; 1 fp32-accurate bf16x6 on
                                     bf16 MFMA everywhere, 2 fp16x3 (as key 10 = 4) everywhere (-1 % on the step: the
@@ -128,11 +130,14 @@ int pis_version(void);
                                    <= 256 channels, 5 H >= 128 (3/4/5 measured slower on the C2 step:
                                    profiles/r3_q8_direct_policy.txt) */
 #define PIS_TUNE_DIRECT_WG 30    /* retired (round 3): the double-buffered direct weight gradient (2-row tiles, 512
-                                    registers per lane) measured slower than the single-buffer kernel; ignored */
+                                    registers per lane) measured slower than the single-buffer kernel, an eight-wave
+                                    form neutral (profiles/r3_q19_wg8.txt); ignored */
 #define PIS_TUNE_WGRAD_T 31      /* fp16x3 weight-gradient GEMM (key 14) on plain 128 x 128 tiles (the Winograd weight
                                     gradient): 1 operands staged as stored (float4 rows, transposed LDS reads, 32-pixel
                                     K-steps, block-wide scales), 0 the column-staged wgrad_h3_kernel */
-#define PIS_TUNE_NKEYS 32
+#define PIS_TUNE_DIRECT_PIPE 32  /* direct fp16x3 input gradient (key 29): 1 (default) the epilogue's ReLU-mask rows
+                                    loaded during the last chunk's MFMAs (enc1.conv1 -12 %), 0 in the epilogue */
+#define PIS_TUNE_NKEYS 33
 #define PIS_DEBUG_NOLOAD (1 << 16)
 int pis_tune(int key, int value);
 /* Tooling (tools/bench_gemm.py): time one batched NT GEMM kernel variant in isolation,
@@ -143,6 +148,11 @@ int pis_tune(int key, int value);
  * 5-12 need K % 32 == 0. */
 int pis_debug_gemm_nt(const float* A, const float* B, float* C, int M, int N, int K, int batch, int variant,
                       pis_stream_t stream);
+/* Tooling (bench.py roofline_loss): one float4 grid-stride launch over n floats of a and b — dst = a + b
+ * when dst is given (12 B per element), else a read reduced to one partial per block (8 B per element):
+ * the floor any kernel moving the loss's bytes meets at the same size and cache state. */
+int pis_debug_stream_probe(const float* a, const float* b, float* dst, int64_t n, float* partial, int grid,
+                           pis_stream_t stream);
 
 /* Scheduling aid: arm an event (hipEvent_t) that the next F(4x4,3x3) convolution launched on this
  * thread (pis_conv3x3_fwd_ex / _dgrad_ex / _fwd_keep / _fwd_pool) records on its stream right after

@@ -57,6 +57,10 @@ __device__ __forceinline__ Remap2 xcd_remap2() {
   return Remap2{l / gx, l % gx};
 }
 
+// 16-bit element offset of 16-B chunk `chunk` (0..3) of row `row` in [row][32] LDS images, the
+// chunk XOR-swizzled by row bits 2..3: conflict-free ds_read_b128 fragments AND ds_write_b64 staging
+__device__ __forceinline__ int x6w8_off(int row, int chunk) { return row * 32 + 8 * (chunk ^ ((row >> 2) & 3)); }
+
 // ---- bf16x6: exact 3-way bf16 split of fp32 operands ------------------------
 // hi = bf16(x), mid = bf16(x - hi), lo = bf16(x - hi - mid); both subtractions are exact, and
 // hi + mid + lo == x (24 significant bits). Two values per step: one v_cvt_pk_bf16_f32 per level,

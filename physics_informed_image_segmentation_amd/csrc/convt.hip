@@ -323,6 +323,211 @@ __global__ __launch_bounds__(256, 2) void convt_gemm_kernel(ConvtGemmArgs g) {
   }
 }
 
+// K-step-32 fp16x3 form (pis_tune key 13 = 4, default): gemm_nt_h3_bk32_kernel's pipeline — ONE LDS
+// buffer of hi / lo planes ([row][32] fp16, x6w8_off swizzle), the loads of K-step kt + 2 issued
+// right after K-step kt + 1 is stored so they land during a whole 24-MFMA phase (the K-step-16
+// double buffer above keeps a quarter of the bytes in flight and waits on every K-step: the
+// shallow, HBM-bound transposed convs ran at 2.4-2.6 TB/s) — with the transposed conv's
+// addressing: the input gradient gathers a 32-wide K chunk of one tap (Cout % 32 == 0); the
+// epilogue goes through LDS per wave (32 rows x 64 columns at a time) so every lane finishes 4
+// consecutive channels of a pixel with 16-B accesses (forward: the 2 x 2 scatter, whole
+// 256-B pixel runs, + bias; input gradient: ReLU mask, accumulate). Needs M, N % 128, w % 32,
+// 16-B aligned operands and channel strides % 4 (launch_convt_gemm checks, else key 13 = 3).
+template <int MODE>
+__global__ __launch_bounds__(256, 3) void convt_h3_kernel(ConvtGemmArgs g) {
+  constexpr int BM = 128, BN = 128, BK = 32, KP = 32, AL = BM * 8 / 256, BL = BN * 8 / 256;
+  __shared__ __attribute__((aligned(16))) _Float16 smem[2 * (BM + BN) * KP];  // 32 KB: planes, then epilogue
+  __shared__ __attribute__((aligned(16))) float sscale[2][4];                // [A|B][staging wave]
+  _Float16(*sA)[BM * KP] = reinterpret_cast<_Float16(*)[BM * KP]>(smem);
+  _Float16(*sB)[BN * KP] = reinterpret_cast<_Float16(*)[BN * KP]>(smem + 2 * BM * KP);
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave & 1, wn = wave >> 1, li = lane & 31, lh = lane >> 5;
+  const int ntn = g.N / BN;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int m0 = (bid / ntn) * BM, n0 = (bid % ntn) * BN;
+  const int q8 = (tid & 7) * 4;
+  const int hw = g.h * g.w;
+  // element offset of each staged A row (dgrad: of its 2x2 block's top-left pixel); forward rows
+  // are 32 apart: one base
+  int64_t arow[MODE == 0 ? 1 : AL];
+  if (MODE == 0) {
+    arow[0] = (int64_t)(m0 + tid / 8) * g.lda;
+  } else {
+#pragma unroll
+    for (int i = 0; i < AL; ++i) {
+      const int m = m0 + tid / 8 + 32 * i;
+      const int b = m / hw, rem = m - b * hw, y = rem / g.w, x = rem - y * g.w;
+      arow[MODE == 0 ? 0 : i] = (((int64_t)b * 2 * g.h + 2 * y) * (2 * g.w) + 2 * x) * g.lda;
+    }
+  }
+  f32x4 ra[AL], rb[BL];
+  auto gload = [&](int k0) {
+    int64_t off = k0 + q8;
+    if (MODE == 1) {  // k = (2 di + dj) Cout + o
+      const int ij = k0 / g.cout;
+      off = ((int64_t)(ij >> 1) * (2 * g.w) + (ij & 1)) * g.lda + (k0 - ij * g.cout) + q8;
+    }
+#pragma unroll
+    for (int i = 0; i < AL; ++i)
+      ra[i] = *reinterpret_cast<const f32x4*>(g.a + (MODE == 0 ? arow[0] + (int64_t)(32 * i) * g.lda : arow[MODE == 0 ? 0 : i]) + off);
+#pragma unroll
+    for (int i = 0; i < BL; ++i)
+      rb[i] = *reinterpret_cast<const f32x4*>(g.bt + (size_t)(n0 + tid / 8 + 32 * i) * g.K + k0 + q8);
+  };
+  float sa = 0.f, sb = 0.f, sa_min = __builtin_inff(), sb_min = __builtin_inff();
+  auto lstore = [&]() {
+    float ma = 0.f, mb = 0.f;
+#pragma unroll
+    for (int i = 0; i < AL; ++i)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) ma = fmaxf(ma, fabsf(ra[i][k]));
+#pragma unroll
+    for (int i = 0; i < BL; ++i)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) mb = fmaxf(mb, fabsf(rb[i][k]));
+    sa = h3_keep(sa, wave_max_nonneg(ma), sa_min);
+    sb = h3_keep(sb, wave_max_nonneg(mb), sb_min);
+    if (lane == 0) {
+      sscale[0][wave] = sa;
+      sscale[1][wave] = sb;
+    }
+#pragma unroll
+    for (int i = 0; i < AL; ++i) {
+      u32x2 h, l;
+      split2h_x4(ra[i] * sa, h, l);
+      const int o = x6w8_off(tid / 8 + 32 * i, q8 >> 3) + (q8 & 7);
+      *reinterpret_cast<u32x2*>(&sA[0][o]) = h;
+      *reinterpret_cast<u32x2*>(&sA[1][o]) = l;
+    }
+#pragma unroll
+    for (int i = 0; i < BL; ++i) {
+      u32x2 h, l;
+      split2h_x4(rb[i] * sb, h, l);
+      const int o = x6w8_off(tid / 8 + 32 * i, q8 >> 3) + (q8 & 7);
+      *reinterpret_cast<u32x2*>(&sB[0][o]) = h;
+      *reinterpret_cast<u32x2*>(&sB[1][o]) = l;
+    }
+  };
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+  const int KT = g.K / BK;
+  gload(0);
+  lstore();
+  if (KT > 1) gload(BK);
+  __syncthreads();
+  f32x4 ua = {1.f, 1.f, 1.f, 1.f};  // accumulator units: A scale per row group r >> 2, B scale of the column
+  float ub = 1.f;
+  for (int kt = 0; kt < KT; ++kt) {
+    const f32x4 na = *reinterpret_cast<const f32x4*>(&sscale[0][0]);
+    const float nb = sscale[1][(li >> 3) & 3];
+    if (kt == 0) {
+      ua = na;
+      ub = nb;
+    } else if (na[0] != ua[0] || na[1] != ua[1] || na[2] != ua[2] || na[3] != ua[3] || nb != ub) {
+      const float rb_ = nb / ub;
+      float f[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) f[q] = na[q] / ua[q] * rb_;
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[a][b][r] *= f[r >> 2];
+      ua = na;
+      ub = nb;
+    }
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      f16x8 af[2][2], bf[2][2];
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+          af[p][a] = *reinterpret_cast<const f16x8*>(&sA[p][x6w8_off(wm * 64 + a * 32 + li, 2 * ks + lh)]);
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+          bf[p][b] = *reinterpret_cast<const f16x8*>(&sB[p][x6w8_off(wn * 64 + b * 32 + li, 2 * ks + lh)]);
+      }
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {  // smallest partial products first
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[1][a], bf[0][b], acc[a][b], 0, 0, 0);
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[0][a], bf[1][b], acc[a][b], 0, 0, 0);
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[0][a], bf[0][b], acc[a][b], 0, 0, 0);
+        }
+    }
+    if (kt + 1 < KT) {
+      __syncthreads();
+      lstore();
+      __syncthreads();
+      if (kt + 2 < KT) gload((kt + 2) * BK);
+    }
+  }
+  // epilogue through LDS: wave's [32 rows][64 columns] fp32 image (8 KB of the 32 KB planes), one
+  // 32-row half (a) at a time; a 32-row run of pixels lies in one image row (w % 32 == 0)
+  float inv[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) inv[q] = 1.f / (ua[q] * ub);  // exact powers of two
+  float* E = reinterpret_cast<float*>(smem) + wave * (32 * 64);
+  const int c4 = 4 * (lane & 15);
+  const int nb0 = n0 + wn * 64 + c4;  // this lane's 4 columns
+  int o = nb0, di = 0, dj = 0;
+  f32x4 bias4 = {0.f, 0.f, 0.f, 0.f};
+  if (MODE == 0) {
+    const int ij = nb0 / g.cout;
+    o = nb0 - ij * g.cout;
+    di = ij >> 1;
+    dj = ij & 1;
+    if (g.bias) bias4 = *reinterpret_cast<const f32x4*>(g.bias + o);
+  }
+#pragma unroll
+  for (int a = 0; a < 2; ++a) {
+    __syncthreads();  // the K loop's last fragment reads (a = 0) / the previous half's reads (a = 1)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        E[((r & 3) + 8 * (r >> 2) + 4 * lh) * 64 + b * 32 + li] = acc[a][b][r] * inv[r >> 2];
+    __syncthreads();
+    const int mb = m0 + wm * 64 + a * 32;  // first row of the half
+    size_t obase = 0;
+    if (MODE == 0) {
+      const int bb = mb / hw, rem = mb - bb * hw, y = rem / g.w, x = rem - y * g.w;
+      obase = ((size_t)bb * 2 * g.h + 2 * y + di) * (2 * g.w) + 2 * x + dj;
+    }
+    f32x4 mk[8], old[8];
+#pragma unroll
+    for (int p = 0; p < 8; ++p) {
+      const int rl = 4 * p + (lane >> 4);
+      mk[p] = f32x4{1.f, 1.f, 1.f, 1.f};
+      old[p] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (MODE == 1) {
+        if (g.flags & PIS_MASK) mk[p] = *reinterpret_cast<const f32x4*>(g.mask + (size_t)(mb + rl) * g.ldm + nb0);
+        if (g.flags & PIS_ACCUMULATE) old[p] = *reinterpret_cast<const f32x4*>(g.dst + (size_t)(mb + rl) * g.ldd + nb0);
+      }
+    }
+#pragma unroll
+    for (int p = 0; p < 8; ++p) {
+      const int rl = 4 * p + (lane >> 4);
+      f32x4 v = *reinterpret_cast<const f32x4*>(&E[rl * 64 + c4]);
+      if (MODE == 0) {
+        *reinterpret_cast<f32x4*>(g.dst + (obase + 2 * (size_t)rl) * g.ldd + o) = v + bias4;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = (mk[p][e] > 0.f ? v[e] : 0.f) + old[p][e];
+        *reinterpret_cast<f32x4*>(g.dst + (size_t)(mb + rl) * g.ldd + nb0) = v;
+      }
+    }
+  }
+}
+
 // 0 = handled, 1 = shape not covered (caller falls back to the implicit GEMM)
 int launch_convt_gemm(int mode, const float* a, int lda, const float* bt, int B, int h, int w, int cin, int cout,
                       const float* bias, const float* mask, int ldm, float* dst, int ldd, int flags,
@@ -335,7 +540,20 @@ int launch_convt_gemm(int mode, const float* a, int lda, const float* bt, int B,
   g.K = mode == 0 ? cin : 4 * cout;
   g.bias = bias; g.mask = mask; g.ldm = ldm; g.dst = dst; g.ldd = ldd; g.flags = flags;
   const int grid = (int)(cdiv(g.M, 128) * cdiv(g.N, 128));
-  const int v = tune_get(PIS_TUNE_CONVT_GEMM), ar = v == 1 ? 1 : v == 3 ? 2 : 0;  // 2 = fp32 MFMA
+  int v = tune_get(PIS_TUNE_CONVT_GEMM);
+  if (v == 4) {
+    auto a16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+    const bool ok = g.M % 128 == 0 && g.N % 128 == 0 && w % 32 == 0 && cout % 32 == 0 && cin % 32 == 0 &&
+                    lda % 4 == 0 && ldd % 4 == 0 && a16(a) && a16(bt) && a16(dst) &&
+                    (mode == 0 ? (!bias || a16(bias)) : (!(flags & PIS_MASK) || (a16(mask) && ldm % 4 == 0)));
+    if (ok) {
+      if (mode == 0) hipLaunchKernelGGL(convt_h3_kernel<0>, dim3(grid), dim3(256), 0, s, g);
+      else hipLaunchKernelGGL(convt_h3_kernel<1>, dim3(grid), dim3(256), 0, s, g);
+      return launch_status(mode == 0 ? "convt_h3_fwd" : "convt_h3_dgrad");
+    }
+    v = 3;
+  }
+  const int ar = v == 1 ? 1 : v == 3 ? 2 : 0;  // 2 = fp32 MFMA
   if (mode == 0 && ar == 2) hipLaunchKernelGGL((convt_gemm_kernel<0, 2>), dim3(grid), dim3(256), 0, s, g);
   else if (mode == 0 && ar == 1) hipLaunchKernelGGL((convt_gemm_kernel<0, 1>), dim3(grid), dim3(256), 0, s, g);
   else if (mode == 0) hipLaunchKernelGGL((convt_gemm_kernel<0, 0>), dim3(grid), dim3(256), 0, s, g);

@@ -40,6 +40,8 @@ struct DirectArgs {
   float* pool;         // [B][H/2][W/2][N] or NULL: also the 2x2 max pool of y
   int B, H, W, C, N;   // C contraction channels (% 16), N outputs (% 64)
   int flags;
+  int dbg;             // timing twins only (pis_tune key 2, wrong results): 1 no global loads after the first
+                       // chunk, 2 no LDS staging after the first chunk, 4 no epilogue
 };
 
 constexpr int DT_H = 8, DT_W = 32, DH_H = DT_H + 2, DH_W = DT_W + 2, DH_P = DH_H * DH_W, DKC = 16;
@@ -91,7 +93,12 @@ __global__ __launch_bounds__(256) void conv3x3_wsplit_kernel(const float* __rest
   }
 }
 
-template <bool POOL>
+// MPF (pis_tune key 32 = 1, default): an input gradient's epilogue ReLU-mask rows are loaded
+// during the last chunk's MFMAs (the last chunk is peeled), in the registers the absent next
+// chunk's loads would use: enc1.conv1 input gradient -12 %, enc2.conv1 -4 % (profiles/r3_q18_*).
+// (A tap loop walked column-shift-major, sharing halo rows between consecutive taps with the next
+// tap's fragments issued ahead, measured neutral: the loop runs at the clock-limited MFMA rate.)
+template <bool POOL, bool MPF = false>
 __global__ __launch_bounds__(256, 2) void conv3x3_h3_kernel(DirectArgs g) {
   __shared__ __attribute__((aligned(16))) char smem[DX_BYTES + DW_BYTES + 64];
   _Float16* sx = reinterpret_cast<_Float16*>(smem);             // [plane][DH_P][16]
@@ -120,6 +127,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_h3_kernel(DirectArgs g) {
   f32x4 xr[DX_PER_T][2];
   u32x4 wr[DW_PER_T];
   auto gload = [&](int k) {
+    if ((g.dbg & 1) && k > 0) return;
 #pragma unroll
     for (int j = 0; j < DX_PER_T; ++j) {
       const int i = tid + 256 * j;
@@ -139,6 +147,20 @@ __global__ __launch_bounds__(256, 2) void conv3x3_h3_kernel(DirectArgs g) {
     for (int j = 0; j < DW_PER_T; ++j) wr[j] = wsrc[tid + 256 * j];
   };
 
+  // epilogue lane map (below): channels n0 + ch4 .. + 3 of pixel pair (lane >> 4) + 4 (k >> 1), k & 1
+  const int ch4 = 4 * (lane & 15);
+  f32x4 mkp[2][8];  // MPF: the ReLU-mask rows of the epilogue, loaded during the last chunk
+  auto mask_prefetch = [&]() {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const size_t pix0 = ((size_t)b * g.H + r0 + 2 * wave + i) * g.W + c0;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const size_t pix = pix0 + 2 * ((lane >> 4) + 4 * (k >> 1)) + (k & 1);
+        mkp[i][k] = *reinterpret_cast<const f32x4*>(g.mask + pix * g.ldm + n0 + ch4);
+      }
+    }
+  };
   f32x16 acc[2][2];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -149,8 +171,10 @@ __global__ __launch_bounds__(256, 2) void conv3x3_h3_kernel(DirectArgs g) {
   float s_cur = 0.f, s_min = __builtin_inff();
 
   gload(0);
-#pragma unroll 1
-  for (int k = 0; k < nk; ++k) {
+  // one chunk; the last one (peeled, LAST) issues the epilogue's mask loads instead of a next chunk's
+  auto chunk = [&](int k, auto last_c) __attribute__((always_inline)) {
+    constexpr bool LAST = decltype(last_c)::value;
+    if (!((g.dbg & 2) && k > 0)) {
     // 1. this chunk's weights into LDS; the halo's block-wide max
     float m = 0.f;
 #pragma unroll
@@ -186,8 +210,10 @@ __global__ __launch_bounds__(256, 2) void conv3x3_h3_kernel(DirectArgs g) {
       }
     }
     __syncthreads();
+    }
     // 3. the next chunk's loads fly during this chunk's MFMAs
-    if (k + 1 < nk) gload(k + 1);
+    if constexpr (!LAST) gload(k + 1);
+    else if (MPF && (g.flags & PIS_MASK)) mask_prefetch();
 #pragma unroll
     for (int tap = 0; tap < 9; ++tap) {
       const int r = tap / 3, s = tap % 3;
@@ -213,7 +239,10 @@ __global__ __launch_bounds__(256, 2) void conv3x3_h3_kernel(DirectArgs g) {
         }
     }
     __syncthreads();
-  }
+  };
+#pragma unroll 1
+  for (int k = 0; k < nk - 1; ++k) chunk(k, std::false_type{});
+  chunk(nk - 1, std::true_type{});
 
   // epilogue: lane (li, lh) holds, for output channel n0 + 32 j + li, image row r0 + 2 wave + i and
   // column c0 + (reg & 3) + 8 (reg >> 2) + 4 lh (the 32x32x16 C/D map). Each image row goes through
@@ -222,10 +251,20 @@ __global__ __launch_bounds__(256, 2) void conv3x3_h3_kernel(DirectArgs g) {
   // are issued together (one memory round trip per row) and a pixel's 64 channels are one 256-B
   // store.
   const float inv_s = 1.f / s_cur;  // exact: a power of two
+  if (g.dbg & 4) {
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) t += acc[i][j][r];
+    if (t == 1.2345f) g.y[tid] = t;
+    return;
+  }
   float* E = reinterpret_cast<float*>(smem) + wave * (32 * 64);  // free since the loop's last barrier
   // float4 phase: lane (l & 15) owns channels n0 + ch4 .. + 3; pixel pair m = (l >> 4) + 4 k of the
   // row (columns 2m, 2m + 1: the 2x2 pool window's columns stay in one lane)
-  const int ch4 = 4 * (lane & 15);
   const f32x4 wi4 = *reinterpret_cast<const f32x4*>(g.winv + n0 + ch4);
   const f32x4 bias4 = g.bias ? *reinterpret_cast<const f32x4*>(g.bias + n0 + ch4) : f32x4{0.f, 0.f, 0.f, 0.f};
   const f32x4 sc4 = (g.flags & PIS_SCALE) ? *reinterpret_cast<const f32x4*>(g.scale + (size_t)b * g.N + n0 + ch4)
@@ -243,8 +282,11 @@ __global__ __launch_bounds__(256, 2) void conv3x3_h3_kernel(DirectArgs g) {
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       const size_t pix = pix0 + 2 * ((lane >> 4) + 4 * (k >> 1)) + (k & 1);
-      mk[k] = (g.flags & PIS_MASK) ? *reinterpret_cast<const f32x4*>(g.mask + pix * g.ldm + n0 + ch4)
-                                   : f32x4{1.f, 1.f, 1.f, 1.f};
+      if (MPF && (g.flags & PIS_MASK))
+        mk[k] = mkp[i][k];
+      else
+        mk[k] = (g.flags & PIS_MASK) ? *reinterpret_cast<const f32x4*>(g.mask + pix * g.ldm + n0 + ch4)
+                                     : f32x4{1.f, 1.f, 1.f, 1.f};
       old[k] = (g.flags & PIS_ACCUMULATE) ? *reinterpret_cast<const f32x4*>(g.y + pix * g.ldy + n0 + ch4)
                                           : f32x4{0.f, 0.f, 0.f, 0.f};
     }
@@ -324,13 +366,17 @@ int launch_direct_h3(const IGemmArgs& a, int B, void* ws, size_t ws_bytes, hipSt
   g.x = a.src; g.ldx = a.lds; g.wp = wp; g.winv = winv; g.bias = a.bias; g.scale = a.scale;
   g.mask = a.mask; g.ldm = a.ldm; g.y = a.dst; g.ldy = a.ldd; g.pool = a.pool;
   g.B = B; g.H = a.H; g.W = a.W; g.C = C; g.N = N; g.flags = a.flags;
+  g.dbg = tune_get(PIS_TUNE_DEBUG_NOLOAD);
   const int blocks = B * (a.H / DT_H) * (a.W / DT_W) * (N / 64);
   const double flop = 2.0 * 9 * (double)B * a.H * a.W * C * N;
   launch_hook("direct_h3", 0, s, flop);
-  if (a.pool)
-    hipLaunchKernelGGL(conv3x3_h3_kernel<true>, dim3(blocks), dim3(256), 0, s, g);
+  const bool mpf = tune_get(PIS_TUNE_DIRECT_PIPE) != 0 && (a.flags & PIS_MASK);
+  if (a.pool)  // a forward: no mask
+    hipLaunchKernelGGL((conv3x3_h3_kernel<true, false>), dim3(blocks), dim3(256), 0, s, g);
+  else if (mpf)
+    hipLaunchKernelGGL((conv3x3_h3_kernel<false, true>), dim3(blocks), dim3(256), 0, s, g);
   else
-    hipLaunchKernelGGL(conv3x3_h3_kernel<false>, dim3(blocks), dim3(256), 0, s, g);
+    hipLaunchKernelGGL((conv3x3_h3_kernel<false, false>), dim3(blocks), dim3(256), 0, s, g);
   launch_hook("direct_h3", 1, s, flop);
   return launch_status("conv3x3_h3");
 }
@@ -362,24 +408,29 @@ struct DirectWArgs {
   float* part;       // [splits][Cout][9][Cin]
   float* part_bias;  // [splits][Cout] or NULL
   int B, H, W, Cin, Cout, splits;
+  int dbg;           // timing twins, as DirectArgs::dbg
 };
 
 constexpr int WT_H = 4, WT_W = 32, WT_P = WT_H * WT_W, WH_H = WT_H + 2, WH_W = WT_W + 2, WH_P = WH_H * WH_W;
 constexpr int WZ_HALFS = WT_P * 64, WX_HALFS = WH_P * 64;                 // per plane
 constexpr int WZ_ITEMS = WT_P * 8, WX_ITEMS = WH_P * 8;                   // 8-channel groups
-constexpr int WZ_PER_T = WZ_ITEMS / 256, WX_PER_T = (WX_ITEMS + 255) / 256;  // 4, 7
 constexpr int WLDS_BYTES = 2 * (WZ_HALFS + WX_HALFS) * 2;
 
 // element offset of channel group (16-B chunk) ch of row `row` in a [row][64] fp16 image
 __device__ __forceinline__ int wsw64(int row, int ch) { return row * 64 + 8 * (ch ^ (((row >> 1) & 1) << 2)); }
 
+// (An eight-wave form — the taps split between the wave halves, 80 accumulator registers, two
+// waves per SIMD — measured within +-2 % per layer, profiles/r3_q19_wg8.txt: not kept.)
 __global__ __launch_bounds__(256, 1) void conv3x3_wgrad_h3_kernel(DirectWArgs g) {
+  constexpr int NW = 4, NT = 64 * NW, WZ_PER_T = WZ_ITEMS / NT, WX_PER_T = (WX_ITEMS + NT - 1) / NT;
+  constexpr int NTAP = 9;
   __shared__ __attribute__((aligned(16))) char smem[WLDS_BYTES + 64];
   _Float16* sz = reinterpret_cast<_Float16*>(smem);                        // [plane][128][64]
   _Float16* sx = reinterpret_cast<_Float16*>(smem + 2 * WZ_HALFS * 2);     // [plane][204][64]
-  float* red = reinterpret_cast<float*>(smem + WLDS_BYTES);                // [2][4] wave maxima
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wi = wave >> 1, wj = wave & 1;  // n-half, c-half
+  float* red = reinterpret_cast<float*>(smem + WLDS_BYTES);                // [2][NW] wave maxima
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wi = (wave >> 1) & 1, wj = wave & 1;  // n-half, c-half
+  constexpr int tap0 = 0, ntap = 9;
   const int ncb = g.Cin / 64, pairs = (g.Cout / 64) * ncb;
   const int pair = blockIdx.x % pairs, split = blockIdx.x / pairs;
   const int n0 = (pair / ncb) * 64, c0 = (pair % ncb) * 64;
@@ -388,18 +439,19 @@ __global__ __launch_bounds__(256, 1) void conv3x3_wgrad_h3_kernel(DirectWArgs g)
 
   f32x4 zr[WZ_PER_T][2], xr[WX_PER_T][2];
   auto gload = [&](int t) {
+    if ((g.dbg & 1) && t != split) return;
     const int b = t / per_img, rem = t - b * per_img, pr0 = (rem / tw_n) * WT_H, pc0 = (rem % tw_n) * WT_W;
     const size_t img = (size_t)b * g.H * g.W;
 #pragma unroll
     for (int j = 0; j < WZ_PER_T; ++j) {
-      const int i = tid + 256 * j, px = i >> 3, cg = i & 7;
+      const int i = tid + NT * j, px = i >> 3, cg = i & 7;
       const float* p = g.dz + (img + (size_t)(pr0 + (px >> 5)) * g.W + pc0 + (px & 31)) * g.ldz + n0 + 8 * cg;
       zr[j][0] = *reinterpret_cast<const f32x4*>(p);
       zr[j][1] = *reinterpret_cast<const f32x4*>(p + 4);
     }
 #pragma unroll
     for (int j = 0; j < WX_PER_T; ++j) {
-      const int i = tid + 256 * j, q = i >> 3, cg = i & 7;
+      const int i = tid + NT * j, q = i >> 3, cg = i & 7;
       xr[j][0] = xr[j][1] = f32x4{0.f, 0.f, 0.f, 0.f};
       if (i < WX_ITEMS) {
         const int qr = q / WH_W, qc = q - qr * WH_W, row = pr0 - 1 + qr, col = pc0 - 1 + qc;
@@ -412,9 +464,9 @@ __global__ __launch_bounds__(256, 1) void conv3x3_wgrad_h3_kernel(DirectWArgs g)
     }
   };
 
-  f32x16 acc[9];
+  f32x16 acc[NTAP];
 #pragma unroll
-  for (int t = 0; t < 9; ++t)
+  for (int t = 0; t < NTAP; ++t)
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
   float bs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // bias partials: channels n0 + 8 (tid & 7) + e
@@ -429,6 +481,7 @@ __global__ __launch_bounds__(256, 1) void conv3x3_wgrad_h3_kernel(DirectWArgs g)
   if (t < ntile) gload(t);
 #pragma unroll 1
   for (; t < ntile; t += g.splits) {
+    if (!((g.dbg & 2) && t != split)) {
     // 1. block maxima of the staged operands
     float mz = 0.f, mx = 0.f;
 #pragma unroll
@@ -443,7 +496,7 @@ __global__ __launch_bounds__(256, 1) void conv3x3_wgrad_h3_kernel(DirectWArgs g)
     mx = wave_max_nonneg(mx);
     if (lane == 0) {
       red[wave] = mz;
-      red[4 + wave] = mx;
+      red[NW + wave] = mx;
     }
     if (do_bias) {
 #pragma unroll
@@ -456,19 +509,24 @@ __global__ __launch_bounds__(256, 1) void conv3x3_wgrad_h3_kernel(DirectWArgs g)
     }
     __syncthreads();
     // 2. this tile's scales; the partial sums re-expressed in them; split into LDS
-    mz = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
-    mx = fmaxf(fmaxf(red[4], red[5]), fmaxf(red[6], red[7]));
+    mz = red[0];
+    mx = red[NW];
+#pragma unroll
+    for (int w = 1; w < NW; ++w) {
+      mz = fmaxf(mz, red[w]);
+      mx = fmaxf(mx, red[NW + w]);
+    }
     const float sz_new = h3_keep(sz_cur, mz, sz_min), sx_new = h3_keep(sx_cur, mx, sx_min);
     if (sz_cur > 0.f && (sz_new != sz_cur || sx_new != sx_cur)) {
       const float f = (sz_new / sz_cur) * (sx_new / sx_cur);
 #pragma unroll
-      for (int k = 0; k < 9; ++k) acc[k] *= f;
+      for (int k = 0; k < NTAP; ++k) acc[k] *= f;
     }
     sz_cur = sz_new;
     sx_cur = sx_new;
 #pragma unroll
     for (int j = 0; j < WZ_PER_T; ++j) {
-      const int i = tid + 256 * j, px = i >> 3, cg = i & 7;
+      const int i = tid + NT * j, px = i >> 3, cg = i & 7;
       u32x2 h0, l0, h1, l1;
       split2h_x4(zr[j][0] * sz_cur, h0, l0);
       split2h_x4(zr[j][1] * sz_cur, h1, l1);
@@ -477,7 +535,7 @@ __global__ __launch_bounds__(256, 1) void conv3x3_wgrad_h3_kernel(DirectWArgs g)
     }
 #pragma unroll
     for (int j = 0; j < WX_PER_T; ++j) {
-      const int i = tid + 256 * j, qq = i >> 3, cg = i & 7;
+      const int i = tid + NT * j, qq = i >> 3, cg = i & 7;
       if (i < WX_ITEMS) {
         u32x2 h0, l0, h1, l1;
         split2h_x4(xr[j][0] * sx_cur, h0, l0);
@@ -487,6 +545,7 @@ __global__ __launch_bounds__(256, 1) void conv3x3_wgrad_h3_kernel(DirectWArgs g)
       }
     }
     __syncthreads();
+    }
     // 3. the next tile's loads fly during this tile's MFMAs
     if (t + g.splits < ntile) gload(t + g.splits);
 #pragma unroll
@@ -503,8 +562,8 @@ __global__ __launch_bounds__(256, 1) void conv3x3_wgrad_h3_kernel(DirectWArgs g)
         a[pl] = __builtin_bit_cast(f16x8, __builtin_shufflevector(lo4, hi4, 0, 1, 2, 3, 4, 5, 6, 7));
       }
 #pragma unroll
-      for (int tap = 0; tap < 9; ++tap) {
-        const int r = tap / 3, s = tap % 3;
+      for (int tt = 0; tt < NTAP; ++tt) {
+        const int tap = tap0 + tt, r = tap / 3, s = tap % 3;
         // B = x (k pixels, columns c): halo pixel (rr + r, cc0 + 8 kh + q (+ 4) + s), channels of cgB
         f16x8 bb[2];
         const int hp = (rr + r) * WH_W + cc0 + 8 * kh + q + s;
@@ -515,9 +574,9 @@ __global__ __launch_bounds__(256, 1) void conv3x3_wgrad_h3_kernel(DirectWArgs g)
           const s16x4 hi4 = tr_read(base + wsw64(hp + 4, cgB) + 4 * (p & 1));
           bb[pl] = __builtin_bit_cast(f16x8, __builtin_shufflevector(lo4, hi4, 0, 1, 2, 3, 4, 5, 6, 7));
         }
-        acc[tap] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[1], bb[0], acc[tap], 0, 0, 0);
-        acc[tap] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[0], bb[1], acc[tap], 0, 0, 0);
-        acc[tap] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[0], bb[0], acc[tap], 0, 0, 0);
+        acc[tt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[1], bb[0], acc[tt], 0, 0, 0);
+        acc[tt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[0], bb[1], acc[tt], 0, 0, 0);
+        acc[tt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[0], bb[0], acc[tt], 0, 0, 0);
       }
     }
     __syncthreads();
@@ -529,12 +588,13 @@ __global__ __launch_bounds__(256, 1) void conv3x3_wgrad_h3_kernel(DirectWArgs g)
   float* slab = g.part + (size_t)split * g.Cout * 9 * g.Cin;
   const int c = c0 + 32 * wj + (lane & 31);
 #pragma unroll
-  for (int tap = 0; tap < 9; ++tap)
+  for (int tt = 0; tt < ntap; ++tt) {
 #pragma unroll
     for (int reg = 0; reg < 16; ++reg) {
       const int n = n0 + 32 * wi + (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5);
-      slab[((size_t)n * 9 + tap) * g.Cin + c] = acc[tap][reg] * inv;
+      slab[((size_t)n * 9 + tap0 + tt) * g.Cin + c] = acc[tt][reg] * inv;
     }
+  }
   if (do_bias) {  // fixed-order reduction over the 32 threads of each channel group
     float* rb = reinterpret_cast<float*>(smem);
 #pragma unroll
@@ -543,7 +603,7 @@ __global__ __launch_bounds__(256, 1) void conv3x3_wgrad_h3_kernel(DirectWArgs g)
     if (tid < 64) {
       const int cg = tid >> 3, e = tid & 7;
       float sum = 0.f;
-      for (int k = 0; k < 32; ++k) sum += rb[(8 * k + cg) * 8 + e];
+      for (int k = 0; k < NT / 8; ++k) sum += rb[(8 * k + cg) * 8 + e];
       g.part_bias[(size_t)split * g.Cout + n0 + tid] = sum;
     }
   }
@@ -573,7 +633,8 @@ int launch_direct_wgrad(const float* x, int ldx, const float* dz, int ldz, float
   DirectWArgs g{};
   g.x = x; g.ldx = ldx; g.dz = dz; g.ldz = ldz;
   g.B = B; g.H = H; g.W = W; g.Cin = Cin; g.Cout = Cout;
-  g.splits = direct_w_splits(B, H, W, Cin, Cout);
+ g.splits = direct_w_splits(B, H, W, Cin, Cout);
+  g.dbg = tune_get(PIS_TUNE_DEBUG_NOLOAD);
   g.part = reinterpret_cast<float*>(ws);
   g.part_bias = db ? g.part + (size_t)g.splits * Cout * 9 * Cin : nullptr;
   const int pairs = (Cout / 64) * (Cin / 64);

@@ -199,6 +199,27 @@ size_t colsum_ws(int64_t npix, int C);
 
 static int64_t head_pix_per_block(int64_t npix) { return std::max<int64_t>(256, cdiv(npix, 2048)); }
 
+// Bandwidth probes for the loss roofline (bench.py 'roofline_loss'): the least a kernel can take to
+// move the loss's algorithmic bytes at its size, under the same cold-cache protocol — one launch,
+// float4 grid-stride, a read of a and b reduced to one partial per block (the forward's 8 B/px) or
+// dst = a + b (the backward's 12 B/px).
+__global__ __launch_bounds__(256) void stream_probe_kernel(const f32x4* __restrict__ a, const f32x4* __restrict__ b,
+                                                           f32x4* __restrict__ dst, int64_t n4, float* partial) {
+  float acc = 0.f;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+    const f32x4 v = a[i] + b[i];
+    if (dst) dst[i] = v;
+    else acc += v[0] + v[1] + v[2] + v[3];
+  }
+  if (!dst) {
+    __shared__ float red[4];
+    acc = wave_sum(acc);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) partial[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+  }
+}
+
 }  // namespace pis
 
 using namespace pis;
@@ -284,4 +305,13 @@ extern "C" int pis_adamw_step(float* p, const float* g, float* m, float* v, int6
                      g, m, v, n, decay, omb1, (float)beta2, omb2, (float)eps, (float)step_size,
                      (float)bc2_sqrt, (float)grad_scale);
   return launch_status("adamw");
+}
+
+extern "C" int pis_debug_stream_probe(const float* a, const float* b, float* dst, int64_t n, float* partial,
+                                      int grid, pis_stream_t stream) {
+  PIS_CHECK_ARG(a && b && n > 0 && n % 4 == 0 && grid > 0 && (dst || partial), "pis_debug_stream_probe: bad arguments");
+  hipLaunchKernelGGL(stream_probe_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream,
+                     reinterpret_cast<const f32x4*>(a), reinterpret_cast<const f32x4*>(b),
+                     reinterpret_cast<f32x4*>(dst), n / 4, partial);
+  return launch_status("stream_probe");
 }

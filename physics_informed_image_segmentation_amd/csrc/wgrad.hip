@@ -919,6 +919,12 @@ constexpr int WT_BUF = 4 * WT_PLANE;             // A hi, A lo, B hi, B lo
 
 __device__ __forceinline__ int wtsw(int row, int chunk) { return row * 128 + 8 * (chunk ^ ((row & 3) << 2)); }
 
+// UP2 (the transposed-conv weight gradient, pis_tune key 13 = 4): A(p, (i, j, o)) = dy at the
+// up-sampled pixel (2y + i, 2x + j) of low-resolution pixel p = (b, y, x); with W % 32 == 0 and
+// 32-aligned split starts a K-step's 32 pixels lie in one image row, so its rows are one base +
+// 2 r pixels apart; the bias partials (column sums of A, blocks of the first column tile) are
+// summed from the raw loads and reduced over the 8 threads of a column group in LDS (fixed order).
+template <bool UP2 = false>
 __global__ __launch_bounds__(256, 2) void wgrad_h3t_kernel(WgradArgs g) {
   const Remap2 rm = xcd_remap2();
   if (rm.batch) {
@@ -943,23 +949,42 @@ __global__ __launch_bounds__(256, 2) void wgrad_h3t_kernel(WgradArgs g) {
   const int srow = tid >> 5, sc4 = tid & 31;
   const float* ga = g.a + m0 + 4 * sc4;
   const float* gb = g.b + n0 + 4 * sc4;
+  int up_ij = 0;
+  if (UP2) {  // this thread's A column group: tap (i, j) = up_ij, channel o
+    const int col = m0 + 4 * sc4;
+    up_ij = col / g.Ca;
+    ga = g.a + (col - up_ij * g.Ca);
+  }
+  const bool do_bias = UP2 && g.part_bias != nullptr && n0 == 0;
+  f32x4 bsum = {0.f, 0.f, 0.f, 0.f};
 
   f32x4 ra[2][4], rb[2][4];
   auto gload = [&](f32x4 (&xa)[4], f32x4 (&xb)[4], int st) __attribute__((always_inline)) {
     const int p0 = p_begin + st * WT_BK;
+    size_t abase = 0;
+    if (UP2) {  // the K-step's 32 pixels: one image row (b, y), columns x0 ..
+      const int hw = g.H * g.W, pb = min(p0, p_end - 1);
+      const int b = pb / hw, rem = pb - b * hw, y = rem / g.W, x0 = (rem - y * g.W) & ~31;
+      abase = (((size_t)b * 2 * g.H + 2 * y + (up_ij >> 1)) * (2 * g.W) + 2 * x0 + (up_ij & 1)) * g.lda;
+    }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       // rows past the split's end: a valid row loaded, zeros kept (no divergent branch)
       const int p = p0 + srow + 8 * j;
       const bool ok = p < p_end;
       const size_t pc = ok ? p : p_begin;
-      const f32x4 va = *reinterpret_cast<const f32x4*>(ga + pc * g.lda);
+      const f32x4 va = UP2 ? *reinterpret_cast<const f32x4*>(ga + abase + (size_t)(ok ? 2 * (srow + 8 * j) : 0) * g.lda)
+                           : *reinterpret_cast<const f32x4*>(ga + pc * g.lda);
       const f32x4 vb = *reinterpret_cast<const f32x4*>(gb + pc * g.ldb);
       xa[j] = ok ? va : f32x4{0.f, 0.f, 0.f, 0.f};
       xb[j] = ok ? vb : f32x4{0.f, 0.f, 0.f, 0.f};
     }
   };
   auto publish = [&](const f32x4 (&xa)[4], const f32x4 (&xb)[4], int par) __attribute__((always_inline)) {
+    if (do_bias) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bsum += xa[j];
+    }
     float ma = 0.f, mb = 0.f;
 #pragma unroll
     for (int j = 0; j < 4; ++j)
@@ -1092,6 +1117,18 @@ __global__ __launch_bounds__(256, 2) void wgrad_h3t_kernel(WgradArgs g) {
         out[(size_t)m * g.Np + n] = acc[a][b][r] * inv;
       }
     }
+  if (do_bias) {  // column sums over the block's pixels: the 8 threads of each column group
+    __syncthreads();
+    f32x4* rb4 = reinterpret_cast<f32x4*>(smem);
+    rb4[tid] = bsum;
+    __syncthreads();
+    if (tid < 32) {
+      f32x4 t = rb4[tid];
+#pragma unroll
+      for (int r = 1; r < 8; ++r) t += rb4[32 * r + tid];
+      *reinterpret_cast<f32x4*>(g.part_bias + (size_t)split * g.Mp + m0 + 4 * tid) = t;
+    }
+  }
 }
 
 static int run_wgrad(const WgradArgs& base, const WgradPlan& pl, hipStream_t s, int batches = 1) {
@@ -1114,7 +1151,7 @@ static int run_wgrad(const WgradArgs& base, const WgradPlan& pl, hipStream_t s, 
     if (tune_get(PIS_TUNE_WGRAD_T) != 0 && pl.bm == 128 && pl.bn == 128 && !a.a_up2 && !a.part_bias &&
         pl.pps % WT_BK == 0 && a.lda % 4 == 0 && a.ldb % 4 == 0 && a.bs_a % 4 == 0 && a.bs_b % 4 == 0 &&
         ((uintptr_t)a.a & 15) == 0 && ((uintptr_t)a.b & 15) == 0) {
-      hipLaunchKernelGGL(wgrad_h3t_kernel, grid, dim3(256), 0, s, a);
+      hipLaunchKernelGGL(wgrad_h3t_kernel<false>, grid, dim3(256), 0, s, a);
       return launch_status("wgrad_h3t");
     }
     if (pl.bm == 128 && pl.bn == 128) hipLaunchKernelGGL((wgrad_h3_kernel<128, 128>), grid, dim3(256), 0, s, a);
@@ -1519,8 +1556,20 @@ extern "C" int pis_conv3x3_wgrad(const float* x, int ldx, const float* dz, int l
   return reduce_slabs(a.part_bias, pl.splits, Cout, db, acc, s);
 }
 
+// key 13 = 4: the transposed-conv weight gradient on the row-staged fp16x3 kernel (wgrad_h3t<UP2>)
+// where it has >= 256 input channels (up2 -11 %, up3 -12 %, up4 -25 %; up1, 128 -> 64 at 256^2,
+// +17 %: it keeps the bf16x6 column-staged kernel; profiles/r3_q17_convt.txt)
+static bool convt_wgrad_t_ok(int B, int H, int W, int Cin, int Cout, int ldx, int lddy, const void* x,
+                             const void* dy) {
+  return tune_get(PIS_TUNE_CONVT_GEMM) == 4 && W % 32 == 0 && (4 * Cout) % 128 == 0 && Cin >= 256 && Cin % 128 == 0 &&
+         ldx % 4 == 0 && lddy % 4 == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)dy & 15) == 0 &&
+         plan_wgrad(4 * Cout, Cin, B * H * W, 4 * Cout, Cin).pps % WT_BK == 0;
+}
+
 extern "C" size_t pis_convt2x2_wgrad_ws(int B, int H, int W, int Cin, int Cout) {
-  return wgrad_ws_bytes(plan_wgrad(4 * Cout, Cin, B * H * W, Cout, Cin));
+  // either plan (key 13 may change after the workspace is sized)
+  return std::max(wgrad_ws_bytes(plan_wgrad(4 * Cout, Cin, B * H * W, Cout, Cin)),
+                  wgrad_ws_bytes(plan_wgrad(4 * Cout, Cin, B * H * W, 4 * Cout, Cin)));
 }
 
 extern "C" int pis_convt2x2_wgrad(const float* x, int ldx, const float* dy, int lddy, float* dw_ijoc,
@@ -1535,6 +1584,21 @@ extern "C" int pis_convt2x2_wgrad(const float* x, int ldx, const float* dy, int 
   hipStream_t s = (hipStream_t)stream;
   const int acc = flags & PIS_ACCUMULATE;
   const int P = B * H * W;
+  if (convt_wgrad_t_ok(B, H, W, Cin, Cout, ldx, lddy, x, dy)) {
+    const WgradPlan pl = plan_wgrad(4 * Cout, Cin, P, 4 * Cout, Cin);  // 128 x 128 tiles (taps may share one)
+    WgradArgs a{};
+    a.a = dy; a.lda = lddy; a.a_up2 = 1; a.Ca = Cout;
+    a.b = x; a.ldb = ldx; a.b_mode = B_PLAIN; a.Cb = Cin;
+    a.B = B; a.H = H; a.W = W; a.P = P; a.Mp = 4 * Cout; a.Np = Cin; a.part = (float*)ws;
+    a.part_bias = db ? bias_slabs(ws, pl) : nullptr;
+    a.pix_per_split = pl.pps;
+    const int tiles = (a.Mp / 128) * (a.Np / 128);
+    hipLaunchKernelGGL(wgrad_h3t_kernel<true>, dim3(tiles * pl.splits), dim3(256), 0, s, a);
+    int rc = launch_status("wgrad_h3t<up2>");
+    if (!rc) rc = reduce_slabs(a.part, pl.splits, (int64_t)a.Mp * a.Np, dw_ijoc, acc, s);
+    if (rc || !db) return rc;
+    return reduce_slabs(a.part_bias, pl.splits * 4, Cout, db, acc, s);
+  }
   const WgradPlan pl = plan_wgrad(4 * Cout, Cin, P, Cout, Cin);
   WgradArgs a{};
   a.a = dy; a.lda = lddy; a.a_up2 = 1; a.Ca = Cout;

@@ -1008,10 +1008,6 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_x6_kernel(
     }
 }
 
-__device__ __forceinline__ int x6w8_off(int row, int chunk) {  // bf16 element offset of a 16-B chunk
-  return row * 32 + 8 * (chunk ^ ((row >> 2) & 3));
-}
-
 // K-step 32 variant of gemm_nt_x6_kernel with ONE LDS buffer (48 KB at 128 x 128, so three
 // blocks still fit a CU): compute, barrier, store the next stage, barrier, issue the loads of
 // the stage after — a load has a whole 48-MFMA compute phase to land, and every 128-B line a
@@ -1143,6 +1139,8 @@ __global__ __launch_bounds__(256, OCC) void gemm_nt_x6_bk32_kernel(const float* 
 // rows r -> (r & 3) + 8 (r >> 2) + 4 lh (A rows staged by wave r >> 2): accumulator register r
 // is in units sA[r >> 2] * sB[(li / 8) % 4], and is re-expressed when a K-step's scales differ.
 //
+// (An epilogue through LDS — 16-B row pieces, 4 rows x 256 B per wave store — measured neutral to
+// -2 % per layer, profiles/r3_q18_gemm_le.txt; the wave index is made scalar: no VGPR spill.)
 template <int BM, int BN, int OCC = 3, bool SC = true>
 __global__ __launch_bounds__(256, OCC) void gemm_nt_h3_bk32_kernel(const float* __restrict__ A,
                                                                 const float* __restrict__ Bm, float* __restrict__ Cm,
@@ -1153,14 +1151,15 @@ __global__ __launch_bounds__(256, OCC) void gemm_nt_h3_bk32_kernel(const float* 
   constexpr int TM = BM / 64, TN = BN / 64;
   constexpr int AL = BM * 8 / 256, BL = BN * 8 / 256;
   static_assert(BM % 128 == 0 && BN % 64 == 0, "row r's staging wave must be r / 8 % 4");
-  __shared__ __attribute__((aligned(16))) _Float16 sA[2][BM * KP];
-  __shared__ __attribute__((aligned(16))) _Float16 sB[2][BN * KP];
+  __shared__ __attribute__((aligned(16))) _Float16 smem[2 * (BM + BN) * KP];
+  _Float16(*sA)[BM * KP] = reinterpret_cast<_Float16(*)[BM * KP]>(smem);
+  _Float16(*sB)[BN * KP] = reinterpret_cast<_Float16(*)[BN * KP]>(smem + 2 * BM * KP);
   __shared__ __attribute__((aligned(16))) float sscale[2][4];  // [A|B][staging wave]
   const Remap2 rm = xcd_remap2();
   A += rm.batch * bsA;
   Bm += rm.batch * bsB;
   Cm += rm.batch * bsC;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave & 1, wn = wave >> 1, li = lane & 31, lh = lane >> 5;
   const int ntn = N / BN;
   const int bid = rm.bid;

@@ -76,9 +76,15 @@ def _fwd(hip, x, w, b, scale, flags, pool=False, ldx_extra=0):
     return (nchw(y.cpu()), nchw(pl.cpu())) if pool else nchw(y.cpu())
 
 
+# kernel variants behind pis_tune: key 32 the input gradient's mask prefetch (default on)
+FWD_VARIANTS = [dict(), dict(k32=0)]
+WG_VARIANTS = [dict()]
+
+
+@pytest.mark.parametrize("variant", FWD_VARIANTS)
 @pytest.mark.parametrize("B,H,W,Cin,Cout", [(2, 16, 64, 64, 64), (1, 8, 32, 128, 64), (2, 16, 32, 64, 128),
                                            (1, 16, 32, 256, 128)])
-def test_direct_fwd_is_fp32_accurate(hip, B, H, W, Cin, Cout):
+def test_direct_fwd_is_fp32_accurate(hip, B, H, W, Cin, Cout, variant):
     g = torch.Generator().manual_seed(61)
     x0 = F.relu(torch.randn(B, Cin, H, W, generator=g, dtype=torch.float64))
     x0[0, :, :8, :8] *= torch.pow(2.0, -60 * torch.rand(Cin, 8, 8, generator=g, dtype=torch.float64))
@@ -89,7 +95,7 @@ def test_direct_fwd_is_fp32_accurate(hip, B, H, W, Cin, Cout):
     for sc in (1.0, 1e-12, 1e6):
         x = (x0 * sc).float().double()
         ref = F.relu(F.conv2d(x, w, b * sc, padding=1)) * scale[:, :, None, None]
-        for name, knobs in (("direct", DIRECT), ("native", NATIVE)):
+        for name, knobs in (("direct", {**DIRECT, **variant}), ("native", NATIVE)):
             with Knobs(hip, **knobs):
                 y = _fwd(hip, x, w, b * sc, scale, RELU | SCALE)
             errs[name, sc] = rel(y, ref)
@@ -113,9 +119,10 @@ def test_direct_fwd_pool_and_row_pitch(hip):
     assert torch.equal(pl, F.max_pool2d(y, 2))  # the pool of exactly the values written
 
 
+@pytest.mark.parametrize("variant", FWD_VARIANTS)
 @pytest.mark.parametrize("B,H,W,Cin,Cout", [(2, 16, 64, 64, 64), (1, 8, 32, 128, 64), (2, 16, 32, 64, 128)])
 @pytest.mark.parametrize("unflipped", [False, True])
-def test_direct_dgrad_is_fp32_accurate(hip, B, H, W, Cin, Cout, unflipped):
+def test_direct_dgrad_is_fp32_accurate(hip, B, H, W, Cin, Cout, unflipped, variant):
     """dx = conv_input(dz, w) * (x > 0) * keep-scale (+ dx), from a flipped copy of the weights or
     from the original ones (PIS_W_UNFLIPPED), for gradient-sized and unit dz."""
     g = torch.Generator().manual_seed(63)
@@ -133,7 +140,7 @@ def test_direct_dgrad_is_fp32_accurate(hip, B, H, W, Cin, Cout, unflipped):
         dz = (dz0 * sc).float().double()
         base = 0.5 * sc  # the accumulated-into gradient, of the same magnitude
         ref = torch.nn.grad.conv2d_input(x.shape, w, dz, padding=1) * (x > 0) * scale[:, :, None, None] + base
-        for name, knobs in (("direct", DIRECT), ("native", NATIVE)):
+        for name, knobs in (("direct", {**DIRECT, **variant}), ("native", NATIVE)):
             with Knobs(hip, **knobs):
                 nws = max(hip.pis_conv3x3_ex_ws(B, H, W, Cin, Cout), 4)
                 ws = torch.empty(nws // 4 + 1, device="cuda")
@@ -175,9 +182,10 @@ def test_direct_mixed_magnitude_chunks(hip):
     assert rel(out["direct"], ref) <= 1.25 * rel(out["native"], ref) + 1e-9
 
 
+@pytest.mark.parametrize("variant", WG_VARIANTS)
 @pytest.mark.parametrize("B,H,W,Cin,Cout", [(2, 16, 64, 64, 64), (1, 8, 32, 128, 64), (2, 16, 32, 64, 128),
                                            (1, 16, 32, 128, 128)])
-def test_direct_wgrad_is_fp32_accurate(hip, B, H, W, Cin, Cout):
+def test_direct_wgrad_is_fp32_accurate(hip, B, H, W, Cin, Cout, variant):
     """dW = sum_p dz[p] x[p + tap] and db = sum_p dz[p] (direct fp16x3 weight gradient, split-K slabs
     reduced in fixed order) against float64: as accurate as the fp32 MFMA weight gradient
     (keys 29 = 0, 14 = 0), for unit and gradient-sized dz, a batch whose second sample's dz is
@@ -196,7 +204,7 @@ def test_direct_wgrad_is_fp32_accurate(hip, B, H, W, Cin, Cout):
         dw_ref = torch.nn.grad.conv2d_weight(x, (Cout, Cin, 3, 3), dz, padding=1)
         db_ref = dz.sum(dim=(0, 2, 3))
         errs = {}
-        for name, knobs in (("direct", DIRECT), ("native", dict(k29=0, k14=0))):
+        for name, knobs in (("direct", {**DIRECT, **variant}), ("native", dict(k29=0, k14=0))):
             with Knobs(hip, **knobs):
                 nws = hip.pis_conv3x3_wgrad_ws(B, H, W, Cin, Cout)
                 ws = torch.empty(nws // 4 + 1, device="cuda")
@@ -214,8 +222,9 @@ def test_direct_wgrad_is_fp32_accurate(hip, B, H, W, Cin, Cout):
             assert errs["direct"][0] < 5e-6 and errs["direct"][1] < 1e-5, (case, errs)
 
 
+@pytest.mark.parametrize("variant", WG_VARIANTS)
 @pytest.mark.parametrize("B,H,W,Cin,Cout", [(2, 16, 64, 64, 64), (2, 16, 32, 128, 128)])
-def test_direct_wgrad_scales_any_magnitude(hip, B, H, W, Cin, Cout):
+def test_direct_wgrad_scales_any_magnitude(hip, B, H, W, Cin, Cout, variant):
     """Without accumulation: gradient-sized (1e-9), tiny (1e-30) and large (1e6) dz and a batch
     mixing 1 and 1e-30 per sample — finite and within 1.25x of the fp32 MFMA path's error."""
     g = torch.Generator().manual_seed(66)
@@ -228,7 +237,7 @@ def test_direct_wgrad_scales_any_magnitude(hip, B, H, W, Cin, Cout):
         dz = dz.float().double()
         dw_ref = torch.nn.grad.conv2d_weight(x, (Cout, Cin, 3, 3), dz, padding=1)
         errs = {}
-        for name, knobs in (("direct", DIRECT), ("native", dict(k29=0, k14=0))):
+        for name, knobs in (("direct", {**DIRECT, **variant}), ("native", dict(k29=0, k14=0))):
             with Knobs(hip, **knobs):
                 nws = hip.pis_conv3x3_wgrad_ws(B, H, W, Cin, Cout)
                 ws = torch.empty(nws // 4 + 1, device="cuda")

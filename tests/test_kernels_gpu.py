@@ -105,7 +105,7 @@ def test_conv3x3_dgrad_wgrad(hip, B, H, W, Cin, Cout):
 
 # every non-default kernel variant behind pis_tune (include/pis_capi.h) stays exact too
 TUNE_VARIANTS = [(4, 1), (4, 2), (4, 3), (5, 0), (6, 2048), (3, 0), (7, 1), (8, 0), (8, 2), (10, 0), (10, 1),
-                 (11, 0), (13, 0), (13, 1), (13, 2), (10, 2), (10, 3), (14, 0), (14, 1), (14, 2), (15, 0), (16, 0), (17, 4), (22, 0), (25, 1), (26, 0), (26, 1), (27, 0), (31, 0)]
+                 (11, 0), (13, 0), (13, 1), (13, 2), (13, 3), (10, 2), (10, 3), (14, 0), (14, 1), (14, 2), (15, 0), (16, 0), (17, 4), (22, 0), (25, 1), (26, 0), (26, 1), (27, 0), (31, 0)]
 
 
 @pytest.mark.parametrize("key,value", TUNE_VARIANTS)
@@ -262,6 +262,52 @@ def test_convt2x2(hip, B, H, W, Cin, Cout):
     assert rel_err(nchw(dx.cpu()), x.grad * (x.detach() > 0)) < 1e-5
     assert rel_err(dw.cpu().permute(3, 2, 0, 1), w.grad) < 1e-5
     assert rel_err(db.cpu(), b.grad) < 1e-5
+
+
+@pytest.mark.parametrize("B,H,W,Cin,Cout,ld_extra", [(2, 16, 32, 128, 64, 64), (1, 8, 64, 256, 128, 0),
+                                                    (1, 8, 32, 512, 256, 0), (2, 4, 32, 1024, 512, 0)])
+def test_convt2x2_k32(hip, B, H, W, Cin, Cout, ld_extra):
+    """The K-step-32 transposed-conv kernel (pis_tune key 13 = 4): forward into a concat slice (+bias),
+    input gradient gathered from a strided dy with the ReLU mask and accumulate, vs fp32 ATen."""
+    prev = hip.pis_tune(13, 4)
+    try:
+        g = torch.Generator().manual_seed(33)
+        x = F.relu(torch.randn(B, Cin, H, W, generator=g))
+        w = torch.randn(Cin, Cout, 2, 2, generator=g) / Cin ** 0.5
+        b = torch.randn(Cout, generator=g)
+        y_ref = F.conv_transpose2d(x, w, b, stride=2)
+        dy = torch.randn(y_ref.shape, generator=g)
+        xr, wr, br = x.clone().requires_grad_(True), w.clone().requires_grad_(True), b.clone().requires_grad_(True)
+        F.conv_transpose2d(xr, wr, br, stride=2).backward(dy)
+        dx_ref = xr.grad * (x > 0)
+        ld = Cout + ld_extra
+        w_ijoc = w.permute(2, 3, 1, 0).contiguous().cuda()
+        xd, bd = nhwc(x).cuda(), b.cuda()
+        yb = torch.zeros(B, 2 * H, 2 * W, ld, device="cuda")
+        assert hip.pis_convt2x2_fwd(xd.data_ptr(), Cin, w_ijoc.data_ptr(), bd.data_ptr(), yb.data_ptr(), ld,
+                                    B, H, W, Cin, Cout, s()) == 0, hip.pis_last_error()
+        dyb = torch.zeros(B, 2 * H, 2 * W, ld, device="cuda")
+        dyb[..., :Cout] = nhwc(dy).cuda()
+        wc = torch.empty(Cin * 4 * Cout, device="cuda")
+        assert hip.pis_convt2x2_prep(w_ijoc.data_ptr(), wc.data_ptr(), Cin, Cout, s()) == 0
+        dx = torch.full((B, H, W, Cin), 0.5, device="cuda")
+        assert hip.pis_convt2x2_dgrad(dyb.data_ptr(), ld, wc.data_ptr(), xd.data_ptr(), Cin, dx.data_ptr(), Cin,
+                                      B, H, W, Cin, Cout, MASK | ACC, s()) == 0, hip.pis_last_error()
+        # weight + bias gradient (the row-staged split-K kernel with the up-sampled A gather), accumulating
+        nws = hip.pis_convt2x2_wgrad_ws(B, H, W, Cin, Cout)
+        ws = torch.empty(nws // 4 + 1, device="cuda")
+        dw = torch.full((2, 2, Cout, Cin), 0.25, device="cuda")
+        db = torch.full((Cout,), 0.25, device="cuda")
+        assert hip.pis_convt2x2_wgrad(xd.data_ptr(), Cin, dyb.data_ptr(), ld, dw.data_ptr(), db.data_ptr(),
+                                      B, H, W, Cin, Cout, ACC, ws.data_ptr(), nws, s()) == 0, hip.pis_last_error()
+        torch.cuda.synchronize()
+        assert rel_err(nchw(yb[..., :Cout].cpu()), y_ref) < 1e-5
+        assert torch.all(yb[..., Cout:] == 0)
+        assert rel_err(nchw(dx.cpu()) - 0.5, dx_ref) < 1e-5
+        assert rel_err(dw.cpu().permute(3, 2, 0, 1) - 0.25, wr.grad) < 1e-5
+        assert rel_err(db.cpu() - 0.25, br.grad) < 1e-5
+    finally:
+        hip.pis_tune(13, prev)
 
 
 def test_maxpool(hip):
@@ -742,7 +788,7 @@ def test_convt_bf16x6_is_fp32_accurate(hip, Cin, Cout):
     wc = torch.empty(Cin * 4 * Cout, device="cuda")
     assert hip.pis_convt2x2_prep(w_ijoc.data_ptr(), wc.data_ptr(), Cin, Cout, s()) == 0
     errs = {}
-    for name, (v13, v14) in {"x6": (1, 1), "h3": (3, 2), "f32": (2, 0)}.items():
+    for name, (v13, v14) in {"x6": (1, 1), "h3": (3, 2), "h3k32": (4, 2), "f32": (2, 0)}.items():
         p13, p14 = hip.pis_tune(13, v13), hip.pis_tune(14, v14)
         try:
             yd = torch.empty(B, 2 * H, 2 * W, Cout, device="cuda")
@@ -763,7 +809,7 @@ def test_convt_bf16x6_is_fp32_accurate(hip, Cin, Cout):
             hip.pis_tune(14, p14)
         errs[name] = [rel_err(nchw(yd.cpu()), y.detach()), rel_err(nchw(dx.cpu()), x.grad),
                       rel_err(dw.cpu().permute(3, 2, 0, 1), w.grad), rel_err(db.cpu(), b.grad)]
-    for v in ("x6", "h3"):
+    for v in ("x6", "h3", "h3k32"):
         for e6, e32 in zip(errs[v], errs["f32"]):
             assert e6 <= 1.25 * e32 + 1e-9, errs
             assert e6 < 5e-6, errs

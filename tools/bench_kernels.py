@@ -47,6 +47,8 @@ def main():
     ap.add_argument("--layers", default="")
     ap.add_argument("--ops", default="fwd,dgrad,wgrad")
     ap.add_argument("--noload", action="store_true", help="also time each variant without global loads")
+    ap.add_argument("--dbg", default="", help="timing twins: pis_tune key 2 levels to time beside each variant "
+                    "(direct kernels: 1 no global loads, 2 no LDS staging, 4 no epilogue; OR-ed)")
     ap.add_argument("--convt", action="store_true", help="time the transposed convs instead")
     ap.add_argument("--tune", action="append", default=[], metavar="KEY=VALUE", help="fixed knobs for every variant")
     args = ap.parse_args()
@@ -100,7 +102,8 @@ def main():
             "wgrad": lambda: lib.pis_conv3x3_wgrad(x.data_ptr(), cin, dz.data_ptr(), cout, dw.data_ptr(),
                                                    db.data_ptr(), B, H, H, cin, cout, 0, ws.data_ptr(), nws, s),
         }
-        vlist = [(v, 0) for v in variants] + ([(v, 1) for v in variants] if args.noload else [])
+        dbg = [int(d) for d in args.dbg.split(",") if d] or ([1] if args.noload else [])
+        vlist = [(v, 0) for v in variants] + [(v, d) for d in dbg for v in variants]
         results = {}
         for _ in range(args.rounds):
             for v, nl in vlist:
@@ -114,7 +117,7 @@ def main():
             line = f"{name:12s} {op:6s}"
             for v, nl in vlist:
                 ms = min(results[(op, v, nl)])
-                line += f"  v{v}{'-nl' if nl else ''}: {ms:7.3f} ms {flops / ms / 1e9:6.1f} TF/s"
+                line += f"  v{v}{f'-d{nl}' if nl else ''}: {ms:7.3f} ms {flops / ms / 1e9:6.1f} TF/s"
             print(line, flush=True)
         del x, dz, w, y, dx, ws, dw
         torch.cuda.empty_cache()
