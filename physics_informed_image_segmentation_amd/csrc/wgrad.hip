@@ -35,6 +35,9 @@ struct WgradArgs {
   // batched launches (gridDim.y > 1, Winograd's 16 GEMMs): per-batch offsets; slab pitch
   int64_t bs_a, bs_b, bs_part, split_stride;     // split_stride 0 = Mp * Np
   int pair;                                      // wgrad_x6: pair-lane staging of 4-pixel operands
+  int dbg;                                       // wgrad_h3t timing twins (pis_tune key 2, wrong results):
+                                                 // 1 no loads after the first two K-steps, 2 no staging
+                                                 // after the first, 4 no slab stores
 };
 
 // BKP pixels per stage: 32 MFMAs per wave between barriers for every tile shape
@@ -960,6 +963,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_h3t_kernel(WgradArgs g) {
 
   f32x4 ra[2][4], rb[2][4];
   auto gload = [&](f32x4 (&xa)[4], f32x4 (&xb)[4], int st) __attribute__((always_inline)) {
+    if ((g.dbg & 1) && st > 1) return;
     const int p0 = p_begin + st * WT_BK;
     size_t abase = 0;
     if (UP2) {  // the K-step's 32 pixels: one image row (b, y), columns x0 ..
@@ -1062,7 +1066,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_h3t_kernel(WgradArgs g) {
         bf[pl][a] = frag(buf + (2 + pl) * WT_PLANE, 0, 64 * wn + 32 * a);
       }
     if (st + 1 < nst) {
-      split_store(ra[nxt], rb[nxt], nxt, s_a[nxt], s_b[nxt]);
+      if (!((g.dbg & 2) && st > 0)) split_store(ra[nxt], rb[nxt], nxt, s_a[nxt], s_b[nxt]);
       if (st + 3 < nst) gload(ra[nxt], rb[nxt], st + 3);
     }
     {  // the partial sums in this K-step's units (exact: powers of two)
@@ -1106,6 +1110,17 @@ __global__ __launch_bounds__(256, 2) void wgrad_h3t_kernel(WgradArgs g) {
   }
   float* out = g.part + (size_t)split * (g.split_stride ? g.split_stride : (int64_t)g.Mp * g.Np);
   const float inv = units != 0.f ? 1.f / units : 0.f;
+  if (g.dbg & 4) {
+    float t = 0.f;
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) t += acc[a][b][r];
+    if (t == 1.2345f) out[tid] = t;
+    return;
+  }
 #pragma unroll
   for (int a = 0; a < 2; ++a)
 #pragma unroll
@@ -1135,6 +1150,7 @@ static int run_wgrad(const WgradArgs& base, const WgradPlan& pl, hipStream_t s, 
   WgradArgs a = base;
   a.pix_per_split = pl.pps;
   a.pair = tune_get(PIS_TUNE_WGRAD_PAIR);
+  a.dbg = tune_get(PIS_TUNE_DEBUG_NOLOAD);
   const int tiles = (a.Mp / pl.bm) * (a.Np / pl.bn);
   const dim3 grid(tiles * pl.splits, batches);
   // key 14 = 3 (auto): fp16x3 where the contraction's output has >= 256 columns (Cin): measured
