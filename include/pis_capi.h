@@ -144,7 +144,8 @@ int pis_tune(int key, int value);
  * C[b] = A[b] . B[b]^T row-major fp32 — 0 bf16x6 128x128 (the Winograd GEMM), 1/2 its
  * no-global-load / no-split timing twins (wrong results), 3 fp32 MFMA, 4 bf16x6 128x64, 5/6 the
  * K-step-32 single-LDS-buffer bf16x6 128x128 (2 / 3 waves per SIMD), 7 its 128x64, 10 / 11 the
- * fp16x3 128x128 GEMM unscaled / with per-K-step scales (11 is the Winograd default), 12 its 128x64.
+ * fp16x3 128x128 GEMM unscaled / with per-K-step scales (11 is the Winograd default), 12 its 128x64,
+ * 13 / 14 11's no-global-load / no-staging timing twins (wrong results).
  * 5-12 need K % 32 == 0. */
 int pis_debug_gemm_nt(const float* A, const float* B, float* C, int M, int N, int K, int batch, int variant,
                       pis_stream_t stream);

@@ -390,9 +390,12 @@ __global__ __launch_bounds__(256, 5) void loss_fwd_rows_kernel(LossRowArgs a) {
     Batch A, Bn;
     load(A, ys);
     for (int y = ys; y < ye; y += 4) {
-      load(Bn, y + 2);  // unconditional: branch-free, exact vmcnt waits
+      // a batch past the segment's end is not loaded (ys, ye are uniform per wave: a wave's lanes
+      // share their row segment, TX >= 64): at C2 a segment is ONE batch, and the two unconditional
+      // prefetches were 2/3 of the loads issued
+      if (y + 2 < ye) load(Bn, y + 2);
       compute(A, y);
-      load(A, y + 4);
+      if (y + 4 < ye) load(A, y + 4);
       if (y + 2 < ye) compute(Bn, y + 2);
     }
   }
@@ -544,7 +547,10 @@ static int loss_rows(int B, int H, int W) {
   // a multiple of RY x LOSS_ROW_BATCH rows (RY row segments per block) so no thread pads its last
   // batch; at least as many rows as keep the block count near the target
   const int ry = 256 / std::min(std::max(W / 4, 1), 256), q = ry * LOSS_ROW_BATCH;
-  int r = (int)std::max<int64_t>(q, cdiv((int64_t)B * H, LOSS_TARGET_BLOCKS));
+  // at least 4 row batches per thread: small problems (C2: 16.8 MB) get fewer, fuller blocks —
+  // 256 instead of 1024 at C2, 21.5 -> 18.0 us cold (profiles/r3_q21_loss_rowmul.txt); the
+  // bandwidth regime (B = 64) keeps ~1024
+  int r = (int)std::max<int64_t>(4 * q, cdiv((int64_t)B * H, LOSS_TARGET_BLOCKS));
   r = (int)cdiv(r, q) * q * std::max(1, tune_get(PIS_TUNE_LOSS_ROWMUL));
   return std::min(r, H);
 }

@@ -927,7 +927,7 @@ __device__ __forceinline__ int wtsw(int row, int chunk) { return row * 128 + 8 *
 // 32-aligned split starts a K-step's 32 pixels lie in one image row, so its rows are one base +
 // 2 r pixels apart; the bias partials (column sums of A, blocks of the first column tile) are
 // summed from the raw loads and reduced over the 8 threads of a column group in LDS (fixed order).
-template <bool UP2 = false>
+template <bool UP2 = false, int D = 2>
 __global__ __launch_bounds__(256, 2) void wgrad_h3t_kernel(WgradArgs g) {
   const Remap2 rm = xcd_remap2();
   if (rm.batch) {
@@ -961,9 +961,9 @@ __global__ __launch_bounds__(256, 2) void wgrad_h3t_kernel(WgradArgs g) {
   const bool do_bias = UP2 && g.part_bias != nullptr && n0 == 0;
   f32x4 bsum = {0.f, 0.f, 0.f, 0.f};
 
-  f32x4 ra[2][4], rb[2][4];
+  f32x4 ra[D][4], rb[D][4];
   auto gload = [&](f32x4 (&xa)[4], f32x4 (&xb)[4], int st) __attribute__((always_inline)) {
-    if ((g.dbg & 1) && st > 1) return;
+    if ((g.dbg & 1) && st >= D) return;
     const int p0 = p_begin + st * WT_BK;
     size_t abase = 0;
     if (UP2) {  // the K-step's 32 pixels: one image row (b, y), columns x0 ..
@@ -1044,17 +1044,22 @@ __global__ __launch_bounds__(256, 2) void wgrad_h3t_kernel(WgradArgs g) {
   float units = 0.f;  // scale product the partial sums are expressed in (0: none yet)
   float s_a[2] = {0.f, 0.f}, s_b[2] = {0.f, 0.f};  // per buffer parity: the staged K-step's scales
 
+  // D register sets: the raw operands of K-step st + D in flight while K-step st multiplies. Set
+  // of K-step k: k % D; LDS buffer: k & 1. (D = 3 measured neutral on every C2 layer,
+  // profiles/r3_q22_wgrad_depth.txt: D = 2 is launched.)
   if (nst > 0) {
-    gload(ra[0], rb[0], 0);
-    if (nst > 1) gload(ra[1], rb[1], 1);
+#pragma unroll
+    for (int k = 0; k < D; ++k)
+      if (k < nst) gload(ra[k], rb[k], k);
     publish(ra[0], rb[0], 0);
     __syncthreads();
     split_store(ra[0], rb[0], 0, s_a[0], s_b[0]);
-    if (nst > 2) gload(ra[0], rb[0], 2);
+    if (nst > D) gload(ra[0], rb[0], D);
   }
-  auto kstep = [&](int st, auto par_c) __attribute__((always_inline)) {
+  auto kstep = [&](int st, auto par_c, auto set_c) __attribute__((always_inline)) {
     constexpr int cur = decltype(par_c)::value, nxt = cur ^ 1;
-    if (st + 1 < nst) publish(ra[nxt], rb[nxt], nxt);
+    constexpr int sn = (decltype(set_c)::value + 1) % D;  // register set of K-step st + 1
+    if (st + 1 < nst) publish(ra[sn], rb[sn], nxt);
     __syncthreads();  // buffer cur staged; buffer nxt's readers (K-step st - 1) done
     const _Float16* buf = smem + cur * WT_BUF;
     f16x8 af[2][2], bf[2][2];
@@ -1066,8 +1071,8 @@ __global__ __launch_bounds__(256, 2) void wgrad_h3t_kernel(WgradArgs g) {
         bf[pl][a] = frag(buf + (2 + pl) * WT_PLANE, 0, 64 * wn + 32 * a);
       }
     if (st + 1 < nst) {
-      if (!((g.dbg & 2) && st > 0)) split_store(ra[nxt], rb[nxt], nxt, s_a[nxt], s_b[nxt]);
-      if (st + 3 < nst) gload(ra[nxt], rb[nxt], st + 3);
+      if (!((g.dbg & 2) && st > 0)) split_store(ra[sn], rb[sn], nxt, s_a[nxt], s_b[nxt]);
+      if (st + 1 + D < nst) gload(ra[sn], rb[sn], st + 1 + D);
     }
     {  // the partial sums in this K-step's units (exact: powers of two)
       const float u = s_a[cur] * s_b[cur];
@@ -1103,10 +1108,25 @@ __global__ __launch_bounds__(256, 2) void wgrad_h3t_kernel(WgradArgs g) {
         }
     }
   };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using I2 = std::integral_constant<int, 2>;
+  if constexpr (D == 2) {
 #pragma unroll 1
-  for (int st = 0; st < nst; st += 2) {
-    kstep(st, std::integral_constant<int, 0>{});
-    if (st + 1 < nst) kstep(st + 1, std::integral_constant<int, 1>{});
+    for (int st = 0; st < nst; st += 2) {
+      kstep(st, I0{}, I0{});
+      if (st + 1 < nst) kstep(st + 1, I1{}, I1{});
+    }
+  } else {  // K-steps by six: buffer parity and register set both repeat
+#pragma unroll 1
+    for (int st = 0; st < nst; st += 6) {
+      kstep(st, I0{}, I0{});
+      if (st + 1 < nst) kstep(st + 1, I1{}, I1{});
+      if (st + 2 < nst) kstep(st + 2, I0{}, I2{});
+      if (st + 3 < nst) kstep(st + 3, I1{}, I0{});
+      if (st + 4 < nst) kstep(st + 4, I0{}, I1{});
+      if (st + 5 < nst) kstep(st + 5, I1{}, I2{});
+    }
   }
   float* out = g.part + (size_t)split * (g.split_stride ? g.split_stride : (int64_t)g.Mp * g.Np);
   const float inv = units != 0.f ? 1.f / units : 0.f;
@@ -1167,7 +1187,7 @@ static int run_wgrad(const WgradArgs& base, const WgradPlan& pl, hipStream_t s, 
     if (tune_get(PIS_TUNE_WGRAD_T) != 0 && pl.bm == 128 && pl.bn == 128 && !a.a_up2 && !a.part_bias &&
         pl.pps % WT_BK == 0 && a.lda % 4 == 0 && a.ldb % 4 == 0 && a.bs_a % 4 == 0 && a.bs_b % 4 == 0 &&
         ((uintptr_t)a.a & 15) == 0 && ((uintptr_t)a.b & 15) == 0) {
-      hipLaunchKernelGGL(wgrad_h3t_kernel<false>, grid, dim3(256), 0, s, a);
+      hipLaunchKernelGGL((wgrad_h3t_kernel<false, 2>), grid, dim3(256), 0, s, a);
       return launch_status("wgrad_h3t");
     }
     if (pl.bm == 128 && pl.bn == 128) hipLaunchKernelGGL((wgrad_h3_kernel<128, 128>), grid, dim3(256), 0, s, a);
@@ -1609,7 +1629,7 @@ extern "C" int pis_convt2x2_wgrad(const float* x, int ldx, const float* dy, int 
     a.part_bias = db ? bias_slabs(ws, pl) : nullptr;
     a.pix_per_split = pl.pps;
     const int tiles = (a.Mp / 128) * (a.Np / 128);
-    hipLaunchKernelGGL(wgrad_h3t_kernel<true>, dim3(tiles * pl.splits), dim3(256), 0, s, a);
+    hipLaunchKernelGGL((wgrad_h3t_kernel<true, 2>), dim3(tiles * pl.splits), dim3(256), 0, s, a);
     int rc = launch_status("wgrad_h3t<up2>");
     if (!rc) rc = reduce_slabs(a.part, pl.splits, (int64_t)a.Mp * a.Np, dw_ijoc, acc, s);
     if (rc || !db) return rc;

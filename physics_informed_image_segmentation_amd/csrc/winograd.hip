@@ -1141,7 +1141,11 @@ __global__ __launch_bounds__(256, OCC) void gemm_nt_x6_bk32_kernel(const float* 
 //
 // (An epilogue through LDS — 16-B row pieces, 4 rows x 256 B per wave store — measured neutral to
 // -2 % per layer, profiles/r3_q18_gemm_le.txt; the wave index is made scalar: no VGPR spill.)
-template <int BM, int BN, int OCC = 3, bool SC = true>
+// DBG (timing twins, pis_debug_gemm_nt variants 13 / 14, wrong results): 1 no global loads after the
+// first two K-steps, 2 no staging after the first (profiles/r3_q22_gemm_twins.txt: staging is 24-44 %
+// of the time, the loads 0-17 %). (Two LDS stages + two register sets at two blocks per CU — one
+// barrier per K-step, loads a K-step further ahead — ran 10-30 % slower: profiles/r3_q23_gemm_db.txt.)
+template <int BM, int BN, int OCC = 3, bool SC = true, int DBG = 0>
 __global__ __launch_bounds__(256, OCC) void gemm_nt_h3_bk32_kernel(const float* __restrict__ A,
                                                                 const float* __restrict__ Bm, float* __restrict__ Cm,
                                                                 int M, int N, int K, int64_t bsA, int64_t bsB,
@@ -1168,6 +1172,7 @@ __global__ __launch_bounds__(256, OCC) void gemm_nt_h3_bk32_kernel(const float* 
   const bool full = m0 + BM <= M && K % BK == 0;
   f32x4 ra[AL], rb[BL];
   auto gload = [&](int k0) {
+    if (DBG == 1 && k0 >= 2 * BK) return;
     const int k = k0 + q8;
 #pragma unroll
     for (int i = 0; i < AL; ++i) {
@@ -1278,7 +1283,7 @@ __global__ __launch_bounds__(256, OCC) void gemm_nt_h3_bk32_kernel(const float* 
     }
     if (kt + 1 < KT) {
       __syncthreads();
-      lstore();
+      if (DBG != 2) lstore();
       __syncthreads();
       if (kt + 2 < KT) gload((kt + 2) * BK);
     }
@@ -2057,7 +2062,8 @@ int launch_wino_wgrad_out(const float* M, int N, int C, float* dw, int accumulat
 // C[b] (M x N) = A[b] (M x K) . B[b]^T (N x K), batch b over gridDim.y, all row-major fp32.
 // variant: 0 bf16x6 128x128, 1 its no-global-load timing twin, 2 its no-split timing twin,
 // 3 fp32 MFMA 128x128, 4 bf16x6 128x64, 5/6 the K-step-32 single-buffer bf16x6 128x128 at 2 / 3
-// waves per SIMD, 7 its 128x64, 10/11 the fp16x3 128x128 unscaled / scaled, 12 its 128x64.
+// waves per SIMD, 7 its 128x64, 10/11 the fp16x3 128x128 unscaled / scaled, 12 its 128x64, 13 / 14
+// the scaled one's no-load / no-staging timing twins (wrong results).
 // Requires N % 128 == 0 (64 for 4, 7, 12), K % 16 == 0 (32 from variant 5).
 extern "C" int pis_debug_gemm_nt(const float* A, const float* B, float* C, int M, int N, int K, int batch,
                                  int variant, pis_stream_t stream) {
@@ -2080,6 +2086,8 @@ extern "C" int pis_debug_gemm_nt(const float* A, const float* B, float* C, int M
     case 10: hipLaunchKernelGGL((gemm_nt_h3_bk32_kernel<128, 128, 3, false>), grid, dim3(256), 0, s, A, B, C, M, N, K, sa, sb, sc); break;
     case 11: hipLaunchKernelGGL((gemm_nt_h3_bk32_kernel<128, 128, 3>), grid, dim3(256), 0, s, A, B, C, M, N, K, sa, sb, sc); break;
     case 12: hipLaunchKernelGGL((gemm_nt_h3_bk32_kernel<128, 64, 4>), grid, dim3(256), 0, s, A, B, C, M, N, K, sa, sb, sc); break;
+    case 13: hipLaunchKernelGGL((gemm_nt_h3_bk32_kernel<128, 128, 3, true, 1>), grid, dim3(256), 0, s, A, B, C, M, N, K, sa, sb, sc); break;
+    case 14: hipLaunchKernelGGL((gemm_nt_h3_bk32_kernel<128, 128, 3, true, 2>), grid, dim3(256), 0, s, A, B, C, M, N, K, sa, sb, sc); break;
     default: set_error("pis_debug_gemm_nt: unknown variant %d", variant); return PIS_ERR_ARG;
   }
   return launch_status("debug_gemm_nt");
