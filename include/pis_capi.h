@@ -170,6 +170,9 @@ int pis_arm_gemm_event(void* event);
  * nodes and allocator blocks). pis_stream_capture_status: hipStreamCaptureStatus (0 none, 1 active,
  * 2 invalidated) or a negative error. */
 int pis_stream_create(int priority, pis_stream_t* out);
+/* pis_stream_create restricted to ncu of the device's CUs (evenly spaced; ncu <= 0: all): a scheduling
+ * experiment for the weight-gradient stream (PIS_SIDE_CUS). */
+int pis_stream_create_cus(int priority, int ncu, pis_stream_t* out);
 int pis_stream_destroy(pis_stream_t stream);
 int pis_stream_capture_status(pis_stream_t stream);
 
@@ -238,10 +241,13 @@ int pis_conv3x3_wgrad_keep(const float* x, int ldx, const float* dz, int ldz, fl
  * U[36][N][C] for the batched GEMMs (followed, with pis_tune(23, 1) and C, N % 64 == 0, by its
  * per-(output, 32-channel chunk) maxima umax[N][C / 32]); for the fused 64->64 contraction the fp16x3 hi / lo planes +
  * one inverse scale per output channel, or with pis_tune(22, 0) the bf16x6 planes: the tune key
- * must not change between this call and the conv call that consumes it).
- * pis_conv3x3_filter_bytes returns its size, 0 when that call would not take the F(4x4,3x3)
- * GEMM path (then PIS_FILTER_READY must not be used). Pass the result as the weight argument
- * with PIS_FILTER_READY (dgrad: with PIS_WINO_PREPARED | PIS_W_UNFLIPPED semantics kept). */
+ * must not change between this call and the conv call that consumes it); where the call takes the
+ * direct fp16x3 kernel (pis_tune key 29) its weight split: fp16 hi / lo planes in the kernel's LDS
+ * image + one inverse scale per output channel.
+ * pis_conv3x3_filter_bytes returns its size, 0 when that call would take neither the F(4x4,3x3)
+ * GEMM path nor the direct kernel (then PIS_FILTER_READY must not be used). Pass the result as the
+ * weight argument with PIS_FILTER_READY (dgrad: with PIS_WINO_PREPARED | PIS_W_UNFLIPPED semantics
+ * kept). pis_conv3x3_filters: the Winograd transforms in one launch, the direct splits in a second. */
 size_t pis_conv3x3_filter_bytes(int B, int H, int W, int Cin, int Cout, int dgrad);
 int pis_conv3x3_filter(const float* w, int B, int H, int W, int Cin, int Cout, int dgrad, void* out,
                        size_t out_bytes, pis_stream_t stream);

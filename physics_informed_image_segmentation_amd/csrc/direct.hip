@@ -61,10 +61,20 @@ __device__ __forceinline__ int dsw(int row, int half) { return row * DKC + 8 * (
 // weights -> [chunk][slice][tap][plane][64][16] fp16 (rows swizzled as dsw), per output scale.
 // dgrad = 0: out channel n, contraction c of w[n][r][s][c] (KRSC); dgrad = 1: out channel c,
 // contraction n of the flipped filter w[n][2-r][2-s][c] (the input gradient).
-__global__ __launch_bounds__(256) void conv3x3_wsplit_kernel(const float* __restrict__ w, int Cin, int Cout,
-                                                             int dgrad, _Float16* __restrict__ out,
-                                                             float* __restrict__ winv) {
-  const int o = blockIdx.x;  // output channel of the contraction
+struct WsplitJob {
+  const float* w;  // KRSC [Cout][3][3][Cin]
+  void* out;       // direct_h3_ws_bytes(C, N): the planes, then 1 / t_n
+  int Cin, Cout, dgrad;
+};
+constexpr int WSPLIT_MAX_JOBS = 40;
+struct WsplitBatch {
+  WsplitJob j[WSPLIT_MAX_JOBS];
+  int start[WSPLIT_MAX_JOBS + 1];
+  int n;
+};
+
+__device__ __forceinline__ void wsplit_one(const float* __restrict__ w, int Cin, int Cout, int dgrad,
+                                           _Float16* __restrict__ out, float* __restrict__ winv, int o) {
   const int C = dgrad ? Cout : Cin, N = dgrad ? Cin : Cout, ns = N / 64;
   const int tid = threadIdx.x;
   auto at = [&](int tap, int k) -> float {
@@ -91,6 +101,24 @@ __global__ __launch_bounds__(256) void conv3x3_wsplit_kernel(const float* __rest
     out[base + off] = hi;
     out[base + 64 * DKC + off] = lo;
   }
+}
+
+__global__ __launch_bounds__(256) void conv3x3_wsplit_kernel(const float* __restrict__ w, int Cin, int Cout,
+                                                             int dgrad, _Float16* __restrict__ out,
+                                                             float* __restrict__ winv) {
+  wsplit_one(w, Cin, Cout, dgrad, out, winv, blockIdx.x);
+}
+
+// several layers' splits in ONE launch (pis_conv3x3_filters: PIS_FILTER_READY for the direct
+// kernel): job k owns blocks [start[k], start[k + 1]), one per output channel of its contraction
+__global__ __launch_bounds__(256) void conv3x3_wsplit_batch_kernel(WsplitBatch wb) {
+  int k = 0;
+  while (k + 1 < wb.n && (int)blockIdx.x >= wb.start[k + 1]) ++k;
+  const WsplitJob& j = wb.j[k];
+  const int C = j.dgrad ? j.Cout : j.Cin, N = j.dgrad ? j.Cin : j.Cout;
+  _Float16* wp = reinterpret_cast<_Float16*>(j.out);
+  float* winv = reinterpret_cast<float*>(reinterpret_cast<char*>(j.out) + (size_t)9 * C * N * 2 * sizeof(_Float16));
+  wsplit_one(j.w, j.Cin, j.Cout, j.dgrad, wp, winv, (int)blockIdx.x - wb.start[k]);
 }
 
 // MPF (pis_tune key 32 = 1, default): an input gradient's epilogue ReLU-mask rows are loaded
@@ -337,6 +365,25 @@ bool direct_h3_wanted(int H, int W, int C, int N, int ldx) {
   return mode == 2 || (hi <= 128 && H >= 256);
 }
 
+// the direct kernel's weight splits of several layers in one launch (KRSC weights; dgrad: the
+// contraction over Cout of the ORIGINAL weights, as launch_direct_h3's dgrad_orig)
+int launch_direct_wsplit_batch(int n, const float* const* w, void* const* out, const int* Cin, const int* Cout,
+                               const int* dgrad, hipStream_t s) {
+  if (n <= 0) return PIS_OK;
+  if (n > WSPLIT_MAX_JOBS) return set_error("direct wsplit batch: too many jobs"), PIS_ERR_ARG;
+  WsplitBatch wb{};
+  wb.n = n;
+  int total = 0;
+  for (int k = 0; k < n; ++k) {
+    wb.j[k] = WsplitJob{w[k], out[k], Cin[k], Cout[k], dgrad[k]};
+    wb.start[k] = total;
+    total += dgrad[k] ? Cin[k] : Cout[k];
+  }
+  wb.start[n] = total;
+  hipLaunchKernelGGL(conv3x3_wsplit_batch_kernel, dim3(total), dim3(256), 0, s, wb);
+  return launch_status("conv3x3_wsplit_batch");
+}
+
 size_t direct_h3_ws_bytes(int C, int N) {
   return (size_t)9 * C * N * 2 * sizeof(_Float16) + (size_t)N * sizeof(float) + 256;
 }
@@ -344,24 +391,31 @@ size_t direct_h3_ws_bytes(int C, int N) {
 // a: the direct conv as pis_conv3x3_fwd_ex / _dgrad_ex build it (src = input, wt = KRSC weights,
 // w_unflipped: an input gradient reading the ORIGINAL weights; otherwise a flipped copy w_flip
 // [c][r][s][n], which is the forward layout of the transposed problem)
-int launch_direct_h3(const IGemmArgs& a, int B, void* ws, size_t ws_bytes, hipStream_t s, bool dgrad_orig) {
+int launch_direct_h3(const IGemmArgs& a, int B, void* ws, size_t ws_bytes, hipStream_t s, bool dgrad_orig,
+                     bool ready) {
   const int C = a.Csrc, N = a.N;
-  if (!direct_h3_shape_ok(a.H, a.W, C, N, a.lds) || ws_bytes < direct_h3_ws_bytes(C, N))
+  if (!direct_h3_shape_ok(a.H, a.W, C, N, a.lds) || (!ready && ws_bytes < direct_h3_ws_bytes(C, N)))
     return set_error("direct conv: shape or workspace not supported"), PIS_ERR_ARG;
   auto a16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
   if (!a16(a.src) || !a16(a.dst) || a.ldd % 4 || ((a.flags & PIS_MASK) && (!a16(a.mask) || a.ldm % 4)) ||
       (a.pool && !a16(a.pool)) || ((a.flags & PIS_SCALE) && !a16(a.scale)) || (a.bias && !a16(a.bias)))
     return set_error("direct conv: input, output, mask, scale, bias and pool must be 16-byte aligned with "
                      "channel strides % 4 == 0"), PIS_ERR_ARG;
-  _Float16* wp = reinterpret_cast<_Float16*>(ws);
-  float* winv = reinterpret_cast<float*>(reinterpret_cast<char*>(ws) + (size_t)9 * C * N * 2 * sizeof(_Float16));
-  // forward (or a flipped copy [Cin'=N][3][3][C] read as KRSC): out N, contraction C
-  if (dgrad_orig)  // original weights w[C][3][3][N] (conv Cout = C, Cin = N): the flipped contraction
-    hipLaunchKernelGGL(conv3x3_wsplit_kernel, dim3(N), dim3(256), 0, s, a.wt, N, C, 1, wp, winv);
-  else
-    hipLaunchKernelGGL(conv3x3_wsplit_kernel, dim3(N), dim3(256), 0, s, a.wt, C, N, 0, wp, winv);
-  int rc = launch_status("conv3x3_wsplit");
-  if (rc) return rc;
+  // ready (PIS_FILTER_READY): a.wt IS the split — planes, then 1 / t_n — from pis_conv3x3_filter(s)
+  void* wsp = ready ? const_cast<float*>(a.wt) : ws;
+  _Float16* wp = reinterpret_cast<_Float16*>(wsp);
+  float* winv = reinterpret_cast<float*>(reinterpret_cast<char*>(wsp) + (size_t)9 * C * N * 2 * sizeof(_Float16));
+  if (!ready) {
+    // forward (or a flipped copy [Cin'=N][3][3][C] read as KRSC): out N, contraction C
+    if (dgrad_orig)  // original weights w[C][3][3][N] (conv Cout = C, Cin = N): the flipped contraction
+      hipLaunchKernelGGL(conv3x3_wsplit_kernel, dim3(N), dim3(256), 0, s, a.wt, N, C, 1, wp, winv);
+    else
+      hipLaunchKernelGGL(conv3x3_wsplit_kernel, dim3(N), dim3(256), 0, s, a.wt, C, N, 0, wp, winv);
+    const int rc = launch_status("conv3x3_wsplit");
+    if (rc) return rc;
+  } else if (((uintptr_t)wsp & 15) != 0) {
+    return set_error("direct conv: the ready split must be 16-byte aligned"), PIS_ERR_ARG;
+  }
   DirectArgs g{};
   g.x = a.src; g.ldx = a.lds; g.wp = wp; g.winv = winv; g.bias = a.bias; g.scale = a.scale;
   g.mask = a.mask; g.ldm = a.ldm; g.y = a.dst; g.ldy = a.ldd; g.pool = a.pool;

@@ -78,7 +78,10 @@ int launch_wino_wgrad_out(const float* M, int N, int C, float* dw, int accumulat
 // launch (dgrad_orig: an input gradient whose a.wt holds the ORIGINAL KRSC weights)
 bool direct_h3_shape_ok(int H, int W, int C, int N, int ldx);
 size_t direct_h3_ws_bytes(int C, int N);
-int launch_direct_h3(const IGemmArgs& a, int B, void* ws, size_t ws_bytes, hipStream_t s, bool dgrad_orig);
+int launch_direct_h3(const IGemmArgs& a, int B, void* ws, size_t ws_bytes, hipStream_t s, bool dgrad_orig,
+                     bool ready = false);
+int launch_direct_wsplit_batch(int n, const float* const* w, void* const* out, const int* Cin, const int* Cout,
+                               const int* dgrad, hipStream_t s);
 // pis_tune key 29's policy for a contraction of C channels into N outputs on an H x W grid
 bool direct_h3_wanted(int H, int W, int C, int N, int ldx);
 // ... and for the layer's weight gradient (the direct fp16x3 wgrad kernel): its workspace, launch

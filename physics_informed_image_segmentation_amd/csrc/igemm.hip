@@ -571,9 +571,11 @@ static int dispatch_conv3x3(const IGemmArgs& a, int B, void* ws, size_t ws_bytes
                             float* keep_v = nullptr, bool v_ready = false) {
   // the direct fp16x3 kernel (pis_tune key 29) where its policy takes the layer; a kept forward
   // transform is then still owed to the layer's Winograd weight gradient
-  if (ws && !a.filter_ready && !v_ready && a.tap_mode == TAP_CONV3 && a.epi == EPI_NHWC &&
-      direct_h3_wanted(a.H, a.W, a.Csrc, a.N, a.lds) && ws_bytes >= direct_h3_ws_bytes(a.Csrc, a.N)) {
-    int rc = launch_direct_h3(a, B, ws, ws_bytes, s, a.w_unflipped != 0);
+  // (PIS_FILTER_READY here: a.wt is the layer's split from pis_conv3x3_filter(s), format 3)
+  if (ws && !v_ready && a.tap_mode == TAP_CONV3 && a.epi == EPI_NHWC &&
+      direct_h3_wanted(a.H, a.W, a.Csrc, a.N, a.lds) &&
+      (a.filter_ready || ws_bytes >= direct_h3_ws_bytes(a.Csrc, a.N))) {
+    int rc = launch_direct_h3(a, B, ws, ws_bytes, s, a.w_unflipped != 0, a.filter_ready);
     if (!rc && keep_v) rc = launch_wino_input(a.src, a.lds, B, a.H, a.W, a.Csrc, keep_v, s, 4);
     return rc;
   }
@@ -657,8 +659,8 @@ extern "C" int pis_conv3x3_fwd_pool(const float* x, int ldx, const float* w_krsc
   a.filter_ready = (flags & PIS_FILTER_READY) != 0;
   // the direct fp16x3 kernel and the F(4x4,3x3) output epilogues pool the tile they just wrote;
   // every other path pools after
-  if (Cin > 1 && ws && !a.filter_ready && direct_h3_wanted(H, W, Cin, Cout, ldx) &&
-      ws_bytes >= direct_h3_ws_bytes(Cin, Cout)) {
+  if (Cin > 1 && ws && direct_h3_wanted(H, W, Cin, Cout, ldx) &&
+      (a.filter_ready || ws_bytes >= direct_h3_ws_bytes(Cin, Cout))) {
     a.pool = pool;
     return dispatch_conv3x3(a, B, ws, ws_bytes, (hipStream_t)stream, kept ? keep : nullptr);
   }
@@ -726,6 +728,8 @@ int launch_wino4_filter_batch(int n, const float* const* w, void* const* out, co
 // kept forward transforms, prepared 32-aligned input gradients)
 static int filter_format(int B, int H, int W, int Cin, int Cout, int dgrad) {
   if (B <= 0 || H <= 0 || W <= 0 || Cin % 4 || Cout % 4 || Cin < 4) return 0;
+  // 3: the call takes the direct fp16x3 kernel — its "filter transform" is the weight split
+  if (dgrad ? direct_h3_wanted(H, W, Cout, Cin, 4) : direct_h3_wanted(H, W, Cin, Cout, 4)) return 3;
   if (dgrad) {
     if (Cin % 32 || Cout % 32 || !wino_wanted_dims(H, W, Cout, Cin)) return 0;
     return wino_filter_format(B, H, W, Cout, Cin, false);
@@ -739,6 +743,7 @@ extern "C" size_t pis_conv3x3_filter_bytes(int B, int H, int W, int Cin, int Cou
   if (f == 0) return 0;
   const size_t nc = (size_t)36 * Cin * Cout;
   const int C = dgrad ? Cout : Cin, N = dgrad ? Cin : Cout;  // contraction, outputs
+  if (f == 3) return direct_h3_ws_bytes(C, N);
   if (f == 2 && tune_get(PIS_TUNE_WINO_GEMM_OUT_H3) != 0)  // fp16x3: hi / lo planes + one scale per output
     return 2 * nc * sizeof(_Float16) + (size_t)N * sizeof(float);
   return f == 2 ? 3 * nc * sizeof(__bf16) : nc * sizeof(float);
@@ -749,6 +754,11 @@ extern "C" int pis_conv3x3_filter(const float* w, int B, int H, int W, int Cin, 
   const int f = filter_format(B, H, W, Cin, Cout, dgrad);
   PIS_CHECK_ARG(w && out && f != 0, "pis_conv3x3_filter: no F(4x4,3x3) GEMM path for these shapes");
   PIS_CHECK_ARG(out_bytes >= pis_conv3x3_filter_bytes(B, H, W, Cin, Cout, dgrad), "pis_conv3x3_filter: output too small");
+  if (f == 3) {  // the direct kernel's split (input gradient: of the ORIGINAL weights)
+    const int dg = dgrad ? 1 : 0;
+    void* o = out;
+    return launch_direct_wsplit_batch(1, &w, &o, &Cin, &Cout, &dg, (hipStream_t)stream);
+  }
   // forward: contraction C = Cin, outputs N = Cout; input gradient: C = Cout, N = Cin
   return dgrad ? launch_wino4_filter_only(w, Cout, Cin, 1, f, out, (hipStream_t)stream)
                : launch_wino4_filter_only(w, Cin, Cout, 0, f, out, (hipStream_t)stream);
@@ -759,17 +769,31 @@ extern "C" int pis_conv3x3_filters(const pis_filter_job* jobs, int n, pis_stream
   const float* w[PIS_FILTER_MAX_JOBS];
   void* out[PIS_FILTER_MAX_JOBS];
   int C[PIS_FILTER_MAX_JOBS], N[PIS_FILTER_MAX_JOBS], dg[PIS_FILTER_MAX_JOBS], fmt[PIS_FILTER_MAX_JOBS];
+  // the direct kernel's splits (format 3) go to a second launch
+  const float* dw[PIS_FILTER_MAX_JOBS];
+  void* dout[PIS_FILTER_MAX_JOBS];
+  int dci[PIS_FILTER_MAX_JOBS], dco[PIS_FILTER_MAX_JOBS], ddg[PIS_FILTER_MAX_JOBS];
+  int nw = 0, nd = 0;
   for (int k = 0; k < n; ++k) {
     const pis_filter_job& j = jobs[k];
     const int f = filter_format(j.B, j.H, j.W, j.Cin, j.Cout, j.dgrad);
-    PIS_CHECK_ARG(j.w && j.out && f != 0, "pis_conv3x3_filters: a job has no F(4x4,3x3) GEMM path");
+    PIS_CHECK_ARG(j.w && j.out && f != 0, "pis_conv3x3_filters: a job has no filter transform (no F(4x4,3x3) GEMM "
+                                          "or direct path)");
     PIS_CHECK_ARG(j.out_bytes >= pis_conv3x3_filter_bytes(j.B, j.H, j.W, j.Cin, j.Cout, j.dgrad),
                   "pis_conv3x3_filters: a job's output is too small");
-    w[k] = j.w; out[k] = j.out; fmt[k] = f; dg[k] = j.dgrad ? 1 : 0;
-    C[k] = j.dgrad ? j.Cout : j.Cin;  // contraction channels
-    N[k] = j.dgrad ? j.Cin : j.Cout;  // output channels
+    if (f == 3) {
+      dw[nd] = j.w; dout[nd] = j.out; dci[nd] = j.Cin; dco[nd] = j.Cout; ddg[nd] = j.dgrad ? 1 : 0;
+      ++nd;
+      continue;
+    }
+    w[nw] = j.w; out[nw] = j.out; fmt[nw] = f; dg[nw] = j.dgrad ? 1 : 0;
+    C[nw] = j.dgrad ? j.Cout : j.Cin;  // contraction channels
+    N[nw] = j.dgrad ? j.Cin : j.Cout;  // output channels
+    ++nw;
   }
-  return launch_wino4_filter_batch(n, w, out, C, N, dg, fmt, (hipStream_t)stream);
+  int rc = nw ? launch_wino4_filter_batch(nw, w, out, C, N, dg, fmt, (hipStream_t)stream) : PIS_OK;
+  if (!rc && nd) rc = launch_direct_wsplit_batch(nd, dw, dout, dci, dco, ddg, (hipStream_t)stream);
+  return rc;
 }
 
 extern "C" int pis_conv3x3_dgrad(const float* dz, int ldz, const float* w_flip, const float* mask,

@@ -331,6 +331,9 @@ class UNetEngine:
     # main stream at the start of the training forward (pis_conv3x3_filters) instead of 34 small,
     # latency-bound launches: measured neutral at C2 (31.29 vs 31.27 ms). Default 0: each conv
     # transforms its own filter.
+    # PIS_FILTER_AHEAD=3: only the direct fp16x3 layers' weight splits (both directions) in ONE launch
+    # at the forward's start: 12 small main-stream launches fewer, six of them in the backward,
+    # where the weight-gradient stream's kernels hold the CUs they would wait for.
     filter_ahead = os.environ.get("PIS_FILTER_AHEAD", "0")
 
     def __init__(self, model: UNet):
@@ -390,7 +393,9 @@ class UNetEngine:
         self.ws2 = torch.empty_like(self.ws) if self.side_stream else self.ws
         # an owned stream, not one of torch's pooled ones: it takes part in any graph capture of
         # the step (graph.StepGraph), and is destroyed with the engine rather than handed on
-        self._side_owner = _hip.OwnedStream(device=dev) if self.side_stream else None
+        # (PIS_SIDE_CUS=n: the side stream's kernels confined to n CUs — a scheduling experiment)
+        cus = int(os.environ.get("PIS_SIDE_CUS", "0"))
+        self._side_owner = _hip.OwnedStream(device=dev, cus=cus) if self.side_stream else None
         self.side = self._side_owner.stream if self.side_stream else None
         # pis_conv3x3_bwd_prep writes a layer's weight-gradient dz transform from the MAIN stream
         # while the side stream may still read the previous layer's: two alternating workspaces
@@ -422,13 +427,17 @@ class UNetEngine:
         self.bev: Dict[int, Optional[torch.cuda.Event]] = {}  # ... for its backward (None: same stream)
         self.filter_jobs = None
         mode = str(self.filter_ahead)
-        if (mode == "1" and self.side is not None) or mode == "2":
+        if (mode == "1" and self.side is not None) or mode in ("2", "3"):
             for name in BLOCK_ORDER:
                 blk = self.m.block(name)
                 lvl = 5 if name == "bottleneck" else int(name[-1])
                 Hl, Wl = H >> (lvl - 1), W >> (lvl - 1)
                 for conv in (blk.conv0, blk.conv1):
-                    if id(conv) not in self.keep:
+                    if conv.in_channels == 1:
+                        continue
+                    # modes 1/2: the layers whose transform is kept for the weight gradient (the
+                    # Winograd ones); mode 3: the others, i.e. the direct kernel's layers
+                    if (id(conv) in self.keep) != (mode != "3"):
                         continue
                     ci, co = conv.in_channels, conv.out_channels
                     nb = lib.pis_conv3x3_filter_bytes(B, Hl, Wl, ci, co, 0)
@@ -439,7 +448,7 @@ class UNetEngine:
                     if nb and not (name == "enc1" and conv is blk.conv0):  # the first conv has no dgrad
                         self.bfilt[id(conv)] = (conv, Hl, Wl, torch.empty((nb + 3) // 4, dtype=torch.float32,
                                                                           device=dev))
-        if mode == "2" and (self.ffilt or self.bfilt):
+        if mode in ("2", "3") and (self.ffilt or self.bfilt):
             jobs = [(t, 0) for t in self.ffilt.values()] + [(t, 1) for t in self.bfilt.values()]
             arr = (_hip.FilterJob * len(jobs))()
             for k, ((conv, Hl, Wl, buf), dg) in enumerate(jobs):
@@ -504,7 +513,7 @@ class UNetEngine:
         flags = PIS_RELU | (PIS_SCALE if scale is not None else 0)
         keep = self.keep.get(id(conv)) if self._keeping else None
         wptr = conv.weight.data_ptr()
-        if keep is not None and id(conv) in self.fev:
+        if id(conv) in self.fev:  # its filter transform (or direct split), computed ahead
             ev = self.fev.pop(id(conv))
             if ev is not None:
                 torch.cuda.current_stream().wait_event(ev)
@@ -730,6 +739,11 @@ class UNetEngine:
                         wf, flags = self.bfilt[id(conv)][3].data_ptr(), flags | PIS_FILTER_READY
                 elif lib.pis_conv3x3_dgrad_direct(B, Hl, Wl, conv.in_channels, conv.out_channels, dz.ld, wsb):
                     wf, flags = conv.weight.data_ptr(), flags | PIS_W_UNFLIPPED  # the direct kernel splits it
+                    if id(conv) in self.bev:  # ... unless its split was computed ahead
+                        ev = self.bev.pop(id(conv))
+                        if ev is not None:
+                            main.wait_event(ev)
+                        wf, flags = self.bfilt[id(conv)][3].data_ptr(), flags | PIS_FILTER_READY
                 else:
                     wf = flipped(conv).data_ptr()
                 call("pis_conv3x3_dgrad_ex", dz.p, dz.ld, wf,

@@ -3,6 +3,8 @@ src/unet.py:29,38's nn.Conv2d (bias, ReLU, Dropout2d keep-scale, the encoder's f
 pool) and its input gradient (ReLU mask of the conv's input, keep-scale, accumulate; flipped or
 original weights) against float64, as accurate as the native fp32 MFMA direct kernel (key 8 = 0)
 for unit, gradient-sized and large operands and for a region spanning 2^-60 .. 1."""
+import ctypes
+
 import pytest
 import torch
 import torch.nn.functional as F
@@ -273,3 +275,78 @@ def test_train_step_with_direct_convs(hip, loss_kw):
     worst = sorted(((tu.rel(p.grad, q.grad), n) for (n, p), q in zip(net.named_parameters(), ref64.parameters())),
                    reverse=True)
     assert worst[0][0] < 1e-4, worst[:5]
+
+
+@pytest.mark.parametrize("cin,cout", [(64, 64), (64, 128), (128, 64)])
+def test_direct_split_ready_bitwise(hip, cin, cout):
+    """The direct kernel's weight split computed ahead (pis_conv3x3_filter / pis_conv3x3_filters, format 3)
+    and passed with PIS_FILTER_READY gives bitwise the forward (plain and with the fused pool) and the
+    input gradient from the original weights that the calls compute with their own split."""
+    from physics_informed_image_segmentation_amd import _hip
+    B, H, W = 1, 256, 64  # H >= 256, <= 128 channels: the direct layers of the default policy
+    g = torch.Generator().manual_seed(71)
+    x = F.relu(torch.randn(B, H, W, cin, generator=g)).cuda()
+    dz = torch.randn(B, H, W, cout, generator=g).cuda()
+    w = (torch.randn(cout, 3, 3, cin, generator=g) * 0.05).cuda()
+    bias = torch.randn(cout, generator=g).cuda()
+    nws = hip.pis_conv3x3_ex_ws(B, H, W, cin, cout)
+    ws = torch.empty(nws // 4 + 1, device="cuda")
+    splits = {}
+    for dg in (0, 1):
+        nb = hip.pis_conv3x3_filter_bytes(B, H, W, cin, cout, dg)
+        assert nb > 0
+        one = torch.empty(nb // 4 + 1, device="cuda")
+        assert hip.pis_conv3x3_filter(w.data_ptr(), B, H, W, cin, cout, dg, one.data_ptr(), nb, s()) == 0
+        splits[dg] = (one, nb)
+    # the batched form writes the same bytes
+    jobs = (_hip.FilterJob * 2)()
+    bat = {}
+    for dg in (0, 1):
+        nb = splits[dg][1]
+        bat[dg] = torch.empty(nb // 4 + 1, device="cuda")
+        jobs[dg] = _hip.FilterJob(w.data_ptr(), bat[dg].data_ptr(), nb, B, H, W, cin, cout, dg)
+    assert hip.pis_conv3x3_filters(ctypes.addressof(jobs), 2, s()) == 0
+    outs = {}
+    for ready in (False, True):
+        wptr, fl = (splits[0][0].data_ptr(), 64) if ready else (w.data_ptr(), 0)
+        y = torch.empty(B, H, W, cout, device="cuda")
+        assert hip.pis_conv3x3_fwd_ex(x.data_ptr(), cin, wptr, bias.data_ptr(), 0, y.data_ptr(), cout, B, H, W,
+                                      cin, cout, RELU | fl, ws.data_ptr(), nws, s()) == 0, hip.pis_last_error()
+        yp = torch.empty(B, H, W, cout, device="cuda")
+        pl = torch.empty(B, H // 2, W // 2, cout, device="cuda")
+        assert hip.pis_conv3x3_fwd_pool(x.data_ptr(), cin, wptr, bias.data_ptr(), 0, yp.data_ptr(), cout, B, H, W,
+                                        cin, cout, RELU | fl, ws.data_ptr(), nws, 0, pl.data_ptr(), s()) == 0
+        dwp, dfl = (splits[1][0].data_ptr(), 64) if ready else (w.data_ptr(), UNFLIPPED)
+        dx = torch.empty(B, H, W, cin, device="cuda")
+        assert hip.pis_conv3x3_dgrad_ex(dz.data_ptr(), cout, dwp, x.data_ptr(), cin, 0, dx.data_ptr(), cin, B, H, W,
+                                        cin, cout, MASK | dfl, ws.data_ptr(), nws, s()) == 0, hip.pis_last_error()
+        outs[ready] = (y, yp, pl, dx)
+    torch.cuda.synchronize()
+    for dg in (0, 1):
+        nb = splits[dg][1]
+        assert torch.equal(splits[dg][0][:nb // 4], bat[dg][:nb // 4])
+    for a, b in zip(outs[False], outs[True]):
+        assert torch.equal(a, b)
+
+
+def test_engine_direct_splits_ahead_bitwise(hip):
+    """PIS_FILTER_AHEAD=3 (the engine computes every direct layer's weight split, both directions,
+    in one launch at the forward's start and passes PIS_FILTER_READY): one training step gives
+    bitwise the outputs and gradients of the default engine."""
+    import importlib
+    from physics_informed_image_segmentation_amd import unet as U
+    tu = importlib.import_module("test_unet_gpu")
+    res = {}
+    prev = U.UNetEngine.filter_ahead
+    try:
+        for mode in ("0", "3"):
+            U.UNetEngine.filter_ahead = mode
+            with Knobs(hip, k29=2):
+                net, ref, u, crit, p_ref, terms, ref64 = tu._step_pair(1, 64, 64, dict())
+            res[mode] = (u.detach().clone(), [p.grad.detach().clone() for p in net.parameters()])
+            del net, ref, ref64
+    finally:
+        U.UNetEngine.filter_ahead = prev
+    assert torch.equal(res["0"][0], res["3"][0])
+    for a, b in zip(res["0"][1], res["3"][1]):
+        assert torch.equal(a, b)
