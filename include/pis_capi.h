@@ -137,7 +137,11 @@ int pis_version(void);
                                     K-steps, block-wide scales), 0 the column-staged wgrad_h3_kernel */
 #define PIS_TUNE_DIRECT_PIPE 32  /* direct fp16x3 input gradient (key 29): 1 (default) the epilogue's ReLU-mask rows
                                     loaded during the last chunk's MFMAs (enc1.conv1 -12 %), 0 in the epilogue */
-#define PIS_TUNE_NKEYS 33
+#define PIS_TUNE_DIRECT_W8 33    /* retired (round 3): an 8-wave two-stage direct forward / input gradient (16-row tiles,
+                                    one block per CU, next chunk's weights by LDS-DMA and its halo split while this
+                                    chunk multiplies) measured 3-14 % slower than the 4-wave kernel
+                                    (profiles/r3_q26_direct_w8.txt); ignored */
+#define PIS_TUNE_NKEYS 34
 #define PIS_DEBUG_NOLOAD (1 << 16)
 int pis_tune(int key, int value);
 /* Tooling (tools/bench_gemm.py): time one batched NT GEMM kernel variant in isolation,
@@ -170,9 +174,6 @@ int pis_arm_gemm_event(void* event);
  * nodes and allocator blocks). pis_stream_capture_status: hipStreamCaptureStatus (0 none, 1 active,
  * 2 invalidated) or a negative error. */
 int pis_stream_create(int priority, pis_stream_t* out);
-/* pis_stream_create restricted to ncu of the device's CUs (evenly spaced; ncu <= 0: all): a scheduling
- * experiment for the weight-gradient stream (PIS_SIDE_CUS). */
-int pis_stream_create_cus(int priority, int ncu, pis_stream_t* out);
 int pis_stream_destroy(pis_stream_t stream);
 int pis_stream_capture_status(pis_stream_t stream);
 

@@ -43,7 +43,6 @@ _SIGNATURES = {
     "pis_set_launch_hook": ([LAUNCH_HOOK_T, P], None),
     "pis_arm_gemm_event": ([P], c_int),
     "pis_stream_create": ([I, ctypes.POINTER(c_void_p)], c_int),
-    "pis_stream_create_cus": ([I, I, ctypes.POINTER(c_void_p)], c_int),
     "pis_stream_destroy": ([P], c_int),
     "pis_stream_capture_status": ([P], c_int),
     "pis_version": ([], c_int),
@@ -185,18 +184,17 @@ class OwnedStream:
     handles dangling (tests/test_graph_gpu.py::test_graph_dropped_without_close reproduced exactly
     that: a segfault in the next eager backward of the graphed model)."""
 
-    def __init__(self, device=None, priority: int = 0, cus: int = 0):
+    def __init__(self, device=None, priority: int = 0):
         self.handle = None
-        key = (priority, cus)
         for i, (h, p) in enumerate(_free_streams):
-            if p == key:
+            if p == priority:
                 self.handle = _free_streams.pop(i)[0]
                 break
         if self.handle is None:
             raw = c_void_p()
-            check(lib().pis_stream_create_cus(priority, cus, ctypes.byref(raw)), "pis_stream_create_cus")
+            check(lib().pis_stream_create(priority, ctypes.byref(raw)), "pis_stream_create")
             self.handle = raw.value
-        self.priority = key
+        self.priority = priority
         self.stream = torch.cuda.ExternalStream(self.handle, device=device)
 
     def capture_status(self) -> int:

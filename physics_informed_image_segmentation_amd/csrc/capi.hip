@@ -1,6 +1,5 @@
 // Error channel, version and tuning table of the pis_* C-ABI (include/pis_capi.h).
 #include <atomic>
-#include <vector>
 #include <cstdarg>
 
 #include "common.h"
@@ -16,7 +15,7 @@ void set_error(const char* fmt, ...) {
 }
 
 // kernel-variant knobs (defaults = the measured best on MI355X)
-static std::atomic<int> g_tune[PIS_TUNE_NKEYS] = {0, 16, 0, 1, 0, 1, 512, 0, 1, 2048, 4, 1, 0, 4, 3, 1, 1, 2, 1, 1, 1, 0, 1, 0, 0, 0, 2, 1, 0, 1, 0, 1, 1};
+static std::atomic<int> g_tune[PIS_TUNE_NKEYS] = {0, 16, 0, 1, 0, 1, 512, 0, 1, 2048, 4, 1, 0, 4, 3, 1, 1, 2, 1, 1, 1, 0, 1, 0, 0, 0, 2, 1, 0, 1, 0, 1, 1, 0};
 
 int tune_get(int key) { return (key > 0 && key < PIS_TUNE_NKEYS) ? g_tune[key].load() : 0; }
 
@@ -55,29 +54,6 @@ extern "C" int pis_stream_create(int priority, pis_stream_t* out) {
   const hipError_t e = hipStreamCreateWithPriority(&s, hipStreamNonBlocking, priority);
   if (e != hipSuccess) {
     pis::set_error("pis_stream_create: %s", hipGetErrorString(e));
-    return PIS_ERR_LAUNCH;
-  }
-  *out = (pis_stream_t)s;
-  return PIS_OK;
-}
-
-// A stream whose kernels may run only on `ncu` of the device's CUs (evenly spaced mask bits); ncu <= 0
-// or >= the CU count: an ordinary stream. Scheduling experiments (PIS_SIDE_CUS, unet.py).
-extern "C" int pis_stream_create_cus(int priority, int ncu, pis_stream_t* out) {
-  PIS_CHECK_ARG(out != nullptr, "pis_stream_create_cus: out is NULL");
-  int dev = 0, ncus = 0;
-  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-    return pis::set_error("pis_stream_create_cus: no device"), PIS_ERR_LAUNCH;
-  if (ncu <= 0 || ncu >= ncus) return pis_stream_create(priority, out);
-  std::vector<uint32_t> mask((ncus + 31) / 32, 0u);
-  for (int i = 0; i < ncu; ++i) {
-    const int b = (int)((int64_t)i * ncus / ncu);
-    mask[b / 32] |= 1u << (b % 32);
-  }
-  hipStream_t s = nullptr;
-  const hipError_t e = hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data());
-  if (e != hipSuccess) {
-    pis::set_error("pis_stream_create_cus: %s", hipGetErrorString(e));
     return PIS_ERR_LAUNCH;
   }
   *out = (pis_stream_t)s;

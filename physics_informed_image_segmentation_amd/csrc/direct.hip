@@ -121,6 +121,88 @@ __global__ __launch_bounds__(256) void conv3x3_wsplit_batch_kernel(WsplitBatch w
   wsplit_one(j.w, j.Cin, j.Cout, j.dgrad, wp, winv, (int)blockIdx.x - wb.start[k]);
 }
 
+// The direct kernels' epilogue (conv3x3_h3_kernel and the 8-wave form): the wave's rows r0 + 2 wave,
+// + 1 from its accumulators, through its own 8 KB of LDS at E.
+template <bool POOL, bool MPF, int MPR = 2>  // MPR: mask rows prefetched (MPF)
+__device__ __forceinline__ void direct_epilogue(const DirectArgs& g, f32x16 (&acc)[2][2], float s_cur, float* E,
+                                                const f32x4 (&mkp)[2][8], int b, int r0, int c0, int n0, int wave,
+                                                int lane, int tid) {
+  const int li = lane & 31, lh = lane >> 5, ch4 = 4 * (lane & 15);
+  // epilogue: lane (li, lh) holds, for output channel n0 + 32 j + li, image row r0 + 2 wave + i and
+  // column c0 + (reg & 3) + 8 (reg >> 2) + 4 lh (the 32x32x16 C/D map). Each image row goes through
+  // the wave's own 8 KB of LDS ([32 px][64 ch], conflict-free both ways) so that every lane then
+  // finishes 4 consecutive channels of 8 pixels with 16-B accesses: its mask / accumulate loads
+  // are issued together (one memory round trip per row) and a pixel's 64 channels are one 256-B
+  // store.
+  const float inv_s = 1.f / s_cur;  // exact: a power of two
+  if (g.dbg & 4) {
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) t += acc[i][j][r];
+    if (t == 1.2345f) g.y[tid] = t;
+    return;
+  }
+  // float4 phase: lane (l & 15) owns channels n0 + ch4 .. + 3; pixel pair m = (l >> 4) + 4 k of the
+  // row (columns 2m, 2m + 1: the 2x2 pool window's columns stay in one lane)
+  const f32x4 wi4 = *reinterpret_cast<const f32x4*>(g.winv + n0 + ch4);
+  const f32x4 bias4 = g.bias ? *reinterpret_cast<const f32x4*>(g.bias + n0 + ch4) : f32x4{0.f, 0.f, 0.f, 0.f};
+  const f32x4 sc4 = (g.flags & PIS_SCALE) ? *reinterpret_cast<const f32x4*>(g.scale + (size_t)b * g.N + n0 + ch4)
+                                          : f32x4{1.f, 1.f, 1.f, 1.f};
+  f32x4 prow0[4];  // POOL: row 2w's column-pair maxima
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = r0 + 2 * wave + i;
+    const size_t pix0 = ((size_t)b * g.H + row) * g.W + c0;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int reg = 0; reg < 16; ++reg) E[((reg & 3) + 8 * (reg >> 2) + 4 * lh) * 64 + 32 * j + li] = acc[i][j][reg];
+    f32x4 mk[8], old[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const size_t pix = pix0 + 2 * ((lane >> 4) + 4 * (k >> 1)) + (k & 1);
+      if (MPF && i < MPR && (g.flags & PIS_MASK))
+        mk[k] = mkp[i][k];
+      else
+        mk[k] = (g.flags & PIS_MASK) ? *reinterpret_cast<const f32x4*>(g.mask + pix * g.ldm + n0 + ch4)
+                                     : f32x4{1.f, 1.f, 1.f, 1.f};
+      old[k] = (g.flags & PIS_ACCUMULATE) ? *reinterpret_cast<const f32x4*>(g.y + pix * g.ldy + n0 + ch4)
+                                          : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int kp = 0; kp < 4; ++kp) {
+      const int m = (lane >> 4) + 4 * kp;
+      f32x4 v[2];
+#pragma unroll
+      for (int d = 0; d < 2; ++d) {
+        const int k = 2 * kp + d;
+        const f32x4 a = *reinterpret_cast<const f32x4*>(&E[(2 * m + d) * 64 + ch4]);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float t = (a[e] * inv_s) * wi4[e] + bias4[e];
+          if (g.flags & PIS_RELU) t = fmaxf(t, 0.f);
+          if (!(mk[k][e] > 0.f)) t = 0.f;
+          v[d][e] = t * sc4[e] + old[k][e];
+        }
+        *reinterpret_cast<f32x4*>(g.y + (pix0 + 2 * m + d) * g.ldy + n0 + ch4) = v[d];
+      }
+      if constexpr (POOL) {
+        const f32x4 cm = vmax4(v[0], v[1]);
+        if (i == 0) {
+          prow0[kp] = cm;
+        } else {
+          const size_t pp = ((size_t)b * (g.H >> 1) + (r0 >> 1) + wave) * (g.W >> 1) + (c0 >> 1) + m;
+          *reinterpret_cast<f32x4*>(g.pool + pp * g.N + n0 + ch4) = vmax4(prow0[kp], cm);
+        }
+      }
+    }
+  }
+}
+
 // MPF (pis_tune key 32 = 1, default): an input gradient's epilogue ReLU-mask rows are loaded
 // during the last chunk's MFMAs (the last chunk is peeled), in the registers the absent next
 // chunk's loads would use: enc1.conv1 input gradient -12 %, enc2.conv1 -4 % (profiles/r3_q18_*).
@@ -272,81 +354,11 @@ __global__ __launch_bounds__(256, 2) void conv3x3_h3_kernel(DirectArgs g) {
   for (int k = 0; k < nk - 1; ++k) chunk(k, std::false_type{});
   chunk(nk - 1, std::true_type{});
 
-  // epilogue: lane (li, lh) holds, for output channel n0 + 32 j + li, image row r0 + 2 wave + i and
-  // column c0 + (reg & 3) + 8 (reg >> 2) + 4 lh (the 32x32x16 C/D map). Each image row goes through
-  // the wave's own 8 KB of LDS ([32 px][64 ch], conflict-free both ways) so that every lane then
-  // finishes 4 consecutive channels of 8 pixels with 16-B accesses: its mask / accumulate loads
-  // are issued together (one memory round trip per row) and a pixel's 64 channels are one 256-B
-  // store.
-  const float inv_s = 1.f / s_cur;  // exact: a power of two
-  if (g.dbg & 4) {
-    float t = 0.f;
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) t += acc[i][j][r];
-    if (t == 1.2345f) g.y[tid] = t;
-    return;
-  }
-  float* E = reinterpret_cast<float*>(smem) + wave * (32 * 64);  // free since the loop's last barrier
-  // float4 phase: lane (l & 15) owns channels n0 + ch4 .. + 3; pixel pair m = (l >> 4) + 4 k of the
-  // row (columns 2m, 2m + 1: the 2x2 pool window's columns stay in one lane)
-  const f32x4 wi4 = *reinterpret_cast<const f32x4*>(g.winv + n0 + ch4);
-  const f32x4 bias4 = g.bias ? *reinterpret_cast<const f32x4*>(g.bias + n0 + ch4) : f32x4{0.f, 0.f, 0.f, 0.f};
-  const f32x4 sc4 = (g.flags & PIS_SCALE) ? *reinterpret_cast<const f32x4*>(g.scale + (size_t)b * g.N + n0 + ch4)
-                                          : f32x4{1.f, 1.f, 1.f, 1.f};
-  f32x4 prow0[4];  // POOL: row 2w's column-pair maxima
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int row = r0 + 2 * wave + i;
-    const size_t pix0 = ((size_t)b * g.H + row) * g.W + c0;
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int reg = 0; reg < 16; ++reg) E[((reg & 3) + 8 * (reg >> 2) + 4 * lh) * 64 + 32 * j + li] = acc[i][j][reg];
-    f32x4 mk[8], old[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const size_t pix = pix0 + 2 * ((lane >> 4) + 4 * (k >> 1)) + (k & 1);
-      if (MPF && (g.flags & PIS_MASK))
-        mk[k] = mkp[i][k];
-      else
-        mk[k] = (g.flags & PIS_MASK) ? *reinterpret_cast<const f32x4*>(g.mask + pix * g.ldm + n0 + ch4)
-                                     : f32x4{1.f, 1.f, 1.f, 1.f};
-      old[k] = (g.flags & PIS_ACCUMULATE) ? *reinterpret_cast<const f32x4*>(g.y + pix * g.ldy + n0 + ch4)
-                                          : f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-#pragma unroll
-    for (int kp = 0; kp < 4; ++kp) {
-      const int m = (lane >> 4) + 4 * kp;
-      f32x4 v[2];
-#pragma unroll
-      for (int d = 0; d < 2; ++d) {
-        const int k = 2 * kp + d;
-        const f32x4 a = *reinterpret_cast<const f32x4*>(&E[(2 * m + d) * 64 + ch4]);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          float t = (a[e] * inv_s) * wi4[e] + bias4[e];
-          if (g.flags & PIS_RELU) t = fmaxf(t, 0.f);
-          if (!(mk[k][e] > 0.f)) t = 0.f;
-          v[d][e] = t * sc4[e] + old[k][e];
-        }
-        *reinterpret_cast<f32x4*>(g.y + (pix0 + 2 * m + d) * g.ldy + n0 + ch4) = v[d];
-      }
-      if constexpr (POOL) {
-        const f32x4 cm = vmax4(v[0], v[1]);
-        if (i == 0) {
-          prow0[kp] = cm;
-        } else {
-          const size_t pp = ((size_t)b * (g.H >> 1) + (r0 >> 1) + wave) * (g.W >> 1) + (c0 >> 1) + m;
-          *reinterpret_cast<f32x4*>(g.pool + pp * g.N + n0 + ch4) = vmax4(prow0[kp], cm);
-        }
-      }
-    }
-  }
+  // epilogue: the wave's 8 KB of LDS, free since the loop's last barrier
+  direct_epilogue<POOL, MPF>(g, acc, s_cur, reinterpret_cast<float*>(smem) + wave * (32 * 64), mkp, b, r0, c0, n0,
+                             wave, lane, tid);
 }
+
 
 bool direct_h3_shape_ok(int H, int W, int C, int N, int ldx) {
   return H % DT_H == 0 && W % DT_W == 0 && C % DKC == 0 && N % 64 == 0 && ldx % 4 == 0 && C >= DKC;
@@ -421,10 +433,10 @@ int launch_direct_h3(const IGemmArgs& a, int B, void* ws, size_t ws_bytes, hipSt
   g.mask = a.mask; g.ldm = a.ldm; g.y = a.dst; g.ldy = a.ldd; g.pool = a.pool;
   g.B = B; g.H = a.H; g.W = a.W; g.C = C; g.N = N; g.flags = a.flags;
   g.dbg = tune_get(PIS_TUNE_DEBUG_NOLOAD);
-  const int blocks = B * (a.H / DT_H) * (a.W / DT_W) * (N / 64);
   const double flop = 2.0 * 9 * (double)B * a.H * a.W * C * N;
-  launch_hook("direct_h3", 0, s, flop);
   const bool mpf = tune_get(PIS_TUNE_DIRECT_PIPE) != 0 && (a.flags & PIS_MASK);
+  const int blocks = B * (a.H / DT_H) * (a.W / DT_W) * (N / 64);
+  launch_hook("direct_h3", 0, s, flop);
   if (a.pool)  // a forward: no mask
     hipLaunchKernelGGL((conv3x3_h3_kernel<true, false>), dim3(blocks), dim3(256), 0, s, g);
   else if (mpf)

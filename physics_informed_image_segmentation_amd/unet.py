@@ -332,8 +332,8 @@ class UNetEngine:
     # latency-bound launches: measured neutral at C2 (31.29 vs 31.27 ms). Default 0: each conv
     # transforms its own filter.
     # PIS_FILTER_AHEAD=3: only the direct fp16x3 layers' weight splits (both directions) in ONE launch
-    # at the forward's start: 12 small main-stream launches fewer, six of them in the backward,
-    # where the weight-gradient stream's kernels hold the CUs they would wait for.
+    # at the forward's start: 12 small main-stream launches fewer, six of them in the backward.
+    # Measured neutral on the C2 step (344.2 vs 344.0 img/s, profiles/r3_q25_ab_env.txt).
     filter_ahead = os.environ.get("PIS_FILTER_AHEAD", "0")
 
     def __init__(self, model: UNet):
@@ -393,9 +393,9 @@ class UNetEngine:
         self.ws2 = torch.empty_like(self.ws) if self.side_stream else self.ws
         # an owned stream, not one of torch's pooled ones: it takes part in any graph capture of
         # the step (graph.StepGraph), and is destroyed with the engine rather than handed on
-        # (PIS_SIDE_CUS=n: the side stream's kernels confined to n CUs — a scheduling experiment)
-        cus = int(os.environ.get("PIS_SIDE_CUS", "0"))
-        self._side_owner = _hip.OwnedStream(device=dev, cus=cus) if self.side_stream else None
+        # (confining this stream to 64 or 128 CUs with a CU mask measured 16 % slower on the step,
+        # profiles/r3_q25_ab_env.txt: the two streams time-share the whole chip)
+        self._side_owner = _hip.OwnedStream(device=dev) if self.side_stream else None
         self.side = self._side_owner.stream if self.side_stream else None
         # pis_conv3x3_bwd_prep writes a layer's weight-gradient dz transform from the MAIN stream
         # while the side stream may still read the previous layer's: two alternating workspaces

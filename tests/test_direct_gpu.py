@@ -323,8 +323,9 @@ def test_direct_split_ready_bitwise(hip, cin, cout):
         outs[ready] = (y, yp, pl, dx)
     torch.cuda.synchronize()
     for dg in (0, 1):
-        nb = splits[dg][1]
-        assert torch.equal(splits[dg][0][:nb // 4], bat[dg][:nb // 4])
+        C, N = (cout, cin) if dg else (cin, cout)  # contraction, outputs
+        nw = 9 * C * N + N  # floats written: the hi / lo fp16 planes, then 1 / t_n (the rest is padding)
+        assert torch.equal(splits[dg][0][:nw], bat[dg][:nw])
     for a, b in zip(outs[False], outs[True]):
         assert torch.equal(a, b)
 
