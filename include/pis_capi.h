@@ -66,7 +66,8 @@ int pis_version(void);
 #define PIS_TUNE_WINOGRAD 8      /* 3x3 convs: 0 direct only; 1 (default) Winograd for fwd/dgrad (*_ex) with >= 256
                                     contraction and >= 128 output channels, for wgrad with >= 128 in and out;
                                     2 Winograd whenever legal */
-#define PIS_TUNE_WINO_WGRAD_BLOCKS 9 /* target workgroups of the 16 batched Winograd weight-gradient GEMMs */
+#define PIS_TUNE_WINO_WGRAD_BLOCKS 9 /* target workgroups of the batched Winograd weight-gradient GEMMs (default 1024;
+                                        2048 until round 3: the C2 step 0.6 % slower, profiles/r3_q33_ab_wgrad_blocks.txt) */
 #define PIS_TUNE_WINO_TILE 10    /* Winograd batched GEMM: 0 generic igemm, 1 lean NT GEMM 128x256 (N % 256 == 0), 2 lean NT GEMM
                                     128x128|64 on fp32 MFMA, 3 the same at fp32 accuracy on bf16 MFMA ("bf16x6": exact
                                     3-way bf16 split of each operand, the six partial products >= 2^-24), 4 (default)
