@@ -423,10 +423,12 @@ int launch_conv3x3(const IGemmArgs& a, hipStream_t s) {
   return launch_status("conv3x3_halo");
 }
 
-// Cin == 1, Cout == 64, W % 64 == 0: block = one 64-pixel row segment of one image; the 3 x 66
-// input window is staged in LDS once, thread (pixel group pg = t / 16, channel quad t % 16)
-// computes pixels pg + 16 k (k < 4) and every wave stores 4 whole pixels (1 KB) per instruction
-// (no per-pixel index divisions, no redundant x loads).
+// Cin == 1, Cout == 64, W % 64 == 0: block = one 64-pixel segment of R image rows; the
+// (R + 2) x 66 input window is staged in LDS once, thread (pixel group pg = t / 16, channel quad
+// t % 16) computes pixels pg + 16 k (k < 4) of each row and every wave stores 4 whole pixels (1 KB)
+// per instruction (no per-pixel index divisions, no redundant x loads). R rows per block amortise
+// the 36 weight loads per thread (R = 4 when H % 4 == 0).
+template <int R>
 __global__ __launch_bounds__(256) void conv3x3_c1_row_kernel(const float* __restrict__ x, int ldx,
                                                              const float* __restrict__ w,
                                                              const float* __restrict__ bias,
@@ -434,14 +436,14 @@ __global__ __launch_bounds__(256) void conv3x3_c1_row_kernel(const float* __rest
                                                              float* __restrict__ y, int ldy, int H, int W,
                                                              int flags) {
   constexpr int Cout = 64, SEG = 64;
-  __shared__ float xs[3][SEG + 2];
-  const int segs = W / SEG;
+  __shared__ float xs[R + 2][SEG + 2];
+  const int segs = W / SEG, hb = H / R;
   const int bh = blockIdx.x / segs, w0 = (blockIdx.x - bh * segs) * SEG;
-  const int b = bh / H, h = bh - b * H;
+  const int b = bh / hb, h0 = (bh - b * hb) * R;
   const int tid = threadIdx.x;
-  if (tid < 3 * (SEG + 2)) {
-    const int r = tid / (SEG + 2), c = tid - r * (SEG + 2);
-    const int hh = h + r - 1, ww = w0 + c - 1;
+  for (int i = tid; i < (R + 2) * (SEG + 2); i += 256) {
+    const int r = i / (SEG + 2), c = i - r * (SEG + 2);
+    const int hh = h0 + r - 1, ww = w0 + c - 1;
     xs[r][c] = (hh >= 0 && hh < H && ww >= 0 && ww < W) ? x[(((size_t)b * H + hh) * W + ww) * ldx] : 0.f;
   }
   const int c4 = (tid & 15) * 4, pg = tid >> 4;
@@ -456,21 +458,24 @@ __global__ __launch_bounds__(256) void conv3x3_c1_row_kernel(const float* __rest
   if (flags & PIS_SCALE) sc = *reinterpret_cast<const f32x4*>(scale + (size_t)b * Cout + c4);
   __syncthreads();
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const int px = pg + 16 * k;
-    f32x4 acc = b4;
+  for (int rr = 0; rr < R; ++rr) {
 #pragma unroll
-    for (int t = 0; t < 9; ++t) {
-      const float xv = xs[t / 3][px + t % 3];
+    for (int k = 0; k < 4; ++k) {
+      const int px = pg + 16 * k;
+      f32x4 acc = b4;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[j] = fmaf(xv, wt[t][j], acc[j]);
+      for (int t = 0; t < 9; ++t) {
+        const float xv = xs[rr + t / 3][px + t % 3];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[j] = fmaf(xv, wt[t][j], acc[j]);
+      }
+      if (flags & PIS_RELU) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[j] = fmaxf(acc[j], 0.f);
+      }
+      acc *= sc;
+      *reinterpret_cast<f32x4*>(y + (((size_t)b * H + h0 + rr) * W + w0 + px) * ldy + c4) = acc;
     }
-    if (flags & PIS_RELU) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[j] = fmaxf(acc[j], 0.f);
-    }
-    acc *= sc;
-    *reinterpret_cast<f32x4*>(y + (((size_t)b * H + h) * W + w0 + px) * ldy + c4) = acc;
   }
 }
 
@@ -685,8 +690,12 @@ extern "C" int pis_conv3x3_fwd_ex(const float* x, int ldx, const float* w_krsc, 
   hipStream_t s = (hipStream_t)stream;
   PIS_CHECK_ARG(!(flags & PIS_FILTER_READY) || Cin > 1, "pis_conv3x3_fwd: PIS_FILTER_READY with Cin == 1");
   if (Cin == 1 && Cout == 64 && W % 64 == 0) {
-    hipLaunchKernelGGL(conv3x3_c1_row_kernel, dim3((unsigned)(B * H * (W / 64))), dim3(256), 0, s, x, ldx, w_krsc,
-                       bias, scale, y, ldy, H, W, flags);
+    if (H % 4 == 0)
+      hipLaunchKernelGGL(conv3x3_c1_row_kernel<4>, dim3((unsigned)(B * (H / 4) * (W / 64))), dim3(256), 0, s, x, ldx,
+                         w_krsc, bias, scale, y, ldy, H, W, flags);
+    else
+      hipLaunchKernelGGL(conv3x3_c1_row_kernel<1>, dim3((unsigned)(B * H * (W / 64))), dim3(256), 0, s, x, ldx,
+                         w_krsc, bias, scale, y, ldy, H, W, flags);
     return launch_status("conv3x3_c1_row");
   }
   if (Cin == 1) {

@@ -1305,46 +1305,54 @@ __global__ __launch_bounds__(256) void wgrad_c1_kernel(const float* __restrict__
   }
 }
 
-// Cin == 1, Cout == 64, W % 64 == 0: blocks walk 64-pixel row segments (grid-stride, fixed
-// grid so the partial slabs stay few); per segment the 3 x 66 input window is staged in LDS and
-// thread (pixel group t / 16, channel quad t % 16) accumulates pixels pg + 16 k: dz is read with
-// whole-pixel float4 rows (1 KB per wave instruction), no per-pixel index divisions.
+// Cin == 1, Cout == 64, W % 64 == 0: blocks walk segments of R image rows x 64 pixels
+// (grid-stride, fixed grid so the partial slabs stay few); per segment the (R + 2) x 66 input
+// window is staged in LDS and thread (pixel group t / 16, channel quad t % 16) accumulates pixels
+// pg + 16 k of each row: dz is read with whole-pixel float4 rows (1 KB per wave instruction), no
+// per-pixel index divisions; R = 4 (H % 4 == 0) puts 16 dz loads per thread between the barriers.
+template <int R>
 __global__ __launch_bounds__(256) void wgrad_c1_row_kernel(const float* __restrict__ x, int ldx,
                                                            const float* __restrict__ dz, int ldz, int B, int H,
                                                            int W, float* __restrict__ part,
                                                            float* __restrict__ part_b) {
   constexpr int Cout = 64, SEG = 64;
-  __shared__ float xs[3][SEG + 2];
+  __shared__ float xs[R + 2][SEG + 2];
   __shared__ f32x4 red[256][10];
   const int tid = threadIdx.x, c4 = (tid & 15) * 4, pg = tid >> 4;
   f32x4 acc[10];
 #pragma unroll
   for (int k = 0; k < 10; ++k) acc[k] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int segs = W / SEG;
-  const int nseg = B * H * segs;
+  const int segs = W / SEG, hb = H / R;
+  const int nseg = B * hb * segs;
   for (int sg = blockIdx.x; sg < nseg; sg += gridDim.x) {
     const int bh = sg / segs, w0 = (sg - bh * segs) * SEG;
-    const int b = bh / H, h = bh - b * H;
+    const int b = bh / hb, h0 = (bh - b * hb) * R;
     __syncthreads();  // the previous segment's window is no longer read
-    if (tid < 3 * (SEG + 2)) {
-      const int r = tid / (SEG + 2), c = tid - r * (SEG + 2);
-      const int hh = h + r - 1, ww = w0 + c - 1;
+    for (int i = tid; i < (R + 2) * (SEG + 2); i += 256) {
+      const int r = i / (SEG + 2), c = i - r * (SEG + 2);
+      const int hh = h0 + r - 1, ww = w0 + c - 1;
       xs[r][c] = (hh >= 0 && hh < H && ww >= 0 && ww < W) ? x[(((size_t)b * H + hh) * W + ww) * ldx] : 0.f;
     }
     __syncthreads();
-    const float* dzr = dz + (((size_t)b * H + h) * W + w0) * ldz + c4;
+    const float* dzr = dz + (((size_t)b * H + h0) * W + w0) * ldz + c4;
+    f32x4 dv[R][4];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int px = pg + 16 * k;
-      const f32x4 dv = *reinterpret_cast<const f32x4*>(dzr + (size_t)px * ldz);
-      acc[9] += dv;
+    for (int rr = 0; rr < R; ++rr)
 #pragma unroll
-      for (int t = 0; t < 9; ++t) {
-        const float xv = xs[t / 3][px + t % 3];
+      for (int k = 0; k < 4; ++k) dv[rr][k] = *reinterpret_cast<const f32x4*>(dzr + ((size_t)rr * W + pg + 16 * k) * ldz);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[t][j] = fmaf(xv, dv[j], acc[t][j]);
+    for (int rr = 0; rr < R; ++rr)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int px = pg + 16 * k;
+        acc[9] += dv[rr][k];
+#pragma unroll
+        for (int t = 0; t < 9; ++t) {
+          const float xv = xs[rr + t / 3][px + t % 3];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[t][j] = fmaf(xv, dv[rr][k][j], acc[t][j]);
+        }
       }
-    }
   }
 #pragma unroll
   for (int k = 0; k < 10; ++k) red[tid][k] = acc[k];
@@ -1556,8 +1564,11 @@ extern "C" int pis_conv3x3_wgrad(const float* x, int ldx, const float* dz, int l
     float* part = (float*)ws;
     float* part_b = db ? part + (size_t)C1_BLOCKS * 9 * Cout : nullptr;
     const bool row = Cout == 64 && W % 64 == 0 && ldz % 4 == 0;
-    if (row)
-      hipLaunchKernelGGL(wgrad_c1_row_kernel, dim3(C1_BLOCKS), dim3(256), 0, s, x, ldx, dz, ldz, B, H, W, part,
+    if (row && H % 4 == 0)
+      hipLaunchKernelGGL(wgrad_c1_row_kernel<4>, dim3(C1_BLOCKS), dim3(256), 0, s, x, ldx, dz, ldz, B, H, W, part,
+                         part_b);
+    else if (row)
+      hipLaunchKernelGGL(wgrad_c1_row_kernel<1>, dim3(C1_BLOCKS), dim3(256), 0, s, x, ldx, dz, ldz, B, H, W, part,
                          part_b);
     else
       hipLaunchKernelGGL(wgrad_c1_kernel, dim3(blocks), dim3(256), 0, s, x, ldx, dz, ldz, B, H, W, Cout, ppb,
