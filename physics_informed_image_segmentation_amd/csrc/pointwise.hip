@@ -106,6 +106,44 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(const float* __restrict__
   }
 }
 
+// head fwd for C == 64 (the U-Net's head): the same 16-lane pixel groups, each taking PP pixels
+// G groups apart (G = the grid's group count) with all PP float4 loads issued before the sums —
+// PP x the bytes in flight of head_fwd_kernel's one load per thread; per pixel the same
+// fixed-order sum, so z and u are bitwise those of head_fwd_kernel
+template <int PP>
+__global__ __launch_bounds__(256) void head_fwd64_kernel(const float* __restrict__ x, int ldx,
+                                                         const float* __restrict__ w,
+                                                         const float* __restrict__ b,
+                                                         float* __restrict__ z, float* __restrict__ u,
+                                                         int64_t npix) {
+  const int sub = threadIdx.x & 15;
+  const int64_t q = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 4;
+  const int64_t G = ((int64_t)gridDim.x * blockDim.x) >> 4;
+  const f32x4 wv = *reinterpret_cast<const f32x4*>(w + 4 * sub);
+  f32x4 xv[PP];
+#pragma unroll
+  for (int k = 0; k < PP; ++k) {
+    const int64_t p = q + k * G;
+    xv[k] = p < npix ? *reinterpret_cast<const f32x4*>(x + p * ldx + 4 * sub) : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+#pragma unroll
+  for (int k = 0; k < PP; ++k) {
+    const int64_t p = q + k * G;
+    float s = 0.f;
+    s = fmaf(xv[k][0], wv[0], s);
+    s = fmaf(xv[k][1], wv[1], s);
+    s = fmaf(xv[k][2], wv[2], s);
+    s = fmaf(xv[k][3], wv[3], s);
+#pragma unroll
+    for (int off = 8; off > 0; off >>= 1) s += __shfl_xor(s, off, 16);
+    if (p < npix && sub == 0) {
+      const float zz = s + b[0];
+      if (z) z[p] = zz;
+      u[p] = 1.f / (1.f + expf(-zz));
+    }
+  }
+}
+
 // head bwd: d = g u (1-u) (or g); dx[p][c] = d w[c] (x[p][c] > 0); per-block partial dw[c], db
 __global__ __launch_bounds__(256) void head_bwd_kernel(const float* __restrict__ x, int ldx,
                                                        const float* __restrict__ w,
@@ -258,6 +296,11 @@ extern "C" int pis_head_fwd(const float* x, int ldx, const float* w, const float
                             float* u, int64_t npix, int C, pis_stream_t stream) {
   PIS_CHECK_ARG(x && w && b && u && npix > 0 && C > 0 && C % 4 == 0 && ldx % 4 == 0,
                 "pis_head_fwd: bad arguments");
+  if (C == 64) {  // 4 pixels per 16-lane group
+    hipLaunchKernelGGL(head_fwd64_kernel<4>, dim3((unsigned)cdiv(cdiv(npix, 4) * 16, 256)), dim3(256), 0,
+                       (hipStream_t)stream, x, ldx, w, b, z, u, npix);
+    return launch_status("head_fwd");
+  }
   hipLaunchKernelGGL(head_fwd_kernel, dim3((unsigned)cdiv(npix * 16, 256)), dim3(256), 0,
                      (hipStream_t)stream, x, ldx, w, b, z, u, npix, C);
   return launch_status("head_fwd");

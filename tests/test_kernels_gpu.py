@@ -1139,3 +1139,22 @@ def test_batched_filter_transforms_match_single(hip):
     torch.cuda.synchronize()
     for w, one, bat, nb in keep:
         assert torch.equal(one[:nb // 4], bat[:nb // 4])
+
+
+@pytest.mark.parametrize("npix,C", [(35, 64), (1, 64), (4099, 64), (35, 32)])
+def test_head_fwd_ragged(hip, npix, C):
+    """pis_head_fwd on pixel counts that are not a multiple of the 4 pixels per lane group of the
+    C == 64 kernel (and the generic path, C == 32): z = x . w + b and u = sigmoid(z)."""
+    g = torch.Generator().manual_seed(9)
+    x = torch.randn(npix, C, generator=g)
+    w = torch.randn(C, generator=g)
+    b = torch.randn(1, generator=g)
+    zd = torch.empty(npix, device="cuda")
+    ud = torch.empty(npix, device="cuda")
+    xd, wd, bd = x.cuda(), w.cuda(), b.cuda()
+    assert hip.pis_head_fwd(xd.data_ptr(), C, wd.data_ptr(), bd.data_ptr(), zd.data_ptr(), ud.data_ptr(),
+                            npix, C, s()) == 0
+    torch.cuda.synchronize()
+    z = x.double() @ w.double() + b.double()
+    assert rel_err(zd.cpu().double(), z) < 1e-6
+    assert rel_err(ud.cpu().double(), torch.sigmoid(z)) < 1e-6
