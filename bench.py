@@ -128,18 +128,70 @@ def fused_bytes(T: int, C: int, N: int, dgrad: int) -> float:
     return 4.0 * (36 * T * C + 36 * N * C + 16 * T * N * (2 if dgrad else 1))
 
 
-def pmc_bytes(substr: str):
-    """Launch-weighted HBM bytes per launch of the kernels whose name contains substr, from the
-    committed rocprofv3 --pmc summary (profiles/pmc_dominant.json), or None."""
+def pmc_bytes(substr):
+    """Launch-weighted HBM bytes per launch of the kernels whose name contains substr (or any of
+    a list of substrings), from the committed rocprofv3 --pmc summary (profiles/pmc_dominant.json),
+    or None."""
     path = os.path.join(HERE, "profiles", "pmc_dominant.json")
     if not os.path.exists(path):
         return None
     with open(path) as f:
         ks = json.load(f).get("kernels", {})
+    subs = [substr] if isinstance(substr, str) else list(substr)
     sel = [(v["hbm_bytes_per_launch"], v["launches"]) for k, v in ks.items()
-           if substr in k and "hbm_bytes_per_launch" in v]
+           if any(x in k for x in subs) and "hbm_bytes_per_launch" in v]
     n = sum(c for _, c in sel)
     return sum(b * c for b, c in sel) / n if n else None
+
+
+def direct_layers(H: int, W: int, c: int = 64):
+    """(name, h, w, Cin, Cout, pooled forward, masked input gradient, has an input gradient) of the
+    3x3 convs the direct fp16x3 kernels take (csrc/direct.hip direct_h3_wanted, pis_tune key 29 as
+    set now); the engine's schedule (unet.py): encoder conv1 forwards are pooled, the input
+    gradients of conv1 layers carry the ReLU mask of their input, conv0 ones do not."""
+    from physics_informed_image_segmentation_amd import _hip
+    mode = _hip.lib().pis_tune(29, -1)
+
+    def wanted(h, w, ci, co):
+        if mode == 0 or ci < 16 or h % 8 or w % 32 or ci % 16 or co % 64:
+            return False
+        lo, hi = min(ci, co), max(ci, co)
+        if mode == 3:
+            return (h >= 256 and hi <= 256) or (h >= 128 and hi <= 256 and lo <= 128)
+        if mode == 4:
+            return h >= 128 and hi <= 256
+        if mode == 5:
+            return h >= 128
+        return mode == 2 or (hi <= 128 and h >= 256)
+
+    convs = []
+    for l in range(1, 5):
+        cl, hl, wl = c << (l - 1), H >> (l - 1), W >> (l - 1)
+        cin0 = 1 if l == 1 else cl // 2
+        convs += [(f"enc{l}.conv0", hl, wl, cin0, cl, False, False, l > 1),
+                  (f"enc{l}.conv1", hl, wl, cl, cl, True, True, True),
+                  (f"dec{l}.conv0", hl, wl, 2 * cl, cl, False, False, True),
+                  (f"dec{l}.conv1", hl, wl, cl, cl, False, True, True)]
+    convs += [("bottleneck.conv0", H >> 4, W >> 4, 8 * c, 8 * c, False, False, True),
+              ("bottleneck.conv1", H >> 4, W >> 4, 8 * c, 8 * c, False, True, True)]
+    return [cv for cv in convs if wanted(cv[1], cv[2], cv[3], cv[4])]
+
+
+def direct_role_launches(H: int, W: int, B: int):
+    """{hook label: [(FLOP, algorithmic HBM bytes)] per launch} of the direct kernels in one step.
+    Bytes: forward x read + y written (+ the pooled copy); input gradient dz read + dx written
+    (+ the ReLU mask of the conv's input); weight gradient x + dz read + dW written once (the
+    split-K slabs are implementation traffic, visible in the PMC figure, not algorithmic)."""
+    out = {"direct_h3_fwd": [], "direct_h3_pool": [], "direct_h3_dgrad": [], "direct_wgrad_h3": []}
+    for _, h, w, ci, co, pool, mask, dg in direct_layers(H, W):
+        P = B * h * w
+        fl = 2.0 * 9 * P * ci * co
+        out["direct_h3_pool" if pool else "direct_h3_fwd"].append(
+            (fl, 4.0 * P * (ci + co) + (4.0 * P / 4 * co if pool else 0.0)))
+        if dg:
+            out["direct_h3_dgrad"].append((fl, 4.0 * P * (co + ci) + (4.0 * P * ci if mask else 0.0)))
+        out["direct_wgrad_h3"].append((fl, 4.0 * P * (ci + co) + 4.0 * 9 * ci * co))
+    return out
 
 
 def fused_wanted(T: int, C: int, N: int) -> bool:
@@ -182,7 +234,25 @@ def loss_call_bytes(name, a):
     if name == "pis_head_loss_bwd":
         B, H, W, C = a[6:10]
         return (8.0 * C + 12.0) * B * H * W
+    if name == "pis_head_loss_fwd":  # the call: kernel + its one-block finalize launch
+        B, H, W, C = a[7:11]
+        return (4.0 * C + 12.0) * B * H * W
     return None
+
+
+# direct-kernel roles: launch-hook label -> (bench key, description, rocprofv3 symbols)
+DIRECT_ROLES = {
+    "direct_h3_fwd": ("roofline_direct_fwd", "conv3x3_h3_kernel<false, false, false, false> (forward, 8 x 32 px x "
+                      "64 ch per block)", ["conv3x3_h3_kernel<false, false, false, false>"]),
+    "direct_h3_pool": ("roofline_direct_pool", "conv3x3_h3_kernel<true, false, false, false> (encoder conv1 forward "
+                       "with the 2x2 max pool in the epilogue)", ["conv3x3_h3_kernel<true, false, false, false>"]),
+    "direct_h3_dgrad": ("roofline_direct_dgrad", "conv3x3_h3_kernel<false, true|false, false, true> (input gradient "
+                        "on the original weights; the ReLU-mask rows prefetched where masked)",
+                        ["conv3x3_h3_kernel<false, true, false, true>", "conv3x3_h3_kernel<false, false, false, true>"]),
+    "direct_wgrad_h3": ("roofline_direct_wgrad", "conv3x3_wgrad_strip_kernel (weight gradient: 2-row tiles walked "
+                        "down column strips, split-K slabs; pis_tune key 34 = 0: the 4-row conv3x3_wgrad_h3_kernel)",
+                        ["conv3x3_wgrad_strip_kernel", "conv3x3_wgrad_h3_kernel"]),
+}
 
 
 class KernelTimer:
@@ -244,8 +314,8 @@ class LossCallTimer:
 
 
 # kernels whose MFMA-busy fraction the bench line quotes: the GEMM-shaped ones and the fused loss
-BUSY_REPORTED = ("gemm_nt", "wgrad_x6", "wgrad_h3", "wino4_gemm_out", "convt_gemm", "conv3x3_h3", "conv3x3_wgrad_h3",
-                 "loss_fwd", "head_loss_bwd", "loss_bwd")
+BUSY_REPORTED = ("gemm_nt", "wgrad_x6", "wgrad_h3", "wino4_gemm_out", "convt_gemm", "convt_h3", "conv3x3_h3",
+                 "conv3x3_wgrad", "loss_fwd", "head_loss", "loss_bwd")
 
 
 def load_pmc(kernel=DOMINANT_KERNEL):
@@ -475,7 +545,9 @@ def main():
 
     def step():
         opt.zero_grad()
-        loss = crit(model(x), t)
+        # u = model(x); loss = crit(u, t) with the head and the loss forward in one kernel
+        # (UNet.forward_with_loss: pis_head_loss_fwd), as train_epoch runs it
+        _, loss = model.forward_with_loss(x, t, crit)
         loss.backward()
         opt.step()
         return loss
@@ -491,8 +563,9 @@ def main():
     # fused-loss C-ABI calls (host-side enqueue only; the GPU stays the bottleneck)
     from physics_informed_image_segmentation_amd import _hip
     ktimer, ftimer, ltimer = KernelTimer(), KernelTimer("wino_gemm_out"), LossCallTimer()
-    dtimer, wtimer = KernelTimer("direct_h3"), KernelTimer("direct_wgrad_h3")
-    _hip.set_launch_hook(lambda *a: (ktimer(*a), ftimer(*a), dtimer(*a), wtimer(*a)))
+    htimer = KernelTimer("head_loss_fwd")  # its hook "flop" carries the launch's algorithmic bytes
+    dtimers = {k: KernelTimer(k) for k in DIRECT_ROLES}
+    _hip.set_launch_hook(lambda *a: (ktimer(*a), ftimer(*a), htimer(*a), *(tm(*a) for tm in dtimers.values())))
     _hip.set_tracer(ltimer)
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -515,22 +588,23 @@ def main():
     n_launch //= args.steps
     nf_launch, f_flop, f_ms = ftimer.summary()
     nf_launch //= args.steps
-    direct_live = {k: tm.summary() for k, tm in (("direct_h3", dtimer), ("direct_wgrad_h3", wtimer))}
+    direct_live = {k: tm.summary() for k, tm in dtimers.items()}
     loss_t = ltimer.summary()
+    nh_launch, h_bytes, h_ms = htimer.summary()
     achieved = flop_per_launch / (ms_per_launch * 1e-3) / 1e12
     # the same kernel with the weight gradients serialised on one stream (no concurrent
     # kernel sharing the CUs): one extra instrumented step after the timed region
     eng = model.engine()
     side, eng.side = eng.side, None
     iso, fiso = KernelTimer(), KernelTimer("wino_gemm_out")
-    diso, wiso = KernelTimer("direct_h3"), KernelTimer("direct_wgrad_h3")
-    _hip.set_launch_hook(lambda *a: (iso(*a), fiso(*a), diso(*a), wiso(*a)))
+    disos = {k: KernelTimer(k) for k in DIRECT_ROLES}
+    _hip.set_launch_hook(lambda *a: (iso(*a), fiso(*a), *(tm(*a) for tm in disos.values())))
     step()
     _hip.set_launch_hook(None)
     eng.side = side
     _, iso_flop, iso_ms = iso.summary()
     _, _, fiso_ms = fiso.summary()
-    direct_iso = {"direct_h3": diso.summary(), "direct_wgrad_h3": wiso.summary()}
+    direct_iso = {k: tm.summary() for k, tm in disos.items()}
     # the pipe the dominant kernel runs on. fp32-class GEMMs on the MFMA pipe: fp16x3 (pis_tune
     # key 10 = 4, the default: per-K-step power-of-two tile scales, hi + lo fp16 split, three
     # fp16 MFMAs per fp32 multiply-add) peaks at the dense fp16 MFMA rate (~2.5 PFLOP/s,
@@ -582,31 +656,35 @@ def main():
             "measured": "live over the timed steps",
             "isolated": {"frac": fb / (fiso_ms * 1e-3) / 8e12 if fiso_ms else None, "avg_launch_ms": fiso_ms,
                          "measured": "one extra step, weight gradients serialised"}}
-    # the direct fp16x3 3x3 convolutions (csrc/direct.hip, the shallow layers): MFMA-bound, priced
-    # in fp32-equivalent FLOPs (2 x 9 x pixels x C x N per launch) against the fp16x3 pipe
+    # the direct fp16x3 3x3 convolutions (csrc/direct.hip, the shallow layers), one roofline per
+    # role — and per kernel symbol (forward, pooled forward, input gradient, weight gradient):
+    # MFMA-bound, priced in fp32-equivalent FLOPs (2 x 9 x pixels x C x N per launch) against the
+    # fp16x3 pipe, with the algorithmic HBM bytes per launch beside the PMC traffic of the same symbols
     h3_peak = 2500.0 / 3.0
     direct_roofs = {}
-    for key, name, kern in (("direct_h3", "roofline_direct", "conv3x3_h3_kernel<POOL> (forward with the fused max "
-                                                                "pool / input gradient, 8 x 32 px x 64 ch per block)"),
-                            ("direct_wgrad_h3", "roofline_direct_wgrad", "conv3x3_wgrad_h3_kernel (weight gradient, "
-                                                                         "split-K slabs)")):
+    role_launches = direct_role_launches(H, W, B)
+    for key, (name, kern, syms) in DIRECT_ROLES.items():
         n_d, fl_d, ms_d = direct_live[key]
         if not n_d:
             continue
         n_d //= args.steps
         _, ifl_d, ims_d = direct_iso[key]
-        stem = "conv3x3_h3_kernel" if key == "direct_h3" else "conv3x3_wgrad_h3_kernel"
         busy = None
         if busy_by_kernel is not None:
-            hits = [v for k, v in busy_by_kernel.items() if stem in k]
+            hits = [v for k, v in busy_by_kernel.items() if any(x in k for x in syms)]
             busy = sum(hits) / len(hits) if hits else None
+        lay = role_launches.get(key, [])
+        alg = (sum(b for _, b in lay) / len(lay)
+               if len(lay) == n_d and abs(sum(f for f, _ in lay) / len(lay) - fl_d) <= 1e-6 * fl_d else None)
         direct_roofs[name] = {
             "bound": "mfma", "kernel": kern, "achieved": fl_d / (ms_d * 1e-3) / 1e12, "peak": h3_peak,
-            "unit": "TFLOP/s", "frac": fl_d / (ms_d * 1e-3) / 1e12 / h3_peak, "traffic": pmc_bytes(stem),
+            "unit": "TFLOP/s", "frac": fl_d / (ms_d * 1e-3) / 1e12 / h3_peak, "traffic": pmc_bytes(syms),
+            "traffic_symbols": syms,
             "pipe": "fp16 MFMA, fp32-class fp16x3 split (3 fp16 products per fp32 multiply-add); fp32-equivalent "
                     "FLOPs of the direct convolution",
             "mfma_busy_frac": busy, "launches_per_step": n_d, "avg_launch_ms": ms_d, "flop_per_launch": fl_d,
-            "ms_per_step": n_d * ms_d, "algorithmic_bytes_per_launch": None,
+            "ms_per_step": n_d * ms_d, "algorithmic_bytes_per_launch": alg,
+            "hbm_frac": alg / (ms_d * 1e-3) / 8e12 if alg else None,
             "measured": "live over the timed steps (HIP events on the launch stream)",
             "isolated": {"achieved": ifl_d / (ims_d * 1e-3) / 1e12 if ims_d else None,
                          "frac": ifl_d / (ims_d * 1e-3) / 1e12 / h3_peak if ims_d else None, "avg_launch_ms": ims_d,
@@ -619,7 +697,7 @@ def main():
                        else f"training images/sec ({H}x{W}, {args.config})"),
             "value": imgs_per_s, "unit": "images/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "fp32 (fp16x3/bf16x6 split MFMA; direct + Winograd convs)", "data": "synthetic",
+            "vs_baseline": None, "dtype": "fp32 (fp16x3 split MFMA, power-of-two block scales; direct + Winograd convs)", "data": "synthetic",
             "config": {"workload": workload,
                        "global_batch": B * world, "image_size": [H, W], "parallelism": f"dp{world}"},
             "roofline": None,
@@ -656,7 +734,17 @@ def main():
                     "measured": ("live over the timed steps (Infinity-Cache warm)" if name == "pis_loss_fwd" else
                                  "live; the loss backward fused into the head backward: bytes are dominated "
                                  "by the 64-channel head input and its gradient, not by the loss")}
-                for name, (t, nb, gbs) in loss_t.items()}, **loss_cold),
+                for name, (t, nb, gbs) in loss_t.items()}, **loss_cold,
+                **({"head_loss_fwd_kernel_live": {
+                    "bound": "hbm", "achieved": h_bytes / (h_ms * 1e-3) / 1e9, "peak": 8000.0, "unit": "GB/s",
+                    "frac": h_bytes / (h_ms * 1e-3) / 8e12, "bytes_per_launch": h_bytes, "avg_launch_ms": h_ms,
+                    "launches_per_step": nh_launch // args.steps, "traffic": pmc_bytes("head_loss_fwd_kernel"),
+                    "kernel": "head_loss_fwd_kernel (the U-Net head's 1x1 conv + sigmoid fused with the whole loss "
+                              "forward: Dice / BCE / RD / PF partials and the per-sample counters)",
+                    "bytes": "head input read (4 C B/px) + targets read (4 B/px) + z and u written (8 B/px); the "
+                             "two halo rows per band re-read from L2 / MALL are not algorithmic",
+                    "measured": "live over the timed steps (HIP events on the launch stream, kernel only; its "
+                                "one-block finalize launch follows)"}} if nh_launch else {})),
             "final_loss": float(loss.item()),
         }
         # the dominant kernel (most GPU time per step) carries the contract's "roofline"; the

@@ -142,7 +142,14 @@ int pis_version(void);
                                     one block per CU, next chunk's weights by LDS-DMA and its halo split while this
                                     chunk multiplies) measured 3-14 % slower than the 4-wave kernel
                                     (profiles/r3_q26_direct_w8.txt); ignored */
-#define PIS_TUNE_NKEYS 34
+#define PIS_TUNE_DIRECT_WSTRIP 34 /* direct fp16x3 weight gradient (key 29): 1 (default) 2-row tiles walked down a
+                                    column strip per block (x halo rows re-read from L2, <= 256 registers per lane,
+                                    51 KB LDS: two blocks per CU, or one beside a main-stream block), 0 the round-3
+                                    4-row kernel (497 registers, one wave fills a SIMD) */
+#define PIS_TUNE_DIRECT_WBLOCKS 35 /* target workgroups of the strip weight gradient (key 34 = 1): default 512 (two per
+                                      CU); the split count is this / (Cout/64 * Cin/64), a multiple of 8 */
+#define PIS_TUNE_HEAD_LOSS_ROWS 36 /* pis_head_loss_fwd: image rows per block (0, default: 8192 / W, at most 16) */
+#define PIS_TUNE_NKEYS 37
 #define PIS_DEBUG_NOLOAD (1 << 16)
 int pis_tune(int key, int value);
 /* Tooling (tools/bench_gemm.py): time one batched NT GEMM kernel variant in isolation,
@@ -175,13 +182,16 @@ int pis_arm_gemm_event(void* event);
  * nodes and allocator blocks). pis_stream_capture_status: hipStreamCaptureStatus (0 none, 1 active,
  * 2 invalidated) or a negative error. */
 int pis_stream_create(int priority, pis_stream_t* out);
+/* pis_stream_destroy: for hosts that own their streams' lifetime; the Python host never calls it (its
+ * owned streams are recycled, never destroyed: PyTorch keeps raw stream handles beyond their users). */
 int pis_stream_destroy(pis_stream_t stream);
 int pis_stream_capture_status(pis_stream_t stream);
 
 /* Profiling hook: called on the launching thread right before (phase 0) and after (phase 1)
- * the enqueue of each heavy kernel ("conv3x3_halo", "wino_gemm", "wgrad3x3_halo",
- * "wino_wgrad_gemm"), with its stream and the MFMA FLOPs it executes, so a profiler can
- * record HIP events on that stream around exactly that kernel. NULL removes it. */
+ * the enqueue of each heavy kernel ("conv3x3_halo", "wino_gemm", "wino_gemm_out", "wgrad3x3_halo",
+ * "wino_wgrad_gemm", "direct_h3_fwd", "direct_h3_pool", "direct_h3_dgrad", "direct_wgrad_h3"), with
+ * its stream and the MFMA FLOPs it executes ("head_loss_fwd": its algorithmic HBM bytes instead), so
+ * a profiler can record HIP events on that stream around exactly that kernel. NULL removes it. */
 typedef void (*pis_launch_hook_t)(const char* kernel, int phase, pis_stream_t stream, double flop,
                                   void* user);
 void pis_set_launch_hook(pis_launch_hook_t fn, void* user);
@@ -192,9 +202,12 @@ void pis_set_launch_hook(pis_launch_hook_t fn, void* user);
 int pis_conv3x3_fwd(const float* x, int ldx, const float* w_krsc, const float* bias,
                     const float* scale, float* y, int ldy, int B, int H, int W, int Cin,
                     int Cout, int flags, pis_stream_t stream);
-/* Same contraction as pis_conv3x3_fwd / pis_conv3x3_dgrad, with a workspace that admits the
- * Winograd F(2x2,3x3) path for channel-heavy layers (2.25x fewer MFMA FLOPs: weight, input and
- * output transforms around 16 batched GEMMs). ws may be NULL (direct path). */
+/* Same contraction as pis_conv3x3_fwd / pis_conv3x3_dgrad, with a workspace that admits the fast
+ * paths: the direct fp16x3 kernel (csrc/direct.hip) on the shallow layers (<= 128 channels both
+ * sides, H >= 256; pis_tune key 29), else Winograd F(4x4,3x3) (4x fewer MFMA FLOPs: filter, input
+ * and output transforms around 36 batched fp16x3 GEMMs, or the fused contraction + output transform
+ * for 64 / 128-channel contractions; F(2x2,3x3) only behind pis_tune(11, 0) or for grids not
+ * divisible by 4). ws may be NULL (the fp32-MFMA halo / implicit-GEMM kernels). */
 size_t pis_conv3x3_ex_ws(int B, int H, int W, int Cin, int Cout);
 int pis_conv3x3_fwd_ex(const float* x, int ldx, const float* w_krsc, const float* bias,
                        const float* scale, float* y, int ldy, int B, int H, int W, int Cin, int Cout,
@@ -350,6 +363,17 @@ int pis_loss_bwd(const float* p, const float* t, int B, int H, int W, const pis_
  * dx = dz w (x > 0), dw = sum dz x, db = sum dz as pis_head_bwd. du_out (may be NULL) receives
  * dL/du, i.e. what pis_loss_bwd writes.
  * W <= 1024. flags: PIS_ACCUMULATE (dw, db). */
+/* The U-Net head (1x1 conv C -> 1 + sigmoid, src/unet.py:206-210) fused with pis_loss_fwd (replaces the
+ * criterion call after model(x), src/train.py:108-110 / src/loss.py:130-160): from the head input x
+ * ([B*H*W][ldx], C == 64) writes z (logits) and u = sigmoid(z) (B*H*W each, bitwise those of
+ * pis_head_fwd) and every loss term / counter / score exactly as pis_loss_fwd(u, t) would; one pass
+ * over x. Applicable when pis_head_loss_fwd_ok(B, H, W, C) (C == 64, W % 64 == 0, W <= 2048); else
+ * use pis_head_fwd + pis_loss_fwd. Workspace pis_head_loss_fwd_ws(B, H, W) bytes. */
+size_t pis_head_loss_fwd_ws(int B, int H, int W);
+int pis_head_loss_fwd_ok(int B, int H, int W, int C);
+int pis_head_loss_fwd(const float* x, int ldx, const float* w, const float* bias, const float* t, float* z,
+                      float* u, int B, int H, int W, int C, const pis_loss_params* prm, float* out_terms,
+                      int* counts, float* scores, void* ws, size_t ws_bytes, pis_stream_t stream);
 size_t pis_head_loss_bwd_ws(int B, int H, int W, int C);
 int pis_head_loss_bwd(const float* x, int ldx, const float* w, const float* u, const float* t,
                       float* du_out, int B, int H, int W, int C, const pis_loss_params* prm,

@@ -208,6 +208,29 @@ def decision_flips(decisions, record, drop_scales=None) -> Dict[str, Tuple[int, 
     return out
 
 
+def near_ties(record, tol: float = 1e-5, drop_scales=None) -> Dict[str, int]:
+    """Per decision site, how many decisions of THIS oracle's record are near-ties: ReLU
+    pre-activations with |value| <= tol * the site's max |value|, and 2x2 pool windows whose two
+    largest elements are within tol * that max (channels a Dropout2d keep-scale zeroes carry no
+    decision). The decisions a run with fp32-class rounding may take differently are among them."""
+    out = {}
+    drop_scales = drop_scales or {}
+    for name, ref in record.items():
+        scale = ref.abs().max().clamp_min(1e-30)
+        if name.startswith("pool"):
+            B, C, H, W = ref.shape
+            win = ref.reshape(B, C, H // 2, 2, W // 2, 2).permute(0, 1, 2, 4, 3, 5).reshape(B, C, H // 2, W // 2, 4)
+            top2 = win.topk(2, dim=-1).values
+            near = (top2[..., 0] - top2[..., 1]) <= tol * scale
+        else:
+            near = ref.abs() <= tol * scale
+            blk = name.rsplit(".", 1)[0]
+            if name.endswith(".0") and blk in drop_scales:
+                near &= (drop_scales[blk] != 0)[:, :, None, None]
+        out[name] = int(near.sum())
+    return out
+
+
 def make_drop_scales(m: UNetRef, B: int, generator: torch.Generator) -> Dict[str, torch.Tensor]:
     """Dropout2d keep-scales per block: bernoulli(1-p)/(1-p) of shape (B, C)
     (same draw ATen's feature_dropout makes: noise (B,C,1,1).bernoulli_(1-p).div_(1-p))."""

@@ -80,6 +80,9 @@ _SIGNATURES = {
     "pis_loss_ws": ([I, I, I], c_size_t),
     "pis_loss_fwd": ([P, P, I, I, I, ctypes.POINTER(LossParams), P, P, P, P, Z, P], c_int),
     "pis_loss_bwd": ([P, P, I, I, I, ctypes.POINTER(LossParams), P, P, P, I, P], c_int),
+    "pis_head_loss_fwd_ws": ([I, I, I], c_size_t),
+    "pis_head_loss_fwd_ok": ([I, I, I, I], c_int),
+    "pis_head_loss_fwd": ([P, I, P, P, P, P, P, I, I, I, I, ctypes.POINTER(LossParams), P, P, P, P, Z, P], c_int),
     "pis_head_loss_bwd_ws": ([I, I, I, I], c_size_t),
     "pis_head_loss_bwd": ([P, I, P, P, P, P, I, I, I, I, ctypes.POINTER(LossParams), P, P, P, I, P, P, I, P, Z,
                            P], c_int),
@@ -169,40 +172,76 @@ def call(name: str, *args) -> None:
     tr.end(tok)
 
 
-_free_streams = []  # owned streams no longer in use: handed to the next OwnedStream, never destroyed
+# owned streams no longer in use, keyed by (device index, priority): handed to the next OwnedStream
+# of the same device and priority, never destroyed
+_free_streams = {}
+# streams closed while a graph capture was running: they join the free list only once no capture
+# runs and their queued work has drained (_reclaim), so the next owner never receives a stream
+# with captured work still pending
+_closing_streams = []
+
+
+def _device_index(device) -> int:
+    if device is None:
+        return torch.cuda.current_device()
+    d = torch.device(device) if not isinstance(device, torch.device) else device
+    if d.type != "cuda":
+        raise HipError(f"OwnedStream: a cuda device is needed, got {d}")
+    return torch.cuda.current_device() if d.index is None else d.index
+
+
+def _reclaim() -> None:
+    if not _closing_streams:
+        return
+    try:
+        if torch.cuda.is_current_stream_capturing():
+            return
+    except Exception:
+        return
+    while _closing_streams:
+        h, dev, prio, ext = _closing_streams.pop()
+        ext.synchronize()
+        _free_streams.setdefault((dev, prio), []).append(h)
 
 
 class OwnedStream:
     """A HIP stream this process owns (pis_stream_create), usable as a torch stream
     (``.stream`` is a torch.cuda.ExternalStream). torch's ``torch.cuda.Stream()`` hands out a
     fixed round-robin pool, so a stream that took part in a graph capture would later be given to
-    unrelated code; an owned stream is recycled only into other OwnedStreams (``close()`` returns
-    it to a free list after its work drains). It is never destroyed: PyTorch keeps raw stream
-    handles beyond the objects that used them — autograd's AccumulateGrad nodes record the stream
-    of the forward that created them and sync with it in every later backward, and the caching
-    allocator tags blocks with their allocation stream — so a destroyed stream would leave those
-    handles dangling (tests/test_graph_gpu.py::test_graph_dropped_without_close reproduced exactly
-    that: a segfault in the next eager backward of the graphed model)."""
+    unrelated code; an owned stream is recycled only into other OwnedStreams of the same device
+    (``close()`` returns it to a free list after its work drains). It is never destroyed
+    (``pis_stream_destroy`` stays in the C-ABI for other hosts; this one does not call it):
+    PyTorch keeps raw stream handles beyond the objects that used them — autograd's
+    AccumulateGrad nodes record the stream of the forward that created them and sync with it in
+    every later backward, and the caching allocator tags blocks with their allocation stream — so
+    a destroyed stream would leave those handles dangling
+    (tests/test_graph_gpu.py::test_graph_dropped_without_close reproduced exactly that: a segfault
+    in the next eager backward of the graphed model).
+
+    The HIP stream is created ON ``device`` (hipStreamCreate uses the calling thread's current
+    device, so the call runs inside ``torch.cuda.device(device)``): a model on cuda:1 gets its
+    weight-gradient stream on cuda:1 even when cuda:0 is current."""
 
     def __init__(self, device=None, priority: int = 0):
-        self.handle = None
-        for i, (h, p) in enumerate(_free_streams):
-            if p == priority:
-                self.handle = _free_streams.pop(i)[0]
-                break
+        _reclaim()
+        self.device_index = _device_index(device)
+        self.priority = priority
+        free = _free_streams.get((self.device_index, priority))
+        self.handle = free.pop() if free else None
         if self.handle is None:
             raw = c_void_p()
-            check(lib().pis_stream_create(priority, ctypes.byref(raw)), "pis_stream_create")
+            with torch.cuda.device(self.device_index):
+                check(lib().pis_stream_create(priority, ctypes.byref(raw)), "pis_stream_create")
             self.handle = raw.value
-        self.priority = priority
-        self.stream = torch.cuda.ExternalStream(self.handle, device=device)
+        self.stream = torch.cuda.ExternalStream(self.handle, device=torch.device("cuda", self.device_index))
 
     def capture_status(self) -> int:
         return lib().pis_stream_capture_status(self.handle)
 
     def close(self) -> None:
-        """Return the stream to the free list once its queued work is done (no sync inside a capture:
-        the work is then waited for by whoever takes the stream next, in stream order)."""
+        """Return the stream to the free list once its queued work is done. Inside a capture no
+        sync is possible: the stream waits on a closing list until the capture has ended and its
+        work has drained (the next OwnedStream() reclaims it)."""
         h, self.handle = self.handle, None
         if not h:
             return
@@ -210,9 +249,11 @@ class OwnedStream:
             capturing = torch.cuda.is_current_stream_capturing()
         except Exception:
             capturing = False
-        if not capturing:
-            self.stream.synchronize()
-        _free_streams.append((h, self.priority))
+        if capturing:
+            _closing_streams.append((h, self.device_index, self.priority, self.stream))
+            return
+        self.stream.synchronize()
+        _free_streams.setdefault((self.device_index, self.priority), []).append(h)
 
     def __del__(self):
         try:

@@ -40,8 +40,9 @@ struct DirectArgs {
   float* pool;         // [B][H/2][W/2][N] or NULL: also the 2x2 max pool of y
   int B, H, W, C, N;   // C contraction channels (% 16), N outputs (% 64)
   int flags;
-  int dbg;             // timing twins only (pis_tune key 2, wrong results): 1 no global loads after the first
-                       // chunk, 2 no LDS staging after the first chunk, 4 no epilogue
+  int dbg;             // timing twins only (pis_tune key 2, wrong results; read only by the TW = true
+                       // instantiations): 1 no global loads after the first chunk, 2 no LDS staging
+                       // after the first chunk, 4 no epilogue
 };
 
 constexpr int DT_H = 8, DT_W = 32, DH_H = DT_H + 2, DH_W = DT_W + 2, DH_P = DH_H * DH_W, DKC = 16;
@@ -123,7 +124,7 @@ __global__ __launch_bounds__(256) void conv3x3_wsplit_batch_kernel(WsplitBatch w
 
 // The direct kernels' epilogue (conv3x3_h3_kernel and the 8-wave form): the wave's rows r0 + 2 wave,
 // + 1 from its accumulators, through its own 8 KB of LDS at E.
-template <bool POOL, bool MPF, int MPR = 2>  // MPR: mask rows prefetched (MPF)
+template <bool POOL, bool MPF, bool TW = false, int MPR = 2>  // MPR: mask rows prefetched (MPF); TW: timing twin
 __device__ __forceinline__ void direct_epilogue(const DirectArgs& g, f32x16 (&acc)[2][2], float s_cur, float* E,
                                                 const f32x4 (&mkp)[2][8], int b, int r0, int c0, int n0, int wave,
                                                 int lane, int tid) {
@@ -135,7 +136,7 @@ __device__ __forceinline__ void direct_epilogue(const DirectArgs& g, f32x16 (&ac
   // are issued together (one memory round trip per row) and a pixel's 64 channels are one 256-B
   // store.
   const float inv_s = 1.f / s_cur;  // exact: a power of two
-  if (g.dbg & 4) {
+  if (TW && (g.dbg & 4)) {
     float t = 0.f;
 #pragma unroll
     for (int i = 0; i < 2; ++i)
@@ -208,7 +209,11 @@ __device__ __forceinline__ void direct_epilogue(const DirectArgs& g, f32x16 (&ac
 // chunk's loads would use: enc1.conv1 input gradient -12 %, enc2.conv1 -4 % (profiles/r3_q18_*).
 // (A tap loop walked column-shift-major, sharing halo rows between consecutive taps with the next
 // tap's fragments issued ahead, measured neutral: the loop runs at the clock-limited MFMA rate.)
-template <bool POOL, bool MPF = false>
+// TW: the timing-twin instantiation (pis_tune key 2 != 0 only); the production kernels carry no
+// debug branch. DG: an input gradient — the same code, its own symbol, so that rocprofv3 and the PMC
+// passes report forward, pooled forward and input gradient separately (the bench's per-role
+// rooflines)
+template <bool POOL, bool MPF = false, bool TW = false, bool DG = false>
 __global__ __launch_bounds__(256, 2) void conv3x3_h3_kernel(DirectArgs g) {
   __shared__ __attribute__((aligned(16))) char smem[DX_BYTES + DW_BYTES + 64];
   _Float16* sx = reinterpret_cast<_Float16*>(smem);             // [plane][DH_P][16]
@@ -237,7 +242,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_h3_kernel(DirectArgs g) {
   f32x4 xr[DX_PER_T][2];
   u32x4 wr[DW_PER_T];
   auto gload = [&](int k) {
-    if ((g.dbg & 1) && k > 0) return;
+    if (TW && (g.dbg & 1) && k > 0) return;
 #pragma unroll
     for (int j = 0; j < DX_PER_T; ++j) {
       const int i = tid + 256 * j;
@@ -284,7 +289,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_h3_kernel(DirectArgs g) {
   // one chunk; the last one (peeled, LAST) issues the epilogue's mask loads instead of a next chunk's
   auto chunk = [&](int k, auto last_c) __attribute__((always_inline)) {
     constexpr bool LAST = decltype(last_c)::value;
-    if (!((g.dbg & 2) && k > 0)) {
+    if (!(TW && (g.dbg & 2) && k > 0)) {
     // 1. this chunk's weights into LDS; the halo's block-wide max
     float m = 0.f;
 #pragma unroll
@@ -355,7 +360,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_h3_kernel(DirectArgs g) {
   chunk(nk - 1, std::true_type{});
 
   // epilogue: the wave's 8 KB of LDS, free since the loop's last barrier
-  direct_epilogue<POOL, MPF>(g, acc, s_cur, reinterpret_cast<float*>(smem) + wave * (32 * 64), mkp, b, r0, c0, n0,
+  direct_epilogue<POOL, MPF, TW>(g, acc, s_cur, reinterpret_cast<float*>(smem) + wave * (32 * 64), mkp, b, r0, c0, n0,
                              wave, lane, tid);
 }
 
@@ -436,14 +441,27 @@ int launch_direct_h3(const IGemmArgs& a, int B, void* ws, size_t ws_bytes, hipSt
   const double flop = 2.0 * 9 * (double)B * a.H * a.W * C * N;
   const bool mpf = tune_get(PIS_TUNE_DIRECT_PIPE) != 0 && (a.flags & PIS_MASK);
   const int blocks = B * (a.H / DT_H) * (a.W / DT_W) * (N / 64);
-  launch_hook("direct_h3", 0, s, flop);
-  if (a.pool)  // a forward: no mask
-    hipLaunchKernelGGL((conv3x3_h3_kernel<true, false>), dim3(blocks), dim3(256), 0, s, g);
-  else if (mpf)
-    hipLaunchKernelGGL((conv3x3_h3_kernel<false, true>), dim3(blocks), dim3(256), 0, s, g);
-  else
-    hipLaunchKernelGGL((conv3x3_h3_kernel<false, false>), dim3(blocks), dim3(256), 0, s, g);
-  launch_hook("direct_h3", 1, s, flop);
+  // the launch hook's label names the role: pooled forward, forward, input gradient
+  const char* role = a.pool ? "direct_h3_pool" : a.is_dgrad ? "direct_h3_dgrad" : "direct_h3_fwd";
+  const dim3 grid(blocks);
+  launch_hook(role, 0, s, flop);
+  if (g.dbg) {  // timing twins (tools/bench_kernels.py --dbg): wrong results by design
+    if (a.pool)
+      hipLaunchKernelGGL((conv3x3_h3_kernel<true, false, true>), grid, dim3(256), 0, s, g);
+    else if (mpf)
+      hipLaunchKernelGGL((conv3x3_h3_kernel<false, true, true>), grid, dim3(256), 0, s, g);
+    else
+      hipLaunchKernelGGL((conv3x3_h3_kernel<false, false, true>), grid, dim3(256), 0, s, g);
+  } else if (a.pool) {  // a forward: no mask
+    hipLaunchKernelGGL((conv3x3_h3_kernel<true, false>), grid, dim3(256), 0, s, g);
+  } else if (!a.is_dgrad) {
+    hipLaunchKernelGGL((conv3x3_h3_kernel<false, false>), grid, dim3(256), 0, s, g);
+  } else if (mpf) {
+    hipLaunchKernelGGL((conv3x3_h3_kernel<false, true, false, true>), grid, dim3(256), 0, s, g);
+  } else {
+    hipLaunchKernelGGL((conv3x3_h3_kernel<false, false, false, true>), grid, dim3(256), 0, s, g);
+  }
+  launch_hook(role, 1, s, flop);
   return launch_status("conv3x3_h3");
 }
 
@@ -487,6 +505,7 @@ __device__ __forceinline__ int wsw64(int row, int ch) { return row * 64 + 8 * (c
 
 // (An eight-wave form — the taps split between the wave halves, 80 accumulator registers, two
 // waves per SIMD — measured within +-2 % per layer, profiles/r3_q19_wg8.txt: not kept.)
+template <bool TW = false>  // TW: timing twin (pis_tune key 2 != 0 only)
 __global__ __launch_bounds__(256, 1) void conv3x3_wgrad_h3_kernel(DirectWArgs g) {
   constexpr int NW = 4, NT = 64 * NW, WZ_PER_T = WZ_ITEMS / NT, WX_PER_T = (WX_ITEMS + NT - 1) / NT;
   constexpr int NTAP = 9;
@@ -505,7 +524,7 @@ __global__ __launch_bounds__(256, 1) void conv3x3_wgrad_h3_kernel(DirectWArgs g)
 
   f32x4 zr[WZ_PER_T][2], xr[WX_PER_T][2];
   auto gload = [&](int t) {
-    if ((g.dbg & 1) && t != split) return;
+    if (TW && (g.dbg & 1) && t != split) return;
     const int b = t / per_img, rem = t - b * per_img, pr0 = (rem / tw_n) * WT_H, pc0 = (rem % tw_n) * WT_W;
     const size_t img = (size_t)b * g.H * g.W;
 #pragma unroll
@@ -547,7 +566,7 @@ __global__ __launch_bounds__(256, 1) void conv3x3_wgrad_h3_kernel(DirectWArgs g)
   if (t < ntile) gload(t);
 #pragma unroll 1
   for (; t < ntile; t += g.splits) {
-    if (!((g.dbg & 2) && t != split)) {
+    if (!(TW && (g.dbg & 2) && t != split)) {
     // 1. block maxima of the staged operands
     float mz = 0.f, mx = 0.f;
 #pragma unroll
@@ -675,6 +694,222 @@ __global__ __launch_bounds__(256, 1) void conv3x3_wgrad_h3_kernel(DirectWArgs g)
   }
 }
 
+// =============================================================================================
+// The direct weight gradient on 2-row tiles walked DOWN a column strip (pis_tune key 34 = 1,
+// VERDICT r3 item 2). Same arithmetic, operand images and MFMA map as conv3x3_wgrad_h3_kernel
+// (rows n, columns (tap, c), 9 accumulator tiles per wave, transposed LDS reads, one power-of-two
+// scale per tile and operand), but a tile is 2 rows x 32 columns (64 pixels) with a 4 x 34 x halo:
+// the raw next-tile loads held in registers during the MFMAs drop from 88 to 56 VGPRs and the LDS
+// image from 85 to 51 KB, so a block fits in 256 registers per lane. Two blocks share a CU (one
+// stages while the other multiplies) — or, in the training step, one weight-gradient block sits
+// beside a main-stream block instead of locking the CU (the 4-row kernel's 497-register waves
+// filled every SIMD's register file). A block owns a contiguous run of tiles ordered row pair
+// fastest, so consecutive tiles are vertical neighbours: the two halo rows a tile shares with
+// the previous one were fetched by this CU a moment ago (L2 / L1 hits), and HBM sees x about once
+// (34/32 for the side columns). With several (n, c) pairs the pairs of one split are dealt to one
+// XCD back to back, so the x / dz tiles they share come from that XCD's L2.
+// =============================================================================================
+constexpr int SW_H = 2, SW_W = 32, SW_P = SW_H * SW_W, SH_H = SW_H + 2, SH_W = SW_W + 2, SH_P = SH_H * SH_W;
+constexpr int SZ_HALFS = SW_P * 64, SX_HALFS = SH_P * 64;  // per plane
+constexpr int SZ_ITEMS = SW_P * 8, SX_ITEMS = SH_P * 8;      // 8-channel groups (32 B of fp32)
+constexpr int SLDS_BYTES = 2 * (SZ_HALFS + SX_HALFS) * 2;
+constexpr int SBIAS_BYTES = 256 * 8 * 4;  // per-thread bias partials (8 channels), in LDS: 8 VGPRs fewer
+
+template <bool TW = false>  // TW: timing twin (pis_tune key 2 != 0 only)
+__global__ __launch_bounds__(256, 2) void conv3x3_wgrad_strip_kernel(DirectWArgs g) {
+  constexpr int NW = 4, NT = 64 * NW, SZ_PER_T = SZ_ITEMS / NT, SX_PER_T = (SX_ITEMS + NT - 1) / NT;
+  constexpr int NTAP = 9;
+  __shared__ __attribute__((aligned(16))) char smem[SLDS_BYTES + SBIAS_BYTES + 64];
+  _Float16* sz = reinterpret_cast<_Float16*>(smem);                     // [plane][64][64]
+  _Float16* sx = reinterpret_cast<_Float16*>(smem + 2 * SZ_HALFS * 2);  // [plane][136][64]
+  f32x4* sbias = reinterpret_cast<f32x4*>(smem + SLDS_BYTES);           // [256 threads][2] bias partials
+  float* red = reinterpret_cast<float*>(smem + SLDS_BYTES + SBIAS_BYTES);  // [2][NW] wave maxima
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wi = (wave >> 1) & 1, wj = wave & 1;  // n-half, c-half
+  const int ncb = g.Cin / 64, pairs = (g.Cout / 64) * ncb;
+  int pair, split;
+  if ((g.splits & 7) == 0) {  // the pairs of split 8 q + x: blocks of XCD x, back to back
+    const int bid = blockIdx.x, xcd = bid & 7, j = bid >> 3;
+    pair = j % pairs;
+    split = (j / pairs) * 8 + xcd;
+  } else {
+    pair = blockIdx.x % pairs;
+    split = blockIdx.x / pairs;
+  }
+  const int n0 = (pair / ncb) * 64, c0 = (pair % ncb) * 64;
+  const int nrp = g.H / SW_H, ncol = g.W / SW_W, per_img = nrp * ncol, ntile = g.B * per_img;
+  const int tps = (ntile + g.splits - 1) / g.splits;
+  const int t_begin = split * tps, t_end = min(ntile, t_begin + tps);
+  const bool do_bias = g.part_bias != nullptr && c0 == 0;
+
+  f32x4 zr[SZ_PER_T][2], xr[SX_PER_T][2];
+  auto gload = [&](int t) __attribute__((always_inline)) {
+    if (TW && (g.dbg & 1) && t != t_begin) return;
+    const int b = t / per_img, rem = t - b * per_img, col = rem / nrp, rp = rem - col * nrp;
+    const int pr0 = SW_H * rp, pc0 = SW_W * col;
+    const size_t img = (size_t)b * g.H * g.W;
+#pragma unroll
+    for (int j = 0; j < SZ_PER_T; ++j) {
+      const int i = tid + NT * j, px = i >> 3, cg = i & 7;
+      const float* p = g.dz + (img + (size_t)(pr0 + (px >> 5)) * g.W + pc0 + (px & 31)) * g.ldz + n0 + 8 * cg;
+      zr[j][0] = *reinterpret_cast<const f32x4*>(p);
+      zr[j][1] = *reinterpret_cast<const f32x4*>(p + 4);
+    }
+#pragma unroll
+    for (int j = 0; j < SX_PER_T; ++j) {
+      const int i = tid + NT * j, q = i >> 3, cg = i & 7;
+      xr[j][0] = xr[j][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (i < SX_ITEMS) {  // the last item: wave 0 only (wave-uniform)
+        const int qr = q / SH_W, qc = q - qr * SH_W, row = pr0 - 1 + qr, cl = pc0 - 1 + qc;
+        if (row >= 0 && row < g.H && cl >= 0 && cl < g.W) {
+          const float* p = g.x + (img + (size_t)row * g.W + cl) * g.ldx + c0 + 8 * cg;
+          xr[j][0] = *reinterpret_cast<const f32x4*>(p);
+          xr[j][1] = *reinterpret_cast<const f32x4*>(p + 4);
+        }
+      }
+    }
+  };
+
+  f32x16 acc[NTAP];
+#pragma unroll
+  for (int t = 0; t < NTAP; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+  // bias partials, channels n0 + 8 (tid & 7) + e: each thread's own LDS slot (no barrier needed)
+  if (do_bias) sbias[2 * tid] = sbias[2 * tid + 1] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float sz_cur = 0.f, sx_cur = 0.f, sz_min = __builtin_inff(), sx_min = __builtin_inff();
+
+  // lane roles in the transposed reads: 16-lane group gq, its row q and 8-B column slot p
+  const int gq = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+  const int kh = gq >> 1;  // k half (pixels 8 kh ..)
+  const int cgA = 4 * wi + 2 * (gq & 1) + (p >> 1), cgB = 4 * wj + 2 * (gq & 1) + (p >> 1);
+
+  if (t_begin < t_end) gload(t_begin);
+#pragma unroll 1
+  for (int t = t_begin; t < t_end; ++t) {
+    if (!(TW && (g.dbg & 2) && t != t_begin)) {
+      // 1. block maxima of the staged operands (+ the bias partials from the raw dz)
+      float mz = 0.f, mx = 0.f;
+#pragma unroll
+      for (int j = 0; j < SZ_PER_T; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) mz = fmaxf(mz, fmaxf(fabsf(zr[j][0][e]), fabsf(zr[j][1][e])));
+#pragma unroll
+      for (int j = 0; j < SX_PER_T; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) mx = fmaxf(mx, fmaxf(fabsf(xr[j][0][e]), fabsf(xr[j][1][e])));
+      mz = wave_max_nonneg(mz);
+      mx = wave_max_nonneg(mx);
+      if (lane == 0) {
+        red[wave] = mz;
+        red[NW + wave] = mx;
+      }
+      if (do_bias) {
+        f32x4 b0 = sbias[2 * tid], b1 = sbias[2 * tid + 1];
+#pragma unroll
+        for (int j = 0; j < SZ_PER_T; ++j) {
+          b0 += zr[j][0];
+          b1 += zr[j][1];
+        }
+        sbias[2 * tid] = b0;
+        sbias[2 * tid + 1] = b1;
+      }
+      __syncthreads();
+      // 2. this tile's scales; the partial sums re-expressed in them (one exact power-of-two factor
+      // at a time); the split planes into LDS
+      mz = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+      mx = fmaxf(fmaxf(red[NW], red[NW + 1]), fmaxf(red[NW + 2], red[NW + 3]));
+      const float sz_new = h3_keep(sz_cur, mz, sz_min), sx_new = h3_keep(sx_cur, mx, sx_min);
+      if (sz_cur > 0.f && (sz_new != sz_cur || sx_new != sx_cur)) {
+        const float fz = sz_new / sz_cur, fx = sx_new / sx_cur;
+#pragma unroll
+        for (int k = 0; k < NTAP; ++k) acc[k] = (acc[k] * fz) * fx;
+      }
+      sz_cur = sz_new;
+      sx_cur = sx_new;
+#pragma unroll
+      for (int j = 0; j < SZ_PER_T; ++j) {
+        const int i = tid + NT * j, px = i >> 3, cg = i & 7;
+        u32x2 h0, l0, h1, l1;
+        split2h_x4(zr[j][0] * sz_cur, h0, l0);
+        split2h_x4(zr[j][1] * sz_cur, h1, l1);
+        *reinterpret_cast<u32x4*>(&sz[wsw64(px, cg)]) = u32x4{h0[0], h0[1], h1[0], h1[1]};
+        *reinterpret_cast<u32x4*>(&sz[SZ_HALFS + wsw64(px, cg)]) = u32x4{l0[0], l0[1], l1[0], l1[1]};
+      }
+#pragma unroll
+      for (int j = 0; j < SX_PER_T; ++j) {
+        const int i = tid + NT * j, qq = i >> 3, cg = i & 7;
+        if (i < SX_ITEMS) {
+          u32x2 h0, l0, h1, l1;
+          split2h_x4(xr[j][0] * sx_cur, h0, l0);
+          split2h_x4(xr[j][1] * sx_cur, h1, l1);
+          *reinterpret_cast<u32x4*>(&sx[wsw64(qq, cg)]) = u32x4{h0[0], h0[1], h1[0], h1[1]};
+          *reinterpret_cast<u32x4*>(&sx[SX_HALFS + wsw64(qq, cg)]) = u32x4{l0[0], l0[1], l1[0], l1[1]};
+        }
+      }
+      __syncthreads();
+    }
+    // 3. the next tile's loads fly during this tile's MFMAs
+    if (t + 1 < t_end) gload(t + 1);
+#pragma unroll 1
+    for (int ks = 0; ks < 4; ++ks) {  // 16-pixel K-steps: tile row ks >> 1, columns 16 (ks & 1) ..
+      const int rr = ks >> 1, cc0 = 16 * (ks & 1);
+      // A = dz^T (rows n, k pixels): pixels 16 ks + 8 kh + q (+ 4) of the tile, channels of cgA
+      f16x8 a[2];
+#pragma unroll
+      for (int pl = 0; pl < 2; ++pl) {
+        const _Float16* base = sz + pl * SZ_HALFS;
+        const int px = 16 * ks + 8 * kh + q;
+        const s16x4 lo4 = tr_read(base + wsw64(px, cgA) + 4 * (p & 1));
+        const s16x4 hi4 = tr_read(base + wsw64(px + 4, cgA) + 4 * (p & 1));
+        a[pl] = __builtin_bit_cast(f16x8, __builtin_shufflevector(lo4, hi4, 0, 1, 2, 3, 4, 5, 6, 7));
+      }
+#pragma unroll
+      for (int tap = 0; tap < NTAP; ++tap) {
+        const int r = tap / 3, s = tap % 3;
+        // B = x (k pixels, columns c): halo pixel (rr + r, cc0 + 8 kh + q (+ 4) + s), channels of cgB
+        f16x8 bb[2];
+        const int hp = (rr + r) * SH_W + cc0 + 8 * kh + q + s;
+#pragma unroll
+        for (int pl = 0; pl < 2; ++pl) {
+          const _Float16* base = sx + pl * SX_HALFS;
+          const s16x4 lo4 = tr_read(base + wsw64(hp, cgB) + 4 * (p & 1));
+          const s16x4 hi4 = tr_read(base + wsw64(hp + 4, cgB) + 4 * (p & 1));
+          bb[pl] = __builtin_bit_cast(f16x8, __builtin_shufflevector(lo4, hi4, 0, 1, 2, 3, 4, 5, 6, 7));
+        }
+        acc[tap] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[1], bb[0], acc[tap], 0, 0, 0);
+        acc[tap] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[0], bb[1], acc[tap], 0, 0, 0);
+        acc[tap] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[0], bb[0], acc[tap], 0, 0, 0);
+      }
+    }
+    __syncthreads();
+  }
+
+  // partial sums / (sz sx), one factor at a time -> slab [split][Cout][9][Cin]: lane column
+  // c0 + 32 wj + (lane & 31), rows n0 + 32 wi + (reg & 3) + 8 (reg >> 2) + 4 (lane >> 5)
+  const float iz = sz_cur > 0.f ? 1.f / sz_cur : 0.f, ix = sx_cur > 0.f ? 1.f / sx_cur : 0.f;
+  float* slab = g.part + (size_t)split * g.Cout * 9 * g.Cin;
+  const int c = c0 + 32 * wj + (lane & 31);
+#pragma unroll
+  for (int tt = 0; tt < NTAP; ++tt) {
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+      const int n = n0 + 32 * wi + (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5);
+      slab[((size_t)n * 9 + tt) * g.Cin + c] = (acc[tt][reg] * iz) * ix;
+    }
+  }
+  if (do_bias) {  // fixed-order reduction over the 32 threads of each channel group
+    const float* rb = reinterpret_cast<const float*>(sbias);
+    __syncthreads();
+    if (tid < 64) {
+      const int cg = tid >> 3, e = tid & 7;
+      float sum = 0.f;
+      for (int k = 0; k < NT / 8; ++k) sum += rb[(8 * k + cg) * 8 + e];
+      g.part_bias[(size_t)split * g.Cout + n0 + tid] = sum;
+    }
+  }
+}
+
 bool direct_w_wanted(int B, int H, int W, int Cin, int Cout, int ldx, int ldz) {
   return B > 0 && H % WT_H == 0 && W % WT_W == 0 && Cin % 64 == 0 && Cout % 64 == 0 && ldz % 4 == 0 &&
          direct_h3_wanted(H, W, Cin, Cout, ldx);
@@ -686,8 +921,22 @@ static int direct_w_splits(int B, int H, int W, int Cin, int Cout) {
   return std::max(1, std::min(ntile, 256 / std::max(1, std::min(pairs, 256))));
 }
 
+// the strip kernel's split count: ~PIS_TUNE_DIRECT_WBLOCKS workgroups over the (n, c) pairs, a
+// multiple of 8 (the pairs of one split on one XCD) where there are enough tiles
+static int direct_ws_splits(int B, int H, int W, int Cin, int Cout) {
+  const int pairs = (Cout / 64) * (Cin / 64);
+  const int ntile = B * (H / SW_H) * (W / SW_W);
+  const int target = std::max(8, tune_get(PIS_TUNE_DIRECT_WBLOCKS));
+  int sp = std::max(1, target / std::max(1, pairs));
+  if (sp >= 8) sp &= ~7;
+  return std::max(1, std::min(sp, ntile));
+}
+
+static bool direct_w_strip() { return tune_get(PIS_TUNE_DIRECT_WSTRIP) != 0; }
+
 size_t direct_w_ws_bytes(int B, int H, int W, int Cin, int Cout) {
-  const int sp = direct_w_splits(B, H, W, Cin, Cout);
+  // room for either kernel (the knobs may change between the size query and the launch)
+  const int sp = std::max(direct_w_splits(B, H, W, Cin, Cout), direct_ws_splits(B, H, W, Cin, Cout));
   return (size_t)sp * Cout * 9 * Cin * sizeof(float) + (size_t)sp * Cout * sizeof(float) + 512;
 }
 
@@ -699,14 +948,23 @@ int launch_direct_wgrad(const float* x, int ldx, const float* dz, int ldz, float
   DirectWArgs g{};
   g.x = x; g.ldx = ldx; g.dz = dz; g.ldz = ldz;
   g.B = B; g.H = H; g.W = W; g.Cin = Cin; g.Cout = Cout;
- g.splits = direct_w_splits(B, H, W, Cin, Cout);
+  const bool strip = direct_w_strip();
+  g.splits = strip ? direct_ws_splits(B, H, W, Cin, Cout) : direct_w_splits(B, H, W, Cin, Cout);
   g.dbg = tune_get(PIS_TUNE_DEBUG_NOLOAD);
   g.part = reinterpret_cast<float*>(ws);
   g.part_bias = db ? g.part + (size_t)g.splits * Cout * 9 * Cin : nullptr;
   const int pairs = (Cout / 64) * (Cin / 64);
   const double flop = 2.0 * 9 * (double)B * H * W * Cin * Cout;
+  const dim3 grid(g.splits * pairs);
   launch_hook("direct_wgrad_h3", 0, s, flop);
-  hipLaunchKernelGGL(conv3x3_wgrad_h3_kernel, dim3(g.splits * pairs), dim3(256), 0, s, g);
+  if (strip && g.dbg)
+    hipLaunchKernelGGL((conv3x3_wgrad_strip_kernel<true>), grid, dim3(256), 0, s, g);
+  else if (strip)
+    hipLaunchKernelGGL((conv3x3_wgrad_strip_kernel<false>), grid, dim3(256), 0, s, g);
+  else if (g.dbg)
+    hipLaunchKernelGGL((conv3x3_wgrad_h3_kernel<true>), grid, dim3(256), 0, s, g);
+  else
+    hipLaunchKernelGGL((conv3x3_wgrad_h3_kernel<false>), grid, dim3(256), 0, s, g);
   launch_hook("direct_wgrad_h3", 1, s, flop);
   int rc = launch_status("conv3x3_wgrad_h3");
   if (!rc) rc = reduce_slabs(g.part, g.splits, (int64_t)Cout * 9 * Cin, dw, acc, s);

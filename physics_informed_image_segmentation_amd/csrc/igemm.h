@@ -33,6 +33,7 @@ struct IGemmArgs {
   float* pool;         // F(4x4,3x3) forward only: also write the 2x2 max pool of dst here ([B][H/2][W/2][N])
   int w_unflipped;     // F(4x4,3x3) input gradient: wt holds the original KRSC weights (no flipped copy)
   int filter_ready;    // F(4x4,3x3): wt holds the layer's filter transform (pis_conv3x3_filter)
+  int is_dgrad;        // an input gradient (pis_conv3x3_dgrad*): labels the direct kernel's launch / symbol
   // batched launches (gridDim.y > 1): per-batch element offsets
   int64_t bs_src, bs_wt, bs_dst;
 };

@@ -828,6 +828,7 @@ extern "C" int pis_conv3x3_dgrad_ex(const float* dz, int ldz, const float* w_fli
   a.flags = flags & (PIS_MASK | PIS_SCALE | PIS_ACCUMULATE);
   a.w_unflipped = (flags & PIS_W_UNFLIPPED) != 0;
   a.filter_ready = (flags & PIS_FILTER_READY) != 0;
+  a.is_dgrad = 1;
   PIS_CHECK_ARG(!a.w_unflipped || (flags & PIS_WINO_PREPARED) ||
                     (ws && direct_h3_wanted(H, W, Cout, Cin, ldz) && ws_bytes >= direct_h3_ws_bytes(Cout, Cin)),
                 "pis_conv3x3_dgrad_ex: PIS_W_UNFLIPPED needs the prepared F(4x4,3x3) path or the direct one");

@@ -713,6 +713,171 @@ __global__ __launch_bounds__(256) void loss_bwd_kernel(LossBwdArgs g) {
 }
 
 // ---------------------------------------------------------------------------
+// Head forward fused with the loss forward (SURVEY §7 hard part 6): the U-Net's
+// 1x1 output conv + sigmoid (src/unet.py:206-210) and every Stage-II loss term with the per-sample
+// counters (src/loss.py:130-160, src/pde.py:124-212, src/metrics.py:57-71) in ONE pass over the
+// 64-channel head input. A block owns R whole image rows of one sample:
+//  1. u of image rows y0-1 .. y0+R (reflect-resolved; the two halo rows recomputed from their own
+//     256 B/px, which the neighbouring bands fetch too: L2 / Infinity-Cache hits) into LDS, 16 lanes
+//     per pixel exactly as head_fwd64_kernel (same fma order and butterfly, so z and u are bitwise
+//     those of pis_head_fwd); the interior rows' z and u are written out (the model's outputs);
+//  2. the loss partials of its R rows from LDS (u and its reflect neighbours) and the targets, as
+//     loss_fwd_kernel; one finalize launch (loss_finalize_rows_kernel) reduces the [B][bands]
+//     partials in fixed order.
+// HBM per pixel: 256 B of x + 4 B of t read, 8 B of z, u written. The loss's own p / t pass (8 B/px,
+// latency-bound at C2) and its launch are gone from the step.
+// ---------------------------------------------------------------------------
+struct HeadLossFwdArgs {
+  const float* x;
+  int ldx;
+  const float* w;
+  const float* bias;
+  float* z;
+  float* u;
+  int R;          // image rows per block
+  LossRowArgs a;  // the loss part: a.g (t, B, H, W, weights, partials), a.rows = R, a.bands, outputs
+};
+
+template <bool RD, bool PF, int PP>
+__global__ __launch_bounds__(256) void head_loss_fwd_kernel(HeadLossFwdArgs h) {
+  constexpr bool ST = RD || PF;
+  extern __shared__ __attribute__((aligned(16))) float su[];  // [R + 2][SW]: image column c at c + 4
+  const LossArgs& g = h.a.g;
+  const int H = g.H, W = g.W, SW = W + 8;
+  const int band = blockIdx.x, b = blockIdx.y;
+  const int y0 = band * h.R, nr = min(h.R, H - y0);
+  const int tid = threadIdx.x, sub = tid & 15, grp = tid >> 4;
+  const size_t HW = (size_t)H * W;
+  const float* xb = h.x + (size_t)b * HW * h.ldx + 4 * sub;
+  const f32x4 wv = *reinterpret_cast<const f32x4*>(h.w + 4 * sub);
+  const float bias = h.bias[0];
+  // 1. u of the staged rows: a chunk is 16 PP consecutive pixels of one staged row (W % (16 PP) == 0),
+  // PP per 16-lane group, every load of the chunk issued before its sums
+  const int cpr = W / (16 * PP), nchunk = (nr + 2) * cpr;
+  for (int ch = 0; ch < nchunk; ++ch) {
+    const int r = ch / cpr, x0 = (ch - r * cpr) * (16 * PP) + grp;  // block-uniform r
+    const int gy = clampi(refl(y0 - 1 + r, H), 0, H - 1);
+    const float* row = xb + (size_t)gy * W * h.ldx;
+    f32x4 xv[PP];
+#pragma unroll
+    for (int j = 0; j < PP; ++j) xv[j] = *reinterpret_cast<const f32x4*>(row + (size_t)(x0 + 16 * j) * h.ldx);
+    const bool interior = r >= 1 && r <= nr;
+    const size_t orow = (size_t)b * HW + (size_t)(y0 - 1 + r) * W;
+#pragma unroll
+    for (int j = 0; j < PP; ++j) {
+      float s = 0.f;
+      s = fmaf(xv[j][0], wv[0], s);
+      s = fmaf(xv[j][1], wv[1], s);
+      s = fmaf(xv[j][2], wv[2], s);
+      s = fmaf(xv[j][3], wv[3], s);
+#pragma unroll
+      for (int off = 8; off > 0; off >>= 1) s += __shfl_xor(s, off, 16);
+      if (sub == 0) {
+        const int xx = x0 + 16 * j;
+        const float zz = s + bias;
+        const float uu = 1.f / (1.f + expf(-zz));
+        su[r * SW + 4 + xx] = uu;
+        if (interior) {
+          h.z[orow + xx] = zz;
+          h.u[orow + xx] = uu;
+        }
+      }
+    }
+  }
+  // the targets of this thread's items in flight across the barriers (TX threads per row, RY rows
+  // per pass; item = 4 pixels)
+  const int W4 = W >> 2, TX = min(W4, 256), RY = 256 / TX;
+  const int q = tid % TX, ry = tid / TX;
+  const float* tt = g.t + (size_t)b * HW;
+  __syncthreads();
+  if (ST) {  // reflect halo columns: column -1 is column 1, column W is column W-2
+    for (int r = tid; r < nr + 2; r += 256) {
+      su[r * SW + 3] = su[r * SW + 5];
+      su[r * SW + 4 + W] = su[r * SW + 2 + W];
+    }
+    __syncthreads();
+  }
+  // 2. the loss partials of rows y0 .. y0 + nr - 1 (staged rows 1 .. nr), as loss_fwd_kernel
+  constexpr float kLn2 = 0.69314718055994531f, kClamp2 = -144.26950408889634f;  // -100 / ln 2
+  float s_it = 0.f, s_p = 0.f, s_t = 0.f, s_bce2 = 0.f, s_rd = 0.f, s_g2 = 0.f, s_q2 = 0.f;
+  int c_i = 0, c_p = 0, c_t = 0;
+  if (ry < RY && q < W4) {
+    for (int r = 1 + ry; r <= nr; r += RY) {
+      const f32x4 tv = *reinterpret_cast<const f32x4*>(tt + (size_t)(y0 - 1 + r) * W + 4 * q);
+      const float* sc = su + r * SW + 4 + 4 * q;
+      const f32x4 pv = *reinterpret_cast<const f32x4*>(sc);
+      f32x4 uv = pv, dv = pv;
+      float lft = 0.f, rgt = 0.f;
+      if (ST) {
+        uv = *reinterpret_cast<const f32x4*>(sc - SW);
+        dv = *reinterpret_cast<const f32x4*>(sc + SW);
+        lft = sc[-1];
+        rgt = sc[4];
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float p = pv[i], t = tv[i];
+        s_it = fmaf(p, t, s_it);
+        s_p += p;
+        s_t += t;
+        s_bce2 += (t - 1.f) * fmaxf(__builtin_amdgcn_logf(1.f - p), kClamp2) -
+                  t * fmaxf(__builtin_amdgcn_logf(p), kClamp2);
+        const bool pb = p > g.thr, tb = t > 0.5f;
+        c_p += pb;
+        c_t += tb;
+        c_i += pb && tb;
+        if (ST) {
+          const float ul = i == 0 ? lft : pv[i - 1], ur = i == 3 ? rgt : pv[i + 1];
+          const float uu = uv[i], ud = dv[i];
+          const float qq = fmaf(-p, p, p);  // p (1 - p)
+          if (RD) {
+            const float lap = (uu + ud) + (ul + ur) - 4.f * p;
+            const float rr = fmaf(g.D, lap, g.rx * qq * (p - g.a));
+            s_rd = fmaf(rr, rr, s_rd);
+          }
+          if (PF) {
+            const float gx = ur - ul, gy2 = ud - uu;  // 2x the central differences
+            s_g2 = fmaf(gx, gx, fmaf(gy2, gy2, s_g2));
+            s_q2 = fmaf(qq, qq, s_q2);
+          }
+        }
+      }
+    }
+  }
+  const float v0 = wave_sum(s_it), v1 = wave_sum(s_p), v2 = wave_sum(s_t), v3 = wave_sum(s_bce2 * kLn2);
+  const float v4 = wave_sum(s_rd), v5 = wave_sum(0.125f * g.eps * s_g2 + s_q2 / g.eps);
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    c_i += __shfl_xor(c_i, off, 64);
+    c_p += __shfl_xor(c_p, off, 64);
+    c_t += __shfl_xor(c_t, off, 64);
+  }
+  __syncthreads();  // su is dead: its first words take the wave partials
+  float* fr = su;                                // [4][6]
+  int* ir = reinterpret_cast<int*>(su + 24);     // [4][3]
+  const int lane = tid & 63, wave = tid >> 6;
+  if (lane == 0) {
+    fr[wave * 6 + 0] = v0;
+    fr[wave * 6 + 1] = v1;
+    fr[wave * 6 + 2] = v2;
+    fr[wave * 6 + 3] = v3;
+    fr[wave * 6 + 4] = v4;
+    fr[wave * 6 + 5] = v5;
+    ir[wave * 3 + 0] = c_i;
+    ir[wave * 3 + 1] = c_p;
+    ir[wave * 3 + 2] = c_t;
+  }
+  __syncthreads();
+  const int blk = b * h.a.bands + band;
+  if (tid < 6) {
+    g.fpart[blk * 6 + tid] = ((fr[tid] + fr[6 + tid]) + fr[12 + tid]) + fr[18 + tid];
+  } else if (tid < 9) {
+    const int j = tid - 6;
+    g.ipart[blk * 3 + j] = ir[j] + ir[3 + j] + ir[6 + j] + ir[9 + j];
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Loss backward fused into the head backward (the consumer of dL/du): one
 // block = R whole image rows. The block stages u for rows y0-2 .. y0+R+1 (reflect
 // resolved, 2 halo columns), the RD residual of rows y0-1 .. y0+R, and dL/dz of
@@ -1031,6 +1196,81 @@ extern "C" int pis_pde_fields_bwd(const float* u, const float* g_lap, const floa
   hipLaunchKernelGGL(pde_fields_bwd_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, u, g_lap, g_residual,
                      g_gradmag2, B, H, W, D, a, du);
   return launch_status("pde_fields_bwd");
+}
+
+// rows per block of the fused head + loss forward: 8192 / W (16 at W = 512: 256 blocks of 18 staged
+// rows at C2, 12.5 % of the head input fetched twice; 8 at W = 1024), pis_tune key 36 overrides
+static int head_loss_fwd_rows(int H, int W) {
+  const int t = tune_get(PIS_TUNE_HEAD_LOSS_ROWS);
+  const int r = t > 0 ? t : std::max(2, std::min(16, 8192 / std::max(1, W)));
+  return std::max(1, std::min(r, H));
+}
+
+// pixels per 16-lane group in flight in the fused head + loss forward (W % (16 PP) == 0), 0: none fits
+static int head_loss_fwd_pp(int W) { return W % 256 == 0 ? 16 : W % 128 == 0 ? 8 : W % 64 == 0 ? 4 : 0; }
+
+extern "C" size_t pis_head_loss_fwd_ws(int B, int H, int W) {
+  const int R = head_loss_fwd_rows(H, W);
+  const size_t nblk = (size_t)B * ((H + R - 1) / R);
+  return 16 + nblk * (6 * sizeof(float) + 3 * sizeof(int)) + 256;
+}
+
+extern "C" int pis_head_loss_fwd_ok(int B, int H, int W, int C) {
+  const int R = head_loss_fwd_rows(H, W);
+  return C == 64 && B > 0 && H >= 2 && W >= 8 && W <= 2048 && head_loss_fwd_pp(W) > 0 &&
+         (int64_t)B * ((H + R - 1) / R) <= LOSS_MAX_BLOCKS;
+}
+
+extern "C" int pis_head_loss_fwd(const float* x, int ldx, const float* w, const float* bias, const float* t,
+                                 float* z, float* u, int B, int H, int W, int C, const pis_loss_params* prm,
+                                 float* out_terms, int* counts, float* scores, void* ws, size_t ws_bytes,
+                                 pis_stream_t stream) {
+  PIS_CHECK_ARG(x && w && bias && t && z && u && prm && out_terms, "pis_head_loss_fwd: bad arguments");
+  PIS_CHECK_ARG(pis_head_loss_fwd_ok(B, H, W, C),
+                "pis_head_loss_fwd: needs C == 64, W % 64 == 0, W <= 2048, H >= 2 and at most 2048 row bands "
+                "(use pis_head_fwd + pis_loss_fwd)");
+  PIS_CHECK_ARG(ldx % 4 == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)t & 15) == 0 && ((uintptr_t)w & 15) == 0,
+                "pis_head_loss_fwd: x, w, t must be 16-byte aligned with ldx % 4 == 0");
+  PIS_CHECK_ARG(ws && ws_bytes >= pis_head_loss_fwd_ws(B, H, W), "pis_head_loss_fwd: workspace too small");
+  HeadLossFwdArgs h{};
+  h.x = x; h.ldx = ldx; h.w = w; h.bias = bias; h.z = z; h.u = u;
+  h.R = head_loss_fwd_rows(H, W);
+  LossArgs& g = h.a.g;
+  g.p = u; g.t = t; g.B = B; g.H = H; g.W = W;
+  g.dice_w = prm->dice_w; g.bce_w = prm->bce_w; g.rd_w = prm->rd_w; g.pf_w = prm->pf_w;
+  g.smooth = prm->smooth; g.D = prm->D; g.a = prm->a; g.eps = prm->eps;
+  g.rx = (prm->flags & PIS_LOSS_NO_REACTION) ? 0.f : 1.f; g.thr = prm->thr;
+  const int bands = (H + h.R - 1) / h.R;
+  const int64_t nblk = (int64_t)B * bands;
+  g.fpart = (float*)((char*)ws + 16);
+  g.ipart = (int*)((char*)ws + 16 + (size_t)nblk * 6 * sizeof(float));
+  h.a.rows = h.R;
+  h.a.bands = bands;
+  h.a.terms = out_terms; h.a.counts = counts; h.a.scores = scores;
+  const bool all = prm->flags & PIS_LOSS_ALL_TERMS;
+  const bool rd = all || prm->rd_w > 0.f, pf = all || prm->pf_w > 0.f;
+  const int pp = head_loss_fwd_pp(W);
+  const size_t smem = (size_t)(h.R + 2) * (W + 8) * sizeof(float);
+  const dim3 grid(bands, B);
+  hipStream_t s = (hipStream_t)stream;
+  const double nbytes = (double)B * H * W * (4.0 * C + 12.0);
+  launch_hook("head_loss_fwd", 0, s, nbytes);
+#define PIS_HLF(RDV, PFV)                                                                                         \
+  do {                                                                                                            \
+    if (pp == 16) hipLaunchKernelGGL((head_loss_fwd_kernel<RDV, PFV, 16>), grid, dim3(256), smem, s, h);          \
+    else if (pp == 8) hipLaunchKernelGGL((head_loss_fwd_kernel<RDV, PFV, 8>), grid, dim3(256), smem, s, h);       \
+    else hipLaunchKernelGGL((head_loss_fwd_kernel<RDV, PFV, 4>), grid, dim3(256), smem, s, h);                    \
+  } while (0)
+  if (rd && pf) PIS_HLF(true, true);
+  else if (rd) PIS_HLF(true, false);
+  else if (pf) PIS_HLF(false, true);
+  else PIS_HLF(false, false);
+#undef PIS_HLF
+  launch_hook("head_loss_fwd", 1, s, nbytes);
+  int rc = launch_status("head_loss_fwd");
+  if (rc) return rc;
+  hipLaunchKernelGGL(loss_finalize_rows_kernel, dim3(1), dim3(256), 0, s, h.a);
+  return launch_status("loss_finalize");
 }
 
 static int head_loss_rows(int H, int W) { return std::max(1, std::min(H, 1024 / std::max(1, W))); }

@@ -927,7 +927,8 @@ __device__ __forceinline__ int wtsw(int row, int chunk) { return row * 128 + 8 *
 // 32-aligned split starts a K-step's 32 pixels lie in one image row, so its rows are one base +
 // 2 r pixels apart; the bias partials (column sums of A, blocks of the first column tile) are
 // summed from the raw loads and reduced over the 8 threads of a column group in LDS (fixed order).
-template <bool UP2 = false, int D = 2>
+// TW: the timing-twin instantiation (pis_tune key 2 != 0 only; the production kernel has no debug branch)
+template <bool UP2 = false, int D = 2, bool TW = false>
 __global__ __launch_bounds__(256, 2) void wgrad_h3t_kernel(WgradArgs g) {
   const Remap2 rm = xcd_remap2();
   if (rm.batch) {
@@ -963,7 +964,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_h3t_kernel(WgradArgs g) {
 
   f32x4 ra[D][4], rb[D][4];
   auto gload = [&](f32x4 (&xa)[4], f32x4 (&xb)[4], int st) __attribute__((always_inline)) {
-    if ((g.dbg & 1) && st >= D) return;
+    if (TW && (g.dbg & 1) && st >= D) return;
     const int p0 = p_begin + st * WT_BK;
     size_t abase = 0;
     if (UP2) {  // the K-step's 32 pixels: one image row (b, y), columns x0 ..
@@ -1041,7 +1042,11 @@ __global__ __launch_bounds__(256, 2) void wgrad_h3t_kernel(WgradArgs g) {
     for (int b = 0; b < 2; ++b)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
-  float units = 0.f;  // scale product the partial sums are expressed in (0: none yet)
+  // the partial sums are in units ua * ub, kept as TWO factors (0: none yet): each scale may be up
+  // to 2^126 (common.h h2_scale_pair), so their product can overflow fp32 when both operands are
+  // small (dz ~ 1e-30 against activations ~ 1e-2); the rescale and the epilogue apply one factor
+  // at a time, every step an exact power of two
+  float ua = 0.f, ub = 0.f;
   float s_a[2] = {0.f, 0.f}, s_b[2] = {0.f, 0.f};  // per buffer parity: the staged K-step's scales
 
   // D register sets: the raw operands of K-step st + D in flight while K-step st multiplies. Set
@@ -1071,20 +1076,21 @@ __global__ __launch_bounds__(256, 2) void wgrad_h3t_kernel(WgradArgs g) {
         bf[pl][a] = frag(buf + (2 + pl) * WT_PLANE, 0, 64 * wn + 32 * a);
       }
     if (st + 1 < nst) {
-      if (!((g.dbg & 2) && st > 0)) split_store(ra[sn], rb[sn], nxt, s_a[nxt], s_b[nxt]);
+      if (!(TW && (g.dbg & 2) && st > 0)) split_store(ra[sn], rb[sn], nxt, s_a[nxt], s_b[nxt]);
       if (st + 1 + D < nst) gload(ra[sn], rb[sn], st + 1 + D);
     }
-    {  // the partial sums in this K-step's units (exact: powers of two)
-      const float u = s_a[cur] * s_b[cur];
-      if (u != units) {
-        if (units != 0.f) {
-          const float f = u / units;
+    {  // the partial sums in this K-step's units (exact: powers of two, one factor at a time)
+      const float sa = s_a[cur], sb = s_b[cur];
+      if (sa != ua || sb != ub) {
+        if (ua != 0.f) {
+          const float fa = sa / ua, fb = sb / ub;
 #pragma unroll
           for (int a = 0; a < 2; ++a)
 #pragma unroll
-            for (int b = 0; b < 2; ++b) acc[a][b] *= f;
+            for (int b = 0; b < 2; ++b) acc[a][b] = (acc[a][b] * fa) * fb;
         }
-        units = u;
+        ua = sa;
+        ub = sb;
       }
     }
 #pragma unroll
@@ -1129,8 +1135,8 @@ __global__ __launch_bounds__(256, 2) void wgrad_h3t_kernel(WgradArgs g) {
     }
   }
   float* out = g.part + (size_t)split * (g.split_stride ? g.split_stride : (int64_t)g.Mp * g.Np);
-  const float inv = units != 0.f ? 1.f / units : 0.f;
-  if (g.dbg & 4) {
+  const float inv_a = ua != 0.f ? 1.f / ua : 0.f, inv_b = ub != 0.f ? 1.f / ub : 0.f;
+  if (TW && (g.dbg & 4)) {
     float t = 0.f;
 #pragma unroll
     for (int a = 0; a < 2; ++a)
@@ -1149,7 +1155,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_h3t_kernel(WgradArgs g) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int m = m0 + 64 * wm + 32 * a + (r & 3) + 8 * (r >> 2) + 4 * lh;
-        out[(size_t)m * g.Np + n] = acc[a][b][r] * inv;
+        out[(size_t)m * g.Np + n] = (acc[a][b][r] * inv_a) * inv_b;
       }
     }
   if (do_bias) {  // column sums over the block's pixels: the 8 threads of each column group
@@ -1187,7 +1193,10 @@ static int run_wgrad(const WgradArgs& base, const WgradPlan& pl, hipStream_t s, 
     if (tune_get(PIS_TUNE_WGRAD_T) != 0 && pl.bm == 128 && pl.bn == 128 && !a.a_up2 && !a.part_bias &&
         pl.pps % WT_BK == 0 && a.lda % 4 == 0 && a.ldb % 4 == 0 && a.bs_a % 4 == 0 && a.bs_b % 4 == 0 &&
         ((uintptr_t)a.a & 15) == 0 && ((uintptr_t)a.b & 15) == 0) {
-      hipLaunchKernelGGL((wgrad_h3t_kernel<false, 2>), grid, dim3(256), 0, s, a);
+      if (a.dbg)
+        hipLaunchKernelGGL((wgrad_h3t_kernel<false, 2, true>), grid, dim3(256), 0, s, a);
+      else
+        hipLaunchKernelGGL((wgrad_h3t_kernel<false, 2>), grid, dim3(256), 0, s, a);
       return launch_status("wgrad_h3t");
     }
     if (pl.bm == 128 && pl.bn == 128) hipLaunchKernelGGL((wgrad_h3_kernel<128, 128>), grid, dim3(256), 0, s, a);
@@ -1459,8 +1468,8 @@ static int wino_wgrad(const float* x, int ldx, const float* dz, int ldz, float* 
   return rc;
 }
 
-extern "C" size_t pis_conv3x3_wgrad_ws(int B, int H, int W, int Cin, int Cout) {
-  if (direct_w_wanted(B, H, W, Cin, Cout, 4, 4)) return direct_w_ws_bytes(B, H, W, Cin, Cout);
+// workspace of the non-direct weight-gradient paths (Winograd, halo, generic)
+static size_t wgrad_ws_nodirect(int B, int H, int W, int Cin, int Cout) {
   const WinoWgradPlan wp = wino_wgrad_plan(B, H, W, Cin, Cout);
   if (wp.use) return wp.total;
   const HaloPlan hp = halo_plan(B, H, W, Cin, Cout);
@@ -1471,6 +1480,11 @@ extern "C" size_t pis_conv3x3_wgrad_ws(int B, int H, int W, int Cin, int Cout) {
   // Cin == 1 computes a padded [Cout][64] tile and compacts it through a staging slab
   const size_t stage = Cin == 1 ? (size_t)Cout * 64 * sizeof(float) + 256 : 0;
   return wgrad_ws_bytes(pl) + stage;
+}
+
+extern "C" size_t pis_conv3x3_wgrad_ws(int B, int H, int W, int Cin, int Cout) {
+  if (direct_w_wanted(B, H, W, Cin, Cout, 4, 4)) return direct_w_ws_bytes(B, H, W, Cin, Cout);
+  return wgrad_ws_nodirect(B, H, W, Cin, Cout);
 }
 
 __global__ void compact_c1_kernel(const float* __restrict__ full, float* __restrict__ dw, int Cout,
@@ -1530,8 +1544,15 @@ extern "C" int pis_conv3x3_wgrad(const float* x, int ldx, const float* dz, int l
   PIS_CHECK_ARG((Cin == 1 || ldx % 4 == 0) && ldz % 4 == 0, "pis_conv3x3_wgrad: ld must be multiples of 4");
   hipStream_t s = (hipStream_t)stream;
   const int acc = flags & PIS_ACCUMULATE;
-  if (direct_w_wanted(B, H, W, Cin, Cout, ldx, ldz) && ws_bytes >= direct_w_ws_bytes(B, H, W, Cin, Cout))
-    return launch_direct_wgrad(x, ldx, dz, ldz, dw_krsc, db, B, H, W, Cin, Cout, acc, ws, ws_bytes, s);
+  // the direct kernel reads x and dz as float4s: 16-B aligned base pointers (a channel slice at an
+  // offset that is not a multiple of 4 floats falls through to the Winograd / halo kernels)
+  if (direct_w_wanted(B, H, W, Cin, Cout, ldx, ldz)) {
+    if (((uintptr_t)x & 15) == 0 && ((uintptr_t)dz & 15) == 0)
+      return launch_direct_wgrad(x, ldx, dz, ldz, dw_krsc, db, B, H, W, Cin, Cout, acc, ws, ws_bytes, s);
+    PIS_CHECK_ARG(ws_bytes >= wgrad_ws_nodirect(B, H, W, Cin, Cout),
+                  "pis_conv3x3_wgrad: x / dz not 16-byte aligned; the non-direct fallback needs a larger "
+                  "workspace than pis_conv3x3_wgrad_ws reports for this (direct) layer");
+  }
   const WinoWgradPlan wp = wino_wgrad_plan(B, H, W, Cin, Cout);
   if (wp.use && ldx % 4 == 0 && ws_bytes >= wp.total)
     return wino_wgrad(x, ldx, dz, ldz, dw_krsc, db, B, H, W, Cin, Cout, acc, wp, ws, s);

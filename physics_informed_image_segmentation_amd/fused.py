@@ -89,9 +89,12 @@ def loss_forward(u: torch.Tensor, t: torch.Tensor, cfg: LossConfig):
 
 class _FusedLoss(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, u, t, cfg: LossConfig, sink: dict):
-        terms, counts, scores = loss_forward(u, t, cfg)
-        sink["terms"], sink["counts"], sink["scores"] = terms, counts, scores
+    def forward(ctx, u, t, cfg: LossConfig, sink: dict, precomputed: bool = False):
+        if precomputed:  # the U-Net's head + loss forward already filled the sink (pis_head_loss_fwd)
+            terms = sink["terms"]
+        else:
+            terms, counts, scores = loss_forward(u, t, cfg)
+            sink["terms"], sink["counts"], sink["scores"] = terms, counts, scores
         ctx.cfg = cfg
         ctx.shape = u.shape
         # produced directly by the U-Net engine? then the backward runs fused with its head
@@ -99,7 +102,8 @@ class _FusedLoss(torch.autograd.Function):
         ctx.gen = getattr(u.grad_fn, "gen", None)
         ctx.save_for_backward(u.detach().contiguous(), t.to(device=u.device, dtype=torch.float32).contiguous(),
                               terms)
-        return terms[0].clone()
+        # a view of the terms buffer (allocated per call, never written again): no copy launch
+        return terms[0]
 
     @staticmethod
     def backward(ctx, g):
@@ -110,11 +114,11 @@ class _FusedLoss(torch.autograd.Function):
         eng = ctx.eng
         if eng is not None and hasattr(eng, "can_fuse_loss") and eng.can_fuse_loss(u, ctx.gen):
             du = eng.fuse_loss_backward(t, ctypes.byref(prm), terms, g)
-            return du.view(ctx.shape), None, None, None
+            return du.view(ctx.shape), None, None, None, None
         du = torch.empty_like(u)
         call("pis_loss_bwd", u.data_ptr(), t.data_ptr(), B, H, W, ctypes.byref(prm), terms.data_ptr(),
              g.data_ptr(), du.data_ptr(), 0, _hip.stream_handle())
-        return du.view(ctx.shape), None, None, None
+        return du.view(ctx.shape), None, None, None, None
 
 
 def fused_loss(u: torch.Tensor, t: torch.Tensor, cfg: LossConfig, sink: dict = None) -> torch.Tensor:
@@ -124,5 +128,13 @@ def fused_loss(u: torch.Tensor, t: torch.Tensor, cfg: LossConfig, sink: dict = N
     if not (torch.is_grad_enabled() and u.requires_grad):
         terms, counts, scores = loss_forward(u, t, cfg)
         sink["terms"], sink["counts"], sink["scores"] = terms, counts, scores
-        return terms[0].clone()
+        return terms[0]
     return _FusedLoss.apply(u, t, cfg, sink)
+
+
+def loss_from_forward(u: torch.Tensor, t: torch.Tensor, cfg: LossConfig, sink: dict) -> torch.Tensor:
+    """The differentiable total loss of terms the U-Net's fused head + loss forward already wrote
+    into ``sink`` (UNet.forward_with_loss): an autograd node with no forward launch of its own."""
+    if not (torch.is_grad_enabled() and u.requires_grad):
+        return sink["terms"][0]
+    return _FusedLoss.apply(u, t, cfg, sink, True)

@@ -75,6 +75,17 @@ class EarlyStopping:
 # step-loop accounting (device side)
 # ----------------------------------------------------------------------------
 
+def _forward_loss(model, images, masks, criterion):
+    """``outputs = model(images); loss = criterion(outputs, masks)`` (src/train.py:108-110,
+    :216-218): this package's U-Net runs its head fused with the loss forward
+    (UNet.forward_with_loss); any other model takes the two calls."""
+    fwd = getattr(model, "forward_with_loss", None)
+    if fwd is not None:
+        return fwd(images, masks, criterion)
+    outputs = model(images)
+    return outputs, criterion(outputs, masks)
+
+
 def _criterion_terms(criterion, outputs, masks):
     """Per-term values of the last criterion call: from the fused launch when the
     criterion is ours, otherwise one extra fused forward on its attributes."""
@@ -243,8 +254,7 @@ def train_epoch(model, dataloader, criterion, optimizer, device, return_componen
             optimizer.zero_grad()
             if bf1 is not None:
                 bf1.before_forward()
-            outputs = model(images)
-            loss = criterion(outputs, masks)
+            outputs, loss = _forward_loss(model, images, masks, criterion)
             terms, scores = _criterion_terms(criterion, outputs, masks)
             meter.add(terms, scores if compute_metrics else None)
             if bf1 is not None:
@@ -273,8 +283,7 @@ def validate(model, dataloader, criterion, device, return_components: bool = Fal
             masks = masks.to(device, non_blocking=True)
             if bf1 is not None:
                 bf1.before_forward()
-            outputs = model(images)
-            criterion(outputs, masks)
+            outputs, _ = _forward_loss(model, images, masks, criterion)
             terms, scores = _criterion_terms(criterion, outputs, masks)
             last = getattr(criterion, "last", {})
             counts = last.get("counts")

@@ -265,6 +265,34 @@ class UNet(nn.Module):
             return eng.forward(x, scales, keep=False)
         return _UNetFunction.apply(x, eng, scales, *params)
 
+    def forward_with_loss(self, x: torch.Tensor, targets: torch.Tensor, criterion) -> Tuple[torch.Tensor, torch.Tensor]:
+        """``u = model(x); loss = criterion(u, targets)`` (src/train.py:108-110) with the head's 1x1 conv +
+        sigmoid and the whole loss forward in ONE kernel (pis_head_loss_fwd: the 64-channel head input
+        is read once, the loss's own pass over u and the targets disappears). Same outputs as the two
+        calls: u, the differentiable loss, and ``criterion.last`` (terms, per-sample counters, scores);
+        the backward is the usual fused head + loss backward. Criteria other than this package's
+        losses, or shapes the fused kernel does not cover, take the two calls."""
+        from .fused import loss_from_forward
+        config = getattr(criterion, "config", None)
+        if not callable(config):
+            u = self(x)
+            return u, criterion(u, targets)
+        cfg = config()
+        t = targets.to(device=x.device, dtype=torch.float32).contiguous()
+        if t.numel() != x.shape[0] * x.shape[2] * x.shape[3]:
+            raise ValueError(f"target shape {tuple(targets.shape)} does not match the input {tuple(x.shape)}")
+        sink: Dict[str, torch.Tensor] = {}
+        eng = self.engine()
+        eng.loss_request = (t, cfg.params(), sink)
+        try:
+            u = self(x)
+        finally:
+            eng.loss_request = None
+        if "terms" not in sink:  # not fusable here: the two calls
+            return u, criterion(u, targets)
+        criterion.last = sink
+        return u, loss_from_forward(u, t, cfg, sink)
+
 
 class _UNetFunction(torch.autograd.Function):
     @staticmethod
@@ -345,6 +373,9 @@ class UNetEngine:
         self._offsets = {id(mod._parameters[pn]): (o, n) for mod, pn, _, _, o, n in model._entries}
         self.last_grad_mode = None
         self.pending_head = None  # dL/du tensor whose head backward already ran fused with the loss
+        # (targets, LossParams, sink) set by UNet.forward_with_loss for the next forward: its head runs
+        # fused with the loss forward (pis_head_loss_fwd) and the loss outputs land in the sink
+        self.loss_request = None
         # HIP events created while a graph capture runs: the captured graph's cross-stream edges
         # were recorded through them, so they are kept (and handed to the StepGraph that owns the
         # graph) instead of being destroyed mid-capture when the local reference goes
@@ -375,6 +406,8 @@ class UNetEngine:
         self.plan_key = key
         self.B, self.H, self.W = B, H, W
         lib = _hip.lib()
+        # the fused head + loss forward's partials (per-block sums, overwritten every call)
+        self.hl_ws = torch.empty((lib.pis_head_loss_fwd_ws(B, H, W) + 15) // 4, dtype=torch.float32, device=dev)
         ws = lib.pis_head_bwd_ws(B * H * W, c)
         if W <= 1024:
             ws = max(ws, lib.pis_head_loss_bwd_ws(B, H, W, c))
@@ -392,7 +425,8 @@ class UNetEngine:
         # weight gradients run on a second stream beside the input-gradient chain (backward)
         self.ws2 = torch.empty_like(self.ws) if self.side_stream else self.ws
         # an owned stream, not one of torch's pooled ones: it takes part in any graph capture of
-        # the step (graph.StepGraph), and is destroyed with the engine rather than handed on
+        # the step (graph.StepGraph); created on the model's device and, when the engine goes,
+        # recycled only into other owned streams of that device (never destroyed: _hip.OwnedStream)
         # (confining this stream to 64 or 128 CUs with a CU mask measured 16 % slower on the step,
         # profiles/r3_q25_ab_env.txt: the two streams time-share the whole chip)
         self._side_owner = _hip.OwnedStream(device=dev) if self.side_stream else None
@@ -594,8 +628,22 @@ class UNetEngine:
             d, dC = d1, Cl
         u = bf["u"] if keep else torch.empty(B, 1, H, W, device=x.device)
         z = bf["z"]
-        call("pis_head_fwd", d.p, d.ld, m.out_conv.weight.data_ptr(), m.out_conv.bias.data_ptr(), z.data_ptr(),
-             u.data_ptr(), B * H * W, c, self._stream())
+        lr, self.loss_request = self.loss_request, None
+        lib = _hip.lib()
+        if lr is not None and lib.pis_head_loss_fwd_ok(B, H, W, c) and d.ld % 4 == 0:
+            # the head + the loss forward in one pass over the head input (forward_with_loss)
+            t, prm, sink = lr
+            dev = x.device
+            terms = torch.empty(_hip.LOSS_NTERMS, dtype=torch.float32, device=dev)
+            counts = torch.empty(B, 3, dtype=torch.int32, device=dev)
+            scores = torch.empty(B, 2, dtype=torch.float32, device=dev)
+            call("pis_head_loss_fwd", d.p, d.ld, m.out_conv.weight.data_ptr(), m.out_conv.bias.data_ptr(),
+                 t.data_ptr(), z.data_ptr(), u.data_ptr(), B, H, W, c, ctypes.byref(prm), terms.data_ptr(),
+                 counts.data_ptr(), scores.data_ptr(), self.hl_ws.data_ptr(), self.hl_ws.numel() * 4, self._stream())
+            sink["terms"], sink["counts"], sink["scores"] = terms, counts, scores
+        else:
+            call("pis_head_fwd", d.p, d.ld, m.out_conv.weight.data_ptr(), m.out_conv.bias.data_ptr(), z.data_ptr(),
+                 u.data_ptr(), B * H * W, c, self._stream())
         m.last_logits = z
         # every forward overwrites the engine's activation buffers: a graph built before it
         # can no longer be backpropagated (its backward raises instead of reading stale data)

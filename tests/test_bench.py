@@ -42,8 +42,9 @@ def test_bench_json_contract():
     # "roofline" is the dominant one of the two conv kernels (the most GPU time per step); both are
     # reported, each against its own bound, with per-launch shapes matching the hook's launch counts
     assert d["roofline"] is d[d["roofline_dominant"]] or d["roofline"] == d[d["roofline_dominant"]]
+    direct = ("roofline_direct_fwd", "roofline_direct_pool", "roofline_direct_dgrad", "roofline_direct_wgrad")
     for name, bound, unit in (("roofline_gemm", "mfma", "TFLOP/s"), ("roofline_fused", "hbm", "GB/s"),
-                              ("roofline_direct", "mfma", "TFLOP/s"), ("roofline_direct_wgrad", "mfma", "TFLOP/s")):
+                              *((k, "mfma", "TFLOP/s") for k in direct)):
         r = d.get(name)
         if name == "roofline_fused" and r is None:
             continue  # every fused-kernel shape may have moved to the direct kernels
@@ -51,10 +52,11 @@ def test_bench_json_contract():
         assert r["bound"] == bound and r["unit"] == unit and 0 < r["frac"] < 1
         assert abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-9
         assert r["launches_per_step"] > 0 and r["avg_launch_ms"] > 0 and r["ms_per_step"] > 0
+        if name in direct:  # per-role algorithmic bytes: the layer table reproduces the hook's launches
+            assert r["algorithmic_bytes_per_launch"] and 0 < r["hbm_frac"] < 1, name
     assert d["roofline_gemm"]["hbm_view"] is not None
     assert d["roofline"]["ms_per_step"] == max(d[k]["ms_per_step"] for k in
-                                               ("roofline_gemm", "roofline_fused", "roofline_direct",
-                                                "roofline_direct_wgrad") if d.get(k))
+                                               ("roofline_gemm", "roofline_fused") + direct if d.get(k))
 
 
 @pytest.mark.gpu

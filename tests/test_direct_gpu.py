@@ -80,7 +80,9 @@ def _fwd(hip, x, w, b, scale, flags, pool=False, ldx_extra=0):
 
 # kernel variants behind pis_tune: key 32 the input gradient's mask prefetch (default on)
 FWD_VARIANTS = [dict(), dict(k32=0)]
-WG_VARIANTS = [dict()]
+# weight gradient: key 34 = 1 (default) the 2-row strip kernel, 0 the 4-row kernel; key 35 = 64: few
+# workgroups, so every block walks many tiles down (and across) column strips and image boundaries
+WG_VARIANTS = [dict(), dict(k34=0), dict(k35=64)]
 
 
 @pytest.mark.parametrize("variant", FWD_VARIANTS)
@@ -186,7 +188,7 @@ def test_direct_mixed_magnitude_chunks(hip):
 
 @pytest.mark.parametrize("variant", WG_VARIANTS)
 @pytest.mark.parametrize("B,H,W,Cin,Cout", [(2, 16, 64, 64, 64), (1, 8, 32, 128, 64), (2, 16, 32, 64, 128),
-                                           (1, 16, 32, 128, 128)])
+                                           (1, 16, 32, 128, 128), (3, 24, 64, 64, 64)])
 def test_direct_wgrad_is_fp32_accurate(hip, B, H, W, Cin, Cout, variant):
     """dW = sum_p dz[p] x[p + tap] and db = sum_p dz[p] (direct fp16x3 weight gradient, split-K slabs
     reduced in fixed order) against float64: as accurate as the fp32 MFMA weight gradient

@@ -10,7 +10,8 @@
   does. Forward, every loss term, the per-sample Dice / IoU counters, every parameter gradient and
   one AdamW step (src/train.py:108-167).
 * C5 shape (1024 x 1024, lambda_RD = 1e-3, lambda_PF = 0) at the ends of the S2 sweep, D = 0.5
-  and D = 100 (run_ablation.py:176-188): the same checks.
+  and D = 100 (run_ablation.py:176-188): the same checks, at B = 1 and at B = 4 (the largest
+  per-rank batch whose float64 oracle fits the GPU box's host memory; C5 runs B = 8 per rank).
 * L_RD at C2 (src/pde.py:124-145): D Lap(u) + f(u) of a near-constant random-init u cancels,
   so fp32 rounding of u is amplified; instead of excluding the term, its error is BOUNDED:
   |L_RD(HIP) - L_RD(fp64)| <= 10 |L_RD(fp32 oracle) - L_RD(fp64)| (or <= 1e-4 relative), i.e.
@@ -49,8 +50,9 @@ def _run(H, W, loss_kws, seed, B=1, keep_net=False):
         net.zero_grad(set_to_none=True)
         crit = DiceBCEPDELoss(pde_weight=kw.get("rd_w", 0.0), phase_field_weight=kw.get("pf_w", 0.0),
                               diffusion_coeff=kw["D"], reaction_threshold=kw["a"], epsilon=kw.get("eps", 0.05))
-        u = net(img.cuda())
-        crit(u, mask.cuda()).backward()
+        # the training step as train_epoch / bench.py run it: the head fused with the loss forward
+        u, loss = net.forward_with_loss(img.cuda(), mask.cuda(), crit)
+        loss.backward()
         torch.cuda.synchronize()
         if decisions is None:
             decisions = net.activation_decisions()
@@ -62,7 +64,9 @@ def _run(H, W, loss_kws, seed, B=1, keep_net=False):
     record = {}
     p64, z64 = rt.unet_forward(ref64, img.double(), {k: v.double() for k, v in scales.items()},
                                decisions=decisions, record=record, return_logits=True)
-    flips = rt.decision_flips(decisions, record, scales)
+    # per site: (flips, worst flip margin, near-ties of the float64 record within 1e-5 of the site's scale)
+    near = rt.near_ties(record, 1e-5, scales)
+    flips = {k: (n, m, near[k]) for k, (n, m) in rt.decision_flips(decisions, record, scales).items()}
     truth = []
     for kw in loss_kws:
         ref64.zero_grad(set_to_none=True)
@@ -82,9 +86,14 @@ def _check_step(hip_run, p64, z64, truth, flips, npx, skip_terms=()):
     for i, k in enumerate(("loss", "dice_loss", "bce_loss", "pde_loss", "phase_field_loss")):
         if k in t64 and k not in skip_terms:
             assert abs(terms[i].item() - t64[k]) <= TOL * abs(t64[k]), (k, terms[i].item(), t64[k])
+    # a flipped decision must be a near-tie of the float64 record (within 1e-5 of the site's scale),
+    # and the flips may be at most half of the record's near-ties (+2): with fp32-class rounding
+    # (~1e-7 of the scale) only a small fraction of the ties within 1e-5 can flip
     bad = {k: v for k, v in flips.items() if v[0]}
-    assert sum(n for n, _ in bad.values()) <= 8 + npx // 8192, bad
-    assert all(margin <= 1e-5 for _, margin in bad.values()), bad
+    assert all(margin <= 1e-5 and n <= nt for n, margin, nt in bad.values()), bad
+    n_near = sum(nt for _, _, nt in flips.values())
+    assert sum(n for n, _, _ in bad.values()) <= 2 + n_near // 2, (bad, n_near)
+    print(f"decision flips {sum(n for n, _, _ in bad.values())} of {n_near} near-ties ({npx} px)")
     worst = sorted(((rel(grads[n], g64[n]), n) for n in g64), reverse=True)
     assert worst[0][0] < TOL, worst[:5]
 
@@ -115,6 +124,29 @@ def test_c5_train_step_d_sweep_ends(hip):
         rd32 = rt.rd_loss(p32.double(), kw["D"], 0.5).item()
         rd64, rd_hip = tr[0]["pde_loss"], run[2][3].item()
         print(f"L_RD at C5, D={kw['D']}: fp64 {rd64:.9e}  HIP {rd_hip:.9e}  fp32 oracle {rd32:.9e}")
+        assert abs(rd_hip - rd64) <= max(10.0 * abs(rd32 - rd64), TOL * abs(rd64)), kw
+
+
+@pytest.mark.timeout(1500)
+def test_c5_batch4_train_step(hip):
+    """BASELINE C5 per rank (run_ablation.py:176-188: 1024 x 1024, lambda_RD = 1e-3, lambda_PF = 0) at
+    B = 4, both ends of the S2 sweep (D = 0.5, D = 100): logits, probabilities, every loss term
+    (L_RD bounded by the fp32 oracle's own error), every parameter gradient against float64 on the
+    HIP decisions. B = 4 is the largest batch whose float64 oracle (forward record + two
+    backwards, ~110 GB of host memory) fits the GPU box's host-memory cap with margin; C5's B = 8
+    per rank would need ~220 GB. B = 4 at 1024^2 is 2x C2's pixel count: the weight gradients'
+    split-K slab counts and slab-reduction regimes, the 1024-wide head / loss rows and the strip
+    weight gradient's multi-strip block ranges at a size B = 1 never reaches."""
+    kws = [dict(rd_w=1e-3, pf_w=0.0, D=D, a=0.5) for D in (0.5, 100.0)]
+    B = 4
+    img, mask, ref, scales, runs, p64, z64, flips, truth = _run(1024, 1024, kws, seed=7, B=B)
+    with torch.no_grad():
+        p32 = ref(img, scales)
+    for kw, run, tr in zip(kws, runs, truth):
+        _check_step(run, p64, z64, tr, flips, B * 1024 * 1024, skip_terms=("pde_loss",))
+        rd32 = rt.rd_loss(p32.double(), kw["D"], 0.5).item()
+        rd64, rd_hip = tr[0]["pde_loss"], run[2][3].item()
+        print(f"L_RD at C5 B=4, D={kw['D']}: fp64 {rd64:.9e}  HIP {rd_hip:.9e}  fp32 oracle {rd32:.9e}")
         assert abs(rd_hip - rd64) <= max(10.0 * abs(rd32 - rd64), TOL * abs(rd64)), kw
 
 

@@ -427,12 +427,13 @@ def test_head_loss_bwd_fused(hip, B, H, W, ldx, kw):
     assert rel_err(db.cpu(), (db_ref + 1).cpu()) < 1e-6
 
 
-def _loss_call(hip, p, t, kw, chain=False, grad_out=None, ws=None):
+def _loss_call(hip, p, t, kw, chain=False, grad_out=None, ws=None, all_terms=True):
     from physics_informed_image_segmentation_amd._hip import LossParams
     import ctypes
     B, H, W = p.shape[0], p.shape[-2], p.shape[-1]
     prm = LossParams(kw.get("dice_w", 0.5), kw.get("bce_w", 0.5), kw.get("rd_w", 0.0), kw.get("pf_w", 0.0),
-                     kw.get("smooth", 1e-6), kw.get("D", 1.0), kw.get("a", 0.5), kw.get("eps", 0.05), 0.5, 1)
+                     kw.get("smooth", 1e-6), kw.get("D", 1.0), kw.get("a", 0.5), kw.get("eps", 0.05), 0.5,
+                     1 if all_terms else 0)
     pd, td = p.contiguous().cuda(), t.contiguous().cuda()
     terms = torch.empty(8, device="cuda")
     counts = torch.empty(B, 3, dtype=torch.int32, device="cuda")
@@ -474,6 +475,113 @@ def test_fused_loss_vs_oracle(hip, shape, kw):
     assert np.array_equal(counts.numpy(), np.stack([i, ph, ts], 1))
     d, u = ln.dice_iou_from_counts(i, ph, ts)
     np.testing.assert_allclose(scores.numpy(), np.stack([d, u], 1), rtol=1e-6)
+
+
+def _c4_prediction(B, H, W, seed):
+    """A prediction-like probability map for the disc masks of rt.synthetic_batch: the mask blurred
+    with noise and squashed into (0, 1), so the stencils see real edges and BCE / Dice real errors."""
+    _, mask = rt.synthetic_batch(B, H, W, seed=42)
+    g = torch.Generator().manual_seed(seed)
+    z = 6.0 * (mask - 0.5) + 2.0 * torch.randn(B, 1, H, W, generator=g)
+    z = F.avg_pool2d(F.pad(z, (2, 2, 2, 2), mode="reflect"), 5, stride=1)
+    return torch.sigmoid(z)[:, 0].float(), mask[:, 0].float()
+
+
+# BASELINE C4 = run_ablation.py:42-83 R1 (Baseline / RD-only / PF-only / RD+PF) at lambda 1e-4, D = 5,
+# a = 0.5, eps = 0.05
+C4_GATINGS = [(0.0, 0.0), (1e-4, 0.0), (0.0, 1e-4), (1e-4, 1e-4)]
+
+
+@pytest.mark.parametrize("rd_w,pf_w", C4_GATINGS)
+def test_fused_loss_c4_grid_vs_oracle(hip, rd_w, pf_w):
+    """C4 at its stated size, (8, 512, 512), through the production gating (no PIS_LOSS_ALL_TERMS: the
+    kernels specialise on the weights, the lambda = 0 instantiation included) on the whole-row band
+    grid the C2 step runs, against the float64 oracle (oracle/loss_numpy.py, src/loss.py:144-160):
+    every term in the total, every pixel of dL/dp (boundaries included), exact per-sample counters."""
+    p, t = _c4_prediction(8, 512, 512, seed=14)
+    kw = dict(rd_w=rd_w, pf_w=pf_w, D=5.0, a=0.5, eps=0.05)
+    terms, counts, scores, dp = _loss_call(hip, p, t, kw, grad_out=0.75, all_terms=False)
+    f = ln.loss_forward(p.numpy(), t.numpy(), **kw)
+    assert terms[0].item() == pytest.approx(f["loss"], rel=1e-5)
+    assert terms[1].item() == pytest.approx(f["dice_loss"], rel=1e-5)
+    assert terms[2].item() == pytest.approx(f["bce_loss"], rel=1e-5)
+    if rd_w > 0:
+        assert terms[3].item() == pytest.approx(f["rd"], rel=1e-4)
+    if pf_w > 0:
+        assert terms[4].item() == pytest.approx(f["pf"], rel=1e-4)
+    gref = ln.loss_backward(p.numpy(), t.numpy(), grad_out=0.75, **kw)
+    assert np.linalg.norm(dp.numpy() - gref) / np.linalg.norm(gref) < 1e-5
+    assert np.abs(dp.numpy() - gref).max() <= 1e-5 * np.abs(gref).max()
+    i, ph, ts = ln.sample_counts(p.numpy(), t.numpy())
+    assert np.array_equal(counts.numpy(), np.stack([i, ph, ts], 1))
+    d, u = ln.dice_iou_from_counts(i, ph, ts)
+    np.testing.assert_allclose(scores.numpy(), np.stack([d, u], 1), rtol=1e-6)
+
+
+def _head_loss_fwd_call(hip, x, ldx, w, b, t, kw, all_terms=False):
+    """pis_head_loss_fwd on x ([B,H,W,ldx], the first 64 channels the head input) -> (z, u, terms,
+    counts, scores) on the host."""
+    from physics_informed_image_segmentation_amd._hip import LossParams
+    B, H, W = t.shape
+    prm = LossParams(0.5, 0.5, kw.get("rd_w", 0.0), kw.get("pf_w", 0.0), 1e-6, kw.get("D", 1.0), kw.get("a", 0.5),
+                     kw.get("eps", 0.05), 0.5, 1 if all_terms else 0)
+    z, u = torch.empty(B, H, W, device="cuda"), torch.empty(B, H, W, device="cuda")
+    terms = torch.empty(8, device="cuda")
+    counts = torch.empty(B, 3, dtype=torch.int32, device="cuda")
+    scores = torch.empty(B, 2, device="cuda")
+    nws = hip.pis_head_loss_fwd_ws(B, H, W)
+    ws = torch.empty(nws // 4 + 1, device="cuda")
+    assert hip.pis_head_loss_fwd_ok(B, H, W, 64) == 1
+    rc = hip.pis_head_loss_fwd(x.data_ptr(), ldx, w.data_ptr(), b.data_ptr(), t.data_ptr(), z.data_ptr(), u.data_ptr(),
+                               B, H, W, 64, ctypes.byref(prm), terms.data_ptr(), counts.data_ptr(), scores.data_ptr(),
+                               ws.data_ptr(), nws, s())
+    assert rc == 0, hip.pis_last_error()
+    torch.cuda.synchronize()
+    return z.cpu(), u.cpu(), terms.cpu(), counts.cpu(), scores.cpu()
+
+
+@pytest.mark.parametrize("B,H,W,ldx", [(2, 64, 64, 64), (1, 48, 128, 128), (3, 2, 64, 64), (1, 40, 1024, 64),
+                                       (2, 37, 512, 64), (8, 512, 512, 64)])
+@pytest.mark.parametrize("rd_w,pf_w", C4_GATINGS)
+def test_head_loss_fwd_fused(hip, B, H, W, ldx, rd_w, pf_w):
+    """pis_head_loss_fwd (the head's 1x1 conv + sigmoid fused with the loss forward, the C2 step's
+    path) == pis_head_fwd then pis_loss_fwd: z and u bitwise, the counters exactly, the terms to fp32
+    summation order; and against the float64 oracle (oracle/loss_numpy.py on the same u): every
+    term in the total, the counters and scores. Shapes: band heights that do not divide H (37),
+    H = 2 (every row a reflect ghost), 1024-wide rows (8 rows per band), the C2 grid (8, 512, 512)
+    under the four R1 gatings (BASELINE C4), a wider row pitch (concat-style ldx)."""
+    from physics_informed_image_segmentation_amd._hip import LossParams
+    g = torch.Generator().manual_seed(31)
+    x = F.relu(torch.randn(B, H, W, ldx, generator=g)).cuda()
+    w = (torch.randn(64, generator=g) * 0.15).cuda()
+    b = torch.tensor([-0.3]).cuda()
+    _, mask = rt.synthetic_batch(B, H, W, seed=42)
+    t = mask[:, 0].contiguous().cuda()
+    kw = dict(rd_w=rd_w, pf_w=pf_w, D=5.0, a=0.5, eps=0.05)
+    z, u, terms, counts, scores = _head_loss_fwd_call(hip, x, ldx, w, b, t, kw)
+    # the unfused pair on the same input
+    z2, u2 = torch.empty(B, H, W, device="cuda"), torch.empty(B, H, W, device="cuda")
+    assert hip.pis_head_fwd(x.data_ptr(), ldx, w.data_ptr(), b.data_ptr(), z2.data_ptr(), u2.data_ptr(), B * H * W, 64,
+                            s()) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(z, z2.cpu()) and torch.equal(u, u2.cpu())
+    ref = _loss_call(hip, u2, t, kw, all_terms=False)
+    np.testing.assert_allclose(terms.numpy(), ref[0].numpy(), rtol=2e-6, atol=1e-12)
+    assert torch.equal(counts, ref[1]) and torch.equal(scores, ref[2])
+    # float64 oracle on the same probabilities
+    f = ln.loss_forward(u.numpy(), t.cpu().numpy(), **kw)
+    assert terms[0].item() == pytest.approx(f["loss"], rel=1e-5)
+    assert terms[1].item() == pytest.approx(f["dice_loss"], rel=1e-5)
+    assert terms[2].item() == pytest.approx(f["bce_loss"], rel=1e-5)
+    if rd_w > 0:
+        assert terms[3].item() == pytest.approx(f["rd"], rel=1e-4)
+    if pf_w > 0:
+        assert terms[4].item() == pytest.approx(f["pf"], rel=1e-4)
+    i, ph, ts = ln.sample_counts(u.numpy(), t.cpu().numpy())
+    assert np.array_equal(counts.numpy(), np.stack([i, ph, ts], 1))
+    # z against fp64 of the same fp32 inputs
+    z64 = (x[..., :64].double() @ w.double() + b.double()).cpu()
+    assert ((z.double() - z64).abs().max() / z64.abs().max()).item() < 1e-6
 
 
 @pytest.mark.parametrize("shape", [(16, 512, 512), (3, 130, 68), (2, 2, 8), (1, 37, 1024), (5, 64, 4096), (4, 5, 20), (64, 512, 512)])
@@ -731,15 +839,18 @@ def test_wgrad_fp16x3_mixed_magnitude_samples(hip, Cin, Cout):
 
 
 @pytest.mark.parametrize("B,H,W,Cin,Cout", [(2, 64, 64, 256, 256), (2, 36, 36, 512, 128), (1, 12, 20, 128, 256)])
-@pytest.mark.parametrize("mags", [(1.0, 1.0), (1.0, 1e-30), (1e-30, 1.0), (1e-9, 1e-9)])
+@pytest.mark.parametrize("mags", [(1.0, 1.0), (1.0, 1e-30), (1e-30, 1.0), (1e-9, 1e-9), (1e-30, 1e-30, 1e-2)])
 def test_wgrad_rowstaged_fp16x3(hip, B, H, W, Cin, Cout, mags):
     """The row-staged fp16x3 Winograd weight-gradient GEMM (pis_tune(31, 1): float4 row loads,
     transposed LDS reads, 32-pixel K-steps, block-wide scales, two register sets in flight) against
     float64, next to the column-staged fp16x3 kernel (31 = 0) and the fp32 MFMA path (14 = 0):
-    K-step counts from 1 to 16 per split with ragged tails (T = 162, 15), and per-sample dz
-    magnitudes 1e30 apart in both orders (the scale jumps inside one accumulation chain)."""
+    K-step counts from 1 to 16 per split with ragged tails (T = 162, 15), per-sample dz
+    magnitudes 1e30 apart in both orders (the scale jumps inside one accumulation chain), and
+    BOTH operands small (dz ~ 1e-30, x ~ 1e-2: the two power-of-two scales multiply to more than
+    fp32's range, so the accumulator units must stay two factors — ADVICE r3)."""
     g = torch.Generator().manual_seed(71)
-    x = F.relu(torch.randn(B, Cin, H, W, generator=g, dtype=torch.float64)).float().double()
+    xm = mags[2] if len(mags) > 2 else 1.0
+    x = (F.relu(torch.randn(B, Cin, H, W, generator=g, dtype=torch.float64)) * xm).float().double()
     dz = torch.randn(B, Cout, H, W, generator=g, dtype=torch.float64)
     for i in range(B):
         dz[i] *= mags[i % 2]

@@ -265,3 +265,45 @@ def test_full_size_forward_and_loss_c2_shape(hip):
     got = crit.last["terms"][:5].cpu()
     for i, k in enumerate(("loss", "dice_loss", "bce_loss", "pde_loss", "phase_field_loss")):
         assert abs(got[i].item() - t[k].item()) <= TOL * abs(t[k].item()), k
+
+
+@pytest.mark.parametrize("B,H,W", [(2, 64, 64), (1, 48, 128)])
+@pytest.mark.parametrize("loss_kw", [dict(), PDE_KW])
+def test_forward_with_loss_matches_two_calls(hip, B, H, W, loss_kw):
+    """UNet.forward_with_loss (the head fused with the loss forward, pis_head_loss_fwd: what
+    train_epoch and bench.py run) == ``u = net(x); loss = crit(u, t)``: u and the logits bitwise, the
+    loss terms to fp32 summation order, the per-sample counters exactly, every parameter gradient
+    to 1e-5 (only the loss sums' rounding differs), in train mode with injected Dropout2d masks;
+    and the eval / no-grad path."""
+    from physics_informed_image_segmentation_amd import DiceBCEPDELoss
+    img, mask = rt.synthetic_batch(B, H, W, seed=11)
+    kw = dict(pde_weight=loss_kw.get("rd_w", 0.0), phase_field_weight=loss_kw.get("pf_w", 0.0),
+              diffusion_coeff=loss_kw.get("D", 1.0), reaction_threshold=0.5, epsilon=loss_kw.get("eps", 0.05))
+    runs = []
+    for fused in (False, True):
+        net, ref = make_pair(5)
+        net.train()
+        net.set_dropout_scales(rt.make_drop_scales(ref, B, torch.Generator().manual_seed(2)))
+        crit = DiceBCEPDELoss(**kw)
+        x, t = img.cuda(), mask.cuda()
+        if fused:
+            u, loss = net.forward_with_loss(x, t, crit)
+        else:
+            u = net(x)
+            loss = crit(u, t)
+        loss.backward()
+        torch.cuda.synchronize()
+        runs.append((u.detach().cpu(), net.last_logits.detach().cpu(), loss.detach().cpu(), crit.last["terms"].cpu(),
+                     crit.last["counts"].cpu(), {n: p.grad.detach().cpu().clone() for n, p in net.named_parameters()}))
+        net.eval()
+        with torch.no_grad():
+            ue, le = net.forward_with_loss(x, t, crit) if fused else (net(x), crit(net(x), t))
+            runs[-1] += (ue.cpu(), le.cpu())
+    a, b = runs
+    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
+    np.testing.assert_allclose(b[3].numpy(), a[3].numpy(), rtol=2e-6, atol=1e-12)
+    assert b[2].item() == pytest.approx(a[2].item(), rel=2e-6)
+    assert torch.equal(a[4], b[4])
+    worst = max(rel(b[5][n], a[5][n]) for n in a[5])
+    assert worst < 1e-5, worst
+    assert torch.equal(a[6], b[6]) and b[7].item() == pytest.approx(a[7].item(), rel=2e-6)
