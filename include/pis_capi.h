@@ -149,7 +149,11 @@ int pis_version(void);
 #define PIS_TUNE_DIRECT_WBLOCKS 35 /* target workgroups of the strip weight gradient (key 34 = 1): default 512 (two per
                                       CU); the split count is this / (Cout/64 * Cin/64), a multiple of 8 */
 #define PIS_TUNE_HEAD_LOSS_ROWS 36 /* pis_head_loss_fwd: image rows per block (0, default: 8192 / W, at most 16) */
-#define PIS_TUNE_NKEYS 37
+#define PIS_TUNE_DIRECT_WGRAD_ALL 37 /* 1: the direct strip weight gradient (key 34 = 1) for EVERY 3x3 layer it covers
+                                        (Cin, Cout % 64, H % 4, W % 32), the Winograd layers' forward / input
+                                        gradient unchanged (no kept input transform, no E half of the dz pass);
+                                        0 (default): the weight gradient follows key 29's layer policy */
+#define PIS_TUNE_NKEYS 38
 #define PIS_DEBUG_NOLOAD (1 << 16)
 int pis_tune(int key, int value);
 /* Tooling (tools/bench_gemm.py): time one batched NT GEMM kernel variant in isolation,

@@ -715,13 +715,21 @@ constexpr int SZ_ITEMS = SW_P * 8, SX_ITEMS = SH_P * 8;      // 8-channel groups
 constexpr int SLDS_BYTES = 2 * (SZ_HALFS + SX_HALFS) * 2;
 constexpr int SBIAS_BYTES = 256 * 8 * 4;  // per-thread bias partials (8 channels), in LDS: 8 VGPRs fewer
 
-template <bool TW = false>  // TW: timing twin (pis_tune key 2 != 0 only)
+// RING (pis_tune key 34 = 2): the x halo rows live in a 4-slot LDS ring (image row h in slot h & 3),
+// so a tile whose predecessor was the tile above it loads, splits and stores only its 2 NEW halo
+// rows (68 of 136 pixels: the split VALU work and LDS stores of x halve, 1.06x instead of 2.1x the
+// x fetches); the first tile of a strip (rp == 0, or the block's first tile) loads all 4. The tile's
+// x scale covers the kept rows too (their max is the previous tile's new-row max); when h3_keep
+// re-chooses it, the kept rows' fp16 planes are re-expressed in LDS by the exact power-of-two ratio
+// (a rise cannot overflow: the new scale fits the tile max; a fall may flush lo bits below 2^-24 of
+// the scaled range, the block-floating-point floor every element already has).
+template <bool TW = false, bool RING = false>  // TW: timing twin (pis_tune key 2 != 0 only)
 __global__ __launch_bounds__(256, 2) void conv3x3_wgrad_strip_kernel(DirectWArgs g) {
   constexpr int NW = 4, NT = 64 * NW, SZ_PER_T = SZ_ITEMS / NT, SX_PER_T = (SX_ITEMS + NT - 1) / NT;
   constexpr int NTAP = 9;
   __shared__ __attribute__((aligned(16))) char smem[SLDS_BYTES + SBIAS_BYTES + 64];
   _Float16* sz = reinterpret_cast<_Float16*>(smem);                     // [plane][64][64]
-  _Float16* sx = reinterpret_cast<_Float16*>(smem + 2 * SZ_HALFS * 2);  // [plane][136][64]
+  _Float16* sx = reinterpret_cast<_Float16*>(smem + 2 * SZ_HALFS * 2);  // [plane][136][64] (RING: 4 slots x 34)
   f32x4* sbias = reinterpret_cast<f32x4*>(smem + SLDS_BYTES);           // [256 threads][2] bias partials
   float* red = reinterpret_cast<float*>(smem + SLDS_BYTES + SBIAS_BYTES);  // [2][NW] wave maxima
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -741,6 +749,8 @@ __global__ __launch_bounds__(256, 2) void conv3x3_wgrad_strip_kernel(DirectWArgs
   const int tps = (ntile + g.splits - 1) / g.splits;
   const int t_begin = split * tps, t_end = min(ntile, t_begin + tps);
   const bool do_bias = g.part_bias != nullptr && c0 == 0;
+  // RING: tile t loads all 4 halo rows when it starts a strip (or the block's range), else rows 2, 3
+  auto full_tile = [&](int t) { return !RING || t == t_begin || (t % nrp) == 0; };
 
   f32x4 zr[SZ_PER_T][2], xr[SX_PER_T][2];
   auto gload = [&](int t) __attribute__((always_inline)) {
@@ -748,6 +758,8 @@ __global__ __launch_bounds__(256, 2) void conv3x3_wgrad_strip_kernel(DirectWArgs
     const int b = t / per_img, rem = t - b * per_img, col = rem / nrp, rp = rem - col * nrp;
     const int pr0 = SW_H * rp, pc0 = SW_W * col;
     const size_t img = (size_t)b * g.H * g.W;
+    const bool full = full_tile(t);
+    const int nx = full ? SX_ITEMS : SX_ITEMS / 2, r_off = full ? 0 : 2;  // block-uniform
 #pragma unroll
     for (int j = 0; j < SZ_PER_T; ++j) {
       const int i = tid + NT * j, px = i >> 3, cg = i & 7;
@@ -759,8 +771,8 @@ __global__ __launch_bounds__(256, 2) void conv3x3_wgrad_strip_kernel(DirectWArgs
     for (int j = 0; j < SX_PER_T; ++j) {
       const int i = tid + NT * j, q = i >> 3, cg = i & 7;
       xr[j][0] = xr[j][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (i < SX_ITEMS) {  // the last item: wave 0 only (wave-uniform)
-        const int qr = q / SH_W, qc = q - qr * SH_W, row = pr0 - 1 + qr, cl = pc0 - 1 + qc;
+      if (i < nx) {  // wave-uniform bounds
+        const int qr = q / SH_W + r_off, qc = q - (q / SH_W) * SH_W, row = pr0 - 1 + qr, cl = pc0 - 1 + qc;
         if (row >= 0 && row < g.H && cl >= 0 && cl < g.W) {
           const float* p = g.x + (img + (size_t)row * g.W + cl) * g.ldx + c0 + 8 * cg;
           xr[j][0] = *reinterpret_cast<const f32x4*>(p);
@@ -778,6 +790,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_wgrad_strip_kernel(DirectWArgs
   // bias partials, channels n0 + 8 (tid & 7) + e: each thread's own LDS slot (no barrier needed)
   if (do_bias) sbias[2 * tid] = sbias[2 * tid + 1] = f32x4{0.f, 0.f, 0.f, 0.f};
   float sz_cur = 0.f, sx_cur = 0.f, sz_min = __builtin_inff(), sx_min = __builtin_inff();
+  float mx_prev = 0.f;  // RING: max |x| of the rows the previous tile loaded (this tile's kept rows)
 
   // lane roles in the transposed reads: 16-lane group gq, its row q and 8-B column slot p
   const int gq = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
@@ -787,6 +800,10 @@ __global__ __launch_bounds__(256, 2) void conv3x3_wgrad_strip_kernel(DirectWArgs
   if (t_begin < t_end) gload(t_begin);
 #pragma unroll 1
   for (int t = t_begin; t < t_end; ++t) {
+    const int rp = (t - (t / per_img) * per_img) % nrp;
+    const bool full = full_tile(t);
+    // RING: halo row k (0..3, image row 2 rp - 1 + k) lives in slot (2 rp - 1 + k) & 3
+    const int slot0 = RING ? ((2 * rp + 3) & 3) : 0;
     if (!(TW && (g.dbg & 2) && t != t_begin)) {
       // 1. block maxima of the staged operands (+ the bias partials from the raw dz)
       float mz = 0.f, mx = 0.f;
@@ -819,11 +836,29 @@ __global__ __launch_bounds__(256, 2) void conv3x3_wgrad_strip_kernel(DirectWArgs
       // at a time); the split planes into LDS
       mz = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
       mx = fmaxf(fmaxf(red[NW], red[NW + 1]), fmaxf(red[NW + 2], red[NW + 3]));
+      const float mx_loaded = mx;
+      if (RING && !full) mx = fmaxf(mx, mx_prev);  // the kept rows belong to this tile too
+      mx_prev = mx_loaded;
       const float sz_new = h3_keep(sz_cur, mz, sz_min), sx_new = h3_keep(sx_cur, mx, sx_min);
       if (sz_cur > 0.f && (sz_new != sz_cur || sx_new != sx_cur)) {
         const float fz = sz_new / sz_cur, fx = sx_new / sx_cur;
 #pragma unroll
         for (int k = 0; k < NTAP; ++k) acc[k] = (acc[k] * fz) * fx;
+      }
+      if (RING && !full && sx_cur > 0.f && sx_new != sx_cur) {
+        // the kept rows (halo rows 0, 1: slots slot0, slot0 + 1) re-expressed in the new scale
+        // (the ratio, up to 2^32, is not an fp16 number: the products are formed in fp32)
+        const float f = sx_new / sx_cur;
+        for (int e = tid; e < 2 * 2 * SH_W * 8; e += NT) {  // (plane, row, pixel, 8-half chunk)
+          const int pl = e / (2 * SH_W * 8), rem2 = e - pl * (2 * SH_W * 8);
+          const int rk = rem2 / (SH_W * 8), pc = rem2 - rk * (SH_W * 8);
+          const int hp = ((slot0 + rk) & 3) * SH_W + (pc >> 3);
+          _Float16* ptr = &sx[pl * SX_HALFS + wsw64(hp, pc & 7)];
+          f16x8 v = *reinterpret_cast<f16x8*>(ptr);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) v[k] = (_Float16)((float)v[k] * f);
+          *reinterpret_cast<f16x8*>(ptr) = v;
+        }
       }
       sz_cur = sz_new;
       sx_cur = sx_new;
@@ -836,15 +871,17 @@ __global__ __launch_bounds__(256, 2) void conv3x3_wgrad_strip_kernel(DirectWArgs
         *reinterpret_cast<u32x4*>(&sz[wsw64(px, cg)]) = u32x4{h0[0], h0[1], h1[0], h1[1]};
         *reinterpret_cast<u32x4*>(&sz[SZ_HALFS + wsw64(px, cg)]) = u32x4{l0[0], l0[1], l1[0], l1[1]};
       }
+      const int nx = full ? SX_ITEMS : SX_ITEMS / 2, r_off = full ? 0 : 2;
 #pragma unroll
       for (int j = 0; j < SX_PER_T; ++j) {
         const int i = tid + NT * j, qq = i >> 3, cg = i & 7;
-        if (i < SX_ITEMS) {
+        if (i < nx) {
+          const int qr = qq / SH_W, row = RING ? (((slot0 + qr + r_off) & 3) * SH_W + (qq - qr * SH_W)) : qq;
           u32x2 h0, l0, h1, l1;
           split2h_x4(xr[j][0] * sx_cur, h0, l0);
           split2h_x4(xr[j][1] * sx_cur, h1, l1);
-          *reinterpret_cast<u32x4*>(&sx[wsw64(qq, cg)]) = u32x4{h0[0], h0[1], h1[0], h1[1]};
-          *reinterpret_cast<u32x4*>(&sx[SX_HALFS + wsw64(qq, cg)]) = u32x4{l0[0], l0[1], l1[0], l1[1]};
+          *reinterpret_cast<u32x4*>(&sx[wsw64(row, cg)]) = u32x4{h0[0], h0[1], h1[0], h1[1]};
+          *reinterpret_cast<u32x4*>(&sx[SX_HALFS + wsw64(row, cg)]) = u32x4{l0[0], l0[1], l1[0], l1[1]};
         }
       }
       __syncthreads();
@@ -869,7 +906,8 @@ __global__ __launch_bounds__(256, 2) void conv3x3_wgrad_strip_kernel(DirectWArgs
         const int r = tap / 3, s = tap % 3;
         // B = x (k pixels, columns c): halo pixel (rr + r, cc0 + 8 kh + q (+ 4) + s), channels of cgB
         f16x8 bb[2];
-        const int hp = (rr + r) * SH_W + cc0 + 8 * kh + q + s;
+        const int hrow = RING ? ((slot0 + rr + r) & 3) : (rr + r);
+        const int hp = hrow * SH_W + cc0 + 8 * kh + q + s;
 #pragma unroll
         for (int pl = 0; pl < 2; ++pl) {
           const _Float16* base = sx + pl * SX_HALFS;
@@ -910,9 +948,14 @@ __global__ __launch_bounds__(256, 2) void conv3x3_wgrad_strip_kernel(DirectWArgs
   }
 }
 
+static bool direct_w_strip() { return tune_get(PIS_TUNE_DIRECT_WSTRIP) != 0; }
+
 bool direct_w_wanted(int B, int H, int W, int Cin, int Cout, int ldx, int ldz) {
-  return B > 0 && H % WT_H == 0 && W % WT_W == 0 && Cin % 64 == 0 && Cout % 64 == 0 && ldz % 4 == 0 &&
-         direct_h3_wanted(H, W, Cin, Cout, ldx);
+  if (!(B > 0 && H % WT_H == 0 && W % WT_W == 0 && Cin % 64 == 0 && Cout % 64 == 0 && ldz % 4 == 0 && ldx % 4 == 0))
+    return false;
+  // key 37: every layer the strip kernel covers, whatever its forward / input gradient run
+  if (tune_get(PIS_TUNE_DIRECT_WGRAD_ALL) != 0 && direct_w_strip()) return true;
+  return direct_h3_wanted(H, W, Cin, Cout, ldx);
 }
 
 static int direct_w_splits(int B, int H, int W, int Cin, int Cout) {
@@ -931,8 +974,6 @@ static int direct_ws_splits(int B, int H, int W, int Cin, int Cout) {
   if (sp >= 8) sp &= ~7;
   return std::max(1, std::min(sp, ntile));
 }
-
-static bool direct_w_strip() { return tune_get(PIS_TUNE_DIRECT_WSTRIP) != 0; }
 
 size_t direct_w_ws_bytes(int B, int H, int W, int Cin, int Cout) {
   // room for either kernel (the knobs may change between the size query and the launch)
@@ -957,10 +998,15 @@ int launch_direct_wgrad(const float* x, int ldx, const float* dz, int ldz, float
   const double flop = 2.0 * 9 * (double)B * H * W * Cin * Cout;
   const dim3 grid(g.splits * pairs);
   launch_hook("direct_wgrad_h3", 0, s, flop);
-  if (strip && g.dbg)
-    hipLaunchKernelGGL((conv3x3_wgrad_strip_kernel<true>), grid, dim3(256), 0, s, g);
+  const bool ring = tune_get(PIS_TUNE_DIRECT_WSTRIP) == 2;
+  if (strip && g.dbg && ring)
+    hipLaunchKernelGGL((conv3x3_wgrad_strip_kernel<true, true>), grid, dim3(256), 0, s, g);
+  else if (strip && g.dbg)
+    hipLaunchKernelGGL((conv3x3_wgrad_strip_kernel<true, false>), grid, dim3(256), 0, s, g);
+  else if (strip && ring)
+    hipLaunchKernelGGL((conv3x3_wgrad_strip_kernel<false, true>), grid, dim3(256), 0, s, g);
   else if (strip)
-    hipLaunchKernelGGL((conv3x3_wgrad_strip_kernel<false>), grid, dim3(256), 0, s, g);
+    hipLaunchKernelGGL((conv3x3_wgrad_strip_kernel<false, false>), grid, dim3(256), 0, s, g);
   else if (g.dbg)
     hipLaunchKernelGGL((conv3x3_wgrad_h3_kernel<true>), grid, dim3(256), 0, s, g);
   else

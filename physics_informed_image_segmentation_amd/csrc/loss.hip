@@ -752,15 +752,19 @@ __global__ __launch_bounds__(256) void head_loss_fwd_kernel(HeadLossFwdArgs h) {
   const f32x4 wv = *reinterpret_cast<const f32x4*>(h.w + 4 * sub);
   const float bias = h.bias[0];
   // 1. u of the staged rows: a chunk is 16 PP consecutive pixels of one staged row (W % (16 PP) == 0),
-  // PP per 16-lane group, every load of the chunk issued before its sums
+  // PP per 16-lane group; two register sets, so the next chunk's loads are in flight while this
+  // one's sums run (at one block per CU nothing else would cover the HBM latency)
   const int cpr = W / (16 * PP), nchunk = (nr + 2) * cpr;
-  for (int ch = 0; ch < nchunk; ++ch) {
+  f32x4 xa[PP], xn[PP];
+  auto load = [&](f32x4 (&xv)[PP], int ch) __attribute__((always_inline)) {
     const int r = ch / cpr, x0 = (ch - r * cpr) * (16 * PP) + grp;  // block-uniform r
     const int gy = clampi(refl(y0 - 1 + r, H), 0, H - 1);
     const float* row = xb + (size_t)gy * W * h.ldx;
-    f32x4 xv[PP];
 #pragma unroll
     for (int j = 0; j < PP; ++j) xv[j] = *reinterpret_cast<const f32x4*>(row + (size_t)(x0 + 16 * j) * h.ldx);
+  };
+  auto head = [&](const f32x4 (&xv)[PP], int ch) __attribute__((always_inline)) {
+    const int r = ch / cpr, x0 = (ch - r * cpr) * (16 * PP) + grp;
     const bool interior = r >= 1 && r <= nr;
     const size_t orow = (size_t)b * HW + (size_t)(y0 - 1 + r) * W;
 #pragma unroll
@@ -783,6 +787,13 @@ __global__ __launch_bounds__(256) void head_loss_fwd_kernel(HeadLossFwdArgs h) {
         }
       }
     }
+  };
+  if (nchunk > 0) load(xa, 0);
+  for (int ch = 0; ch < nchunk; ch += 2) {  // ping-pong register sets (no copies)
+    if (ch + 1 < nchunk) load(xn, ch + 1);
+    head(xa, ch);
+    if (ch + 2 < nchunk) load(xa, ch + 2);
+    if (ch + 1 < nchunk) head(xn, ch + 1);
   }
   // the targets of this thread's items in flight across the barriers (TX threads per row, RY rows
   // per pass; item = 4 pixels)

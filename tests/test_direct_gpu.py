@@ -82,7 +82,7 @@ def _fwd(hip, x, w, b, scale, flags, pool=False, ldx_extra=0):
 FWD_VARIANTS = [dict(), dict(k32=0)]
 # weight gradient: key 34 = 1 (default) the 2-row strip kernel, 0 the 4-row kernel; key 35 = 64: few
 # workgroups, so every block walks many tiles down (and across) column strips and image boundaries
-WG_VARIANTS = [dict(), dict(k34=0), dict(k35=64)]
+WG_VARIANTS = [dict(), dict(k34=0), dict(k35=64), dict(k34=2), dict(k34=2, k35=64)]
 
 
 @pytest.mark.parametrize("variant", FWD_VARIANTS)
@@ -257,15 +257,50 @@ def test_direct_wgrad_scales_any_magnitude(hip, B, H, W, Cin, Cout, variant):
         assert errs["direct"] < 5e-6, (case, errs)
 
 
+@pytest.mark.parametrize("variant", WG_VARIANTS)
+def test_direct_wgrad_x_magnitude_down_the_strip(hip, variant):
+    """x whose magnitude changes down the image (rows 0-7 ~1, 8-15 ~1e-12, 16-23 ~1e9): the strip
+    kernels' tiles walk down a column, so the x scale is re-chosen inside one accumulation chain and
+    (ring variant, key 34 = 2) the kept halo rows are re-expressed in the new scale in LDS — finite
+    and within 1.25x of the fp32 MFMA path's error against float64."""
+    B, H, W, Cin, Cout = 2, 24, 64, 64, 128
+    g = torch.Generator().manual_seed(67)
+    x = F.relu(torch.randn(B, Cin, H, W, generator=g, dtype=torch.float64))
+    x[:, :, 8:16] *= 1e-12
+    x[:, :, 16:] *= 1e9
+    x = x.float().double()
+    dz = torch.randn(B, Cout, H, W, generator=g, dtype=torch.float64).float().double()
+    dw_ref = torch.nn.grad.conv2d_weight(x, (Cout, Cin, 3, 3), dz, padding=1)
+    xd = nhwc(x.float()).cuda()
+    errs = {}
+    for name, knobs in (("direct", {**DIRECT, **variant}), ("native", dict(k29=0, k14=0))):
+        with Knobs(hip, **knobs):
+            nws = hip.pis_conv3x3_wgrad_ws(B, H, W, Cin, Cout)
+            ws = torch.empty(nws // 4 + 1, device="cuda")
+            dw = torch.empty(Cout, 3, 3, Cin, device="cuda")
+            rc = hip.pis_conv3x3_wgrad(xd.data_ptr(), Cin, nhwc(dz.float()).cuda().data_ptr(), Cout, dw.data_ptr(),
+                                       0, B, H, W, Cin, Cout, 0, ws.data_ptr(), nws, s())
+            assert rc == 0, hip.pis_last_error()
+            torch.cuda.synchronize()
+        dwc = dw.cpu().double().permute(0, 3, 1, 2)
+        assert torch.isfinite(dwc).all(), name
+        errs[name] = rel(dwc, dw_ref)
+    assert errs["direct"] <= 1.25 * errs["native"] + 1e-9, errs
+    assert errs["direct"] < 5e-6, errs
+
+
+@pytest.mark.parametrize("knobs", [dict(k29=2), dict(k37=1), dict(k37=1, k35=64), dict(k37=1, k34=2)])
 @pytest.mark.parametrize("loss_kw", [dict(), dict(rd_w=1e-2, pf_w=1e-2, D=5.0, a=0.5, eps=0.05)])
-def test_train_step_with_direct_convs(hip, loss_kw):
+def test_train_step_with_direct_convs(hip, loss_kw, knobs):
     """The whole training step with every eligible conv on the direct kernels (key 29 = 2: forward
-    with the fused pool, input gradients from the original weights, weight gradients): outputs,
+    with the fused pool, input gradients from the original weights, weight gradients), or only the
+    weight gradients everywhere on the direct strip kernel beside the Winograd forward / input
+    gradients (key 37 = 1; with few workgroups, key 35 = 64, each walking many strips): outputs,
     loss terms and every parameter gradient against the float64 oracle on the HIP decisions at
     the north-star 1e-4 (tests/test_unet_gpu.py's check)."""
     import importlib
     tu = importlib.import_module("test_unet_gpu")
-    with Knobs(hip, k29=2):
+    with Knobs(hip, **knobs):
         net, ref, u, crit, p_ref, terms, ref64 = tu._step_pair(2, 64, 64, loss_kw)
     assert tu.rel(u, p_ref) < 1e-4
     got = crit.last["terms"].cpu()

@@ -33,9 +33,20 @@ def rel(a, b):
     return ((a - b).norm() / max(b.norm().item(), 1e-30)).item()
 
 
-def _run(H, W, loss_kws, seed, B=1, keep_net=False):
+def _progress(capsys):
+    """A line to the real stdout (past pytest's capture) per phase of a long test: the GPU box takes a
+    command that prints nothing for 3 minutes for hung, and the float64 oracle of a C5-size step
+    runs for minutes."""
+    def log(msg):
+        with capsys.disabled():
+            print(f"  [{msg}]", flush=True)
+    return log
+
+
+def _run(H, W, loss_kws, seed, B=1, keep_net=False, log=None):
     """One HIP training step per loss config (same weights, same dropout masks) and the float64
     oracle on the first run's decisions (one forward, one backward per config)."""
+    log = log or (lambda msg: None)
     from physics_informed_image_segmentation_amd import DiceBCEPDELoss, UNet
     img, mask = rt.synthetic_batch(B, H, W, seed=seed)
     torch.manual_seed(seed)
@@ -59,6 +70,7 @@ def _run(H, W, loss_kws, seed, B=1, keep_net=False):
         hip_runs.append((u.detach().cpu(), net.last_logits.detach().cpu(), crit.last["terms"].cpu(),
                          {n: p.grad.detach().cpu().clone() for n, p in net.named_parameters()},
                          crit.last["counts"].cpu()))
+    log(f"HIP steps done ({B}x{H}x{W}); float64 oracle forward")
     ref64 = rt.UNetRef().double().train()
     ref64.load_state_dict(ref.state_dict())
     record = {}
@@ -69,6 +81,7 @@ def _run(H, W, loss_kws, seed, B=1, keep_net=False):
     flips = {k: (n, m, near[k]) for k, (n, m) in rt.decision_flips(decisions, record, scales).items()}
     truth = []
     for kw in loss_kws:
+        log(f"float64 oracle backward {kw}")
         ref64.zero_grad(set_to_none=True)
         t64 = rt.loss_terms(p64, mask.double(), **kw)
         t64["loss"].backward(retain_graph=True)
@@ -128,7 +141,7 @@ def test_c5_train_step_d_sweep_ends(hip):
 
 
 @pytest.mark.timeout(1500)
-def test_c5_batch4_train_step(hip):
+def test_c5_batch4_train_step(hip, capsys):
     """BASELINE C5 per rank (run_ablation.py:176-188: 1024 x 1024, lambda_RD = 1e-3, lambda_PF = 0) at
     B = 4, both ends of the S2 sweep (D = 0.5, D = 100): logits, probabilities, every loss term
     (L_RD bounded by the fp32 oracle's own error), every parameter gradient against float64 on the
@@ -139,7 +152,9 @@ def test_c5_batch4_train_step(hip):
     weight gradient's multi-strip block ranges at a size B = 1 never reaches."""
     kws = [dict(rd_w=1e-3, pf_w=0.0, D=D, a=0.5) for D in (0.5, 100.0)]
     B = 4
-    img, mask, ref, scales, runs, p64, z64, flips, truth = _run(1024, 1024, kws, seed=7, B=B)
+    log = _progress(capsys)
+    img, mask, ref, scales, runs, p64, z64, flips, truth = _run(1024, 1024, kws, seed=7, B=B, log=log)
+    log("fp32 oracle forward (the L_RD bound)")
     with torch.no_grad():
         p32 = ref(img, scales)
     for kw, run, tr in zip(kws, runs, truth):
@@ -150,7 +165,7 @@ def test_c5_batch4_train_step(hip):
         assert abs(rd_hip - rd64) <= max(10.0 * abs(rd32 - rd64), TOL * abs(rd64)), kw
 
 
-def test_c2_batch8_train_step(hip):
+def test_c2_batch8_train_step(hip, capsys):
     """BASELINE configs[1] exactly: B = 8, 512 x 512, Stage II (lambda_RD = lambda_PF = 1e-4, D = 5,
     a = 0.5, eps = 0.05), train mode with injected Dropout2d masks. Logits, probabilities, every
     loss term (L_RD bounded by the fp32 oracle's own error), every parameter gradient against
@@ -159,7 +174,8 @@ def test_c2_batch8_train_step(hip):
     from physics_informed_image_segmentation_amd import AdamW
     kw = dict(rd_w=1e-4, pf_w=1e-4, D=5.0, a=0.5, eps=0.05)
     B = 8
-    img, mask, ref, scales, runs, p64, z64, flips, truth, net = _run(512, 512, [kw], seed=42, B=B, keep_net=True)
+    img, mask, ref, scales, runs, p64, z64, flips, truth, net = _run(512, 512, [kw], seed=42, B=B, keep_net=True,
+                                                                     log=_progress(capsys))
     _check_step(runs[0], p64, z64, truth[0], flips, B * 512 * 512, skip_terms=("pde_loss",))
     u, z, terms, grads, counts = runs[0]
     with torch.no_grad():

@@ -65,7 +65,7 @@ def main():
         model, opt = models[name]
         UNetEngine.filter_ahead = str(dict(variants)[name].get("fa", fa_default))
         opt.zero_grad()
-        crit(model(x), t).backward()
+        model.forward_with_loss(x, t, crit)[1].backward()  # the step as bench.py / train_epoch run it
         opt.step()
 
     def run(name, kv):
