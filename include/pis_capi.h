@@ -142,18 +142,25 @@ int pis_version(void);
                                     one block per CU, next chunk's weights by LDS-DMA and its halo split while this
                                     chunk multiplies) measured 3-14 % slower than the 4-wave kernel
                                     (profiles/r3_q26_direct_w8.txt); ignored */
-#define PIS_TUNE_DIRECT_WSTRIP 34 /* direct fp16x3 weight gradient (key 29): 1 (default) 2-row tiles walked down a
-                                    column strip per block (x halo rows re-read from L2, <= 256 registers per lane,
-                                    51 KB LDS: two blocks per CU, or one beside a main-stream block), 0 the round-3
-                                    4-row kernel (497 registers, one wave fills a SIMD) */
+#define PIS_TUNE_DIRECT_WSTRIP 34 /* direct fp16x3 weight gradient (key 29): 0 (default) the round-3 4-row kernel (497
+                                    registers: one wave fills a SIMD, so main-stream blocks wait for its CUs);
+                                    1 2-row tiles walked down a column strip per block (250 registers, 59 KB LDS:
+                                    two blocks per CU, or one beside a main-stream block), 2 the same with the x
+                                    halo rows in an LDS ring. Measured (tools/ab_tune.py, one model): 1 / 2 are
+                                    1.6-1.8 % SLOWER on the C2 step — the co-resident main-stream input gradients
+                                    slow down more than the lockout cost (profiles/r4_a_*, r4_b_ab_wblk.txt) */
 #define PIS_TUNE_DIRECT_WBLOCKS 35 /* target workgroups of the strip weight gradient (key 34 = 1): default 512 (two per
                                       CU); the split count is this / (Cout/64 * Cin/64), a multiple of 8 */
 #define PIS_TUNE_HEAD_LOSS_ROWS 36 /* pis_head_loss_fwd: image rows per block (0, default: 8192 / W, at most 16) */
-#define PIS_TUNE_DIRECT_WGRAD_ALL 37 /* 1: the direct strip weight gradient (key 34 = 1) for EVERY 3x3 layer it covers
-                                        (Cin, Cout % 64, H % 4, W % 32), the Winograd layers' forward / input
+#define PIS_TUNE_DIRECT_WGRAD_ALL 37 /* 1: the direct strip weight gradient (key 34 = 1 or 2) for EVERY 3x3 layer it
+                                        covers (Cin, Cout % 64, H % 4, W % 32), the Winograd layers' forward / input
                                         gradient unchanged (no kept input transform, no E half of the dz pass);
-                                        0 (default): the weight gradient follows key 29's layer policy */
-#define PIS_TUNE_NKEYS 38
+                                        0 (default): the weight gradient follows key 29's layer policy. Measured
+                                        6.3 % slower on the C2 step (the deep layers' 4x Winograd FLOP saving wins,
+                                        profiles/r4_a_bench_k37_1.json) */
+#define PIS_TUNE_HEAD_LOSS_WIDE 38 /* pis_head_loss_fwd with W % 512 == 0: 1 (default) 1024-thread blocks (16 waves,
+                                       one staged row per chunk), 0 the 256-thread form */
+#define PIS_TUNE_NKEYS 39
 #define PIS_DEBUG_NOLOAD (1 << 16)
 int pis_tune(int key, int value);
 /* Tooling (tools/bench_gemm.py): time one batched NT GEMM kernel variant in isolation,

@@ -196,6 +196,17 @@ __device__ __forceinline__ int wsw(int row, int k) {
   return row * 16 + ((((k >> 3) ^ ((row >> 2) ^ (row >> 3))) & 1) << 3) + (k & 7);
 }
 
+// sum of v over each aligned group of 16 lanes (a DPP row), returned in every lane of the group:
+// xor-1 and xor-2 quad permutes, then row_half_mirror (lane i <-> 7 - i) and row_mirror (i <-> 15 - i).
+// VALU only (no LDS traffic, unlike a 16-wide __shfl_xor); every lane's result is the same bits
+__device__ __forceinline__ float group16_sum(float v) {
+  v += dpp_f<0xB1, 0xf>(v);   // quad_perm [1,0,3,2]
+  v += dpp_f<0x4E, 0xf>(v);   // quad_perm [2,3,0,1]
+  v += dpp_f<0x141, 0xf>(v);  // row_half_mirror
+  v += dpp_f<0x140, 0xf>(v);  // row_mirror
+  return v;
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);

@@ -719,7 +719,7 @@ __global__ __launch_bounds__(256) void loss_bwd_kernel(LossBwdArgs g) {
 // 64-channel head input. A block owns R whole image rows of one sample:
 //  1. u of image rows y0-1 .. y0+R (reflect-resolved; the two halo rows recomputed from their own
 //     256 B/px, which the neighbouring bands fetch too: L2 / Infinity-Cache hits) into LDS, 16 lanes
-//     per pixel exactly as head_fwd64_kernel (same fma order and butterfly, so z and u are bitwise
+//     per pixel exactly as head_fwd64_kernel (same fma order and DPP row sum, so z and u are bitwise
 //     those of pis_head_fwd); the interior rows' z and u are written out (the model's outputs);
 //  2. the loss partials of its R rows from LDS (u and its reflect neighbours) and the targets, as
 //     loss_fwd_kernel; one finalize launch (loss_finalize_rows_kernel) reduces the [B][bands]
@@ -738,8 +738,11 @@ struct HeadLossFwdArgs {
   LossRowArgs a;  // the loss part: a.g (t, B, H, W, weights, partials), a.rows = R, a.bands, outputs
 };
 
-template <bool RD, bool PF, int PP>
-__global__ __launch_bounds__(256) void head_loss_fwd_kernel(HeadLossFwdArgs h) {
+// NT threads per block (NG = NT / 16 pixel groups): 1024 at W % 512 == 0 (C2: 256 blocks of 16
+// waves, four waves per SIMD to cover the HBM latency; one staged row per chunk), else 256
+template <bool RD, bool PF, int PP, int NT = 256>
+__global__ __launch_bounds__(NT) void head_loss_fwd_kernel(HeadLossFwdArgs h) {
+  constexpr int NG = NT / 16, NWV = NT / 64;
   constexpr bool ST = RD || PF;
   extern __shared__ __attribute__((aligned(16))) float su[];  // [R + 2][SW]: image column c at c + 4
   const LossArgs& g = h.a.g;
@@ -751,20 +754,20 @@ __global__ __launch_bounds__(256) void head_loss_fwd_kernel(HeadLossFwdArgs h) {
   const float* xb = h.x + (size_t)b * HW * h.ldx + 4 * sub;
   const f32x4 wv = *reinterpret_cast<const f32x4*>(h.w + 4 * sub);
   const float bias = h.bias[0];
-  // 1. u of the staged rows: a chunk is 16 PP consecutive pixels of one staged row (W % (16 PP) == 0),
+  // 1. u of the staged rows: a chunk is NG PP consecutive pixels of one staged row (W % (NG PP) == 0),
   // PP per 16-lane group; two register sets, so the next chunk's loads are in flight while this
-  // one's sums run (at one block per CU nothing else would cover the HBM latency)
-  const int cpr = W / (16 * PP), nchunk = (nr + 2) * cpr;
+  // one's sums run
+  const int cpr = W / (NG * PP), nchunk = (nr + 2) * cpr;
   f32x4 xa[PP], xn[PP];
   auto load = [&](f32x4 (&xv)[PP], int ch) __attribute__((always_inline)) {
-    const int r = ch / cpr, x0 = (ch - r * cpr) * (16 * PP) + grp;  // block-uniform r
+    const int r = ch / cpr, x0 = (ch - r * cpr) * (NG * PP) + grp;  // block-uniform r
     const int gy = clampi(refl(y0 - 1 + r, H), 0, H - 1);
     const float* row = xb + (size_t)gy * W * h.ldx;
 #pragma unroll
-    for (int j = 0; j < PP; ++j) xv[j] = *reinterpret_cast<const f32x4*>(row + (size_t)(x0 + 16 * j) * h.ldx);
+    for (int j = 0; j < PP; ++j) xv[j] = *reinterpret_cast<const f32x4*>(row + (size_t)(x0 + NG * j) * h.ldx);
   };
   auto head = [&](const f32x4 (&xv)[PP], int ch) __attribute__((always_inline)) {
-    const int r = ch / cpr, x0 = (ch - r * cpr) * (16 * PP) + grp;
+    const int r = ch / cpr, x0 = (ch - r * cpr) * (NG * PP) + grp;
     const bool interior = r >= 1 && r <= nr;
     const size_t orow = (size_t)b * HW + (size_t)(y0 - 1 + r) * W;
 #pragma unroll
@@ -774,10 +777,9 @@ __global__ __launch_bounds__(256) void head_loss_fwd_kernel(HeadLossFwdArgs h) {
       s = fmaf(xv[j][1], wv[1], s);
       s = fmaf(xv[j][2], wv[2], s);
       s = fmaf(xv[j][3], wv[3], s);
-#pragma unroll
-      for (int off = 8; off > 0; off >>= 1) s += __shfl_xor(s, off, 16);
+      s = group16_sum(s);  // as head_fwd64_kernel (csrc/pointwise.hip): z bitwise pis_head_fwd's
       if (sub == 0) {
-        const int xx = x0 + 16 * j;
+        const int xx = x0 + NG * j;
         const float zz = s + bias;
         const float uu = 1.f / (1.f + expf(-zz));
         su[r * SW + 4 + xx] = uu;
@@ -797,12 +799,12 @@ __global__ __launch_bounds__(256) void head_loss_fwd_kernel(HeadLossFwdArgs h) {
   }
   // the targets of this thread's items in flight across the barriers (TX threads per row, RY rows
   // per pass; item = 4 pixels)
-  const int W4 = W >> 2, TX = min(W4, 256), RY = 256 / TX;
+  const int W4 = W >> 2, TX = min(W4, NT), RY = NT / TX;
   const int q = tid % TX, ry = tid / TX;
   const float* tt = g.t + (size_t)b * HW;
   __syncthreads();
   if (ST) {  // reflect halo columns: column -1 is column 1, column W is column W-2
-    for (int r = tid; r < nr + 2; r += 256) {
+    for (int r = tid; r < nr + 2; r += NT) {
       su[r * SW + 3] = su[r * SW + 5];
       su[r * SW + 4 + W] = su[r * SW + 2 + W];
     }
@@ -864,8 +866,8 @@ __global__ __launch_bounds__(256) void head_loss_fwd_kernel(HeadLossFwdArgs h) {
     c_t += __shfl_xor(c_t, off, 64);
   }
   __syncthreads();  // su is dead: its first words take the wave partials
-  float* fr = su;                                // [4][6]
-  int* ir = reinterpret_cast<int*>(su + 24);     // [4][3]
+  float* fr = su;                                    // [NWV][6]
+  int* ir = reinterpret_cast<int*>(su + 6 * NWV);    // [NWV][3]
   const int lane = tid & 63, wave = tid >> 6;
   if (lane == 0) {
     fr[wave * 6 + 0] = v0;
@@ -880,11 +882,17 @@ __global__ __launch_bounds__(256) void head_loss_fwd_kernel(HeadLossFwdArgs h) {
   }
   __syncthreads();
   const int blk = b * h.a.bands + band;
-  if (tid < 6) {
-    g.fpart[blk * 6 + tid] = ((fr[tid] + fr[6 + tid]) + fr[12 + tid]) + fr[18 + tid];
+  if (tid < 6) {  // the waves in fixed order
+    float v = fr[tid];
+#pragma unroll
+    for (int w = 1; w < NWV; ++w) v += fr[6 * w + tid];
+    g.fpart[blk * 6 + tid] = v;
   } else if (tid < 9) {
     const int j = tid - 6;
-    g.ipart[blk * 3 + j] = ir[j] + ir[3 + j] + ir[6 + j] + ir[9 + j];
+    int c = ir[j];
+#pragma unroll
+    for (int w = 1; w < NWV; ++w) c += ir[3 * w + j];
+    g.ipart[blk * 3 + j] = c;
   }
 }
 
@@ -1217,12 +1225,15 @@ static int head_loss_fwd_rows(int H, int W) {
   return std::max(1, std::min(r, H));
 }
 
-// pixels per 16-lane group in flight in the fused head + loss forward (W % (16 PP) == 0), 0: none fits
+// pixels per 16-lane group in flight in the fused head + loss forward (W % (NG PP) == 0), 0: none fits;
+// W % 512 == 0 runs 1024-thread blocks (64 groups x 8 pixels: one 512-pixel row per chunk)
 static int head_loss_fwd_pp(int W) { return W % 256 == 0 ? 16 : W % 128 == 0 ? 8 : W % 64 == 0 ? 4 : 0; }
+static bool head_loss_fwd_wide(int W) { return W % 512 == 0 && tune_get(PIS_TUNE_HEAD_LOSS_WIDE) != 0; }
 
 extern "C" size_t pis_head_loss_fwd_ws(int B, int H, int W) {
-  const int R = head_loss_fwd_rows(H, W);
-  const size_t nblk = (size_t)B * ((H + R - 1) / R);
+  // sized for one row per block, so a later key-36 change cannot outgrow a planned workspace
+  const size_t nblk = (size_t)B * H;
+  (void)W;
   return 16 + nblk * (6 * sizeof(float) + 3 * sizeof(int)) + 256;
 }
 
@@ -1261,6 +1272,7 @@ extern "C" int pis_head_loss_fwd(const float* x, int ldx, const float* w, const 
   const bool all = prm->flags & PIS_LOSS_ALL_TERMS;
   const bool rd = all || prm->rd_w > 0.f, pf = all || prm->pf_w > 0.f;
   const int pp = head_loss_fwd_pp(W);
+  const bool wide = head_loss_fwd_wide(W);
   const size_t smem = (size_t)(h.R + 2) * (W + 8) * sizeof(float);
   const dim3 grid(bands, B);
   hipStream_t s = (hipStream_t)stream;
@@ -1268,7 +1280,8 @@ extern "C" int pis_head_loss_fwd(const float* x, int ldx, const float* w, const 
   launch_hook("head_loss_fwd", 0, s, nbytes);
 #define PIS_HLF(RDV, PFV)                                                                                         \
   do {                                                                                                            \
-    if (pp == 16) hipLaunchKernelGGL((head_loss_fwd_kernel<RDV, PFV, 16>), grid, dim3(256), smem, s, h);          \
+    if (wide) hipLaunchKernelGGL((head_loss_fwd_kernel<RDV, PFV, 8, 1024>), grid, dim3(1024), smem, s, h);        \
+    else if (pp == 16) hipLaunchKernelGGL((head_loss_fwd_kernel<RDV, PFV, 16>), grid, dim3(256), smem, s, h);     \
     else if (pp == 8) hipLaunchKernelGGL((head_loss_fwd_kernel<RDV, PFV, 8>), grid, dim3(256), smem, s, h);       \
     else hipLaunchKernelGGL((head_loss_fwd_kernel<RDV, PFV, 4>), grid, dim3(256), smem, s, h);                    \
   } while (0)

@@ -97,8 +97,7 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(const float* __restrict__
       s = fmaf(xv[2], wv[2], s);
       s = fmaf(xv[3], wv[3], s);
     }
-#pragma unroll
-  for (int off = 8; off > 0; off >>= 1) s += __shfl_xor(s, off, 16);
+  s = group16_sum(s);
   if (ok && sub == 0) {
     const float zz = s + b[0];
     if (z) z[p] = zz;
@@ -109,7 +108,7 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(const float* __restrict__
 // head fwd for C == 64 (the U-Net's head): the same 16-lane pixel groups, each taking PP pixels
 // G groups apart (G = the grid's group count) with all PP float4 loads issued before the sums —
 // PP x the bytes in flight of head_fwd_kernel's one load per thread; per pixel the same
-// fixed-order sum, so z and u are bitwise those of head_fwd_kernel
+// fixed-order sum (group16_sum), so z and u are bitwise those of head_loss_fwd_kernel
 template <int PP>
 __global__ __launch_bounds__(256) void head_fwd64_kernel(const float* __restrict__ x, int ldx,
                                                          const float* __restrict__ w,
@@ -134,8 +133,7 @@ __global__ __launch_bounds__(256) void head_fwd64_kernel(const float* __restrict
     s = fmaf(xv[k][1], wv[1], s);
     s = fmaf(xv[k][2], wv[2], s);
     s = fmaf(xv[k][3], wv[3], s);
-#pragma unroll
-    for (int off = 8; off > 0; off >>= 1) s += __shfl_xor(s, off, 16);
+    s = group16_sum(s);  // the same fixed order as head_loss_fwd_kernel (csrc/loss.hip): bitwise equal z
     if (p < npix && sub == 0) {
       const float zz = s + b[0];
       if (z) z[p] = zz;

@@ -80,9 +80,10 @@ def _fwd(hip, x, w, b, scale, flags, pool=False, ldx_extra=0):
 
 # kernel variants behind pis_tune: key 32 the input gradient's mask prefetch (default on)
 FWD_VARIANTS = [dict(), dict(k32=0)]
-# weight gradient: key 34 = 1 (default) the 2-row strip kernel, 0 the 4-row kernel; key 35 = 64: few
-# workgroups, so every block walks many tiles down (and across) column strips and image boundaries
-WG_VARIANTS = [dict(), dict(k34=0), dict(k35=64), dict(k34=2), dict(k34=2, k35=64)]
+# weight gradient: key 34 = 0 (default) the 4-row kernel, 1 the 2-row strip kernel, 2 the strip kernel
+# with the LDS halo ring; key 35 = 64: few workgroups, so every strip block walks many tiles down (and
+# across) column strips and image boundaries
+WG_VARIANTS = [dict(), dict(k34=1), dict(k34=1, k35=64), dict(k34=2), dict(k34=2, k35=64)]
 
 
 @pytest.mark.parametrize("variant", FWD_VARIANTS)
@@ -289,7 +290,7 @@ def test_direct_wgrad_x_magnitude_down_the_strip(hip, variant):
     assert errs["direct"] < 5e-6, errs
 
 
-@pytest.mark.parametrize("knobs", [dict(k29=2), dict(k37=1), dict(k37=1, k35=64), dict(k37=1, k34=2)])
+@pytest.mark.parametrize("knobs", [dict(k29=2), dict(k37=1, k34=1), dict(k37=1, k34=1, k35=64), dict(k37=1, k34=2)])
 @pytest.mark.parametrize("loss_kw", [dict(), dict(rd_w=1e-2, pf_w=1e-2, D=5.0, a=0.5, eps=0.05)])
 def test_train_step_with_direct_convs(hip, loss_kw, knobs):
     """The whole training step with every eligible conv on the direct kernels (key 29 = 2: forward

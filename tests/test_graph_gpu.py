@@ -85,7 +85,8 @@ def test_graph_dropped_without_close(hip):
     gc.collect()
     from physics_informed_image_segmentation_amd import _hip as hipmod
     assert cap.handle is None  # closed by the collector ...
-    assert any(h == cap_handle for h, _ in hipmod._free_streams)  # ... and recycled, never destroyed
+    # ... and recycled (free list keyed by (device, priority)), never destroyed
+    assert any(cap_handle in hs for hs in hipmod._free_streams.values())
     assert side.capture_status() == 0
     for _ in range(2):  # the same model, eagerly
         o.zero_grad(set_to_none=True)
@@ -124,3 +125,22 @@ def test_graph_refuses_data_parallel_and_detached_grads(hip):
     with pytest.raises(RuntimeError, match="captured gradient"):
         sg.step()
     sg.close()
+
+
+def test_owned_stream_device_and_recycling(hip):
+    """_hip.OwnedStream: the HIP stream is created on the requested device (not merely
+    labelled with it) and a closed stream is handed only to a new owner of the same device and
+    priority."""
+    from physics_informed_image_segmentation_amd import _hip as hipmod
+    dev = torch.device("cuda", 0)
+    a = hipmod.OwnedStream(device=dev)
+    assert a.stream.device == dev and a.device_index == 0
+    h = a.handle
+    a.close()
+    assert any(h in hs for (d, p), hs in hipmod._free_streams.items() if d == 0 and p == 0)
+    b = hipmod.OwnedStream(device=dev)
+    assert b.handle == h  # recycled
+    c = hipmod.OwnedStream(device=dev, priority=-1)
+    assert c.handle != h  # another priority never receives it
+    b.close()
+    c.close()

@@ -26,7 +26,13 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=4)
     ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--tune", action="append", default=[], metavar="KEY=VALUE")
+    ap.add_argument("--variants", default="default,side_hi,main_hi,serial,sync_gemm,sync_dgrad")
     args = ap.parse_args()
+    from physics_informed_image_segmentation_amd import _hip
+    for kv in args.tune:
+        k, v = (int(z) for z in kv.split("="))
+        _hip.lib().pis_tune(k, v)
     dev = torch.device("cuda")
     g = torch.Generator().manual_seed(42)
     imgs, masks = zip(*[disc_sample(512, 512, g) for _ in range(8)])
@@ -42,7 +48,7 @@ def main():
 
     def step():
         opt.zero_grad()
-        crit(model(x), t).backward()
+        model.forward_with_loss(x, t, crit)[1].backward()  # the step as bench.py runs it
         opt.step()
 
     step()  # plans the engine (buffers, side stream)
@@ -71,7 +77,7 @@ def main():
 
     res = {}
     for _ in range(args.rounds):
-        for v in ("default", "side_hi", "main_hi", "serial", "sync_gemm", "sync_dgrad"):
+        for v in args.variants.split(","):
             res.setdefault(v, []).append(run(v))
     for v, ms in res.items():
         ms.sort()
