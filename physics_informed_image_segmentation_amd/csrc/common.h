@@ -115,8 +115,6 @@ __device__ __forceinline__ float h3_scale(float m) {
   return __uint_as_float((unsigned)(sb > 254 ? 254 : sb) << 23);
 }
 
-// max over the wave of v >= 0 (DPP row shifts + row broadcasts: VALU only, no LDS round trip),
-// returned uniform
 // the scale for a tile of max m given the current scale: kept while m * cur stays in [2^7, 2^15)
 // (fp16 digits for everything above 2^-10 of the max, 2x headroom), so accumulators are rarely
 // rescaled; else re-chosen (h3_scale). cur = 0 always re-chooses; an all-zero K-step keeps cur.
@@ -148,14 +146,48 @@ template <int CTRL, int RMASK>
 __device__ __forceinline__ float dpp_f(float x) {
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, RMASK, 0xf, true));
 }
-__device__ __forceinline__ float wave_max_nonneg(float v) {
-  v = fmaxf(v, dpp_f<0x111, 0xf>(v));  // row_shr:1
-  v = fmaxf(v, dpp_f<0x112, 0xf>(v));  // row_shr:2
-  v = fmaxf(v, dpp_f<0x114, 0xf>(v));  // row_shr:4
-  v = fmaxf(v, dpp_f<0x118, 0xf>(v));  // row_shr:8: lane 15 of each row holds the row's max
-  v = fmaxf(v, dpp_f<0x142, 0xa>(v));  // row_bcast:15
-  v = fmaxf(v, dpp_f<0x143, 0xc>(v));  // row_bcast:31: lane 63 holds the wave's max
-  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+// max |x| over the 4 N values of x (>= 0): one v_max3_f32 with |.| source modifiers per pair.
+// Written out because fmaxf chains get a quieting v_max per operand (maxnum canonicalization) and
+// only partly fuse into v_max3; a quiet NaN operand is skipped as fmaxf would skip it.
+template <int N>
+__device__ __forceinline__ float absmax_x4(const f32x4 (&x)[N]) {
+  float m = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4 * N; i += 2)
+    asm("v_max3_f32 %0, |%1|, |%2|, %0" : "+v"(m) : "v"(x[i >> 2][i & 3]), "v"(x[i >> 2][(i & 3) + 1]));
+  return m;
+}
+
+// max over a wave of v >= 0 (DPP row shifts + row broadcasts: VALU only, no LDS round trip),
+// returned uniform
+template <int N, int M>
+__device__ __forceinline__ float absmax_x4(const f32x4 (&x)[N][M]) {
+  float m = 0.f;
+#pragma unroll
+  for (int i = 0; i < N; ++i)
+#pragma unroll
+    for (int j = 0; j < M; ++j) {
+      asm("v_max3_f32 %0, |%1|, |%2|, %0" : "+v"(m) : "v"(x[i][j][0]), "v"(x[i][j][1]));
+      asm("v_max3_f32 %0, |%1|, |%2|, %0" : "+v"(m) : "v"(x[i][j][2]), "v"(x[i][j][3]));
+    }
+  return m;
+}
+
+// (on the bit patterns: for v >= 0, NaN-free, unsigned order is float order, and integer max
+// has no maxnum canonicalization, so each step is one v_max_u32 with the DPP folded in)
+template <int CTRL, int RMASK>
+__device__ __forceinline__ unsigned dpp_u(unsigned x) {
+  return (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, RMASK, 0xf, true);
+}
+__device__ __forceinline__ float wave_max_nonneg(float f) {
+  unsigned v = __float_as_uint(f);
+  v = max(v, dpp_u<0x111, 0xf>(v));  // row_shr:1
+  v = max(v, dpp_u<0x112, 0xf>(v));  // row_shr:2
+  v = max(v, dpp_u<0x114, 0xf>(v));  // row_shr:4
+  v = max(v, dpp_u<0x118, 0xf>(v));  // row_shr:8: lane 15 of each row holds the row's max
+  v = max(v, dpp_u<0x142, 0xa>(v));  // row_bcast:15
+  v = max(v, dpp_u<0x143, 0xc>(v));  // row_bcast:31: lane 63 holds the wave's max
+  return __uint_as_float(__builtin_amdgcn_readlane(v, 63));
 }
 
 // 16-byte load from a wave-uniform base (SGPRs) at an unsigned 32-bit per-lane byte offset, as a
@@ -168,11 +200,12 @@ __device__ __forceinline__ u32x4 buf_load16(const void* base, uint32_t off) {
 
 // max of v >= 0 over each aligned group of 8 lanes, returned in every lane of the group (two quad
 // permutes + row_half_mirror)
-__device__ __forceinline__ float group8_max_nonneg(float v) {
-  v = fmaxf(v, dpp_f<0xB1, 0xf>(v));   // quad_perm [1,0,3,2]
-  v = fmaxf(v, dpp_f<0x4E, 0xf>(v));   // quad_perm [2,3,0,1]
-  v = fmaxf(v, dpp_f<0x141, 0xf>(v));  // row_half_mirror: the other quad of the 8
-  return v;
+__device__ __forceinline__ float group8_max_nonneg(float f) {
+  unsigned v = __float_as_uint(f);    // bit-pattern max, as wave_max_nonneg
+  v = max(v, dpp_u<0xB1, 0xf>(v));   // quad_perm [1,0,3,2]
+  v = max(v, dpp_u<0x4E, 0xf>(v));   // quad_perm [2,3,0,1]
+  v = max(v, dpp_u<0x141, 0xf>(v));  // row_half_mirror: the other quad of the 8
+  return __uint_as_float(v);
 }
 
 // the fp16x3 scale s = 2^(13 - e) for a group max m in [2^e, 2^(e+1)) (as h3_scale) and its exact

@@ -102,17 +102,8 @@ __global__ __launch_bounds__(256, 2) void convt_gemm_kernel(ConvtGemmArgs g) {
   float sa_min = __builtin_inff(), sb_min = __builtin_inff();  // ... and the smallest so far
   auto lstore = [&](int buf) {
     if constexpr (H3) {
-      float ma = 0.f, mb = 0.f;
-#pragma unroll
-      for (int i = 0; i < AL; ++i)
-#pragma unroll
-        for (int k = 0; k < 4; ++k) ma = fmaxf(ma, fabsf(ra[i][k]));
-#pragma unroll
-      for (int i = 0; i < BL; ++i)
-#pragma unroll
-        for (int k = 0; k < 4; ++k) mb = fmaxf(mb, fabsf(rb[i][k]));
-      sa = h3_keep(sa, wave_max_nonneg(ma), sa_min);
-      sb = h3_keep(sb, wave_max_nonneg(mb), sb_min);
+      sa = h3_keep(sa, wave_max_nonneg(absmax_x4(ra)), sa_min);
+      sb = h3_keep(sb, wave_max_nonneg(absmax_x4(rb)), sb_min);
       if (lane == 0) {
         sscale[buf][0][wave] = sa;
         sscale[buf][1][wave] = sb;
@@ -376,17 +367,8 @@ __global__ __launch_bounds__(256, 3) void convt_h3_kernel(ConvtGemmArgs g) {
   };
   float sa = 0.f, sb = 0.f, sa_min = __builtin_inff(), sb_min = __builtin_inff();
   auto lstore = [&]() {
-    float ma = 0.f, mb = 0.f;
-#pragma unroll
-    for (int i = 0; i < AL; ++i)
-#pragma unroll
-      for (int k = 0; k < 4; ++k) ma = fmaxf(ma, fabsf(ra[i][k]));
-#pragma unroll
-    for (int i = 0; i < BL; ++i)
-#pragma unroll
-      for (int k = 0; k < 4; ++k) mb = fmaxf(mb, fabsf(rb[i][k]));
-    sa = h3_keep(sa, wave_max_nonneg(ma), sa_min);
-    sb = h3_keep(sb, wave_max_nonneg(mb), sb_min);
+    sa = h3_keep(sa, wave_max_nonneg(absmax_x4(ra)), sa_min);
+    sb = h3_keep(sb, wave_max_nonneg(absmax_x4(rb)), sb_min);
     if (lane == 0) {
       sscale[0][wave] = sa;
       sscale[1][wave] = sb;

@@ -291,12 +291,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_h3_kernel(DirectArgs g) {
     constexpr bool LAST = decltype(last_c)::value;
     if (!(TW && (g.dbg & 2) && k > 0)) {
     // 1. this chunk's weights into LDS; the halo's block-wide max
-    float m = 0.f;
-#pragma unroll
-    for (int j = 0; j < DX_PER_T; ++j)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) m = fmaxf(m, fmaxf(fabsf(xr[j][0][e]), fabsf(xr[j][1][e])));
-    m = wave_max_nonneg(m);
+    float m = wave_max_nonneg(absmax_x4(xr));
     if (lane == 0) red[wave] = m;
 #pragma unroll
     for (int j = 0; j < DW_PER_T; ++j) reinterpret_cast<u32x4*>(sw)[tid + 256 * j] = wr[j];
@@ -568,17 +563,8 @@ __global__ __launch_bounds__(256, 1) void conv3x3_wgrad_h3_kernel(DirectWArgs g)
   for (; t < ntile; t += g.splits) {
     if (!(TW && (g.dbg & 2) && t != split)) {
     // 1. block maxima of the staged operands
-    float mz = 0.f, mx = 0.f;
-#pragma unroll
-    for (int j = 0; j < WZ_PER_T; ++j)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) mz = fmaxf(mz, fmaxf(fabsf(zr[j][0][e]), fabsf(zr[j][1][e])));
-#pragma unroll
-    for (int j = 0; j < WX_PER_T; ++j)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) mx = fmaxf(mx, fmaxf(fabsf(xr[j][0][e]), fabsf(xr[j][1][e])));
-    mz = wave_max_nonneg(mz);
-    mx = wave_max_nonneg(mx);
+    float mz = wave_max_nonneg(absmax_x4(zr));
+    float mx = wave_max_nonneg(absmax_x4(xr));
     if (lane == 0) {
       red[wave] = mz;
       red[NW + wave] = mx;

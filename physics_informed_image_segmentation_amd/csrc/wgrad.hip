@@ -928,7 +928,11 @@ __device__ __forceinline__ int wtsw(int row, int chunk) { return row * 128 + 8 *
 // 2 r pixels apart; the bias partials (column sums of A, blocks of the first column tile) are
 // summed from the raw loads and reduced over the 8 threads of a column group in LDS (fixed order).
 // TW: the timing-twin instantiation (pis_tune key 2 != 0 only; the production kernel has no debug branch)
-template <bool UP2 = false, int D = 2, bool TW = false>
+// EX: every split is whole K-steps (P % 32 == 0; the plan's pps is a multiple of 32) and every
+// operand row offset fits 31 bits: no per-row tail test, and the plain operands are read by
+// buffer loads from the block's base (32-bit lane offset + a wave-uniform row offset per j)
+// instead of 64-bit per-lane address arithmetic. Same loads, same sums (bitwise equal).
+template <bool UP2 = false, int D = 2, bool TW = false, bool EX = false>
 __global__ __launch_bounds__(256, 2) void wgrad_h3t_kernel(WgradArgs g) {
   const Remap2 rm = xcd_remap2();
   if (rm.batch) {
@@ -963,8 +967,31 @@ __global__ __launch_bounds__(256, 2) void wgrad_h3t_kernel(WgradArgs g) {
   f32x4 bsum = {0.f, 0.f, 0.f, 0.f};
 
   f32x4 ra[D][4], rb[D][4];
+  // EX: buffer resources at the block's column bases; lane offsets of row p_begin + srow
+  const __amdgpu_buffer_rsrc_t rsa = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(g.a + m0), (short)0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsb = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(g.b + n0), (short)0, 0x7fffffff, 0x00020000);
+  const uint32_t la0 = 4u * ((uint32_t)(p_begin + srow) * (uint32_t)g.lda + 4u * sc4);
+  const uint32_t lb0 = 4u * ((uint32_t)(p_begin + srow) * (uint32_t)g.ldb + 4u * sc4);
   auto gload = [&](f32x4 (&xa)[4], f32x4 (&xb)[4], int st) __attribute__((always_inline)) {
     if (TW && (g.dbg & 1) && st >= D) return;
+    if constexpr (EX) {  // rows p_begin + 32 st + srow + 8 j, all inside the split
+      const uint32_t ra_s = 4u * (uint32_t)(st * WT_BK) * (uint32_t)g.lda, rb_s = 4u * (uint32_t)(st * WT_BK) * (uint32_t)g.ldb;
+      size_t abase = 0;
+      if (UP2) {
+        const int p0 = p_begin + st * WT_BK;
+        const int hw = g.H * g.W, b = p0 / hw, rem = p0 - b * hw, y = rem / g.W, x0 = rem - y * g.W;
+        abase = (((size_t)b * 2 * g.H + 2 * y + (up_ij >> 1)) * (2 * g.W) + 2 * x0 + (up_ij & 1)) * g.lda;
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (UP2)
+          xa[j] = *reinterpret_cast<const f32x4*>(ga + abase + (size_t)(2 * (srow + 8 * j)) * g.lda);
+        else
+          xa[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsa, la0, ra_s + 4u * (uint32_t)(8 * j) * (uint32_t)g.lda, 0));
+        xb[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsb, lb0, rb_s + 4u * (uint32_t)(8 * j) * (uint32_t)g.ldb, 0));
+      }
+      return;
+    }
     const int p0 = p_begin + st * WT_BK;
     size_t abase = 0;
     if (UP2) {  // the K-step's 32 pixels: one image row (b, y), columns x0 ..
@@ -990,16 +1017,8 @@ __global__ __launch_bounds__(256, 2) void wgrad_h3t_kernel(WgradArgs g) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) bsum += xa[j];
     }
-    float ma = 0.f, mb = 0.f;
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        ma = fmaxf(ma, fabsf(xa[j][e]));
-        mb = fmaxf(mb, fabsf(xb[j][e]));
-      }
-    ma = wave_max_nonneg(ma);
-    mb = wave_max_nonneg(mb);
+    const float ma = wave_max_nonneg(absmax_x4(xa));
+    const float mb = wave_max_nonneg(absmax_x4(xb));
     if (lane == 0) {
       red[par][0][wave] = ma;
       red[par][1][wave] = mb;
@@ -1007,8 +1026,12 @@ __global__ __launch_bounds__(256, 2) void wgrad_h3t_kernel(WgradArgs g) {
   };
   float sa_last = 0.f, sb_last = 0.f, sa_min = __builtin_inff(), sb_min = __builtin_inff();
   auto split_store = [&](const f32x4 (&xa)[4], const f32x4 (&xb)[4], int par, float& sa, float& sb) __attribute__((always_inline)) {
-    const float ma = fmaxf(fmaxf(red[par][0][0], red[par][0][1]), fmaxf(red[par][0][2], red[par][0][3]));
-    const float mb = fmaxf(fmaxf(red[par][1][0], red[par][1][1]), fmaxf(red[par][1][2], red[par][1][3]));
+    auto umax4 = [](const float (&r)[4]) __attribute__((always_inline)) {  // r >= 0: bit-pattern max
+      return __uint_as_float(max(max(__float_as_uint(r[0]), __float_as_uint(r[1])),
+                                 max(__float_as_uint(r[2]), __float_as_uint(r[3]))));
+    };
+    const float ma = umax4(red[par][0]);
+    const float mb = umax4(red[par][1]);
     sa = sa_last = h3_keep(sa_last, ma, sa_min);
     sb = sb_last = h3_keep(sb_last, mb, sb_min);
     _Float16* buf = smem + par * WT_BUF;
@@ -1172,6 +1195,13 @@ __global__ __launch_bounds__(256, 2) void wgrad_h3t_kernel(WgradArgs g) {
   }
 }
 
+// wgrad_h3t_kernel's EX form: whole K-steps in every split (pix_per_split is a multiple of 32) and
+// 31-bit row offsets for the buffer loads (the batch offsets go into the base pointers)
+static bool h3t_exact(const WgradArgs& a) {
+  return a.P % WT_BK == 0 && a.pix_per_split % WT_BK == 0 &&
+         ((int64_t)a.P + WT_BK) * std::max(a.a_up2 ? 0 : a.lda, a.ldb) * 4 < (int64_t(1) << 31);
+}
+
 static int run_wgrad(const WgradArgs& base, const WgradPlan& pl, hipStream_t s, int batches = 1) {
   WgradArgs a = base;
   a.pix_per_split = pl.pps;
@@ -1195,6 +1225,8 @@ static int run_wgrad(const WgradArgs& base, const WgradPlan& pl, hipStream_t s, 
         ((uintptr_t)a.a & 15) == 0 && ((uintptr_t)a.b & 15) == 0) {
       if (a.dbg)
         hipLaunchKernelGGL((wgrad_h3t_kernel<false, 2, true>), grid, dim3(256), 0, s, a);
+      else if (h3t_exact(a))
+        hipLaunchKernelGGL((wgrad_h3t_kernel<false, 2, false, true>), grid, dim3(256), 0, s, a);
       else
         hipLaunchKernelGGL((wgrad_h3t_kernel<false, 2>), grid, dim3(256), 0, s, a);
       return launch_status("wgrad_h3t");
@@ -1661,7 +1693,10 @@ extern "C" int pis_convt2x2_wgrad(const float* x, int ldx, const float* dy, int 
     a.part_bias = db ? bias_slabs(ws, pl) : nullptr;
     a.pix_per_split = pl.pps;
     const int tiles = (a.Mp / 128) * (a.Np / 128);
-    hipLaunchKernelGGL((wgrad_h3t_kernel<true, 2>), dim3(tiles * pl.splits), dim3(256), 0, s, a);
+    if (h3t_exact(a))
+      hipLaunchKernelGGL((wgrad_h3t_kernel<true, 2, false, true>), dim3(tiles * pl.splits), dim3(256), 0, s, a);
+    else
+      hipLaunchKernelGGL((wgrad_h3t_kernel<true, 2>), dim3(tiles * pl.splits), dim3(256), 0, s, a);
     int rc = launch_status("wgrad_h3t<up2>");
     if (!rc) rc = reduce_slabs(a.part, pl.splits, (int64_t)a.Mp * a.Np, dw_ijoc, acc, s);
     if (rc || !db) return rc;
