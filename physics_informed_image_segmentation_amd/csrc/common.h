@@ -95,15 +95,22 @@ __device__ __forceinline__ void split3_x4(f32x4 v, u32x2& h, u32x2& m, u32x2& l)
 // of two per wave and K-step; the three products lo*hi, hi*lo, hi*hi on fp16 MFMA
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x2_t __attribute__((ext_vector_type(2)));
+// hi: v_cvt_pk_f16_f32 per pair; lo: one v_fma_mix{lo,hi}_f16 per value, fp16(v - hi) with the
+// fp16 hi read straight from its half of the packed register (1.5 VALU per value; widening hi back
+// to fp32 first took 2.5). The residual v - hi is exact in fp32 (v has 24 significant bits, hi
+// its leading 11), so rounding it once to fp16 inside the fma gives the same lo as the widened form.
 __device__ __forceinline__ void split2h_x4(f32x4 v, u32x2& h, u32x2& l) {
-  // packed: v_cvt_pk_f16_f32 (hi), v_cvt_f32_f16 x2 + v_pk_add_f32 (residual), v_cvt_pk_f16_f32 (lo)
   typedef float f2 __attribute__((ext_vector_type(2)));
   const f2 a = {v[0], v[1]}, b = {v[2], v[3]};
-  const f16x2_t ha = __builtin_convertvector(a, f16x2_t), hb = __builtin_convertvector(b, f16x2_t);
-  const f16x2_t la = __builtin_convertvector(a - __builtin_convertvector(ha, f2), f16x2_t);
-  const f16x2_t lb = __builtin_convertvector(b - __builtin_convertvector(hb, f2), f16x2_t);
-  h = u32x2{__builtin_bit_cast(unsigned, ha), __builtin_bit_cast(unsigned, hb)};
-  l = u32x2{__builtin_bit_cast(unsigned, la), __builtin_bit_cast(unsigned, lb)};
+  const unsigned ha = __builtin_bit_cast(unsigned, __builtin_convertvector(a, f16x2_t));
+  const unsigned hb = __builtin_bit_cast(unsigned, __builtin_convertvector(b, f16x2_t));
+  unsigned la, lb;
+  asm("v_fma_mixlo_f16 %0, %1, 1.0, -%2 op_sel_hi:[0,0,1]" : "=v"(la) : "v"(v[0]), "v"(ha));
+  asm("v_fma_mixhi_f16 %0, %1, 1.0, -%2 op_sel:[0,0,1] op_sel_hi:[0,0,1]" : "+v"(la) : "v"(v[1]), "v"(ha));
+  asm("v_fma_mixlo_f16 %0, %1, 1.0, -%2 op_sel_hi:[0,0,1]" : "=v"(lb) : "v"(v[2]), "v"(hb));
+  asm("v_fma_mixhi_f16 %0, %1, 1.0, -%2 op_sel:[0,0,1] op_sel_hi:[0,0,1]" : "+v"(lb) : "v"(v[3]), "v"(hb));
+  h = u32x2{ha, hb};
+  l = u32x2{la, lb};
 }
 
 // 2^(13 - e) for m in [2^e, 2^(e+1)): m * scale lands in [2^13, 2^14), 4x under fp16's largest

@@ -1171,20 +1171,38 @@ __global__ __launch_bounds__(256, OCC) void gemm_nt_h3_bk32_kernel(const float* 
   const int q8 = (tid & 7) * 4;
   const bool full = m0 + BM <= M && K % BK == 0;
   f32x4 ra[AL], rb[BL];
+  // full tiles (every launch of the training step): straight-line buffer loads from the block's
+  // first A / B row (SGPR resources), one 32-bit lane offset for both operands (row tid / 8,
+  // column q8) and a wave-uniform offset per row group i and K-step; rows of one block tile span
+  // BM * K * 4 bytes (< 2 GiB for any K the host admits)
+  const __amdgpu_buffer_rsrc_t rsa =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(A + (size_t)m0 * K), (short)0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsb =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(Bm + (size_t)n0 * K), (short)0, 0x7fffffff, 0x00020000);
+  const uint32_t vo = 4u * ((uint32_t)(tid / 8) * (uint32_t)K + (uint32_t)q8);
   auto gload = [&](int k0) {
     if (DBG == 1 && k0 >= 2 * BK) return;
+    if (full) {
+#pragma unroll
+      for (int i = 0; i < AL; ++i)
+        ra[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsa, vo, 4u * (uint32_t)(32 * i * K + k0), 0));
+#pragma unroll
+      for (int i = 0; i < BL; ++i)
+        rb[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsb, vo, 4u * (uint32_t)(32 * i * K + k0), 0));
+      return;
+    }
     const int k = k0 + q8;
 #pragma unroll
     for (int i = 0; i < AL; ++i) {
       const int m = m0 + (tid + i * 256) / 8;
       ra[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (full || (m < M && k < K)) ra[i] = *reinterpret_cast<const f32x4*>(A + (size_t)m * K + k);
+      if (m < M && k < K) ra[i] = *reinterpret_cast<const f32x4*>(A + (size_t)m * K + k);
     }
 #pragma unroll
     for (int i = 0; i < BL; ++i) {
       const int n = n0 + (tid + i * 256) / 8;
       rb[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (full || k < K) rb[i] = *reinterpret_cast<const f32x4*>(Bm + (size_t)n * K + k);
+      if (k < K) rb[i] = *reinterpret_cast<const f32x4*>(Bm + (size_t)n * K + k);
     }
   };
   float sa = 0.f, sb = 0.f;  // the wave's current scales (h3_keep)
