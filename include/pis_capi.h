@@ -160,7 +160,11 @@ int pis_version(void);
                                         profiles/r4_a_bench_k37_1.json) */
 #define PIS_TUNE_HEAD_LOSS_WIDE 38 /* pis_head_loss_fwd with W % 512 == 0: 1 (default) 1024-thread blocks (16 waves,
                                        one staged row per chunk), 0 the 256-thread form */
-#define PIS_TUNE_NKEYS 39
+#define PIS_TUNE_WGRAD_T_DEPTH 39 /* wgrad_h3t_kernel's whole-K-step (EX) form: raw operands of K-step st + D in
+                                      flight while K-step st multiplies; 2 (default) or 3 (two / three register
+                                      sets; 3 measured neutral on the step, 21.93 vs 21.91 ms:
+                                      profiles/r4_f_ab.txt) */
+#define PIS_TUNE_NKEYS 40
 #define PIS_DEBUG_NOLOAD (1 << 16)
 int pis_tune(int key, int value);
 /* Tooling (tools/bench_gemm.py): time one batched NT GEMM kernel variant in isolation,

@@ -1225,6 +1225,8 @@ static int run_wgrad(const WgradArgs& base, const WgradPlan& pl, hipStream_t s, 
         ((uintptr_t)a.a & 15) == 0 && ((uintptr_t)a.b & 15) == 0) {
       if (a.dbg)
         hipLaunchKernelGGL((wgrad_h3t_kernel<false, 2, true>), grid, dim3(256), 0, s, a);
+      else if (h3t_exact(a) && tune_get(PIS_TUNE_WGRAD_T_DEPTH) == 3)
+        hipLaunchKernelGGL((wgrad_h3t_kernel<false, 3, false, true>), grid, dim3(256), 0, s, a);
       else if (h3t_exact(a))
         hipLaunchKernelGGL((wgrad_h3t_kernel<false, 2, false, true>), grid, dim3(256), 0, s, a);
       else
