@@ -164,7 +164,12 @@ int pis_version(void);
                                       flight while K-step st multiplies; 2 (default) or 3 (two / three register
                                       sets; 3 measured neutral on the step, 21.93 vs 21.91 ms:
                                       profiles/r4_f_ab.txt) */
-#define PIS_TUNE_NKEYS 40
+#define PIS_TUNE_DZ_VW 40 /* channels per thread of the F(3x3,4x4) dz passes (pis_conv3x3_bwd_prep's merged V + E
+                               pass, the weight gradient's E pass): 2 (default where 256 % (N / 2) == 0) or 4
+                               (the float4 form: 256 + 30 registers, one wave per SIMD). Measured neutral on the
+                               step (21.95 vs 22.02 ms, profiles/r4_g_ab.txt; the passes run at 5-5.9 TB/s
+                               isolated either way) */
+#define PIS_TUNE_NKEYS 41
 #define PIS_DEBUG_NOLOAD (1 << 16)
 int pis_tune(int key, int value);
 /* Tooling (tools/bench_gemm.py): time one batched NT GEMM kernel variant in isolation,

@@ -71,6 +71,7 @@ int launch_wino_input(const float* x, int ldx, int B, int H, int W, int C, float
 int launch_wino_dz(const float* dz, int ldz, int B, int H, int W, int N, float* E, hipStream_t s, int m,
                    float* bpart = nullptr);
 int wino_dz_blocks(int B, int H, int W, int N, int m);
+int wino_dz_blocks_max(int B, int H, int W, int N, int m);  // over pis_tune key 40
 // M: nsplit split-K slabs sstride floats apart, summed in slab order (nsplit > 1 needs m == 4)
 int launch_wino_wgrad_out(const float* M, int N, int C, float* dw, int accumulate, hipStream_t s, int m,
                           int nsplit = 1, int64_t sstride = 0);

@@ -1448,7 +1448,7 @@ static WinoWgradPlan wino_wgrad_plan(int B, int H, int W, int Cin, int Cout) {
   p.off_cs = p.off_M + M;
   // bias gradient: per-block sums out of the F(3x3,4x4) dz transform, else a channel-sum pass
   p.fused_bias = p.m == 4 && 256 % (Cout / 4) == 0;
-  const size_t cs = p.fused_bias ? (size_t)wino_dz_blocks(B, H, W, Cout, 4) * Cout * sizeof(float)
+  const size_t cs = p.fused_bias ? (size_t)wino_dz_blocks_max(B, H, W, Cout, 4) * Cout * sizeof(float)
                                  : colsum_ws((int64_t)B * H * W, Cout);
   p.total = p.off_cs + al(cs) + 256;
   return p;

@@ -639,24 +639,25 @@ __host__ __device__ constexpr float w4_at3(int i, int k) {
 
 // E[xi][t][n] = (G4 e G4^T)[xi], e = dz at output pixels (4ty + i, 4tx + j); bsum += the tile's
 // channel sums (the bias gradient)
+template <int VW = 4>
 __device__ __forceinline__ void wino4_dz_item(const float* __restrict__ dz, int ldz, int H, int W, int N,
                                               float* __restrict__ E, int64_t TN, int64_t t, int b, int ty, int tx,
-                                              int n, f32x4& bsum) {
-  f32x4 v[6][6];
+                                              int n, fvec<VW>& bsum) {
+  fvec<VW> v[6][6];
 #pragma unroll
   for (int i = 0; i < 6; ++i)
 #pragma unroll
-    for (int j = 0; j < 6; ++j) v[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < 6; ++j) v[i][j] = (fvec<VW>)0.f;
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
-    f32x4 d[4];
+    fvec<VW> d[4];
 #pragma unroll
     for (int l = 0; l < 4; ++l)
-      d[l] = *reinterpret_cast<const f32x4*>(dz + (((size_t)b * H + 4 * ty + k) * W + 4 * tx + l) * ldz + n);
+      d[l] = *reinterpret_cast<const fvec<VW>*>(dz + (((size_t)b * H + 4 * ty + k) * W + 4 * tx + l) * ldz + n);
     bsum += (d[0] + d[1]) + (d[2] + d[3]);
 #pragma unroll
     for (int j = 0; j < 6; ++j) {
-      f32x4 r = f32x4{0.f, 0.f, 0.f, 0.f};
+      fvec<VW> r = (fvec<VW>)0.f;
 #pragma unroll
       for (int l = 0; l < 4; ++l) axpy_c(r, w4_g4(j, l), d[l]);
 #pragma unroll
@@ -665,62 +666,67 @@ __device__ __forceinline__ void wino4_dz_item(const float* __restrict__ dz, int 
   }
 #pragma unroll
   for (int xi = 0; xi < 36; ++xi)
-    *reinterpret_cast<f32x4*>(E + (size_t)xi * TN + t * N + n) = v[xi / 6][xi % 6];
+    *reinterpret_cast<fvec<VW>*>(E + (size_t)xi * TN + t * N + n) = v[xi / 6][xi % 6];
 }
 
-// bpart[blockIdx.x][N] = fixed-order block reduction of the threads sharing a channel quad
-// (tid mod n4n; with 256 * gridDim.x a multiple of N / 4 a thread's channels never change
-// across its grid-stride items)
-__device__ __forceinline__ void wino4_bias_partials(f32x4 bsum, int N, float* __restrict__ bpart) {
-  const int n4n = N / 4;
-  __shared__ f32x4 red[256];
+// bpart[blockIdx.x][N] = fixed-order block reduction of the threads sharing a channel group
+// (tid mod N / VW; with 256 a multiple of N / VW a thread's channels never change across its
+// grid-stride items)
+template <int VW = 4>
+__device__ __forceinline__ void wino4_bias_partials(fvec<VW> bsum, int N, float* __restrict__ bpart) {
+  const int nvn = N / VW;
+  __shared__ fvec<VW> red[256];
   red[threadIdx.x] = bsum;
   __syncthreads();
-  if ((int)threadIdx.x < n4n) {
-    f32x4 acc = red[threadIdx.x];
-    for (int k = threadIdx.x + n4n; k < 256; k += n4n) acc += red[k];
-    *reinterpret_cast<f32x4*>(bpart + (size_t)blockIdx.x * N + 4 * threadIdx.x) = acc;
+  if ((int)threadIdx.x < nvn) {
+    fvec<VW> acc = red[threadIdx.x];
+    for (int k = threadIdx.x + nvn; k < 256; k += nvn) acc += red[k];
+    *reinterpret_cast<fvec<VW>*>(bpart + (size_t)blockIdx.x * N + VW * threadIdx.x) = acc;
   }
 }
 
 // With bpart != NULL it also leaves the bias gradient's per-block channel sums in
 // bpart[blockIdx.x][N] (every dz pixel belongs to exactly one tile).
+template <int VW = 4>
 __global__ __launch_bounds__(256) void wino4_dz_kernel(const float* __restrict__ dz, int ldz, int B, int H, int W,
                                                        int N, float* __restrict__ E, float* __restrict__ bpart) {
-  const int n4n = N / 4, TW = W / 4, TH = H / 4;
+  const int nvn = N / VW, TW = W / 4, TH = H / 4;
   const int64_t T = (int64_t)B * TH * TW, TN = T * N;
-  f32x4 bsum = {0.f, 0.f, 0.f, 0.f};
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < T * n4n; e += (int64_t)gridDim.x * blockDim.x) {
+  fvec<VW> bsum = (fvec<VW>)0.f;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < T * nvn; e += (int64_t)gridDim.x * blockDim.x) {
     int64_t t;
     int n, b, rem;
-    tile_decode(e, n4n, TH * TW, t, n, b, rem);
+    tile_decode<VW>(e, nvn, TH * TW, t, n, b, rem);
     const int ty = rem / TW, tx = rem - ty * TW;
-    wino4_dz_item(dz, ldz, H, W, N, E, TN, t, b, ty, tx, n, bsum);
+    wino4_dz_item<VW>(dz, ldz, H, W, N, E, TN, t, b, ty, tx, n, bsum);
   }
-  if (bpart) wino4_bias_partials(bsum, N, bpart);
+  if (bpart) wino4_bias_partials<VW>(bsum, N, bpart);
 }
 
 // One pass over a layer's dz for both of its backward products: V = the input gradient's
 // F(4x4,3x3) input transform of dz (as wino4_input_kernel) and E = the weight gradient's
 // F(3x3,4x4) transform + bias partials (as wino4_dz_kernel); the second half re-reads the tile's
 // 4x4 interior from cache instead of HBM. Same grid as wino4_dz_kernel (bpart layout).
-template <bool TM = false>
+// VW channels per thread (dz_vw: 2 where 256 is a multiple of N / 2, so the bias partials keep
+// one channel pair per thread; half the registers of the float4 form, whose 256 + 30 kept it at one
+// wave per SIMD)
+template <bool TM = false, int VW = 4>
 __global__ __launch_bounds__(256) void wino4_dz2_kernel(const float* __restrict__ dz, int ldz, int B, int H, int W,
                                                         int N, float* __restrict__ V, float* __restrict__ E,
                                                         float* __restrict__ bpart, float* __restrict__ tmax = nullptr) {
-  const int n4n = N / 4, TW = W / 4, TH = H / 4;
+  const int nvn = N / VW, TW = W / 4, TH = H / 4;
   const int64_t T = (int64_t)B * TH * TW, TN = T * N;
-  f32x4 bsum = {0.f, 0.f, 0.f, 0.f};
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < T * n4n; e += (int64_t)gridDim.x * blockDim.x) {
+  fvec<VW> bsum = (fvec<VW>)0.f;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < T * nvn; e += (int64_t)gridDim.x * blockDim.x) {
     int64_t t;
     int n, b, rem;
-    tile_decode(e, n4n, TH * TW, t, n, b, rem);
+    tile_decode<VW>(e, nvn, TH * TW, t, n, b, rem);
     const int ty = rem / TW, tx = rem - ty * TW;
-    const float m = wino4_input_item<4, TM>(dz, ldz, H, W, N, V, TN, t, b, ty, tx, n);
-    if constexpr (TM) tile_max_store<4>(m, N, n, t, tmax);
-    wino4_dz_item(dz, ldz, H, W, N, E, TN, t, b, ty, tx, n, bsum);
+    const float m = wino4_input_item<VW, TM>(dz, ldz, H, W, N, V, TN, t, b, ty, tx, n);
+    if constexpr (TM) tile_max_store<VW>(m, N, n, t, tmax);
+    wino4_dz_item<VW>(dz, ldz, H, W, N, E, TN, t, b, ty, tx, n, bsum);
   }
-  if (bpart) wino4_bias_partials(bsum, N, bpart);
+  if (bpart) wino4_bias_partials<VW>(bsum, N, bpart);
 }
 
 // dw[n][r][s][c] (+)= (AT3 M AT3^T)[r][s], M[xi][n][c] the reduced tile sums
@@ -763,6 +769,72 @@ __global__ __launch_bounds__(256) void wino4_wgrad_out_kernel(const float* __res
         float* o = dw + ((size_t)n * 9 + i * 3 + j) * C + c;
         *o = accumulate ? *o + y[i][j] : y[i][j];
       }
+  }
+}
+
+// The same as a block-tiled pass (NC % 64 == 0: every F(3x3,4x4) layer with 64-multiple channels).
+// The one-thread-per-(n, c) form above ran at 0.7 TB/s in the step (profiles/r4_e: 36 x nsplit
+// dependent-latency loads per thread, 256 blocks of 256 threads for a 256 x 256 layer). Here a
+// block owns 64 consecutive (n, c): pass 1 sums the split slabs of its 36 x 64 M entries, 9 per
+// thread, 4 slabs per unrolled step so 36 loads are in flight, into LDS; pass 2 runs the output
+// transform with 3 threads per entry (one row i of the 3 x 3 each). Same sums in the same order as
+// wino4_wgrad_out_kernel: bitwise equal.
+__global__ __launch_bounds__(256) void wino4_wgrad_out_tiled_kernel(const float* __restrict__ M, int N, int C,
+                                                                    float* __restrict__ dw, int accumulate,
+                                                                    int nsplit, int64_t sstride) {
+  __shared__ float sm[36][65];
+  const int64_t NC = (int64_t)N * C;
+  const int64_t e0 = (int64_t)blockIdx.x * 64;
+  const int tid = threadIdx.x, el = tid & 63, xg = tid >> 6;  // entry e0 + el, xi = xg + 4 q
+  {
+    const float* src[9];
+#pragma unroll
+    for (int q = 0; q < 9; ++q) src[q] = M + (size_t)(xg + 4 * q) * NC + e0 + el;
+    float v[9];
+#pragma unroll
+    for (int q = 0; q < 9; ++q) v[q] = src[q][0];
+    int sp = 1;
+    for (; sp + 3 < nsplit; sp += 4) {
+      float a[9][4];
+#pragma unroll
+      for (int q = 0; q < 9; ++q)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) a[q][u] = src[q][(size_t)(sp + u) * sstride];
+#pragma unroll
+      for (int q = 0; q < 9; ++q) v[q] = (((v[q] + a[q][0]) + a[q][1]) + a[q][2]) + a[q][3];
+    }
+    for (; sp < nsplit; ++sp)
+#pragma unroll
+      for (int q = 0; q < 9; ++q) v[q] += src[q][(size_t)sp * sstride];
+#pragma unroll
+    for (int q = 0; q < 9; ++q) sm[xg + 4 * q][el] = v[q];
+  }
+  __syncthreads();
+  if (tid >= 192) return;
+  const int i = tid >> 6;  // output row r = i of entry el
+  float y[3] = {0.f, 0.f, 0.f};
+#pragma unroll
+  for (int k = 0; k < 6; ++k) {
+    float m[6];
+#pragma unroll
+    for (int l = 0; l < 6; ++l) m[l] = sm[k * 6 + l][el];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      float r = 0.f;
+#pragma unroll
+      for (int l = 0; l < 6; ++l) axpy_c(r, w4_at3(j, l), m[l]);
+      const float a = i == 0 ? w4_at3(0, k) : i == 1 ? w4_at3(1, k) : w4_at3(2, k);
+      if (a == 1.f) y[j] += r;
+      else if (a == -1.f) y[j] -= r;
+      else if (a != 0.f) y[j] += a * r;  // as axpy_c (contracted to the same fma)
+    }
+  }
+  const int64_t e = e0 + el;
+  const int n = (int)(e / C), c = (int)(e - (int64_t)n * C);
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    float* o = dw + ((size_t)n * 9 + i * 3 + j) * C + c;
+    *o = accumulate ? *o + y[j] : y[j];
   }
 }
 
@@ -1980,15 +2052,26 @@ int launch_wino_input(const float* x, int ldx, int B, int H, int W, int C, float
   return launch_status("wino_input");
 }
 
+// channels per thread of the F(3x3,4x4) dz passes (pis_tune key 40): 2 where 256 is a multiple of
+// N / 2 (the bias partials' channel-group rule), else 4
+static int dz_vw(int N) { return tune_get(PIS_TUNE_DZ_VW) == 2 && N % 2 == 0 && 256 % (N / 2) == 0 ? 2 : 4; }
+
+// blocks of the F(3x3,4x4) dz pass = rows of its bias partials; dz_bias_rows_max: for any key 40
 int wino_dz_blocks(int B, int H, int W, int N, int m) {
-  return grid_of((int64_t)B * (H / m) * (W / m) * (N / 4));
+  return grid_of((int64_t)B * (H / m) * (W / m) * (N / (m == 4 ? dz_vw(N) : 4)));
+}
+int wino_dz_blocks_max(int B, int H, int W, int N, int m) {
+  return std::max(grid_of((int64_t)B * (H / m) * (W / m) * (N / 4)),
+                  m == 4 && N % 2 == 0 ? grid_of((int64_t)B * (H / m) * (W / m) * (N / 2)) : 0);
 }
 
 int launch_wino_dz(const float* dz, int ldz, int B, int H, int W, int N, float* E, hipStream_t s, int m,
                    float* bpart) {
   const int64_t T = (int64_t)B * (H / m) * (W / m);
-  if (m == 4)
-    hipLaunchKernelGGL(wino4_dz_kernel, dim3(grid_of(T * (N / 4))), dim3(256), 0, s, dz, ldz, B, H, W, N, E, bpart);
+  if (m == 4 && dz_vw(N) == 2)
+    hipLaunchKernelGGL(wino4_dz_kernel<2>, dim3(grid_of(T * (N / 2))), dim3(256), 0, s, dz, ldz, B, H, W, N, E, bpart);
+  else if (m == 4)
+    hipLaunchKernelGGL(wino4_dz_kernel<4>, dim3(grid_of(T * (N / 4))), dim3(256), 0, s, dz, ldz, B, H, W, N, E, bpart);
   else
     hipLaunchKernelGGL(wino_dz_kernel, dim3(grid_of(T * (N / 4))), dim3(256), 0, s, dz, ldz, B, H, W, N, E);
   return launch_status("wino_dz");
@@ -1997,12 +2080,16 @@ int launch_wino_dz(const float* dz, int ldz, int B, int H, int W, int N, float* 
 int launch_wino_dz2(const float* dz, int ldz, int B, int H, int W, int N, float* V, float* E, float* bpart,
                     hipStream_t s, float* tmax) {
   const int64_t T = (int64_t)B * (H / 4) * (W / 4);
-  if (tmax)
-    hipLaunchKernelGGL((wino4_dz2_kernel<true>), dim3(grid_of(T * (N / 4))), dim3(256), 0, s, dz, ldz, B, H, W, N, V,
-                       E, bpart, tmax);
+  const int vw = dz_vw(N);
+  const dim3 grid(grid_of(T * (N / vw)));
+  if (tmax && vw == 2)
+    hipLaunchKernelGGL((wino4_dz2_kernel<true, 2>), grid, dim3(256), 0, s, dz, ldz, B, H, W, N, V, E, bpart, tmax);
+  else if (tmax)
+    hipLaunchKernelGGL((wino4_dz2_kernel<true, 4>), grid, dim3(256), 0, s, dz, ldz, B, H, W, N, V, E, bpart, tmax);
+  else if (vw == 2)
+    hipLaunchKernelGGL((wino4_dz2_kernel<false, 2>), grid, dim3(256), 0, s, dz, ldz, B, H, W, N, V, E, bpart, nullptr);
   else
-    hipLaunchKernelGGL((wino4_dz2_kernel<false>), dim3(grid_of(T * (N / 4))), dim3(256), 0, s, dz, ldz, B, H, W, N, V,
-                       E, bpart, nullptr);
+    hipLaunchKernelGGL((wino4_dz2_kernel<false, 4>), grid, dim3(256), 0, s, dz, ldz, B, H, W, N, V, E, bpart, nullptr);
   return launch_status("wino_dz2");
 }
 
@@ -2056,7 +2143,10 @@ bool wino_fused_h3_planned(int B, int H, int W, int C, int N) {
 
 int launch_wino_wgrad_out(const float* M, int N, int C, float* dw, int accumulate, hipStream_t s, int m,
                           int nsplit, int64_t sstride) {
-  if (m == 4)
+  if (m == 4 && ((int64_t)N * C) % 64 == 0)
+    hipLaunchKernelGGL(wino4_wgrad_out_tiled_kernel, dim3((unsigned)((int64_t)N * C / 64)), dim3(256), 0, s, M, N, C,
+                       dw, accumulate, nsplit, sstride);
+  else if (m == 4)
     hipLaunchKernelGGL(wino4_wgrad_out_kernel, dim3(grid_of((int64_t)N * C)), dim3(256), 0, s, M, N, C, dw,
                        accumulate, nsplit, sstride);
   else if (nsplit == 1)

@@ -105,7 +105,7 @@ def test_conv3x3_dgrad_wgrad(hip, B, H, W, Cin, Cout):
 
 # every non-default kernel variant behind pis_tune (include/pis_capi.h) stays exact too
 TUNE_VARIANTS = [(4, 1), (4, 2), (4, 3), (5, 0), (6, 2048), (3, 0), (7, 1), (8, 0), (8, 2), (10, 0), (10, 1),
-                 (11, 0), (13, 0), (13, 1), (13, 2), (13, 3), (10, 2), (10, 3), (14, 0), (14, 1), (14, 2), (15, 0), (16, 0), (17, 4), (22, 0), (25, 1), (26, 0), (26, 1), (27, 0), (31, 0), (39, 3)]
+                 (11, 0), (13, 0), (13, 1), (13, 2), (13, 3), (10, 2), (10, 3), (14, 0), (14, 1), (14, 2), (15, 0), (16, 0), (17, 4), (22, 0), (25, 1), (26, 0), (26, 1), (27, 0), (31, 0), (39, 3), (40, 4)]
 
 
 @pytest.mark.parametrize("key,value", TUNE_VARIANTS)
@@ -883,6 +883,28 @@ def test_wgrad_rowstaged_fp16x3(hip, B, H, W, Cin, Cout, mags):
     assert torch.equal(outs["h3row"], outs["h3row_d3"])
     assert errs["h3row"] <= 1.25 * errs["f32"] + 1e-9, errs
     assert errs["h3row"] < 5e-6, errs
+
+
+def test_wino_wgrad_split_slabs(hip):
+    """The F(3x3,4x4) weight gradient with split-K slabs summed inside the block-tiled output
+    transform (wino4_wgrad_out_tiled_kernel: T = 1024 tiles -> 2 slabs per output) against float64,
+    plain and accumulating into an existing gradient."""
+    B, H, W, Cin, Cout = 4, 64, 64, 256, 256
+    g = torch.Generator().manual_seed(73)
+    x = F.relu(torch.randn(B, Cin, H, W, generator=g, dtype=torch.float64)).float().double()
+    dz = torch.randn(B, Cout, H, W, generator=g, dtype=torch.float64).float().double()
+    dw_ref = torch.nn.grad.conv2d_weight(x, (Cout, Cin, 3, 3), dz, padding=1)
+    xd, dzd = nhwc(x.float()).cuda(), nhwc(dz.float()).cuda()
+    nws = hip.pis_conv3x3_wgrad_ws(B, H, W, Cin, Cout)
+    ws = torch.empty(nws // 4 + 1, device="cuda")
+    dw0 = torch.randn(Cout, 3, 3, Cin, generator=g).cuda()
+    for flags in (0, 8):  # PIS_ACCUMULATE
+        dw = dw0.clone()
+        rc = hip.pis_conv3x3_wgrad(xd.data_ptr(), Cin, dzd.data_ptr(), Cout, dw.data_ptr(), 0, B, H, W, Cin, Cout,
+                                   flags, ws.data_ptr(), nws, s())
+        assert rc == 0, hip.pis_last_error()
+        ref = dw_ref.permute(0, 2, 3, 1) + (dw0.cpu().double() if flags else 0)
+        assert rel_err(dw.cpu().double(), ref) < 5e-6
 
 
 @pytest.mark.parametrize("Cin,Cout", [(128, 64), (512, 256)])
