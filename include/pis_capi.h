@@ -169,7 +169,16 @@ int pis_version(void);
                                (the float4 form: 256 + 30 registers, one wave per SIMD). Measured neutral on the
                                step (21.95 vs 22.02 ms, profiles/r4_g_ab.txt; the passes run at 5-5.9 TB/s
                                isolated either way) */
-#define PIS_TUNE_NKEYS 41
+#define PIS_TUNE_GEMM_256 41 /* Winograd fwd / dgrad GEMM: 1 the fp16x3 256 x 256 kernel (8 waves, operands by
+                                  LDS-DMA into two 64-KB stages, per-wave scales, hi / lo split at fragment
+                                  read), 2 the same with 16-deep K-steps through a 4-stage ring (counted vmcnt,
+                                  one raw barrier per K-step), where T, N % 256 == 0 and the launch has >= 512
+                                  blocks; 0 (default) the 128 x 128 register-staged kernel. Both measured 25-40 %
+                                  slower per GEMM (profiles/r4_i_gemm_256.txt, r4_j_gemm_256_ring.txt) and 3 %
+                                  on the step: the read-time split doubles the split VALU and its scale chain
+                                  (fragment reads -> wave max -> split -> MFMA) serialises each K-step at two
+                                  waves per SIMD */
+#define PIS_TUNE_NKEYS 42
 #define PIS_DEBUG_NOLOAD (1 << 16)
 int pis_tune(int key, int value);
 /* Tooling (tools/bench_gemm.py): time one batched NT GEMM kernel variant in isolation,

@@ -105,7 +105,7 @@ def test_conv3x3_dgrad_wgrad(hip, B, H, W, Cin, Cout):
 
 # every non-default kernel variant behind pis_tune (include/pis_capi.h) stays exact too
 TUNE_VARIANTS = [(4, 1), (4, 2), (4, 3), (5, 0), (6, 2048), (3, 0), (7, 1), (8, 0), (8, 2), (10, 0), (10, 1),
-                 (11, 0), (13, 0), (13, 1), (13, 2), (13, 3), (10, 2), (10, 3), (14, 0), (14, 1), (14, 2), (15, 0), (16, 0), (17, 4), (22, 0), (25, 1), (26, 0), (26, 1), (27, 0), (31, 0), (39, 3), (40, 4)]
+                 (11, 0), (13, 0), (13, 1), (13, 2), (13, 3), (10, 2), (10, 3), (14, 0), (14, 1), (14, 2), (15, 0), (16, 0), (17, 4), (22, 0), (25, 1), (26, 0), (26, 1), (27, 0), (31, 0), (39, 3), (40, 4), (41, 1), (41, 2)]
 
 
 @pytest.mark.parametrize("key,value", TUNE_VARIANTS)
@@ -195,6 +195,18 @@ def test_conv3x3_ex_winograd(hip, B, H, W, Cin, Cout, mode):
         assert rel_err(db.cpu() - 0.25, dz.sum(dim=(0, 2, 3))) < 1e-5
     finally:
         hip.pis_tune(8, prev)
+
+
+@pytest.mark.parametrize("mode", [1, 2])
+def test_conv3x3_gemm_256_shape(hip, mode):
+    """pis_tune(41, 1 / 2) where it engages: T = 4096 tiles x 256 outputs (576 blocks of the
+    256 x 256 LDS-DMA GEMM, two 32-deep stages / the 4-stage ring) for the forward and the input
+    gradient, against fp32 ATen."""
+    prev = hip.pis_tune(41, mode)
+    try:
+        test_conv3x3_ex_winograd(hip, 4, 128, 128, 256, 256, 1)
+    finally:
+        hip.pis_tune(41, prev)
 
 
 def test_conv3x3_c1_wgrad(hip):
@@ -760,6 +772,41 @@ def test_winograd_gemm_fp16x3_scales_any_magnitude(hip):
     for scale in (1e-12, 1e-6, 1e6):
         assert errs[4, scale] <= 1.05 * errs[4, 1.0] + 1e-9, errs
         assert errs[4, scale] <= 1.25 * errs[2, scale] + 1e-9, errs
+
+
+@pytest.mark.parametrize("dist", ["randn", "tiny", "wide", "rows"])
+def test_gemm_256_lds_dma(hip, dist):
+    """The fp16x3 256 x 256 GEMM fed by LDS-DMA (pis_debug_gemm_nt variant 15, pis_tune key 41:
+    per-wave power-of-two scales per 16-deep K-step, hi / lo split at fragment read) against
+    float64, beside the 128 x 128 fp16x3 kernel (11) and the native fp32 MFMA one (3): unit,
+    gradient-sized (A x 1e-9, B x 1e-3), row-wise 10^5-spread and 10^30-apart row blocks."""
+    batch, M, N, K = 3, 512, 512, 160
+    g = torch.Generator().manual_seed(81)
+    A = torch.randn(batch, M, K, generator=g, dtype=torch.float64)
+    Bm = torch.randn(batch, N, K, generator=g, dtype=torch.float64)
+    if dist == "tiny":
+        A *= 1e-9
+        Bm *= 1e-3
+    elif dist == "wide":
+        A *= 10.0 ** (-5 * torch.rand(batch, M, 1, generator=g, dtype=torch.float64))
+    elif dist == "rows":  # K-steps 1e30 apart inside one accumulation chain, and block rows too
+        A[:, :, 64:96] *= 1e-30
+        A[:, 256:] *= 1e15
+    A, Bm = A.float().double(), Bm.float().double()
+    ref = torch.bmm(A, Bm.transpose(1, 2))
+    Ad, Bd = A.float().cuda(), Bm.float().cuda()
+    errs = {}
+    for v in (3, 11, 15, 16):
+        Cm = torch.full((batch, M, N), float("nan"), device="cuda")
+        rc = hip.pis_debug_gemm_nt(Ad.data_ptr(), Bd.data_ptr(), Cm.data_ptr(), M, N, K, batch, v, s())
+        assert rc == 0, hip.pis_last_error()
+        torch.cuda.synchronize()
+        out = Cm.cpu().double()
+        assert torch.isfinite(out).all(), v
+        errs[v] = ((out - ref).norm() / ref.norm()).item()
+    for v in (15, 16):
+        assert errs[v] <= 1.25 * errs[3] + 1e-12, errs
+        assert errs[v] < 5e-6, errs
 
 
 @pytest.mark.parametrize("Cin,Cout", [(256, 256), (512, 128), (64, 128), (128, 64)])
