@@ -148,7 +148,11 @@ int pis_version(void);
                                     two blocks per CU, or one beside a main-stream block), 2 the same with the x
                                     halo rows in an LDS ring. Measured (tools/ab_tune.py, one model): 1 / 2 are
                                     1.6-1.8 % SLOWER on the C2 step — the co-resident main-stream input gradients
-                                    slow down more than the lockout cost (profiles/r4_a_*, r4_b_ab_wblk.txt) */
+                                    slow down more than the lockout cost (profiles/r4_a_*, r4_b_ab_wblk.txt);
+                                    3 the 2-row tiles software-pipelined at one block per CU (two LDS images, two
+                                    register sets, the next tile's split in the MFMAs' basic block; bitwise the
+                                    strip kernel's sums): 12-25 % slower per launch than the 4-row kernel,
+                                    1.8 % on the step (profiles/r4_k_*) */
 #define PIS_TUNE_DIRECT_WBLOCKS 35 /* target workgroups of the strip weight gradient (key 34 = 1): default 512 (two per
                                       CU); the split count is this / (Cout/64 * Cin/64), a multiple of 8 */
 #define PIS_TUNE_HEAD_LOSS_ROWS 36 /* pis_head_loss_fwd: image rows per block (0, default: 8192 / W, at most 16) */

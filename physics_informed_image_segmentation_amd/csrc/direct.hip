@@ -934,7 +934,243 @@ __global__ __launch_bounds__(256, 2) void conv3x3_wgrad_strip_kernel(DirectWArgs
   }
 }
 
-static bool direct_w_strip() { return tune_get(PIS_TUNE_DIRECT_WSTRIP) != 0; }
+// =============================================================================================
+// The same 2-row strip tiles software-pipelined for ONE block per CU (pis_tune key 34 = 3): with
+// one wave per SIMD nothing else hides the staging of a tile (wave maxima, split, LDS stores) or
+// its loads, which the timing twins put at 38 % of the 4-row kernel's time (profiles/r4_h). Two LDS
+// images (2 x 50 KB) and two register sets: while tile t is multiplied from image t & 1, tile t + 1
+// (its scale already known) is split into the other image from register set (t + 1) & 1 — in the
+// same basic block as the MFMAs, so its VALU and LDS stores issue in their gaps — and tile t + 2,
+// loaded a whole tile earlier, has its wave maxima published for the next iteration. One barrier
+// per tile. Same arithmetic per tile as the strip kernel (one power-of-two scale per tile and
+// operand, h3_keep, the accumulators re-expressed when a tile's scales change): bitwise equal to it.
+template <bool TW = false>
+__global__ __launch_bounds__(256, 1) void conv3x3_wgrad_db_kernel(DirectWArgs g) {
+  constexpr int NW = 4, NT = 64 * NW, SZ_PER_T = SZ_ITEMS / NT, SX_PER_T = (SX_ITEMS + NT - 1) / NT;
+  constexpr int NTAP = 9, IMG = SLDS_BYTES;
+  __shared__ __attribute__((aligned(16))) char smem[2 * SLDS_BYTES + SBIAS_BYTES + 64 + 2048];
+  f32x4* sbias = reinterpret_cast<f32x4*>(smem + 2 * SLDS_BYTES);
+  float* red = reinterpret_cast<float*>(smem + 2 * SLDS_BYTES + SBIAS_BYTES);  // [parity][z | x][NW]
+  _Float16* dummy = reinterpret_cast<_Float16*>(smem + 2 * SLDS_BYTES + SBIAS_BYTES + 64);  // 2 KB sink
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wi = (wave >> 1) & 1, wj = wave & 1;
+  const int ncb = g.Cin / 64, pairs = (g.Cout / 64) * ncb;
+  int pair, split;
+  if ((g.splits & 7) == 0) {
+    const int bid = blockIdx.x, xcd = bid & 7, j = bid >> 3;
+    pair = j % pairs;
+    split = (j / pairs) * 8 + xcd;
+  } else {
+    pair = blockIdx.x % pairs;
+    split = blockIdx.x / pairs;
+  }
+  const int n0 = (pair / ncb) * 64, c0 = (pair % ncb) * 64;
+  const int nrp = g.H / SW_H, ncol = g.W / SW_W, per_img = nrp * ncol, ntile = g.B * per_img;
+  const int tps = (ntile + g.splits - 1) / g.splits;
+  const int t_begin = split * tps, t_end = min(ntile, t_begin + tps);
+  const bool do_bias = g.part_bias != nullptr && c0 == 0;
+
+  f32x4 zr[2][SZ_PER_T][2], xr[2][SX_PER_T][2];  // [register set]
+  auto gload = [&](auto set_c, int t) __attribute__((always_inline)) {
+    constexpr int S = decltype(set_c)::value;
+    if (TW && (g.dbg & 1) && t > t_begin + 1) return;
+    const int b = t / per_img, rem = t - b * per_img, col = rem / nrp, rp = rem - col * nrp;
+    const int pr0 = SW_H * rp, pc0 = SW_W * col;
+    const size_t img = (size_t)b * g.H * g.W;
+#pragma unroll
+    for (int j = 0; j < SZ_PER_T; ++j) {
+      const int i = tid + NT * j, px = i >> 3, cg = i & 7;
+      const float* p = g.dz + (img + (size_t)(pr0 + (px >> 5)) * g.W + pc0 + (px & 31)) * g.ldz + n0 + 8 * cg;
+      zr[S][j][0] = *reinterpret_cast<const f32x4*>(p);
+      zr[S][j][1] = *reinterpret_cast<const f32x4*>(p + 4);
+    }
+#pragma unroll
+    for (int j = 0; j < SX_PER_T; ++j) {  // branch-free: clamped address, zero selected
+      const int i = tid + NT * j, q = i >> 3, cg = i & 7;
+      const int qr = q / SH_W, qc = q - qr * SH_W, row = pr0 - 1 + qr, cl = pc0 - 1 + qc;
+      const bool ok = i < SX_ITEMS && row >= 0 && row < g.H && cl >= 0 && cl < g.W;
+      const float* p = g.x + (img + (size_t)min(max(row, 0), g.H - 1) * g.W + min(max(cl, 0), g.W - 1)) * g.ldx + c0 + 8 * cg;
+      const f32x4 v0 = *reinterpret_cast<const f32x4*>(p), v1 = *reinterpret_cast<const f32x4*>(p + 4);
+      xr[S][j][0] = ok ? v0 : f32x4{0.f, 0.f, 0.f, 0.f};
+      xr[S][j][1] = ok ? v1 : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  // wave maxima of a loaded set into red[par] (+ the bias partials from its raw dz)
+  auto publish = [&](auto set_c, int par) __attribute__((always_inline)) {
+    constexpr int S = decltype(set_c)::value;
+    const float mz = wave_max_nonneg(absmax_x4(zr[S]));
+    const float mx = wave_max_nonneg(absmax_x4(xr[S]));
+    if (lane == 0) {
+      red[par * 2 * NW + wave] = mz;
+      red[par * 2 * NW + NW + wave] = mx;
+    }
+    if (do_bias) {
+      f32x4 b0 = sbias[2 * tid], b1 = sbias[2 * tid + 1];
+#pragma unroll
+      for (int j = 0; j < SZ_PER_T; ++j) {
+        b0 += zr[S][j][0];
+        b1 += zr[S][j][1];
+      }
+      sbias[2 * tid] = b0;
+      sbias[2 * tid + 1] = b1;
+    }
+  };
+  // the last staged tile's scales (h3_keep hysteresis, as the strip kernel's sz_cur / sx_cur)
+  float sz_st = 0.f, sx_st = 0.f, sz_min = __builtin_inff(), sx_min = __builtin_inff();
+  auto scales = [&](int par, float& sz, float& sx) __attribute__((always_inline)) {
+    const float* r = red + par * 2 * NW;
+    auto umax4 = [](const float* v) __attribute__((always_inline)) {  // v >= 0: bit-pattern max
+      return __uint_as_float(max(max(__float_as_uint(v[0]), __float_as_uint(v[1])),
+                                 max(__float_as_uint(v[2]), __float_as_uint(v[3]))));
+    };
+    sz = sz_st = h3_keep(sz_st, umax4(r), sz_min);
+    sx = sx_st = h3_keep(sx_st, umax4(r + NW), sx_min);
+  };
+  auto stage = [&](auto set_c, int im, float sz, float sx) __attribute__((always_inline)) {
+    constexpr int S = decltype(set_c)::value;
+    _Float16* dz_img = reinterpret_cast<_Float16*>(smem + im * IMG);
+    _Float16* x_img = reinterpret_cast<_Float16*>(smem + im * IMG + 2 * SZ_HALFS * 2);
+#pragma unroll
+    for (int j = 0; j < SZ_PER_T; ++j) {
+      const int i = tid + NT * j, px = i >> 3, cg = i & 7;
+      u32x2 h0, l0, h1, l1;
+      split2h_x4(zr[S][j][0] * sz, h0, l0);
+      split2h_x4(zr[S][j][1] * sz, h1, l1);
+      *reinterpret_cast<u32x4*>(&dz_img[wsw64(px, cg)]) = u32x4{h0[0], h0[1], h1[0], h1[1]};
+      *reinterpret_cast<u32x4*>(&dz_img[SZ_HALFS + wsw64(px, cg)]) = u32x4{l0[0], l0[1], l1[0], l1[1]};
+    }
+#pragma unroll
+    for (int j = 0; j < SX_PER_T; ++j) {  // items past the halo (wave 0, j = 4) store to a dummy slot
+      const int i = tid + NT * j, qq = i >> 3, cg = i & 7;
+      const bool ok = i < SX_ITEMS;
+      u32x2 h0, l0, h1, l1;
+      split2h_x4(xr[S][j][0] * sx, h0, l0);
+      split2h_x4(xr[S][j][1] * sx, h1, l1);
+      _Float16* dh = ok ? &x_img[wsw64(qq, cg)] : dummy + 16 * lane;
+      _Float16* dl = ok ? &x_img[SX_HALFS + wsw64(qq, cg)] : dummy + 16 * lane + 8;
+      *reinterpret_cast<u32x4*>(dh) = u32x4{h0[0], h0[1], h1[0], h1[1]};
+      *reinterpret_cast<u32x4*>(dl) = u32x4{l0[0], l0[1], l1[0], l1[1]};
+    }
+  };
+
+  f32x16 acc[NTAP];
+#pragma unroll
+  for (int t = 0; t < NTAP; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+  if (do_bias) sbias[2 * tid] = sbias[2 * tid + 1] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int gq = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+  const int kh = gq >> 1;
+  const int cgA = 4 * wi + 2 * (gq & 1) + (p >> 1), cgB = 4 * wj + 2 * (gq & 1) + (p >> 1);
+  auto mfma_tile = [&](int im) __attribute__((always_inline)) {
+    const _Float16* dz_img = reinterpret_cast<const _Float16*>(smem + im * IMG);
+    const _Float16* x_img = reinterpret_cast<const _Float16*>(smem + im * IMG + 2 * SZ_HALFS * 2);
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const int rr = ks >> 1, cc0 = 16 * (ks & 1);
+      f16x8 a[2];
+#pragma unroll
+      for (int pl = 0; pl < 2; ++pl) {
+        const _Float16* base = dz_img + pl * SZ_HALFS;
+        const int px = 16 * ks + 8 * kh + q;
+        const s16x4 lo4 = tr_read(base + wsw64(px, cgA) + 4 * (p & 1));
+        const s16x4 hi4 = tr_read(base + wsw64(px + 4, cgA) + 4 * (p & 1));
+        a[pl] = __builtin_bit_cast(f16x8, __builtin_shufflevector(lo4, hi4, 0, 1, 2, 3, 4, 5, 6, 7));
+      }
+#pragma unroll
+      for (int tap = 0; tap < NTAP; ++tap) {
+        const int r = tap / 3, s = tap % 3;
+        f16x8 bb[2];
+        const int hp = (rr + r) * SH_W + cc0 + 8 * kh + q + s;
+#pragma unroll
+        for (int pl = 0; pl < 2; ++pl) {
+          const _Float16* base = x_img + pl * SX_HALFS;
+          const s16x4 lo4 = tr_read(base + wsw64(hp, cgB) + 4 * (p & 1));
+          const s16x4 hi4 = tr_read(base + wsw64(hp + 4, cgB) + 4 * (p & 1));
+          bb[pl] = __builtin_bit_cast(f16x8, __builtin_shufflevector(lo4, hi4, 0, 1, 2, 3, 4, 5, 6, 7));
+        }
+        acc[tap] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[1], bb[0], acc[tap], 0, 0, 0);
+        acc[tap] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[0], bb[1], acc[tap], 0, 0, 0);
+        acc[tap] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[0], bb[0], acc[tap], 0, 0, 0);
+      }
+    }
+  };
+
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  float uz = 0.f, ux = 0.f;  // the accumulators' units
+  float szn = 0.f, sxn = 0.f;  // the scales of the tile staged last (the next one to multiply)
+  const int nt = t_end - t_begin;
+  if (nt > 0) {
+    gload(I0{}, t_begin);
+    if (nt > 1) gload(I1{}, t_begin + 1);
+    publish(I0{}, 0);
+    __syncthreads();
+    scales(0, szn, sxn);
+    stage(I0{}, 0, szn, sxn);
+    if (nt > 1) publish(I1{}, 1);
+    __syncthreads();
+  }
+  // tile k: image k & 1; its successor's raw data in set (k + 1) & 1 with maxima in red[(k + 1) & 1];
+  // set k & 1 is free and takes tile k + 2
+  auto iter = [&](int k, auto cur_c) __attribute__((always_inline)) {
+    constexpr int CUR = decltype(cur_c)::value, NXT = CUR ^ 1;
+    using ICUR = std::integral_constant<int, CUR>;
+    using INXT = std::integral_constant<int, NXT>;
+    if (uz != szn || ux != sxn) {  // this tile's scales differ from the partial sums' units
+      if (uz != 0.f) {
+        const float fz = szn / uz, fx = sxn / ux;
+#pragma unroll
+        for (int tp = 0; tp < NTAP; ++tp) acc[tp] = (acc[tp] * fz) * fx;
+      }
+      uz = szn;
+      ux = sxn;
+    }
+    const bool has1 = k + 1 < nt, has2 = k + 2 < nt;
+    float sz1 = 0.f, sx1 = 0.f;
+    if (has1) scales(NXT, sz1, sx1);
+    gload(ICUR{}, t_begin + min(k + 2, nt - 1));  // unconditional (a valid tile past the end): no branch
+    mfma_tile(CUR);
+    // unconditional (branch-free, so it shares the MFMAs' basic block): on the last tile it writes
+    // stale registers into the image nobody reads again
+    if (!(TW && (g.dbg & 2))) stage(INXT{}, NXT, sz1, sx1);
+    if (has2) publish(ICUR{}, CUR);
+    __syncthreads();
+    szn = sz1;
+    sxn = sx1;
+  };
+#pragma unroll 1
+  for (int k = 0; k < nt; k += 2) {
+    iter(k, I0{});
+    if (k + 1 < nt) iter(k + 1, I1{});
+  }
+
+  const float iz = uz > 0.f ? 1.f / uz : 0.f, ix = ux > 0.f ? 1.f / ux : 0.f;
+  float* slab = g.part + (size_t)split * g.Cout * 9 * g.Cin;
+  const int c = c0 + 32 * wj + (lane & 31);
+#pragma unroll
+  for (int tt = 0; tt < NTAP; ++tt) {
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+      const int n = n0 + 32 * wi + (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5);
+      slab[((size_t)n * 9 + tt) * g.Cin + c] = (acc[tt][reg] * iz) * ix;
+    }
+  }
+  if (do_bias) {
+    const float* rb = reinterpret_cast<const float*>(sbias);
+    __syncthreads();
+    if (tid < 64) {
+      const int cg = tid >> 3, e = tid & 7;
+      float sum = 0.f;
+      for (int k = 0; k < NT / 8; ++k) sum += rb[(8 * k + cg) * 8 + e];
+      g.part_bias[(size_t)split * g.Cout + n0 + tid] = sum;
+    }
+  }
+}
+
+static bool direct_w_strip() { return tune_get(PIS_TUNE_DIRECT_WSTRIP) != 0 && tune_get(PIS_TUNE_DIRECT_WSTRIP) != 3; }
+static bool direct_w_db() { return tune_get(PIS_TUNE_DIRECT_WSTRIP) == 3; }
+
 
 bool direct_w_wanted(int B, int H, int W, int Cin, int Cout, int ldx, int ldz) {
   if (!(B > 0 && H % WT_H == 0 && W % WT_W == 0 && Cin % 64 == 0 && Cout % 64 == 0 && ldz % 4 == 0 && ldx % 4 == 0))
@@ -952,10 +1188,11 @@ static int direct_w_splits(int B, int H, int W, int Cin, int Cout) {
 
 // the strip kernel's split count: ~PIS_TUNE_DIRECT_WBLOCKS workgroups over the (n, c) pairs, a
 // multiple of 8 (the pairs of one split on one XCD) where there are enough tiles
-static int direct_ws_splits(int B, int H, int W, int Cin, int Cout) {
+// (cap: the double-buffered kernel, one block per CU, takes at most 256 workgroups)
+static int direct_ws_splits(int B, int H, int W, int Cin, int Cout, int cap = 1 << 30) {
   const int pairs = (Cout / 64) * (Cin / 64);
   const int ntile = B * (H / SW_H) * (W / SW_W);
-  const int target = std::max(8, tune_get(PIS_TUNE_DIRECT_WBLOCKS));
+  const int target = std::max(8, std::min(cap, tune_get(PIS_TUNE_DIRECT_WBLOCKS)));
   int sp = std::max(1, target / std::max(1, pairs));
   if (sp >= 8) sp &= ~7;
   return std::max(1, std::min(sp, ntile));
@@ -975,8 +1212,9 @@ int launch_direct_wgrad(const float* x, int ldx, const float* dz, int ldz, float
   DirectWArgs g{};
   g.x = x; g.ldx = ldx; g.dz = dz; g.ldz = ldz;
   g.B = B; g.H = H; g.W = W; g.Cin = Cin; g.Cout = Cout;
-  const bool strip = direct_w_strip();
-  g.splits = strip ? direct_ws_splits(B, H, W, Cin, Cout) : direct_w_splits(B, H, W, Cin, Cout);
+  const bool strip = direct_w_strip(), dbuf = direct_w_db();
+  g.splits = dbuf ? direct_ws_splits(B, H, W, Cin, Cout, 256)
+             : strip ? direct_ws_splits(B, H, W, Cin, Cout) : direct_w_splits(B, H, W, Cin, Cout);
   g.dbg = tune_get(PIS_TUNE_DEBUG_NOLOAD);
   g.part = reinterpret_cast<float*>(ws);
   g.part_bias = db ? g.part + (size_t)g.splits * Cout * 9 * Cin : nullptr;
@@ -985,7 +1223,11 @@ int launch_direct_wgrad(const float* x, int ldx, const float* dz, int ldz, float
   const dim3 grid(g.splits * pairs);
   launch_hook("direct_wgrad_h3", 0, s, flop);
   const bool ring = tune_get(PIS_TUNE_DIRECT_WSTRIP) == 2;
-  if (strip && g.dbg && ring)
+  if (dbuf && g.dbg)
+    hipLaunchKernelGGL((conv3x3_wgrad_db_kernel<true>), grid, dim3(256), 0, s, g);
+  else if (dbuf)
+    hipLaunchKernelGGL((conv3x3_wgrad_db_kernel<false>), grid, dim3(256), 0, s, g);
+  else if (strip && g.dbg && ring)
     hipLaunchKernelGGL((conv3x3_wgrad_strip_kernel<true, true>), grid, dim3(256), 0, s, g);
   else if (strip && g.dbg)
     hipLaunchKernelGGL((conv3x3_wgrad_strip_kernel<true, false>), grid, dim3(256), 0, s, g);
