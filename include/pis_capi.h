@@ -182,7 +182,12 @@ int pis_version(void);
                                   on the step: the read-time split doubles the split VALU and its scale chain
                                   (fragment reads -> wave max -> split -> MFMA) serialises each K-step at two
                                   waves per SIMD */
-#define PIS_TUNE_NKEYS 42
+#define PIS_TUNE_LAST_WGRAD_MAIN 42 /* host schedule (physics_informed_image_segmentation_amd/unet.py): 1 (default) the
+                                         step's last weight gradient (enc1.conv0) on the main stream, idle after
+                                         enc1.conv1's input gradient, beside the side stream's enc1.conv1 weight
+                                         gradient; 0 on the side stream after it (measured neutral: 22.67 vs
+                                         22.66 ms, profiles/r4_l_ab_sched.txt) */
+#define PIS_TUNE_NKEYS 43
 #define PIS_DEBUG_NOLOAD (1 << 16)
 int pis_tune(int key, int value);
 /* Tooling (tools/bench_gemm.py): time one batched NT GEMM kernel variant in isolation,

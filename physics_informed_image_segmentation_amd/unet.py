@@ -882,6 +882,17 @@ class UNetEngine:
             if l > 1:
                 g_pool = _Buf(gb(f"g_pool{l - 1}", B, Hl, Wl, Cl // 2), Cl // 2)
                 conv_bwd(blk.conv0, _Buf(bf[f"pool{l - 1}"], Cl // 2), g_a, g_pool, Hl, Wl, None, None)
+            elif (side is not main and m.grad_ready_hook is None and self.keep.get(id(blk.conv0)) is None
+                  and lib.pis_tune(_hip.PIS_TUNE_LAST_WGRAD_MAIN, -1) != 0
+                  and lib.pis_conv3x3_wgrad_ws(B, Hl, Wl, m.in_channels, blk.conv0.out_channels) <= wsb):
+                # the step's last weight gradient (enc1.conv0, input channels = the image's): its dz
+                # is the main stream's last product and the main stream is idle after it, while the
+                # side stream still runs enc1.conv1's weight gradient — so it runs here, in the
+                # main stream's workspace (free after enc1.conv1's input gradient), beside that tail
+                conv = blk.conv0
+                call("pis_conv3x3_wgrad_keep", self.x.data_ptr(), m.in_channels, g_a.p, g_a.ld,
+                     self._gptr(conv.weight), self._gptr(conv.bias), B, Hl, Wl, m.in_channels, conv.out_channels,
+                     acc, ws, wsb, 0, st)
             else:
                 conv_bwd(blk.conv0, _Buf(self.x, m.in_channels), g_a, None, Hl, Wl, None, None)
 
