@@ -187,7 +187,13 @@ int pis_version(void);
                                          enc1.conv1's input gradient, beside the side stream's enc1.conv1 weight
                                          gradient; 0 on the side stream after it (measured neutral: 22.67 vs
                                          22.66 ms, profiles/r4_l_ab_sched.txt) */
-#define PIS_TUNE_NKEYS 43
+#define PIS_TUNE_DIRECT_W_VWALK 43 /* the 4-row direct weight gradient (key 34 = 0): 1 (default) each block walks a
+                                        contiguous run of tiles down the image columns (vertical neighbours share
+                                        two x halo rows: L2 hits) with the pairs of one split on one XCD; 0 the
+                                        round-3 strided tile order. HBM reads per launch 2218 -> 1674 MB on
+                                        dec1.conv0 (1.38x -> 1.04x algorithmic; enc1.conv1 1.03x either way,
+                                        profiles/r4_o_direct_wgrad_traffic.txt), time unchanged (r4_n) */
+#define PIS_TUNE_NKEYS 44
 #define PIS_DEBUG_NOLOAD (1 << 16)
 int pis_tune(int key, int value);
 /* Tooling (tools/bench_gemm.py): time one batched NT GEMM kernel variant in isolation,

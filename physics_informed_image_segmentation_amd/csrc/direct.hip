@@ -488,6 +488,7 @@ struct DirectWArgs {
   float* part_bias;  // [splits][Cout] or NULL
   int B, H, W, Cin, Cout, splits;
   int dbg;           // timing twins, as DirectArgs::dbg
+  int vwalk;         // 4-row kernel (pis_tune key 43): 1 contiguous tile runs walked down the columns
 };
 
 constexpr int WT_H = 4, WT_W = 32, WT_P = WT_H * WT_W, WH_H = WT_H + 2, WH_W = WT_W + 2, WH_P = WH_H * WH_W;
@@ -512,15 +513,31 @@ __global__ __launch_bounds__(256, 1) void conv3x3_wgrad_h3_kernel(DirectWArgs g)
   const int wi = (wave >> 1) & 1, wj = wave & 1;  // n-half, c-half
   constexpr int tap0 = 0, ntap = 9;
   const int ncb = g.Cin / 64, pairs = (g.Cout / 64) * ncb;
-  const int pair = blockIdx.x % pairs, split = blockIdx.x / pairs;
+  // vwalk (key 43): a block owns a contiguous run of tiles ordered row-quad fastest, so consecutive
+  // tiles are vertical neighbours sharing two x halo rows (fetched a tile ago: L2 hits, x read from
+  // HBM ~1.06x instead of 1.59x), and the pairs of one split go to one XCD back to back (they share
+  // its dz / x tiles); else tiles t = split, split + splits, ... in row-major order
+  int pair, split;
+  if (g.vwalk && (g.splits & 7) == 0) {
+    const int bid = blockIdx.x, xcd = bid & 7, j = bid >> 3;
+    pair = j % pairs;
+    split = (j / pairs) * 8 + xcd;
+  } else {
+    pair = blockIdx.x % pairs;
+    split = blockIdx.x / pairs;
+  }
   const int n0 = (pair / ncb) * 64, c0 = (pair % ncb) * 64;
-  const int tw_n = g.W / WT_W, per_img = (g.H / WT_H) * tw_n, ntile = g.B * per_img;
+  const int tw_n = g.W / WT_W, nrq = g.H / WT_H, per_img = nrq * tw_n, ntile = g.B * per_img;
   const bool do_bias = g.part_bias != nullptr && c0 == 0;
+  const int tps = (ntile + g.splits - 1) / g.splits;
+  const int t_begin = g.vwalk ? split * tps : split, t_end = g.vwalk ? min(ntile, t_begin + tps) : ntile;
+  const int t_step = g.vwalk ? 1 : g.splits;
 
   f32x4 zr[WZ_PER_T][2], xr[WX_PER_T][2];
   auto gload = [&](int t) {
-    if (TW && (g.dbg & 1) && t != split) return;
-    const int b = t / per_img, rem = t - b * per_img, pr0 = (rem / tw_n) * WT_H, pc0 = (rem % tw_n) * WT_W;
+    if (TW && (g.dbg & 1) && t != t_begin) return;
+    const int b = t / per_img, rem = t - b * per_img;
+    const int pr0 = (g.vwalk ? rem % nrq : rem / tw_n) * WT_H, pc0 = (g.vwalk ? rem / nrq : rem % tw_n) * WT_W;
     const size_t img = (size_t)b * g.H * g.W;
 #pragma unroll
     for (int j = 0; j < WZ_PER_T; ++j) {
@@ -557,11 +574,11 @@ __global__ __launch_bounds__(256, 1) void conv3x3_wgrad_h3_kernel(DirectWArgs g)
   const int kh = gq >> 1;  // k half (pixels 8 kh ..)
   const int cgA = 4 * wi + 2 * (gq & 1) + (p >> 1), cgB = 4 * wj + 2 * (gq & 1) + (p >> 1);
 
-  int t = split;
-  if (t < ntile) gload(t);
+  int t = t_begin;
+  if (t < t_end) gload(t);
 #pragma unroll 1
-  for (; t < ntile; t += g.splits) {
-    if (!(TW && (g.dbg & 2) && t != split)) {
+  for (; t < t_end; t += t_step) {
+    if (!(TW && (g.dbg & 2) && t != t_begin)) {
     // 1. block maxima of the staged operands
     float mz = wave_max_nonneg(absmax_x4(zr));
     float mx = wave_max_nonneg(absmax_x4(xr));
@@ -618,7 +635,7 @@ __global__ __launch_bounds__(256, 1) void conv3x3_wgrad_h3_kernel(DirectWArgs g)
     __syncthreads();
     }
     // 3. the next tile's loads fly during this tile's MFMAs
-    if (t + g.splits < ntile) gload(t + g.splits);
+    if (t + t_step < t_end) gload(t + t_step);
 #pragma unroll
     for (int ks = 0; ks < 8; ++ks) {  // 16-pixel K-steps: tile row ks >> 1, columns 16 (ks & 1) ..
       const int rr = ks >> 1, cc0 = 16 * (ks & 1);
@@ -1216,6 +1233,7 @@ int launch_direct_wgrad(const float* x, int ldx, const float* dz, int ldz, float
   g.splits = dbuf ? direct_ws_splits(B, H, W, Cin, Cout, 256)
              : strip ? direct_ws_splits(B, H, W, Cin, Cout) : direct_w_splits(B, H, W, Cin, Cout);
   g.dbg = tune_get(PIS_TUNE_DEBUG_NOLOAD);
+  g.vwalk = tune_get(PIS_TUNE_DIRECT_W_VWALK);
   g.part = reinterpret_cast<float*>(ws);
   g.part_bias = db ? g.part + (size_t)g.splits * Cout * 9 * Cin : nullptr;
   const int pairs = (Cout / 64) * (Cin / 64);

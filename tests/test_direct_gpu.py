@@ -83,7 +83,7 @@ FWD_VARIANTS = [dict(), dict(k32=0)]
 # weight gradient: key 34 = 0 (default) the 4-row kernel, 1 the 2-row strip kernel, 2 the strip kernel
 # with the LDS halo ring, 3 the strip tiles double-buffered at one block per CU; key 35 = 64: few
 # workgroups, so every strip block walks many tiles down (and across) column strips and image boundaries
-WG_VARIANTS = [dict(), dict(k34=1), dict(k34=1, k35=64), dict(k34=2), dict(k34=2, k35=64), dict(k34=3)]
+WG_VARIANTS = [dict(), dict(k43=0), dict(k34=1), dict(k34=1, k35=64), dict(k34=2), dict(k34=2, k35=64), dict(k34=3)]
 
 
 @pytest.mark.parametrize("variant", FWD_VARIANTS)
