@@ -193,7 +193,11 @@ int pis_version(void);
                                         round-3 strided tile order. HBM reads per launch 2218 -> 1674 MB on
                                         dec1.conv0 (1.38x -> 1.04x algorithmic; enc1.conv1 1.03x either way,
                                         profiles/r4_o_direct_wgrad_traffic.txt), time unchanged (r4_n) */
-#define PIS_TUNE_NKEYS 44
+#define PIS_TUNE_DIRECT_WGRAD_MAIN 44 /* host schedule (unet.py): 1 a direct layer's weight gradient on the main stream
+                                           right after its input gradient; 0 (default) on the weight-gradient
+                                           stream beside the main stream's next work (1 measured neutral:
+                                           22.18 vs 22.11 ms, profiles/r4_p_ab_direct_wgrad_main.txt) */
+#define PIS_TUNE_NKEYS 45
 #define PIS_DEBUG_NOLOAD (1 << 16)
 int pis_tune(int key, int value);
 /* Tooling (tools/bench_gemm.py): time one batched NT GEMM kernel variant in isolation,

@@ -291,7 +291,7 @@ def test_direct_wgrad_x_magnitude_down_the_strip(hip, variant):
 
 
 @pytest.mark.parametrize("knobs", [dict(k29=2), dict(k37=1, k34=1), dict(k37=1, k34=1, k35=64), dict(k37=1, k34=2),
-                                   dict(k29=2, k34=3)])
+                                   dict(k29=2, k34=3), dict(k44=1), dict(k29=2, k44=1)])
 @pytest.mark.parametrize("loss_kw", [dict(), dict(rd_w=1e-2, pf_w=1e-2, D=5.0, a=0.5, eps=0.05)])
 def test_train_step_with_direct_convs(hip, loss_kw, knobs):
     """The whole training step with every eligible conv on the direct kernels (key 29 = 2: forward
