@@ -747,8 +747,14 @@ __global__ __launch_bounds__(NT) void head_loss_fwd_kernel(HeadLossFwdArgs h) {
   extern __shared__ __attribute__((aligned(16))) float su[];  // [R + 2][SW]: image column c at c + 4
   const LossArgs& g = h.a.g;
   const int H = g.H, W = g.W, SW = W + 8;
-  const int band = blockIdx.x, b = blockIdx.y;
+  // XCD-grouped (consecutive bands of a sample on one XCD, xcd_remap2) and alternating walk
+  // direction (even bands bottom-up, odd bands top-down): the two blocks on either side of a band
+  // boundary fetch its two rows at the same time — both at their start, or both at their end — so
+  // the second fetch of a halo row is an L2 hit instead of an HBM read
+  const Remap2 rmp = xcd_remap2();
+  const int band = rmp.bid, b = rmp.batch;
   const int y0 = band * h.R, nr = min(h.R, H - y0);
+  const bool rev = (band & 1) == 0;
   const int tid = threadIdx.x, sub = tid & 15, grp = tid >> 4;
   const size_t HW = (size_t)H * W;
   const float* xb = h.x + (size_t)b * HW * h.ldx + 4 * sub;
@@ -759,15 +765,16 @@ __global__ __launch_bounds__(NT) void head_loss_fwd_kernel(HeadLossFwdArgs h) {
   // one's sums run
   const int cpr = W / (NG * PP), nchunk = (nr + 2) * cpr;
   f32x4 xa[PP], xn[PP];
+  auto srow = [&](int ch) { const int r = ch / cpr; return rev ? nr + 1 - r : r; };  // staged row of chunk ch
   auto load = [&](f32x4 (&xv)[PP], int ch) __attribute__((always_inline)) {
-    const int r = ch / cpr, x0 = (ch - r * cpr) * (NG * PP) + grp;  // block-uniform r
+    const int r = srow(ch), x0 = (ch - (ch / cpr) * cpr) * (NG * PP) + grp;  // block-uniform r
     const int gy = clampi(refl(y0 - 1 + r, H), 0, H - 1);
     const float* row = xb + (size_t)gy * W * h.ldx;
 #pragma unroll
     for (int j = 0; j < PP; ++j) xv[j] = *reinterpret_cast<const f32x4*>(row + (size_t)(x0 + NG * j) * h.ldx);
   };
   auto head = [&](const f32x4 (&xv)[PP], int ch) __attribute__((always_inline)) {
-    const int r = ch / cpr, x0 = (ch - r * cpr) * (NG * PP) + grp;
+    const int r = srow(ch), x0 = (ch - (ch / cpr) * cpr) * (NG * PP) + grp;
     const bool interior = r >= 1 && r <= nr;
     const size_t orow = (size_t)b * HW + (size_t)(y0 - 1 + r) * W;
 #pragma unroll
