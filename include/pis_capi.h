@@ -163,7 +163,8 @@ int pis_version(void);
                                         6.3 % slower on the C2 step (the deep layers' 4x Winograd FLOP saving wins,
                                         profiles/r4_a_bench_k37_1.json) */
 #define PIS_TUNE_HEAD_LOSS_WIDE 38 /* pis_head_loss_fwd with W % 512 == 0: 1 (default) 1024-thread blocks (16 waves,
-                                       one staged row per chunk), 0 the 256-thread form */
+                                       one staged row per chunk), 2 the same with three register sets in flight
+                                       (measured equal, profiles/r4_q_head_loss_fwd.txt), 0 the 256-thread form */
 #define PIS_TUNE_WGRAD_T_DEPTH 39 /* wgrad_h3t_kernel's whole-K-step (EX) form: raw operands of K-step st + D in
                                       flight while K-step st multiplies; 2 (default) or 3 (two / three register
                                       sets; 3 measured neutral on the step, 21.93 vs 21.91 ms:

@@ -740,7 +740,8 @@ struct HeadLossFwdArgs {
 
 // NT threads per block (NG = NT / 16 pixel groups): 1024 at W % 512 == 0 (C2: 256 blocks of 16
 // waves, four waves per SIMD to cover the HBM latency; one staged row per chunk), else 256
-template <bool RD, bool PF, int PP, int NT = 256>
+// D3 (pis_tune key 38 = 2): three register sets, so two chunks' loads are in flight while one is summed
+template <bool RD, bool PF, int PP, int NT = 256, bool D3 = false>
 __global__ __launch_bounds__(NT) void head_loss_fwd_kernel(HeadLossFwdArgs h) {
   constexpr int NG = NT / 16, NWV = NT / 64;
   constexpr bool ST = RD || PF;
@@ -797,12 +798,26 @@ __global__ __launch_bounds__(NT) void head_loss_fwd_kernel(HeadLossFwdArgs h) {
       }
     }
   };
-  if (nchunk > 0) load(xa, 0);
-  for (int ch = 0; ch < nchunk; ch += 2) {  // ping-pong register sets (no copies)
-    if (ch + 1 < nchunk) load(xn, ch + 1);
-    head(xa, ch);
-    if (ch + 2 < nchunk) load(xa, ch + 2);
-    if (ch + 1 < nchunk) head(xn, ch + 1);
+  if constexpr (D3) {
+    f32x4 xc[PP];
+    if (nchunk > 0) load(xa, 0);
+    if (nchunk > 1) load(xn, 1);
+    for (int ch = 0; ch < nchunk; ch += 3) {  // a ring of three register sets (no copies)
+      if (ch + 2 < nchunk) load(xc, ch + 2);
+      head(xa, ch);
+      if (ch + 3 < nchunk) load(xa, ch + 3);
+      if (ch + 1 < nchunk) head(xn, ch + 1);
+      if (ch + 4 < nchunk) load(xn, ch + 4);
+      if (ch + 2 < nchunk) head(xc, ch + 2);
+    }
+  } else {
+    if (nchunk > 0) load(xa, 0);
+    for (int ch = 0; ch < nchunk; ch += 2) {  // ping-pong register sets (no copies)
+      if (ch + 1 < nchunk) load(xn, ch + 1);
+      head(xa, ch);
+      if (ch + 2 < nchunk) load(xa, ch + 2);
+      if (ch + 1 < nchunk) head(xn, ch + 1);
+    }
   }
   // the targets of this thread's items in flight across the barriers (TX threads per row, RY rows
   // per pass; item = 4 pixels)
@@ -1280,6 +1295,7 @@ extern "C" int pis_head_loss_fwd(const float* x, int ldx, const float* w, const 
   const bool rd = all || prm->rd_w > 0.f, pf = all || prm->pf_w > 0.f;
   const int pp = head_loss_fwd_pp(W);
   const bool wide = head_loss_fwd_wide(W);
+  const bool wide3 = wide && tune_get(PIS_TUNE_HEAD_LOSS_WIDE) == 2;
   const size_t smem = (size_t)(h.R + 2) * (W + 8) * sizeof(float);
   const dim3 grid(bands, B);
   hipStream_t s = (hipStream_t)stream;
@@ -1287,7 +1303,8 @@ extern "C" int pis_head_loss_fwd(const float* x, int ldx, const float* w, const 
   launch_hook("head_loss_fwd", 0, s, nbytes);
 #define PIS_HLF(RDV, PFV)                                                                                         \
   do {                                                                                                            \
-    if (wide) hipLaunchKernelGGL((head_loss_fwd_kernel<RDV, PFV, 8, 1024>), grid, dim3(1024), smem, s, h);        \
+    if (wide && wide3) hipLaunchKernelGGL((head_loss_fwd_kernel<RDV, PFV, 8, 1024, true>), grid, dim3(1024), smem, s, h); \
+    else if (wide) hipLaunchKernelGGL((head_loss_fwd_kernel<RDV, PFV, 8, 1024>), grid, dim3(1024), smem, s, h);   \
     else if (pp == 16) hipLaunchKernelGGL((head_loss_fwd_kernel<RDV, PFV, 16>), grid, dim3(256), smem, s, h);     \
     else if (pp == 8) hipLaunchKernelGGL((head_loss_fwd_kernel<RDV, PFV, 8>), grid, dim3(256), smem, s, h);       \
     else hipLaunchKernelGGL((head_loss_fwd_kernel<RDV, PFV, 4>), grid, dim3(256), smem, s, h);                    \
