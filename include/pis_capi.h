@@ -198,7 +198,10 @@ int pis_version(void);
                                            right after its input gradient; 0 (default) on the weight-gradient
                                            stream beside the main stream's next work (1 measured neutral:
                                            22.18 vs 22.11 ms, profiles/r4_p_ab_direct_wgrad_main.txt) */
-#define PIS_TUNE_NKEYS 45
+#define PIS_TUNE_GEMM_PRIO 45 /* Winograd fwd / dgrad GEMM (128 x 128): 1 its MFMA phase at wave priority 1
+                                   (s_setprio) against the co-resident blocks' staging; 0 (default) none
+                                   (1 measured neutral: 22.10 vs 22.13 ms, profiles/r4_s_ab_gemm_prio.txt) */
+#define PIS_TUNE_NKEYS 46
 #define PIS_DEBUG_NOLOAD (1 << 16)
 int pis_tune(int key, int value);
 /* Tooling (tools/bench_gemm.py): time one batched NT GEMM kernel variant in isolation,

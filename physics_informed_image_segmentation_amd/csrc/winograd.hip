@@ -1217,7 +1217,8 @@ __global__ __launch_bounds__(256, OCC) void gemm_nt_x6_bk32_kernel(const float* 
 // first two K-steps, 2 no staging after the first (profiles/r3_q22_gemm_twins.txt: staging is 24-44 %
 // of the time, the loads 0-17 %). (Two LDS stages + two register sets at two blocks per CU — one
 // barrier per K-step, loads a K-step further ahead — ran 10-30 % slower: profiles/r3_q23_gemm_db.txt.)
-template <int BM, int BN, int OCC = 3, bool SC = true, int DBG = 0>
+// PRIO (pis_tune key 45): the MFMA phase at wave priority 1 (s_setprio), the staging at 0
+template <int BM, int BN, int OCC = 3, bool SC = true, int DBG = 0, bool PRIO = false>
 __global__ __launch_bounds__(256, OCC) void gemm_nt_h3_bk32_kernel(const float* __restrict__ A,
                                                                 const float* __restrict__ Bm, float* __restrict__ Cm,
                                                                 int M, int N, int K, int64_t bsA, int64_t bsB,
@@ -1341,6 +1342,7 @@ __global__ __launch_bounds__(256, OCC) void gemm_nt_h3_bk32_kernel(const float* 
         ub = nb;
       }
     }
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       f16x8 af[2][TM], bf[2][TN];
@@ -1362,6 +1364,7 @@ __global__ __launch_bounds__(256, OCC) void gemm_nt_h3_bk32_kernel(const float* 
           acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[0][a], bf[0][b], acc[a][b], 0, 0, 0);
         }
     }
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
     if (kt + 1 < KT) {
       __syncthreads();
       if (DBG != 2) lstore();
@@ -2219,8 +2222,12 @@ int launch_wino3x3(const IGemmArgs& a, int B, void* ws, hipStream_t s, float* ke
                            (int64_t)N * C, T * N);
     } else if (N % 128 == 0) {
       const dim3 grid((int)cdiv(T, 128) * (N / 128), nxi);
-      hipLaunchKernelGGL((gemm_nt_h3_bk32_kernel<128, 128, 3>), grid, dim3(256), 0, s, V, U, Mt, (int)T, N, C,
-                         T * C, (int64_t)N * C, T * N);
+      if (tune_get(PIS_TUNE_GEMM_PRIO) != 0)
+        hipLaunchKernelGGL((gemm_nt_h3_bk32_kernel<128, 128, 3, true, 0, true>), grid, dim3(256), 0, s, V, U, Mt,
+                           (int)T, N, C, T * C, (int64_t)N * C, T * N);
+      else
+        hipLaunchKernelGGL((gemm_nt_h3_bk32_kernel<128, 128, 3>), grid, dim3(256), 0, s, V, U, Mt, (int)T, N, C,
+                           T * C, (int64_t)N * C, T * N);
     } else {
       const dim3 grid((int)cdiv(T, 128) * (N / 64), nxi);
       hipLaunchKernelGGL((gemm_nt_h3_bk32_kernel<128, 64, 4>), grid, dim3(256), 0, s, V, U, Mt, (int)T, N, C,
