@@ -201,7 +201,11 @@ int pis_version(void);
 #define PIS_TUNE_GEMM_PRIO 45 /* Winograd fwd / dgrad GEMM (128 x 128): 1 its MFMA phase at wave priority 1
                                    (s_setprio) against the co-resident blocks' staging; 0 (default) none
                                    (1 measured neutral: 22.10 vs 22.13 ms, profiles/r4_s_ab_gemm_prio.txt) */
-#define PIS_TUNE_NKEYS 46
+#define PIS_TUNE_WINO_OUT_MPF 46 /* Winograd output transform of a masked input gradient: 1 (default) the tile's
+                                      ReLU-mask rows loaded with its M values (one memory round trip per tile,
+                                      151 VGPRs); 0 in the epilogue. Step 22.25 -> 22.04 ms
+                                      (profiles/r4_t_ab_wino_out_mpf.txt) */
+#define PIS_TUNE_NKEYS 47
 #define PIS_DEBUG_NOLOAD (1 << 16)
 int pis_tune(int key, int value);
 /* Tooling (tools/bench_gemm.py): time one batched NT GEMM kernel variant in isolation,

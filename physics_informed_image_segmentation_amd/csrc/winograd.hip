@@ -132,6 +132,25 @@ __device__ __forceinline__ f32x4 conv_epilogue4m(const IGemmArgs& g, size_t pix,
   return v;
 }
 
+// VW channels with the mask already loaded (mk; ignored without PIS_MASK)
+template <int VW>
+__device__ __forceinline__ fvec<VW> conv_epilogue_vm(const IGemmArgs& g, size_t pix, int n, fvec<VW> v, fvec<VW> sc4,
+                                                     fvec<VW> mk) {
+  if (g.flags & PIS_RELU) {
+#pragma unroll
+    for (int k = 0; k < VW; ++k) v[k] = fmaxf(v[k], 0.f);
+  }
+  if (g.flags & PIS_MASK) {
+#pragma unroll
+    for (int k = 0; k < VW; ++k) v[k] = mk[k] > 0.f ? v[k] : 0.f;
+  }
+  v *= sc4;
+  float* dst = g.dst + pix * g.ldd + n;
+  if (g.flags & PIS_ACCUMULATE) v += *reinterpret_cast<const fvec<VW>*>(dst);
+  *reinterpret_cast<fvec<VW>*>(dst) = v;
+  return v;
+}
+
 template <int VW = 4>
 __device__ __forceinline__ fvec<VW> max4(fvec<VW> a, fvec<VW> b, fvec<VW> c, fvec<VW> d) {
   fvec<VW> m;
@@ -562,8 +581,9 @@ __global__ __launch_bounds__(256) void wino4_input_kernel(const float* __restric
 }
 
 // Y = AT M AT^T per tile and VW output channels (pis_tune key 17), then the direct kernels' conv
-// epilogue
-template <int VW>
+// epilogue. MPF (input gradients with a ReLU mask, pis_tune key 46): the tile's 16 mask rows are
+// loaded with its M values, so the epilogue does not wait for a second memory round trip.
+template <int VW, bool MPF = false>
 __global__ __launch_bounds__(256) void wino4_output_kernel(const float* __restrict__ Mt, IGemmArgs g, int B) {
   const int N = g.N, n4n = N / VW, TW = g.W / 4, TH = g.H / 4;
   const int64_t T = (int64_t)B * TH * TW, TN = T * N;
@@ -572,6 +592,16 @@ __global__ __launch_bounds__(256) void wino4_output_kernel(const float* __restri
     int n, b, rem;
     tile_decode<VW>(e, n4n, TH * TW, t, n, b, rem);
     const int ty = rem / TW, tx = rem - ty * TW;
+    fvec<VW> mk[4][4];
+    if constexpr (MPF) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const size_t pix = ((size_t)b * g.H + 4 * ty + i) * g.W + 4 * tx + j;
+          mk[i][j] = *reinterpret_cast<const fvec<VW>*>(g.mask + pix * g.ldm + n);
+        }
+    }
     fvec<VW> y[4][4];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -600,7 +630,8 @@ __global__ __launch_bounds__(256) void wino4_output_kernel(const float* __restri
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const size_t pix = ((size_t)b * g.H + 4 * ty + i) * g.W + 4 * tx + j;
-        o[i][j] = conv_epilogue4<VW>(g, pix, n, y[i][j] + bias4, sc4);
+        if constexpr (MPF) o[i][j] = conv_epilogue_vm<VW>(g, pix, n, y[i][j] + bias4, sc4, mk[i][j]);
+        else o[i][j] = conv_epilogue4<VW>(g, pix, n, y[i][j] + bias4, sc4);
       }
     if (g.pool) {  // the tile's four 2x2 max-pool outputs (the encoder's MaxPool2d)
 #pragma unroll
@@ -2016,7 +2047,10 @@ static int grid_of(int64_t work) { return (int)std::max<int64_t>(1, std::min<int
 // tools/bench_kernels.py --key 17: 2 channels halve the registers, +2-11 % on the 512^2-256^2 layers)
 static void launch_wino4_output(const float* Mt, const IGemmArgs& a, int B, int64_t T, int N, hipStream_t s) {
   if (tune_get(PIS_TUNE_WINO_VW) != 4)
-    hipLaunchKernelGGL(wino4_output_kernel<2>, dim3(grid_of(T * (N / 2))), dim3(256), 0, s, Mt, a, B);
+    if ((a.flags & PIS_MASK) && a.mask && tune_get(PIS_TUNE_WINO_OUT_MPF) != 0)
+      hipLaunchKernelGGL((wino4_output_kernel<2, true>), dim3(grid_of(T * (N / 2))), dim3(256), 0, s, Mt, a, B);
+    else
+      hipLaunchKernelGGL(wino4_output_kernel<2>, dim3(grid_of(T * (N / 2))), dim3(256), 0, s, Mt, a, B);
   else
     hipLaunchKernelGGL(wino4_output_kernel<4>, dim3(grid_of(T * (N / 4))), dim3(256), 0, s, Mt, a, B);
 }
