@@ -203,8 +203,8 @@ int pis_version(void);
                                    (1 measured neutral: 22.10 vs 22.13 ms, profiles/r4_s_ab_gemm_prio.txt) */
 #define PIS_TUNE_WINO_OUT_MPF 46 /* Winograd output transform of a masked input gradient: 1 (default) the tile's
                                       ReLU-mask rows loaded with its M values (one memory round trip per tile,
-                                      151 VGPRs); 0 in the epilogue. Step 22.25 -> 22.04 ms
-                                      (profiles/r4_t_ab_wino_out_mpf.txt) */
+                                      151 VGPRs); 0 in the epilogue. Step 22.25 -> 22.04 ms on one box, 22.43 ->
+                                      22.39 on another (profiles/r4_t_ab_wino_out_mpf.txt, r4_u_*): 0.2-0.9 % */
 #define PIS_TUNE_NKEYS 47
 #define PIS_DEBUG_NOLOAD (1 << 16)
 int pis_tune(int key, int value);
