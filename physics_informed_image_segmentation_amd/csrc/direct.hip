@@ -636,36 +636,68 @@ __global__ __launch_bounds__(256, 1) void conv3x3_wgrad_h3_kernel(DirectWArgs g)
     }
     // 3. the next tile's loads fly during this tile's MFMAs
     if (t + t_step < t_end) gload(t + t_step);
+    // Halo-row-major: the 8 A fragments (tile row rr, column half cc: pixels 16 (2 rr + cc) + 8 kh +
+    // q (+ 4), channels of cgA) are read once; then for each halo row h and column half cc the 3 B
+    // fragments (halo pixel (h, 16 cc + 8 kh + q (+ 4) + s), channels of cgB) serve every tap row r
+    // with rr = h - r. Each accumulator still takes its (rr, cc) contributions in K-step order
+    // 2 rr + cc, three MFMAs each in the same order, so the sums are bitwise those of a loop over
+    // 16-pixel K-steps — but each B fragment is read once per tile, one step AHEAD: the
+    // sched_group_barriers issue step st + 1's 12 reads before step st's 9-27 MFMAs, whose time
+    // hides their latency (the compiler's own schedule waited on each tap's reads right before its
+    // MFMAs: lgkmcnt(0) inside the MFMA stream, profiles/r4_w_*).
+    f16x8 af[4][2][2];
 #pragma unroll
-    for (int ks = 0; ks < 8; ++ks) {  // 16-pixel K-steps: tile row ks >> 1, columns 16 (ks & 1) ..
-      const int rr = ks >> 1, cc0 = 16 * (ks & 1);
-      // A = dz^T (rows n, k pixels): pixels 16 ks + 8 kh + q (+ 4) of the tile, channels of cgA
-      f16x8 a[2];
+    for (int rr = 0; rr < 4; ++rr)
 #pragma unroll
-      for (int pl = 0; pl < 2; ++pl) {
-        const _Float16* base = sz + pl * WZ_HALFS;
-        const int px = 16 * ks + 8 * kh + q;
-        const s16x4 lo4 = tr_read(base + wsw64(px, cgA) + 4 * (p & 1));
-        const s16x4 hi4 = tr_read(base + wsw64(px + 4, cgA) + 4 * (p & 1));
-        a[pl] = __builtin_bit_cast(f16x8, __builtin_shufflevector(lo4, hi4, 0, 1, 2, 3, 4, 5, 6, 7));
-      }
+      for (int cc = 0; cc < 2; ++cc)
 #pragma unroll
-      for (int tt = 0; tt < NTAP; ++tt) {
-        const int tap = tap0 + tt, r = tap / 3, s = tap % 3;
-        // B = x (k pixels, columns c): halo pixel (rr + r, cc0 + 8 kh + q (+ 4) + s), channels of cgB
-        f16x8 bb[2];
-        const int hp = (rr + r) * WH_W + cc0 + 8 * kh + q + s;
+        for (int pl = 0; pl < 2; ++pl) {
+          const _Float16* base = sz + pl * WZ_HALFS;
+          const int px = 16 * (2 * rr + cc) + 8 * kh + q;
+          const s16x4 lo4 = tr_read(base + wsw64(px, cgA) + 4 * (p & 1));
+          const s16x4 hi4 = tr_read(base + wsw64(px + 4, cgA) + 4 * (p & 1));
+          af[rr][cc][pl] = __builtin_bit_cast(f16x8, __builtin_shufflevector(lo4, hi4, 0, 1, 2, 3, 4, 5, 6, 7));
+        }
+    f16x8 bf[2][3][2];
+    auto bload = [&](int st, int buf) __attribute__((always_inline)) {
+      const int h = st >> 1, cc0 = 16 * (st & 1);
+#pragma unroll
+      for (int s = 0; s < 3; ++s) {
+        const int hp = h * WH_W + cc0 + 8 * kh + q + s;
 #pragma unroll
         for (int pl = 0; pl < 2; ++pl) {
           const _Float16* base = sx + pl * WX_HALFS;
           const s16x4 lo4 = tr_read(base + wsw64(hp, cgB) + 4 * (p & 1));
           const s16x4 hi4 = tr_read(base + wsw64(hp + 4, cgB) + 4 * (p & 1));
-          bb[pl] = __builtin_bit_cast(f16x8, __builtin_shufflevector(lo4, hi4, 0, 1, 2, 3, 4, 5, 6, 7));
+          bf[buf][s][pl] = __builtin_bit_cast(f16x8, __builtin_shufflevector(lo4, hi4, 0, 1, 2, 3, 4, 5, 6, 7));
         }
-        acc[tt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[1], bb[0], acc[tt], 0, 0, 0);
-        acc[tt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[0], bb[1], acc[tt], 0, 0, 0);
-        acc[tt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[0], bb[0], acc[tt], 0, 0, 0);
       }
+    };
+    bload(0, 0);
+    __builtin_amdgcn_sched_group_barrier(0x100, 44, 0);  // LDS reads: the A fragments, step 0's B
+#pragma unroll
+    for (int st = 0; st < 12; ++st) {  // (h, cc) = (st >> 1, st & 1)
+      const int h = st >> 1, cc = st & 1, cur = st & 1;
+      if (st + 1 < 12) bload(st + 1, cur ^ 1);
+#pragma unroll
+      for (int r = 0; r < 3; ++r) {
+        const int rr = h - r;
+        if (rr < 0 || rr > 3) continue;
+#pragma unroll
+        for (int s = 0; s < 3; ++s) {
+          const int tt = 3 * r + s;
+          acc[tt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[rr][cc][1], bf[cur][s][0], acc[tt], 0, 0, 0);
+          acc[tt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[rr][cc][0], bf[cur][s][1], acc[tt], 0, 0, 0);
+          acc[tt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[rr][cc][0], bf[cur][s][0], acc[tt], 0, 0, 0);
+        }
+      }
+      if (st + 1 < 12) __builtin_amdgcn_sched_group_barrier(0x100, 12, 0);  // next step's reads,
+      if (h == 0 || h == 5)                                                  // then this step's MFMAs
+        __builtin_amdgcn_sched_group_barrier(0x008, 9, 0);
+      else if (h == 1 || h == 4)
+        __builtin_amdgcn_sched_group_barrier(0x008, 18, 0);
+      else
+        __builtin_amdgcn_sched_group_barrier(0x008, 27, 0);
     }
     __syncthreads();
   }
