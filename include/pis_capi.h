@@ -155,7 +155,9 @@ int pis_version(void);
                                     1.8 % on the step (profiles/r4_k_*) */
 #define PIS_TUNE_DIRECT_WBLOCKS 35 /* target workgroups of the strip weight gradient (key 34 = 1): default 512 (two per
                                       CU); the split count is this / (Cout/64 * Cin/64), a multiple of 8 */
-#define PIS_TUNE_HEAD_LOSS_ROWS 36 /* pis_head_loss_fwd: image rows per block (0, default: 8192 / W, at most 16) */
+#define PIS_TUNE_HEAD_LOSS_ROWS 36 /* pis_head_loss_fwd: image rows per block (0, default: 4096 / W, at most 16,
+                                       doubled while the row bands exceed 2048; 8 at C2 measured 131 us against
+                                       134-145 at 16, profiles/r4_ah_head_loss_rows.txt) */
 #define PIS_TUNE_DIRECT_WGRAD_ALL 37 /* 1: the direct strip weight gradient (key 34 = 1 or 2) for EVERY 3x3 layer it
                                         covers (Cin, Cout % 64, H % 4, W % 32), the Winograd layers' forward / input
                                         gradient unchanged (no kept input transform, no E half of the dz pass);

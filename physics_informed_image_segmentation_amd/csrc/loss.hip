@@ -1239,11 +1239,16 @@ extern "C" int pis_pde_fields_bwd(const float* u, const float* g_lap, const floa
   return launch_status("pde_fields_bwd");
 }
 
-// rows per block of the fused head + loss forward: 8192 / W (16 at W = 512: 256 blocks of 18 staged
-// rows at C2, 12.5 % of the head input fetched twice; 8 at W = 1024), pis_tune key 36 overrides
-static int head_loss_fwd_rows(int H, int W) {
+// rows per block of the fused head + loss forward: 4096 / W, i.e. 4096 pixels (8 at W = 512: 512
+// blocks of 10 staged rows at C2, two per CU; 4 at W = 1024), doubled while the batch's row bands
+// exceed LOSS_MAX_BLOCKS; pis_tune key 36 overrides. At C2 8 rows ran the kernel in 131 us against
+// 134-145 us at 16 and 144 at 4 (0.54 vs 0.48-0.52 of 8 TB/s live; profiles/r4_ah_head_loss_rows.txt)
+// although a quarter of the head input is fetched twice (the halo rows, mostly from L2)
+static int head_loss_fwd_rows(int B, int H, int W) {
   const int t = tune_get(PIS_TUNE_HEAD_LOSS_ROWS);
-  const int r = t > 0 ? t : std::max(2, std::min(16, 8192 / std::max(1, W)));
+  int r = t > 0 ? t : std::max(2, std::min(16, 4096 / std::max(1, W)));
+  if (t <= 0)
+    while (r < H && (int64_t)B * ((H + r - 1) / r) > LOSS_MAX_BLOCKS) r *= 2;
   return std::max(1, std::min(r, H));
 }
 
@@ -1260,7 +1265,7 @@ extern "C" size_t pis_head_loss_fwd_ws(int B, int H, int W) {
 }
 
 extern "C" int pis_head_loss_fwd_ok(int B, int H, int W, int C) {
-  const int R = head_loss_fwd_rows(H, W);
+  const int R = head_loss_fwd_rows(B, H, W);
   return C == 64 && B > 0 && H >= 2 && W >= 8 && W <= 2048 && head_loss_fwd_pp(W) > 0 &&
          (int64_t)B * ((H + R - 1) / R) <= LOSS_MAX_BLOCKS;
 }
@@ -1278,7 +1283,7 @@ extern "C" int pis_head_loss_fwd(const float* x, int ldx, const float* w, const 
   PIS_CHECK_ARG(ws && ws_bytes >= pis_head_loss_fwd_ws(B, H, W), "pis_head_loss_fwd: workspace too small");
   HeadLossFwdArgs h{};
   h.x = x; h.ldx = ldx; h.w = w; h.bias = bias; h.z = z; h.u = u;
-  h.R = head_loss_fwd_rows(H, W);
+  h.R = head_loss_fwd_rows(B, H, W);
   LossArgs& g = h.a.g;
   g.p = u; g.t = t; g.B = B; g.H = H; g.W = W;
   g.dice_w = prm->dice_w; g.bce_w = prm->bce_w; g.rd_w = prm->rd_w; g.pf_w = prm->pf_w;
