@@ -250,8 +250,7 @@ DIRECT_ROLES = {
                         "on the original weights; the ReLU-mask rows prefetched where masked)",
                         ["conv3x3_h3_kernel<false, true, false, true>", "conv3x3_h3_kernel<false, false, false, true>"]),
     "direct_wgrad_h3": ("roofline_direct_wgrad", "conv3x3_wgrad_h3_kernel (weight gradient: 4-row tiles, split-K "
-                        "slabs; pis_tune key 34 = 1 / 2: the 2-row column-strip conv3x3_wgrad_strip_kernel)",
-                        ["conv3x3_wgrad_strip_kernel", "conv3x3_wgrad_h3_kernel"]),
+                        "slabs)", ["conv3x3_wgrad_h3_kernel"]),
 }
 
 

@@ -142,49 +142,24 @@ int pis_version(void);
                                     one block per CU, next chunk's weights by LDS-DMA and its halo split while this
                                     chunk multiplies) measured 3-14 % slower than the 4-wave kernel
                                     (profiles/r3_q26_direct_w8.txt); ignored */
-#define PIS_TUNE_DIRECT_WSTRIP 34 /* direct fp16x3 weight gradient (key 29): 0 (default) the round-3 4-row kernel (497
-                                    registers: one wave fills a SIMD, so main-stream blocks wait for its CUs);
-                                    1 2-row tiles walked down a column strip per block (250 registers, 59 KB LDS:
-                                    two blocks per CU, or one beside a main-stream block), 2 the same with the x
-                                    halo rows in an LDS ring. Measured (tools/ab_tune.py, one model): 1 / 2 are
-                                    1.6-1.8 % SLOWER on the C2 step — the co-resident main-stream input gradients
-                                    slow down more than the lockout cost (profiles/r4_a_*, r4_b_ab_wblk.txt);
-                                    3 the 2-row tiles software-pipelined at one block per CU (two LDS images, two
-                                    register sets, the next tile's split in the MFMAs' basic block; bitwise the
-                                    strip kernel's sums): 12-25 % slower per launch than the 4-row kernel,
-                                    1.8 % on the step (profiles/r4_k_*) */
-#define PIS_TUNE_DIRECT_WBLOCKS 35 /* target workgroups of the strip weight gradient (key 34 = 1): default 512 (two per
-                                      CU); the split count is this / (Cout/64 * Cin/64), a multiple of 8 */
+#define PIS_TUNE_DIRECT_WSTRIP 34 /* retired (round 5): the 2-row strip, LDS-ring and software-pipelined direct weight
+                                     gradients measured 1.6-1.8 % slower on the C2 step than the 4-row kernel
+                                     (profiles/r4_a_*, r4_b_ab_wblk.txt, r4_k_*); removed, the key is ignored */
+#define PIS_TUNE_DIRECT_WBLOCKS 35 /* retired (round 5) with key 34; ignored */
 #define PIS_TUNE_HEAD_LOSS_ROWS 36 /* pis_head_loss_fwd: image rows per block (0, default: 4096 / W, at most 16,
                                        doubled while the row bands exceed 2048; 8 at C2 measured 131 us against
                                        134-145 at 16, profiles/r4_ah_head_loss_rows.txt) */
-#define PIS_TUNE_DIRECT_WGRAD_ALL 37 /* 1: the direct strip weight gradient (key 34 = 1 or 2) for EVERY 3x3 layer it
-                                        covers (Cin, Cout % 64, H % 4, W % 32), the Winograd layers' forward / input
-                                        gradient unchanged (no kept input transform, no E half of the dz pass);
-                                        0 (default): the weight gradient follows key 29's layer policy. Measured
-                                        6.3 % slower on the C2 step (the deep layers' 4x Winograd FLOP saving wins,
-                                        profiles/r4_a_bench_k37_1.json) */
+#define PIS_TUNE_DIRECT_WGRAD_ALL 37 /* retired (round 5): the strip weight gradient on every layer was 6.3 % slower
+                                        (profiles/r4_a_bench_k37_1.json); ignored */
 #define PIS_TUNE_HEAD_LOSS_WIDE 38 /* pis_head_loss_fwd with W % 512 == 0: 1 (default) 1024-thread blocks (16 waves,
                                        one staged row per chunk), 2 the same with three register sets in flight
                                        (measured equal, profiles/r4_q_head_loss_fwd.txt), 0 the 256-thread form */
-#define PIS_TUNE_WGRAD_T_DEPTH 39 /* wgrad_h3t_kernel's whole-K-step (EX) form: raw operands of K-step st + D in
-                                      flight while K-step st multiplies; 2 (default) or 3 (two / three register
-                                      sets; 3 measured neutral on the step, 21.93 vs 21.91 ms:
-                                      profiles/r4_f_ab.txt) */
-#define PIS_TUNE_DZ_VW 40 /* channels per thread of the F(3x3,4x4) dz passes (pis_conv3x3_bwd_prep's merged V + E
-                               pass, the weight gradient's E pass): 2 (default where 256 % (N / 2) == 0) or 4
-                               (the float4 form: 256 + 30 registers, one wave per SIMD). Measured neutral on the
-                               step (21.95 vs 22.02 ms, profiles/r4_g_ab.txt; the passes run at 5-5.9 TB/s
-                               isolated either way) */
-#define PIS_TUNE_GEMM_256 41 /* Winograd fwd / dgrad GEMM: 1 the fp16x3 256 x 256 kernel (8 waves, operands by
-                                  LDS-DMA into two 64-KB stages, per-wave scales, hi / lo split at fragment
-                                  read), 2 the same with 16-deep K-steps through a 4-stage ring (counted vmcnt,
-                                  one raw barrier per K-step), where T, N % 256 == 0 and the launch has >= 512
-                                  blocks; 0 (default) the 128 x 128 register-staged kernel. Both measured 25-40 %
-                                  slower per GEMM (profiles/r4_i_gemm_256.txt, r4_j_gemm_256_ring.txt) and 3 %
-                                  on the step: the read-time split doubles the split VALU and its scale chain
-                                  (fragment reads -> wave max -> split -> MFMA) serialises each K-step at two
-                                  waves per SIMD */
+#define PIS_TUNE_WGRAD_T_DEPTH 39 /* retired (round 5): a third register set in wgrad_h3t_kernel was neutral
+                                      (profiles/r4_f_ab.txt); two sets always; ignored */
+#define PIS_TUNE_DZ_VW 40 /* retired (round 5): the dz passes take 2 channels per thread wherever 256 % (N / 2) == 0
+                               (4 otherwise; the choice measured neutral, profiles/r4_g_ab.txt); ignored */
+#define PIS_TUNE_GEMM_256 41 /* retired (round 5): the 256 x 256 LDS-DMA fp16x3 GEMMs measured 25-40 % slower per GEMM
+                                  (profiles/r4_i_gemm_256.txt, r4_j_gemm_256_ring.txt); removed; ignored */
 #define PIS_TUNE_LAST_WGRAD_MAIN 42 /* host schedule (physics_informed_image_segmentation_amd/unet.py): 1 (default) the
                                          step's last weight gradient (enc1.conv0) on the main stream, idle after
                                          enc1.conv1's input gradient, beside the side stream's enc1.conv1 weight
@@ -196,13 +171,10 @@ int pis_version(void);
                                         round-3 strided tile order. HBM reads per launch 2218 -> 1674 MB on
                                         dec1.conv0 (1.38x -> 1.04x algorithmic; enc1.conv1 1.03x either way,
                                         profiles/r4_o_direct_wgrad_traffic.txt), time unchanged (r4_n) */
-#define PIS_TUNE_DIRECT_WGRAD_MAIN 44 /* host schedule (unet.py): 1 a direct layer's weight gradient on the main stream
-                                           right after its input gradient; 0 (default) on the weight-gradient
-                                           stream beside the main stream's next work (1 measured neutral:
-                                           22.18 vs 22.11 ms, profiles/r4_p_ab_direct_wgrad_main.txt) */
-#define PIS_TUNE_GEMM_PRIO 45 /* Winograd fwd / dgrad GEMM (128 x 128): 1 its MFMA phase at wave priority 1
-                                   (s_setprio) against the co-resident blocks' staging; 0 (default) none
-                                   (1 measured neutral: 22.10 vs 22.13 ms, profiles/r4_s_ab_gemm_prio.txt) */
+#define PIS_TUNE_DIRECT_WGRAD_MAIN 44 /* retired (round 5): direct weight gradients on the main stream were neutral
+                                           (profiles/r4_p_ab_direct_wgrad_main.txt); ignored */
+#define PIS_TUNE_GEMM_PRIO 45 /* retired (round 5): s_setprio in the Winograd GEMM was neutral
+                                   (profiles/r4_s_ab_gemm_prio.txt); ignored */
 #define PIS_TUNE_WINO_OUT_MPF 46 /* Winograd output transform of a masked input gradient: 1 (default) the tile's
                                       ReLU-mask rows loaded with its M values (one memory round trip per tile,
                                       151 VGPRs); 0 in the epilogue. Step 22.25 -> 22.04 ms on one box, 22.43 ->

@@ -180,17 +180,24 @@ def unet_forward(m: UNetRef, x: torch.Tensor, drop_scales=None, return_logits=Fa
     return (p, z) if return_logits else p
 
 
-def decision_flips(decisions, record, drop_scales=None) -> Dict[str, Tuple[int, float]]:
+def site_maxima(record) -> Dict[str, float]:
+    """max |value| per decision site of a record (the scale decision_flips / near_ties measure
+    margins in); a batch evaluated in chunks takes the max over its chunks' maxima."""
+    return {k: float(v.abs().max()) for k, v in record.items()}
+
+
+def decision_flips(decisions, record, drop_scales=None, site_scale=None) -> Dict[str, Tuple[int, float]]:
     """Where a run's ReLU / max-pool decisions differ from the ones this oracle makes
     on ``record`` (its own pre-activations): per site (count, worst margin), the
     margin being |pre-activation| for a ReLU and the gap between the window max and
-    the chosen element for a pool, relative to the site's max |value|. Channels a
+    the chosen element for a pool, relative to the site's max |value| (``site_scale``
+    overrides it: a chunk of a batch measured in the whole batch's scale). Channels a
     Dropout2d keep-scale zeroes (``drop_scales``) carry no decision and are skipped."""
     out = {}
     drop_scales = drop_scales or {}
     for name, dec in decisions.items():
         ref = record[name]
-        scale = ref.abs().max().clamp_min(1e-30)
+        scale = ref.abs().max().clamp_min(1e-30) if site_scale is None else max(site_scale[name], 1e-30)
         if name.startswith("pool"):
             B, C, H, W = ref.shape
             win = ref.reshape(B, C, H // 2, 2, W // 2, 2).permute(0, 1, 2, 4, 3, 5).reshape(B, C, H // 2, W // 2, 4)
@@ -208,15 +215,16 @@ def decision_flips(decisions, record, drop_scales=None) -> Dict[str, Tuple[int, 
     return out
 
 
-def near_ties(record, tol: float = 1e-5, drop_scales=None) -> Dict[str, int]:
+def near_ties(record, tol: float = 1e-5, drop_scales=None, site_scale=None) -> Dict[str, int]:
     """Per decision site, how many decisions of THIS oracle's record are near-ties: ReLU
-    pre-activations with |value| <= tol * the site's max |value|, and 2x2 pool windows whose two
-    largest elements are within tol * that max (channels a Dropout2d keep-scale zeroes carry no
-    decision). The decisions a run with fp32-class rounding may take differently are among them."""
+    pre-activations with |value| <= tol * the site's max |value| (or ``site_scale``'s), and 2x2
+    pool windows whose two largest elements are within tol * that max (channels a Dropout2d
+    keep-scale zeroes carry no decision). The decisions a run with fp32-class rounding may take
+    differently are among them."""
     out = {}
     drop_scales = drop_scales or {}
     for name, ref in record.items():
-        scale = ref.abs().max().clamp_min(1e-30)
+        scale = ref.abs().max().clamp_min(1e-30) if site_scale is None else max(site_scale[name], 1e-30)
         if name.startswith("pool"):
             B, C, H, W = ref.shape
             win = ref.reshape(B, C, H // 2, 2, W // 2, 2).permute(0, 1, 2, 4, 3, 5).reshape(B, C, H // 2, W // 2, 4)
@@ -229,6 +237,95 @@ def near_ties(record, tol: float = 1e-5, drop_scales=None) -> Dict[str, int]:
                 near &= (drop_scales[blk] != 0)[:, :, None, None]
         out[name] = int(near.sum())
     return out
+
+
+def whole_truth(ref: "UNetRef", img, mask, scales, decisions, loss_kws, log=None):
+    """The float64 truth of one training step per loss config on given ReLU / max-pool decisions:
+    (p64, z64, flips {site: (n, worst margin, near-ties)}, [(terms, {param: grad})] per config)."""
+    log = log or (lambda msg: None)
+    ref64 = UNetRef().double().train()
+    ref64.load_state_dict(ref.state_dict())
+    record = {}
+    log("float64 oracle forward")
+    p64, z64 = unet_forward(ref64, img.double(), {k: v.double() for k, v in scales.items()},
+                            decisions=decisions, record=record, return_logits=True)
+    near = near_ties(record, 1e-5, scales)
+    flips = {k: (n, m, near[k]) for k, (n, m) in decision_flips(decisions, record, scales).items()}
+    del record
+    truth = []
+    for kw in loss_kws:
+        log(f"float64 oracle backward {kw}")
+        ref64.zero_grad(set_to_none=True)
+        t64 = loss_terms(p64, mask.double(), **kw)
+        t64["loss"].backward(retain_graph=True)
+        truth.append(({k: float(torch.as_tensor(v).detach()) for k, v in t64.items()},
+                      {n: q.grad.detach().clone() for n, q in ref64.named_parameters()}))
+    return p64.detach(), z64.detach(), flips, truth
+
+
+def chunked_truth(ref: "UNetRef", img, mask, scales, decisions, loss_kws, chunk: int, log=None):
+    """whole_truth for a batch whose float64 graph does not fit host memory (C5: B = 8 at 1024^2
+    would need ~220 GB). The U-Net has no cross-sample coupling (no normalisation layer,
+    src/unet.py:19-67; Dropout2d masks injected per sample), and the loss couples the samples only
+    through its whole-batch sums (Dice's I, P, T and the 1/N of the means, src/loss.py:130-160). So:
+      1. per chunk of ``chunk`` images, the float64 forward on the decisions without a graph: the
+         probabilities, the logits and each decision site's max |value| over the batch;
+      2. the loss terms and dL/dp on the WHOLE batch's float64 probabilities (loss_terms);
+      3. per chunk again, the forward with a graph and one backward per loss config seeded with
+         that chunk's slice of dL/dp; parameter gradients summed over the chunks; the chunk's
+         decision flips / near-ties measured in the whole batch's site scales.
+    Equal to whole_truth up to float64 summation order (tests/test_oracle.py)."""
+    log = log or (lambda msg: None)
+    B = img.shape[0]
+    ref64 = UNetRef().double().train()
+    ref64.load_state_dict(ref.state_dict())
+    s64 = {k: v.double() for k, v in scales.items()}
+
+    def sl(d, c0):
+        return {k: v[c0:c0 + chunk] for k, v in d.items()}
+
+    ps, zs, smax = [], [], {}
+    with torch.no_grad():
+        for c0 in range(0, B, chunk):
+            log(f"float64 oracle forward, images {c0}..{min(B, c0 + chunk) - 1}")
+            rec = {}
+            p, z = unet_forward(ref64, img[c0:c0 + chunk].double(), sl(s64, c0), decisions=sl(decisions, c0),
+                                record=rec, return_logits=True)
+            for k, v in site_maxima(rec).items():
+                smax[k] = max(smax.get(k, 0.0), v)
+            ps.append(p)
+            zs.append(z)
+            del rec
+    p64, z64 = torch.cat(ps), torch.cat(zs)
+    del ps, zs
+    terms, seeds = [], []
+    for kw in loss_kws:
+        pl = p64.clone().requires_grad_(True)
+        t64 = loss_terms(pl, mask.double(), **kw)
+        t64["loss"].backward()
+        terms.append({k: float(torch.as_tensor(v).detach()) for k, v in t64.items()})
+        seeds.append(pl.grad.detach())
+    grads = [dict() for _ in loss_kws]
+    flips, near = {}, {}
+    for c0 in range(0, B, chunk):
+        log(f"float64 oracle forward + {len(loss_kws)} backward(s), images {c0}..{min(B, c0 + chunk) - 1}")
+        rec = {}
+        dec = sl(decisions, c0)
+        p = unet_forward(ref64, img[c0:c0 + chunk].double(), sl(s64, c0), decisions=dec, record=rec)
+        for k, v in near_ties(rec, 1e-5, sl(scales, c0), site_scale=smax).items():
+            near[k] = near.get(k, 0) + v
+        for k, (n, m) in decision_flips(dec, rec, sl(scales, c0), site_scale=smax).items():
+            n0, m0 = flips.get(k, (0, 0.0))
+            flips[k] = (n0 + n, max(m0, m))
+        del rec
+        for i in range(len(loss_kws)):
+            ref64.zero_grad(set_to_none=True)
+            p.backward(seeds[i][c0:c0 + chunk], retain_graph=i + 1 < len(loss_kws))
+            for n, q in ref64.named_parameters():
+                grads[i][n] = grads[i][n] + q.grad if n in grads[i] else q.grad.detach().clone()
+        del p
+    flips = {k: (n, m, near[k]) for k, (n, m) in flips.items()}
+    return p64, z64, flips, list(zip(terms, grads))
 
 
 def make_drop_scales(m: UNetRef, B: int, generator: torch.Generator) -> Dict[str, torch.Tensor]:

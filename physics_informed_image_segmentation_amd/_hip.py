@@ -19,7 +19,7 @@ LIB_PATH = os.path.join(_HERE, "_lib", "libpis.so")
 PIS_RELU, PIS_SCALE, PIS_MASK, PIS_ACCUMULATE, PIS_WINO_PREPARED, PIS_W_UNFLIPPED = 1, 2, 4, 8, 16, 32
 PIS_FILTER_READY = 64
 PIS_LOSS_ALL_TERMS, PIS_LOSS_CHAIN_SIGMOID, PIS_LOSS_NO_REACTION = 1, 2, 4
-PIS_TUNE_LAST_WGRAD_MAIN, PIS_TUNE_DIRECT_WGRAD_MAIN = 42, 44  # include/pis_capi.h: host schedule knobs (unet.py)
+PIS_TUNE_LAST_WGRAD_MAIN = 42  # include/pis_capi.h: host schedule knob (unet.py)
 LOSS_NTERMS = 8
 TERM_TOTAL, TERM_DICE, TERM_BCE, TERM_RD, TERM_PF, TERM_I, TERM_P, TERM_T = range(8)
 

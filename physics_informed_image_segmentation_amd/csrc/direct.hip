@@ -729,503 +729,11 @@ __global__ __launch_bounds__(256, 1) void conv3x3_wgrad_h3_kernel(DirectWArgs g)
   }
 }
 
-// =============================================================================================
-// The direct weight gradient on 2-row tiles walked DOWN a column strip (pis_tune key 34 = 1,
-// VERDICT r3 item 2). Same arithmetic, operand images and MFMA map as conv3x3_wgrad_h3_kernel
-// (rows n, columns (tap, c), 9 accumulator tiles per wave, transposed LDS reads, one power-of-two
-// scale per tile and operand), but a tile is 2 rows x 32 columns (64 pixels) with a 4 x 34 x halo:
-// the raw next-tile loads held in registers during the MFMAs drop from 88 to 56 VGPRs and the LDS
-// image from 85 to 51 KB, so a block fits in 256 registers per lane. Two blocks share a CU (one
-// stages while the other multiplies) — or, in the training step, one weight-gradient block sits
-// beside a main-stream block instead of locking the CU (the 4-row kernel's 497-register waves
-// filled every SIMD's register file). A block owns a contiguous run of tiles ordered row pair
-// fastest, so consecutive tiles are vertical neighbours: the two halo rows a tile shares with
-// the previous one were fetched by this CU a moment ago (L2 / L1 hits), and HBM sees x about once
-// (34/32 for the side columns). With several (n, c) pairs the pairs of one split are dealt to one
-// XCD back to back, so the x / dz tiles they share come from that XCD's L2.
-// =============================================================================================
-constexpr int SW_H = 2, SW_W = 32, SW_P = SW_H * SW_W, SH_H = SW_H + 2, SH_W = SW_W + 2, SH_P = SH_H * SH_W;
-constexpr int SZ_HALFS = SW_P * 64, SX_HALFS = SH_P * 64;  // per plane
-constexpr int SZ_ITEMS = SW_P * 8, SX_ITEMS = SH_P * 8;      // 8-channel groups (32 B of fp32)
-constexpr int SLDS_BYTES = 2 * (SZ_HALFS + SX_HALFS) * 2;
-constexpr int SBIAS_BYTES = 256 * 8 * 4;  // per-thread bias partials (8 channels), in LDS: 8 VGPRs fewer
-
-// RING (pis_tune key 34 = 2): the x halo rows live in a 4-slot LDS ring (image row h in slot h & 3),
-// so a tile whose predecessor was the tile above it loads, splits and stores only its 2 NEW halo
-// rows (68 of 136 pixels: the split VALU work and LDS stores of x halve, 1.06x instead of 2.1x the
-// x fetches); the first tile of a strip (rp == 0, or the block's first tile) loads all 4. The tile's
-// x scale covers the kept rows too (their max is the previous tile's new-row max); when h3_keep
-// re-chooses it, the kept rows' fp16 planes are re-expressed in LDS by the exact power-of-two ratio
-// (a rise cannot overflow: the new scale fits the tile max; a fall may flush lo bits below 2^-24 of
-// the scaled range, the block-floating-point floor every element already has).
-template <bool TW = false, bool RING = false>  // TW: timing twin (pis_tune key 2 != 0 only)
-__global__ __launch_bounds__(256, 2) void conv3x3_wgrad_strip_kernel(DirectWArgs g) {
-  constexpr int NW = 4, NT = 64 * NW, SZ_PER_T = SZ_ITEMS / NT, SX_PER_T = (SX_ITEMS + NT - 1) / NT;
-  constexpr int NTAP = 9;
-  __shared__ __attribute__((aligned(16))) char smem[SLDS_BYTES + SBIAS_BYTES + 64];
-  _Float16* sz = reinterpret_cast<_Float16*>(smem);                     // [plane][64][64]
-  _Float16* sx = reinterpret_cast<_Float16*>(smem + 2 * SZ_HALFS * 2);  // [plane][136][64] (RING: 4 slots x 34)
-  f32x4* sbias = reinterpret_cast<f32x4*>(smem + SLDS_BYTES);           // [256 threads][2] bias partials
-  float* red = reinterpret_cast<float*>(smem + SLDS_BYTES + SBIAS_BYTES);  // [2][NW] wave maxima
-  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wi = (wave >> 1) & 1, wj = wave & 1;  // n-half, c-half
-  const int ncb = g.Cin / 64, pairs = (g.Cout / 64) * ncb;
-  int pair, split;
-  if ((g.splits & 7) == 0) {  // the pairs of split 8 q + x: blocks of XCD x, back to back
-    const int bid = blockIdx.x, xcd = bid & 7, j = bid >> 3;
-    pair = j % pairs;
-    split = (j / pairs) * 8 + xcd;
-  } else {
-    pair = blockIdx.x % pairs;
-    split = blockIdx.x / pairs;
-  }
-  const int n0 = (pair / ncb) * 64, c0 = (pair % ncb) * 64;
-  const int nrp = g.H / SW_H, ncol = g.W / SW_W, per_img = nrp * ncol, ntile = g.B * per_img;
-  const int tps = (ntile + g.splits - 1) / g.splits;
-  const int t_begin = split * tps, t_end = min(ntile, t_begin + tps);
-  const bool do_bias = g.part_bias != nullptr && c0 == 0;
-  // RING: tile t loads all 4 halo rows when it starts a strip (or the block's range), else rows 2, 3
-  auto full_tile = [&](int t) { return !RING || t == t_begin || (t % nrp) == 0; };
-
-  f32x4 zr[SZ_PER_T][2], xr[SX_PER_T][2];
-  auto gload = [&](int t) __attribute__((always_inline)) {
-    if (TW && (g.dbg & 1) && t != t_begin) return;
-    const int b = t / per_img, rem = t - b * per_img, col = rem / nrp, rp = rem - col * nrp;
-    const int pr0 = SW_H * rp, pc0 = SW_W * col;
-    const size_t img = (size_t)b * g.H * g.W;
-    const bool full = full_tile(t);
-    const int nx = full ? SX_ITEMS : SX_ITEMS / 2, r_off = full ? 0 : 2;  // block-uniform
-#pragma unroll
-    for (int j = 0; j < SZ_PER_T; ++j) {
-      const int i = tid + NT * j, px = i >> 3, cg = i & 7;
-      const float* p = g.dz + (img + (size_t)(pr0 + (px >> 5)) * g.W + pc0 + (px & 31)) * g.ldz + n0 + 8 * cg;
-      zr[j][0] = *reinterpret_cast<const f32x4*>(p);
-      zr[j][1] = *reinterpret_cast<const f32x4*>(p + 4);
-    }
-#pragma unroll
-    for (int j = 0; j < SX_PER_T; ++j) {
-      const int i = tid + NT * j, q = i >> 3, cg = i & 7;
-      xr[j][0] = xr[j][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (i < nx) {  // wave-uniform bounds
-        const int qr = q / SH_W + r_off, qc = q - (q / SH_W) * SH_W, row = pr0 - 1 + qr, cl = pc0 - 1 + qc;
-        if (row >= 0 && row < g.H && cl >= 0 && cl < g.W) {
-          const float* p = g.x + (img + (size_t)row * g.W + cl) * g.ldx + c0 + 8 * cg;
-          xr[j][0] = *reinterpret_cast<const f32x4*>(p);
-          xr[j][1] = *reinterpret_cast<const f32x4*>(p + 4);
-        }
-      }
-    }
-  };
-
-  f32x16 acc[NTAP];
-#pragma unroll
-  for (int t = 0; t < NTAP; ++t)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
-  // bias partials, channels n0 + 8 (tid & 7) + e: each thread's own LDS slot (no barrier needed)
-  if (do_bias) sbias[2 * tid] = sbias[2 * tid + 1] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float sz_cur = 0.f, sx_cur = 0.f, sz_min = __builtin_inff(), sx_min = __builtin_inff();
-  float mx_prev = 0.f;  // RING: max |x| of the rows the previous tile loaded (this tile's kept rows)
-
-  // lane roles in the transposed reads: 16-lane group gq, its row q and 8-B column slot p
-  const int gq = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
-  const int kh = gq >> 1;  // k half (pixels 8 kh ..)
-  const int cgA = 4 * wi + 2 * (gq & 1) + (p >> 1), cgB = 4 * wj + 2 * (gq & 1) + (p >> 1);
-
-  if (t_begin < t_end) gload(t_begin);
-#pragma unroll 1
-  for (int t = t_begin; t < t_end; ++t) {
-    const int rp = (t - (t / per_img) * per_img) % nrp;
-    const bool full = full_tile(t);
-    // RING: halo row k (0..3, image row 2 rp - 1 + k) lives in slot (2 rp - 1 + k) & 3
-    const int slot0 = RING ? ((2 * rp + 3) & 3) : 0;
-    if (!(TW && (g.dbg & 2) && t != t_begin)) {
-      // 1. block maxima of the staged operands (+ the bias partials from the raw dz)
-      float mz = 0.f, mx = 0.f;
-#pragma unroll
-      for (int j = 0; j < SZ_PER_T; ++j)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) mz = fmaxf(mz, fmaxf(fabsf(zr[j][0][e]), fabsf(zr[j][1][e])));
-#pragma unroll
-      for (int j = 0; j < SX_PER_T; ++j)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) mx = fmaxf(mx, fmaxf(fabsf(xr[j][0][e]), fabsf(xr[j][1][e])));
-      mz = wave_max_nonneg(mz);
-      mx = wave_max_nonneg(mx);
-      if (lane == 0) {
-        red[wave] = mz;
-        red[NW + wave] = mx;
-      }
-      if (do_bias) {
-        f32x4 b0 = sbias[2 * tid], b1 = sbias[2 * tid + 1];
-#pragma unroll
-        for (int j = 0; j < SZ_PER_T; ++j) {
-          b0 += zr[j][0];
-          b1 += zr[j][1];
-        }
-        sbias[2 * tid] = b0;
-        sbias[2 * tid + 1] = b1;
-      }
-      __syncthreads();
-      // 2. this tile's scales; the partial sums re-expressed in them (one exact power-of-two factor
-      // at a time); the split planes into LDS
-      mz = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
-      mx = fmaxf(fmaxf(red[NW], red[NW + 1]), fmaxf(red[NW + 2], red[NW + 3]));
-      const float mx_loaded = mx;
-      if (RING && !full) mx = fmaxf(mx, mx_prev);  // the kept rows belong to this tile too
-      mx_prev = mx_loaded;
-      const float sz_new = h3_keep(sz_cur, mz, sz_min), sx_new = h3_keep(sx_cur, mx, sx_min);
-      if (sz_cur > 0.f && (sz_new != sz_cur || sx_new != sx_cur)) {
-        const float fz = sz_new / sz_cur, fx = sx_new / sx_cur;
-#pragma unroll
-        for (int k = 0; k < NTAP; ++k) acc[k] = (acc[k] * fz) * fx;
-      }
-      if (RING && !full && sx_cur > 0.f && sx_new != sx_cur) {
-        // the kept rows (halo rows 0, 1: slots slot0, slot0 + 1) re-expressed in the new scale
-        // (the ratio, up to 2^32, is not an fp16 number: the products are formed in fp32)
-        const float f = sx_new / sx_cur;
-        for (int e = tid; e < 2 * 2 * SH_W * 8; e += NT) {  // (plane, row, pixel, 8-half chunk)
-          const int pl = e / (2 * SH_W * 8), rem2 = e - pl * (2 * SH_W * 8);
-          const int rk = rem2 / (SH_W * 8), pc = rem2 - rk * (SH_W * 8);
-          const int hp = ((slot0 + rk) & 3) * SH_W + (pc >> 3);
-          _Float16* ptr = &sx[pl * SX_HALFS + wsw64(hp, pc & 7)];
-          f16x8 v = *reinterpret_cast<f16x8*>(ptr);
-#pragma unroll
-          for (int k = 0; k < 8; ++k) v[k] = (_Float16)((float)v[k] * f);
-          *reinterpret_cast<f16x8*>(ptr) = v;
-        }
-      }
-      sz_cur = sz_new;
-      sx_cur = sx_new;
-#pragma unroll
-      for (int j = 0; j < SZ_PER_T; ++j) {
-        const int i = tid + NT * j, px = i >> 3, cg = i & 7;
-        u32x2 h0, l0, h1, l1;
-        split2h_x4(zr[j][0] * sz_cur, h0, l0);
-        split2h_x4(zr[j][1] * sz_cur, h1, l1);
-        *reinterpret_cast<u32x4*>(&sz[wsw64(px, cg)]) = u32x4{h0[0], h0[1], h1[0], h1[1]};
-        *reinterpret_cast<u32x4*>(&sz[SZ_HALFS + wsw64(px, cg)]) = u32x4{l0[0], l0[1], l1[0], l1[1]};
-      }
-      const int nx = full ? SX_ITEMS : SX_ITEMS / 2, r_off = full ? 0 : 2;
-#pragma unroll
-      for (int j = 0; j < SX_PER_T; ++j) {
-        const int i = tid + NT * j, qq = i >> 3, cg = i & 7;
-        if (i < nx) {
-          const int qr = qq / SH_W, row = RING ? (((slot0 + qr + r_off) & 3) * SH_W + (qq - qr * SH_W)) : qq;
-          u32x2 h0, l0, h1, l1;
-          split2h_x4(xr[j][0] * sx_cur, h0, l0);
-          split2h_x4(xr[j][1] * sx_cur, h1, l1);
-          *reinterpret_cast<u32x4*>(&sx[wsw64(row, cg)]) = u32x4{h0[0], h0[1], h1[0], h1[1]};
-          *reinterpret_cast<u32x4*>(&sx[SX_HALFS + wsw64(row, cg)]) = u32x4{l0[0], l0[1], l1[0], l1[1]};
-        }
-      }
-      __syncthreads();
-    }
-    // 3. the next tile's loads fly during this tile's MFMAs
-    if (t + 1 < t_end) gload(t + 1);
-#pragma unroll 1
-    for (int ks = 0; ks < 4; ++ks) {  // 16-pixel K-steps: tile row ks >> 1, columns 16 (ks & 1) ..
-      const int rr = ks >> 1, cc0 = 16 * (ks & 1);
-      // A = dz^T (rows n, k pixels): pixels 16 ks + 8 kh + q (+ 4) of the tile, channels of cgA
-      f16x8 a[2];
-#pragma unroll
-      for (int pl = 0; pl < 2; ++pl) {
-        const _Float16* base = sz + pl * SZ_HALFS;
-        const int px = 16 * ks + 8 * kh + q;
-        const s16x4 lo4 = tr_read(base + wsw64(px, cgA) + 4 * (p & 1));
-        const s16x4 hi4 = tr_read(base + wsw64(px + 4, cgA) + 4 * (p & 1));
-        a[pl] = __builtin_bit_cast(f16x8, __builtin_shufflevector(lo4, hi4, 0, 1, 2, 3, 4, 5, 6, 7));
-      }
-#pragma unroll
-      for (int tap = 0; tap < NTAP; ++tap) {
-        const int r = tap / 3, s = tap % 3;
-        // B = x (k pixels, columns c): halo pixel (rr + r, cc0 + 8 kh + q (+ 4) + s), channels of cgB
-        f16x8 bb[2];
-        const int hrow = RING ? ((slot0 + rr + r) & 3) : (rr + r);
-        const int hp = hrow * SH_W + cc0 + 8 * kh + q + s;
-#pragma unroll
-        for (int pl = 0; pl < 2; ++pl) {
-          const _Float16* base = sx + pl * SX_HALFS;
-          const s16x4 lo4 = tr_read(base + wsw64(hp, cgB) + 4 * (p & 1));
-          const s16x4 hi4 = tr_read(base + wsw64(hp + 4, cgB) + 4 * (p & 1));
-          bb[pl] = __builtin_bit_cast(f16x8, __builtin_shufflevector(lo4, hi4, 0, 1, 2, 3, 4, 5, 6, 7));
-        }
-        acc[tap] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[1], bb[0], acc[tap], 0, 0, 0);
-        acc[tap] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[0], bb[1], acc[tap], 0, 0, 0);
-        acc[tap] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[0], bb[0], acc[tap], 0, 0, 0);
-      }
-    }
-    __syncthreads();
-  }
-
-  // partial sums / (sz sx), one factor at a time -> slab [split][Cout][9][Cin]: lane column
-  // c0 + 32 wj + (lane & 31), rows n0 + 32 wi + (reg & 3) + 8 (reg >> 2) + 4 (lane >> 5)
-  const float iz = sz_cur > 0.f ? 1.f / sz_cur : 0.f, ix = sx_cur > 0.f ? 1.f / sx_cur : 0.f;
-  float* slab = g.part + (size_t)split * g.Cout * 9 * g.Cin;
-  const int c = c0 + 32 * wj + (lane & 31);
-#pragma unroll
-  for (int tt = 0; tt < NTAP; ++tt) {
-#pragma unroll
-    for (int reg = 0; reg < 16; ++reg) {
-      const int n = n0 + 32 * wi + (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5);
-      slab[((size_t)n * 9 + tt) * g.Cin + c] = (acc[tt][reg] * iz) * ix;
-    }
-  }
-  if (do_bias) {  // fixed-order reduction over the 32 threads of each channel group
-    const float* rb = reinterpret_cast<const float*>(sbias);
-    __syncthreads();
-    if (tid < 64) {
-      const int cg = tid >> 3, e = tid & 7;
-      float sum = 0.f;
-      for (int k = 0; k < NT / 8; ++k) sum += rb[(8 * k + cg) * 8 + e];
-      g.part_bias[(size_t)split * g.Cout + n0 + tid] = sum;
-    }
-  }
-}
-
-// =============================================================================================
-// The same 2-row strip tiles software-pipelined for ONE block per CU (pis_tune key 34 = 3): with
-// one wave per SIMD nothing else hides the staging of a tile (wave maxima, split, LDS stores) or
-// its loads, which the timing twins put at 38 % of the 4-row kernel's time (profiles/r4_h). Two LDS
-// images (2 x 50 KB) and two register sets: while tile t is multiplied from image t & 1, tile t + 1
-// (its scale already known) is split into the other image from register set (t + 1) & 1 — in the
-// same basic block as the MFMAs, so its VALU and LDS stores issue in their gaps — and tile t + 2,
-// loaded a whole tile earlier, has its wave maxima published for the next iteration. One barrier
-// per tile. Same arithmetic per tile as the strip kernel (one power-of-two scale per tile and
-// operand, h3_keep, the accumulators re-expressed when a tile's scales change): bitwise equal to it.
-template <bool TW = false>
-__global__ __launch_bounds__(256, 1) void conv3x3_wgrad_db_kernel(DirectWArgs g) {
-  constexpr int NW = 4, NT = 64 * NW, SZ_PER_T = SZ_ITEMS / NT, SX_PER_T = (SX_ITEMS + NT - 1) / NT;
-  constexpr int NTAP = 9, IMG = SLDS_BYTES;
-  __shared__ __attribute__((aligned(16))) char smem[2 * SLDS_BYTES + SBIAS_BYTES + 64 + 2048];
-  f32x4* sbias = reinterpret_cast<f32x4*>(smem + 2 * SLDS_BYTES);
-  float* red = reinterpret_cast<float*>(smem + 2 * SLDS_BYTES + SBIAS_BYTES);  // [parity][z | x][NW]
-  _Float16* dummy = reinterpret_cast<_Float16*>(smem + 2 * SLDS_BYTES + SBIAS_BYTES + 64);  // 2 KB sink
-  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wi = (wave >> 1) & 1, wj = wave & 1;
-  const int ncb = g.Cin / 64, pairs = (g.Cout / 64) * ncb;
-  int pair, split;
-  if ((g.splits & 7) == 0) {
-    const int bid = blockIdx.x, xcd = bid & 7, j = bid >> 3;
-    pair = j % pairs;
-    split = (j / pairs) * 8 + xcd;
-  } else {
-    pair = blockIdx.x % pairs;
-    split = blockIdx.x / pairs;
-  }
-  const int n0 = (pair / ncb) * 64, c0 = (pair % ncb) * 64;
-  const int nrp = g.H / SW_H, ncol = g.W / SW_W, per_img = nrp * ncol, ntile = g.B * per_img;
-  const int tps = (ntile + g.splits - 1) / g.splits;
-  const int t_begin = split * tps, t_end = min(ntile, t_begin + tps);
-  const bool do_bias = g.part_bias != nullptr && c0 == 0;
-
-  f32x4 zr[2][SZ_PER_T][2], xr[2][SX_PER_T][2];  // [register set]
-  auto gload = [&](auto set_c, int t) __attribute__((always_inline)) {
-    constexpr int S = decltype(set_c)::value;
-    if (TW && (g.dbg & 1) && t > t_begin + 1) return;
-    const int b = t / per_img, rem = t - b * per_img, col = rem / nrp, rp = rem - col * nrp;
-    const int pr0 = SW_H * rp, pc0 = SW_W * col;
-    const size_t img = (size_t)b * g.H * g.W;
-#pragma unroll
-    for (int j = 0; j < SZ_PER_T; ++j) {
-      const int i = tid + NT * j, px = i >> 3, cg = i & 7;
-      const float* p = g.dz + (img + (size_t)(pr0 + (px >> 5)) * g.W + pc0 + (px & 31)) * g.ldz + n0 + 8 * cg;
-      zr[S][j][0] = *reinterpret_cast<const f32x4*>(p);
-      zr[S][j][1] = *reinterpret_cast<const f32x4*>(p + 4);
-    }
-#pragma unroll
-    for (int j = 0; j < SX_PER_T; ++j) {  // branch-free: clamped address, zero selected
-      const int i = tid + NT * j, q = i >> 3, cg = i & 7;
-      const int qr = q / SH_W, qc = q - qr * SH_W, row = pr0 - 1 + qr, cl = pc0 - 1 + qc;
-      const bool ok = i < SX_ITEMS && row >= 0 && row < g.H && cl >= 0 && cl < g.W;
-      const float* p = g.x + (img + (size_t)min(max(row, 0), g.H - 1) * g.W + min(max(cl, 0), g.W - 1)) * g.ldx + c0 + 8 * cg;
-      const f32x4 v0 = *reinterpret_cast<const f32x4*>(p), v1 = *reinterpret_cast<const f32x4*>(p + 4);
-      xr[S][j][0] = ok ? v0 : f32x4{0.f, 0.f, 0.f, 0.f};
-      xr[S][j][1] = ok ? v1 : f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-  };
-  // wave maxima of a loaded set into red[par] (+ the bias partials from its raw dz)
-  auto publish = [&](auto set_c, int par) __attribute__((always_inline)) {
-    constexpr int S = decltype(set_c)::value;
-    const float mz = wave_max_nonneg(absmax_x4(zr[S]));
-    const float mx = wave_max_nonneg(absmax_x4(xr[S]));
-    if (lane == 0) {
-      red[par * 2 * NW + wave] = mz;
-      red[par * 2 * NW + NW + wave] = mx;
-    }
-    if (do_bias) {
-      f32x4 b0 = sbias[2 * tid], b1 = sbias[2 * tid + 1];
-#pragma unroll
-      for (int j = 0; j < SZ_PER_T; ++j) {
-        b0 += zr[S][j][0];
-        b1 += zr[S][j][1];
-      }
-      sbias[2 * tid] = b0;
-      sbias[2 * tid + 1] = b1;
-    }
-  };
-  // the last staged tile's scales (h3_keep hysteresis, as the strip kernel's sz_cur / sx_cur)
-  float sz_st = 0.f, sx_st = 0.f, sz_min = __builtin_inff(), sx_min = __builtin_inff();
-  auto scales = [&](int par, float& sz, float& sx) __attribute__((always_inline)) {
-    const float* r = red + par * 2 * NW;
-    auto umax4 = [](const float* v) __attribute__((always_inline)) {  // v >= 0: bit-pattern max
-      return __uint_as_float(max(max(__float_as_uint(v[0]), __float_as_uint(v[1])),
-                                 max(__float_as_uint(v[2]), __float_as_uint(v[3]))));
-    };
-    sz = sz_st = h3_keep(sz_st, umax4(r), sz_min);
-    sx = sx_st = h3_keep(sx_st, umax4(r + NW), sx_min);
-  };
-  auto stage = [&](auto set_c, int im, float sz, float sx) __attribute__((always_inline)) {
-    constexpr int S = decltype(set_c)::value;
-    _Float16* dz_img = reinterpret_cast<_Float16*>(smem + im * IMG);
-    _Float16* x_img = reinterpret_cast<_Float16*>(smem + im * IMG + 2 * SZ_HALFS * 2);
-#pragma unroll
-    for (int j = 0; j < SZ_PER_T; ++j) {
-      const int i = tid + NT * j, px = i >> 3, cg = i & 7;
-      u32x2 h0, l0, h1, l1;
-      split2h_x4(zr[S][j][0] * sz, h0, l0);
-      split2h_x4(zr[S][j][1] * sz, h1, l1);
-      *reinterpret_cast<u32x4*>(&dz_img[wsw64(px, cg)]) = u32x4{h0[0], h0[1], h1[0], h1[1]};
-      *reinterpret_cast<u32x4*>(&dz_img[SZ_HALFS + wsw64(px, cg)]) = u32x4{l0[0], l0[1], l1[0], l1[1]};
-    }
-#pragma unroll
-    for (int j = 0; j < SX_PER_T; ++j) {  // items past the halo (wave 0, j = 4) store to a dummy slot
-      const int i = tid + NT * j, qq = i >> 3, cg = i & 7;
-      const bool ok = i < SX_ITEMS;
-      u32x2 h0, l0, h1, l1;
-      split2h_x4(xr[S][j][0] * sx, h0, l0);
-      split2h_x4(xr[S][j][1] * sx, h1, l1);
-      _Float16* dh = ok ? &x_img[wsw64(qq, cg)] : dummy + 16 * lane;
-      _Float16* dl = ok ? &x_img[SX_HALFS + wsw64(qq, cg)] : dummy + 16 * lane + 8;
-      *reinterpret_cast<u32x4*>(dh) = u32x4{h0[0], h0[1], h1[0], h1[1]};
-      *reinterpret_cast<u32x4*>(dl) = u32x4{l0[0], l0[1], l1[0], l1[1]};
-    }
-  };
-
-  f32x16 acc[NTAP];
-#pragma unroll
-  for (int t = 0; t < NTAP; ++t)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
-  if (do_bias) sbias[2 * tid] = sbias[2 * tid + 1] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int gq = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
-  const int kh = gq >> 1;
-  const int cgA = 4 * wi + 2 * (gq & 1) + (p >> 1), cgB = 4 * wj + 2 * (gq & 1) + (p >> 1);
-  auto mfma_tile = [&](int im) __attribute__((always_inline)) {
-    const _Float16* dz_img = reinterpret_cast<const _Float16*>(smem + im * IMG);
-    const _Float16* x_img = reinterpret_cast<const _Float16*>(smem + im * IMG + 2 * SZ_HALFS * 2);
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      const int rr = ks >> 1, cc0 = 16 * (ks & 1);
-      f16x8 a[2];
-#pragma unroll
-      for (int pl = 0; pl < 2; ++pl) {
-        const _Float16* base = dz_img + pl * SZ_HALFS;
-        const int px = 16 * ks + 8 * kh + q;
-        const s16x4 lo4 = tr_read(base + wsw64(px, cgA) + 4 * (p & 1));
-        const s16x4 hi4 = tr_read(base + wsw64(px + 4, cgA) + 4 * (p & 1));
-        a[pl] = __builtin_bit_cast(f16x8, __builtin_shufflevector(lo4, hi4, 0, 1, 2, 3, 4, 5, 6, 7));
-      }
-#pragma unroll
-      for (int tap = 0; tap < NTAP; ++tap) {
-        const int r = tap / 3, s = tap % 3;
-        f16x8 bb[2];
-        const int hp = (rr + r) * SH_W + cc0 + 8 * kh + q + s;
-#pragma unroll
-        for (int pl = 0; pl < 2; ++pl) {
-          const _Float16* base = x_img + pl * SX_HALFS;
-          const s16x4 lo4 = tr_read(base + wsw64(hp, cgB) + 4 * (p & 1));
-          const s16x4 hi4 = tr_read(base + wsw64(hp + 4, cgB) + 4 * (p & 1));
-          bb[pl] = __builtin_bit_cast(f16x8, __builtin_shufflevector(lo4, hi4, 0, 1, 2, 3, 4, 5, 6, 7));
-        }
-        acc[tap] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[1], bb[0], acc[tap], 0, 0, 0);
-        acc[tap] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[0], bb[1], acc[tap], 0, 0, 0);
-        acc[tap] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[0], bb[0], acc[tap], 0, 0, 0);
-      }
-    }
-  };
-
-  using I0 = std::integral_constant<int, 0>;
-  using I1 = std::integral_constant<int, 1>;
-  float uz = 0.f, ux = 0.f;  // the accumulators' units
-  float szn = 0.f, sxn = 0.f;  // the scales of the tile staged last (the next one to multiply)
-  const int nt = t_end - t_begin;
-  if (nt > 0) {
-    gload(I0{}, t_begin);
-    if (nt > 1) gload(I1{}, t_begin + 1);
-    publish(I0{}, 0);
-    __syncthreads();
-    scales(0, szn, sxn);
-    stage(I0{}, 0, szn, sxn);
-    if (nt > 1) publish(I1{}, 1);
-    __syncthreads();
-  }
-  // tile k: image k & 1; its successor's raw data in set (k + 1) & 1 with maxima in red[(k + 1) & 1];
-  // set k & 1 is free and takes tile k + 2
-  auto iter = [&](int k, auto cur_c) __attribute__((always_inline)) {
-    constexpr int CUR = decltype(cur_c)::value, NXT = CUR ^ 1;
-    using ICUR = std::integral_constant<int, CUR>;
-    using INXT = std::integral_constant<int, NXT>;
-    if (uz != szn || ux != sxn) {  // this tile's scales differ from the partial sums' units
-      if (uz != 0.f) {
-        const float fz = szn / uz, fx = sxn / ux;
-#pragma unroll
-        for (int tp = 0; tp < NTAP; ++tp) acc[tp] = (acc[tp] * fz) * fx;
-      }
-      uz = szn;
-      ux = sxn;
-    }
-    const bool has1 = k + 1 < nt, has2 = k + 2 < nt;
-    float sz1 = 0.f, sx1 = 0.f;
-    if (has1) scales(NXT, sz1, sx1);
-    gload(ICUR{}, t_begin + min(k + 2, nt - 1));  // unconditional (a valid tile past the end): no branch
-    mfma_tile(CUR);
-    // unconditional (branch-free, so it shares the MFMAs' basic block): on the last tile it writes
-    // stale registers into the image nobody reads again
-    if (!(TW && (g.dbg & 2))) stage(INXT{}, NXT, sz1, sx1);
-    if (has2) publish(ICUR{}, CUR);
-    __syncthreads();
-    szn = sz1;
-    sxn = sx1;
-  };
-#pragma unroll 1
-  for (int k = 0; k < nt; k += 2) {
-    iter(k, I0{});
-    if (k + 1 < nt) iter(k + 1, I1{});
-  }
-
-  const float iz = uz > 0.f ? 1.f / uz : 0.f, ix = ux > 0.f ? 1.f / ux : 0.f;
-  float* slab = g.part + (size_t)split * g.Cout * 9 * g.Cin;
-  const int c = c0 + 32 * wj + (lane & 31);
-#pragma unroll
-  for (int tt = 0; tt < NTAP; ++tt) {
-#pragma unroll
-    for (int reg = 0; reg < 16; ++reg) {
-      const int n = n0 + 32 * wi + (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5);
-      slab[((size_t)n * 9 + tt) * g.Cin + c] = (acc[tt][reg] * iz) * ix;
-    }
-  }
-  if (do_bias) {
-    const float* rb = reinterpret_cast<const float*>(sbias);
-    __syncthreads();
-    if (tid < 64) {
-      const int cg = tid >> 3, e = tid & 7;
-      float sum = 0.f;
-      for (int k = 0; k < NT / 8; ++k) sum += rb[(8 * k + cg) * 8 + e];
-      g.part_bias[(size_t)split * g.Cout + n0 + tid] = sum;
-    }
-  }
-}
-
-static bool direct_w_strip() { return tune_get(PIS_TUNE_DIRECT_WSTRIP) != 0 && tune_get(PIS_TUNE_DIRECT_WSTRIP) != 3; }
-static bool direct_w_db() { return tune_get(PIS_TUNE_DIRECT_WSTRIP) == 3; }
 
 
 bool direct_w_wanted(int B, int H, int W, int Cin, int Cout, int ldx, int ldz) {
   if (!(B > 0 && H % WT_H == 0 && W % WT_W == 0 && Cin % 64 == 0 && Cout % 64 == 0 && ldz % 4 == 0 && ldx % 4 == 0))
     return false;
-  // key 37: every layer the strip kernel covers, whatever its forward / input gradient run
-  if (tune_get(PIS_TUNE_DIRECT_WGRAD_ALL) != 0 && direct_w_strip()) return true;
   return direct_h3_wanted(H, W, Cin, Cout, ldx);
 }
 
@@ -1235,21 +743,8 @@ static int direct_w_splits(int B, int H, int W, int Cin, int Cout) {
   return std::max(1, std::min(ntile, 256 / std::max(1, std::min(pairs, 256))));
 }
 
-// the strip kernel's split count: ~PIS_TUNE_DIRECT_WBLOCKS workgroups over the (n, c) pairs, a
-// multiple of 8 (the pairs of one split on one XCD) where there are enough tiles
-// (cap: the double-buffered kernel, one block per CU, takes at most 256 workgroups)
-static int direct_ws_splits(int B, int H, int W, int Cin, int Cout, int cap = 1 << 30) {
-  const int pairs = (Cout / 64) * (Cin / 64);
-  const int ntile = B * (H / SW_H) * (W / SW_W);
-  const int target = std::max(8, std::min(cap, tune_get(PIS_TUNE_DIRECT_WBLOCKS)));
-  int sp = std::max(1, target / std::max(1, pairs));
-  if (sp >= 8) sp &= ~7;
-  return std::max(1, std::min(sp, ntile));
-}
-
 size_t direct_w_ws_bytes(int B, int H, int W, int Cin, int Cout) {
-  // room for either kernel (the knobs may change between the size query and the launch)
-  const int sp = std::max(direct_w_splits(B, H, W, Cin, Cout), direct_ws_splits(B, H, W, Cin, Cout));
+  const int sp = direct_w_splits(B, H, W, Cin, Cout);
   return (size_t)sp * Cout * 9 * Cin * sizeof(float) + (size_t)sp * Cout * sizeof(float) + 512;
 }
 
@@ -1261,9 +756,7 @@ int launch_direct_wgrad(const float* x, int ldx, const float* dz, int ldz, float
   DirectWArgs g{};
   g.x = x; g.ldx = ldx; g.dz = dz; g.ldz = ldz;
   g.B = B; g.H = H; g.W = W; g.Cin = Cin; g.Cout = Cout;
-  const bool strip = direct_w_strip(), dbuf = direct_w_db();
-  g.splits = dbuf ? direct_ws_splits(B, H, W, Cin, Cout, 256)
-             : strip ? direct_ws_splits(B, H, W, Cin, Cout) : direct_w_splits(B, H, W, Cin, Cout);
+  g.splits = direct_w_splits(B, H, W, Cin, Cout);
   g.dbg = tune_get(PIS_TUNE_DEBUG_NOLOAD);
   g.vwalk = tune_get(PIS_TUNE_DIRECT_W_VWALK);
   g.part = reinterpret_cast<float*>(ws);
@@ -1272,20 +765,7 @@ int launch_direct_wgrad(const float* x, int ldx, const float* dz, int ldz, float
   const double flop = 2.0 * 9 * (double)B * H * W * Cin * Cout;
   const dim3 grid(g.splits * pairs);
   launch_hook("direct_wgrad_h3", 0, s, flop);
-  const bool ring = tune_get(PIS_TUNE_DIRECT_WSTRIP) == 2;
-  if (dbuf && g.dbg)
-    hipLaunchKernelGGL((conv3x3_wgrad_db_kernel<true>), grid, dim3(256), 0, s, g);
-  else if (dbuf)
-    hipLaunchKernelGGL((conv3x3_wgrad_db_kernel<false>), grid, dim3(256), 0, s, g);
-  else if (strip && g.dbg && ring)
-    hipLaunchKernelGGL((conv3x3_wgrad_strip_kernel<true, true>), grid, dim3(256), 0, s, g);
-  else if (strip && g.dbg)
-    hipLaunchKernelGGL((conv3x3_wgrad_strip_kernel<true, false>), grid, dim3(256), 0, s, g);
-  else if (strip && ring)
-    hipLaunchKernelGGL((conv3x3_wgrad_strip_kernel<false, true>), grid, dim3(256), 0, s, g);
-  else if (strip)
-    hipLaunchKernelGGL((conv3x3_wgrad_strip_kernel<false, false>), grid, dim3(256), 0, s, g);
-  else if (g.dbg)
+  if (g.dbg)
     hipLaunchKernelGGL((conv3x3_wgrad_h3_kernel<true>), grid, dim3(256), 0, s, g);
   else
     hipLaunchKernelGGL((conv3x3_wgrad_h3_kernel<false>), grid, dim3(256), 0, s, g);

@@ -836,10 +836,11 @@ __global__ __launch_bounds__(NT) void head_loss_fwd_kernel(HeadLossFwdArgs h) {
   constexpr float kLn2 = 0.69314718055994531f, kClamp2 = -144.26950408889634f;  // -100 / ln 2
   float s_it = 0.f, s_p = 0.f, s_t = 0.f, s_bce2 = 0.f, s_rd = 0.f, s_g2 = 0.f, s_q2 = 0.f;
   int c_i = 0, c_p = 0, c_t = 0;
-  if (ry < RY && q < W4) {
+  // W4 > NT (W > 4 NT, e.g. W = 1280 at 256 threads): a thread walks every TX-th item of its rows
+  for (int xq = q; ry < RY && xq < W4; xq += TX) {
     for (int r = 1 + ry; r <= nr; r += RY) {
-      const f32x4 tv = *reinterpret_cast<const f32x4*>(tt + (size_t)(y0 - 1 + r) * W + 4 * q);
-      const float* sc = su + r * SW + 4 + 4 * q;
+      const f32x4 tv = *reinterpret_cast<const f32x4*>(tt + (size_t)(y0 - 1 + r) * W + 4 * xq);
+      const float* sc = su + r * SW + 4 + 4 * xq;
       const f32x4 pv = *reinterpret_cast<const f32x4*>(sc);
       f32x4 uv = pv, dv = pv;
       float lft = 0.f, rgt = 0.f;
@@ -1264,10 +1265,15 @@ extern "C" size_t pis_head_loss_fwd_ws(int B, int H, int W) {
   return 16 + nblk * (6 * sizeof(float) + 3 * sizeof(int)) + 256;
 }
 
+// the staged u rows, (R + 2) x (W + 8) floats, must fit one workgroup's LDS (160 KB on gfx950); a
+// shape that does not (e.g. B = 128 at 1024^2: R = 64, 272 KB) takes pis_head_fwd + pis_loss_fwd
+static constexpr size_t kHeadLossFwdMaxLds = 160 * 1024;
+static size_t head_loss_fwd_smem(int R, int W) { return (size_t)(R + 2) * (W + 8) * sizeof(float); }
+
 extern "C" int pis_head_loss_fwd_ok(int B, int H, int W, int C) {
   const int R = head_loss_fwd_rows(B, H, W);
   return C == 64 && B > 0 && H >= 2 && W >= 8 && W <= 2048 && head_loss_fwd_pp(W) > 0 &&
-         (int64_t)B * ((H + R - 1) / R) <= LOSS_MAX_BLOCKS;
+         (int64_t)B * ((H + R - 1) / R) <= LOSS_MAX_BLOCKS && head_loss_fwd_smem(R, W) <= kHeadLossFwdMaxLds;
 }
 
 extern "C" int pis_head_loss_fwd(const float* x, int ldx, const float* w, const float* bias, const float* t,
@@ -1276,8 +1282,8 @@ extern "C" int pis_head_loss_fwd(const float* x, int ldx, const float* w, const 
                                  pis_stream_t stream) {
   PIS_CHECK_ARG(x && w && bias && t && z && u && prm && out_terms, "pis_head_loss_fwd: bad arguments");
   PIS_CHECK_ARG(pis_head_loss_fwd_ok(B, H, W, C),
-                "pis_head_loss_fwd: needs C == 64, W % 64 == 0, W <= 2048, H >= 2 and at most 2048 row bands "
-                "(use pis_head_fwd + pis_loss_fwd)");
+                "pis_head_loss_fwd: needs C == 64, W % 64 == 0, W <= 2048, H >= 2, at most 2048 row bands "
+                "and staged rows within 160 KB of LDS (use pis_head_fwd + pis_loss_fwd)");
   PIS_CHECK_ARG(ldx % 4 == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)t & 15) == 0 && ((uintptr_t)w & 15) == 0,
                 "pis_head_loss_fwd: x, w, t must be 16-byte aligned with ldx % 4 == 0");
   PIS_CHECK_ARG(ws && ws_bytes >= pis_head_loss_fwd_ws(B, H, W), "pis_head_loss_fwd: workspace too small");
@@ -1301,7 +1307,7 @@ extern "C" int pis_head_loss_fwd(const float* x, int ldx, const float* w, const 
   const int pp = head_loss_fwd_pp(W);
   const bool wide = head_loss_fwd_wide(W);
   const bool wide3 = wide && tune_get(PIS_TUNE_HEAD_LOSS_WIDE) == 2;
-  const size_t smem = (size_t)(h.R + 2) * (W + 8) * sizeof(float);
+  const size_t smem = head_loss_fwd_smem(h.R, W);
   const dim3 grid(bands, B);
   hipStream_t s = (hipStream_t)stream;
   const double nbytes = (double)B * H * W * (4.0 * C + 12.0);

@@ -1225,8 +1225,6 @@ static int run_wgrad(const WgradArgs& base, const WgradPlan& pl, hipStream_t s, 
         ((uintptr_t)a.a & 15) == 0 && ((uintptr_t)a.b & 15) == 0) {
       if (a.dbg)
         hipLaunchKernelGGL((wgrad_h3t_kernel<false, 2, true>), grid, dim3(256), 0, s, a);
-      else if (h3t_exact(a) && tune_get(PIS_TUNE_WGRAD_T_DEPTH) == 3)
-        hipLaunchKernelGGL((wgrad_h3t_kernel<false, 3, false, true>), grid, dim3(256), 0, s, a);
       else if (h3t_exact(a))
         hipLaunchKernelGGL((wgrad_h3t_kernel<false, 2, false, true>), grid, dim3(256), 0, s, a);
       else
@@ -1581,10 +1579,13 @@ extern "C" int pis_conv3x3_wgrad(const float* x, int ldx, const float* dz, int l
   // the direct kernel reads x and dz as float4s: 16-B aligned base pointers (a channel slice at an
   // offset that is not a multiple of 4 floats falls through to the Winograd / halo kernels)
   if (direct_w_wanted(B, H, W, Cin, Cout, ldx, ldz)) {
-    if (((uintptr_t)x & 15) == 0 && ((uintptr_t)dz & 15) == 0)
+    // (a workspace smaller than the direct kernel's slabs falls through to the kernels below, as
+    // does a misaligned operand)
+    if (((uintptr_t)x & 15) == 0 && ((uintptr_t)dz & 15) == 0 && ws_bytes >= direct_w_ws_bytes(B, H, W, Cin, Cout))
       return launch_direct_wgrad(x, ldx, dz, ldz, dw_krsc, db, B, H, W, Cin, Cout, acc, ws, ws_bytes, s);
     PIS_CHECK_ARG(ws_bytes >= wgrad_ws_nodirect(B, H, W, Cin, Cout),
-                  "pis_conv3x3_wgrad: x / dz not 16-byte aligned; the non-direct fallback needs a larger "
+                  "pis_conv3x3_wgrad: x / dz not 16-byte aligned or workspace below the direct kernel's; "
+                  "the non-direct fallback needs a larger "
                   "workspace than pis_conv3x3_wgrad_ws reports for this (direct) layer");
   }
   const WinoWgradPlan wp = wino_wgrad_plan(B, H, W, Cin, Cout);

@@ -1248,8 +1248,7 @@ __global__ __launch_bounds__(256, OCC) void gemm_nt_x6_bk32_kernel(const float* 
 // first two K-steps, 2 no staging after the first (profiles/r3_q22_gemm_twins.txt: staging is 24-44 %
 // of the time, the loads 0-17 %). (Two LDS stages + two register sets at two blocks per CU — one
 // barrier per K-step, loads a K-step further ahead — ran 10-30 % slower: profiles/r3_q23_gemm_db.txt.)
-// PRIO (pis_tune key 45): the MFMA phase at wave priority 1 (s_setprio), the staging at 0
-template <int BM, int BN, int OCC = 3, bool SC = true, int DBG = 0, bool PRIO = false>
+template <int BM, int BN, int OCC = 3, bool SC = true, int DBG = 0>
 __global__ __launch_bounds__(256, OCC) void gemm_nt_h3_bk32_kernel(const float* __restrict__ A,
                                                                 const float* __restrict__ Bm, float* __restrict__ Cm,
                                                                 int M, int N, int K, int64_t bsA, int64_t bsB,
@@ -1373,7 +1372,6 @@ __global__ __launch_bounds__(256, OCC) void gemm_nt_h3_bk32_kernel(const float* 
         ub = nb;
       }
     }
-    if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       f16x8 af[2][TM], bf[2][TN];
@@ -1395,7 +1393,6 @@ __global__ __launch_bounds__(256, OCC) void gemm_nt_h3_bk32_kernel(const float* 
           acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[0][a], bf[0][b], acc[a][b], 0, 0, 0);
         }
     }
-    if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
     if (kt + 1 < KT) {
       __syncthreads();
       if (DBG != 2) lstore();
@@ -1415,274 +1412,6 @@ __global__ __launch_bounds__(256, OCC) void gemm_nt_h3_bk32_kernel(const float* 
       for (int r = 0; r < 16; ++r) {
         const int ml = wm * (BM / 2) + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh, m = m0 + ml;
         if (m < M) Cm[(size_t)m * N + n] = acc[a][b][r] * inv[r >> 2];
-      }
-    }
-}
-
-// ---- fp16x3 on a 256 x 256 tile, operands by LDS-DMA, split at fragment read (pis_tune key 41) ----
-// The 128 x 128 kernel above stages through registers (ds_write of the split planes between two
-// barriers: 30-37 % of its time, profiles/r4_h twins) and re-reads every operand row N/128 times
-// through L2. Here one block of 8 waves (2 along M x 4 along N, 128 x 64 outputs each) owns a
-// 256 x 256 tile; each 32-deep K-tile of both operands arrives as raw fp32 by global_load_lds_dwordx4
-// (64 KB, no VGPRs, no ds_write) into one of two LDS stages while the other is multiplied. A wave
-// reads its fragments as fp32 (two ds_read_b128 per 8-K fragment), takes ITS OWN power-of-two scale
-// per 16-deep K-step from its fragments' max (h3_keep, wave-uniform, so its accumulators share one
-// unit), splits them into hi / lo fp16 in registers and runs the three products. LDS image: one
-// operand K-tile is [256 rows][8 chunks of 4 fp32]; chunk c of row r sits at physical chunk
-// c ^ ((r >> 1) & 7), which puts each ds_read_b128 lane group on 16 distinct 16-B slots of the
-// 256-B bank row (the LDS-DMA writes stay lane-linear: the permutation is applied to the SOURCE
-// address of each lane). M, N % 256 == 0, K % 32 == 0.
-constexpr int G2_BK = 32;
-constexpr int G2_TILE_BYTES = 256 * G2_BK * 4;  // one operand's K-tile: 32 KB
-constexpr int G2_STAGE_BYTES = 2 * G2_TILE_BYTES;
-
-__device__ __forceinline__ int g2_off(int row, int chunk) { return row * 128 + 16 * (chunk ^ ((row >> 1) & 7)); }
-
-__global__ __launch_bounds__(512, 1) void gemm_nt_h3_256_kernel(const float* __restrict__ A,
-                                                               const float* __restrict__ Bm, float* __restrict__ Cm,
-                                                               int M, int N, int K, int64_t bsA, int64_t bsB,
-                                                               int64_t bsC) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * G2_STAGE_BYTES];  // [stage][A | B] 128 KB
-  const Remap2 rm = xcd_remap2();
-  A += rm.batch * bsA;
-  Bm += rm.batch * bsB;
-  Cm += rm.batch * bsC;
-  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave & 1, wn = wave >> 1, li = lane & 31, lh = lane >> 5;
-  const int ntn = N / 256;
-  const int m0 = (rm.bid / ntn) * 256, n0 = (rm.bid % ntn) * 256;
-  const int KT = K / G2_BK;
-  // LDS-DMA: wave w fills 1-KB pieces 4 w .. 4 w + 3 of each operand (8 rows each); lane l of a
-  // piece lands at byte 16 l = row l / 8, physical chunk l % 8, and loads the logical chunk there
-  const int prow = lane >> 3, pch = lane & 7;
-  auto issue = [&](int kt, int st) __attribute__((always_inline)) {
-    char* base = smem + st * G2_STAGE_BYTES;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int p = 4 * wave + i, row = 8 * p + prow, c = pch ^ ((row >> 1) & 7);
-      const float* ga = A + (size_t)(m0 + row) * K + kt * G2_BK + 4 * c;
-      const float* gb = Bm + (size_t)(n0 + row) * K + kt * G2_BK + 4 * c;
-      __builtin_amdgcn_global_load_lds(ga, (__attribute__((address_space(3))) void*)(base + 1024 * p), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds(gb, (__attribute__((address_space(3))) void*)(base + G2_TILE_BYTES + 1024 * p),
-                                       16, 0, 0);
-    }
-  };
-
-  f32x16 acc[4][2];
-#pragma unroll
-  for (int a = 0; a < 4; ++a)
-#pragma unroll
-    for (int b = 0; b < 2; ++b)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
-  float ua = 0.f, ub = 0.f;  // the accumulators' units (two factors; 0: none yet)
-  float sa_cur = 0.f, sb_cur = 0.f, sa_min = __builtin_inff(), sb_min = __builtin_inff();
-
-  issue(0, 0);
-  for (int kt = 0; kt < KT; ++kt) {
-    __syncthreads();  // K-tile kt has landed (vmcnt(0)); every wave is done with the other stage
-    if (kt + 1 < KT) issue(kt + 1, (kt + 1) & 1);
-    const char* sA = smem + (kt & 1) * G2_STAGE_BYTES;
-    const char* sB = sA + G2_TILE_BYTES;
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const int c0 = 4 * ks + 2 * lh;  // this lane's 8 K values: logical chunks c0, c0 + 1
-      f32x4 ar[4][2], br[2][2];
-#pragma unroll
-      for (int a = 0; a < 4; ++a) {
-        const int r = wm * 128 + a * 32 + li;
-        ar[a][0] = *reinterpret_cast<const f32x4*>(sA + g2_off(r, c0));
-        ar[a][1] = *reinterpret_cast<const f32x4*>(sA + g2_off(r, c0 + 1));
-      }
-#pragma unroll
-      for (int b = 0; b < 2; ++b) {
-        const int r = wn * 64 + b * 32 + li;
-        br[b][0] = *reinterpret_cast<const f32x4*>(sB + g2_off(r, c0));
-        br[b][1] = *reinterpret_cast<const f32x4*>(sB + g2_off(r, c0 + 1));
-      }
-      const float sa = sa_cur = h3_keep(sa_cur, wave_max_nonneg(absmax_x4(ar)), sa_min);
-      const float sb = sb_cur = h3_keep(sb_cur, wave_max_nonneg(absmax_x4(br)), sb_min);
-      if (sa != ua || sb != ub) {  // wave-uniform: re-express the partial sums in the new units
-        if (ua != 0.f) {
-          const float fa = sa / ua, fb = sb / ub;
-#pragma unroll
-          for (int a = 0; a < 4; ++a)
-#pragma unroll
-            for (int b = 0; b < 2; ++b) acc[a][b] = (acc[a][b] * fa) * fb;
-        }
-        ua = sa;
-        ub = sb;
-      }
-      f16x8 af[2][4], bf[2][2];  // [hi | lo]
-#pragma unroll
-      for (int a = 0; a < 4; ++a) {
-        u32x2 h0, l0, h1, l1;
-        split2h_x4(ar[a][0] * sa, h0, l0);
-        split2h_x4(ar[a][1] * sa, h1, l1);
-        af[0][a] = __builtin_bit_cast(f16x8, u32x4{h0[0], h0[1], h1[0], h1[1]});
-        af[1][a] = __builtin_bit_cast(f16x8, u32x4{l0[0], l0[1], l1[0], l1[1]});
-      }
-#pragma unroll
-      for (int b = 0; b < 2; ++b) {
-        u32x2 h0, l0, h1, l1;
-        split2h_x4(br[b][0] * sb, h0, l0);
-        split2h_x4(br[b][1] * sb, h1, l1);
-        bf[0][b] = __builtin_bit_cast(f16x8, u32x4{h0[0], h0[1], h1[0], h1[1]});
-        bf[1][b] = __builtin_bit_cast(f16x8, u32x4{l0[0], l0[1], l1[0], l1[1]});
-      }
-#pragma unroll
-      for (int a = 0; a < 4; ++a)
-#pragma unroll
-        for (int b = 0; b < 2; ++b) {
-          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[1][a], bf[0][b], acc[a][b], 0, 0, 0);
-          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[0][a], bf[1][b], acc[a][b], 0, 0, 0);
-          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[0][a], bf[0][b], acc[a][b], 0, 0, 0);
-        }
-    }
-  }
-  const float ia = ua != 0.f ? 1.f / ua : 0.f, ib = ub != 0.f ? 1.f / ub : 0.f;
-#pragma unroll
-  for (int a = 0; a < 4; ++a)
-#pragma unroll
-    for (int b = 0; b < 2; ++b) {
-      const int n = n0 + wn * 64 + b * 32 + li;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = m0 + wm * 128 + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-        Cm[(size_t)m * N + n] = (acc[a][b][r] * ia) * ib;
-      }
-    }
-}
-
-// The same tile and split with 16-deep K-steps through a 4-stage LDS ring (32 KB per stage): the
-// LDS-DMA of K-step k + 3 is issued right after the barrier of K-step k, each wave waits only for
-// ITS oldest DMA group (counted `s_waitcnt vmcnt(8)`: two younger groups of 4 stay in flight across
-// the raw barrier, cdna_hip_programming.md 'Pipelining across barriers'), and the one barrier per
-// K-step both publishes K-step k and retires every wave's reads of K-step k - 1, whose stage the
-// new DMA overwrites. LDS image per operand and stage: [256 rows][4 chunks of 4 fp32], chunk c of
-// row r at c ^ ((r >> 2) & 3) (16 distinct 16-B slots per ds_read_b128 lane group).
-constexpr int G3_BK = 16, G3_NS = 4;
-constexpr int G3_TILE_BYTES = 256 * G3_BK * 4;  // 16 KB
-constexpr int G3_STAGE_BYTES = 2 * G3_TILE_BYTES;
-
-__device__ __forceinline__ int g3_off(int row, int chunk) { return row * 64 + 16 * (chunk ^ ((row >> 2) & 3)); }
-
-__global__ __launch_bounds__(512, 1) void gemm_nt_h3_256r_kernel(const float* __restrict__ A,
-                                                                const float* __restrict__ Bm, float* __restrict__ Cm,
-                                                                int M, int N, int K, int64_t bsA, int64_t bsB,
-                                                                int64_t bsC) {
-  __shared__ __attribute__((aligned(16))) char smem[G3_NS * G3_STAGE_BYTES];  // 128 KB
-  const Remap2 rm = xcd_remap2();
-  A += rm.batch * bsA;
-  Bm += rm.batch * bsB;
-  Cm += rm.batch * bsC;
-  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave & 1, wn = wave >> 1, li = lane & 31, lh = lane >> 5;
-  const int ntn = N / 256;
-  const int m0 = (rm.bid / ntn) * 256, n0 = (rm.bid % ntn) * 256;
-  const int KS = K / G3_BK;
-  // a 1-KB LDS-DMA piece = 16 rows x 64 B; wave w fills pieces 2 w, 2 w + 1 of each operand;
-  // lane l lands at row l / 4, physical chunk l % 4
-  const int prow = lane >> 2, pch = lane & 3;
-  auto issue = [&](int k) __attribute__((always_inline)) {
-    char* base = smem + (k % G3_NS) * G3_STAGE_BYTES;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int p = 2 * wave + i, row = 16 * p + prow, c = pch ^ ((row >> 2) & 3);
-      const float* ga = A + (size_t)(m0 + row) * K + k * G3_BK + 4 * c;
-      const float* gb = Bm + (size_t)(n0 + row) * K + k * G3_BK + 4 * c;
-      __builtin_amdgcn_global_load_lds(ga, (__attribute__((address_space(3))) void*)(base + 1024 * p), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds(gb, (__attribute__((address_space(3))) void*)(base + G3_TILE_BYTES + 1024 * p),
-                                       16, 0, 0);
-    }
-  };
-  f32x16 acc[4][2];
-#pragma unroll
-  for (int a = 0; a < 4; ++a)
-#pragma unroll
-    for (int b = 0; b < 2; ++b)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
-  float ua = 0.f, ub = 0.f;
-  float sa_cur = 0.f, sb_cur = 0.f, sa_min = __builtin_inff(), sb_min = __builtin_inff();
-
-  // prologue: K-steps 0 .. 2 in flight (4 DMA per wave each)
-#pragma unroll
-  for (int k = 0; k < G3_NS - 1; ++k)
-    if (k < KS) issue(k);
-  for (int k = 0; k < KS; ++k) {
-    // this wave's DMA groups of K-steps k + 1, k + 2 may stay in flight (fewer near the end)
-    if (k + 2 < KS) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else if (k + 1 < KS) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of K-step k - 1 are done
-    __builtin_amdgcn_s_barrier();
-    if (k + G3_NS - 1 < KS) issue(k + G3_NS - 1);  // into the stage K-step k - 1 used
-    const char* sA = smem + (k % G3_NS) * G3_STAGE_BYTES;
-    const char* sB = sA + G3_TILE_BYTES;
-    const int c0 = 2 * lh;
-    f32x4 ar[4][2], br[2][2];
-#pragma unroll
-    for (int a = 0; a < 4; ++a) {
-      const int r = wm * 128 + a * 32 + li;
-      ar[a][0] = *reinterpret_cast<const f32x4*>(sA + g3_off(r, c0));
-      ar[a][1] = *reinterpret_cast<const f32x4*>(sA + g3_off(r, c0 + 1));
-    }
-#pragma unroll
-    for (int b = 0; b < 2; ++b) {
-      const int r = wn * 64 + b * 32 + li;
-      br[b][0] = *reinterpret_cast<const f32x4*>(sB + g3_off(r, c0));
-      br[b][1] = *reinterpret_cast<const f32x4*>(sB + g3_off(r, c0 + 1));
-    }
-    const float sa = sa_cur = h3_keep(sa_cur, wave_max_nonneg(absmax_x4(ar)), sa_min);
-    const float sb = sb_cur = h3_keep(sb_cur, wave_max_nonneg(absmax_x4(br)), sb_min);
-    if (sa != ua || sb != ub) {
-      if (ua != 0.f) {
-        const float fa = sa / ua, fb = sb / ub;
-#pragma unroll
-        for (int a = 0; a < 4; ++a)
-#pragma unroll
-          for (int b = 0; b < 2; ++b) acc[a][b] = (acc[a][b] * fa) * fb;
-      }
-      ua = sa;
-      ub = sb;
-    }
-    f16x8 af[2][4], bf[2][2];
-#pragma unroll
-    for (int a = 0; a < 4; ++a) {
-      u32x2 h0, l0, h1, l1;
-      split2h_x4(ar[a][0] * sa, h0, l0);
-      split2h_x4(ar[a][1] * sa, h1, l1);
-      af[0][a] = __builtin_bit_cast(f16x8, u32x4{h0[0], h0[1], h1[0], h1[1]});
-      af[1][a] = __builtin_bit_cast(f16x8, u32x4{l0[0], l0[1], l1[0], l1[1]});
-    }
-#pragma unroll
-    for (int b = 0; b < 2; ++b) {
-      u32x2 h0, l0, h1, l1;
-      split2h_x4(br[b][0] * sb, h0, l0);
-      split2h_x4(br[b][1] * sb, h1, l1);
-      bf[0][b] = __builtin_bit_cast(f16x8, u32x4{h0[0], h0[1], h1[0], h1[1]});
-      bf[1][b] = __builtin_bit_cast(f16x8, u32x4{l0[0], l0[1], l1[0], l1[1]});
-    }
-#pragma unroll
-    for (int a = 0; a < 4; ++a)
-#pragma unroll
-      for (int b = 0; b < 2; ++b) {
-        acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[1][a], bf[0][b], acc[a][b], 0, 0, 0);
-        acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[0][a], bf[1][b], acc[a][b], 0, 0, 0);
-        acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[0][a], bf[0][b], acc[a][b], 0, 0, 0);
-      }
-  }
-  const float ia = ua != 0.f ? 1.f / ua : 0.f, ib = ub != 0.f ? 1.f / ub : 0.f;
-#pragma unroll
-  for (int a = 0; a < 4; ++a)
-#pragma unroll
-    for (int b = 0; b < 2; ++b) {
-      const int n = n0 + wn * 64 + b * 32 + li;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = m0 + wm * 128 + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-        Cm[(size_t)m * N + n] = (acc[a][b][r] * ia) * ib;
       }
     }
 }
@@ -2244,24 +1973,11 @@ int launch_wino3x3(const IGemmArgs& a, int B, void* ws, hipStream_t s, float* ke
                        (int64_t)N * C, T * N);
     rc = launch_status("wino_gemm");
   } else if (v == 4 && N % 64 == 0 && C % 32 == 0) {
-    // fp16x3 with per-K-step power-of-two tile scales (gemm_nt_h3_bk32_kernel); key 41: the 256 x 256
-    // LDS-DMA kernel where the shape tiles by 256 and gives at least 2 blocks per CU
-    if (tune_get(PIS_TUNE_GEMM_256) != 0 && T % 256 == 0 && N % 256 == 0 && (T / 256) * (N / 256) * nxi >= 512) {
-      const dim3 grid((int)(T / 256) * (N / 256), nxi);
-      if (tune_get(PIS_TUNE_GEMM_256) == 2)
-        hipLaunchKernelGGL(gemm_nt_h3_256r_kernel, grid, dim3(512), 0, s, V, U, Mt, (int)T, N, C, T * C,
-                           (int64_t)N * C, T * N);
-      else
-        hipLaunchKernelGGL(gemm_nt_h3_256_kernel, grid, dim3(512), 0, s, V, U, Mt, (int)T, N, C, T * C,
-                           (int64_t)N * C, T * N);
-    } else if (N % 128 == 0) {
+    // fp16x3 with per-K-step power-of-two tile scales (gemm_nt_h3_bk32_kernel)
+    if (N % 128 == 0) {
       const dim3 grid((int)cdiv(T, 128) * (N / 128), nxi);
-      if (tune_get(PIS_TUNE_GEMM_PRIO) != 0)
-        hipLaunchKernelGGL((gemm_nt_h3_bk32_kernel<128, 128, 3, true, 0, true>), grid, dim3(256), 0, s, V, U, Mt,
-                           (int)T, N, C, T * C, (int64_t)N * C, T * N);
-      else
-        hipLaunchKernelGGL((gemm_nt_h3_bk32_kernel<128, 128, 3>), grid, dim3(256), 0, s, V, U, Mt, (int)T, N, C,
-                           T * C, (int64_t)N * C, T * N);
+      hipLaunchKernelGGL((gemm_nt_h3_bk32_kernel<128, 128, 3>), grid, dim3(256), 0, s, V, U, Mt, (int)T, N, C,
+                         T * C, (int64_t)N * C, T * N);
     } else {
       const dim3 grid((int)cdiv(T, 128) * (N / 64), nxi);
       hipLaunchKernelGGL((gemm_nt_h3_bk32_kernel<128, 64, 4>), grid, dim3(256), 0, s, V, U, Mt, (int)T, N, C,
@@ -2372,7 +2088,9 @@ int launch_wino_input(const float* x, int ldx, int B, int H, int W, int C, float
 
 // channels per thread of the F(3x3,4x4) dz passes (pis_tune key 40): 2 where 256 is a multiple of
 // N / 2 (the bias partials' channel-group rule), else 4
-static int dz_vw(int N) { return tune_get(PIS_TUNE_DZ_VW) == 2 && N % 2 == 0 && 256 % (N / 2) == 0 ? 2 : 4; }
+// channels per thread of the dz passes: 2 where 256 % (N / 2) == 0 (144-162 registers; the float4
+// form, needed for N = 1024, holds 256 + 30 and one wave per SIMD; measured neutral on the step)
+static int dz_vw(int N) { return N % 2 == 0 && 256 % (N / 2) == 0 ? 2 : 4; }
 
 // blocks of the F(3x3,4x4) dz pass = rows of its bias partials; dz_bias_rows_max: for any key 40
 int wino_dz_blocks(int B, int H, int W, int N, int m) {
@@ -2505,16 +2223,6 @@ extern "C" int pis_debug_gemm_nt(const float* A, const float* B, float* C, int M
     case 11: hipLaunchKernelGGL((gemm_nt_h3_bk32_kernel<128, 128, 3>), grid, dim3(256), 0, s, A, B, C, M, N, K, sa, sb, sc); break;
     case 12: hipLaunchKernelGGL((gemm_nt_h3_bk32_kernel<128, 64, 4>), grid, dim3(256), 0, s, A, B, C, M, N, K, sa, sb, sc); break;
     case 13: hipLaunchKernelGGL((gemm_nt_h3_bk32_kernel<128, 128, 3, true, 1>), grid, dim3(256), 0, s, A, B, C, M, N, K, sa, sb, sc); break;
-    case 15:
-      PIS_CHECK_ARG(M % 256 == 0 && N % 256 == 0, "pis_debug_gemm_nt: variant 15 needs M, N % 256 == 0");
-      hipLaunchKernelGGL(gemm_nt_h3_256_kernel, dim3((M / 256) * (N / 256), batch), dim3(512), 0, s, A, B, C, M, N, K,
-                         sa, sb, sc);
-      break;
-    case 16:
-      PIS_CHECK_ARG(M % 256 == 0 && N % 256 == 0, "pis_debug_gemm_nt: variant 16 needs M, N % 256 == 0");
-      hipLaunchKernelGGL(gemm_nt_h3_256r_kernel, dim3((M / 256) * (N / 256), batch), dim3(512), 0, s, A, B, C, M, N,
-                         K, sa, sb, sc);
-      break;
     case 14: hipLaunchKernelGGL((gemm_nt_h3_bk32_kernel<128, 128, 3, true, 2>), grid, dim3(256), 0, s, A, B, C, M, N, K, sa, sb, sc); break;
     default: set_error("pis_debug_gemm_nt: unknown variant %d", variant); return PIS_ERR_ARG;
   }

@@ -122,19 +122,25 @@ class _FusedLoss(torch.autograd.Function):
 
 
 def fused_loss(u: torch.Tensor, t: torch.Tensor, cfg: LossConfig, sink: dict = None) -> torch.Tensor:
-    """Differentiable total loss (0-dim); per-term values land in ``sink``."""
+    """Differentiable total loss (0-dim); per-term values land in ``sink``.
+
+    In grad mode the returned loss is a view of ``sink["terms"]`` (no copy launch in the step):
+    modifying it in place (``loss /= k``) raises autograd's custom-Function view error; write
+    ``loss = loss / k`` instead. In no-grad mode it is a copy, so in-place updates never reach the
+    logged terms."""
     if sink is None:
         sink = {}
     if not (torch.is_grad_enabled() and u.requires_grad):
         terms, counts, scores = loss_forward(u, t, cfg)
         sink["terms"], sink["counts"], sink["scores"] = terms, counts, scores
-        return terms[0]
+        return terms[0].clone()
     return _FusedLoss.apply(u, t, cfg, sink)
 
 
 def loss_from_forward(u: torch.Tensor, t: torch.Tensor, cfg: LossConfig, sink: dict) -> torch.Tensor:
     """The differentiable total loss of terms the U-Net's fused head + loss forward already wrote
-    into ``sink`` (UNet.forward_with_loss): an autograd node with no forward launch of its own."""
+    into ``sink`` (UNet.forward_with_loss): an autograd node with no forward launch of its own.
+    Same aliasing rule as ``fused_loss``: a view of the terms in grad mode, a copy otherwise."""
     if not (torch.is_grad_enabled() and u.requires_grad):
-        return sink["terms"][0]
+        return sink["terms"][0].clone()
     return _FusedLoss.apply(u, t, cfg, sink, True)

@@ -799,17 +799,6 @@ class UNetEngine:
                      dx.p, dx.ld, B, Hl, Wl, conv.in_channels, conv.out_channels, flags, ws, wsb, st)
 
             sync = self.side_sync if (prep and dx is not None and side is not main) else "prep"
-            if (not prep and dx is not None and side is not main and m.grad_ready_hook is None
-                    and lib.pis_tune(_hip.PIS_TUNE_DIRECT_WGRAD_MAIN, -1) != 0
-                    and lib.pis_conv3x3_dgrad_direct(B, Hl, Wl, conv.in_channels, conv.out_channels, dz.ld, wsb)
-                    and lib.pis_conv3x3_wgrad_ws(B, Hl, Wl, conv.in_channels, conv.out_channels) <= wsb):
-                # key 44: a direct layer's weight gradient on the main stream after its input
-                # gradient, in the main workspace (the two MFMA-bound kernels in sequence instead of
-                # side by side)
-                dgrad()
-                call("pis_conv3x3_wgrad_keep", x.p, x.ld, dz.p, dz.ld, self._gptr(conv.weight),
-                     self._gptr(conv.bias), B, Hl, Wl, conv.in_channels, conv.out_channels, acc, ws, wsb, 0, st)
-                return
             if sync == "prep":  # the weight gradient starts as soon as dz's transforms exist
                 to_side()
                 wgrad()

@@ -37,3 +37,14 @@ def test_argument_errors_are_reported_not_thrown():
     rc = lib.pis_conv3x3_fwd(0, 4, 0, 0, 0, 0, 4, 1, 4, 4, 4, 4, 0, 0)
     assert rc == -1
     assert b"pis_conv3x3_fwd" in lib.pis_last_error()
+
+
+def test_head_loss_fwd_ok_bounds_lds():
+    """The fused head + loss forward is refused (the Python side then takes pis_head_fwd +
+    pis_loss_fwd) when its staged rows would exceed a workgroup's 160 KB of LDS:
+    B = 128 at 1024^2 doubles the bands to 64 rows, (64 + 2) x 1032 x 4 B = 272 KB."""
+    lib = _hip.lib()
+    assert lib.pis_head_loss_fwd_ok(8, 512, 512, 64) == 1
+    assert lib.pis_head_loss_fwd_ok(8, 1024, 1024, 64) == 1
+    assert lib.pis_head_loss_fwd_ok(128, 1024, 1024, 64) == 0
+    assert lib.pis_head_loss_fwd_ok(1, 16, 1280, 64) == 1

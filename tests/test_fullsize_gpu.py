@@ -10,8 +10,8 @@
   does. Forward, every loss term, the per-sample Dice / IoU counters, every parameter gradient and
   one AdamW step (src/train.py:108-167).
 * C5 shape (1024 x 1024, lambda_RD = 1e-3, lambda_PF = 0) at the ends of the S2 sweep, D = 0.5
-  and D = 100 (run_ablation.py:176-188): the same checks, at B = 1 and at B = 4 (the largest
-  per-rank batch whose float64 oracle fits the GPU box's host memory; C5 runs B = 8 per rank).
+  and D = 100 (run_ablation.py:176-188): the same checks, at B = 1 and at C5's own B = 8 per rank
+  (float64 truth built in 2-image chunks, _run_chunked).
 * L_RD at C2 (src/pde.py:124-145): D Lap(u) + f(u) of a near-constant random-init u cancels,
   so fp32 rounding of u is amplified; instead of excluding the term, its error is BOUNDED:
   |L_RD(HIP) - L_RD(fp64)| <= 10 |L_RD(fp32 oracle) - L_RD(fp64)| (or <= 1e-4 relative), i.e.
@@ -43,10 +43,9 @@ def _progress(capsys):
     return log
 
 
-def _run(H, W, loss_kws, seed, B=1, keep_net=False, log=None):
-    """One HIP training step per loss config (same weights, same dropout masks) and the float64
-    oracle on the first run's decisions (one forward, one backward per config)."""
-    log = log or (lambda msg: None)
+def _hip_steps(H, W, loss_kws, seed, B, log):
+    """One HIP training step per loss config (same weights, same dropout masks) -> (img, mask, the
+    fp32 oracle module, scales, runs, the first run's decisions, the HIP net)."""
     from physics_informed_image_segmentation_amd import DiceBCEPDELoss, UNet
     img, mask = rt.synthetic_batch(B, H, W, seed=seed)
     torch.manual_seed(seed)
@@ -70,25 +69,27 @@ def _run(H, W, loss_kws, seed, B=1, keep_net=False, log=None):
         hip_runs.append((u.detach().cpu(), net.last_logits.detach().cpu(), crit.last["terms"].cpu(),
                          {n: p.grad.detach().cpu().clone() for n, p in net.named_parameters()},
                          crit.last["counts"].cpu()))
-    log(f"HIP steps done ({B}x{H}x{W}); float64 oracle forward")
-    ref64 = rt.UNetRef().double().train()
-    ref64.load_state_dict(ref.state_dict())
-    record = {}
-    p64, z64 = rt.unet_forward(ref64, img.double(), {k: v.double() for k, v in scales.items()},
-                               decisions=decisions, record=record, return_logits=True)
-    # per site: (flips, worst flip margin, near-ties of the float64 record within 1e-5 of the site's scale)
-    near = rt.near_ties(record, 1e-5, scales)
-    flips = {k: (n, m, near[k]) for k, (n, m) in rt.decision_flips(decisions, record, scales).items()}
-    truth = []
-    for kw in loss_kws:
-        log(f"float64 oracle backward {kw}")
-        ref64.zero_grad(set_to_none=True)
-        t64 = rt.loss_terms(p64, mask.double(), **kw)
-        t64["loss"].backward(retain_graph=True)
-        truth.append(({k: float(v) for k, v in t64.items()},
-                      {n: q.grad.detach().clone() for n, q in ref64.named_parameters()}))
+    log(f"HIP steps done ({B}x{H}x{W})")
+    return img, mask, ref, scales, hip_runs, decisions, net
+
+
+def _run(H, W, loss_kws, seed, B=1, keep_net=False, log=None):
+    """One HIP training step per loss config (same weights, same dropout masks) and the float64
+    oracle on the first run's decisions (one forward, one backward per config)."""
+    log = log or (lambda msg: None)
+    img, mask, ref, scales, hip_runs, decisions, net = _hip_steps(H, W, loss_kws, seed, B, log)
+    p64, z64, flips, truth = rt.whole_truth(ref, img, mask, scales, decisions, loss_kws, log)
     if keep_net:
         return img, mask, ref, scales, hip_runs, p64, z64, flips, truth, net
+    return img, mask, ref, scales, hip_runs, p64, z64, flips, truth
+
+
+def _run_chunked(H, W, loss_kws, seed, B, chunk, log):
+    """_run for a batch whose float64 oracle does not fit host memory whole (C5: B = 8 at 1024^2
+    would need ~220 GB): the truth from rt.chunked_truth (per-chunk forward, whole-batch loss and
+    dL/dp, per-chunk backward; pinned to the whole-batch oracle by tests/test_oracle.py)."""
+    img, mask, ref, scales, hip_runs, decisions, _ = _hip_steps(H, W, loss_kws, seed, B, log)
+    p64, z64, flips, truth = rt.chunked_truth(ref, img, mask, scales, decisions, loss_kws, chunk, log)
     return img, mask, ref, scales, hip_runs, p64, z64, flips, truth
 
 
@@ -140,28 +141,29 @@ def test_c5_train_step_d_sweep_ends(hip):
         assert abs(rd_hip - rd64) <= max(10.0 * abs(rd32 - rd64), TOL * abs(rd64)), kw
 
 
-@pytest.mark.timeout(1500)
-def test_c5_batch4_train_step(hip, capsys):
-    """BASELINE C5 per rank (run_ablation.py:176-188: 1024 x 1024, lambda_RD = 1e-3, lambda_PF = 0) at
-    B = 4, both ends of the S2 sweep (D = 0.5, D = 100): logits, probabilities, every loss term
-    (L_RD bounded by the fp32 oracle's own error), every parameter gradient against float64 on the
-    HIP decisions. B = 4 is the largest batch whose float64 oracle (forward record + two
-    backwards, ~110 GB of host memory) fits the GPU box's host-memory cap with margin; C5's B = 8
-    per rank would need ~220 GB. B = 4 at 1024^2 is 2x C2's pixel count: the weight gradients'
-    split-K slab counts and slab-reduction regimes, the 1024-wide head / loss rows and the strip
-    weight gradient's multi-strip block ranges at a size B = 1 never reaches."""
+@pytest.mark.timeout(2400)
+def test_c5_batch8_train_step(hip, capsys):
+    """BASELINE C5 per rank exactly (run_ablation.py:176-188: B = 8, 1024 x 1024, lambda_RD = 1e-3,
+    lambda_PF = 0) at both ends of the S2 sweep (D = 0.5, D = 100): logits, probabilities, every loss
+    term (L_RD bounded by the fp32 oracle's own error), every parameter gradient against float64 on
+    the HIP decisions. The float64 truth is built in 2-image chunks
+    (_run_chunked: per-chunk forward, whole-batch loss and dL/dp, per-chunk backward) since the
+    whole batch's float64 graph would need ~220 GB of host memory. B = 8 at 1024^2 is 4x C2's pixel
+    count: the weight gradients' split-K slab counts and slab-reduction regimes, the 1024-wide head
+    / loss rows and the direct weight gradient's block ranges at the largest size the bench runs."""
     kws = [dict(rd_w=1e-3, pf_w=0.0, D=D, a=0.5) for D in (0.5, 100.0)]
-    B = 4
+    B = 8
     log = _progress(capsys)
-    img, mask, ref, scales, runs, p64, z64, flips, truth = _run(1024, 1024, kws, seed=7, B=B, log=log)
+    img, mask, ref, scales, runs, p64, z64, flips, truth = _run_chunked(1024, 1024, kws, seed=7, B=B, chunk=2,
+                                                                       log=log)
     log("fp32 oracle forward (the L_RD bound)")
     with torch.no_grad():
-        p32 = ref(img, scales)
+        p32 = torch.cat([ref(img[c0:c0 + 2], {k: v[c0:c0 + 2] for k, v in scales.items()}) for c0 in range(0, B, 2)])
     for kw, run, tr in zip(kws, runs, truth):
         _check_step(run, p64, z64, tr, flips, B * 1024 * 1024, skip_terms=("pde_loss",))
         rd32 = rt.rd_loss(p32.double(), kw["D"], 0.5).item()
         rd64, rd_hip = tr[0]["pde_loss"], run[2][3].item()
-        print(f"L_RD at C5 B=4, D={kw['D']}: fp64 {rd64:.9e}  HIP {rd_hip:.9e}  fp32 oracle {rd32:.9e}")
+        print(f"L_RD at C5 B=8, D={kw['D']}: fp64 {rd64:.9e}  HIP {rd_hip:.9e}  fp32 oracle {rd32:.9e}")
         assert abs(rd_hip - rd64) <= max(10.0 * abs(rd32 - rd64), TOL * abs(rd64)), kw
 
 

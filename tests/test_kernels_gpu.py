@@ -105,7 +105,7 @@ def test_conv3x3_dgrad_wgrad(hip, B, H, W, Cin, Cout):
 
 # every non-default kernel variant behind pis_tune (include/pis_capi.h) stays exact too
 TUNE_VARIANTS = [(4, 1), (4, 2), (4, 3), (5, 0), (6, 2048), (3, 0), (7, 1), (8, 0), (8, 2), (10, 0), (10, 1),
-                 (11, 0), (13, 0), (13, 1), (13, 2), (13, 3), (10, 2), (10, 3), (14, 0), (14, 1), (14, 2), (15, 0), (16, 0), (17, 4), (22, 0), (25, 1), (26, 0), (26, 1), (27, 0), (31, 0), (39, 3), (40, 4), (41, 1), (41, 2), (45, 1), (46, 0)]
+                 (11, 0), (13, 0), (13, 1), (13, 2), (13, 3), (10, 2), (10, 3), (14, 0), (14, 1), (14, 2), (15, 0), (16, 0), (17, 4), (22, 0), (25, 1), (26, 0), (26, 1), (27, 0), (31, 0), (46, 0)]
 
 
 @pytest.mark.parametrize("key,value", TUNE_VARIANTS)
@@ -195,18 +195,6 @@ def test_conv3x3_ex_winograd(hip, B, H, W, Cin, Cout, mode):
         assert rel_err(db.cpu() - 0.25, dz.sum(dim=(0, 2, 3))) < 1e-5
     finally:
         hip.pis_tune(8, prev)
-
-
-@pytest.mark.parametrize("mode", [1, 2])
-def test_conv3x3_gemm_256_shape(hip, mode):
-    """pis_tune(41, 1 / 2) where it engages: T = 4096 tiles x 256 outputs (576 blocks of the
-    256 x 256 LDS-DMA GEMM, two 32-deep stages / the 4-stage ring) for the forward and the input
-    gradient, against fp32 ATen."""
-    prev = hip.pis_tune(41, mode)
-    try:
-        test_conv3x3_ex_winograd(hip, 4, 128, 128, 256, 256, 1)
-    finally:
-        hip.pis_tune(41, prev)
 
 
 def test_conv3x3_c1_wgrad(hip):
@@ -530,6 +518,57 @@ def test_fused_loss_c4_grid_vs_oracle(hip, rd_w, pf_w):
     np.testing.assert_allclose(scores.numpy(), np.stack([d, u], 1), rtol=1e-6)
 
 
+@pytest.mark.parametrize("rd_w,pf_w", C4_GATINGS)
+def test_head_loss_bwd_c4_grid_vs_oracle(hip, rd_w, pf_w):
+    """The C2 step's loss backward is head_loss_bwd_kernel<RD, PF> (the loss adjoint fused into the
+    head backward), not loss_bwd_kernel: here it runs at the C2 grid (8, 512, 512) under the four R1
+    gatings (BASELINE C4, run_ablation.py:42-83) through the production gating, against float64:
+    oracle/loss_numpy.py:loss_backward (src/loss.py:114-162, src/pde.py:124-212) -> dL/du at every
+    pixel, the sigmoid chain (src/unet.py:206-210) -> dL/dz, and the 64-channel 1x1 head's
+    gradients dx = dz w [x > 0], dw = sum dz x, db = sum dz (src/unet.py:157) at every pixel and
+    channel."""
+    from physics_informed_image_segmentation_amd._hip import LossParams
+    B, H, W, C = 8, 512, 512, 64
+    u, t = _c4_prediction(B, H, W, seed=15)
+    g = torch.Generator().manual_seed(16)
+    x = F.relu(torch.randn(B, H, W, C, generator=g))
+    w = torch.randn(C, generator=g) * 0.1
+    kw = dict(rd_w=rd_w, pf_w=pf_w, D=5.0, a=0.5, eps=0.05)
+    prm = LossParams(0.5, 0.5, rd_w, pf_w, 1e-6, 5.0, 0.5, 0.05, 0.5, 0)
+    ud, td, xd, wd = u.cuda(), t.cuda(), x.cuda(), w.cuda()
+    terms = torch.empty(8, device="cuda")
+    lws = torch.zeros(hip.pis_loss_ws(B, H, W) // 4 + 1, device="cuda")
+    assert hip.pis_loss_fwd(ud.data_ptr(), td.data_ptr(), B, H, W, ctypes.byref(prm), terms.data_ptr(), 0, 0,
+                            lws.data_ptr(), lws.numel() * 4, s()) == 0
+    fws = torch.empty(hip.pis_head_loss_bwd_ws(B, H, W, C) // 4 + 1, device="cuda")
+    du = torch.empty(B, H, W, device="cuda")
+    dx = torch.empty(B, H, W, C, device="cuda")
+    dw, db = torch.empty(C, device="cuda"), torch.empty(1, device="cuda")
+    rc = hip.pis_head_loss_bwd(xd.data_ptr(), C, wd.data_ptr(), ud.data_ptr(), td.data_ptr(), du.data_ptr(), B, H, W,
+                               C, ctypes.byref(prm), terms.data_ptr(), 0, dx.data_ptr(), C, dw.data_ptr(),
+                               db.data_ptr(), 0, fws.data_ptr(), fws.numel() * 4, s())
+    assert rc == 0, hip.pis_last_error()
+    torch.cuda.synchronize()
+    del xd
+    gref = ln.loss_backward(u.numpy(), t.numpy(), **kw)  # float64 dL/du
+    du_h = du.cpu().numpy()
+    assert np.linalg.norm(du_h - gref) / np.linalg.norm(gref) < 1e-5
+    assert np.abs(du_h - gref).max() <= 1e-5 * np.abs(gref).max()  # every pixel, boundaries included
+    u64 = u.double()
+    dz64 = torch.from_numpy(gref) * u64 * (1.0 - u64)  # sigmoid chain
+    x64 = x.reshape(-1, C).double()
+    dw64 = x64.t() @ dz64.reshape(-1)
+    db64 = dz64.sum()
+    assert rel_err(dw.cpu().double(), dw64) < 1e-5
+    assert abs(db.item() - db64.item()) <= 1e-5 * dz64.abs().sum().item()  # fp32 summation bound
+    dx_h = dx.cpu().reshape(-1, C)
+    scale = (dz64.abs().max() * w.double().abs().max()).item()
+    for i0 in range(0, x64.shape[0], 1 << 19):  # every pixel and channel, in chunks
+        sl = slice(i0, i0 + (1 << 19))
+        dx64 = dz64.reshape(-1)[sl, None] * w.double()[None, :] * (x64[sl] > 0)
+        assert (dx_h[sl].double() - dx64).abs().max().item() <= 1e-5 * scale
+
+
 def _head_loss_fwd_call(hip, x, ldx, w, b, t, kw, all_terms=False):
     """pis_head_loss_fwd on x ([B,H,W,ldx], the first 64 channels the head input) -> (z, u, terms,
     counts, scores) on the host."""
@@ -553,7 +592,7 @@ def _head_loss_fwd_call(hip, x, ldx, w, b, t, kw, all_terms=False):
 
 
 @pytest.mark.parametrize("B,H,W,ldx", [(2, 64, 64, 64), (1, 48, 128, 128), (3, 2, 64, 64), (1, 40, 1024, 64),
-                                       (2, 37, 512, 64), (8, 512, 512, 64)])
+                                       (2, 37, 512, 64), (8, 512, 512, 64), (1, 11, 1280, 64), (2, 9, 2048, 64)])
 @pytest.mark.parametrize("rd_w,pf_w", C4_GATINGS)
 def test_head_loss_fwd_fused(hip, B, H, W, ldx, rd_w, pf_w):
     """pis_head_loss_fwd (the head's 1x1 conv + sigmoid fused with the loss forward, the C2 step's
@@ -561,8 +600,9 @@ def test_head_loss_fwd_fused(hip, B, H, W, ldx, rd_w, pf_w):
     summation order; and against the float64 oracle (oracle/loss_numpy.py on the same u): every
     term in the total, the counters and scores. Shapes: band heights that do not divide H (37),
     H = 2 (every row a reflect ghost), 1024-wide rows (8 rows per band), the C2 grid (8, 512, 512)
-    under the four R1 gatings (BASELINE C4), a wider row pitch (concat-style ldx)."""
-    from physics_informed_image_segmentation_amd._hip import LossParams
+    under the four R1 gatings (BASELINE C4), a wider row pitch (concat-style ldx), and rows wider
+    than 4 x 256 threads (1280: 256-thread blocks walk 320 column items; 2048) so a thread's loss
+    pass covers several column items."""
     g = torch.Generator().manual_seed(31)
     x = F.relu(torch.randn(B, H, W, ldx, generator=g)).cuda()
     w = (torch.randn(64, generator=g) * 0.15).cuda()
@@ -596,7 +636,7 @@ def test_head_loss_fwd_fused(hip, B, H, W, ldx, rd_w, pf_w):
     assert ((z.double() - z64).abs().max() / z64.abs().max()).item() < 1e-6
 
 
-@pytest.mark.parametrize("B,H,W", [(2, 37, 512), (8, 512, 512), (1, 40, 1024)])
+@pytest.mark.parametrize("B,H,W", [(2, 37, 512), (8, 512, 512), (1, 40, 1024), (1, 13, 2048)])
 def test_head_loss_fwd_variants(hip, B, H, W):
     """pis_tune(38): the 256-thread bands (0), the 1024-thread bands (1) and the same with three
     register sets in flight (2) give bitwise the same z, u and counters, and the same terms to fp32

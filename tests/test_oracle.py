@@ -150,3 +150,36 @@ def test_decision_conditioned_forward_matches_free_forward():
     flipped["enc2.0"].view(-1)[0] ^= True
     n, margin = rt.decision_flips(flipped, rec2)["enc2.0"]
     assert n == 1 and margin > 0
+
+
+def test_chunked_truth_equals_whole_truth():
+    """rt.chunked_truth (the C5 B = 8 float64 truth: per-chunk forward / backward, whole-batch loss
+    and dL/dp) equals rt.whole_truth on a batch both fit: probabilities, logits, every term and
+    every parameter gradient, and the same decision-flip / near-tie counts. Decisions are the fp32
+    oracle's own (a stand-in for a HIP run's), so some sites differ from float64's."""
+    B, H, W = 3, 32, 32
+    img, mask = rt.synthetic_batch(B, H, W, seed=3)
+    torch.manual_seed(3)
+    ref = rt.UNetRef(1, 1, 64).train()
+    scales = rt.make_drop_scales(ref, B, torch.Generator().manual_seed(3))
+    rec32 = {}
+    with torch.no_grad():
+        rt.unet_forward(ref, img, scales, record=rec32)
+    decisions = {}
+    for k, v in rec32.items():
+        if k.startswith("pool"):
+            b, c, h, w = v.shape
+            win = v.reshape(b, c, h // 2, 2, w // 2, 2).permute(0, 1, 2, 4, 3, 5).reshape(b, c, h // 2, w // 2, 4)
+            decisions[k] = win.argmax(-1)
+        else:
+            decisions[k] = v > 0
+    kws = [dict(rd_w=1e-2, pf_w=1e-2, D=5.0, a=0.5, eps=0.05), dict(rd_w=1e-3, D=100.0, a=0.5)]
+    p_w, z_w, f_w, t_w = rt.whole_truth(ref, img, mask, scales, decisions, kws)
+    p_c, z_c, f_c, t_c = rt.chunked_truth(ref, img, mask, scales, decisions, kws, chunk=2)
+    assert torch.allclose(p_w, p_c, rtol=0, atol=1e-15) and torch.allclose(z_w, z_c, rtol=0, atol=1e-13)
+    assert {k: (v[0], v[2]) for k, v in f_w.items()} == {k: (v[0], v[2]) for k, v in f_c.items()}
+    for (tw, gw), (tc, gc) in zip(t_w, t_c):
+        for k in tw:
+            assert abs(tw[k] - tc[k]) <= 1e-12 * max(abs(tw[k]), 1e-30), k
+        for n in gw:
+            assert ((gc[n] - gw[n]).norm() / gw[n].norm().clamp_min(1e-300)).item() < 1e-10, n
