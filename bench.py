@@ -496,6 +496,37 @@ def launch(n: int) -> int:
     return rc
 
 
+def dist_summary(bucketer, device, backend):
+    """N > 1: what the process group actually formed and how much of the gradient all-reduce the
+    backward left exposed: the backend, the world size as formed,
+    RCCL's version, the bucket plan, and per rank the mean / worst exposed all-reduce ms over the
+    timed steps (GradBucketer.exposed_ms: later stream's last gradient kernel -> all-reduces
+    waited for), gathered to every rank (the max over ranks is the figure that bounds the step)."""
+    per_step = bucketer.exposed_ms()
+    world, rank = dist.get_world_size(), dist.get_rank()
+    mine = torch.zeros(2 * world, dtype=torch.float64, device=device if backend == "nccl" else "cpu")
+    if per_step:
+        mine[rank] = sum(per_step) / len(per_step)
+        mine[world + rank] = max(per_step)
+    dist.all_reduce(mine, op=dist.ReduceOp.SUM)
+    mean_r, worst_r = mine[:world].tolist(), mine[world:].tolist()
+    rccl = None
+    if dist.get_backend() == "nccl":
+        try:
+            v = torch.cuda.nccl.version()
+            rccl = ".".join(str(x) for x in v) if isinstance(v, tuple) else str(v)
+        except Exception:  # noqa: BLE001 - informational only
+            rccl = None
+    return {
+        "backend": dist.get_backend(), "world_size_formed": world, "rccl_version": rccl,
+        "grad_bytes": int(bucketer.model.arena.numel()) * 4, "buckets": len(bucketer.buckets),
+        "bucket_bytes": bucketer.bucket_bytes,
+        "exposed_allreduce_ms": {"max_over_ranks": max(mean_r), "worst_step_max_over_ranks": max(worst_r),
+                                 "mean_per_rank": mean_r, "steps": len(per_step)},
+        "measured": "HIP events: after each rank's last gradient kernel on both streams vs after "
+                    "GradBucketer.finish() waited for the bucketed all-reduces (per timed step)"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -535,8 +566,7 @@ def main():
     torch.manual_seed(42)
     model = UNet(1, 1, 64).to(device).train()
     broadcast_parameters(model)
-    if world > 1:
-        GradBucketer(model)
+    bucketer = GradBucketer(model) if world > 1 else None
     torch.cuda.manual_seed(42 + rank)  # Dropout2d masks per rank (train() does the same)
     crit = DiceBCEPDELoss(**loss_kw)
     opt = AdamW(model.parameters(), lr=LR, weight_decay=1e-5, grad_scale=1.0 / world)
@@ -566,6 +596,8 @@ def main():
     dtimers = {k: KernelTimer(k) for k in DIRECT_ROLES}
     _hip.set_launch_hook(lambda *a: (ktimer(*a), ftimer(*a), htimer(*a), *(tm(*a) for tm in dtimers.values())))
     _hip.set_tracer(ltimer)
+    if bucketer is not None:
+        bucketer.timing = True
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = step()
@@ -580,6 +612,10 @@ def main():
         dt = tt.item()
     ms = dt / args.steps * 1e3
     imgs_per_s = world * B * args.steps / dt
+    dist_info = None
+    if bucketer is not None:
+        bucketer.timing = False
+        dist_info = dist_summary(bucketer, device, args.backend)
 
     _hip.set_tracer(None)
     _hip.set_launch_hook(None)
@@ -757,6 +793,8 @@ def main():
                  **{k: v["ms_per_step"] for k, v in direct_roofs.items()}}
         out["roofline_dominant"] = max(cands, key=cands.get)
         out["roofline"] = out[out["roofline_dominant"]]
+        if dist_info is not None:
+            out["distributed"] = dist_info
         if world == 1 and not args.no_cpu_baseline and args.config == "c2":
             out["cpu_baseline"] = cpu_baseline()
         print(json.dumps(out))

@@ -73,7 +73,13 @@ class GradBucketer:
         self.model = model
         self.pg = process_group
         self.world = dist.get_world_size(process_group)
+        self.bucket_bytes = bucket_bytes
         self.buckets = plan_buckets(model.arena_entries(), model.arena.numel(), bucket_bytes)
+        # timing (bench.py): per step, HIP events at the end of the backward's compute on both
+        # streams and after the all-reduces have been waited for -> the exposed all-reduce time
+        self.timing = False
+        self._marks = None
+        self._events: List = []
         self._reset()
         model.grad_ready_hook = self
 
@@ -109,6 +115,16 @@ class GradBucketer:
         self.works.append(dist.all_reduce(g[blo:bhi], op=dist.ReduceOp.SUM, group=self.pg, async_op=True))
         self.launched[i] = True
 
+    def mark_backward_done(self, main, side) -> None:
+        """Engine callback right before ``finish``: every gradient kernel is enqueued on ``main`` /
+        ``side``. With ``timing`` set, an event on each marks where the compute ends."""
+        if not self.timing:
+            return
+        e_main, e_side = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e_main.record(main)
+        e_side.record(side)
+        self._marks = (e_main, e_side)
+
     def finish(self) -> None:
         """After backward: launch anything left, make the compute stream wait."""
         while self.next_bucket < len(self.buckets):
@@ -116,7 +132,21 @@ class GradBucketer:
             self.next_bucket += 1
         for w in self.works:
             w.wait()
+        if self._marks is not None:  # the current stream now waits for every all-reduce
+            e_after = torch.cuda.Event(enable_timing=True)
+            e_after.record()
+            self._events.append((*self._marks, e_after))
+            self._marks = None
         self._reset()
+
+    def exposed_ms(self) -> List[float]:
+        """Per timed step (``timing`` set), the all-reduce time NOT hidden behind the backward: from
+        the later of the two streams' last gradient kernel to the point where the gradients are
+        summed on every rank. Synchronises the device; clears the record."""
+        torch.cuda.synchronize()
+        out = [max(0.0, min(em.elapsed_time(ea), es.elapsed_time(ea))) for em, es, ea in self._events]
+        self._events = []
+        return out
 
 
 def allreduce_scalars(t: torch.Tensor, op=None) -> torch.Tensor:

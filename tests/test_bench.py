@@ -74,6 +74,13 @@ def test_bench_launches_n_ranks():
     assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "dp2" and d["config"]["global_batch"] == 16
     assert abs(d["value"] - 16 * 1000.0 / d["ms_per_step"]) < 1e-6 * d["value"]  # 2 ranks x 8 images
     assert "cpu_baseline" not in d
+    # what the process group formed and the all-reduce time the backward left exposed, per rank
+    dd = d["distributed"]
+    assert dd["backend"] == "gloo" and dd["world_size_formed"] == 2 and dd["buckets"] >= 2
+    ex = dd["exposed_allreduce_ms"]
+    assert ex["steps"] == 2 and len(ex["mean_per_rank"]) == 2
+    assert all(v >= 0.0 for v in ex["mean_per_rank"])
+    assert ex["max_over_ranks"] == max(ex["mean_per_rank"]) and ex["worst_step_max_over_ranks"] >= ex["max_over_ranks"]
 
 
 def test_bench_rejects_world_mismatch():

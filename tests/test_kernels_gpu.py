@@ -839,41 +839,6 @@ def test_winograd_gemm_fp16x3_scales_any_magnitude(hip):
         assert errs[4, scale] <= 1.25 * errs[2, scale] + 1e-9, errs
 
 
-@pytest.mark.parametrize("dist", ["randn", "tiny", "wide", "rows"])
-def test_gemm_256_lds_dma(hip, dist):
-    """The fp16x3 256 x 256 GEMM fed by LDS-DMA (pis_debug_gemm_nt variant 15, pis_tune key 41:
-    per-wave power-of-two scales per 16-deep K-step, hi / lo split at fragment read) against
-    float64, beside the 128 x 128 fp16x3 kernel (11) and the native fp32 MFMA one (3): unit,
-    gradient-sized (A x 1e-9, B x 1e-3), row-wise 10^5-spread and 10^30-apart row blocks."""
-    batch, M, N, K = 3, 512, 512, 160
-    g = torch.Generator().manual_seed(81)
-    A = torch.randn(batch, M, K, generator=g, dtype=torch.float64)
-    Bm = torch.randn(batch, N, K, generator=g, dtype=torch.float64)
-    if dist == "tiny":
-        A *= 1e-9
-        Bm *= 1e-3
-    elif dist == "wide":
-        A *= 10.0 ** (-5 * torch.rand(batch, M, 1, generator=g, dtype=torch.float64))
-    elif dist == "rows":  # K-steps 1e30 apart inside one accumulation chain, and block rows too
-        A[:, :, 64:96] *= 1e-30
-        A[:, 256:] *= 1e15
-    A, Bm = A.float().double(), Bm.float().double()
-    ref = torch.bmm(A, Bm.transpose(1, 2))
-    Ad, Bd = A.float().cuda(), Bm.float().cuda()
-    errs = {}
-    for v in (3, 11, 15, 16):
-        Cm = torch.full((batch, M, N), float("nan"), device="cuda")
-        rc = hip.pis_debug_gemm_nt(Ad.data_ptr(), Bd.data_ptr(), Cm.data_ptr(), M, N, K, batch, v, s())
-        assert rc == 0, hip.pis_last_error()
-        torch.cuda.synchronize()
-        out = Cm.cpu().double()
-        assert torch.isfinite(out).all(), v
-        errs[v] = ((out - ref).norm() / ref.norm()).item()
-    for v in (15, 16):
-        assert errs[v] <= 1.25 * errs[3] + 1e-12, errs
-        assert errs[v] < 5e-6, errs
-
-
 @pytest.mark.parametrize("Cin,Cout", [(256, 256), (512, 128), (64, 128), (128, 64)])
 def test_winograd_wgrad_bf16x6_is_fp32_accurate(hip, Cin, Cout):
     """The bf16x6 (pis_tune(14, 1)) and fp16x3 (pis_tune(14, 2)) weight-gradient GEMMs against

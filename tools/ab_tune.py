@@ -4,7 +4,8 @@ GPU (box-to-box variance is ~3 %; same-process interleaving is not).
     python tools/ab_tune.py --variants "base;20=0;15=0,17=4" [--rounds 4] [--steps 10] [--shared]
 
 Each variant is a comma list of KEY=VALUE (include/pis_capi.h PIS_TUNE_*); "base" = defaults;
-"fa=0|1|2" plans that variant's engine with PIS_FILTER_AHEAD = that value (unet.py).
+"fa=0|1|2" plans that variant's engine with PIS_FILTER_AHEAD = that value, "dwm=0|1" runs the direct
+layers' weight gradients on the main stream (PIS_DIRECT_WGRAD_MAIN; unet.py).
 """
 import argparse
 import os
@@ -21,7 +22,12 @@ from physics_informed_image_segmentation_amd.dataset import disc_sample  # noqa:
 def parse(v):
     if v.strip() in ("", "base"):
         return {}
-    return {(k if k == "fa" else int(k)): int(x) for k, x in (kv.split("=") for kv in v.split(","))}
+    return {(k if k in HOST else int(k)): int(x) for k, x in (kv.split("=") for kv in v.split(","))}
+
+
+# host-side engine attributes a variant may set (unet.UNetEngine): fa = filter_ahead, dwm =
+# direct_wgrad_main
+HOST = {"fa": "filter_ahead", "dwm": "direct_wgrad_main"}
 
 
 def main():
@@ -35,7 +41,7 @@ def main():
     args = ap.parse_args()
     lib = _hip.lib()
     variants = [(v.strip(), parse(v)) for v in args.variants.split(";")]
-    keys = sorted({k for _, kv in variants for k in kv if k != "fa"})
+    keys = sorted({k for _, kv in variants for k in kv if k not in HOST})
     defaults = {k: lib.pis_tune(k, -1) for k in keys}
     dev = torch.device("cuda")
     g = torch.Generator().manual_seed(42)
@@ -59,11 +65,12 @@ def main():
         models[name] = (m, AdamW(m.parameters(), lr=1e-5, weight_decay=1e-5))
 
     from physics_informed_image_segmentation_amd.unet import UNetEngine
-    fa_default = UNetEngine.filter_ahead
+    host_default = {k: getattr(UNetEngine, a) for k, a in HOST.items()}
 
     def step(name):
         model, opt = models[name]
-        UNetEngine.filter_ahead = str(dict(variants)[name].get("fa", fa_default))
+        for k, a in HOST.items():
+            setattr(UNetEngine, a, str(dict(variants)[name].get(k, host_default[k])))
         opt.zero_grad()
         model.forward_with_loss(x, t, crit)[1].backward()  # the step as bench.py / train_epoch run it
         opt.step()
