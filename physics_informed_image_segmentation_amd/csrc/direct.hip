@@ -748,7 +748,8 @@ size_t direct_w_ws_bytes(int B, int H, int W, int Cin, int Cout) {
   return (size_t)sp * Cout * 9 * Cin * sizeof(float) + (size_t)sp * Cout * sizeof(float) + 512;
 }
 
-int reduce_slabs(const float* part, int splits, int64_t n, float* dst, int accumulate, hipStream_t s);
+int reduce_slabs2(const float* part, int splits, int64_t n, float* dst, const float* part_b, int splits_b,
+                  int64_t n_b, float* dst_b, int accumulate, hipStream_t s);
 
 int launch_direct_wgrad(const float* x, int ldx, const float* dz, int ldz, float* dw, float* db, int B, int H, int W,
                         int Cin, int Cout, int acc, void* ws, size_t ws_bytes, hipStream_t s) {
@@ -771,8 +772,8 @@ int launch_direct_wgrad(const float* x, int ldx, const float* dz, int ldz, float
     hipLaunchKernelGGL((conv3x3_wgrad_h3_kernel<false>), grid, dim3(256), 0, s, g);
   launch_hook("direct_wgrad_h3", 1, s, flop);
   int rc = launch_status("conv3x3_wgrad_h3");
-  if (!rc) rc = reduce_slabs(g.part, g.splits, (int64_t)Cout * 9 * Cin, dw, acc, s);
-  if (!rc && db) rc = reduce_slabs(g.part_bias, g.splits, Cout, db, acc, s);
+  // weights and bias in one launch (fixed-order sums, deterministic)
+  if (!rc) rc = reduce_slabs2(g.part, g.splits, (int64_t)Cout * 9 * Cin, dw, g.part_bias, g.splits, Cout, db, acc, s);
   return rc;
 }
 

@@ -73,8 +73,20 @@ int launch_wino_dz(const float* dz, int ldz, int B, int H, int W, int N, float* 
 int wino_dz_blocks(int B, int H, int W, int N, int m);
 int wino_dz_blocks_max(int B, int H, int W, int N, int m);  // over pis_tune key 40
 // M: nsplit split-K slabs sstride floats apart, summed in slab order (nsplit > 1 needs m == 4)
+// The F(3x3,4x4) weight gradient's bias gradient, folded into its output-transform launch:
+// db[n] (+)= scale x sum_{r < rows} part[r][n] (fixed order), part = the GEMM's [split][N] column
+// sums of E plane WINO4_BIAS_XI; rows == 0: none
+struct WgradOutBias {
+  const float* part;
+  int rows;
+  float* db;
+  float scale;
+};
+// E[7] = E[(1, 1)] = c^2 x (sum of the tile's 16 dz values), c = fp32(1/3) (w4_g4 row 1: the point 1)
+constexpr int WINO4_BIAS_XI = 7;
+constexpr float WINO4_BIAS_SCALE = (float)(1.0 / ((double)(1.0f / 3.0f) * (double)(1.0f / 3.0f)));
 int launch_wino_wgrad_out(const float* M, int N, int C, float* dw, int accumulate, hipStream_t s, int m,
-                          int nsplit = 1, int64_t sstride = 0);
+                          int nsplit = 1, int64_t sstride = 0, WgradOutBias bias = WgradOutBias{});
 
 // direct 3x3 conv in fp16x3 (direct.hip): shapes it covers, its workspace (split weights), the
 // launch (dgrad_orig: an input gradient whose a.wt holds the ORIGINAL KRSC weights)

@@ -17,6 +17,8 @@
 namespace pis {
 
 int reduce_slabs(const float* part, int splits, int64_t n, float* dst, int accumulate, hipStream_t s);
+int reduce_slabs2(const float* part, int splits, int64_t n, float* dst, const float* part_b, int splits_b,
+                  int64_t n_b, float* dst_b, int accumulate, hipStream_t s);
 
 __device__ __forceinline__ int refl(int i, int n) { return i < 0 ? -i : (i >= n ? 2 * n - 2 - i : i); }
 __device__ __forceinline__ int clampi(int i, int lo, int hi) { return i < lo ? lo : (i > hi ? hi : i); }
@@ -1375,7 +1377,8 @@ extern "C" int pis_head_loss_bwd(const float* x, int ldx, const float* w, const 
   else hipLaunchKernelGGL((head_loss_bwd_kernel<false, false>), grid, dim3(256), smem, s, g);
   int rc = launch_status("head_loss_bwd");
   const int acc = flags & PIS_ACCUMULATE;
-  if (!rc) rc = reduce_slabs(g.part, (int)(grid.x * grid.y), C, dw, acc, s);
-  if (!rc && db) rc = reduce_slabs(g.part_b, (int)(grid.x * grid.y), 1, db, acc, s);
+  // dw and db in one launch (fixed-order sums, deterministic)
+  if (!rc) rc = reduce_slabs2(g.part, (int)(grid.x * grid.y), C, dw, db ? g.part_b : nullptr, (int)(grid.x * grid.y), 1,
+                              db, acc, s);
   return rc;
 }

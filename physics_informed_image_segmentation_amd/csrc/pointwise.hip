@@ -229,6 +229,8 @@ __global__ void adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
 }
 
 int reduce_slabs(const float* part, int splits, int64_t n, float* dst, int accumulate, hipStream_t s);
+int reduce_slabs2(const float* part, int splits, int64_t n, float* dst, const float* part_b, int splits_b,
+                  int64_t n_b, float* dst_b, int accumulate, hipStream_t s);
 int colsum(const float* src, int ld, int64_t npix, int C, float* out, int accumulate, void* ws,
            size_t ws_bytes, hipStream_t s);
 size_t colsum_ws(int64_t npix, int C);
@@ -325,8 +327,7 @@ extern "C" int pis_head_bwd(const float* x, int ldx, const float* w, const float
   hipLaunchKernelGGL(head_bwd_kernel, dim3(blocks), dim3(256), 0, s, x, ldx, w, g, u, dx, lddx, npix,
                      C, ppb, part, part_b);
   int rc = launch_status("head_bwd");
-  if (!rc) rc = reduce_slabs(part, blocks, C, dw, acc, s);
-  if (!rc && db) rc = reduce_slabs(part_b, blocks, 1, db, acc, s);
+  if (!rc) rc = reduce_slabs2(part, blocks, C, dw, db ? part_b : nullptr, blocks, 1, db, acc, s);
   return rc;
 }
 

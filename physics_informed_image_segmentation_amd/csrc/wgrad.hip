@@ -35,6 +35,9 @@ struct WgradArgs {
   // batched launches (gridDim.y > 1, Winograd's 16 GEMMs): per-batch offsets; slab pitch
   int64_t bs_a, bs_b, bs_part, split_stride;     // split_stride 0 = Mp * Np
   int pair;                                      // wgrad_x6: pair-lane staging of 4-pixel operands
+  int bias_xi;                                   // batched launches: the batch whose column sums of A are
+                                                 // the bias partials (Winograd: 7, E's (1, 1) plane; 0 when
+                                                 // the launch has one batch)
   int dbg;                                       // wgrad_h3t timing twins (pis_tune key 2, wrong results):
                                                  // 1 no loads after the first two K-steps, 2 no staging
                                                  // after the first, 4 no slab stores
@@ -65,7 +68,7 @@ __global__ __launch_bounds__(256) void wgrad_f32_kernel(WgradArgs g) {
   const int m0 = tm * BM, n0 = tn * BN;
   const int p_begin = split * g.pix_per_split;
   const int p_end = min(g.P, p_begin + g.pix_per_split);
-  const bool do_bias = g.part_bias != nullptr && tn == 0;
+  const bool do_bias = g.part_bias != nullptr && tn == 0 && rm.batch == g.bias_xi;
 
   // tap of this tile (tiles never straddle a tap)
   int a_dr = 0, a_ds = 0, a_c0 = m0;
@@ -423,6 +426,87 @@ __global__ __launch_bounds__(256) void reduce_rows_chunk_kernel(float* __restric
   }
 }
 
+// Two slab reductions in ONE launch (a weight gradient's [split][n] slabs and its bias gradient's
+// [split][Cout] partials): the blocks of the second follow the first's; each block runs
+// reduce_slabs_kernel's fixed-order sums on its own job (float4 or scalar columns per job). Same
+// sums in the same order as two reduce_slabs_pitched launches: bitwise equal, one launch fewer.
+struct SlabJob {
+  const float* part;
+  float* dst;
+  int64_t n, pitch;
+  int splits, accumulate;
+  int vec, cols, blocks;  // launch plan (slab_job_plan)
+};
+
+static SlabJob slab_job_plan(const float* part, int splits, int64_t n, int64_t pitch, float* dst, int accumulate) {
+  SlabJob j{part, dst, n, pitch, splits, accumulate, 1, 1, 0};
+  const bool v4 = (n % 4 == 0) && (pitch % 4 == 0) && ((uintptr_t)part % 16 == 0) && ((uintptr_t)dst % 16 == 0);
+  j.vec = v4 ? 4 : 1;
+  const int64_t nv = n / j.vec;
+  const int gmax = splits >= 1024 ? 256 : 64;  // as reduce_slabs_pitched
+  int gwant = 1;
+  while (gwant < gmax && gwant < splits) gwant *= 2;
+  int cols = std::max(splits >= 1024 ? 1 : 4, 256 / gwant);
+  while (cols > 1 && cols / 2 >= nv) cols /= 2;
+  j.cols = cols;
+  j.blocks = (int)cdiv(nv, cols);
+  return j;
+}
+
+template <int VEC>
+__device__ __forceinline__ void reduce_slab_job(const SlabJob& j, int blk) {
+  typedef float vec __attribute__((ext_vector_type(VEC)));
+  const int cols = j.cols, groups = 256 / cols;
+  const int gi = threadIdx.x / cols, c = threadIdx.x - gi * cols;
+  const int64_t nv = j.n / VEC;
+  const int64_t col = (int64_t)blk * cols + c;
+  vec s = (vec)(0.f);
+  if (col < nv) {
+    vec s8[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s8[u] = (vec)(0.f);
+    int k = gi;
+    for (; k + 7 * groups < j.splits; k += 8 * groups) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        s8[u] += *reinterpret_cast<const vec*>(j.part + (size_t)(k + u * groups) * j.pitch + col * VEC);
+    }
+    for (int u = 0; k < j.splits; k += groups, ++u)
+      s8[u & 7] += *reinterpret_cast<const vec*>(j.part + (size_t)k * j.pitch + col * VEC);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s += s8[u];
+  }
+  __shared__ vec red[256];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int stride = groups / 2; stride >= 1; stride /= 2) {
+    if (gi < stride) red[gi * cols + c] += red[(gi + stride) * cols + c];
+    __syncthreads();
+  }
+  if (gi == 0 && col < nv) {
+    vec t = j.accumulate ? *reinterpret_cast<vec*>(j.dst + col * VEC) : (vec)(0.f);
+    *reinterpret_cast<vec*>(j.dst + col * VEC) = t + red[c];
+  }
+}
+
+__global__ __launch_bounds__(256) void reduce_slabs2_kernel(SlabJob a, SlabJob b) {
+  const bool first = (int)blockIdx.x < a.blocks;
+  const SlabJob& j = first ? a : b;
+  const int blk = first ? (int)blockIdx.x : (int)blockIdx.x - a.blocks;
+  if (j.vec == 4) reduce_slab_job<4>(j, blk);
+  else reduce_slab_job<1>(j, blk);
+}
+
+// the two reductions of a weight gradient (weights, then bias; bias may be NULL) in one launch
+int reduce_slabs2(const float* part, int splits, int64_t n, float* dst, const float* part_b, int splits_b,
+                  int64_t n_b, float* dst_b, int accumulate, hipStream_t s) {
+  const SlabJob a = slab_job_plan(part, splits, n, n, dst, accumulate);
+  if (!dst_b) return reduce_slabs_pitched(part, splits, n, n, dst, accumulate, s);
+  const SlabJob b = slab_job_plan(part_b, splits_b, n_b, n_b, dst_b, accumulate);
+  hipLaunchKernelGGL(reduce_slabs2_kernel, dim3(a.blocks + b.blocks), dim3(256), 0, s, a, b);
+  return launch_status("reduce_slabs2");
+}
+
 // NOTE: may overwrite part (every caller passes its own partial-slab scratch)
 int reduce_slabs(const float* part, int splits, int64_t n, float* dst, int accumulate, hipStream_t s) {
   const bool v4 = (n % 4 == 0) && ((uintptr_t)part % 16 == 0) && ((uintptr_t)dst % 16 == 0);
@@ -613,7 +697,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_x6_kernel(WgradArgs g) {
   const int ap = pa ? 8 * (tid / (2 * BM)) + 4 * (tid & 1) : (tid / BM) * EA;
   const int bn = pb ? (tid >> 1) % BN : tid % BN;
   const int bp = pb ? 8 * (tid / (2 * BN)) + 4 * (tid & 1) : (tid / BN) * EB;
-  const bool do_bias = g.part_bias != nullptr && n0 == 0;
+  const bool do_bias = g.part_bias != nullptr && n0 == 0 && rm.batch == g.bias_xi;
   // a_up2 (transposed-conv weight gradient): the tile's (i, j) tap of the 2x2 output block
   int a_dr = 0, a_ds = 0, a_c0 = m0;
   if (g.a_up2) { const int ij = m0 / g.Ca; a_dr = ij >> 1; a_ds = ij & 1; a_c0 = m0 - ij * g.Ca; }
@@ -753,7 +837,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_h3_kernel(WgradArgs g) {
   const int p_end = min(g.P, p_begin + g.pix_per_split);
   const int am = tid / TPA, ap = (tid % TPA) * EA;
   const int bn = tid / TPB, bp = (tid % TPB) * EB;
-  const bool do_bias = g.part_bias != nullptr && n0 == 0;
+  const bool do_bias = g.part_bias != nullptr && n0 == 0 && rm.batch == g.bias_xi;
   int a_dr = 0, a_ds = 0, a_c0 = m0;
   if (g.a_up2) { const int ij = m0 / g.Ca; a_dr = ij >> 1; a_ds = ij & 1; a_c0 = m0 - ij * g.Ca; }
   const int HW = g.H * g.W;
@@ -963,7 +1047,9 @@ __global__ __launch_bounds__(256, 2) void wgrad_h3t_kernel(WgradArgs g) {
     up_ij = col / g.Ca;
     ga = g.a + (col - up_ij * g.Ca);
   }
-  const bool do_bias = UP2 && g.part_bias != nullptr && n0 == 0;
+  // bias partials = column sums of A over the block's pixels: the transposed conv's dy (UP2), or the
+  // Winograd weight gradient's E plane xi = bias_xi (E[7] = (1/3)^2 x the 4x4 tile's dz sum)
+  const bool do_bias = g.part_bias != nullptr && n0 == 0 && rm.batch == g.bias_xi;
   f32x4 bsum = {0.f, 0.f, 0.f, 0.f};
 
   f32x4 ra[D][4], rb[D][4];
@@ -1220,7 +1306,7 @@ static int run_wgrad(const WgradArgs& base, const WgradPlan& pl, hipStream_t s, 
   if ((x6 == 2 || (x6 == 3 && cin >= 256)) && plain && pl.pps % 16 == 0 &&
       (!a.a_up2 || a.W % 8 == 0)) {
     // key 31: the row-staged kernel for plain 128 x 128 tiles (float4 rows: 16-B aligned)
-    if (tune_get(PIS_TUNE_WGRAD_T) != 0 && pl.bm == 128 && pl.bn == 128 && !a.a_up2 && !a.part_bias &&
+    if (tune_get(PIS_TUNE_WGRAD_T) != 0 && pl.bm == 128 && pl.bn == 128 && !a.a_up2 &&
         pl.pps % WT_BK == 0 && a.lda % 4 == 0 && a.ldb % 4 == 0 && a.bs_a % 4 == 0 && a.bs_b % 4 == 0 &&
         ((uintptr_t)a.a & 15) == 0 && ((uintptr_t)a.b & 15) == 0) {
       if (a.dbg)
@@ -1414,7 +1500,7 @@ __global__ __launch_bounds__(256) void wgrad_c1_row_kernel(const float* __restri
 // [split][xi][Cout][Cin], one fixed-order reduction), dW = A^T M A; the bias gradient is a
 // channel sum of dz.
 struct WinoWgradPlan {
-  bool use, fused_bias;
+  bool use, fused_bias, gemm_bias;
   int m, nxi;
   int64_t T;
   WgradPlan gemm;
@@ -1444,10 +1530,13 @@ static WinoWgradPlan wino_wgrad_plan(int B, int H, int W, int Cin, int Cout) {
   p.off_part = V + E;
   p.off_M = p.off_part + part;
   p.off_cs = p.off_M + M;
-  // bias gradient: per-block sums out of the F(3x3,4x4) dz transform, else a channel-sum pass
-  p.fused_bias = p.m == 4 && 256 % (Cout / 4) == 0;
-  const size_t cs = p.fused_bias ? (size_t)wino_dz_blocks_max(B, H, W, Cout, 4) * Cout * sizeof(float)
-                                 : colsum_ws((int64_t)B * H * W, Cout);
+  // bias gradient. F(3x3,4x4): the GEMM's blocks of plane xi = 7 sum their E rows per column
+  // (E[7] = (1/3)^2 x the tile's dz sum, w4_g4 row 1) into [split][Cout] partials, which the output
+  // transform's bias blocks reduce in fixed order (no pass, no launch of its own). Else a
+  // channel-sum pass over dz.
+  p.gemm_bias = p.m == 4 && ((int64_t)Cout * Cin) % 64 == 0;
+  p.fused_bias = false;
+  const size_t cs = p.gemm_bias ? (size_t)p.gemm.splits * Cout * sizeof(float) : colsum_ws((int64_t)B * H * W, Cout);
   p.total = p.off_cs + al(cs) + 256;
   return p;
 }
@@ -1471,32 +1560,31 @@ static int wino_wgrad(const float* x, int ldx, const float* dz, int ldz, float* 
   int rc = 0;
   if (keep_v && p.m == 4) V = const_cast<float*>(keep_v);  // the forward's transform of x
   else rc = launch_wino_input(x, ldx, B, H, W, Cin, V, s, p.m);
-  float* bpart = (db && p.fused_bias) ? (float*)(base + p.off_cs) : nullptr;
-  if (!rc && !e_ready) rc = launch_wino_dz(dz, ldz, B, H, W, Cout, E, s, p.m, bpart);
+  if (!rc && !e_ready) rc = launch_wino_dz(dz, ldz, B, H, W, Cout, E, s, p.m, nullptr);
   if (rc) return rc;
+  float* gbias = (db && p.gemm_bias) ? (float*)(base + p.off_cs) : nullptr;
   WgradArgs a{};
   a.a = E; a.lda = Cout; a.a_up2 = 0; a.Ca = Cout;
   a.b = V; a.ldb = Cin; a.b_mode = B_PLAIN; a.Cb = Cin;
   a.B = 1; a.H = 1; a.W = (int)p.T; a.P = (int)p.T; a.Mp = Cout; a.Np = Cin;
-  a.part = part; a.part_bias = nullptr;
+  a.part = part; a.part_bias = gbias; a.bias_xi = WINO4_BIAS_XI;
   a.bs_a = p.T * Cout; a.bs_b = p.T * Cin; a.bs_part = (int64_t)Cout * Cin;
   a.split_stride = (int64_t)p.nxi * Cout * Cin;
   const double flop = 2.0 * p.nxi * (double)p.T * Cout * Cin;
   launch_hook("wino_wgrad_gemm", 0, s, flop);
   rc = run_wgrad(a, p.gemm, s, p.nxi);
   launch_hook("wino_wgrad_gemm", 1, s, flop);
-  // few slabs over many weights: the output transform sums them itself (no reduced copy of the
-  // 36 planes); many slabs over few weights keep the parallel slab reduction
-  if (p.m == 4 && p.gemm.splits <= 8 && (int64_t)Cout * Cin >= 65536) {
-    if (!rc) rc = launch_wino_wgrad_out(part, Cout, Cin, dw, acc, s, p.m, p.gemm.splits, a.split_stride);
+  // up to 16 split slabs: the output transform sums them itself (no reduced copy of the 36 planes:
+  // the separate slab reduction of a 14-slab 128 x 256 layer read 66 MB at 0.8 TB/s); many slabs
+  // keep the parallel slab reduction
+  const WgradOutBias bf{gbias, gbias ? p.gemm.splits : 0, db, WINO4_BIAS_SCALE};
+  if (p.m == 4 && p.gemm.splits <= 16) {
+    if (!rc) rc = launch_wino_wgrad_out(part, Cout, Cin, dw, acc, s, p.m, p.gemm.splits, a.split_stride, bf);
   } else {
     if (!rc) rc = reduce_slabs_pitched(part, p.gemm.splits, a.split_stride, a.split_stride, M, 0, s);
-    if (!rc) rc = launch_wino_wgrad_out(M, Cout, Cin, dw, acc, s, p.m);
+    if (!rc) rc = launch_wino_wgrad_out(M, Cout, Cin, dw, acc, s, p.m, 1, 0, bf);
   }
-  if (!rc && db) {
-    if (bpart) rc = reduce_slabs(bpart, wino_dz_blocks(B, H, W, Cout, 4), Cout, db, acc, s);
-    else rc = colsum(dz, ldz, (int64_t)B * H * W, Cout, db, acc, base + p.off_cs, p.total - p.off_cs, s);
-  }
+  if (!rc && db && !gbias) rc = colsum(dz, ldz, (int64_t)B * H * W, Cout, db, acc, base + p.off_cs, p.total - p.off_cs, s);
   return rc;
 }
 
@@ -1556,9 +1644,9 @@ extern "C" int pis_conv3x3_bwd_prep(const float* dz, int ldz, int B, int H, int 
   float* V = wino_v_slot(ws_dgrad, Cout, Cin);
   char* base = (char*)ws_wgrad;
   float* E = (float*)(base + wp.off_E);
-  float* bpart = wp.fused_bias ? (float*)(base + wp.off_cs) : nullptr;
   float* tmax = wino_fused_h3_planned(B, H, W, Cout, Cin) ? wino_tmax_slot(ws_dgrad, B, H, W, Cout, Cin) : nullptr;
-  const int rc = launch_wino_dz2(dz, ldz, B, H, W, Cout, V, E, bpart, (hipStream_t)stream, tmax);
+  // (no bias partials: the weight gradient's GEMM sums them from E, wino_wgrad_plan gemm_bias)
+  const int rc = launch_wino_dz2(dz, ldz, B, H, W, Cout, V, E, nullptr, (hipStream_t)stream, tmax);
   // the dgrad_ex that consumes this V checks that it decides the same tile-maxima format
   if (!rc) wino_prep_record(ws_dgrad, B, H, W, Cout, Cin, tmax != nullptr);
   return rc ? rc : 1;
@@ -1608,9 +1696,9 @@ extern "C" int pis_conv3x3_wgrad(const float* x, int ldx, const float* dz, int l
       hipLaunchKernelGGL((wgrad3x3_halo_kernel<1>), dim3(tiles * hp.splits), dim3(256), 0, s, a);
     launch_hook("wgrad3x3_halo", 1, s, flop);
     int rc = launch_status("wgrad3x3_halo");
-    if (!rc) rc = reduce_slabs(a.part, hp.splits, (int64_t)Cout * 9 * Cin, dw_krsc, acc, s);
-    if (rc || !db) return rc;
-    return reduce_slabs(a.part_bias, hp.splits, Cout, db, acc, s);
+    if (!rc) rc = reduce_slabs2(a.part, hp.splits, (int64_t)Cout * 9 * Cin, dw_krsc, a.part_bias, hp.splits, Cout, db,
+                                acc, s);
+    return rc;
   }
   if (Cin == 1 && tune_get(PIS_TUNE_C1_WGRAD) == 0) {
     PIS_CHECK_ARG(Cout <= 1024 && Cout % 4 == 0, "pis_conv3x3_wgrad: Cin == 1 needs Cout % 4 == 0, <= 1024");
@@ -1631,8 +1719,7 @@ extern "C" int pis_conv3x3_wgrad(const float* x, int ldx, const float* dz, int l
                          part, part_b);
     int rc = launch_status("wgrad_c1");
     const int nslab = row ? C1_BLOCKS : blocks;
-    if (!rc) rc = reduce_slabs(part, nslab, (int64_t)9 * Cout, dw_krsc, acc, s);
-    if (!rc && db) rc = reduce_slabs(part_b, nslab, Cout, db, acc, s);
+    if (!rc) rc = reduce_slabs2(part, nslab, (int64_t)9 * Cout, dw_krsc, db ? part_b : nullptr, nslab, Cout, db, acc, s);
     return rc;
   }
   const WgradPlan pl = conv_plan(B, H, W, Cin, Cout);
@@ -1653,7 +1740,7 @@ extern "C" int pis_conv3x3_wgrad(const float* x, int ldx, const float* dz, int l
       rc = launch_status("compact_c1");
     }
   } else {
-    rc = reduce_slabs(a.part, pl.splits, (int64_t)a.Mp * a.Np, dw_krsc, acc, s);
+    return reduce_slabs2(a.part, pl.splits, (int64_t)a.Mp * a.Np, dw_krsc, a.part_bias, pl.splits, Cout, db, acc, s);
   }
   if (rc || !db) return rc;
   return reduce_slabs(a.part_bias, pl.splits, Cout, db, acc, s);
@@ -1701,9 +1788,10 @@ extern "C" int pis_convt2x2_wgrad(const float* x, int ldx, const float* dy, int 
     else
       hipLaunchKernelGGL((wgrad_h3t_kernel<true, 2>), dim3(tiles * pl.splits), dim3(256), 0, s, a);
     int rc = launch_status("wgrad_h3t<up2>");
-    if (!rc) rc = reduce_slabs(a.part, pl.splits, (int64_t)a.Mp * a.Np, dw_ijoc, acc, s);
-    if (rc || !db) return rc;
-    return reduce_slabs(a.part_bias, pl.splits * 4, Cout, db, acc, s);
+    // weights + bias (slabs [split][i][j][o]: 4 splits slabs of Cout) in one launch
+    if (!rc) rc = reduce_slabs2(a.part, pl.splits, (int64_t)a.Mp * a.Np, dw_ijoc, a.part_bias, pl.splits * 4, Cout, db,
+                                acc, s);
+    return rc;
   }
   const WgradPlan pl = plan_wgrad(4 * Cout, Cin, P, Cout, Cin);
   WgradArgs a{};
@@ -1712,8 +1800,8 @@ extern "C" int pis_convt2x2_wgrad(const float* x, int ldx, const float* dy, int 
   a.B = B; a.H = H; a.W = W; a.P = P; a.Mp = 4 * Cout; a.Np = Cin; a.part = (float*)ws;
   a.part_bias = db ? bias_slabs(ws, pl) : nullptr;
   int rc = run_wgrad(a, pl, s);
-  if (!rc) rc = reduce_slabs(a.part, pl.splits, (int64_t)a.Mp * a.Np, dw_ijoc, acc, s);
-  if (rc || !db) return rc;
-  // bias slabs are [split][i][j][o]: 4*splits slabs of Cout
-  return reduce_slabs(a.part_bias, pl.splits * 4, Cout, db, acc, s);
+  // weights + bias (slabs [split][i][j][o]: 4 splits slabs of Cout) in one launch
+  if (!rc) rc = reduce_slabs2(a.part, pl.splits, (int64_t)a.Mp * a.Np, dw_ijoc, a.part_bias, pl.splits * 4, Cout, db,
+                              acc, s);
+  return rc;
 }

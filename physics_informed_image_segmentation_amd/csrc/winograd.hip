@@ -810,12 +810,33 @@ __global__ __launch_bounds__(256) void wino4_wgrad_out_kernel(const float* __res
 // thread, 4 slabs per unrolled step so 36 loads are in flight, into LDS; pass 2 runs the output
 // transform with 3 threads per entry (one row i of the 3 x 3 each). Same sums in the same order as
 // wino4_wgrad_out_kernel: bitwise equal.
+// The first nb blocks are the bias gradient's (WgradOutBias): 256 channels each, every thread one
+// channel summed over the partial rows in order, so the weight gradient's bias costs no launch.
 __global__ __launch_bounds__(256) void wino4_wgrad_out_tiled_kernel(const float* __restrict__ M, int N, int C,
                                                                     float* __restrict__ dw, int accumulate,
-                                                                    int nsplit, int64_t sstride) {
+                                                                    int nsplit, int64_t sstride, WgradOutBias bias,
+                                                                    int nb) {
+  if ((int)blockIdx.x < nb) {
+    const int n = blockIdx.x * 256 + threadIdx.x;
+    if (n < N) {
+      const float* pp = bias.part + n;
+      float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;  // four chains, combined in a fixed order
+      int r = 0;
+      for (; r + 3 < bias.rows; r += 4) {
+        s0 += pp[(size_t)r * N];
+        s1 += pp[(size_t)(r + 1) * N];
+        s2 += pp[(size_t)(r + 2) * N];
+        s3 += pp[(size_t)(r + 3) * N];
+      }
+      for (; r < bias.rows; ++r) s0 += pp[(size_t)r * N];
+      const float v = ((s0 + s1) + (s2 + s3)) * bias.scale;
+      bias.db[n] = accumulate ? bias.db[n] + v : v;
+    }
+    return;
+  }
   __shared__ float sm[36][65];
   const int64_t NC = (int64_t)N * C;
-  const int64_t e0 = (int64_t)blockIdx.x * 64;
+  const int64_t e0 = (int64_t)(blockIdx.x - nb) * 64;
   const int tid = threadIdx.x, el = tid & 63, xg = tid >> 6;  // entry e0 + el, xi = xg + 4 q
   {
     const float* src[9];
@@ -2178,11 +2199,14 @@ bool wino_fused_h3_planned(int B, int H, int W, int C, int N) {
 }
 
 int launch_wino_wgrad_out(const float* M, int N, int C, float* dw, int accumulate, hipStream_t s, int m,
-                          int nsplit, int64_t sstride) {
-  if (m == 4 && ((int64_t)N * C) % 64 == 0)
-    hipLaunchKernelGGL(wino4_wgrad_out_tiled_kernel, dim3((unsigned)((int64_t)N * C / 64)), dim3(256), 0, s, M, N, C,
-                       dw, accumulate, nsplit, sstride);
-  else if (m == 4)
+                          int nsplit, int64_t sstride, WgradOutBias bias) {
+  if (bias.rows > 0 && !(m == 4 && ((int64_t)N * C) % 64 == 0))
+    return set_error("wino_wgrad_out: the folded bias needs the tiled F(3x3,4x4) transform"), PIS_ERR_ARG;
+  if (m == 4 && ((int64_t)N * C) % 64 == 0) {
+    const int nb = bias.rows > 0 ? (N + 255) / 256 : 0;
+    hipLaunchKernelGGL(wino4_wgrad_out_tiled_kernel, dim3((unsigned)((int64_t)N * C / 64 + nb)), dim3(256), 0, s, M,
+                       N, C, dw, accumulate, nsplit, sstride, bias, nb);
+  } else if (m == 4)
     hipLaunchKernelGGL(wino4_wgrad_out_kernel, dim3(grid_of((int64_t)N * C)), dim3(256), 0, s, M, N, C, dw,
                        accumulate, nsplit, sstride);
   else if (nsplit == 1)

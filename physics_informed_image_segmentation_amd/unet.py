@@ -363,9 +363,9 @@ class UNetEngine:
     # at the forward's start: 12 small main-stream launches fewer, six of them in the backward.
     # Measured neutral on the C2 step (344.2 vs 344.0 img/s, profiles/r3_q25_ab_env.txt).
     filter_ahead = os.environ.get("PIS_FILTER_AHEAD", "0")
-    # "1": every direct-kernel layer's weight gradient on the main stream right after its input
-    # gradient (see _backward); "0": on the weight-gradient stream
-    direct_wgrad_main = os.environ.get("PIS_DIRECT_WGRAD_MAIN", "0")
+    # "1" (default): every direct-kernel layer's weight gradient on the main stream right after its
+    # input gradient (see the backward); "0": on the weight-gradient stream
+    direct_wgrad_main = os.environ.get("PIS_DIRECT_WGRAD_MAIN", "1")
 
     def __init__(self, model: UNet):
         self.m = model
@@ -803,15 +803,21 @@ class UNetEngine:
 
             sync = self.side_sync if (prep and dx is not None and side is not main) else "prep"
             if (self.direct_wgrad_main == "1" and not prep and dx is not None and side is not main
-                    and m.grad_ready_hook is None
                     and lib.pis_conv3x3_dgrad_direct(B, Hl, Wl, conv.in_channels, conv.out_channels, dz.ld, wsb)
                     and lib.pis_conv3x3_wgrad_ws(B, Hl, Wl, conv.in_channels, conv.out_channels) <= wsb):
                 # a direct layer's weight gradient on the main stream right after its input gradient,
                 # in the main workspace: the two MFMA-bound kernels in sequence instead of the weight
-                # gradient's one-wave-per-SIMD blocks locking every CU under the main stream's work
+                # gradient's one-wave-per-SIMD blocks (497 registers per lane) locking every CU under
+                # the main stream's work. Step-neutral (22.37 vs 22.38 ms, profiles/r5_c_*), but each
+                # direct kernel then runs at its own rate: the weight gradient 0.23 -> 0.41 of the
+                # fp16x3 pipe live, the input gradient 0.35 -> 0.44, the convT input gradients 2.07 ->
+                # 1.41 ms per step
                 dgrad()
                 call("pis_conv3x3_wgrad_keep", x.p, x.ld, dz.p, dz.ld, self._gptr(conv.weight),
                      self._gptr(conv.bias), B, Hl, Wl, conv.in_channels, conv.out_channels, acc, ws, wsb, 0, st)
+                if m.grad_ready_hook is not None:  # DDP: the bucket's all-reduce runs from the side
+                    to_side()                      # stream, which now waits for this weight gradient
+                    ready_on_side(conv.weight, conv.bias)
                 return
             if sync == "prep":  # the weight gradient starts as soon as dz's transforms exist
                 to_side()
