@@ -763,6 +763,15 @@ __global__ __launch_bounds__(NT) void head_loss_fwd_kernel(HeadLossFwdArgs h) {
   const float* xb = h.x + (size_t)b * HW * h.ldx + 4 * sub;
   const f32x4 wv = *reinterpret_cast<const f32x4*>(h.w + 4 * sub);
   const float bias = h.bias[0];
+  // the loss pass's first target item of this thread (row 1 + ry, column item q), loaded now so
+  // its HBM latency hides under the head pass instead of following the barrier (at C2 every
+  // thread has exactly this one item)
+  const int W4 = W >> 2, TX = min(W4, NT), RY = NT / TX;
+  const int q = tid % TX, ry = tid / TX;
+  const float* tt = h.a.g.t + (size_t)b * HW;
+  const bool tpre_ok = ry < RY && q < W4 && 1 + ry <= nr;
+  f32x4 tpre = {0.f, 0.f, 0.f, 0.f};
+  if (tpre_ok) tpre = *reinterpret_cast<const f32x4*>(tt + (size_t)(y0 + ry) * W + 4 * q);
   // 1. u of the staged rows: a chunk is NG PP consecutive pixels of one staged row (W % (NG PP) == 0),
   // PP per 16-lane group; two register sets, so the next chunk's loads are in flight while this
   // one's sums run
@@ -821,11 +830,7 @@ __global__ __launch_bounds__(NT) void head_loss_fwd_kernel(HeadLossFwdArgs h) {
       if (ch + 1 < nchunk) head(xn, ch + 1);
     }
   }
-  // the targets of this thread's items in flight across the barriers (TX threads per row, RY rows
-  // per pass; item = 4 pixels)
-  const int W4 = W >> 2, TX = min(W4, NT), RY = NT / TX;
-  const int q = tid % TX, ry = tid / TX;
-  const float* tt = g.t + (size_t)b * HW;
+  // loss pass: TX threads per row, RY rows per pass; item = 4 pixels
   __syncthreads();
   if (ST) {  // reflect halo columns: column -1 is column 1, column W is column W-2
     for (int r = tid; r < nr + 2; r += NT) {
@@ -841,7 +846,8 @@ __global__ __launch_bounds__(NT) void head_loss_fwd_kernel(HeadLossFwdArgs h) {
   // W4 > NT (W > 4 NT, e.g. W = 1280 at 256 threads): a thread walks every TX-th item of its rows
   for (int xq = q; ry < RY && xq < W4; xq += TX) {
     for (int r = 1 + ry; r <= nr; r += RY) {
-      const f32x4 tv = *reinterpret_cast<const f32x4*>(tt + (size_t)(y0 - 1 + r) * W + 4 * xq);
+      const f32x4 tv = (xq == q && r == 1 + ry) ? tpre  // prefetched at the kernel's start
+                                                : *reinterpret_cast<const f32x4*>(tt + (size_t)(y0 - 1 + r) * W + 4 * xq);
       const float* sc = su + r * SW + 4 + 4 * xq;
       const f32x4 pv = *reinterpret_cast<const f32x4*>(sc);
       f32x4 uv = pv, dv = pv;
