@@ -191,12 +191,6 @@ int pis_tune(int key, int value);
  * 5-12 need K % 32 == 0. */
 int pis_debug_gemm_nt(const float* A, const float* B, float* C, int M, int N, int K, int batch, int variant,
                       pis_stream_t stream);
-/* Tooling (tools/bench_gemm.py variant 20): the batched NT GEMM on pre-split fp16x3 operands
- * (csrc/gemm_h2p.hip): with split = 1, A's and B's rows are first split into hi / lo fp16 planes
- * with one power-of-two scale per row (into ws); split = 0 reuses the planes of the last call, so
- * only the GEMM is timed. M, N % 128 == 0, K % 32 == 0; ws >= 4 (M + N) K batch + 4 (M + N) batch + 64. */
-int pis_debug_gemm_h2p(const float* A, const float* B, float* C, int M, int N, int K, int batch, void* ws,
-                       size_t ws_bytes, int split, pis_stream_t stream);
 /* Tooling (bench.py roofline_loss): one float4 grid-stride launch over n floats of a and b — dst = a + b
  * when dst is given (12 B per element), else a read reduced to one partial per block (8 B per element):
  * the floor any kernel moving the loss's bytes meets at the same size and cache state. */

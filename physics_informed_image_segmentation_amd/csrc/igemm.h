@@ -73,17 +73,6 @@ int launch_wino_dz(const float* dz, int ldz, int B, int H, int W, int N, float* 
 int wino_dz_blocks(int B, int H, int W, int N, int m);
 int wino_dz_blocks_max(int B, int H, int W, int N, int m);  // over pis_tune key 40
 // M: nsplit split-K slabs sstride floats apart, summed in slab order (nsplit > 1 needs m == 4)
-// pre-split fp16x3 batched NT GEMM (gemm_h2p.hip): C = ia[m] ib[n] sum_k (Ah Bh + Ah Bl + Al Bh)
-struct H2pArgs {
-  const _Float16 *ah, *al, *bh, *bl;  // [batch][rows][K] hi / lo planes of the scaled rows
-  const float *ia, *ib;               // [batch][rows] inverse row scales
-  float* c;                           // [batch][M][N]
-  int M, N, K;
-  int64_t bsa, bsb, bsc, bsia, bsib;  // batch strides (elements)
-};
-int launch_gemm_h2p(const H2pArgs& g, int batch, hipStream_t s);
-int launch_split_rows_h2(const float* X, int64_t nrows, int K, _Float16* hi, _Float16* lo, float* inv, hipStream_t s);
-
 // The F(3x3,4x4) weight gradient's bias gradient, folded into its output-transform launch:
 // db[n] (+)= scale x sum_{r < rows} part[r][n] (fixed order), part = the GEMM's [split][N] column
 // sums of E plane WINO4_BIAS_XI; rows == 0: none

@@ -5,9 +5,7 @@ C[xi] (T x N) = V[xi] (T x C) . U[xi]^T, T = 8 H W / 16 tiles.
 
     python tools/bench_gemm.py [--variants 0,1,2,3] [--rounds 3] [--check]
 
-variants: see pis_debug_gemm_nt in include/pis_capi.h; 20 = the pre-split fp16x3 GEMM
-(pis_debug_gemm_h2p: operands split by rows once, untimed, then only the GEMM timed). TF/s are
-fp32-equivalent.
+variants: see pis_debug_gemm_nt in include/pis_capi.h. TF/s are fp32-equivalent.
 """
 import argparse
 import os
@@ -53,28 +51,18 @@ def main():
             Bm *= 1e4
         Cm = torch.empty(36, T, N, device="cuda")
         bptr = {}
-        h2ws = None
-        if 20 in variants:
-            nb = 4 * (T + N) * C * 36 + 4 * 36 * (T + N) + 64
-            h2ws = torch.empty(nb // 4 + 1, device="cuda")
-
-        def call(v, first=False):
-            if v == 20:
-                return lib.pis_debug_gemm_h2p(A.data_ptr(), Bm.data_ptr(), Cm.data_ptr(), T, N, C, 36, h2ws.data_ptr(),
-                                              h2ws.numel() * 4, 1 if first else 0, s)
-            return lib.pis_debug_gemm_nt(A.data_ptr(), bptr.get(v, Bm.data_ptr()), Cm.data_ptr(), T, N, C, 36, v, s)
         flop = 2.0 * 36 * T * N * C
         res = {}
         for _ in range(args.rounds):
             for v in variants:
-                rc = call(v, True)
+                rc = lib.pis_debug_gemm_nt(A.data_ptr(), bptr.get(v, Bm.data_ptr()), Cm.data_ptr(), T, N, C, 36, v, s)
                 if rc != 0:  # shape not covered by this variant
                     res.setdefault(v, []).append(float("inf"))
                     continue
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
                 for _ in range(args.reps):
-                    call(v)
+                    lib.pis_debug_gemm_nt(A.data_ptr(), bptr.get(v, Bm.data_ptr()), Cm.data_ptr(), T, N, C, 36, v, s)
                 e1.record()
                 torch.cuda.synchronize()
                 res.setdefault(v, []).append(e0.elapsed_time(e1) / args.reps)
@@ -88,7 +76,7 @@ def main():
             for v in variants:
                 if v in (1, 2, 9, 13, 14) or min(res[v]) == float("inf"):
                     continue
-                call(v, True)
+                lib.pis_debug_gemm_nt(A.data_ptr(), bptr.get(v, Bm.data_ptr()), Cm.data_ptr(), T, N, C, 36, v, s)
                 torch.cuda.synchronize()
                 err = ((Cm[:2].double() - ref).norm() / ref.norm()).item()
                 print(f"    v{v} rel err {err:.2e}", flush=True)
