@@ -1,6 +1,6 @@
-"""Data-parallel path on CPU (gloo, world_size 2): bucket planning over the
-gradient arena, the backward-order launch protocol of GradBucketer, the
-summed result, the metric all-reduce and the parameter broadcast."""
+"""Data-parallel path on CPU (gloo, world_size 2 and 8 — C3's rank count): bucket planning over
+the gradient arena, the backward-order launch protocol of GradBucketer, the summed result, the
+metric all-reduce and the parameter broadcast."""
 import os
 import socket
 
@@ -87,17 +87,18 @@ def _worker(rank, world, port, q):
         progressive = 0 < launched_trace[len(m.entries) // 2] < len(bk.buckets)
         t = torch.tensor([1.0 * rank, 2.0, 3.0], dtype=torch.float64)
         allreduce_scalars(t)
-        ok_metrics = t.tolist() == [1.0, 4.0, 6.0]
+        ok_metrics = t.tolist() == [float(sum(range(world))), 2.0 * world, 3.0 * world]
         q.put((rank, ok and ok_bcast and ok_metrics, progressive, len(bk.buckets)))
     finally:
         dist.destroy_process_group()
 
 
-def test_gloo_world2_bucketed_allreduce():
+@pytest.mark.parametrize("world", [2, 8])
+def test_gloo_bucketed_allreduce(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=120) for _ in procs]
