@@ -179,11 +179,7 @@ int pis_version(void);
                                       ReLU-mask rows loaded with its M values (one memory round trip per tile,
                                       151 VGPRs); 0 in the epilogue. Step 22.25 -> 22.04 ms on one box, 22.43 ->
                                       22.39 on another (profiles/r4_t_ab_wino_out_mpf.txt, r4_u_*): 0.2-0.9 % */
-#define PIS_TUNE_HEAD_LOSS_HALO 47 /* pis_head_loss_fwd: 0 (default) each row band stages only its own rows and
-                                       the RD / PF terms of the rows next to a band boundary run in a small
-                                       second kernel over u (head_loss_bnd_kernel); 1 the round-4 form, two
-                                       halo rows per band recomputed from the 64-channel head input */
-#define PIS_TUNE_NKEYS 48
+#define PIS_TUNE_NKEYS 47
 #define PIS_DEBUG_NOLOAD (1 << 16)
 int pis_tune(int key, int value);
 /* Tooling (tools/bench_gemm.py): time one batched NT GEMM kernel variant in isolation,

@@ -284,7 +284,6 @@ struct LossRowArgs {
   LossArgs g;
   int rows;             // image rows per block
   int bands;            // blocks per sample
-  int fextra;           // fpart rows after the B x bands block rows (head_loss_bnd_kernel's), 0: none
   float* terms;
   int* counts;
   float* scores;
@@ -463,12 +462,11 @@ __global__ __launch_bounds__(256) void loss_finalize_rows_kernel(LossRowArgs a) 
   __shared__ int si[LOSS_MAX_BLOCKS * 3];
   float v[PB][6];
   int vi[PI];
-  const int nfrow = nblk + a.fextra;
 #pragma unroll
   for (int i = 0; i < PB; ++i) {
     const int k = tid + 256 * i;
 #pragma unroll
-    for (int j = 0; j < 6; ++j) v[i][j] = k < nfrow ? g.fpart[k * 6 + j] : 0.f;
+    for (int j = 0; j < 6; ++j) v[i][j] = k < nblk ? g.fpart[k * 6 + j] : 0.f;
   }
 #pragma unroll
   for (int i = 0; i < PI; ++i) {
@@ -745,17 +743,11 @@ struct HeadLossFwdArgs {
 // NT threads per block (NG = NT / 16 pixel groups): 1024 at W % 512 == 0 (C2: 256 blocks of 16
 // waves, four waves per SIMD to cover the HBM latency; one staged row per chunk), else 256
 // D3 (pis_tune key 38 = 2): three register sets, so two chunks' loads are in flight while one is summed
-// HALO = false (no halo rows): the block stages only its own R rows; the RD / PF terms of a row
-// whose vertical neighbour lies in another band (the band's first and last rows, unless the image
-// edge reflects back into the band) are left to head_loss_bnd_kernel, which reads u of the rows
-// around each band boundary back from HBM. HALO = true: the round-4 form (two halo rows per band
-// recomputed from their 256 B/px of x).
-template <bool RD, bool PF, int PP, int NT = 256, bool D3 = false, bool HALO = true>
+template <bool RD, bool PF, int PP, int NT = 256, bool D3 = false>
 __global__ __launch_bounds__(NT) void head_loss_fwd_kernel(HeadLossFwdArgs h) {
   constexpr int NG = NT / 16, NWV = NT / 64;
   constexpr bool ST = RD || PF;
-  constexpr int HR = HALO ? 1 : 0;  // staged row of image row y0
-  extern __shared__ __attribute__((aligned(16))) float su[];  // [R + 2 HR][SW]: image column c at c + 4
+  extern __shared__ __attribute__((aligned(16))) float su[];  // [R + 2][SW]: image column c at c + 4
   const LossArgs& g = h.a.g;
   const int H = g.H, W = g.W, SW = W + 8;
   // XCD-grouped (consecutive bands of a sample on one XCD, xcd_remap2) and alternating walk
@@ -765,7 +757,7 @@ __global__ __launch_bounds__(NT) void head_loss_fwd_kernel(HeadLossFwdArgs h) {
   const Remap2 rmp = xcd_remap2();
   const int band = rmp.bid, b = rmp.batch;
   const int y0 = band * h.R, nr = min(h.R, H - y0);
-  const bool rev = HALO && (band & 1) == 0;
+  const bool rev = (band & 1) == 0;
   const int tid = threadIdx.x, sub = tid & 15, grp = tid >> 4;
   const size_t HW = (size_t)H * W;
   const float* xb = h.x + (size_t)b * HW * h.ldx + 4 * sub;
@@ -777,26 +769,26 @@ __global__ __launch_bounds__(NT) void head_loss_fwd_kernel(HeadLossFwdArgs h) {
   const int W4 = W >> 2, TX = min(W4, NT), RY = NT / TX;
   const int q = tid % TX, ry = tid / TX;
   const float* tt = h.a.g.t + (size_t)b * HW;
-  const bool tpre_ok = ry < RY && q < W4 && ry < nr;
+  const bool tpre_ok = ry < RY && q < W4 && 1 + ry <= nr;
   f32x4 tpre = {0.f, 0.f, 0.f, 0.f};
   if (tpre_ok) tpre = *reinterpret_cast<const f32x4*>(tt + (size_t)(y0 + ry) * W + 4 * q);
   // 1. u of the staged rows: a chunk is NG PP consecutive pixels of one staged row (W % (NG PP) == 0),
   // PP per 16-lane group; two register sets, so the next chunk's loads are in flight while this
   // one's sums run
-  const int cpr = W / (NG * PP), nchunk = (nr + 2 * HR) * cpr;
+  const int cpr = W / (NG * PP), nchunk = (nr + 2) * cpr;
   f32x4 xa[PP], xn[PP];
   auto srow = [&](int ch) { const int r = ch / cpr; return rev ? nr + 1 - r : r; };  // staged row of chunk ch
   auto load = [&](f32x4 (&xv)[PP], int ch) __attribute__((always_inline)) {
     const int r = srow(ch), x0 = (ch - (ch / cpr) * cpr) * (NG * PP) + grp;  // block-uniform r
-    const int gy = clampi(refl(y0 - HR + r, H), 0, H - 1);
+    const int gy = clampi(refl(y0 - 1 + r, H), 0, H - 1);
     const float* row = xb + (size_t)gy * W * h.ldx;
 #pragma unroll
     for (int j = 0; j < PP; ++j) xv[j] = *reinterpret_cast<const f32x4*>(row + (size_t)(x0 + NG * j) * h.ldx);
   };
   auto head = [&](const f32x4 (&xv)[PP], int ch) __attribute__((always_inline)) {
     const int r = srow(ch), x0 = (ch - (ch / cpr) * cpr) * (NG * PP) + grp;
-    const bool interior = !HALO || (r >= 1 && r <= nr);
-    const size_t orow = (size_t)b * HW + (size_t)(y0 - HR + r) * W;
+    const bool interior = r >= 1 && r <= nr;
+    const size_t orow = (size_t)b * HW + (size_t)(y0 - 1 + r) * W;
 #pragma unroll
     for (int j = 0; j < PP; ++j) {
       float s = 0.f;
@@ -841,38 +833,28 @@ __global__ __launch_bounds__(NT) void head_loss_fwd_kernel(HeadLossFwdArgs h) {
   // loss pass: TX threads per row, RY rows per pass; item = 4 pixels
   __syncthreads();
   if (ST) {  // reflect halo columns: column -1 is column 1, column W is column W-2
-    for (int r = tid; r < nr + 2 * HR; r += NT) {
+    for (int r = tid; r < nr + 2; r += NT) {
       su[r * SW + 3] = su[r * SW + 5];
       su[r * SW + 4 + W] = su[r * SW + 2 + W];
     }
     __syncthreads();
   }
-  // 2. the loss partials of rows y0 .. y0 + nr - 1 (staged rows HR .. nr - 1 + HR), as loss_fwd_kernel
+  // 2. the loss partials of rows y0 .. y0 + nr - 1 (staged rows 1 .. nr), as loss_fwd_kernel
   constexpr float kLn2 = 0.69314718055994531f, kClamp2 = -144.26950408889634f;  // -100 / ln 2
   float s_it = 0.f, s_p = 0.f, s_t = 0.f, s_bce2 = 0.f, s_rd = 0.f, s_g2 = 0.f, s_q2 = 0.f;
   int c_i = 0, c_p = 0, c_t = 0;
   // W4 > NT (W > 4 NT, e.g. W = 1280 at 256 threads): a thread walks every TX-th item of its rows
   for (int xq = q; ry < RY && xq < W4; xq += TX) {
-    for (int r = HR + ry; r < nr + HR; r += RY) {
-      const int y = y0 + r - HR;
-      const f32x4 tv = (xq == q && r == HR + ry) ? tpre  // prefetched at the kernel's start
-                                                 : *reinterpret_cast<const f32x4*>(tt + (size_t)y * W + 4 * xq);
+    for (int r = 1 + ry; r <= nr; r += RY) {
+      const f32x4 tv = (xq == q && r == 1 + ry) ? tpre  // prefetched at the kernel's start
+                                                : *reinterpret_cast<const f32x4*>(tt + (size_t)(y0 - 1 + r) * W + 4 * xq);
       const float* sc = su + r * SW + 4 + 4 * xq;
       const f32x4 pv = *reinterpret_cast<const f32x4*>(sc);
       f32x4 uv = pv, dv = pv;
       float lft = 0.f, rgt = 0.f;
-      // the row's vertical neighbours (reflect at the image edges) inside this band's staged rows?
-      // (always with halo rows; else the band's edge rows go to head_loss_bnd_kernel)
-      int ru = r - 1, rdn = r + 1;
-      bool inb = true;
-      if (!HALO) {
-        ru = (y == 0 ? 1 : y - 1) - y0;
-        rdn = (y == H - 1 ? H - 2 : y + 1) - y0;
-        inb = ru >= 0 && ru < nr && rdn >= 0 && rdn < nr;
-      }
-      if (ST && inb) {
-        uv = *reinterpret_cast<const f32x4*>(su + ru * SW + 4 + 4 * xq);
-        dv = *reinterpret_cast<const f32x4*>(su + rdn * SW + 4 + 4 * xq);
+      if (ST) {
+        uv = *reinterpret_cast<const f32x4*>(sc - SW);
+        dv = *reinterpret_cast<const f32x4*>(sc + SW);
         lft = sc[-1];
         rgt = sc[4];
       }
@@ -888,7 +870,7 @@ __global__ __launch_bounds__(NT) void head_loss_fwd_kernel(HeadLossFwdArgs h) {
         c_p += pb;
         c_t += tb;
         c_i += pb && tb;
-        if (ST && inb) {
+        if (ST) {
           const float ul = i == 0 ? lft : pv[i - 1], ur = i == 3 ? rgt : pv[i + 1];
           const float uu = uv[i], ud = dv[i];
           const float qq = fmaf(-p, p, p);  // p (1 - p)
@@ -942,60 +924,6 @@ __global__ __launch_bounds__(NT) void head_loss_fwd_kernel(HeadLossFwdArgs h) {
 #pragma unroll
     for (int w = 1; w < NWV; ++w) c += ir[3 * w + j];
     g.ipart[blk * 3 + j] = c;
-  }
-}
-
-// The RD / PF terms of the two rows on either side of each band boundary (the rows the no-halo
-// head_loss_fwd_kernel leaves out: their vertical neighbour lies in the other band), from u read
-// back from HBM (written by that kernel just before, on the same stream), with the same arithmetic
-// per pixel. Block (k, b): the boundary between bands k and k + 1 of sample b, rows y1 - 1 and y1
-// (y1 = (k + 1) R; at the image's last row the reflect resolves inside these two rows). Its sums go
-// to fpart row B bands + b (bands - 1) + k (terms 4 and 5; the finalize adds every row in order).
-template <bool RD, bool PF>
-__global__ __launch_bounds__(256) void head_loss_bnd_kernel(LossRowArgs a, int R) {
-  const LossArgs& g = a.g;
-  const int H = g.H, W = g.W, W4 = W >> 2, k = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
-  const int y1 = (k + 1) * R;
-  const float* u = g.p + (size_t)b * H * W;
-  float s_rd = 0.f, s_g2 = 0.f, s_q2 = 0.f;
-  for (int it = tid; it < 2 * W4; it += 256) {
-    const int y = y1 - 1 + it / W4, xq = it % W4;
-    const int yu = y == 0 ? 1 : y - 1, yd = y == H - 1 ? H - 2 : y + 1;
-    const float* rc = u + (size_t)y * W;
-    const f32x4 pv = *reinterpret_cast<const f32x4*>(rc + 4 * xq);
-    const f32x4 uv = *reinterpret_cast<const f32x4*>(u + (size_t)yu * W + 4 * xq);
-    const f32x4 dv = *reinterpret_cast<const f32x4*>(u + (size_t)yd * W + 4 * xq);
-    const float lft = rc[xq == 0 ? 1 : 4 * xq - 1], rgt = rc[xq == W4 - 1 ? W - 2 : 4 * xq + 4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const float p = pv[i];
-      const float ul = i == 0 ? lft : pv[i - 1], ur = i == 3 ? rgt : pv[i + 1];
-      const float uu = uv[i], ud = dv[i];
-      const float qq = fmaf(-p, p, p);  // p (1 - p)
-      if (RD) {
-        const float lap = (uu + ud) + (ul + ur) - 4.f * p;
-        const float rr = fmaf(g.D, lap, g.rx * qq * (p - g.a));
-        s_rd = fmaf(rr, rr, s_rd);
-      }
-      if (PF) {
-        const float gx = ur - ul, gy2 = ud - uu;  // 2x the central differences
-        s_g2 = fmaf(gx, gx, fmaf(gy2, gy2, s_g2));
-        s_q2 = fmaf(qq, qq, s_q2);
-      }
-    }
-  }
-  const float v4 = wave_sum(s_rd), v5 = wave_sum(0.125f * g.eps * s_g2 + s_q2 / g.eps);
-  __shared__ float red[4][2];
-  const int lane = tid & 63, wave = tid >> 6;
-  if (lane == 0) {
-    red[wave][0] = v4;
-    red[wave][1] = v5;
-  }
-  __syncthreads();
-  if (tid < 6) {
-    float v = 0.f;
-    if (tid >= 4) v = ((red[0][tid - 4] + red[1][tid - 4]) + red[2][tid - 4]) + red[3][tid - 4];
-    g.fpart[((size_t)g.B * a.bands + (size_t)b * (a.bands - 1) + k) * 6 + tid] = v;
   }
 }
 
@@ -1335,19 +1263,12 @@ extern "C" int pis_pde_fields_bwd(const float* u, const float* g_lap, const floa
 // exceed LOSS_MAX_BLOCKS; pis_tune key 36 overrides. At C2 8 rows ran the kernel in 131 us against
 // 134-145 us at 16 and 144 at 4 (0.54 vs 0.48-0.52 of 8 TB/s live; profiles/r4_ah_head_loss_rows.txt)
 // although a quarter of the head input is fetched twice (the halo rows, mostly from L2)
-static bool head_loss_fwd_halo() { return tune_get(PIS_TUNE_HEAD_LOSS_HALO) != 0; }
-// finalize rows of a band split: one per band, plus (no-halo form) one per band boundary
-static int64_t head_loss_fwd_frows(int B, int H, int R) {
-  const int64_t bands = (H + R - 1) / R;
-  return (int64_t)B * bands + (head_loss_fwd_halo() ? 0 : (int64_t)B * (bands - 1));
-}
 static int head_loss_fwd_rows(int B, int H, int W) {
   const int t = tune_get(PIS_TUNE_HEAD_LOSS_ROWS);
   int r = t > 0 ? t : std::max(2, std::min(16, 4096 / std::max(1, W)));
   if (t <= 0)
-    while (r < H && head_loss_fwd_frows(B, H, r) > LOSS_MAX_BLOCKS) r *= 2;
-  // the no-halo form needs >= 2 rows per band (a band's first and last rows differ)
-  return std::max(head_loss_fwd_halo() ? 1 : 2, std::min(r, H));
+    while (r < H && (int64_t)B * ((H + r - 1) / r) > LOSS_MAX_BLOCKS) r *= 2;
+  return std::max(1, std::min(r, H));
 }
 
 // pixels per 16-lane group in flight in the fused head + loss forward (W % (NG PP) == 0), 0: none fits;
@@ -1356,24 +1277,21 @@ static int head_loss_fwd_pp(int W) { return W % 256 == 0 ? 16 : W % 128 == 0 ? 8
 static bool head_loss_fwd_wide(int W) { return W % 512 == 0 && tune_get(PIS_TUNE_HEAD_LOSS_WIDE) != 0; }
 
 extern "C" size_t pis_head_loss_fwd_ws(int B, int H, int W) {
-  // sized for one row per block (and a boundary row per block), so a later key-36 change cannot
-  // outgrow a planned workspace
+  // sized for one row per block, so a later key-36 change cannot outgrow a planned workspace
   const size_t nblk = (size_t)B * H;
   (void)W;
-  return 16 + nblk * (2 * 6 * sizeof(float) + 3 * sizeof(int)) + 256;
+  return 16 + nblk * (6 * sizeof(float) + 3 * sizeof(int)) + 256;
 }
 
 // the staged u rows, (R + 2) x (W + 8) floats, must fit one workgroup's LDS (160 KB on gfx950); a
 // shape that does not (e.g. B = 128 at 1024^2: R = 64, 272 KB) takes pis_head_fwd + pis_loss_fwd
 static constexpr size_t kHeadLossFwdMaxLds = 160 * 1024;
-static size_t head_loss_fwd_smem(int R, int W) {
-  return (size_t)(R + (head_loss_fwd_halo() ? 2 : 0)) * (W + 8) * sizeof(float);
-}
+static size_t head_loss_fwd_smem(int R, int W) { return (size_t)(R + 2) * (W + 8) * sizeof(float); }
 
 extern "C" int pis_head_loss_fwd_ok(int B, int H, int W, int C) {
   const int R = head_loss_fwd_rows(B, H, W);
   return C == 64 && B > 0 && H >= 2 && W >= 8 && W <= 2048 && head_loss_fwd_pp(W) > 0 &&
-         head_loss_fwd_frows(B, H, R) <= LOSS_MAX_BLOCKS && head_loss_fwd_smem(R, W) <= kHeadLossFwdMaxLds;
+         (int64_t)B * ((H + R - 1) / R) <= LOSS_MAX_BLOCKS && head_loss_fwd_smem(R, W) <= kHeadLossFwdMaxLds;
 }
 
 extern "C" int pis_head_loss_fwd(const float* x, int ldx, const float* w, const float* bias, const float* t,
@@ -1396,17 +1314,14 @@ extern "C" int pis_head_loss_fwd(const float* x, int ldx, const float* w, const 
   g.smooth = prm->smooth; g.D = prm->D; g.a = prm->a; g.eps = prm->eps;
   g.rx = (prm->flags & PIS_LOSS_NO_REACTION) ? 0.f : 1.f; g.thr = prm->thr;
   const int bands = (H + h.R - 1) / h.R;
-  const bool halo = head_loss_fwd_halo();
-  const int64_t nfrow = head_loss_fwd_frows(B, H, h.R);
+  const int64_t nblk = (int64_t)B * bands;
   g.fpart = (float*)((char*)ws + 16);
-  g.ipart = (int*)((char*)ws + 16 + (size_t)nfrow * 6 * sizeof(float));
+  g.ipart = (int*)((char*)ws + 16 + (size_t)nblk * 6 * sizeof(float));
   h.a.rows = h.R;
   h.a.bands = bands;
-  h.a.fextra = (int)(nfrow - (int64_t)B * bands);
   h.a.terms = out_terms; h.a.counts = counts; h.a.scores = scores;
   const bool all = prm->flags & PIS_LOSS_ALL_TERMS;
   const bool rd = all || prm->rd_w > 0.f, pf = all || prm->pf_w > 0.f;
-  if (!(rd || pf)) h.a.fextra = 0;  // no stencil terms: no boundary rows
   const int pp = head_loss_fwd_pp(W);
   const bool wide = head_loss_fwd_wide(W);
   const bool wide3 = wide && tune_get(PIS_TUNE_HEAD_LOSS_WIDE) == 2;
@@ -1415,27 +1330,19 @@ extern "C" int pis_head_loss_fwd(const float* x, int ldx, const float* w, const 
   hipStream_t s = (hipStream_t)stream;
   const double nbytes = (double)B * H * W * (4.0 * C + 12.0);
   launch_hook("head_loss_fwd", 0, s, nbytes);
-#define PIS_HLF2(RDV, PFV, HL)                                                                                    \
+#define PIS_HLF(RDV, PFV)                                                                                         \
   do {                                                                                                            \
-    if (wide && wide3) hipLaunchKernelGGL((head_loss_fwd_kernel<RDV, PFV, 8, 1024, true, HL>), grid, dim3(1024), smem, s, h); \
-    else if (wide) hipLaunchKernelGGL((head_loss_fwd_kernel<RDV, PFV, 8, 1024, false, HL>), grid, dim3(1024), smem, s, h); \
-    else if (pp == 16) hipLaunchKernelGGL((head_loss_fwd_kernel<RDV, PFV, 16, 256, false, HL>), grid, dim3(256), smem, s, h); \
-    else if (pp == 8) hipLaunchKernelGGL((head_loss_fwd_kernel<RDV, PFV, 8, 256, false, HL>), grid, dim3(256), smem, s, h); \
-    else hipLaunchKernelGGL((head_loss_fwd_kernel<RDV, PFV, 4, 256, false, HL>), grid, dim3(256), smem, s, h);    \
-    if (!HL && bands > 1 && ((RDV) || (PFV)))                                                                     \
-      hipLaunchKernelGGL((head_loss_bnd_kernel<RDV, PFV>), dim3(bands - 1, B), dim3(256), 0, s, h.a, h.R);       \
-  } while (0)
-#define PIS_HLF(RDV, PFV)                \
-  do {                                   \
-    if (halo) PIS_HLF2(RDV, PFV, true);  \
-    else PIS_HLF2(RDV, PFV, false);      \
+    if (wide && wide3) hipLaunchKernelGGL((head_loss_fwd_kernel<RDV, PFV, 8, 1024, true>), grid, dim3(1024), smem, s, h); \
+    else if (wide) hipLaunchKernelGGL((head_loss_fwd_kernel<RDV, PFV, 8, 1024>), grid, dim3(1024), smem, s, h);   \
+    else if (pp == 16) hipLaunchKernelGGL((head_loss_fwd_kernel<RDV, PFV, 16>), grid, dim3(256), smem, s, h);     \
+    else if (pp == 8) hipLaunchKernelGGL((head_loss_fwd_kernel<RDV, PFV, 8>), grid, dim3(256), smem, s, h);       \
+    else hipLaunchKernelGGL((head_loss_fwd_kernel<RDV, PFV, 4>), grid, dim3(256), smem, s, h);                    \
   } while (0)
   if (rd && pf) PIS_HLF(true, true);
   else if (rd) PIS_HLF(true, false);
   else if (pf) PIS_HLF(false, true);
   else PIS_HLF(false, false);
 #undef PIS_HLF
-#undef PIS_HLF2
   launch_hook("head_loss_fwd", 1, s, nbytes);
   int rc = launch_status("head_loss_fwd");
   if (rc) return rc;

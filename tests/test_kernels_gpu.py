@@ -636,12 +636,11 @@ def test_head_loss_fwd_fused(hip, B, H, W, ldx, rd_w, pf_w):
     assert ((z.double() - z64).abs().max() / z64.abs().max()).item() < 1e-6
 
 
-@pytest.mark.parametrize("B,H,W", [(2, 37, 512), (8, 512, 512), (1, 40, 1024), (1, 13, 2048), (3, 9, 2048)])
+@pytest.mark.parametrize("B,H,W", [(2, 37, 512), (8, 512, 512), (1, 40, 1024), (1, 13, 2048)])
 def test_head_loss_fwd_variants(hip, B, H, W):
     """pis_tune(38): the 256-thread bands (0), the 1024-thread bands (1) and the same with three
-    register sets in flight (2); pis_tune(47): the no-halo bands with the band-boundary kernel (0,
-    default) and the halo-row bands (1) — bitwise the same z, u and counters, and the same terms to
-    fp32 summation order."""
+    register sets in flight (2) give bitwise the same z, u and counters, and the same terms to fp32
+    summation order."""
     g = torch.Generator().manual_seed(37)
     x = F.relu(torch.randn(B, H, W, 64, generator=g)).cuda()
     w = (torch.randn(64, generator=g) * 0.15).cuda()
@@ -650,17 +649,16 @@ def test_head_loss_fwd_variants(hip, B, H, W):
     t = mask[:, 0].contiguous().cuda()
     kw = dict(rd_w=1e-4, pf_w=1e-4, D=5.0, a=0.5, eps=0.05)
     outs = {}
-    for key, v in ((38, 0), (38, 1), (38, 2), (47, 1), (47, 0)):
-        prev = hip.pis_tune(key, v)
+    for v in (0, 1, 2):
+        prev = hip.pis_tune(38, v)
         try:
-            outs[key, v] = _head_loss_fwd_call(hip, x, 64, w, b, t, kw)
+            outs[v] = _head_loss_fwd_call(hip, x, 64, w, b, t, kw)
         finally:
-            hip.pis_tune(key, prev)
-    base = outs[38, 0]
-    for kv, out in outs.items():
+            hip.pis_tune(38, prev)
+    for v in (1, 2):
         for k in (0, 1, 3, 4):  # z, u, counts, scores
-            assert torch.equal(out[k], base[k]), (kv, k)
-        np.testing.assert_allclose(out[2].numpy(), base[2].numpy(), rtol=2e-6, atol=1e-12)
+            assert torch.equal(outs[v][k], outs[0][k]), (v, k)
+        np.testing.assert_allclose(outs[v][2].numpy(), outs[0][2].numpy(), rtol=2e-6, atol=1e-12)
 
 
 @pytest.mark.parametrize("shape", [(16, 512, 512), (3, 130, 68), (2, 2, 8), (1, 37, 1024), (5, 64, 4096), (4, 5, 20), (64, 512, 512)])
