@@ -3,7 +3,10 @@ reference training step. Never imported by the product package.
 
 Every function cites the reference file:line whose behaviour it restates.
 Arithmetic is stock ATen on CPU (the same ops the reference calls), in the
-dtype of the inputs (fp32 for parity, fp64 for gradchecks).
+dtype of the inputs (fp32 for parity, fp64 for gradchecks). The one exception is
+the float64 truth of the full-size GPU tests (whole_truth / chunked_truth with
+device="cuda"): the same float64 ops evaluated by the GPU's ATen, pinned to the
+CPU evaluation by tests/test_fullsize_gpu.py::test_float64_truth_device_independent.
 """
 from __future__ import annotations
 
@@ -239,11 +242,24 @@ def near_ties(record, tol: float = 1e-5, drop_scales=None, site_scale=None) -> D
     return out
 
 
-def whole_truth(ref: "UNetRef", img, mask, scales, decisions, loss_kws, log=None):
+def _on(device, img, mask, scales, decisions):
+    """The truth's inputs on ``device`` (None: where they are)."""
+    if device is None:
+        return img, mask, scales, decisions
+    mv = lambda d: {k: v.to(device) for k, v in d.items()}  # noqa: E731
+    return img.to(device), mask.to(device), mv(scales), mv(decisions)
+
+
+def whole_truth(ref: "UNetRef", img, mask, scales, decisions, loss_kws, log=None, device=None):
     """The float64 truth of one training step per loss config on given ReLU / max-pool decisions:
-    (p64, z64, flips {site: (n, worst margin, near-ties)}, [(terms, {param: grad})] per config)."""
+    (p64, z64, flips {site: (n, worst margin, near-ties)}, [(terms, {param: grad})] per config).
+    ``device``: where the float64 arithmetic runs (None: the inputs' device, the CPU in the CPU
+    suite). The full-size GPU tests evaluate it on the GPU's float64 ATen — the same ops in the
+    same dtype, pinned to the CPU evaluation by tests/test_fullsize_gpu.py — and get the results
+    back on the CPU."""
     log = log or (lambda msg: None)
-    ref64 = UNetRef().double().train()
+    img, mask, scales, decisions = _on(device, img, mask, scales, decisions)
+    ref64 = UNetRef().double().train().to(img.device)
     ref64.load_state_dict(ref.state_dict())
     record = {}
     log("float64 oracle forward")
@@ -259,11 +275,11 @@ def whole_truth(ref: "UNetRef", img, mask, scales, decisions, loss_kws, log=None
         t64 = loss_terms(p64, mask.double(), **kw)
         t64["loss"].backward(retain_graph=True)
         truth.append(({k: float(torch.as_tensor(v).detach()) for k, v in t64.items()},
-                      {n: q.grad.detach().clone() for n, q in ref64.named_parameters()}))
-    return p64.detach(), z64.detach(), flips, truth
+                      {n: q.grad.detach().cpu().clone() for n, q in ref64.named_parameters()}))
+    return p64.detach().cpu(), z64.detach().cpu(), flips, truth
 
 
-def chunked_truth(ref: "UNetRef", img, mask, scales, decisions, loss_kws, chunk: int, log=None):
+def chunked_truth(ref: "UNetRef", img, mask, scales, decisions, loss_kws, chunk: int, log=None, device=None):
     """whole_truth for a batch whose float64 graph does not fit host memory (C5: B = 8 at 1024^2
     would need ~220 GB). The U-Net has no cross-sample coupling (no normalisation layer,
     src/unet.py:19-67; Dropout2d masks injected per sample), and the loss couples the samples only
@@ -274,10 +290,12 @@ def chunked_truth(ref: "UNetRef", img, mask, scales, decisions, loss_kws, chunk:
       3. per chunk again, the forward with a graph and one backward per loss config seeded with
          that chunk's slice of dL/dp; parameter gradients summed over the chunks; the chunk's
          decision flips / near-ties measured in the whole batch's site scales.
-    Equal to whole_truth up to float64 summation order (tests/test_oracle.py)."""
+    Equal to whole_truth up to float64 summation order (tests/test_oracle.py). ``device`` as for
+    whole_truth."""
     log = log or (lambda msg: None)
+    img, mask, scales, decisions = _on(device, img, mask, scales, decisions)
     B = img.shape[0]
-    ref64 = UNetRef().double().train()
+    ref64 = UNetRef().double().train().to(img.device)
     ref64.load_state_dict(ref.state_dict())
     s64 = {k: v.double() for k, v in scales.items()}
 
@@ -325,7 +343,8 @@ def chunked_truth(ref: "UNetRef", img, mask, scales, decisions, loss_kws, chunk:
                 grads[i][n] = grads[i][n] + q.grad if n in grads[i] else q.grad.detach().clone()
         del p
     flips = {k: (n, m, near[k]) for k, (n, m) in flips.items()}
-    return p64, z64, flips, list(zip(terms, grads))
+    grads = [{n: g.cpu() for n, g in gi.items()} for gi in grads]
+    return p64.cpu(), z64.cpu(), flips, list(zip(terms, grads))
 
 
 def make_drop_scales(m: UNetRef, B: int, generator: torch.Generator) -> Dict[str, torch.Tensor]:
@@ -356,7 +375,7 @@ _GY = torch.tensor([[0.0, -0.5, 0.0], [0.0, 0.0, 0.0], [0.0, 0.5, 0.0]])
 
 def _stencil(u: torch.Tensor, k: torch.Tensor) -> torch.Tensor:
     up = F.pad(u, (1, 1, 1, 1), mode="reflect")  # src/pde.py:67,164
-    return F.conv2d(up, k.to(u.dtype)[None, None], padding=0)
+    return F.conv2d(up, k.to(u.device, u.dtype)[None, None], padding=0)
 
 
 def laplacian(u):  # src/pde.py:49-79

@@ -26,6 +26,9 @@ from oracle import reference_torch as rt
 
 pytestmark = pytest.mark.gpu
 TOL = 1e-4
+# where the float64 truth runs: the GPU's float64 ATen (minutes on the host cores per C5-size
+# step, seconds here); pinned to the CPU evaluation by test_float64_truth_device_independent
+DEV64 = "cuda"
 
 
 def rel(a, b):
@@ -78,18 +81,18 @@ def _run(H, W, loss_kws, seed, B=1, keep_net=False, log=None):
     oracle on the first run's decisions (one forward, one backward per config)."""
     log = log or (lambda msg: None)
     img, mask, ref, scales, hip_runs, decisions, net = _hip_steps(H, W, loss_kws, seed, B, log)
-    p64, z64, flips, truth = rt.whole_truth(ref, img, mask, scales, decisions, loss_kws, log)
+    p64, z64, flips, truth = rt.whole_truth(ref, img, mask, scales, decisions, loss_kws, log, device=DEV64)
     if keep_net:
         return img, mask, ref, scales, hip_runs, p64, z64, flips, truth, net
     return img, mask, ref, scales, hip_runs, p64, z64, flips, truth
 
 
 def _run_chunked(H, W, loss_kws, seed, B, chunk, log):
-    """_run for a batch whose float64 oracle does not fit host memory whole (C5: B = 8 at 1024^2
+    """_run for a batch whose float64 oracle graph is too big to build whole (C5: B = 8 at 1024^2
     would need ~220 GB): the truth from rt.chunked_truth (per-chunk forward, whole-batch loss and
     dL/dp, per-chunk backward; pinned to the whole-batch oracle by tests/test_oracle.py)."""
     img, mask, ref, scales, hip_runs, decisions, _ = _hip_steps(H, W, loss_kws, seed, B, log)
-    p64, z64, flips, truth = rt.chunked_truth(ref, img, mask, scales, decisions, loss_kws, chunk, log)
+    p64, z64, flips, truth = rt.chunked_truth(ref, img, mask, scales, decisions, loss_kws, chunk, log, device=DEV64)
     return img, mask, ref, scales, hip_runs, p64, z64, flips, truth
 
 
@@ -110,6 +113,24 @@ def _check_step(hip_run, p64, z64, truth, flips, npx, skip_terms=()):
     print(f"decision flips {sum(n for n, _, _ in bad.values())} of {n_near} near-ties ({npx} px)")
     worst = sorted(((rel(grads[n], g64[n]), n) for n in g64), reverse=True)
     assert worst[0][0] < TOL, worst[:5]
+
+
+def test_float64_truth_device_independent(hip):
+    """The float64 truth evaluated on the GPU (DEV64) equals the CPU evaluation to float64
+    rounding: whole_truth and chunked_truth, every loss term, every parameter gradient, the
+    decision flips and near-ties (a 2-image 64 x 64 Stage II step and a C5-style loss)."""
+    kws = [dict(rd_w=1e-4, pf_w=1e-4, D=5.0, a=0.5, eps=0.05), dict(rd_w=1e-3, pf_w=0.0, D=100.0, a=0.5)]
+    img, mask, ref, scales, _, decisions, _ = _hip_steps(64, 64, kws, 3, 2, lambda msg: None)
+    for f, extra in ((rt.whole_truth, ()), (rt.chunked_truth, (1,))):
+        cpu = f(ref, img, mask, scales, decisions, kws, *extra)
+        gpu = f(ref, img, mask, scales, decisions, kws, *extra, device=DEV64)
+        assert gpu[0].device.type == "cpu" and rel(gpu[0], cpu[0]) < 1e-12 and rel(gpu[1], cpu[1]) < 1e-12
+        assert gpu[2].keys() == cpu[2].keys()
+        for k, (n, m, nt) in cpu[2].items():
+            assert gpu[2][k][0] == n and gpu[2][k][2] == nt and abs(gpu[2][k][1] - m) < 1e-12, k
+        for (tg, gg), (tc, gc) in zip(gpu[3], cpu[3]):
+            assert all(abs(tg[k] - tc[k]) <= 1e-12 * max(abs(tc[k]), 1e-30) for k in tc), (tg, tc)
+            assert max(rel(gg[n], gc[n]) for n in gc) < 1e-10
 
 
 def test_c2_train_step_every_gradient_and_rd_bound(hip):
@@ -148,7 +169,7 @@ def test_c5_batch8_train_step(hip, capsys):
     term (L_RD bounded by the fp32 oracle's own error), every parameter gradient against float64 on
     the HIP decisions. The float64 truth is built in 2-image chunks
     (_run_chunked: per-chunk forward, whole-batch loss and dL/dp, per-chunk backward) since the
-    whole batch's float64 graph would need ~220 GB of host memory. B = 8 at 1024^2 is 4x C2's pixel
+    whole batch's float64 graph would need ~220 GB. B = 8 at 1024^2 is 4x C2's pixel
     count: the weight gradients' split-K slab counts and slab-reduction regimes, the 1024-wide head
     / loss rows and the direct weight gradient's block ranges at the largest size the bench runs."""
     kws = [dict(rd_w=1e-3, pf_w=0.0, D=D, a=0.5) for D in (0.5, 100.0)]
