@@ -475,7 +475,7 @@ def train_step(m: UNetRef, opt, x, t, loss_kw: dict, drop_scales=None):
     terms = loss_terms(p, t, **loss_kw)
     terms["loss"].backward()
     opt.step()
-    return p.detach(), {k: float(v) for k, v in terms.items()}
+    return p.detach(), {k: float(v.detach()) for k, v in terms.items()}
 
 
 # ---------------------------------------------------------------------------

@@ -353,16 +353,23 @@ class UNetEngine:
     # PIS_FILTER_AHEAD=1: the F(4x4,3x3) filter transforms of a step (forward: the layers' weights;
     # backward: their rotated input-gradient form) run on the side stream, idle during the forward,
     # at its start, and the main stream's convs wait on one event each instead of transforming
-    # their own. Measured 1.5 % SLOWER at C2 (tools/ab_tune.py: 31.48 vs 31.01 ms, and 31.39 vs
-    # 30.95 with the backward's transforms at the start of the backward).
+    # their own. Measured 1.5 % SLOWER at C2 in round 2 (tools/ab_tune.py: 31.48 vs 31.01 ms, and
+    # 31.39 vs 30.95 with the backward's transforms at the start of the backward).
     # PIS_FILTER_AHEAD=2: every filter transform of the step (both directions) in ONE launch on the
     # main stream at the start of the training forward (pis_conv3x3_filters) instead of 34 small,
-    # latency-bound launches: measured neutral at C2 (31.29 vs 31.27 ms). Default 0: each conv
+    # latency-bound launches: measured neutral at C2 in round 2 (31.29 vs 31.27 ms). 0: each conv
     # transforms its own filter.
     # PIS_FILTER_AHEAD=3: only the direct fp16x3 layers' weight splits (both directions) in ONE launch
     # at the forward's start: 12 small main-stream launches fewer, six of them in the backward.
     # Measured neutral on the C2 step (344.2 vs 344.0 img/s, profiles/r3_q25_ab_env.txt).
-    filter_ahead = os.environ.get("PIS_FILTER_AHEAD", "0")
+    # PIS_FILTER_AHEAD=4: 2 and 3 together (the direct splits, then the Winograd transforms: two
+    # launches on the main stream at the forward's start); 5 (default since round 5): the same two
+    # launches on the side stream (idle during the forward), the first consumer of each waiting on
+    # its event. With the direct layers' weight gradients on the main stream (below), the main
+    # stream is the step's critical path and its ~34 small latency-bound transform launches show:
+    # 5 vs 0 is 21.47-21.55 vs 21.85-22.48 ms over four same-process A/B runs, 2 at 21.46-21.91,
+    # 3 at 21.68-21.96 (profiles/r5_j_ab_filter_ahead.txt).
+    filter_ahead = os.environ.get("PIS_FILTER_AHEAD", "5")
     # "1" (default): every direct-kernel layer's weight gradient on the main stream right after its
     # input gradient (see the backward); "0": on the weight-gradient stream
     direct_wgrad_main = os.environ.get("PIS_DIRECT_WGRAD_MAIN", "1")
@@ -463,8 +470,12 @@ class UNetEngine:
         self.fev: Dict[int, Optional[torch.cuda.Event]] = {}  # filters computed for this forward
         self.bev: Dict[int, Optional[torch.cuda.Event]] = {}  # ... for its backward (None: same stream)
         self.filter_jobs = None
+        self.filter_jobs_d = None  # modes 4 / 5: the direct layers' splits (the Winograd ones in filter_jobs)
         mode = str(self.filter_ahead)
-        if (mode == "1" and self.side is not None) or mode in ("2", "3"):
+        if mode == "5" and self.side is None:
+            mode = "4"
+        self._fa_mode = mode
+        if (mode == "1" and self.side is not None) or mode in ("2", "3", "4", "5"):
             for name in BLOCK_ORDER:
                 blk = self.m.block(name)
                 lvl = 5 if name == "bottleneck" else int(name[-1])
@@ -474,7 +485,7 @@ class UNetEngine:
                         continue
                     # modes 1/2: the layers whose transform is kept for the weight gradient (the
                     # Winograd ones); mode 3: the others, i.e. the direct kernel's layers
-                    if (id(conv) in self.keep) != (mode != "3"):
+                    if mode in ("1", "2", "3") and (id(conv) in self.keep) != (mode != "3"):
                         continue
                     ci, co = conv.in_channels, conv.out_channels
                     nb = lib.pis_conv3x3_filter_bytes(B, Hl, Wl, ci, co, 0)
@@ -485,13 +496,20 @@ class UNetEngine:
                     if nb and not (name == "enc1" and conv is blk.conv0):  # the first conv has no dgrad
                         self.bfilt[id(conv)] = (conv, Hl, Wl, torch.empty((nb + 3) // 4, dtype=torch.float32,
                                                                           device=dev))
-        if mode in ("2", "3") and (self.ffilt or self.bfilt):
+        if mode in ("2", "3", "4", "5") and (self.ffilt or self.bfilt):
             jobs = [(t, 0) for t in self.ffilt.values()] + [(t, 1) for t in self.bfilt.values()]
-            arr = (_hip.FilterJob * len(jobs))()
-            for k, ((conv, Hl, Wl, buf), dg) in enumerate(jobs):
-                arr[k] = _hip.FilterJob(conv.weight.data_ptr(), buf.data_ptr(), buf.numel() * 4, B, Hl, Wl,
-                                        conv.in_channels, conv.out_channels, dg)
-            self.filter_jobs = arr
+
+            def table(sel):
+                arr = (_hip.FilterJob * len(sel))()
+                for k, ((conv, Hl, Wl, buf), dg) in enumerate(sel):
+                    arr[k] = _hip.FilterJob(conv.weight.data_ptr(), buf.data_ptr(), buf.numel() * 4, B, Hl, Wl,
+                                            conv.in_channels, conv.out_channels, dg)
+                return arr
+            if mode in ("4", "5"):  # two tables: the direct splits first (enc1.conv1 needs its split next)
+                self.filter_jobs_d = table([j for j in jobs if id(j[0][0]) not in self.keep])
+                self.filter_jobs = table([j for j in jobs if id(j[0][0]) in self.keep])
+            else:
+                self.filter_jobs = table(jobs)
 
     def _filters_ahead(self, table, dgrad: int, order):
         """Launch the filter transforms of `table` on the side stream (after everything the main
@@ -508,6 +526,34 @@ class UNetEngine:
                 ev.record(side)
                 events[cid] = ev
         return events
+
+    def _filters_batched(self):
+        """PIS_FILTER_AHEAD 4 / 5: every filter operand of the step — the direct layers' weight splits
+        (one launch), then the Winograd layers' transforms, both directions (a second) — at the
+        training forward's start. Mode 4 on the main stream (no events); mode 5 on the side stream,
+        idle during the forward, with one event per launch that the first consumer of each kind
+        waits for (every later consumer, forward or backward, follows it on the main stream)."""
+        main = torch.cuda.current_stream()
+        tables = [t for t in (self.filter_jobs_d, self.filter_jobs) if t is not None and len(t)]
+        self.fev = dict.fromkeys(self.ffilt)
+        self.bev = dict.fromkeys(self.bfilt)
+        if self._fa_mode == "4" or self.side is None:  # (side None: the serialised A/B step)
+            for t in tables:
+                call("pis_conv3x3_filters", ctypes.addressof(t), len(t), main.cuda_stream)
+            return
+        side = self.side
+        side.wait_stream(main)  # the weights are final (the previous step's optimizer)
+        with torch.cuda.stream(side):
+            for t in tables:
+                call("pis_conv3x3_filters", ctypes.addressof(t), len(t), side.cuda_stream)
+                ev = self._event()
+                ev.record(side)
+                first = next((cid for cid in self.ffilt if any(j.w == self.ffilt[cid][0].weight.data_ptr() and
+                                                                 j.dgrad == 0 for j in t)), None)
+                if first is None:  # no forward consumer in this table: order the main stream now
+                    main.wait_event(ev)
+                else:
+                    self.fev[first] = ev
 
     def _event(self) -> torch.cuda.Event:
         ev = torch.cuda.Event()
@@ -591,7 +637,9 @@ class UNetEngine:
         # the side stream is idle during the forward: it transforms every filter of the step there,
         # the forward's in layer order, then the input gradients' (backward order)
         self.fev, self.bev = {}, {}
-        if keep and self.filter_jobs is not None:  # one launch, same stream: no events
+        if keep and self.filter_jobs_d is not None:  # modes 4 / 5: all of them, in two launches
+            self._filters_batched()
+        elif keep and self.filter_jobs is not None:  # one launch, same stream: no events
             call("pis_conv3x3_filters", ctypes.addressof(self.filter_jobs), len(self.filter_jobs), self._stream())
             self.fev = dict.fromkeys(self.ffilt)
             self.bev = dict.fromkeys(self.bfilt)

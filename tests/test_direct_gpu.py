@@ -365,16 +365,18 @@ def test_direct_split_ready_bitwise(hip, cin, cout):
 
 
 def test_engine_direct_splits_ahead_bitwise(hip):
-    """PIS_FILTER_AHEAD=3 (the engine computes every direct layer's weight split, both directions,
-    in one launch at the forward's start and passes PIS_FILTER_READY): one training step gives
-    bitwise the outputs and gradients of the default engine."""
+    """PIS_FILTER_AHEAD 2 / 3 / 4 / 5 (the engine computes the Winograd layers' filter transforms
+    (2), the direct layers' weight splits (3) or both (4: two launches on the main stream; 5: on the
+    side stream behind events), both directions, at the forward's start and passes
+    PIS_FILTER_READY): one training step gives bitwise the outputs and gradients of the default
+    engine."""
     import importlib
     from physics_informed_image_segmentation_amd import unet as U
     tu = importlib.import_module("test_unet_gpu")
     res = {}
     prev = U.UNetEngine.filter_ahead
     try:
-        for mode in ("0", "3"):
+        for mode in ("0", "2", "3", "4", "5"):
             U.UNetEngine.filter_ahead = mode
             with Knobs(hip, k29=2):
                 net, ref, u, crit, p_ref, terms, ref64 = tu._step_pair(1, 64, 64, dict())
@@ -382,6 +384,7 @@ def test_engine_direct_splits_ahead_bitwise(hip):
             del net, ref, ref64
     finally:
         U.UNetEngine.filter_ahead = prev
-    assert torch.equal(res["0"][0], res["3"][0])
-    for a, b in zip(res["0"][1], res["3"][1]):
-        assert torch.equal(a, b)
+    for mode in ("2", "3", "4", "5"):
+        assert torch.equal(res["0"][0], res[mode][0]), mode
+        for a, b in zip(res["0"][1], res[mode][1]):
+            assert torch.equal(a, b), mode

@@ -4,7 +4,7 @@ GPU (box-to-box variance is ~3 %; same-process interleaving is not).
     python tools/ab_tune.py --variants "base;20=0;15=0,17=4" [--rounds 4] [--steps 10] [--shared]
 
 Each variant is a comma list of KEY=VALUE (include/pis_capi.h PIS_TUNE_*); "base" = defaults;
-"fa=0|1|2" plans that variant's engine with PIS_FILTER_AHEAD = that value, "dwm=0|1" runs the direct
+"fa=0..5" plans that variant's engine with PIS_FILTER_AHEAD = that value, "dwm=0|1" runs the direct
 layers' weight gradients on the main stream (PIS_DIRECT_WGRAD_MAIN; unet.py).
 """
 import argparse
