@@ -383,6 +383,7 @@ class UNetEngine:
         self._offsets = {id(mod._parameters[pn]): (o, n) for mod, pn, _, _, o, n in model._entries}
         self.last_grad_mode = None
         self.pending_head = None  # dL/du tensor whose head backward already ran fused with the loss
+        self.convt_ready = False  # the transposed convs' input-gradient weights prepared by the forward
         # (targets, LossParams, sink) set by UNet.forward_with_loss for the next forward: its head runs
         # fused with the loss forward (pis_head_loss_fwd) and the loss outputs land in the sink
         self.loss_request = None
@@ -540,12 +541,15 @@ class UNetEngine:
         if self._fa_mode == "4" or self.side is None:  # (side None: the serialised A/B step)
             for t in tables:
                 call("pis_conv3x3_filters", ctypes.addressof(t), len(t), main.cuda_stream)
+            self._convt_prep(main.cuda_stream)
             return
         side = self.side
         side.wait_stream(main)  # the weights are final (the previous step's optimizer)
         with torch.cuda.stream(side):
-            for t in tables:
+            for i, t in enumerate(tables):
                 call("pis_conv3x3_filters", ctypes.addressof(t), len(t), side.cuda_stream)
+                if i + 1 == len(tables):  # ... and the transposed convs' input-gradient weights
+                    self._convt_prep(side.cuda_stream)
                 ev = self._event()
                 ev.record(side)
                 first = next((cid for cid in self.ffilt if any(j.w == self.ffilt[cid][0].weight.data_ptr() and
@@ -554,6 +558,15 @@ class UNetEngine:
                     main.wait_event(ev)
                 else:
                     self.fev[first] = ev
+
+    def _convt_prep(self, stream):
+        """The four transposed convs' input-gradient weight layouts (pis_convt2x2_prep) for the
+        coming backward, which then skips them (``convt_ready``)."""
+        for l in (1, 2, 3, 4):
+            up = getattr(self.m, f"up{l}")
+            t = self._gbuf(f"prep_up{l}", up.weight.numel())
+            call("pis_convt2x2_prep", up.weight.data_ptr(), t.data_ptr(), up.in_channels, up.out_channels, stream)
+        self.convt_ready = True
 
     def _event(self) -> torch.cuda.Event:
         ev = torch.cuda.Event()
@@ -637,6 +650,7 @@ class UNetEngine:
         # the side stream is idle during the forward: it transforms every filter of the step there,
         # the forward's in layer order, then the input gradients' (backward order)
         self.fev, self.bev = {}, {}
+        self.convt_ready = False
         if keep and self.filter_jobs_d is not None:  # modes 4 / 5: all of them, in two launches
             self._filters_batched()
         elif keep and self.filter_jobs is not None:  # one launch, same stream: no events
@@ -795,8 +809,10 @@ class UNetEngine:
         for l in (1, 2, 3, 4):
             up = getattr(m, f"up{l}")
             t = gb(f"prep_up{l}", up.weight.numel())
-            call("pis_convt2x2_prep", up.weight.data_ptr(), t.data_ptr(), up.in_channels, up.out_channels, st)
+            if not self.convt_ready:  # (else prepared with the filter operands at the forward's start)
+                call("pis_convt2x2_prep", up.weight.data_ptr(), t.data_ptr(), up.in_channels, up.out_channels, st)
             flips[id(up)] = t
+        self.convt_ready = False
 
         lib = _hip.lib()
         nprep = [0]
@@ -892,16 +908,20 @@ class UNetEngine:
         fused, self.pending_head = self.pending_head, None
         if fused is not None and du.data_ptr() == fused.data_ptr():
             # the loss backward already ran the head backward (pis_head_loss_bwd): g_d1 is
-            # written and the head's dW/db wait in the scratch; only their arena update is left
+            # written and the head's dW/db wait in the scratch; only their arena update is left —
+            # weight-gradient work, so on the side stream in its workspace, off the critical path
             hs = self.head_scratch
-            call("pis_colsum", hs.data_ptr(), c, 1, c, self._gptr(m.out_conv.weight), acc, ws, wsb, st)
-            call("pis_colsum", hs.data_ptr() + 4 * c, 1, 1, 1, self._gptr(m.out_conv.bias), acc, ws, wsb, st)
+            to_side()
+            hws = ws2 if side is not main else ws
+            call("pis_colsum", hs.data_ptr(), c, 1, c, self._gptr(m.out_conv.weight), acc, hws, wsb, sst)
+            call("pis_colsum", hs.data_ptr() + 4 * c, 1, 1, 1, self._gptr(m.out_conv.bias), acc, hws, wsb, sst)
+            ready_on_side(m.out_conv.weight, m.out_conv.bias)
         else:
             du = du.contiguous()
             call("pis_head_bwd", d1.p, d1.ld, m.out_conv.weight.data_ptr(), du.data_ptr(), self.u.data_ptr(),
                  g_d1.p, g_d1.ld, self._gptr(m.out_conv.weight), self._gptr(m.out_conv.bias), B * H * W, c, acc,
                  ws, wsb, st)
-        self._ready(m.out_conv.weight, m.out_conv.bias)
+            self._ready(m.out_conv.weight, m.out_conv.bias)
 
         g_top = g_d1  # dz of dec_l.conv1
         for l in (1, 2, 3, 4):
