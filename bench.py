@@ -98,7 +98,8 @@ def wino_gemm_launches(H: int, W: int, B: int, c: int = 64):
     out = []
     for hl, wl, ci, co in convs:
         T = B * (hl // 4) * (wl // 4)
-        out += [(T, C, N) for C, N in ((ci, co), (co, ci)) if not fused_wanted(T, C, N)]
+        out += [(T, C, N) for C, N in ((ci, co), (co, ci))
+                if not direct_wanted(hl, wl, C, N) and not fused_wanted(T, C, N)]
     return out
 
 
@@ -116,7 +117,8 @@ def fused_launches(H: int, W: int, B: int, c: int = 64):
     out = []
     for hl, wl, ci, co in convs:
         T = B * (hl // 4) * (wl // 4)
-        out += [(T, C, N, dg) for C, N, dg in ((ci, co, 0), (co, ci, 1)) if fused_wanted(T, C, N)]
+        out += [(T, C, N, dg) for C, N, dg in ((ci, co, 0), (co, ci, 1))
+                if not direct_wanted(hl, wl, C, N) and fused_wanted(T, C, N)]
     return out
 
 
@@ -192,6 +194,23 @@ def direct_role_launches(H: int, W: int, B: int):
             out["direct_h3_dgrad"].append((fl, 4.0 * P * (co + ci) + (4.0 * P * ci if mask else 0.0)))
         out["direct_wgrad_h3"].append((fl, 4.0 * P * (ci + co) + 4.0 * 9 * ci * co))
     return out
+
+
+def direct_wanted(H: int, W: int, C: int, N: int) -> bool:
+    """csrc/direct.hip direct_h3_wanted (pis_tune key 29 as set now): the 3x3 convs (both
+    directions) that run the direct fp16x3 kernels instead of a Winograd pipeline."""
+    from physics_informed_image_segmentation_amd import _hip
+    mode = _hip.lib().pis_tune(29, -1)
+    if mode == 0 or H % 8 or W % 32 or C % 16 or N % 64 or C < 16:
+        return False
+    lo, hi = min(C, N), max(C, N)
+    if mode == 3:
+        return (H >= 256 and hi <= 256) or (H >= 128 and hi <= 256 and lo <= 128)
+    if mode == 4:
+        return H >= 128 and hi <= 256
+    if mode == 5:
+        return H >= 128
+    return mode == 2 or (hi <= 128 and H >= 256)
 
 
 def fused_wanted(T: int, C: int, N: int) -> bool:
@@ -455,6 +474,38 @@ def loss_standalone(u: torch.Tensor, t: torch.Tensor, loss_kw: dict, reps: int =
                       "avg_call_ms": floor[0], "achieved": fgbs, "frac": fgbs / 8000.0,
                       "loss_over_floor": ms / floor[0]}}
     return out
+
+
+def hbm_probe(device, reps: int = 10) -> dict:
+    """The box's attainable streaming rate, for context beside the HBM rooflines (which are priced
+    against the 8 TB/s datasheet figure): stream_probe_kernel (a float4 grid-stride loop) reading
+    two 256 MiB arrays and writing a third (768 MiB per launch, 2:1 read:write), best over its grid
+    sizes, median of ``reps`` launches each. MI355X_MICROARCH.md quotes 6.29 TB/s for a float4 copy."""
+    from physics_informed_image_segmentation_amd import _hip
+    lib = _hip.lib()
+    n = 64 << 20  # floats per array
+    a = torch.ones(n, device=device)
+    b = torch.ones(n, device=device)
+    c = torch.empty(n, device=device)
+    st = torch.cuda.current_stream().cuda_stream
+    best = None
+    for grid in (256, 512, 1024, 2048, 4096, 8192):
+        evs = []
+        for _ in range(reps + 1):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            if lib.pis_debug_stream_probe(a.data_ptr(), b.data_ptr(), c.data_ptr(), n, 0, grid, st) != 0:
+                raise RuntimeError(lib.pis_last_error().decode())
+            e1.record()
+            evs.append((e0, e1))
+        torch.cuda.synchronize()
+        ms = statistics.median(x.elapsed_time(y) for x, y in evs[1:])
+        if best is None or ms < best[0]:
+            best = (ms, grid)
+    gbs = 12.0 * n / (best[0] * 1e-3) / 1e9
+    del a, b, c
+    return {"kernel": "stream_probe_kernel (read 2 x 256 MiB, write 256 MiB, float4 grid-stride)", "grid": best[1],
+            "avg_launch_ms": best[0], "achieved": gbs, "unit": "GB/s", "frac_of_8tbs": gbs / 8000.0}
 
 
 def _free_port() -> int:
@@ -725,6 +776,7 @@ def main():
                          "frac": ifl_d / (ims_d * 1e-3) / 1e12 / h3_peak if ims_d else None, "avg_launch_ms": ims_d,
                          "measured": "one extra step, weight gradients serialised"}}
     loss_cold = loss_standalone(model.engine().u, t, loss_kw)
+    hbm = hbm_probe(device)
     if rank == 0:
         flops = conv_flops_per_image(H, W) * B
         out = {
@@ -781,7 +833,12 @@ def main():
                     "measured": "live over the timed steps (HIP events on the launch stream, kernel only; its "
                                 "one-block finalize launch follows)"}} if nh_launch else {})),
             "final_loss": float(loss.item()),
+            # context for the HBM rooflines above (priced against 8 TB/s): this box's streaming rate
+            "hbm_probe": hbm,
         }
+        for r in (out["roofline_loss"].get("head_loss_fwd_kernel_live"), fused_roof):
+            if r:
+                r["frac_of_hbm_probe"] = r["achieved"] / hbm["achieved"]
         # the dominant kernel (most GPU time per step) carries the contract's "roofline"; the
         # other of the two conv kernels stays beside it
         g_ms, f_ms_step = n_launch * ms_per_launch, (nf_launch * f_ms if fused_roof else 0.0)

@@ -22,12 +22,12 @@ from physics_informed_image_segmentation_amd.dataset import disc_sample  # noqa:
 def parse(v):
     if v.strip() in ("", "base"):
         return {}
-    return {(k if k in HOST else int(k)): int(x) for k, x in (kv.split("=") for kv in v.split(","))}
+    return {(k if k in HOST else int(k)): (x if k in HOST else int(x)) for k, x in (kv.split("=") for kv in v.split(","))}
 
 
 # host-side engine attributes a variant may set (unet.UNetEngine): fa = filter_ahead, dwm =
-# direct_wgrad_main
-HOST = {"fa": "filter_ahead", "dwm": "direct_wgrad_main"}
+# direct_wgrad_main, ss = side_sync (prep / gemm / dgrad)
+HOST = {"fa": "filter_ahead", "dwm": "direct_wgrad_main", "ss": "side_sync"}
 
 
 def main():
