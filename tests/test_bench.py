@@ -46,15 +46,19 @@ def test_bench_json_contract():
     for name, bound, unit in (("roofline_gemm", "mfma", "TFLOP/s"), ("roofline_fused", "hbm", "GB/s"),
                               *((k, "mfma", "TFLOP/s") for k in direct)):
         r = d.get(name)
-        if name == "roofline_fused" and r is None:
-            continue  # every fused-kernel shape may have moved to the direct kernels
-        assert r is not None, name
+        assert r is not None, name  # (the launch tables leave the direct layers out: the fused
+        # kernel's two C2 launches are priced again)
         assert r["bound"] == bound and r["unit"] == unit and 0 < r["frac"] < 1
         assert abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-9
         assert r["launches_per_step"] > 0 and r["avg_launch_ms"] > 0 and r["ms_per_step"] > 0
         if name in direct:  # per-role algorithmic bytes: the layer table reproduces the hook's launches
             assert r["algorithmic_bytes_per_launch"] and 0 < r["hbm_frac"] < 1, name
     assert d["roofline_gemm"]["hbm_view"] is not None
+    # the box's streaming rate beside the HBM rooflines, and each HBM roofline against it
+    hp = d["hbm_probe"]
+    assert hp["unit"] == "GB/s" and 2000 < hp["achieved"] < 8000 and abs(hp["frac_of_8tbs"] - hp["achieved"] / 8000) < 1e-9
+    for r in (d["roofline_fused"], d["roofline_loss"]["head_loss_fwd_kernel_live"]):
+        assert abs(r["frac_of_hbm_probe"] - r["achieved"] / hp["achieved"]) < 1e-9
     assert d["roofline"]["ms_per_step"] == max(d[k]["ms_per_step"] for k in
                                                ("roofline_gemm", "roofline_fused") + direct if d.get(k))
 
