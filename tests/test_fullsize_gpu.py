@@ -11,7 +11,9 @@
   one AdamW step (src/train.py:108-167).
 * C5 shape (1024 x 1024, lambda_RD = 1e-3, lambda_PF = 0) at the ends of the S2 sweep, D = 0.5
   and D = 100 (run_ablation.py:176-188): the same checks, at B = 1 and at C5's own B = 8 per rank
-  (float64 truth built in 2-image chunks, _run_chunked).
+  (float64 truth built in 2-image chunks, _run_chunked); every D of the sweep at B = 1.
+* C4 (the R1 gatings, run_ablation.py:42-83) at C2's B = 8: (0, 0), (1e-4, 0), (0, 1e-4) beside
+  the Stage-II (1e-4, 1e-4) test — each gating specialises the fused head + loss kernels.
 * L_RD at C2 (src/pde.py:124-145): D Lap(u) + f(u) of a near-constant random-init u cancels,
   so fp32 rounding of u is amplified; instead of excluding the term, its error is BOUNDED:
   |L_RD(HIP) - L_RD(fp64)| <= 10 |L_RD(fp32 oracle) - L_RD(fp64)| (or <= 1e-4 relative), i.e.
@@ -186,6 +188,43 @@ def test_c5_batch8_train_step(hip, capsys):
         rd64, rd_hip = tr[0]["pde_loss"], run[2][3].item()
         print(f"L_RD at C5 B=8, D={kw['D']}: fp64 {rd64:.9e}  HIP {rd_hip:.9e}  fp32 oracle {rd32:.9e}")
         assert abs(rd_hip - rd64) <= max(10.0 * abs(rd32 - rd64), TOL * abs(rd64)), kw
+
+
+def test_c5_d_sweep_every_value(hip):
+    """The whole S2 sweep of C5 (run_ablation.py:176-188: lambda_RD = 1e-3, lambda_PF = 0,
+    D in {0.5, 1, 2, 5, 10, 100}) at 1024 x 1024: per D one HIP training step from the same weights
+    and dropout masks, logits / probabilities / terms / every parameter gradient against the float64
+    truth on the HIP decisions, L_RD under the fp32 oracle's own error bound."""
+    kws = [dict(rd_w=1e-3, pf_w=0.0, D=D, a=0.5) for D in (0.5, 1.0, 2.0, 5.0, 10.0, 100.0)]
+    img, mask, ref, scales, runs, p64, z64, flips, truth = _run(1024, 1024, kws, seed=11)
+    with torch.no_grad():
+        p32 = ref(img, scales)
+    for kw, run, tr in zip(kws, runs, truth):
+        _check_step(run, p64, z64, tr, flips, 1024 * 1024, skip_terms=("pde_loss",))
+        rd32 = rt.rd_loss(p32.double(), kw["D"], 0.5).item()
+        rd64, rd_hip = tr[0]["pde_loss"], run[2][3].item()
+        assert abs(rd_hip - rd64) <= max(10.0 * abs(rd32 - rd64), TOL * abs(rd64)), kw
+
+
+def test_c4_gatings_batch8_train_step(hip, capsys):
+    """C4 (run_ablation.py:42-83: (lambda_RD, lambda_PF) in {(0, 0), (1e-4, 0), (0, 1e-4)}; the
+    fourth, (1e-4, 1e-4), is test_c2_batch8_train_step) at C2's own batch, B = 8 at 512 x 512: each
+    gating specialises the fused head + loss kernels (forward and backward), so every term and every
+    parameter gradient is checked against float64 per gating."""
+    kws = [dict(rd_w=0.0, pf_w=0.0, D=5.0, a=0.5, eps=0.05), dict(rd_w=1e-4, pf_w=0.0, D=5.0, a=0.5, eps=0.05),
+           dict(rd_w=0.0, pf_w=1e-4, D=5.0, a=0.5, eps=0.05)]
+    B = 8
+    img, mask, ref, scales, runs, p64, z64, flips, truth = _run(512, 512, kws, seed=13, B=B, log=_progress(capsys))
+    with torch.no_grad():
+        p32 = ref(img, scales)
+    for kw, run, tr in zip(kws, runs, truth):
+        _check_step(run, p64, z64, tr, flips, B * 512 * 512, skip_terms=("pde_loss",))
+        if kw["rd_w"] > 0:
+            rd32 = rt.rd_loss(p32.double(), 5.0, 0.5).item()
+            rd64, rd_hip = tr[0]["pde_loss"], run[2][3].item()
+            assert abs(rd_hip - rd64) <= max(10.0 * abs(rd32 - rd64), TOL * abs(rd64)), kw
+        else:
+            assert "pde_loss" not in tr[0]
 
 
 def test_c2_batch8_train_step(hip, capsys):
