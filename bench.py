@@ -130,12 +130,19 @@ def fused_bytes(T: int, C: int, N: int, dgrad: int) -> float:
     return 4.0 * (36 * T * C + 36 * N * C + 16 * T * N * (2 if dgrad else 1))
 
 
-def pmc_bytes(substr):
+# the configuration the committed PMC counters (profiles/pmc_dominant.json) were collected on:
+# another --config reports its PMC fields as null instead of these
+PMC_CONFIG = "c2"
+PMC_NOTE = ("PMC counters (HBM traffic, MFMA busy) are collected on C2 only (profiles/pmc_dominant.json); "
+            "null for this config rather than C2's figures")
+
+
+def pmc_bytes(substr, config=PMC_CONFIG):
     """Launch-weighted HBM bytes per launch of the kernels whose name contains substr (or any of
     a list of substrings), from the committed rocprofv3 --pmc summary (profiles/pmc_dominant.json),
-    or None."""
+    or None (also for a config the summary was not collected on)."""
     path = os.path.join(HERE, "profiles", "pmc_dominant.json")
-    if not os.path.exists(path):
+    if config != PMC_CONFIG or not os.path.exists(path):
         return None
     with open(path) as f:
         ks = json.load(f).get("kernels", {})
@@ -336,12 +343,13 @@ BUSY_REPORTED = ("gemm_nt", "wgrad_x6", "wgrad_h3", "wino4_gemm_out", "convt_gem
                  "conv3x3_wgrad", "loss_fwd", "head_loss", "loss_bwd")
 
 
-def load_pmc(kernel=DOMINANT_KERNEL):
+def load_pmc(kernel=DOMINANT_KERNEL, config=PMC_CONFIG):
     """Per-launch HBM bytes and MFMA-busy fraction of the dominant kernel from the committed
     rocprofv3 --pmc summary (tools/pmc_summary.py: FETCH_SIZE x2 gfx950 correction +
-    WRITE_SIZE; SQ_VALU_MFMA_BUSY_CYCLES over GRBM_GUI_ACTIVE / 8 x 1024 SIMDs)."""
+    WRITE_SIZE; SQ_VALU_MFMA_BUSY_CYCLES over GRBM_GUI_ACTIVE / 8 x 1024 SIMDs); all None for a
+    config the summary was not collected on."""
     path = os.path.join(HERE, "profiles", "pmc_dominant.json")
-    if not os.path.exists(path):
+    if config != PMC_CONFIG or not os.path.exists(path):
         return None, None, None
     with open(path) as f:
         d = json.load(f)
@@ -657,10 +665,16 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    rank_ms = None
     if world > 1:
-        tt = torch.tensor([dt], device=device, dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        dt = tt.item()
+        # every rank's own time (straggling), then the max over ranks for the line
+        tt = torch.zeros(world, device=device if args.backend == "nccl" else "cpu", dtype=torch.float64)
+        tt[rank] = dt
+        dist.all_reduce(tt, op=dist.ReduceOp.SUM)
+        per = [v / args.steps * 1e3 for v in tt.tolist()]
+        rank_ms = {"min": min(per), "max": max(per), "per_rank": per,
+                   "measured": "each rank's own barrier-to-barrier time / steps; ms_per_step is the max"}
+        dt = max(tt.tolist())
     ms = dt / args.steps * 1e3
     imgs_per_s = world * B * args.steps / dt
     dist_info = None
@@ -705,7 +719,8 @@ def main():
             "fp32-equivalent FLOPs" if x6 else "fp32 MFMA")
     # gemm_nt_h3_bk32_kernel / gemm_nt_x6_bk32_kernel (K % 32 == 0, every C2 layer)
     kname = "gemm_nt_h3_" if h3 else "gemm_nt_x6_" if x6 else DOMINANT_KERNEL
-    traffic, mfma_busy, busy_by_kernel = load_pmc(kname)
+    traffic, mfma_busy, busy_by_kernel = load_pmc(kname, args.config)
+    pmc = lambda sub: pmc_bytes(sub, args.config)  # noqa: E731
     # the same launches against BOTH bounds (per launch max of FLOP / pipe peak and algorithmic
     # bytes / 8 TB/s): only valid when the shape list reproduces the launches the hook timed
     gl = wino_gemm_launches(H, W, B)
@@ -735,7 +750,7 @@ def main():
                                       "F(4x4,3x3) contractions fused with the output transform, 64 / 128-channel "
                                       "contractions into <= 256 outputs)",
             "achieved": fb / (f_ms * 1e-3) / 1e9, "peak": 8000.0, "unit": "GB/s",
-            "frac": fb / (f_ms * 1e-3) / 8e12, "traffic": pmc_bytes("wino4_gemm_out"),
+            "frac": fb / (f_ms * 1e-3) / 8e12, "traffic": pmc("wino4_gemm_out"),
             "bytes_per_launch": fb, "launches_per_step": nf_launch, "avg_launch_ms": f_ms,
             "flop_per_launch": f_flop, "mfma_tflops": f_flop / (f_ms * 1e-3) / 1e12,
             "bytes": "V read + filter planes read once + output written (+ the input gradient's ReLU mask read)",
@@ -764,7 +779,7 @@ def main():
                if len(lay) == n_d and abs(sum(f for f, _ in lay) / len(lay) - fl_d) <= 1e-6 * fl_d else None)
         direct_roofs[name] = {
             "bound": "mfma", "kernel": kern, "achieved": fl_d / (ms_d * 1e-3) / 1e12, "peak": h3_peak,
-            "unit": "TFLOP/s", "frac": fl_d / (ms_d * 1e-3) / 1e12 / h3_peak, "traffic": pmc_bytes(syms),
+            "unit": "TFLOP/s", "frac": fl_d / (ms_d * 1e-3) / 1e12 / h3_peak, "traffic": pmc(syms),
             "traffic_symbols": syms,
             "pipe": "fp16 MFMA, fp32-class fp16x3 split (3 fp16 products per fp32 multiply-add); fp32-equivalent "
                     "FLOPs of the direct convolution",
@@ -825,7 +840,7 @@ def main():
                 **({"head_loss_fwd_kernel_live": {
                     "bound": "hbm", "achieved": h_bytes / (h_ms * 1e-3) / 1e9, "peak": 8000.0, "unit": "GB/s",
                     "frac": h_bytes / (h_ms * 1e-3) / 8e12, "bytes_per_launch": h_bytes, "avg_launch_ms": h_ms,
-                    "launches_per_step": nh_launch // args.steps, "traffic": pmc_bytes("head_loss_fwd_kernel"),
+                    "launches_per_step": nh_launch // args.steps, "traffic": pmc("head_loss_fwd_kernel"),
                     "kernel": "head_loss_fwd_kernel (the U-Net head's 1x1 conv + sigmoid fused with the whole loss "
                               "forward: Dice / BCE / RD / PF partials and the per-sample counters)",
                     "bytes": "head input read (4 C B/px) + targets read (4 B/px) + z and u written (8 B/px); the "
@@ -852,6 +867,9 @@ def main():
         out["roofline"] = out[out["roofline_dominant"]]
         if dist_info is not None:
             out["distributed"] = dist_info
+            out["ms_per_step_by_rank"] = rank_ms
+        if args.config != PMC_CONFIG:
+            out["pmc_note"] = PMC_NOTE
         if world == 1 and not args.no_cpu_baseline and args.config == "c2":
             out["cpu_baseline"] = cpu_baseline()
         print(json.dumps(out))

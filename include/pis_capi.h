@@ -100,7 +100,9 @@ int pis_version(void);
 #define PIS_TUNE_LOSS_ROWMUL 19  /* whole-row loss forward: rows per block multiplier (1 default: about 1024 blocks;
                                     2, 4: fewer blocks, more row batches per thread) */
 #define PIS_TUNE_SLAB_CHUNKS 20  /* thousands of partial slabs over <= 1024 columns (bias gradients): 1 (default)
-                                    two-pass chunked row reduction, 0 one column per block */
+                                    two-pass chunked row reduction, 0 one column per block. Applies to
+                                    reduce_slabs and weights-only reduce_slabs2 calls; a weights + bias
+                                    pair is always one merged single-pass launch (csrc/wgrad.hip) */
 #define PIS_TUNE_WGRAD_PAIR 21   /* bf16x6 weight-gradient GEMM, 64-wide operand tiles: 0 (default) one 4-pixel run per
                                     lane (2-way conflicted ds_write_b64), 1 lane pairs stage the two 8-B halves of one 16-B
                                     chunk (conflict-free; the two 128-B pixel rows per load cost more: enc1.conv1 -4 %, up1
@@ -171,8 +173,11 @@ int pis_version(void);
                                         round-3 strided tile order. HBM reads per launch 2218 -> 1674 MB on
                                         dec1.conv0 (1.38x -> 1.04x algorithmic; enc1.conv1 1.03x either way,
                                         profiles/r4_o_direct_wgrad_traffic.txt), time unchanged (r4_n) */
-#define PIS_TUNE_DIRECT_WGRAD_MAIN 44 /* retired (round 5): direct weight gradients on the main stream were neutral
-                                           (profiles/r4_p_ab_direct_wgrad_main.txt); ignored */
+#define PIS_TUNE_DIRECT_WGRAD_MAIN 44 /* retired as a tune key (ignored): the choice moved to the host schedule's
+                                           PIS_DIRECT_WGRAD_MAIN environment variable (unet.py), whose default
+                                           since round 5 is 1 = direct weight gradients on the main stream, the
+                                           side stream ordered after them before its next weight gradient or
+                                           bucket all-reduce */
 #define PIS_TUNE_GEMM_PRIO 45 /* retired (round 5): s_setprio in the Winograd GEMM was neutral
                                    (profiles/r4_s_ab_gemm_prio.txt); ignored */
 #define PIS_TUNE_WINO_OUT_MPF 46 /* Winograd output transform of a masked input gradient: 1 (default) the tile's

@@ -71,7 +71,7 @@ int launch_wino_input(const float* x, int ldx, int B, int H, int W, int C, float
 int launch_wino_dz(const float* dz, int ldz, int B, int H, int W, int N, float* E, hipStream_t s, int m,
                    float* bpart = nullptr);
 int wino_dz_blocks(int B, int H, int W, int N, int m);
-int wino_dz_blocks_max(int B, int H, int W, int N, int m);  // over pis_tune key 40
+int wino_dz_blocks_max(int B, int H, int W, int N, int m);  // the largest grid a dz pass of F(m x m) launches (rows of bias partials)
 // M: nsplit split-K slabs sstride floats apart, summed in slab order (nsplit > 1 needs m == 4)
 // The F(3x3,4x4) weight gradient's bias gradient, folded into its output-transform launch:
 // db[n] (+)= scale x sum_{r < rows} part[r][n] (fixed order), part = the GEMM's [split][N] column

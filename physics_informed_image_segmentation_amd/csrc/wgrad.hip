@@ -497,11 +497,23 @@ __global__ __launch_bounds__(256) void reduce_slabs2_kernel(SlabJob a, SlabJob b
   else reduce_slab_job<1>(j, blk);
 }
 
-// the two reductions of a weight gradient (weights, then bias; bias may be NULL) in one launch
+int reduce_slabs(const float* part, int splits, int64_t n, float* dst, int accumulate, hipStream_t s);
+
+// reduce_slabs' chunked two-pass regime (many slabs of a short row, PIS_TUNE_SLAB_CHUNKS)
+static bool slabs_chunked(const float* part, int splits, int64_t n, const float* dst) {
+  const bool v4 = (n % 4 == 0) && ((uintptr_t)part % 16 == 0) && ((uintptr_t)dst % 16 == 0);
+  return v4 && splits >= 1024 && n <= 1024 && tune_get(PIS_TUNE_SLAB_CHUNKS) != 0;
+}
+
+// the two reductions of a weight gradient (weights, then bias) in one launch. A weights-only call
+// (bias NULL) is reduce_slabs itself, chunked regime (key 20) included. A weights + bias pair is
+// always the merged single-pass launch, whatever key 20 says: the pair's extra launches of the
+// chunked form cost more than the merged launch saves on the few pairs in that regime (round 5's
+// reduction glue, 53 -> 14 launches per step). NOTE: like reduce_slabs, may overwrite part.
 int reduce_slabs2(const float* part, int splits, int64_t n, float* dst, const float* part_b, int splits_b,
                   int64_t n_b, float* dst_b, int accumulate, hipStream_t s) {
+  if (!dst_b) return reduce_slabs(part, splits, n, dst, accumulate, s);
   const SlabJob a = slab_job_plan(part, splits, n, n, dst, accumulate);
-  if (!dst_b) return reduce_slabs_pitched(part, splits, n, n, dst, accumulate, s);
   const SlabJob b = slab_job_plan(part_b, splits_b, n_b, n_b, dst_b, accumulate);
   hipLaunchKernelGGL(reduce_slabs2_kernel, dim3(a.blocks + b.blocks), dim3(256), 0, s, a, b);
   return launch_status("reduce_slabs2");
@@ -509,8 +521,7 @@ int reduce_slabs2(const float* part, int splits, int64_t n, float* dst, const fl
 
 // NOTE: may overwrite part (every caller passes its own partial-slab scratch)
 int reduce_slabs(const float* part, int splits, int64_t n, float* dst, int accumulate, hipStream_t s) {
-  const bool v4 = (n % 4 == 0) && ((uintptr_t)part % 16 == 0) && ((uintptr_t)dst % 16 == 0);
-  if (v4 && splits >= 1024 && n <= 1024 && tune_get(PIS_TUNE_SLAB_CHUNKS) != 0) {
+  if (slabs_chunked(part, splits, n, dst)) {
     const int G = std::min(256, splits / 16);
     const int chunk = (int)cdiv(splits, G), nblk = (int)cdiv(splits, chunk);
     hipLaunchKernelGGL(reduce_rows_chunk_kernel, dim3(nblk), dim3(256), 0, s, const_cast<float*>(part), splits,

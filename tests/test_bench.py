@@ -85,6 +85,40 @@ def test_bench_launches_n_ranks():
     assert ex["steps"] == 2 and len(ex["mean_per_rank"]) == 2
     assert all(v >= 0.0 for v in ex["mean_per_rank"])
     assert ex["max_over_ranks"] == max(ex["mean_per_rank"]) and ex["worst_step_max_over_ranks"] >= ex["max_over_ranks"]
+    # each rank's own step time (straggling): the line's ms_per_step is their maximum
+    rm = d["ms_per_step_by_rank"]
+    assert len(rm["per_rank"]) == 2 and all(v > 0 for v in rm["per_rank"])
+    assert rm["min"] == min(rm["per_rank"]) and rm["max"] == max(rm["per_rank"])
+    assert abs(rm["max"] - d["ms_per_step"]) <= 1e-9 * d["ms_per_step"]
+
+
+@pytest.mark.gpu
+def test_bench_other_config_reports_no_c2_counters():
+    """A --config other than C2 must not carry C2's committed PMC counters as its own (VERDICT r5
+    weak #11): traffic / MFMA-busy fields are null and the line says why."""
+    out = subprocess.run([sys.executable, os.path.join(HERE, "bench.py"), "--config", "c4-rd", "--steps", "2",
+                          "--warmup", "1", "--no-cpu-baseline"], capture_output=True, text=True, timeout=110, cwd=HERE)
+    assert out.returncode == 0, out.stderr[-2000:]
+    d = json.loads([ln for ln in out.stdout.splitlines() if ln.startswith("{")][-1])
+    assert "C2 only" in d["pmc_note"]
+    g = d["roofline_gemm"]
+    assert g["traffic"] is None and g["mfma_busy_frac"] is None and g["mfma_busy_by_kernel"] is None
+    for k in ("roofline_fused", "roofline_direct_fwd", "roofline_direct_wgrad"):
+        if d.get(k):
+            assert d[k]["traffic"] is None, k
+    assert d["roofline_loss"]["head_loss_fwd_kernel_live"]["traffic"] is None
+
+
+def test_pmc_fields_only_for_the_profiled_config():
+    """profiles/pmc_dominant.json holds C2's counters: read for C2, None for every other config."""
+    b = _bench()
+    assert b.PMC_CONFIG == "c2"
+    for cfg in ("c4-rd", "c5"):
+        assert b.load_pmc(b.DOMINANT_KERNEL, cfg) == (None, None, None)
+        assert b.pmc_bytes("gemm_nt_h3_", cfg) is None
+    traffic, busy, by_kernel = b.load_pmc("gemm_nt_h3_", "c2")
+    assert traffic and 0 < busy < 1 and by_kernel
+    assert b.pmc_bytes("gemm_nt_h3_", "c2") > 0
 
 
 def test_bench_rejects_world_mismatch():

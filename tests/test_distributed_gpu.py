@@ -44,9 +44,12 @@ def _loss():
     return DiceBCEPDELoss(pde_weight=1e-2, phase_field_weight=1e-2, diffusion_coeff=5.0, epsilon=0.05)
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, k29=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.cuda.set_device(0)
+    if k29 is not None:
+        from physics_informed_image_segmentation_amd import _hip
+        _hip.lib().pis_tune(29, k29)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from physics_informed_image_segmentation_amd.distributed import GradBucketer, broadcast_parameters
@@ -67,11 +70,15 @@ def _worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_two_rank_bucketed_allreduce_on_gpu(hip):
+# k29 = 2 engages the direct fp16x3 layers at 64 x 64 (the default picks none there): their weight
+# gradients run on the MAIN stream and the weight-gradient stream is ordered after them before a
+# bucket's all-reduce is issued from it; a missing order would all-reduce stale bytes
+@pytest.mark.parametrize("k29", [None, 2], ids=["default", "direct"])
+def test_two_rank_bucketed_allreduce_on_gpu(hip, k29):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, k29)) for r in range(2)]
     for p in procs:
         p.start()
     res = dict((r, (g, nb)) for r, g, nb in (q.get(timeout=300) for _ in procs))
@@ -79,15 +86,21 @@ def test_two_rank_bucketed_allreduce_on_gpu(hip):
         p.join(timeout=120)
     assert all(p.exitcode == 0 for p in procs)
     # expectation: per-shard gradients from the same kernels, summed
-    net = _model()
-    crit = _loss()
-    total = torch.zeros_like(net.arena)
-    for r in range(2):
-        net.zero_grad(set_to_none=True)
-        x, t = _shard(r)
-        crit(net(x), t).backward()
-        total += net.grad_arena()
-    total = total.cpu()
+    from physics_informed_image_segmentation_amd import _hip
+    prev = _hip.lib().pis_tune(29, k29) if k29 is not None else None
+    try:
+        net = _model()
+        crit = _loss()
+        total = torch.zeros_like(net.arena)
+        for r in range(2):
+            net.zero_grad(set_to_none=True)
+            x, t = _shard(r)
+            crit(net(x), t).backward()
+            total += net.grad_arena()
+        total = total.cpu()
+    finally:
+        if prev is not None:
+            _hip.lib().pis_tune(29, prev)
     for r in range(2):
         g, nb = res[r]
         g = torch.from_numpy(g)

@@ -56,10 +56,13 @@ def _run(bucketed):
             torch.stack(losses).cpu().numpy().copy(), nb)
 
 
-def _worker(port, q):
+def _worker(port, q, k29):
     import torch.distributed as dist
+    from physics_informed_image_segmentation_amd import _hip
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.cuda.set_device(0)
+    if k29 is not None:
+        _hip.lib().pis_tune(29, k29)
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
     try:
         assert dist.get_backend() == "nccl"
@@ -70,10 +73,14 @@ def _worker(port, q):
         dist.destroy_process_group()
 
 
-def test_rccl_bucketed_step_equals_single_process(hip):
+# k29 = 2: every 3x3 conv the direct fp16x3 kernels can take runs them (at 64 x 64 the default
+# picks none), so the direct weight gradients — on the MAIN stream, the side stream ordered after
+# them before a bucket's all-reduce starts — feed the RCCL buckets
+@pytest.mark.parametrize("k29", [None, 2], ids=["default", "direct"])
+def test_rccl_bucketed_step_equals_single_process(hip, k29):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    p = ctx.Process(target=_worker, args=(_free_port(), q))
+    p = ctx.Process(target=_worker, args=(_free_port(), q, k29))
     p.start()
     plain, rccl = q.get(timeout=300)
     p.join(timeout=120)
