@@ -202,6 +202,11 @@ int pis_debug_gemm_nt(const float* A, const float* B, float* C, int M, int N, in
 int pis_debug_stream_probe(const float* a, const float* b, float* dst, int64_t n, float* partial, int grid,
                            pis_stream_t stream);
 
+/* Tooling (tools/bench_head_loss.py --probe): read n floats (n % 4096 == 0) in 16-KB chunks with 1024-thread
+ * blocks, eight chunks in flight per lane: mode 0 grid-stride sweep (concurrent reads in one window),
+ * mode 1 one contiguous run per block (the row-band kernels' order); partial[grid * 16] wave sums. */
+int pis_debug_band_probe(const float* a, int64_t n, int mode, float* partial, int grid, pis_stream_t stream);
+
 /* Scheduling aid: arm an event (hipEvent_t) that the next F(4x4,3x3) convolution launched on this
  * thread (pis_conv3x3_fwd_ex / _dgrad_ex / _fwd_keep / _fwd_pool) records on its stream right after
  * its 36 contractions, before the output transform; the slot then disarms. Lets a caller start

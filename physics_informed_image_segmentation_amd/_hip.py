@@ -51,6 +51,7 @@ _SIGNATURES = {
     "pis_tune": ([I, I], c_int),
     "pis_debug_gemm_nt": ([P, P, P, I, I, I, I, I, P], c_int),
     "pis_debug_stream_probe": ([P, P, P, L, P, I, P], c_int),
+    "pis_debug_band_probe": ([P, L, I, P, I, P], c_int),
     "pis_conv3x3_dgrad_direct": ([I, I, I, I, I, I, Z], c_int),
     "pis_conv3x3_bwd_prep": ([P, I, I, I, I, I, I, P, Z, P, Z, P], c_int),
     "pis_conv3x3_filter_bytes": ([I, I, I, I, I, I], c_size_t),

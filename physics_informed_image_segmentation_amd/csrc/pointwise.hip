@@ -258,6 +258,28 @@ __global__ __launch_bounds__(256) void stream_probe_kernel(const f32x4* __restri
   }
 }
 
+// Access-order probe (tooling): a 1024-thread block per CU reads 16-KB chunks (one float4 per lane),
+// eight chunks in flight per lane. mode 0 sweeps: pass i of block p reads chunk i * grid + p, so the
+// grid's concurrent reads sit in one window; mode 1 bands: block p reads its own contiguous run of
+// chunks (the row-band kernels' order: concurrent reads spread over the whole buffer).
+__global__ __launch_bounds__(1024) void band_probe_kernel(const f32x4* __restrict__ a, int64_t nchunk, int mode,
+                                                          float* partial) {
+  const int64_t per = nchunk / gridDim.x;
+  float acc = 0.f;
+  for (int64_t i = 0; i + 8 <= per; i += 8) {
+    f32x4 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int64_t c = mode == 0 ? (i + u) * gridDim.x + blockIdx.x : blockIdx.x * per + i + u;
+      v[u] = a[c * 1024 + threadIdx.x];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc += (v[u][0] + v[u][1]) + (v[u][2] + v[u][3]);
+  }
+  acc = wave_sum(acc);
+  if ((threadIdx.x & 63) == 0) partial[blockIdx.x * 16 + (threadIdx.x >> 6)] = acc;
+}
+
 }  // namespace pis
 
 using namespace pis;
@@ -356,4 +378,13 @@ extern "C" int pis_debug_stream_probe(const float* a, const float* b, float* dst
                      reinterpret_cast<const f32x4*>(a), reinterpret_cast<const f32x4*>(b),
                      reinterpret_cast<f32x4*>(dst), n / 4, partial);
   return launch_status("stream_probe");
+}
+
+extern "C" int pis_debug_band_probe(const float* a, int64_t n, int mode, float* partial, int grid,
+                                    pis_stream_t stream) {
+  PIS_CHECK_ARG(a && partial && grid > 0 && n % 4096 == 0 && (mode == 0 || mode == 1),
+                "pis_debug_band_probe: bad arguments");
+  hipLaunchKernelGGL(band_probe_kernel, dim3(grid), dim3(1024), 0, (hipStream_t)stream,
+                     reinterpret_cast<const f32x4*>(a), n / 4096, mode, partial);
+  return launch_status("band_probe");
 }
