@@ -14,8 +14,6 @@
 // No MFMA anywhere: these are bandwidth-bound stencils.
 #include "common.h"
 
-#include <mutex>
-
 namespace pis {
 
 int reduce_slabs(const float* part, int splits, int64_t n, float* dst, int accumulate, hipStream_t s);
@@ -930,436 +928,6 @@ __global__ __launch_bounds__(NT) void head_loss_fwd_kernel(HeadLossFwdArgs h) {
 }
 
 // ---------------------------------------------------------------------------
-// The same fused head + loss forward with the loss STREAMED behind the head (pis_tune(38, 3), W % 512
-// == 0, W <= 2048). head_loss_fwd_kernel runs its blocks in two phases — every
-// staged row's head, a barrier, then the loss of the band — so at C2 (512 blocks, one 1024-thread
-// block per CU by registers: two rounds) each round ends in a loss phase and a reduction that move
-// no bytes. Here the loss of staged row m runs right after staged row m + 1's head (one barrier per
-// row): the rows' loads stream on while a 1/G share of the threads (G = 1024 / (W / 4) row groups,
-// rotating per row) computes it, its targets loaded a row ahead. z and u are staged in LDS and
-// written by that row group as whole float4 rows (the 16-lane head groups stored one scalar per
-// pixel: twice as many store instructions as the head input's loads). The fixed-order finalize runs
-// in the grid's last block to finish (ticket: one agent-scope add per block after its partials are
-// stored write-through (sc1) and waited for; the last block reads them with sc1 loads —
-// MI355X_MICROARCH.md 'inter-workgroup visibility', first hand-off row), so the call is one launch.
-// Same head arithmetic (z, u bitwise pis_head_fwd's), same per-pixel loss formulas.
-// ---------------------------------------------------------------------------
-constexpr int LOSS_TICKET_SLOTS = 64;
-__device__ unsigned g_loss_ticket[LOSS_TICKET_SLOTS];  // zero at load; each use leaves it zero
-
-template <typename T>
-__device__ __forceinline__ void st_sc1(T* p, T v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
-template <typename T>
-__device__ __forceinline__ T ld_sc1(const T* p) {
-  return __hip_atomic_load(const_cast<T*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// the block partials (wave sums in a fixed order) of the nine running sums, stored write-through;
-// returns true in every thread of the block that finished last (ticket >= 0), which then holds
-// every block's partials
-template <int NT>
-__device__ __forceinline__ bool store_partials_ticket(const LossArgs& g, int blk, int nblk, int ticket, float* lds,
-                                                      float v0, float v1, float v2, float v3, float v4, float v5,
-                                                      int c_i, int c_p, int c_t) {
-  constexpr int NWV = NT / 64;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  __syncthreads();  // lds is free
-  float* fr = lds;                                  // [NWV][6]
-  int* ir = reinterpret_cast<int*>(lds + 6 * NWV);  // [NWV][3]
-  int* flag = ir + 3 * NWV;
-  if (lane == 0) {
-    fr[wave * 6 + 0] = v0;
-    fr[wave * 6 + 1] = v1;
-    fr[wave * 6 + 2] = v2;
-    fr[wave * 6 + 3] = v3;
-    fr[wave * 6 + 4] = v4;
-    fr[wave * 6 + 5] = v5;
-    ir[wave * 3 + 0] = c_i;
-    ir[wave * 3 + 1] = c_p;
-    ir[wave * 3 + 2] = c_t;
-  }
-  __syncthreads();
-  if (wave == 0) {  // lanes 0..8 store; the same wave then waits for them and takes the ticket
-    if (lane < 6) {
-      float v = fr[lane];
-#pragma unroll
-      for (int w = 1; w < NWV; ++w) v += fr[6 * w + lane];
-      st_sc1(&g.fpart[blk * 6 + lane], v);
-    } else if (lane < 9) {
-      const int j = lane - 6;
-      int c = ir[j];
-#pragma unroll
-      for (int w = 1; w < NWV; ++w) c += ir[3 * w + j];
-      st_sc1(&g.ipart[blk * 3 + j], c);
-    }
-    if (ticket >= 0) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (lane == 0) {
-        const unsigned old =
-            __hip_atomic_fetch_add(&g_loss_ticket[ticket], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        *flag = old == (unsigned)(nblk - 1);
-      }
-    }
-  }
-  if (ticket < 0) return false;
-  __syncthreads();
-  return *flag != 0;
-}
-
-// the fixed-order finalize of loss_finalize_rows_kernel by NT threads of the last block (sc1 loads
-// of every block's partials); resets the ticket
-template <int NT>
-__device__ void finalize_rows_block(const LossRowArgs& a, int ticket, float* lds, const float* bpart = nullptr,
-                                    int npairs = 0) {
-  const LossArgs& g = a.g;
-  const int nblk = g.B * a.bands, tid = threadIdx.x;
-  constexpr int NWV = NT / 64, PB = LOSS_MAX_BLOCKS / NT, PI = LOSS_MAX_BLOCKS * 3 / NT;
-  double* red = reinterpret_cast<double*>(lds);         // [NWV][6]
-  int* si = reinterpret_cast<int*>(lds + 2 * 6 * NWV);  // [LOSS_MAX_BLOCKS * 3]
-  float v[PB][6];
-  int vi[PI];
-#pragma unroll
-  for (int i = 0; i < PB; ++i) {
-    const int k = tid + NT * i;
-#pragma unroll
-    for (int j = 0; j < 6; ++j) v[i][j] = k < nblk ? ld_sc1(&g.fpart[k * 6 + j]) : 0.f;
-  }
-#pragma unroll
-  for (int i = 0; i < PI; ++i) {
-    const int k = tid + NT * i;
-    vi[i] = k < nblk * 3 ? ld_sc1(&g.ipart[k]) : 0;
-  }
-  if (tid == 0) st_sc1(&g_loss_ticket[ticket], 0u);  // every block has added: ready for the next launch
-  __syncthreads();  // lds (the caller's partial scratch) is free
-#pragma unroll
-  for (int i = 0; i < PI; ++i) si[tid + NT * i] = vi[i];
-  // doubles as loss_finalize_rows_kernel: thread k owns blocks k, k + NT, ... (a different but
-  // fixed association from its 256-thread form)
-  double s[6];
-#pragma unroll
-  for (int j = 0; j < 6; ++j) {
-    s[j] = 0.0;
-#pragma unroll
-    for (int i = 0; i < PB; ++i) s[j] += (double)v[i][j];
-    s[j] = wave_sum_d(s[j]);
-  }
-  const int lane = tid & 63, wave = tid >> 6;
-  if (lane == 0)
-#pragma unroll
-    for (int j = 0; j < 6; ++j) red[wave * 6 + j] = s[j];
-  __syncthreads();
-  {
-    const int bps = a.bands;
-    int G = 1;
-    while (G < 64 && g.B * G * 2 <= NT) G *= 2;
-    const int grp = tid / G, gl = tid % G, ngrp = NT / G;
-    const int iters = (g.B + ngrp - 1) / ngrp;
-    for (int it = 0; it < iters; ++it) {
-      const int b = grp + it * ngrp;
-      int ci = 0, cp = 0, ct = 0;
-      if (b < g.B)
-        for (int k = gl; k < bps; k += G) {
-          const int blk = b * bps + k;
-          ci += si[blk * 3 + 0];
-          cp += si[blk * 3 + 1];
-          ct += si[blk * 3 + 2];
-        }
-      for (int off = 1; off < G; off <<= 1) {
-        ci += __shfl_xor(ci, off, 64);
-        cp += __shfl_xor(cp, off, 64);
-        ct += __shfl_xor(ct, off, 64);
-      }
-      if (gl == 0 && b < g.B) store_counts(a, b, ci, cp, ct);
-    }
-  }
-  // the band-boundary pairs' stencil terms (head_loss_fwd_pipe_kernel): wave 0, fixed order
-  double b0 = 0.0, b1 = 0.0;
-  if (npairs > 0 && wave == 0) {
-    for (int k = lane; k < npairs; k += 64) {
-      b0 += (double)ld_sc1(&bpart[2 * k]);
-      b1 += (double)ld_sc1(&bpart[2 * k + 1]);
-    }
-    b0 = wave_sum_d(b0);
-    b1 = wave_sum_d(b1);
-  }
-  if (tid == 0) {
-    double tot[6];
-#pragma unroll
-    for (int j = 0; j < 6; ++j) {
-      tot[j] = red[j];
-#pragma unroll
-      for (int w = 1; w < NWV; ++w) tot[j] += red[w * 6 + j];
-    }
-    tot[4] += b0;
-    tot[5] += b1;
-    finalize_rows_store(g, tot, a.terms);
-  }
-}
-
-// LDS floats the finalize needs (red doubles + the counters)
-template <int NT>
-constexpr size_t finalize_rows_lds_floats() { return 2 * 6 * (NT / 64) + 3 * LOSS_MAX_BLOCKS; }
-
-// 16-byte global store / load that bypass the CU's L1 (sc1, write-through): the band-boundary hand-off
-// (MI355X_MICROARCH.md 'inter-workgroup visibility', first hand-off row). The load waits for itself
-// (the compiler does not track inline-asm loads): callers issue ONE per thread before a barrier.
-__device__ __forceinline__ void st16_sc1(float* p, f32x4 v) {
-  asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
-}
-__device__ __forceinline__ f32x4 ld16_sc1(const float* p) {
-  f32x4 v;
-  asm volatile("global_load_dwordx4 %0, %1, off sc1\n\ts_waitcnt vmcnt(0)" : "=v"(v) : "v"(p) : "memory");
-  return v;
-}
-
-// Band-boundary tickets: pair (k - 1, k) of sample b is slot b (bands - 1) + k - 1; each of the two
-// blocks adds 1 once its u rows are stored, the second (add returned 1) takes the pair's stencil terms
-// and resets the counter
-__device__ unsigned g_loss_bticket[LOSS_TICKET_SLOTS][LOSS_MAX_BLOCKS];
-
-// DBG (timing twins, wrong results; pis_tune(38, 4 / 5 / 6)): 1 the loads only (no head, no loss), 2 no loss
-// rows, 3 no z / u stores
-//
-// No halo rows: a band stages only its own rows (head_loss_fwd_kernel recomputes u of the two rows
-// beside its band from their 256 B/px: a quarter more loads at C2, L2 hits that still cost their
-// issue). A row whose stencil neighbours (reflect-resolved) lie in the band gets every term from its
-// owner; the two rows beside an internal band boundary get their pointwise terms (Dice, BCE, the
-// counters, W(u)) from their owners and their stencil terms (the RD residual, |grad u|^2) from the
-// block of the pair that finishes second, which reads the four rows around the boundary back (sc1)
-// into LDS: bpart[pair][2], summed in a fixed order by the finalize. The sigmoid runs per batch of G
-// rows on every lane (not on one lane of each 16-lane head group).
-template <bool RD, bool PF, int DBG = 0>
-__global__ __launch_bounds__(1024) void head_loss_fwd_pipe_kernel(HeadLossFwdArgs h, int ticket, float* bpart) {
-  constexpr int NT = 1024, PP = 8, NG = NT / 16;
-  constexpr bool ST = RD || PF;
-  extern __shared__ __attribute__((aligned(16))) float su[];  // u [R][SW] (column c at c + 4), then z [R][SW]
-  const LossArgs& g = h.a.g;
-  const int H = g.H, W = g.W, SW = W + 8;
-  float* sz = su + (size_t)h.R * SW;
-  const Remap2 rmp = xcd_remap2();  // consecutive bands of a sample on one XCD
-  const int band = rmp.bid, b = rmp.batch, bands = h.a.bands;
-  const int y0 = band * h.R, nr = min(h.R, H - y0);
-  const int tid = threadIdx.x, sub = tid & 15, grp = tid >> 4;
-  const size_t HW = (size_t)H * W;
-  const float* xb = h.x + (size_t)b * HW * h.ldx + 4 * sub;
-  const f32x4 wv = *reinterpret_cast<const f32x4*>(h.w + 4 * sub);
-  const float bias = h.bias[0];
-  const int W4 = W >> 2, G = NT / W4;  // loss: row group lg (G of them, W4 threads each, one 4-px item per thread)
-  const int lg = tid / W4, q = tid - lg * W4;
-  const float* tt = g.t + (size_t)b * HW;
-  const size_t obase = (size_t)b * HW;
-  const int cpr = W / (NG * PP), nchunk = nr * cpr;
-  f32x4 xa[PP], xn[PP];
-  // the targets of this thread's next loss row (a batch = up to G consecutive rows; row mdone + lg is
-  // thread group lg's), fetched a whole batch ahead: right after the previous batch
-  f32x4 tq = {0.f, 0.f, 0.f, 0.f};
-  auto fetch_t = [&](int m) __attribute__((always_inline)) {
-    if (lg < G && m < nr) tq = *reinterpret_cast<const f32x4*>(tt + (size_t)(y0 + m) * W + 4 * q);
-  };
-  auto load = [&](f32x4 (&xv)[PP], int ch) __attribute__((always_inline)) {
-    const int r = ch / cpr, x0 = (ch - r * cpr) * (NG * PP) + grp;
-    const float* row = xb + (size_t)(y0 + r) * W * h.ldx;
-#pragma unroll
-    for (int j = 0; j < PP; ++j) xv[j] = *reinterpret_cast<const f32x4*>(row + (size_t)(x0 + NG * j) * h.ldx);
-  };
-  float dbg_sink = 0.f;
-  auto head = [&](const f32x4 (&xv)[PP], int ch) __attribute__((always_inline)) {
-    const int r = ch / cpr, x0 = (ch - r * cpr) * (NG * PP) + grp;
-    if constexpr (DBG == 1) {
-#pragma unroll
-      for (int j = 0; j < PP; ++j) dbg_sink += (xv[j][0] + xv[j][1]) + (xv[j][2] + xv[j][3]);
-      return;
-    }
-#pragma unroll
-    for (int j = 0; j < PP; ++j) {
-      float s = 0.f;
-      s = fmaf(xv[j][0], wv[0], s);
-      s = fmaf(xv[j][1], wv[1], s);
-      s = fmaf(xv[j][2], wv[2], s);
-      s = fmaf(xv[j][3], wv[3], s);
-      s = group16_sum(s);  // as head_fwd64_kernel (csrc/pointwise.hip): z bitwise pis_head_fwd's
-      if (sub == 0) sz[r * SW + 4 + x0 + NG * j] = s + bias;
-    }
-  };
-  constexpr float kLn2 = 0.69314718055994531f, kClamp2 = -144.26950408889634f;  // -100 / ln 2
-  float s_it = 0.f, s_p = 0.f, s_t = 0.f, s_bce2 = 0.f, s_rd = 0.f, s_g2 = 0.f, s_q2 = 0.f;
-  int c_i = 0, c_p = 0, c_t = 0;
-  // the stencil terms of one 4-pixel item: p its u, uv / dv the rows above / below, lft / rgt the
-  // reflect-resolved left / right neighbours
-  auto stencil = [&](const f32x4& pv, const f32x4& uv, const f32x4& dv, float lft, float rgt, float& rd,
-                     float& g2) __attribute__((always_inline)) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const float p = pv[i];
-      const float ul = i == 0 ? lft : pv[i - 1], ur = i == 3 ? rgt : pv[i + 1];
-      const float uu = uv[i], ud = dv[i];
-      if (RD) {
-        const float qq = fmaf(-p, p, p);  // p (1 - p)
-        const float lap = (uu + ud) + (ul + ur) - 4.f * p;
-        const float rr = fmaf(g.D, lap, g.rx * qq * (p - g.a));
-        rd = fmaf(rr, rr, rd);
-      }
-      if (PF) {
-        const float gx = ur - ul, gy2 = ud - uu;  // 2x the central differences
-        g2 = fmaf(gx, gx, fmaf(gy2, gy2, g2));
-      }
-    }
-  };
-  // loss row m (staged row m = image row y0 + m): pointwise terms always, stencil terms when both
-  // reflect-resolved vertical neighbours are rows of this band
-  auto loss_row = [&](int m) __attribute__((always_inline)) {
-    const int y = y0 + m;
-    const float* sc = su + m * SW + 4 + 4 * q;
-    const f32x4 pv = *reinterpret_cast<const f32x4*>(sc);
-    const size_t o = obase + (size_t)y * W + 4 * q;
-    if (DBG == 3) {
-    } else if (m < 2 || m >= nr - 2) {
-      st16_sc1(h.u + o, pv);  // rows a boundary hand-off may read back
-    } else {
-      *reinterpret_cast<f32x4*>(h.u + o) = pv;
-    }
-    if (DBG != 3) *reinterpret_cast<f32x4*>(h.z + o) = *reinterpret_cast<const f32x4*>(sz + m * SW + 4 + 4 * q);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const float p = pv[i], t = tq[i];
-      s_it = fmaf(p, t, s_it);
-      s_p += p;
-      s_t += t;
-      s_bce2 += (t - 1.f) * fmaxf(__builtin_amdgcn_logf(1.f - p), kClamp2) - t * fmaxf(__builtin_amdgcn_logf(p), kClamp2);
-      const bool pb = p > g.thr, tb = t > 0.5f;
-      c_p += pb;
-      c_t += tb;
-      c_i += pb && tb;
-      if (PF) {
-        const float qq = fmaf(-p, p, p);
-        s_q2 = fmaf(qq, qq, s_q2);
-      }
-    }
-    if (ST) {
-      const int yu = refl(y - 1, H), yd = refl(y + 1, H);
-      if (yu >= y0 && yu < y0 + nr && yd >= y0 && yd < y0 + nr) {
-        const f32x4 uv = *reinterpret_cast<const f32x4*>(su + (yu - y0) * SW + 4 + 4 * q);
-        const f32x4 dv = *reinterpret_cast<const f32x4*>(su + (yd - y0) * SW + 4 + 4 * q);
-        const float lft = q == 0 ? sc[1] : sc[-1];       // reflect: column -1 is column 1
-        const float rgt = 4 * q + 4 == W ? sc[2] : sc[4];  // column W is column W - 2
-        stencil(pv, uv, dv, lft, rgt, s_rd, s_g2);
-      }
-    }
-  };
-  // loss rows in batches of up to G: row m is ready once row m + 1 is staged (the last row at once). A
-  // batch first turns the z of every staged row not yet converted into u (1 / (1 + e^-z), every lane
-  // busy), then each thread takes one 4-pixel item: the loss work is spread over all waves and runs
-  // while the next chunks' loads are in flight (two barriers per batch)
-  int mdone = 0, cdone = 0;
-  fetch_t(lg);
-  auto after = [&](int ch) __attribute__((always_inline)) {
-    const int k = ch / cpr;
-    if (ch - k * cpr != cpr - 1) return;  // staged row k not complete yet
-    const int ready = k == nr - 1 ? nr : k;
-    if (ready - mdone < G && k != nr - 1) return;
-    __syncthreads();
-    if ((DBG == 0 || DBG == 3) && lg < G) {
-      for (int r = cdone + lg; r <= k; r += G) {  // thread (lg, q): float4 q of rows cdone + lg, + 2 G, ...
-        const f32x4 zz = *reinterpret_cast<const f32x4*>(sz + r * SW + 4 + 4 * q);
-        f32x4 uu;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) uu[i] = 1.f / (1.f + expf(-zz[i]));  // as pis_head_fwd: u bitwise
-        *reinterpret_cast<f32x4*>(su + r * SW + 4 + 4 * q) = uu;
-      }
-    }
-    cdone = k + 1;
-    __syncthreads();
-    const int m = mdone + lg;
-    if ((DBG == 0 || DBG == 3) && lg < G && m < ready) loss_row(m);
-    mdone = ready;
-    fetch_t(mdone + lg);
-  };
-  if (nchunk > 0) load(xa, 0);
-  for (int ch = 0; ch < nchunk; ch += 2) {  // ping-pong register sets (no copies)
-    if (ch + 1 < nchunk) load(xn, ch + 1);
-    head(xa, ch);
-    after(ch);
-    if (ch + 2 < nchunk) load(xa, ch + 2);
-    if (ch + 1 < nchunk) {
-      head(xn, ch + 1);
-      after(ch + 1);
-    }
-  }
-  if (DBG == 1) s_it += dbg_sink;
-  const int lane = tid & 63, wave = tid >> 6;
-  int* sflag = reinterpret_cast<int*>(su + 2 * (size_t)h.R * SW);  // [2]: the pairs this block takes
-  // 1. the band-boundary pairs: both neighbours' u rows stored (sc1, waited for), then one add each
-  if (ST) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's u stores
-    __syncthreads();
-    if (tid == 0) {
-      int take0 = 0, take1 = 0;
-      if (ticket >= 0 && band > 0)
-        take0 = __hip_atomic_fetch_add(&g_loss_bticket[ticket][b * (bands - 1) + band - 1], 1u, __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT) == 1u;
-      if (ticket >= 0 && band < bands - 1)
-        take1 = __hip_atomic_fetch_add(&g_loss_bticket[ticket][b * (bands - 1) + band], 1u, __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT) == 1u;
-      sflag[0] = take0;
-      sflag[1] = take1;
-    }
-    __syncthreads();
-    const int take0 = sflag[0], take1 = sflag[1];
-    for (int side = 0; side < 2; ++side) {
-      if (!(side == 0 ? take0 : take1)) continue;
-      // pair (kb - 1, kb): rows a = yc - 1 (band kb - 1's last) and c = yc (band kb's first)
-      const int kb = side == 0 ? band : band + 1, pair = b * (bands - 1) + kb - 1;
-      const int yc = kb * h.R, ya = yc - 1;
-      const int ra = refl(ya - 1, H), rd3 = refl(yc + 1, H);
-      float* sb = su;  // [4][SW] (column c at c + 4): rows ya - 1, ya, yc, yc + 1 (reflect-resolved)
-      __syncthreads();  // su is free (the previous pair's reads are done)
-      for (int e = tid; e < 4 * W4; e += NT) {
-        const int r = e / W4, c4 = e - r * W4;
-        const int yr = r == 0 ? ra : r == 1 ? ya : r == 2 ? yc : rd3;
-        *reinterpret_cast<f32x4*>(sb + r * SW + 4 + 4 * c4) = ld16_sc1(h.u + obase + (size_t)yr * W + 4 * c4);
-      }
-      __syncthreads();
-      float rd = 0.f, g2 = 0.f;
-      if (tid < 2 * W4) {
-        const int which = tid / W4, c4 = tid - which * W4;  // 0: row a (rows 0, 1, 2), 1: row c (1, 2, 3)
-        const float* sc = sb + (1 + which) * SW + 4 + 4 * c4;
-        const f32x4 pv = *reinterpret_cast<const f32x4*>(sc);
-        const f32x4 uv = *reinterpret_cast<const f32x4*>(sc - SW), dv = *reinterpret_cast<const f32x4*>(sc + SW);
-        const float lft = c4 == 0 ? sc[1] : sc[-1], rgt = 4 * c4 + 4 == W ? sc[2] : sc[4];
-        stencil(pv, uv, dv, lft, rgt, rd, g2);
-      }
-      const float vr = wave_sum(rd), vg = wave_sum(0.125f * g.eps * g2);
-      __syncthreads();
-      float* fr = su + 4 * SW;  // [NT / 64][2]
-      if (lane == 0) {
-        fr[2 * wave] = vr;
-        fr[2 * wave + 1] = vg;
-      }
-      __syncthreads();
-      if (tid < 2) {  // wave 0: stored write-through before its ticket add below
-        float v = fr[tid];
-#pragma unroll
-        for (int w = 1; w < NT / 64; ++w) v += fr[2 * w + tid];
-        st_sc1(&bpart[pair * 2 + tid], v);
-      }
-      if (tid == 0) st_sc1(&g_loss_bticket[ticket][pair], 0u);  // both blocks have added: ready for the next launch
-    }
-  }
-  // 2. the block partials and the grid ticket; the last block runs the finalize
-  const float v0 = wave_sum(s_it), v1 = wave_sum(s_p), v2 = wave_sum(s_t), v3 = wave_sum(s_bce2 * kLn2);
-  const float v4 = wave_sum(s_rd), v5 = wave_sum(0.125f * g.eps * s_g2 + s_q2 / g.eps);
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) {
-    c_i += __shfl_xor(c_i, off, 64);
-    c_p += __shfl_xor(c_p, off, 64);
-    c_t += __shfl_xor(c_t, off, 64);
-  }
-  const int nblk = g.B * bands;
-  if (store_partials_ticket<NT>(g, b * bands + band, nblk, ticket, su, v0, v1, v2, v3, v4, v5, c_i, c_p, c_t))
-    finalize_rows_block<NT>(h.a, ticket, su, ST ? bpart : nullptr, ST ? g.B * (bands - 1) : 0);
-}
-
-// ---------------------------------------------------------------------------
 // Loss backward fused into the head backward (the consumer of dL/du): one
 // block = R whole image rows. The block stages u for rows y0-2 .. y0+R+1 (reflect
 // resolved, 2 halo columns), the RD residual of rows y0-1 .. y0+R, and dL/dz of
@@ -1709,38 +1277,16 @@ static int head_loss_fwd_pp(int W) { return W % 256 == 0 ? 16 : W % 128 == 0 ? 8
 static bool head_loss_fwd_wide(int W) { return W % 512 == 0 && tune_get(PIS_TUNE_HEAD_LOSS_WIDE) != 0; }
 
 extern "C" size_t pis_head_loss_fwd_ws(int B, int H, int W) {
-  // sized for one row per block, so a later key-36 change cannot outgrow a planned workspace; the
-  // streamed form (key 38 = 3) adds 2 floats per band boundary after the counters
+  // sized for one row per block, so a later key-36 change cannot outgrow a planned workspace
   const size_t nblk = (size_t)B * H;
   (void)W;
-  return 16 + nblk * (6 * sizeof(float) + 3 * sizeof(int) + 2 * sizeof(float)) + 256;
+  return 16 + nblk * (6 * sizeof(float) + 3 * sizeof(int)) + 256;
 }
 
 // the staged u rows, (R + 2) x (W + 8) floats, must fit one workgroup's LDS (160 KB on gfx950); a
 // shape that does not (e.g. B = 128 at 1024^2: R = 64, 272 KB) takes pis_head_fwd + pis_loss_fwd
 static constexpr size_t kHeadLossFwdMaxLds = 160 * 1024;
 static size_t head_loss_fwd_smem(int R, int W) { return (size_t)(R + 2) * (W + 8) * sizeof(float); }
-
-// the streamed form's LDS: the band's u and z rows + 2 flags, at least the boundary hand-off's 4 rows
-// and the last block's finalize
-static size_t head_loss_pipe_smem(int R, int W) {
-  const size_t f = 2 * (size_t)R * (W + 8) + 2;
-  return std::max({f, 4 * (size_t)(W + 8) + 32, finalize_rows_lds_floats<1024>()}) * sizeof(float);
-}
-
-// a ticket slot (g_loss_ticket) per stream: launches on one stream run in order, so a slot is never
-// used by two launches at once; -1 when every slot is taken (the caller launches the finalize)
-static int loss_ticket_slot(hipStream_t s) {
-  static std::mutex mu;
-  static hipStream_t keys[LOSS_TICKET_SLOTS];
-  static int n = 0;
-  std::lock_guard<std::mutex> lk(mu);
-  for (int i = 0; i < n; ++i)
-    if (keys[i] == s) return i;
-  if (n == LOSS_TICKET_SLOTS) return -1;
-  keys[n] = s;
-  return n++;
-}
 
 extern "C" int pis_head_loss_fwd_ok(int B, int H, int W, int C) {
   const int R = head_loss_fwd_rows(B, H, W);
@@ -1783,25 +1329,6 @@ extern "C" int pis_head_loss_fwd(const float* x, int ldx, const float* w, const 
   const dim3 grid(bands, B);
   hipStream_t s = (hipStream_t)stream;
   const double nbytes = (double)B * H * W * (4.0 * C + 12.0);
-  const int k38 = tune_get(PIS_TUNE_HEAD_LOSS_WIDE);
-  const int ticket = wide && k38 >= 3 && h.R >= 2 && W <= 2048 && head_loss_pipe_smem(h.R, W) <= kHeadLossFwdMaxLds
-                         ? loss_ticket_slot(s) : -1;
-  if (ticket >= 0) {
-    // the streamed form (one launch: the band boundaries' stencil terms and the finalize are taken by
-    // blocks of the grid itself); without a free ticket slot the halo form below runs instead
-    float* bpart = (float*)((char*)g.ipart + (size_t)nblk * 3 * sizeof(int));
-    const size_t psm = head_loss_pipe_smem(h.R, W);
-    launch_hook("head_loss_fwd", 0, s, nbytes);
-    if (k38 == 4) hipLaunchKernelGGL((head_loss_fwd_pipe_kernel<true, true, 1>), grid, dim3(1024), psm, s, h, ticket, bpart);
-    else if (k38 == 5) hipLaunchKernelGGL((head_loss_fwd_pipe_kernel<true, true, 2>), grid, dim3(1024), psm, s, h, ticket, bpart);
-    else if (k38 >= 6) hipLaunchKernelGGL((head_loss_fwd_pipe_kernel<true, true, 3>), grid, dim3(1024), psm, s, h, ticket, bpart);
-    else if (rd && pf) hipLaunchKernelGGL((head_loss_fwd_pipe_kernel<true, true>), grid, dim3(1024), psm, s, h, ticket, bpart);
-    else if (rd) hipLaunchKernelGGL((head_loss_fwd_pipe_kernel<true, false>), grid, dim3(1024), psm, s, h, ticket, bpart);
-    else if (pf) hipLaunchKernelGGL((head_loss_fwd_pipe_kernel<false, true>), grid, dim3(1024), psm, s, h, ticket, bpart);
-    else hipLaunchKernelGGL((head_loss_fwd_pipe_kernel<false, false>), grid, dim3(1024), psm, s, h, ticket, bpart);
-    launch_hook("head_loss_fwd", 1, s, nbytes);
-    return launch_status("head_loss_fwd_pipe");
-  }
   launch_hook("head_loss_fwd", 0, s, nbytes);
 #define PIS_HLF(RDV, PFV)                                                                                         \
   do {                                                                                                            \

@@ -639,12 +639,11 @@ def test_head_loss_fwd_fused(hip, B, H, W, ldx, rd_w, pf_w):
 @pytest.mark.parametrize("B,H,W", [(2, 37, 512), (8, 512, 512), (1, 40, 1024), (1, 13, 2048), (3, 2, 512),
                                    (16, 512, 512)])
 def test_head_loss_fwd_variants(hip, B, H, W):
-    """pis_tune(38): the 256-thread bands (0), the 1024-thread bands (1), the same with three
-    register sets in flight (2) and the streamed form with the finalize in the last block (3) give
-    bitwise the same z, u and counters, and the same terms to fp32 summation order; the streamed
-    form's ticket leaves itself ready for the next launch (three calls, bitwise the same). Shapes:
-    ragged bands (37), H = 2 (every staged row a reflect ghost), 1024 / 2048-wide rows (2 / 4 chunks
-    per row, 4 / 2 loss row groups), C2, and 2x C2's batch (more blocks than CUs)."""
+    """pis_tune(38): the 256-thread bands (0), the 1024-thread bands (1) and the same with three
+    register sets in flight (2) give bitwise the same z, u and counters, and the same terms to fp32
+    summation order; repeated calls are bitwise the same. Shapes: ragged bands (37), H = 2 (every
+    staged row a reflect ghost), 1024 / 2048-wide rows (2 / 4 chunks per row), C2, and 2x C2's
+    batch."""
     g = torch.Generator().manual_seed(37)
     x = F.relu(torch.randn(B, H, W, 64, generator=g)).cuda()
     w = (torch.randn(64, generator=g) * 0.15).cuda()
@@ -653,17 +652,17 @@ def test_head_loss_fwd_variants(hip, B, H, W):
     t = mask[:, 0].contiguous().cuda()
     kw = dict(rd_w=1e-4, pf_w=1e-4, D=5.0, a=0.5, eps=0.05)
     outs = {}
-    for v in (0, 1, 2, 3):
+    for v in (0, 1, 2):
         prev = hip.pis_tune(38, v)
         try:
             outs[v] = _head_loss_fwd_call(hip, x, 64, w, b, t, kw)
-            if v == 3:
+            if v == 1:
                 for _ in range(2):
                     again = _head_loss_fwd_call(hip, x, 64, w, b, t, kw)
                     assert all(torch.equal(a_, b_) for a_, b_ in zip(again, outs[v]))
         finally:
             hip.pis_tune(38, prev)
-    for v in (1, 2, 3):
+    for v in (1, 2):
         for k in (0, 1, 3, 4):  # z, u, counts, scores
             assert torch.equal(outs[v][k], outs[0][k]), (v, k)
         np.testing.assert_allclose(outs[v][2].numpy(), outs[0][2].numpy(), rtol=2e-6, atol=1e-12)

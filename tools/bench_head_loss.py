@@ -24,7 +24,7 @@ def main():
     ap.add_argument("--H", type=int, default=512)
     ap.add_argument("--W", type=int, default=512)
     ap.add_argument("--reps", type=int, default=20)
-    ap.add_argument("--variants", default="1,3,1,3", help="key38[:key36] list")
+    ap.add_argument("--variants", default="1,2,1,2", help="key38[:key36] list")
     ap.add_argument("--probe", action="store_true", help="also time pis_debug_band_probe: sweep vs band order")
     args = ap.parse_args()
     lib = _hip.lib()
