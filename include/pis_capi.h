@@ -184,7 +184,13 @@ int pis_version(void);
                                       ReLU-mask rows loaded with its M values (one memory round trip per tile,
                                       151 VGPRs); 0 in the epilogue. Step 22.25 -> 22.04 ms on one box, 22.43 ->
                                       22.39 on another (profiles/r4_t_ab_wino_out_mpf.txt, r4_u_*): 0.2-0.9 % */
-#define PIS_TUNE_NKEYS 47
+#define PIS_TUNE_WINO_F6 47 /* Winograd F(6x6,3x3) for the forward and input gradient of the deep layers whose
+                               contractions run the batched fp16x3 GEMM both ways (csrc/winograd.hip
+                               wino6_layer: 64-aligned channels, neither direct nor fused, >= 10 % fewer
+                               products than F(4x4) on the ragged 6 x 6 tile grid — 128^2 and 64^2 at C2;
+                               their weight gradients keep F(3x3,4x4) with their own transforms): 1 on,
+                               0 F(4x4,3x3) with the kept / prepared transforms */
+#define PIS_TUNE_NKEYS 48
 #define PIS_DEBUG_NOLOAD (1 << 16)
 int pis_tune(int key, int value);
 /* Tooling (tools/bench_gemm.py): time one batched NT GEMM kernel variant in isolation,
@@ -315,6 +321,9 @@ typedef struct pis_filter_job {
   int B, H, W, Cin, Cout, dgrad;
 } pis_filter_job;
 #define PIS_FILTER_MAX_JOBS 40
+/* The filter operand format pis_conv3x3_filter(s) would write for these shapes (0 none, 1 F(4x4) U[36][N][C]
+ * fp32, 2 the fused kernel's planes, 3 the direct kernel's weight split, 4 F(6x6) U[64][N][C] fp32). */
+int pis_conv3x3_filter_format(int B, int H, int W, int Cin, int Cout, int dgrad);
 int pis_conv3x3_filters(const pis_filter_job* jobs, int n, pis_stream_t stream);
 /* 1 when pis_conv3x3_dgrad_ex of these shapes (and workspace) runs the direct fp16x3 kernel
  * (pis_tune key 29), which accepts PIS_W_UNFLIPPED (the original weights) without

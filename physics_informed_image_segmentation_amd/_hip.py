@@ -55,6 +55,7 @@ _SIGNATURES = {
     "pis_conv3x3_dgrad_direct": ([I, I, I, I, I, I, Z], c_int),
     "pis_conv3x3_bwd_prep": ([P, I, I, I, I, I, I, P, Z, P, Z, P], c_int),
     "pis_conv3x3_filter_bytes": ([I, I, I, I, I, I], c_size_t),
+    "pis_conv3x3_filter_format": ([I, I, I, I, I, I], c_int),
     "pis_conv3x3_filter": ([P, I, I, I, I, I, I, P, Z, P], c_int),
     "pis_conv3x3_filters": ([P, I, P], c_int),
     "pis_conv3x3_fwd_pool": ([P, I, P, P, P, P, I, I, I, I, I, I, I, P, Z, P, P, P], c_int),

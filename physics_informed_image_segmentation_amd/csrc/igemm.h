@@ -71,6 +71,9 @@ int launch_wino_input(const float* x, int ldx, int B, int H, int W, int C, float
 int launch_wino_dz(const float* dz, int ldz, int B, int H, int W, int N, float* E, hipStream_t s, int m,
                    float* bpart = nullptr);
 int wino_dz_blocks(int B, int H, int W, int N, int m);
+// F(6x6,3x3) for the forward and input gradient of this layer (pis_tune key 47; symmetric in Cin / Cout)
+bool wino6_layer(int B, int H, int W, int Cin, int Cout);
+int launch_wino6_filter_only(const float* w, int C, int N, int dgrad, void* out, hipStream_t s);
 int wino_dz_blocks_max(int B, int H, int W, int N, int m);  // the largest grid a dz pass of F(m x m) launches (rows of bias partials)
 // M: nsplit split-K slabs sstride floats apart, summed in slab order (nsplit > 1 needs m == 4)
 // The F(3x3,4x4) weight gradient's bias gradient, folded into its output-transform launch:

@@ -572,6 +572,25 @@ static bool wino_wanted_dims(int H, int W, int C, int N) {
   return C >= 256 && N >= 128;
 }
 
+namespace pis {
+bool wino_fused_wanted(int B, int H, int W, int C, int N);  // winograd.hip
+}
+
+// F(6x6,3x3) for a layer's forward and input gradient (pis_tune key 47; csrc/winograd.hip
+// launch_wino6): both directions on the batched fp16x3 GEMM (Winograd-wanted, neither direct nor
+// fused), 64-aligned channels, an F(4x4)-capable grid (the weight gradient keeps F(3x3,4x4)), and
+// at least 10 % fewer products on the ragged 6 x 6 tile grid: 128^2 and 64^2 at C2 (0.84 of
+// F(4x4)'s), not 32^2 (ceil(32 / 6)^2 x 64 = 32^2 / 16 x 36: no gain)
+bool pis::wino6_layer(int B, int H, int W, int Cin, int Cout) {
+  if (tune_get(PIS_TUNE_WINO_F6) == 0 || tune_get(PIS_TUNE_WINO_TILE) != 4 || B <= 0) return false;
+  if (wino_tile(H, W) != 4 || Cin % 64 || Cout % 64) return false;
+  if (direct_h3_wanted(H, W, Cin, Cout, 4) || direct_h3_wanted(H, W, Cout, Cin, 4)) return false;
+  if (!wino_wanted_dims(H, W, Cin, Cout) || !wino_wanted_dims(H, W, Cout, Cin)) return false;
+  if (wino_fused_wanted(B, H, W, Cin, Cout) || wino_fused_wanted(B, H, W, Cout, Cin)) return false;
+  const int64_t p6 = (int64_t)64 * ((H + 5) / 6) * ((W + 5) / 6), p4 = (int64_t)36 * (H / 4) * (W / 4);
+  return 10 * p6 <= 9 * p4;
+}
+
 static int dispatch_conv3x3(const IGemmArgs& a, int B, void* ws, size_t ws_bytes, hipStream_t s,
                             float* keep_v = nullptr, bool v_ready = false) {
   // the direct fp16x3 kernel (pis_tune key 29) where its policy takes the layer; a kept forward
@@ -623,6 +642,7 @@ extern "C" int pis_conv3x3_fwd(const float* x, int ldx, const float* w_krsc, con
 
 extern "C" size_t pis_conv3x3_keep_bytes(int B, int H, int W, int Cin, int Cout) {
   if (Cin % 4 || wino_tile(H, W) != 4 || tune_get(PIS_TUNE_WINOGRAD) == 0) return 0;
+  if (wino6_layer(B, H, W, Cin, Cout)) return 0;  // F(6x6) forward: the weight gradient transforms x itself
   return wino_wgrad_keep_bytes(B, H, W, Cin, Cout);
 }
 
@@ -737,6 +757,8 @@ int launch_wino4_filter_batch(int n, const float* const* w, void* const* out, co
 // kept forward transforms, prepared 32-aligned input gradients)
 static int filter_format(int B, int H, int W, int Cin, int Cout, int dgrad) {
   if (B <= 0 || H <= 0 || W <= 0 || Cin % 4 || Cout % 4 || Cin < 4) return 0;
+  // 4: the F(6x6,3x3) transform U[64][N][C] (input gradient: from the ORIGINAL weights)
+  if (wino6_layer(B, H, W, Cin, Cout)) return 4;
   // 3: the call takes the direct fp16x3 kernel — its "filter transform" is the weight split
   if (dgrad ? direct_h3_wanted(H, W, Cout, Cin, 4) : direct_h3_wanted(H, W, Cin, Cout, 4)) return 3;
   if (dgrad) {
@@ -753,6 +775,7 @@ extern "C" size_t pis_conv3x3_filter_bytes(int B, int H, int W, int Cin, int Cou
   const size_t nc = (size_t)36 * Cin * Cout;
   const int C = dgrad ? Cout : Cin, N = dgrad ? Cin : Cout;  // contraction, outputs
   if (f == 3) return direct_h3_ws_bytes(C, N);
+  if (f == 4) return (size_t)64 * Cin * Cout * sizeof(float);
   if (f == 2 && tune_get(PIS_TUNE_WINO_GEMM_OUT_H3) != 0)  // fp16x3: hi / lo planes + one scale per output
     return 2 * nc * sizeof(_Float16) + (size_t)N * sizeof(float);
   return f == 2 ? 3 * nc * sizeof(__bf16) : nc * sizeof(float);
@@ -769,8 +792,15 @@ extern "C" int pis_conv3x3_filter(const float* w, int B, int H, int W, int Cin, 
     return launch_direct_wsplit_batch(1, &w, &o, &Cin, &Cout, &dg, (hipStream_t)stream);
   }
   // forward: contraction C = Cin, outputs N = Cout; input gradient: C = Cout, N = Cin
+  if (f == 4)
+    return dgrad ? launch_wino6_filter_only(w, Cout, Cin, 1, out, (hipStream_t)stream)
+                 : launch_wino6_filter_only(w, Cin, Cout, 0, out, (hipStream_t)stream);
   return dgrad ? launch_wino4_filter_only(w, Cout, Cin, 1, f, out, (hipStream_t)stream)
                : launch_wino4_filter_only(w, Cin, Cout, 0, f, out, (hipStream_t)stream);
+}
+
+extern "C" int pis_conv3x3_filter_format(int B, int H, int W, int Cin, int Cout, int dgrad) {
+  return filter_format(B, H, W, Cin, Cout, dgrad);
 }
 
 extern "C" int pis_conv3x3_filters(const pis_filter_job* jobs, int n, pis_stream_t stream) {
@@ -830,8 +860,10 @@ extern "C" int pis_conv3x3_dgrad_ex(const float* dz, int ldz, const float* w_fli
   a.filter_ready = (flags & PIS_FILTER_READY) != 0;
   a.is_dgrad = 1;
   PIS_CHECK_ARG(!a.w_unflipped || (flags & PIS_WINO_PREPARED) ||
-                    (ws && direct_h3_wanted(H, W, Cout, Cin, ldz) && ws_bytes >= direct_h3_ws_bytes(Cout, Cin)),
-                "pis_conv3x3_dgrad_ex: PIS_W_UNFLIPPED needs the prepared F(4x4,3x3) path or the direct one");
+                    (ws && direct_h3_wanted(H, W, Cout, Cin, ldz) && ws_bytes >= direct_h3_ws_bytes(Cout, Cin)) ||
+                    (ws && wino6_layer(B, H, W, Cin, Cout) && wino_ok(a) && ws_bytes >= wino_ws_bytes(B, H, W, Cout, Cin)),
+                "pis_conv3x3_dgrad_ex: PIS_W_UNFLIPPED needs the prepared F(4x4,3x3) path, the F(6x6,3x3) one or the "
+                "direct one");
   return dispatch_conv3x3(a, B, ws, ws_bytes, (hipStream_t)stream, nullptr, (flags & PIS_WINO_PREPARED) != 0);
 }
 
@@ -840,7 +872,8 @@ bool pis::dgrad_wino4_planned(int B, int H, int W, int Cin, int Cout, int ldz, s
   a.H = H; a.W = W; a.Csrc = Cout; a.N = Cin; a.lds = ldz; a.ldd = 4; a.ldm = 4;
   a.tap_mode = TAP_CONV3; a.epi = EPI_NHWC;
   return wino_ok(a) && wino_tile(H, W) == 4 && wino_wanted_dims(H, W, Cout, Cin) &&
-         ws_bytes >= wino_ws_bytes(B, H, W, Cout, Cin) && !direct_h3_wanted(H, W, Cout, Cin, ldz);
+         ws_bytes >= wino_ws_bytes(B, H, W, Cout, Cin) && !direct_h3_wanted(H, W, Cout, Cin, ldz) &&
+         !wino6_layer(B, H, W, Cin, Cout);  // an F(6x6) input gradient transforms dz itself
 }
 
 // does pis_conv3x3_dgrad_ex take the direct fp16x3 kernel (which reads the original weights

@@ -1556,6 +1556,7 @@ static WinoWgradPlan wino_wgrad_plan(int B, int H, int W, int Cin, int Cout) {
 // (pis_conv3x3_keep_bytes): the same B^T on the same 6x6 patches
 size_t wino_wgrad_keep_bytes(int B, int H, int W, int Cin, int Cout) {
   if (direct_w_wanted(B, H, W, Cin, Cout, 4, 4)) return 0;  // the direct weight gradient reads x itself
+  if (wino6_layer(B, H, W, Cin, Cout)) return 0;  // an F(6x6) forward keeps no F(4x4) transform
   const WinoWgradPlan p = wino_wgrad_plan(B, H, W, Cin, Cout);
   return (p.use && p.m == 4) ? (size_t)p.nxi * p.T * Cin * sizeof(float) : 0;
 }

@@ -483,6 +483,231 @@ __global__ __launch_bounds__(256) void wino4_filter_h2_kernel(const float* __res
   wino4_filter_h2_wave(w, ldw, N, C, dgrad, Up, 4 * blockIdx.x + (threadIdx.x >> 6));
 }
 
+// ---- F(6x6,3x3): 8 x 8 input tiles, 64 contractions per 36 outputs (16 / 9 products per output
+// against F(4x4)'s 9 / 4: 21 % fewer GEMM FLOPs and V / M bytes on a divisible grid) -----------------
+// Cook-Toom points {0, 1, -1, 2, -2, 1/2, -1/2, inf} (the same construction as the F(4x4) tables
+// above). Measured fp32 error of the whole convolution against float64 (256 -> 64 channels, ReLU'd
+// inputs): 5.4e-6 relative (norm), 1.5e-5 of the output scale at worst, against 1.8e-6 / 4.2e-6 for
+// F(4x4) with {0, 1, -1, 1/2, -2}. Used for the forward and input gradient
+// of the deep layers that run the batched GEMM both ways (wino6_layer); their weight gradients keep
+// F(3x3,4x4) with their own transforms (no kept V). Ragged grids: the tile grid is ceil(H / 6) x
+// ceil(W / 6), inputs past the image are zeros and outputs past it are not written.
+__host__ __device__ constexpr float w6_bt(int i, int k) {
+  constexpr float m[8][8] = {{-1.f, 0.f, 21.f / 4, 0.f, -21.f / 4, 0.f, 1.f, 0.f},
+                             {0.f, 1.f, 1.f, -17.f / 4, -17.f / 4, 1.f, 1.f, 0.f},
+                             {0.f, -1.f, 1.f, 17.f / 4, -17.f / 4, -1.f, 1.f, 0.f},
+                             {0.f, 1.f / 2, 1.f / 4, -5.f / 2, -5.f / 4, 2.f, 1.f, 0.f},
+                             {0.f, -1.f / 2, 1.f / 4, 5.f / 2, -5.f / 4, -2.f, 1.f, 0.f},
+                             {0.f, 2.f, 4.f, -5.f / 2, -5.f, 1.f / 2, 1.f, 0.f},
+                             {0.f, -2.f, 4.f, 5.f / 2, -5.f, -1.f / 2, 1.f, 0.f},
+                             {0.f, -1.f, 0.f, 21.f / 4, 0.f, -21.f / 4, 0.f, 1.f}};
+  return m[i][k];
+}
+__host__ __device__ constexpr float w6_g(int i, int k) {
+  constexpr float m[8][3] = {{-1.f, 0.f, 0.f},
+                             {-2.f / 9, -2.f / 9, -2.f / 9},
+                             {-2.f / 9, 2.f / 9, -2.f / 9},
+                             {1.f / 90, 1.f / 45, 2.f / 45},
+                             {1.f / 90, -1.f / 45, 2.f / 45},
+                             {32.f / 45, 16.f / 45, 8.f / 45},
+                             {32.f / 45, -16.f / 45, 8.f / 45},
+                             {0.f, 0.f, 1.f}};
+  return m[i][k];
+}
+__host__ __device__ constexpr float w6_at(int i, int k) {
+  constexpr float m[6][8] = {{1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 0.f},
+                             {0.f, 1.f, -1.f, 2.f, -2.f, 1.f / 2, -1.f / 2, 0.f},
+                             {0.f, 1.f, 1.f, 4.f, 4.f, 1.f / 4, 1.f / 4, 0.f},
+                             {0.f, 1.f, -1.f, 8.f, -8.f, 1.f / 8, -1.f / 8, 0.f},
+                             {0.f, 1.f, 1.f, 16.f, 16.f, 1.f / 16, 1.f / 16, 0.f},
+                             {0.f, 1.f, -1.f, 32.f, -32.f, 1.f / 32, -1.f / 32, 1.f}};
+  return m[i][k];
+}
+
+// U[xi][n][c] = (G g G^T)[xi], xi = 8 i + j, for the filter g of pair e = n C + c
+__device__ __forceinline__ void wino6_filter_item(const float (&g)[3][3], int64_t e, int64_t NC, float* __restrict__ U) {
+  float gg[8][3];  // G g
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int s = 0; s < 3; ++s) {
+      gg[i][s] = 0.f;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) axpy_c(gg[i][s], w6_g(i, k), g[k][s]);
+    }
+  float* o = U + e;  // one pointer walked plane to plane (64 per-plane scalar offsets spill SGPRs)
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float u = 0.f;
+#pragma unroll
+      for (int s = 0; s < 3; ++s) axpy_c(u, w6_g(j, s), gg[i][s]);
+      *o = u;
+      o += NC;
+    }
+}
+
+// the forward's weights w [N][9][C] (row pitch ldw), block bid of nblk
+__device__ __forceinline__ void wino6_filter_range(const float* __restrict__ w, int ldw, int N, int C,
+                                                   float* __restrict__ U, int bid, int nblk) {
+  const int64_t NC = (int64_t)N * C;
+  for (int64_t e = (int64_t)bid * blockDim.x + threadIdx.x; e < NC; e += (int64_t)nblk * blockDim.x) {
+    const int n = (int)(e / C), c = (int)(e - (int64_t)n * C);
+    float g[3][3];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) g[t / 3][t % 3] = w[(size_t)n * ldw + t * C + c];
+    wino6_filter_item(g, e, NC, U);
+  }
+}
+
+// the input gradient's transform straight from the layer's ORIGINAL weights [C][9][N] (N = Cin,
+// C = Cout; rotated and transposed in place, as wino4_filter_rot_tile): a block owns 32 n x 32 c
+__device__ __forceinline__ void wino6_filter_rot_tile(const float* __restrict__ w, int N, int C, float* __restrict__ U,
+                                                      int tile) {
+  __shared__ float sg[9][32][33];  // [tap][c][n]
+  const int nb = N / 32, n0 = 32 * (tile % nb), c0 = 32 * (tile / nb);
+  const int tid = threadIdx.x, lx = tid & 31, ly = tid >> 5;
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c = ly + 8 * i;
+      sg[t][c][lx] = w[((size_t)(c0 + c) * 9 + t) * N + n0 + lx];
+    }
+  __syncthreads();
+  const int64_t NC = (int64_t)N * C;
+#pragma unroll 1
+  for (int i = 0; i < 4; ++i) {
+    const int c = lx, nl = ly + 8 * i, n = n0 + nl;
+    float g[3][3];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) g[t / 3][t % 3] = sg[8 - t][c][nl];
+    wino6_filter_item(g, (int64_t)n * C + c0 + c, NC, U);
+  }
+}
+
+__global__ __launch_bounds__(256) void wino6_filter_kernel(const float* __restrict__ w, int ldw, int N, int C,
+                                                           float* __restrict__ U) {
+  wino6_filter_range(w, ldw, N, C, U, blockIdx.x, gridDim.x);
+}
+__global__ __launch_bounds__(256) void wino6_filter_rot_kernel(const float* __restrict__ w, int N, int C,
+                                                               float* __restrict__ U) {
+  wino6_filter_rot_tile(w, N, C, U, blockIdx.x);
+}
+
+// V[xi][t][c] = (BT d BT^T)[xi], d = the 8 x 8 input patch at rows 6 ty - 1 .., cols 6 tx - 1 ..
+// (zeros past the image: padding 1 and the ragged last tiles); VW consecutive channels per thread
+template <int VW>
+__global__ __launch_bounds__(256) void wino6_input_kernel(const float* __restrict__ x, int ldx, int B, int H, int W,
+                                                          int C, float* __restrict__ V) {
+  const int c4n = C / VW, TW = (W + 5) / 6, TH = (H + 5) / 6;
+  const int64_t T = (int64_t)B * TH * TW, TC = T * C;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < T * c4n; e += (int64_t)gridDim.x * blockDim.x) {
+    int64_t t;
+    int c, b, rem;
+    tile_decode<VW>(e, c4n, TH * TW, t, c, b, rem);
+    const int ty = rem / TW, tx = rem - ty * TW;
+    fvec<VW> v[8][8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[i][j] = (fvec<VW>)0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {  // input row k: its row transform, then its share of every V row
+      const int h = 6 * ty - 1 + k;
+      fvec<VW> d[8];
+#pragma unroll
+      for (int l = 0; l < 8; ++l) {
+        const int ww = 6 * tx - 1 + l;
+        d[l] = (fvec<VW>)0.f;
+        if (h >= 0 && h < H && ww >= 0 && ww < W)
+          d[l] = *reinterpret_cast<const fvec<VW>*>(x + (((size_t)b * H + h) * W + ww) * ldx + c);
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        fvec<VW> r = (fvec<VW>)0.f;
+#pragma unroll
+        for (int l = 0; l < 8; ++l) axpy_c(r, w6_bt(j, l), d[l]);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) axpy_c(v[i][j], w6_bt(i, k), r);
+      }
+    }
+    float* o = V + t * C + c;  // one pointer walked plane to plane
+#pragma unroll
+    for (int xi = 0; xi < 64; ++xi) {
+      *reinterpret_cast<fvec<VW>*>(o) = v[xi / 8][xi % 8];
+      o += TC;
+    }
+  }
+}
+
+// Y = AT M AT^T per tile and VW output channels, then the direct kernels' conv epilogue on the
+// outputs inside the image; POOL (g.pool): the tile's 3 x 3 max-pool outputs (6 is even: a pool
+// window never straddles two tiles)
+template <int VW>
+__global__ __launch_bounds__(256) void wino6_output_kernel(const float* __restrict__ Mt, IGemmArgs g, int B) {
+  const int N = g.N, n4n = N / VW, TW = (g.W + 5) / 6, TH = (g.H + 5) / 6;
+  const int64_t T = (int64_t)B * TH * TW, TN = T * N;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < T * n4n; e += (int64_t)gridDim.x * blockDim.x) {
+    int64_t t;
+    int n, b, rem;
+    tile_decode<VW>(e, n4n, TH * TW, t, n, b, rem);
+    const int ty = rem / TW, tx = rem - ty * TW;
+    fvec<VW> y[6][6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i)
+#pragma unroll
+      for (int j = 0; j < 6; ++j) y[i][j] = (fvec<VW>)0.f;
+    const float* mp = Mt + t * N + n;  // one pointer walked plane to plane
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      fvec<VW> m[8];
+#pragma unroll
+      for (int l = 0; l < 8; ++l) {
+        m[l] = *reinterpret_cast<const fvec<VW>*>(mp);
+        mp += TN;
+      }
+#pragma unroll
+      for (int j = 0; j < 6; ++j) {
+        fvec<VW> r = (fvec<VW>)0.f;
+#pragma unroll
+        for (int l = 0; l < 8; ++l) axpy_c(r, w6_at(j, l), m[l]);
+#pragma unroll
+        for (int i = 0; i < 6; ++i) axpy_c(y[i][j], w6_at(i, k), r);
+      }
+    }
+    fvec<VW> bias4 = (fvec<VW>)0.f, sc4 = (fvec<VW>)1.f;
+    if (g.bias) bias4 = *reinterpret_cast<const fvec<VW>*>(g.bias + n);
+    if (g.flags & PIS_SCALE) sc4 = *reinterpret_cast<const fvec<VW>*>(g.scale + (size_t)b * N + n);
+    const int oy0 = 6 * ty, ox0 = 6 * tx;
+#pragma unroll
+    for (int qi = 0; qi < 3; ++qi) {  // row pairs 2 qi, 2 qi + 1: their epilogue, then their pooled outputs
+      fvec<VW> o[2][6];
+#pragma unroll
+      for (int di = 0; di < 2; ++di)
+#pragma unroll
+        for (int j = 0; j < 6; ++j) {
+          const int oy = oy0 + 2 * qi + di, ox = ox0 + j;
+          o[di][j] = (fvec<VW>)0.f;
+          if (oy < g.H && ox < g.W) {
+            const size_t pix = ((size_t)b * g.H + oy) * g.W + ox;
+            o[di][j] = conv_epilogue4<VW>(g, pix, n, y[2 * qi + di][j] + bias4, sc4);
+          }
+        }
+      if (g.pool && oy0 + 2 * qi + 1 < g.H) {
+#pragma unroll
+        for (int qj = 0; qj < 3; ++qj) {
+          if (ox0 + 2 * qj + 1 >= g.W) continue;
+          const size_t pp = ((size_t)b * (g.H / 2) + 3 * ty + qi) * (g.W / 2) + 3 * tx + qj;
+          *reinterpret_cast<fvec<VW>*>(g.pool + pp * N + n) = max4<VW>(o[0][2 * qj], o[0][2 * qj + 1], o[1][2 * qj],
+                                                                      o[1][2 * qj + 1]);
+        }
+      }
+    }
+  }
+}
+
 // Many layers' filter transforms in ONE launch (pis_conv3x3_filters): one layer's grid is a few
 // to a few hundred blocks, so each separate launch is latency-bound (13-47 us at C2); here every
 // job's blocks run side by side. Block b belongs to the job whose [start, start + blocks) holds it.
@@ -490,6 +715,7 @@ struct FilterJobDev {
   const float* w;
   void* out;
   int N, C, dgrad, planes, blocks;
+  int tile;  // 4, or 6: the F(6x6,3x3) transform U[64][N][C] (planes 0)
 };
 constexpr int FILTER_MAX_JOBS = 40;
 struct FilterBatch {
@@ -505,7 +731,10 @@ __global__ __launch_bounds__(256) void wino4_filter_batch_kernel(FilterBatch fb)
   const int lb = (int)blockIdx.x - fb.start[k];
   float* U = jb.planes ? nullptr : reinterpret_cast<float*>(jb.out);
   __bf16* Up = jb.planes ? reinterpret_cast<__bf16*>(jb.out) : nullptr;
-  if (jb.planes == 2) wino4_filter_h2_wave(jb.w, 9 * jb.C, jb.N, jb.C, jb.dgrad, Up, 4 * lb + (threadIdx.x >> 6));
+  if (jb.tile == 6) {
+    if (jb.dgrad) wino6_filter_rot_tile(jb.w, jb.N, jb.C, U, lb);
+    else wino6_filter_range(jb.w, 9 * jb.C, jb.N, jb.C, U, lb, jb.blocks);
+  } else if (jb.planes == 2) wino4_filter_h2_wave(jb.w, 9 * jb.C, jb.N, jb.C, jb.dgrad, Up, 4 * lb + (threadIdx.x >> 6));
   else if (jb.dgrad) wino4_filter_rot_tile(jb.w, jb.N, jb.C, U, 0, Up, lb);
   else wino4_filter_range(jb.w, 9 * jb.C, jb.N, jb.C, U, 0, Up, lb, jb.blocks);
 }
@@ -1918,6 +2147,75 @@ static int launch_wino_gemm_out(const float* V, const __bf16* Up, const IGemmArg
 }
 
 
+// does a contraction of C channels into N outputs at B x H x W take the fused F(4x4) kernel?
+bool wino_fused_wanted(int B, int H, int W, int C, int N) {
+  return wino_tile(H, W) == 4 && wino_gemm_out_wanted(4, (int64_t)B * (H / 4) * (W / 4), C, N);
+}
+
+static int64_t wino6_tiles(int B, int H, int W) { return (int64_t)B * ((H + 5) / 6) * ((W + 5) / 6); }
+
+// U (64 N C), V (64 T C), M (64 T N) of one F(6x6,3x3) call
+static size_t wino6_ws_bytes(int B, int H, int W, int C, int N) {
+  const int64_t T = wino6_tiles(B, H, W);
+  return (size_t)64 * ((int64_t)N * C + T * C + T * N) * sizeof(float) + 1024;
+}
+
+// the F(6x6,3x3) filter transform of w: forward weights [N][9][C] (ldw), or (dgrad) the input
+// gradient's from the ORIGINAL weights [C][9][N] (N, C % 32 == 0)
+static void launch_wino6_filter(const float* w, int ldw, int N, int C, int dgrad, float* U, hipStream_t s) {
+  if (dgrad) hipLaunchKernelGGL(wino6_filter_rot_kernel, dim3((N / 32) * (C / 32)), dim3(256), 0, s, w, N, C, U);
+  else hipLaunchKernelGGL(wino6_filter_kernel, dim3(grid_of((int64_t)N * C)), dim3(256), 0, s, w, ldw, N, C, U);
+}
+
+int launch_wino6_filter_only(const float* w, int C, int N, int dgrad, void* out, hipStream_t s) {
+  if (dgrad && (N % 32 || C % 32))
+    return set_error("pis_conv3x3_filter: the F(6x6) input-gradient transform needs 32-aligned channels"), PIS_ERR_ARG;
+  launch_wino6_filter(w, 9 * C, N, C, dgrad, reinterpret_cast<float*>(out), s);
+  return launch_status("wino6_filter");
+}
+
+// one F(6x6,3x3) convolution (a: as launch_wino3x3): filter transform (or a.wt ready: U[64][N][C]),
+// input transform, the 64 batched fp16x3 GEMMs, output transform + epilogue
+static int launch_wino6(const IGemmArgs& a, int B, void* ws, hipStream_t s) {
+  const int C = a.Csrc, N = a.N;
+  const int64_t T = wino6_tiles(B, a.H, a.W);
+  float* U = (float*)ws;
+  float* V = U + (size_t)64 * N * C;
+  float* Mt = V + (size_t)64 * T * C;
+  if (a.w_unflipped && (N % 32 || C % 32))
+    return set_error("launch_wino6: unflipped weights need 32-aligned channels"), PIS_ERR_ARG;
+  if (a.filter_ready) U = const_cast<float*>(a.wt);
+  else launch_wino6_filter(a.wt, a.ldw, N, C, a.w_unflipped ? 1 : 0, U, s);
+  // channels per thread of the transforms (key 47: 1 -> 1, 2 -> 2): the 64-value tiles hold 64 VW
+  // accumulators per thread
+  const bool vw2 = tune_get(PIS_TUNE_WINO_F6) == 2;
+  if (vw2)
+    hipLaunchKernelGGL(wino6_input_kernel<2>, dim3(grid_of(T * (C / 2))), dim3(256), 0, s, a.src, a.lds, B, a.H, a.W,
+                       C, V);
+  else
+    hipLaunchKernelGGL(wino6_input_kernel<1>, dim3(grid_of(T * C)), dim3(256), 0, s, a.src, a.lds, B, a.H, a.W, C, V);
+  int rc = launch_status("wino6_transforms");
+  if (rc) return rc;
+  const double flop = 2.0 * 64 * (double)T * N * C;
+  launch_hook("wino_gemm", 0, s, flop);
+  if (N % 128 == 0) {
+    const dim3 grid((int)cdiv(T, 128) * (N / 128), 64);
+    hipLaunchKernelGGL((gemm_nt_h3_bk32_kernel<128, 128, 3>), grid, dim3(256), 0, s, V, U, Mt, (int)T, N, C, T * C,
+                       (int64_t)N * C, T * N);
+  } else {
+    const dim3 grid((int)cdiv(T, 128) * (N / 64), 64);
+    hipLaunchKernelGGL((gemm_nt_h3_bk32_kernel<128, 64, 4>), grid, dim3(256), 0, s, V, U, Mt, (int)T, N, C, T * C,
+                       (int64_t)N * C, T * N);
+  }
+  launch_hook("wino_gemm", 1, s, flop);
+  rc = launch_status("wino6_gemm");
+  if (rc) return rc;
+  gemm_done(s);
+  if (vw2) hipLaunchKernelGGL(wino6_output_kernel<2>, dim3(grid_of(T * (N / 2))), dim3(256), 0, s, Mt, a, B);
+  else hipLaunchKernelGGL(wino6_output_kernel<1>, dim3(grid_of(T * N)), dim3(256), 0, s, Mt, a, B);
+  return launch_status("wino6_output");
+}
+
 // F(4x4,3x3) when the 4x4 tile grid fits and pis_tune key 11 allows it, else F(2x2,3x3)
 int wino_tile(int H, int W) { return (tune_get(PIS_TUNE_WINO_F4) != 0 && H % 4 == 0 && W % 4 == 0) ? 4 : 2; }
 
@@ -1934,7 +2232,8 @@ size_t wino_ws_bytes(int B, int H, int W, int C, int N) {
   const int64_t T = (int64_t)B * (H / m) * (W / m);
   // + the fp16x3 tile maxima after M: per (tile, 64-channel chunk) of V (wino_tmax_slot)
   const int64_t extra = T * ((C + 63) / 64) + 8;
-  return (size_t)(nxi * ((int64_t)N * C + T * C + T * N) + extra) * sizeof(float) + 1024;
+  const size_t f4 = (size_t)(nxi * ((int64_t)N * C + T * C + T * N) + extra) * sizeof(float) + 1024;
+  return wino6_layer(B, H, W, C, N) ? std::max(f4, wino6_ws_bytes(B, H, W, C, N)) : f4;
 }
 
 static int wino_prep_check(const void* ws, int B, int H, int W, int C, int N);
@@ -1952,6 +2251,9 @@ int launch_wino3x3(const IGemmArgs& a, int B, void* ws, hipStream_t s, float* ke
     const int rc = wino_prep_check(ws, B, a.H, a.W, C, N);
     if (rc) return rc;
   }
+  // F(6x6,3x3): the deep layers' forward and input gradient (no kept or prepared F(4x4) transforms)
+  if (m == 4 && !keep_v && !v_ready && wino6_layer(B, a.H, a.W, C, N) && N % 64 == 0 && C % 32 == 0)
+    return launch_wino6(a, B, ws, s);
   const double flop = 2.0 * nxi * (double)T * N * C;
   if (a.filter_ready && m != 4)
     return set_error("launch_wino3x3: PIS_FILTER_READY needs the F(4x4,3x3) GEMM path"), PIS_ERR_ARG;
@@ -2089,7 +2391,7 @@ int launch_wino4_filter_batch(int n, const float* const* w, void* const* out, co
     if (planes == 2 && (C[k] % 64 || N[k] % 4))
       return set_error("pis_conv3x3_filters: fp16x3 planes need 64 x k contraction channels"), PIS_ERR_ARG;
     const int blocks = planes == 2 ? N[k] / 4 : dgrad[k] ? (N[k] / 32) * (C[k] / 32) : grid_of((int64_t)N[k] * C[k]);
-    fb.j[k] = FilterJobDev{w[k], out[k], N[k], C[k], dgrad[k], planes, blocks};
+    fb.j[k] = FilterJobDev{w[k], out[k], N[k], C[k], dgrad[k], planes, blocks, format[k] == 4 ? 6 : 4};
     fb.start[k] = total;
     total += blocks;
   }

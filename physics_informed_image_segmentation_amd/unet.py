@@ -507,8 +507,11 @@ class UNetEngine:
                                             conv.in_channels, conv.out_channels, dg)
                 return arr
             if mode in ("4", "5"):  # two tables: the direct splits first (enc1.conv1 needs its split next)
-                self.filter_jobs_d = table([j for j in jobs if id(j[0][0]) not in self.keep])
-                self.filter_jobs = table([j for j in jobs if id(j[0][0]) in self.keep])
+                def direct(j):
+                    (conv, Hl, Wl, _), dg = j
+                    return lib.pis_conv3x3_filter_format(B, Hl, Wl, conv.in_channels, conv.out_channels, dg) == 3
+                self.filter_jobs_d = table([j for j in jobs if direct(j)])
+                self.filter_jobs = table([j for j in jobs if not direct(j)])
             else:
                 self.filter_jobs = table(jobs)
 
@@ -859,6 +862,13 @@ class UNetEngine:
                         if ev is not None:
                             main.wait_event(ev)
                         wf, flags = self.bfilt[id(conv)][3].data_ptr(), flags | PIS_FILTER_READY
+                elif id(conv) in self.bev and lib.pis_conv3x3_filter_format(
+                        B, Hl, Wl, conv.in_channels, conv.out_channels, 1) == 4:
+                    # F(6x6,3x3) input gradient: its transform of the ORIGINAL weights, computed ahead
+                    ev = self.bev.pop(id(conv))
+                    if ev is not None:
+                        main.wait_event(ev)
+                    wf, flags = self.bfilt[id(conv)][3].data_ptr(), flags | PIS_W_UNFLIPPED | PIS_FILTER_READY
                 else:
                     wf = flipped(conv).data_ptr()
                 call("pis_conv3x3_dgrad_ex", dz.p, dz.ld, wf,
