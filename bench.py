@@ -82,7 +82,7 @@ def conv_flops_per_image(H: int, W: int, c: int = 64) -> float:
 
 
 def wino_gemm_launches(H: int, W: int, B: int, c: int = 64):
-    """(T, C, N) of every batched Winograd GEMM launch ("wino_gemm") of one training step: the
+    """(T, C, N, planes) of every batched Winograd GEMM launch ("wino_gemm") of one training step: the
     forward and input gradient of each F(4x4,3x3) 3x3 conv (T = B H W / 16 tiles, contraction C,
     N outputs), in no particular order — the 64 / 128-channel contractions into <= 256 outputs run
     the fused contraction + output transform kernel instead (fused_wanted), and enc1.conv0 (Cin = 1) the VALU row kernels (csrc/winograd.hip
@@ -98,9 +98,20 @@ def wino_gemm_launches(H: int, W: int, B: int, c: int = 64):
     out = []
     for hl, wl, ci, co in convs:
         T = B * (hl // 4) * (wl // 4)
-        out += [(T, C, N) for C, N in ((ci, co), (co, ci))
+        if wino6_layer(B, hl, wl, ci, co):  # F(6x6,3x3) both ways: 64 planes over the 6 x 6 tile grid
+            T6 = B * ((hl + 5) // 6) * ((wl + 5) // 6)
+            out += [(T6, ci, co, 64), (T6, co, ci, 64)]
+            continue
+        out += [(T, C, N, 36) for C, N in ((ci, co), (co, ci))
                 if not direct_wanted(hl, wl, C, N) and not fused_wanted(T, C, N)]
     return out
+
+
+def wino6_layer(B: int, H: int, W: int, Cin: int, Cout: int) -> bool:
+    """csrc/igemm.hip wino6_layer (pis_tune key 47 as set now): the layers whose forward and input
+    gradient run Winograd F(6x6,3x3)."""
+    from physics_informed_image_segmentation_amd import _hip
+    return _hip.lib().pis_conv3x3_filter_format(B, H, W, Cin, Cout, 0) == 4
 
 
 def fused_launches(H: int, W: int, B: int, c: int = 64):
@@ -235,8 +246,8 @@ def gemm_attainable(launches, pipe_peak_tflops: float, hbm_gbs: float = 8000.0):
     algorithmic bytes being V read + U read + M written once (36 fp32 planes each). Returns
     (FLOP, bytes, roofline seconds, FLOP-only seconds, bytes-only seconds), summed."""
     fl = by = tmin = tf = tb = 0.0
-    for T, C, N in launches:
-        f, b = 2.0 * 36 * T * C * N, 4.0 * 36 * (T * C + N * C + T * N)
+    for T, C, N, nxi in launches:
+        f, b = 2.0 * nxi * T * C * N, 4.0 * nxi * (T * C + N * C + T * N)
         fl, by = fl + f, by + b
         tf, tb = tf + f / (pipe_peak_tflops * 1e12), tb + b / (hbm_gbs * 1e9)
         tmin += max(f / (pipe_peak_tflops * 1e12), b / (hbm_gbs * 1e9))
@@ -735,9 +746,11 @@ def main():
             "step_bytes_s": g_tb, "step_flop_s": g_tf,
             "attainable_frac": g_tmin / (n_launch * ms_per_launch * 1e-3),
             "attainable_frac_isolated": g_tmin / (n_launch * iso_ms * 1e-3),
-            "hbm_bound_launches": sum(1 for T, C, N in gl if 4.0 * 36 * (T * C + N * C + T * N) / 8e12 >
-                                      2.0 * 36 * T * C * N / (peak * 1e12)),
-            "note": "algorithmic bytes = V read + U read + M written once (4 B x 36 planes); attainable = "
+            "hbm_bound_launches": sum(1 for T, C, N, nxi in gl if 4.0 * nxi * (T * C + N * C + T * N) / 8e12 >
+                                      2.0 * nxi * T * C * N / (peak * 1e12)),
+            "f6_launches": sum(1 for *_, nxi in gl if nxi == 64),
+            "note": "algorithmic bytes = V read + U read + M written once (4 B x 36 planes, 64 for the F(6x6,3x3) "
+                    "launches); attainable = "
                     "sum over the step's launches of max(FLOP / pipe peak, bytes / 8 TB/s) / their measured "
                     "time: the GEMMs are mostly HBM-bound (the 36 fp32 M planes)"}
     # the fused contraction + output transform (wino4_gemm_out_x6_kernel): HBM-bound by design
@@ -806,7 +819,8 @@ def main():
             "roofline_gemm": {"bound": "mfma", "kernel": ("gemm_nt_h3_bk32_kernel<128, 128|64>" if h3 else
                                                      "gemm_nt_x6_bk32_kernel<128, 128|64>" if x6 else
                                                      "gemm_nt_kernel<128, 128|64>")
-                         + f" ({DOMINANT}: the 36 batched GEMMs of Winograd F(4x4,3x3) fwd/dgrad)",
+                         + f" ({DOMINANT}: the batched GEMMs of Winograd fwd/dgrad: 36 per F(4x4,3x3) launch, "
+                           "64 per F(6x6,3x3) launch)",
                          "achieved": achieved, "peak": peak,
                          "unit": "TFLOP/s", "frac": achieved / peak, "traffic": traffic, "pipe": pipe,
                          "fp32_mfma_peak_frac": achieved / 157.3,

@@ -188,8 +188,13 @@ int pis_version(void);
                                contractions run the batched fp16x3 GEMM both ways (csrc/winograd.hip
                                wino6_layer: 64-aligned channels, neither direct nor fused, >= 10 % fewer
                                products than F(4x4) on the ragged 6 x 6 tile grid — 128^2 and 64^2 at C2;
-                               their weight gradients keep F(3x3,4x4) with their own transforms): 1 on,
-                               0 F(4x4,3x3) with the kept / prepared transforms */
+                               their weight gradients keep F(3x3,4x4) with their own transforms): 0
+                               (default) F(4x4,3x3) with the kept / prepared transforms; 1 F(6x6), one
+                               channel per thread in the transforms; 2 two channels; 3 two channels with
+                               runtime-looped (lower-register) transforms. Measured slower on the C2 step
+                               (358.7 vs 366.8 img/s, profiles/r6_f6*): the GEMMs -12 % per F(6x6)
+                               launch but the 64-value transforms run at ~0.65 of F(4x4)'s bytes/s and
+                               the weight gradients' own transforms load the side stream */
 #define PIS_TUNE_NKEYS 48
 #define PIS_DEBUG_NOLOAD (1 << 16)
 int pis_tune(int key, int value);

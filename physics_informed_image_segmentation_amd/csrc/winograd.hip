@@ -642,10 +642,81 @@ __global__ __launch_bounds__(256) void wino6_input_kernel(const float* __restric
   }
 }
 
+// The same input transform at two channels per thread with HALF the accumulators (pis_tune(47, 3)):
+// V rows 0..3, then 4..7, each from all eight input rows (the second pass re-reads the patch from
+// L1 / L2): 8-B accesses at about half the registers of the one-pass form (212 -> ~100)
+__constant__ float c_w6_bt[8][8] = {{-1.f, 0.f, 21.f / 4, 0.f, -21.f / 4, 0.f, 1.f, 0.f},
+                                    {0.f, 1.f, 1.f, -17.f / 4, -17.f / 4, 1.f, 1.f, 0.f},
+                                    {0.f, -1.f, 1.f, 17.f / 4, -17.f / 4, -1.f, 1.f, 0.f},
+                                    {0.f, 1.f / 2, 1.f / 4, -5.f / 2, -5.f / 4, 2.f, 1.f, 0.f},
+                                    {0.f, -1.f / 2, 1.f / 4, 5.f / 2, -5.f / 4, -2.f, 1.f, 0.f},
+                                    {0.f, 2.f, 4.f, -5.f / 2, -5.f, 1.f / 2, 1.f, 0.f},
+                                    {0.f, -2.f, 4.f, 5.f / 2, -5.f, -1.f / 2, 1.f, 0.f},
+                                    {0.f, -1.f, 0.f, 21.f / 4, 0.f, -21.f / 4, 0.f, 1.f}};
+
+__global__ __launch_bounds__(256, 4) void wino6_input2h_kernel(const float* __restrict__ x, int ldx, int B, int H, int W,
+                                                            int C, float* __restrict__ V) {
+  constexpr int VW = 2;
+  const int c4n = C / VW, TW = (W + 5) / 6, TH = (H + 5) / 6;
+  const int64_t T = (int64_t)B * TH * TW, TC = T * C;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < T * c4n; e += (int64_t)gridDim.x * blockDim.x) {
+    int64_t t;
+    int c, b, rem;
+    tile_decode<VW>(e, c4n, TH * TW, t, c, b, rem);
+    const int ty = rem / TW, tx = rem - ty * TW;
+#pragma unroll 1
+    for (int hf = 0; hf < 2; ++hf) {  // V rows 4 hf .. 4 hf + 3 (the row factor from constant memory)
+      fvec<VW> v[4][8];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[i][j] = (fvec<VW>)0.f;
+#pragma unroll 1
+      for (int k = 0; k < 8; ++k) {
+        const int h = 6 * ty - 1 + k;
+        fvec<VW> d[8];
+#pragma unroll
+        for (int l = 0; l < 8; ++l) {
+          const int ww = 6 * tx - 1 + l;
+          d[l] = (fvec<VW>)0.f;
+          if (h >= 0 && h < H && ww >= 0 && ww < W)
+            d[l] = *reinterpret_cast<const fvec<VW>*>(x + (((size_t)b * H + h) * W + ww) * ldx + c);
+        }
+        float f[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) f[i] = c_w6_bt[4 * hf + i][k];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          fvec<VW> r = (fvec<VW>)0.f;
+#pragma unroll
+          for (int l = 0; l < 8; ++l) axpy_c(r, w6_bt(j, l), d[l]);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) v[i][j] += f[i] * r;
+        }
+      }
+      float* o = V + (size_t)(32 * hf) * TC + t * C + c;
+#pragma unroll
+      for (int xi = 0; xi < 32; ++xi) {
+        *reinterpret_cast<fvec<VW>*>(o) = v[xi / 8][xi % 8];
+        o += TC;
+      }
+    }
+  }
+}
+
+__constant__ float c_w6_at[6][8] = {{1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 0.f},
+                                    {0.f, 1.f, -1.f, 2.f, -2.f, 1.f / 2, -1.f / 2, 0.f},
+                                    {0.f, 1.f, 1.f, 4.f, 4.f, 1.f / 4, 1.f / 4, 0.f},
+                                    {0.f, 1.f, -1.f, 8.f, -8.f, 1.f / 8, -1.f / 8, 0.f},
+                                    {0.f, 1.f, 1.f, 16.f, 16.f, 1.f / 16, 1.f / 16, 0.f},
+                                    {0.f, 1.f, -1.f, 32.f, -32.f, 1.f / 32, -1.f / 32, 1.f}};
+
 // Y = AT M AT^T per tile and VW output channels, then the direct kernels' conv epilogue on the
 // outputs inside the image; POOL (g.pool): the tile's 3 x 3 max-pool outputs (6 is even: a pool
 // window never straddles two tiles)
-template <int VW>
+// RT (pis_tune(47, 3)): the eight M rows walked in a runtime loop (the column factor AT[i][k] from
+// constant memory): the loads of one row in flight at a time, ~half the registers of the unrolled form
+template <int VW, bool RT = false>
 __global__ __launch_bounds__(256) void wino6_output_kernel(const float* __restrict__ Mt, IGemmArgs g, int B) {
   const int N = g.N, n4n = N / VW, TW = (g.W + 5) / 6, TH = (g.H + 5) / 6;
   const int64_t T = (int64_t)B * TH * TW, TN = T * N;
@@ -660,6 +731,23 @@ __global__ __launch_bounds__(256) void wino6_output_kernel(const float* __restri
 #pragma unroll
       for (int j = 0; j < 6; ++j) y[i][j] = (fvec<VW>)0.f;
     const float* mp = Mt + t * N + n;  // one pointer walked plane to plane
+    if constexpr (RT) {
+#pragma unroll 1
+      for (int k = 0; k < 8; ++k) {
+        fvec<VW> m[8];
+#pragma unroll
+        for (int l = 0; l < 8; ++l) m[l] = *reinterpret_cast<const fvec<VW>*>(mp + (size_t)l * TN);
+        mp += 8 * TN;
+#pragma unroll
+        for (int j = 0; j < 6; ++j) {
+          fvec<VW> r = (fvec<VW>)0.f;
+#pragma unroll
+          for (int l = 0; l < 8; ++l) axpy_c(r, w6_at(j, l), m[l]);
+#pragma unroll
+          for (int i = 0; i < 6; ++i) y[i][j] += c_w6_at[i][k] * r;
+        }
+      }
+    } else {
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       fvec<VW> m[8];
@@ -676,6 +764,7 @@ __global__ __launch_bounds__(256) void wino6_output_kernel(const float* __restri
 #pragma unroll
         for (int i = 0; i < 6; ++i) axpy_c(y[i][j], w6_at(i, k), r);
       }
+    }
     }
     fvec<VW> bias4 = (fvec<VW>)0.f, sc4 = (fvec<VW>)1.f;
     if (g.bias) bias4 = *reinterpret_cast<const fvec<VW>*>(g.bias + n);
@@ -2188,8 +2277,12 @@ static int launch_wino6(const IGemmArgs& a, int B, void* ws, hipStream_t s) {
   else launch_wino6_filter(a.wt, a.ldw, N, C, a.w_unflipped ? 1 : 0, U, s);
   // channels per thread of the transforms (key 47: 1 -> 1, 2 -> 2): the 64-value tiles hold 64 VW
   // accumulators per thread
-  const bool vw2 = tune_get(PIS_TUNE_WINO_F6) == 2;
-  if (vw2)
+  const int f6 = tune_get(PIS_TUNE_WINO_F6);
+  const bool vw2 = f6 == 2;
+  if (f6 == 3)
+    hipLaunchKernelGGL(wino6_input2h_kernel, dim3(grid_of(T * (C / 2))), dim3(256), 0, s, a.src, a.lds, B, a.H, a.W,
+                       C, V);
+  else if (vw2)
     hipLaunchKernelGGL(wino6_input_kernel<2>, dim3(grid_of(T * (C / 2))), dim3(256), 0, s, a.src, a.lds, B, a.H, a.W,
                        C, V);
   else
@@ -2211,7 +2304,8 @@ static int launch_wino6(const IGemmArgs& a, int B, void* ws, hipStream_t s) {
   rc = launch_status("wino6_gemm");
   if (rc) return rc;
   gemm_done(s);
-  if (vw2) hipLaunchKernelGGL(wino6_output_kernel<2>, dim3(grid_of(T * (N / 2))), dim3(256), 0, s, Mt, a, B);
+  if (f6 == 3) hipLaunchKernelGGL((wino6_output_kernel<2, true>), dim3(grid_of(T * (N / 2))), dim3(256), 0, s, Mt, a, B);
+  else if (vw2) hipLaunchKernelGGL(wino6_output_kernel<2>, dim3(grid_of(T * (N / 2))), dim3(256), 0, s, Mt, a, B);
   else hipLaunchKernelGGL(wino6_output_kernel<1>, dim3(grid_of(T * N)), dim3(256), 0, s, Mt, a, B);
   return launch_status("wino6_output");
 }
