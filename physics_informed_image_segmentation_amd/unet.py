@@ -373,6 +373,13 @@ class UNetEngine:
     # "1" (default): every direct-kernel layer's weight gradient on the main stream right after its
     # input gradient (see the backward); "0": on the weight-gradient stream
     direct_wgrad_main = os.environ.get("PIS_DIRECT_WGRAD_MAIN", "1")
+    # a prepared layer whose input gradient runs the fused contraction + output transform (one
+    # 139-KB block per CU: it cannot share a CU, so beside the side stream's weight gradient it
+    # waits for whole CUs — dec2.conv0 at C2: 1.13 ms live, 0.45 ms alone): "1" (default) runs that
+    # layer's weight gradient on the main stream right after its input gradient. Step-neutral
+    # (21.68 / 21.62 / 22.03 vs 21.71 / 21.61 / 22.03 ms, interleaved, profiles/r6_ab2_fused_wgrad_main.txt),
+    # but the fused kernel runs at its own rate: 0.667 -> 0.459 ms per launch live
+    fused_wgrad_main = os.environ.get("PIS_FUSED_WGRAD_MAIN", "1")
 
     def __init__(self, model: UNet):
         self.m = model
@@ -875,6 +882,17 @@ class UNetEngine:
                      mask.p if mask is not None else 0, mask.ld if mask is not None else 0, ptr(scale),
                      dx.p, dx.ld, B, Hl, Wl, conv.in_channels, conv.out_channels, flags, ws, wsb, st)
 
+            if (self.fused_wgrad_main == "1" and prep and dx is not None and side is not main
+                    and lib.pis_conv3x3_filter_format(B, Hl, Wl, conv.in_channels, conv.out_channels, 1) == 2):
+                dgrad()
+                call("pis_conv3x3_wgrad_keep", x.p, x.ld, dz.p, dz.ld, self._gptr(conv.weight),
+                     self._gptr(conv.bias), B, Hl, Wl, conv.in_channels, conv.out_channels,
+                     acc | PIS_WINO_PREPARED, wsw, wswb, ptr(kept), st)
+                self.ws3_free[(nprep[0] - 1) & 1] = None  # written and read on the main stream
+                if m.grad_ready_hook is not None:
+                    to_side()
+                    ready_on_side(conv.weight, conv.bias)
+                return
             sync = self.side_sync if (prep and dx is not None and side is not main) else "prep"
             if (self.direct_wgrad_main == "1" and not prep and dx is not None and side is not main
                     and lib.pis_conv3x3_dgrad_direct(B, Hl, Wl, conv.in_channels, conv.out_channels, dz.ld, wsb)
