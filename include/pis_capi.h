@@ -195,7 +195,11 @@ int pis_version(void);
                                (358.7 vs 366.8 img/s, profiles/r6_f6*): the GEMMs -12 % per F(6x6)
                                launch but the 64-value transforms run at ~0.65 of F(4x4)'s bytes/s and
                                the weight gradients' own transforms load the side stream */
-#define PIS_TUNE_NKEYS 48
+#define PIS_TUNE_WGRAD_OUT 48 /* the F(3x3,4x4) weight gradient's slab sum + output transform
+                                 (csrc/winograd.hip launch_wino_wgrad_out): 0 64 entries per block, one
+                                 float per lane per slab row; 1 (default) float4 lanes, 64-256 entries
+                                 per block (bitwise equal: same sums in the same order) */
+#define PIS_TUNE_NKEYS 49
 #define PIS_DEBUG_NOLOAD (1 << 16)
 int pis_tune(int key, int value);
 /* Tooling (tools/bench_gemm.py): time one batched NT GEMM kernel variant in isolation,

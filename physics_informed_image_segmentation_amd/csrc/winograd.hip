@@ -1208,6 +1208,101 @@ __global__ __launch_bounds__(256) void wino4_wgrad_out_tiled_kernel(const float*
   }
 }
 
+// wino4_wgrad_out_tiled_kernel with 16-B lanes (pis_tune key 48 = 1, default; C % 4 == 0). The
+// scalar form moved 256 B per wave load over 36 x nsplit strided rows and ran at 1.14 TB/s
+// (71.6 MB in 62.7 us per launch, profiles/r5_final2). Here a block owns EPB = 64 / 128 / 256
+// consecutive (n, c) entries; pass 1: each lane sums the split slabs of 4 consecutive entries of
+// plane rows xi = xg, xg + G, ... (EPB / 4 lanes per row, G = 1024 / EPB rows at a time, two
+// slabs per unrolled step: up to 18 float4 loads in flight, 1 KB per wave load at EPB = 256);
+// pass 2: 3 EPB / 4 lanes, each one output row i of 4 entries, float4 LDS reads and dw stores.
+// Same sums in the same order per element: bitwise equal to the scalar forms.
+template <int EPB>
+__global__ __launch_bounds__(256) void wino4_wgrad_out_v4_kernel(const float* __restrict__ M, int N, int C,
+                                                                 float* __restrict__ dw, int accumulate, int nsplit,
+                                                                 int64_t sstride, WgradOutBias bias, int nb) {
+  constexpr int L = EPB / 4, G = 256 / L, Q = (36 + G - 1) / G;
+  if ((int)blockIdx.x < nb) {  // the bias gradient, as wino4_wgrad_out_tiled_kernel
+    const int n = blockIdx.x * 256 + threadIdx.x;
+    if (n < N) {
+      const float* pp = bias.part + n;
+      float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+      int r = 0;
+      for (; r + 3 < bias.rows; r += 4) {
+        s0 += pp[(size_t)r * N];
+        s1 += pp[(size_t)(r + 1) * N];
+        s2 += pp[(size_t)(r + 2) * N];
+        s3 += pp[(size_t)(r + 3) * N];
+      }
+      for (; r < bias.rows; ++r) s0 += pp[(size_t)r * N];
+      const float v = ((s0 + s1) + (s2 + s3)) * bias.scale;
+      bias.db[n] = accumulate ? bias.db[n] + v : v;
+    }
+    return;
+  }
+  __shared__ __attribute__((aligned(16))) float sm[36][EPB + 4];
+  const int64_t NC = (int64_t)N * C;
+  const int64_t e0 = (int64_t)(blockIdx.x - nb) * EPB;
+  const int tid = threadIdx.x, l4 = tid % L, xg = tid / L;
+  {
+    const float* src[Q];
+    f32x4 v[Q];
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const int xi = xg + G * q;
+      src[q] = M + (size_t)(xi < 36 ? xi : 0) * NC + e0 + 4 * l4;
+      v[q] = xi < 36 ? *reinterpret_cast<const f32x4*>(src[q]) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    int sp = 1;
+    for (; sp + 1 < nsplit; sp += 2) {
+      f32x4 a[Q][2];
+#pragma unroll
+      for (int q = 0; q < Q; ++q)
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+          if (xg + G * q < 36) a[q][u] = *reinterpret_cast<const f32x4*>(src[q] + (size_t)(sp + u) * sstride);
+#pragma unroll
+      for (int q = 0; q < Q; ++q)
+        if (xg + G * q < 36) v[q] = (v[q] + a[q][0]) + a[q][1];
+    }
+    for (; sp < nsplit; ++sp)
+#pragma unroll
+      for (int q = 0; q < Q; ++q)
+        if (xg + G * q < 36) v[q] += *reinterpret_cast<const f32x4*>(src[q] + (size_t)sp * sstride);
+#pragma unroll
+    for (int q = 0; q < Q; ++q)
+      if (xg + G * q < 36) *reinterpret_cast<f32x4*>(&sm[xg + G * q][4 * l4]) = v[q];
+  }
+  __syncthreads();
+  if (tid >= 3 * L) return;
+  const int i = tid / L, e4 = tid % L;  // output row r = i of entries 4 e4 .. 4 e4 + 3
+  f32x4 y[3];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) y[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int k = 0; k < 6; ++k) {
+    f32x4 m[6];
+#pragma unroll
+    for (int l = 0; l < 6; ++l) m[l] = *reinterpret_cast<const f32x4*>(&sm[k * 6 + l][4 * e4]);
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      f32x4 r = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int l = 0; l < 6; ++l) axpy_c(r, w4_at3(j, l), m[l]);
+      const float a = i == 0 ? w4_at3(0, k) : i == 1 ? w4_at3(1, k) : w4_at3(2, k);
+      if (a == 1.f) y[j] += r;
+      else if (a == -1.f) y[j] -= r;
+      else if (a != 0.f) y[j] += a * r;
+    }
+  }
+  const int64_t e = e0 + 4 * e4;
+  const int n = (int)(e / C), c = (int)(e - (int64_t)n * C);
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    f32x4* o = reinterpret_cast<f32x4*>(dw + ((size_t)n * 9 + i * 3 + j) * C + c);
+    *o = accumulate ? *o + y[j] : y[j];
+  }
+}
+
 // ---- the batched GEMMs (16 or 36): C[z][m][n] = sum_k A[z][m][k] B[z][n][k] ------------
 // Both operands K-contiguous ("NT"), plain row-major C, no epilogue: a lean kernel for the
 // Winograd contractions. Block tile BM x BN (4 waves, 2 x 2, each (BM/2) x (BN/2) as 32x32 MFMA
@@ -2598,7 +2693,24 @@ int launch_wino_wgrad_out(const float* M, int N, int C, float* dw, int accumulat
                           int nsplit, int64_t sstride, WgradOutBias bias) {
   if (bias.rows > 0 && !(m == 4 && ((int64_t)N * C) % 64 == 0))
     return set_error("wino_wgrad_out: the folded bias needs the tiled F(3x3,4x4) transform"), PIS_ERR_ARG;
-  if (m == 4 && ((int64_t)N * C) % 64 == 0) {
+  const int64_t NC = (int64_t)N * C;
+  auto a16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+  if (m == 4 && NC % 64 == 0 && C % 4 == 0 && tune_get(PIS_TUNE_WGRAD_OUT) == 1 && a16(M) && a16(dw) &&
+      sstride % 4 == 0) {
+    // the widest block that still leaves >= 512 blocks (every CU busy twice)
+    const int nb = bias.rows > 0 ? (N + 255) / 256 : 0;
+    const int epb = (NC % 256 == 0 && NC / 256 >= 512) ? 256 : (NC % 128 == 0 && NC / 128 >= 512) ? 128 : 64;
+    const dim3 grid((unsigned)(NC / epb + nb));
+    if (epb == 256)
+      hipLaunchKernelGGL(wino4_wgrad_out_v4_kernel<256>, grid, dim3(256), 0, s, M, N, C, dw, accumulate, nsplit,
+                         sstride, bias, nb);
+    else if (epb == 128)
+      hipLaunchKernelGGL(wino4_wgrad_out_v4_kernel<128>, grid, dim3(256), 0, s, M, N, C, dw, accumulate, nsplit,
+                         sstride, bias, nb);
+    else
+      hipLaunchKernelGGL(wino4_wgrad_out_v4_kernel<64>, grid, dim3(256), 0, s, M, N, C, dw, accumulate, nsplit,
+                         sstride, bias, nb);
+  } else if (m == 4 && ((int64_t)N * C) % 64 == 0) {
     const int nb = bias.rows > 0 ? (N + 255) / 256 : 0;
     hipLaunchKernelGGL(wino4_wgrad_out_tiled_kernel, dim3((unsigned)((int64_t)N * C / 64 + nb)), dim3(256), 0, s, M,
                        N, C, dw, accumulate, nsplit, sstride, bias, nb);

@@ -991,6 +991,40 @@ def test_wino_wgrad_split_slabs(hip):
         assert rel_err(dw.cpu().double(), ref) < 5e-6
 
 
+@pytest.mark.parametrize("B,H,W,Cin,Cout", [(4, 64, 64, 256, 256), (2, 32, 32, 512, 512), (2, 64, 64, 128, 64),
+                                             (1, 48, 40, 128, 256), (8, 128, 128, 256, 256)])
+def test_wino_wgrad_out_float4_bitwise(hip, B, H, W, Cin, Cout):
+    """The float4 slab sum + output transform (pis_tune(48, 1), 64 / 128 / 256 entries per block by
+    layer size) writes the weight and folded bias gradients bitwise as the scalar tiled form
+    (48 = 0), plain and accumulating, and both sit at the F(3x3,4x4) accuracy against float64."""
+    g = torch.Generator().manual_seed(B + H + Cin)
+    x = F.relu(torch.randn(B, Cin, H, W, generator=g)).double()
+    dz = torch.randn(B, Cout, H, W, generator=g).double()
+    dw_ref = torch.nn.grad.conv2d_weight(x, (Cout, Cin, 3, 3), dz, padding=1).permute(0, 2, 3, 1)
+    xd, dzd = nhwc(x.float()).cuda(), nhwc(dz.float()).cuda()
+    nws = hip.pis_conv3x3_wgrad_ws(B, H, W, Cin, Cout)
+    ws = torch.empty(nws // 4 + 1, device="cuda")
+    dw0, db0 = torch.randn(Cout, 3, 3, Cin, generator=g).cuda(), torch.randn(Cout, generator=g).cuda()
+    outs = {}
+    for key in (0, 1):
+        prev = hip.pis_tune(48, key)
+        try:
+            for flags in (0, 8):  # PIS_ACCUMULATE
+                dw, db = dw0.clone(), db0.clone()
+                rc = hip.pis_conv3x3_wgrad(xd.data_ptr(), Cin, dzd.data_ptr(), Cout, dw.data_ptr(), db.data_ptr(), B,
+                                           H, W, Cin, Cout, flags, ws.data_ptr(), nws, s())
+                assert rc == 0, hip.pis_last_error()
+                torch.cuda.synchronize()
+                outs[key, flags] = (dw.cpu(), db.cpu())
+        finally:
+            hip.pis_tune(48, prev)
+    for flags in (0, 8):
+        assert torch.equal(outs[0, flags][0], outs[1, flags][0]), flags
+        assert torch.equal(outs[0, flags][1], outs[1, flags][1]), flags
+    assert rel_err(outs[1, 0][0].double(), dw_ref) < 5e-6
+    assert rel_err(outs[1, 0][1].double(), dz.sum(dim=(0, 2, 3))) < 1e-5
+
+
 @pytest.mark.parametrize("Cin,Cout", [(128, 64), (512, 256)])
 def test_convt_bf16x6_is_fp32_accurate(hip, Cin, Cout):
     """Transposed conv forward / input gradient (key 13: 1 bf16x6, 3 fp16x3 vs 2 fp32 MFMA) and
