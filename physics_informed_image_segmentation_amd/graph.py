@@ -45,7 +45,13 @@ class StepGraph:
     the events, the engine, then the stream. ``close()`` also runs when the StepGraph is garbage
     collected without it."""
 
-    def __init__(self, model: UNet, criterion, optimizer, x: torch.Tensor, target: torch.Tensor, warmup: int = 2):
+    def __init__(self, model: UNet, criterion, optimizer, x: torch.Tensor, target: torch.Tensor, warmup: int = 2,
+                 fused_loss: bool = False, before_capture=None):
+        """``fused_loss``: the step runs ``model.forward_with_loss`` (the head + loss forward in one
+        kernel, as bench.py and train_epoch do) instead of ``criterion(model(x), target)``.
+        ``before_capture``: called once after the eager warm-up steps, right before the capture
+        (bench.py clears its launch-hook timers there, so the events the hooks record during the
+        capture — graph nodes, re-recorded by every replay — are the only ones they hold)."""
         if not x.is_cuda:
             raise RuntimeError("StepGraph needs the model and batch on the GPU")
         if model.grad_ready_hook is not None or (dist.is_available() and dist.is_initialized()
@@ -53,6 +59,7 @@ class StepGraph:
             raise RuntimeError("StepGraph captures a single-process step: data-parallel all-reduces "
                                "(GradBucketer) cannot be replayed from a graph")
         self.graph = None
+        self.fused_loss = fused_loss
         self.model, self.criterion, self.opt = model, criterion, optimizer
         self.x, self.t = x, target
         B = x.shape[0]
@@ -79,8 +86,10 @@ class StepGraph:
         # captured on the warm-up stream: autograd's AccumulateGrad nodes remember the stream they
         # were created on, and one created on another stream syncs with it mid-capture (a model
         # that already ran eager steps on the default stream crashes torch-ROCm's capture_end)
+        if before_capture is not None:
+            before_capture()
         with torch.cuda.graph(self.graph, stream=side):
-            self.loss = criterion(model(self.x), self.t)
+            self.loss = self._forward_loss()
             self.loss.backward()
         # the events the capture recorded through, including the engine's workspace fences
         self._events = list(self.engine.capture_events) + [e for e in self.engine.ws3_free if e is not None]
@@ -93,10 +102,15 @@ class StepGraph:
         for n, p, _ in self.blocks:
             self.scales[n].bernoulli_(1.0 - p).div_(1.0 - p)
 
+    def _forward_loss(self):
+        if self.fused_loss:
+            return self.model.forward_with_loss(self.x, self.t, self.criterion)[1]
+        return self.criterion(self.model(self.x), self.t)
+
     def _eager(self):
         self._refill()
         self.opt.zero_grad(set_to_none=True)
-        loss = self.criterion(self.model(self.x), self.t)
+        loss = self._forward_loss()
         loss.backward()
         self.opt.step()
         return loss

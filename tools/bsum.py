@@ -14,4 +14,5 @@ for path in sys.argv[1:]:
         print(f"{path}: {d['value']:.1f} img/s {d['ms_per_step']:.3f} ms  gemm {d['roofline_gemm']['frac']:.3f} "
               f"({d['roofline_gemm']['ms_per_step']:.2f} ms)  hl_fwd kernel {hk.get('frac', 0):.3f} "
               f"({hk.get('avg_launch_ms', 0) * 1e3:.1f} us) call {hc.get('frac', 0):.3f} "
-              f"({hc.get('avg_call_ms', 0) * 1e3:.1f} us)  loss_fwd/floor {lf.get('floor', {}).get('loss_over_floor', 0):.2f}")
+              f"({hc.get('avg_call_ms', 0) * 1e3:.1f} us)  loss_fwd/floor {lf.get('floor', {}).get('loss_over_floor', 0):.2f}"
+              f"  mode {d.get('step_mode', 'eager')[:9]} eager {d.get('ms_per_step_eager') or 0:.3f} ms")

@@ -27,6 +27,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--part", default="parity,timing")
+    ap.add_argument("--fused", action="store_true", help="head + loss forward in one kernel (UNet.forward_with_loss), "
+                    "as bench.py's step")
     args = ap.parse_args()
     dev = torch.device("cuda")
     g = torch.Generator().manual_seed(42)
@@ -34,9 +36,12 @@ def main():
     x, t = torch.stack(imgs).to(dev), torch.stack(masks).to(dev)
     crit = DiceBCEPDELoss(pde_weight=1e-4, phase_field_weight=1e-4, diffusion_coeff=5.0, epsilon=0.05)
 
+    def fwd_loss(m):
+        return m.forward_with_loss(x, t, crit)[1] if args.fused else crit(m(x), t)
+
     def eager_step(m, opt):
         opt.zero_grad(set_to_none=True)
-        crit(m(x), t).backward()
+        fwd_loss(m).backward()
         opt.step()
 
     def capture(m, opt):
@@ -50,7 +55,7 @@ def main():
         graph = torch.cuda.CUDAGraph()
         opt.zero_grad(set_to_none=True)
         with torch.cuda.graph(graph, stream=s):
-            crit(m(x), t).backward()
+            fwd_loss(m).backward()
         return graph
 
     if "parity" in args.part:
