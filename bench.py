@@ -286,8 +286,9 @@ DIRECT_ROLES = {
     "direct_h3_dgrad": ("roofline_direct_dgrad", "conv3x3_h3_kernel<false, true|false, false, true> (input gradient "
                         "on the original weights; the ReLU-mask rows prefetched where masked)",
                         ["conv3x3_h3_kernel<false, true, false, true>", "conv3x3_h3_kernel<false, false, false, true>"]),
-    "direct_wgrad_h3": ("roofline_direct_wgrad", "conv3x3_wgrad_h3_kernel (weight gradient: 4-row tiles, split-K "
-                        "slabs)", ["conv3x3_wgrad_h3_kernel"]),
+    "direct_wgrad_h3": ("roofline_direct_wgrad", "conv3x3_wgrad_h3r_kernel<2> (weight gradient: 2-row tiles, two "
+                        "blocks per CU, split-K slabs; pis_tune(49, 4): the 4-row conv3x3_wgrad_h3_kernel)",
+                        ["conv3x3_wgrad_h3r_kernel", "conv3x3_wgrad_h3_kernel"]),
 }
 
 

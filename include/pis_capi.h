@@ -199,7 +199,12 @@ int pis_version(void);
                                  (csrc/winograd.hip launch_wino_wgrad_out): 0 64 entries per block, one
                                  float per lane per slab row; 1 (default) float4 lanes, 64-256 entries
                                  per block (bitwise equal: same sums in the same order) */
-#define PIS_TUNE_NKEYS 49
+#define PIS_TUNE_DIRECT_W_ROWS 49 /* the direct weight gradient's tile rows (csrc/direct.hip): 2 (default) two
+                                     blocks per CU (51 KB LDS, <= 256 registers each), no register prefetch;
+                                     4 (any other value) one block per CU, the next tile's loads in registers.
+                                     2 vs 4: -2..-10 % per layer isolated, step 22.08 -> 21.76 ms
+                                     (profiles/r6_d1_direct_wgrad_rows.txt) */
+#define PIS_TUNE_NKEYS 50
 #define PIS_DEBUG_NOLOAD (1 << 16)
 int pis_tune(int key, int value);
 /* Tooling (tools/bench_gemm.py): time one batched NT GEMM kernel variant in isolation,

@@ -17,7 +17,7 @@ void set_error(const char* fmt, ...) {
 // kernel-variant knobs (defaults = the measured best on MI355X)
 static std::atomic<int> g_tune[PIS_TUNE_NKEYS] = {0, 16, 0, 1, 0, 1, 512, 0, 1, 1024, 4, 1, 0, 4, 3, 1, 1, 2,
                                                    1, 1, 1, 0, 1, 0, 0, 0, 2, 1, 0, 1, 0, 1, 1, 0, 0, 512, 0, 0, 1, 2, 2, 0, 1, 1, 0, 0, 1,
-                                                   0, 1};
+                                                   0, 1, 2};
 
 int tune_get(int key) { return (key > 0 && key < PIS_TUNE_NKEYS) ? g_tune[key].load() : 0; }
 

@@ -730,6 +730,219 @@ __global__ __launch_bounds__(256, 1) void conv3x3_wgrad_h3_kernel(DirectWArgs g)
 }
 
 
+// The same weight gradient on TH-row tiles (pis_tune key 49 = TH = 2): two blocks per CU instead of
+// one. The 4-row kernel above runs ONE wave per SIMD (85 KB LDS, ~290 registers), so nothing hides
+// its staging (global loads, block maxima, split, LDS stores: ~35 % of its time, the timing twins
+// of profiles/r4_h_*). Here a tile is TH x 32 pixels: dz 64 px x 64 ch and the (TH + 2) x 34 x halo
+// in hi / lo planes = 51 KB of LDS at TH = 2, no register prefetch of the next tile (its loads are
+// issued at the top of each tile: the second block of the CU computes meanwhile), <= 256 registers
+// -> two independent blocks per CU, one staging while the other multiplies. Same per-tile
+// arithmetic as the 4-row kernel (tile scales, halo-row-major MFMA order); the sums differ from it
+// only by the tile grouping (fp32-class either way; tests/test_direct_gpu.py).
+template <int TH>
+__global__ __launch_bounds__(256, 2) void conv3x3_wgrad_h3r_kernel(DirectWArgs g) {
+  constexpr int NW = 4, NT = 64 * NW, NTAP = 9;
+  constexpr int TP = TH * WT_W, HHh = TH + 2, HP = HHh * WH_W;  // tile pixels, halo rows, halo pixels
+  constexpr int ZH = TP * 64, XH = HP * 64;                       // fp16 per plane
+  constexpr int ZI = TP * 8, XI = HP * 8;                         // 8-channel groups
+  constexpr int Z_PER_T = ZI / NT, X_PER_T = (XI + NT - 1) / NT;
+  static_assert(ZI % NT == 0, "dz items tile the block");
+  __shared__ __attribute__((aligned(16))) char smem[2 * (ZH + XH) * 2 + 64];
+  _Float16* sz = reinterpret_cast<_Float16*>(smem);
+  _Float16* sx = reinterpret_cast<_Float16*>(smem + 2 * ZH * 2);
+  float* red = reinterpret_cast<float*>(smem + 2 * (ZH + XH) * 2);
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wi = (wave >> 1) & 1, wj = wave & 1;  // n-half, c-half
+  const int ncb = g.Cin / 64, pairs = (g.Cout / 64) * ncb;
+  int pair, split;
+  if (g.vwalk && (g.splits & 7) == 0) {
+    const int bid = blockIdx.x, xcd = bid & 7, j = bid >> 3;
+    pair = j % pairs;
+    split = (j / pairs) * 8 + xcd;
+  } else {
+    pair = blockIdx.x % pairs;
+    split = blockIdx.x / pairs;
+  }
+  const int n0 = (pair / ncb) * 64, c0 = (pair % ncb) * 64;
+  const int tw_n = g.W / WT_W, nrq = g.H / TH, per_img = nrq * tw_n, ntile = g.B * per_img;
+  const bool do_bias = g.part_bias != nullptr && c0 == 0;
+  const int tps = (ntile + g.splits - 1) / g.splits;
+  const int t_begin = g.vwalk ? split * tps : split, t_end = g.vwalk ? min(ntile, t_begin + tps) : ntile;
+  const int t_step = g.vwalk ? 1 : g.splits;
+
+  f32x16 acc[NTAP];
+#pragma unroll
+  for (int t = 0; t < NTAP; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+  float bs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  float sz_cur = 0.f, sx_cur = 0.f, sz_min = __builtin_inff(), sx_min = __builtin_inff();
+  const int gq = lane >> 4, q0 = (lane & 15) >> 2, p = lane & 3;
+  const int kh0 = gq >> 1;
+  const int cgA0 = 4 * wi + 2 * (gq & 1) + (p >> 1), cgB0 = 4 * wj + 2 * (gq & 1) + (p >> 1);
+
+#pragma unroll 1
+  for (int t = t_begin; t < t_end; t += t_step) {
+    // 1. this tile's global loads, block maxima
+    f32x4 zr[Z_PER_T][2], xr[X_PER_T][2];
+    {
+      const int b = t / per_img, rem = t - b * per_img;
+      const int pr0 = (g.vwalk ? rem % nrq : rem / tw_n) * TH, pc0 = (g.vwalk ? rem / nrq : rem % tw_n) * WT_W;
+      const size_t img = (size_t)b * g.H * g.W;
+#pragma unroll
+      for (int j = 0; j < Z_PER_T; ++j) {
+        const int i = tid + NT * j, px = i >> 3, cg = i & 7;
+        const float* pz = g.dz + (img + (size_t)(pr0 + (px >> 5)) * g.W + pc0 + (px & 31)) * g.ldz + n0 + 8 * cg;
+        zr[j][0] = *reinterpret_cast<const f32x4*>(pz);
+        zr[j][1] = *reinterpret_cast<const f32x4*>(pz + 4);
+      }
+#pragma unroll
+      for (int j = 0; j < X_PER_T; ++j) {
+        const int i = tid + NT * j, qq = i >> 3, cg = i & 7;
+        xr[j][0] = xr[j][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (i < XI) {
+          const int qr = qq / WH_W, qc = qq - qr * WH_W, row = pr0 - 1 + qr, col = pc0 - 1 + qc;
+          if (row >= 0 && row < g.H && col >= 0 && col < g.W) {
+            const float* px_ = g.x + (img + (size_t)row * g.W + col) * g.ldx + c0 + 8 * cg;
+            xr[j][0] = *reinterpret_cast<const f32x4*>(px_);
+            xr[j][1] = *reinterpret_cast<const f32x4*>(px_ + 4);
+          }
+        }
+      }
+    }
+    float mz = wave_max_nonneg(absmax_x4(zr));
+    float mx = wave_max_nonneg(absmax_x4(xr));
+    if (lane == 0) {
+      red[wave] = mz;
+      red[NW + wave] = mx;
+    }
+    if (do_bias) {
+#pragma unroll
+      for (int j = 0; j < Z_PER_T; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          bs[e] += zr[j][0][e];
+          bs[4 + e] += zr[j][1][e];
+        }
+    }
+    __syncthreads();  // also: the previous tile's fragment reads are done
+    // 2. scales, accumulators re-expressed, split into LDS
+    mz = red[0];
+    mx = red[NW];
+#pragma unroll
+    for (int w = 1; w < NW; ++w) {
+      mz = fmaxf(mz, red[w]);
+      mx = fmaxf(mx, red[NW + w]);
+    }
+    const float sz_new = h3_keep(sz_cur, mz, sz_min), sx_new = h3_keep(sx_cur, mx, sx_min);
+    if (sz_cur > 0.f && (sz_new != sz_cur || sx_new != sx_cur)) {
+      const float f = (sz_new / sz_cur) * (sx_new / sx_cur);
+#pragma unroll
+      for (int k = 0; k < NTAP; ++k) acc[k] *= f;
+    }
+    sz_cur = sz_new;
+    sx_cur = sx_new;
+#pragma unroll
+    for (int j = 0; j < Z_PER_T; ++j) {
+      const int i = tid + NT * j, px = i >> 3, cg = i & 7;
+      u32x2 h0, l0, h1, l1;
+      split2h_x4(zr[j][0] * sz_cur, h0, l0);
+      split2h_x4(zr[j][1] * sz_cur, h1, l1);
+      *reinterpret_cast<u32x4*>(&sz[wsw64(px, cg)]) = u32x4{h0[0], h0[1], h1[0], h1[1]};
+      *reinterpret_cast<u32x4*>(&sz[ZH + wsw64(px, cg)]) = u32x4{l0[0], l0[1], l1[0], l1[1]};
+    }
+#pragma unroll
+    for (int j = 0; j < X_PER_T; ++j) {
+      const int i = tid + NT * j, qq = i >> 3, cg = i & 7;
+      if (i < XI) {
+        u32x2 h0, l0, h1, l1;
+        split2h_x4(xr[j][0] * sx_cur, h0, l0);
+        split2h_x4(xr[j][1] * sx_cur, h1, l1);
+        *reinterpret_cast<u32x4*>(&sx[wsw64(qq, cg)]) = u32x4{h0[0], h0[1], h1[0], h1[1]};
+        *reinterpret_cast<u32x4*>(&sx[XH + wsw64(qq, cg)]) = u32x4{l0[0], l0[1], l1[0], l1[1]};
+      }
+    }
+    __syncthreads();
+    // 3. halo-row-major MFMA phase (as the 4-row kernel): A fragments once per tile, each B fragment
+    // once per halo row
+    // the fragment addresses are tile-invariant: laundered per tile so the compiler recomputes them
+    // instead of keeping ~100 of them live across the tile loop (two waves per SIMD: <= 256 registers)
+    int q = q0, kh = kh0, cgA = cgA0, cgB = cgB0;
+    asm volatile("" : "+v"(q), "+v"(kh), "+v"(cgA), "+v"(cgB));
+    f16x8 af[TH][2][2];
+#pragma unroll
+    for (int rr = 0; rr < TH; ++rr)
+#pragma unroll
+      for (int cc = 0; cc < 2; ++cc)
+#pragma unroll
+        for (int pl = 0; pl < 2; ++pl) {
+          const _Float16* base = sz + pl * ZH;
+          const int px = 16 * (2 * rr + cc) + 8 * kh + q;
+          const s16x4 lo4 = tr_read(base + wsw64(px, cgA) + 4 * (p & 1));
+          const s16x4 hi4 = tr_read(base + wsw64(px + 4, cgA) + 4 * (p & 1));
+          af[rr][cc][pl] = __builtin_bit_cast(f16x8, __builtin_shufflevector(lo4, hi4, 0, 1, 2, 3, 4, 5, 6, 7));
+        }
+    // one B fragment set (registers: two waves per SIMD need <= 256; the SIMD's other wave hides
+    // the LDS latency the 4-row kernel's read-ahead set hides)
+    f16x8 bf[3][2];
+#pragma unroll
+    for (int st = 0; st < 2 * HHh; ++st) {  // (h, cc) = (st >> 1, st & 1)
+      const int h = st >> 1, cc = st & 1;
+#pragma unroll
+      for (int s = 0; s < 3; ++s) {
+        const int hp = h * WH_W + 16 * cc + 8 * kh + q + s;
+#pragma unroll
+        for (int pl = 0; pl < 2; ++pl) {
+          const _Float16* base = sx + pl * XH;
+          const s16x4 lo4 = tr_read(base + wsw64(hp, cgB) + 4 * (p & 1));
+          const s16x4 hi4 = tr_read(base + wsw64(hp + 4, cgB) + 4 * (p & 1));
+          bf[s][pl] = __builtin_bit_cast(f16x8, __builtin_shufflevector(lo4, hi4, 0, 1, 2, 3, 4, 5, 6, 7));
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 3; ++r) {
+        const int rr = h - r;
+        if (rr < 0 || rr >= TH) continue;
+#pragma unroll
+        for (int s = 0; s < 3; ++s) {
+          const int tt = 3 * r + s;
+          acc[tt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[rr][cc][1], bf[s][0], acc[tt], 0, 0, 0);
+          acc[tt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[rr][cc][0], bf[s][1], acc[tt], 0, 0, 0);
+          acc[tt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[rr][cc][0], bf[s][0], acc[tt], 0, 0, 0);
+        }
+      }
+    }
+  }
+
+  const float inv = (sz_cur > 0.f) ? (1.f / sz_cur) * (1.f / sx_cur) : 0.f;
+  float* slab = g.part + (size_t)split * g.Cout * 9 * g.Cin;
+  const int c = c0 + 32 * wj + (lane & 31);
+#pragma unroll
+  for (int tt = 0; tt < NTAP; ++tt) {
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+      const int n = n0 + 32 * wi + (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5);
+      slab[((size_t)n * 9 + tt) * g.Cin + c] = acc[tt][reg] * inv;
+    }
+  }
+  if (do_bias) {
+    __syncthreads();  // the last tile's fragment reads are done before the LDS is reused
+    float* rb = reinterpret_cast<float*>(smem);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) rb[tid * 8 + e] = bs[e];
+    __syncthreads();
+    if (tid < 64) {
+      const int cg = tid >> 3, e = tid & 7;
+      float sum = 0.f;
+      for (int k = 0; k < NT / 8; ++k) sum += rb[(8 * k + cg) * 8 + e];
+      g.part_bias[(size_t)split * g.Cout + n0 + tid] = sum;
+    }
+  }
+}
+
+
+// tile rows of the direct weight gradient: 4 (one block per CU) or 2 (pis_tune key 49: two per CU)
+static int direct_w_rows() { return tune_get(PIS_TUNE_DIRECT_W_ROWS) == 2 ? 2 : WT_H; }
 
 bool direct_w_wanted(int B, int H, int W, int Cin, int Cout, int ldx, int ldz) {
   if (!(B > 0 && H % WT_H == 0 && W % WT_W == 0 && Cin % 64 == 0 && Cout % 64 == 0 && ldz % 4 == 0 && ldx % 4 == 0))
@@ -737,10 +950,12 @@ bool direct_w_wanted(int B, int H, int W, int Cin, int Cout, int ldx, int ldz) {
   return direct_h3_wanted(H, W, Cin, Cout, ldx);
 }
 
+// blocks: one per CU (4-row tiles) or two (2-row tiles), split over the (Cout, Cin) 64-blocks
 static int direct_w_splits(int B, int H, int W, int Cin, int Cout) {
+  const int rows = direct_w_rows(), target = rows == 2 ? 512 : 256;
   const int pairs = (Cout / 64) * (Cin / 64);
-  const int ntile = B * (H / WT_H) * (W / WT_W);
-  return std::max(1, std::min(ntile, 256 / std::max(1, std::min(pairs, 256))));
+  const int ntile = B * (H / rows) * (W / WT_W);
+  return std::max(1, std::min(ntile, target / std::max(1, std::min(pairs, target))));
 }
 
 size_t direct_w_ws_bytes(int B, int H, int W, int Cin, int Cout) {
@@ -768,6 +983,8 @@ int launch_direct_wgrad(const float* x, int ldx, const float* dz, int ldz, float
   launch_hook("direct_wgrad_h3", 0, s, flop);
   if (g.dbg)
     hipLaunchKernelGGL((conv3x3_wgrad_h3_kernel<true>), grid, dim3(256), 0, s, g);
+  else if (direct_w_rows() == 2)
+    hipLaunchKernelGGL((conv3x3_wgrad_h3r_kernel<2>), grid, dim3(256), 0, s, g);
   else
     hipLaunchKernelGGL((conv3x3_wgrad_h3_kernel<false>), grid, dim3(256), 0, s, g);
   launch_hook("direct_wgrad_h3", 1, s, flop);

@@ -83,8 +83,9 @@ def _fwd(hip, x, w, b, scale, flags, pool=False, ldx_extra=0):
 # kernel variants behind pis_tune: key 32 the input gradient's mask prefetch (default on)
 FWD_VARIANTS = [dict(), dict(k32=0)]
 # weight gradient: key 43 = 1 (default) each block walks a contiguous run of tiles down the image
-# columns, 0 the strided round-3 tile order
-WG_VARIANTS = [dict(), dict(k43=0)]
+# columns, 0 the strided round-3 tile order; key 49 = 2 (default): 2-row tiles, two blocks per CU, 4:
+# the 4-row kernel
+WG_VARIANTS = [dict(), dict(k43=0), dict(k49=4), dict(k49=4, k43=0)]
 
 
 @pytest.mark.parametrize("variant", FWD_VARIANTS)
@@ -290,7 +291,7 @@ def test_direct_wgrad_x_magnitude_down_the_strip(hip, variant):
     assert errs["direct"] < 5e-6, errs
 
 
-@pytest.mark.parametrize("knobs", [dict(k29=2), dict(k29=2, k43=0)])
+@pytest.mark.parametrize("knobs", [dict(k29=2), dict(k29=2, k43=0), dict(k29=2, k49=4)])
 @pytest.mark.parametrize("loss_kw", [dict(), dict(rd_w=1e-2, pf_w=1e-2, D=5.0, a=0.5, eps=0.05)])
 def test_train_step_with_direct_convs(hip, loss_kw, knobs):
     """The whole training step with every eligible conv on the direct kernels (key 29 = 2: forward
