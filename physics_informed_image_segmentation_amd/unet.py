@@ -380,6 +380,9 @@ class UNetEngine:
     # (21.68 / 21.62 / 22.03 vs 21.71 / 21.61 / 22.03 ms, interleaved, profiles/r6_ab2_fused_wgrad_main.txt),
     # but the fused kernel runs at its own rate: 0.667 -> 0.459 ms per launch live
     fused_wgrad_main = os.environ.get("PIS_FUSED_WGRAD_MAIN", "1")
+    # the U-Net levels (digits 1-4) whose transposed conv's weight gradient runs on the main stream
+    # right after its input gradient, in the main workspace, instead of on the weight-gradient stream
+    convt_wgrad_main = os.environ.get("PIS_CONVT_WGRAD_MAIN", "")
 
     def __init__(self, model: UNet):
         self.m = model
@@ -968,11 +971,21 @@ class UNetEngine:
             else:
                 xin = _Buf(bf[f"d1_{l + 1}"], up.in_channels)
             Hh, Wh = Hl // 2, Wl // 2
+            g_in = _Buf(gb(f"g_upin{l}", B, Hh, Wh, up.in_channels), up.in_channels)
+            if str(l) in self.convt_wgrad_main and side is not main:
+                call("pis_convt2x2_dgrad", g_cat.p, g_cat.ld, flips[id(up)].data_ptr(), xin.p, xin.ld, g_in.p,
+                     g_in.ld, B, Hh, Wh, up.in_channels, up.out_channels, PIS_MASK, st)
+                call("pis_convt2x2_wgrad", xin.p, xin.ld, g_cat.p, g_cat.ld, self._gptr(up.weight),
+                     self._gptr(up.bias), B, Hh, Wh, up.in_channels, up.out_channels, acc, ws, wsb, st)
+                if m.grad_ready_hook is not None:
+                    to_side()
+                    ready_on_side(up.weight, up.bias)
+                g_top = g_in
+                continue
             to_side()
             call("pis_convt2x2_wgrad", xin.p, xin.ld, g_cat.p, g_cat.ld, self._gptr(up.weight), self._gptr(up.bias),
                  B, Hh, Wh, up.in_channels, up.out_channels, acc, ws2, wsb, sst)
             ready_on_side(up.weight, up.bias)
-            g_in = _Buf(gb(f"g_upin{l}", B, Hh, Wh, up.in_channels), up.in_channels)
             call("pis_convt2x2_dgrad", g_cat.p, g_cat.ld, flips[id(up)].data_ptr(), xin.p, xin.ld, g_in.p, g_in.ld,
                  B, Hh, Wh, up.in_channels, up.out_channels, PIS_MASK, st)
             g_top = g_in

@@ -448,3 +448,33 @@ def test_engine_direct_splits_ahead_bitwise(hip):
         assert torch.equal(res["0"][0], res[mode][0]), mode
         for a, b in zip(res["0"][1], res[mode][1]):
             assert torch.equal(a, b), mode
+
+
+def test_engine_schedule_knobs_bitwise(hip):
+    """The backward's stream placements (unet.UNetEngine): the direct layers' weight gradients
+    (PIS_DIRECT_WGRAD_MAIN), the fused-input-gradient layer's weight gradient (PIS_FUSED_WGRAD_MAIN)
+    and the transposed convs' weight gradients (PIS_CONVT_WGRAD_MAIN levels) on the main stream or
+    the weight-gradient stream run the same kernels on the same splits, so one training step is
+    bitwise the same either way — B = 1 at 256 x 256 engages all three (direct 256^2 layers, the
+    fused dec2.conv0 input gradient at 128^2, four transposed convs)."""
+    from physics_informed_image_segmentation_amd import unet as U
+    assert hip.pis_conv3x3_filter_format(1, 256, 256, 64, 64, 0) == 3  # direct
+    assert hip.pis_conv3x3_filter_format(1, 128, 128, 256, 128, 1) == 2  # fused input gradient
+    knobs = (("direct_wgrad_main", "0"), ("fused_wgrad_main", "0"), ("convt_wgrad_main", "1234"))
+    prev = {a: getattr(U.UNetEngine, a) for a, _ in knobs}
+    res = {}
+    try:
+        u, grads, _ = _hip_step(1, 256, 256)
+        res["default"] = (u, grads)
+        for a, v in knobs:
+            setattr(U.UNetEngine, a, v)
+            u, grads, _ = _hip_step(1, 256, 256)
+            res[a] = (u, grads)
+            setattr(U.UNetEngine, a, prev[a])
+    finally:
+        for a, v in prev.items():
+            setattr(U.UNetEngine, a, v)
+    for a, _ in knobs:
+        assert torch.equal(res["default"][0], res[a][0]), a
+        for g0, g1 in zip(res["default"][1], res[a][1]):
+            assert torch.equal(g0, g1), a

@@ -27,7 +27,8 @@ def parse(v):
 
 # host-side engine attributes a variant may set (unet.UNetEngine): fa = filter_ahead, dwm =
 # direct_wgrad_main, ss = side_sync (prep / gemm / dgrad)
-HOST = {"fa": "filter_ahead", "dwm": "direct_wgrad_main", "ss": "side_sync"}
+HOST = {"fa": "filter_ahead", "dwm": "direct_wgrad_main", "ss": "side_sync", "fwm": "fused_wgrad_main",
+        "cwm": "convt_wgrad_main"}
 
 
 def main():
