@@ -182,6 +182,20 @@ def test_c2_train_step_every_gradient_and_rd_bound(hip):
     assert e_hip <= max(10.0 * e_ref, TOL * abs(rd64)), (e_hip, e_ref)
 
 
+def test_c2_train_step_wino6_opt_in(hip):
+    """The opt-in Winograd F(6x6,3x3) deep layers (pis_tune(47, 1): the 128^2 and 64^2 layers of a
+    512^2 image, forward and input gradient) through one whole C2-size training step against the
+    float64 truth at the north-star 1e-4 (per tensor and per element), as the default path."""
+    prev = hip.pis_tune(47, 1)
+    try:
+        assert hip.pis_conv3x3_filter_format(1, 128, 128, 256, 256, 0) == 4  # an F(6x6) layer
+        kw = dict(rd_w=1e-4, pf_w=1e-4, D=5.0, a=0.5, eps=0.05)
+        img, mask, ref, scales, runs, p64, z64, flips, truth = _run(512, 512, [kw], seed=43)
+    finally:
+        hip.pis_tune(47, prev)
+    _check_step(runs[0], p64, z64, truth[0], flips, 512 * 512, skip_terms=("pde_loss",))
+
+
 def test_c5_train_step_d_sweep_ends(hip):
     kws = [dict(rd_w=1e-3, pf_w=0.0, D=D, a=0.5) for D in (0.5, 100.0)]
     img, mask, ref, scales, runs, p64, z64, flips, truth = _run(1024, 1024, kws, seed=5)
