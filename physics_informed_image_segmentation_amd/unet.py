@@ -371,7 +371,8 @@ class UNetEngine:
     # 3 at 21.68-21.96 (profiles/r5_j_ab_filter_ahead.txt).
     filter_ahead = os.environ.get("PIS_FILTER_AHEAD", "5")
     # "1" (default): every direct-kernel layer's weight gradient on the main stream right after its
-    # input gradient (see the backward); "0": on the weight-gradient stream
+    # input gradient (see the backward); "0": on the weight-gradient stream; "dec": the decoder's on
+    # the main stream, the encoder's on the weight-gradient stream
     direct_wgrad_main = os.environ.get("PIS_DIRECT_WGRAD_MAIN", "1")
     # a prepared layer whose input gradient runs the fused contraction + output transform (one
     # 139-KB block per CU: it cannot share a CU, so beside the side stream's weight gradient it
@@ -829,6 +830,7 @@ class UNetEngine:
 
         lib = _hip.lib()
         nprep = [0]
+        enc_convs = {id(cv) for l in (1, 2, 3, 4) for cv in (m.block(f"enc{l}").conv0, m.block(f"enc{l}").conv1)}
 
         def conv_bwd(conv, x: _Buf, dz: _Buf, dx: Optional[_Buf], Hl, Wl, mask: Optional[_Buf], scale):
             kept = self.keep.get(id(conv))
@@ -897,7 +899,8 @@ class UNetEngine:
                     ready_on_side(conv.weight, conv.bias)
                 return
             sync = self.side_sync if (prep and dx is not None and side is not main) else "prep"
-            if (self.direct_wgrad_main == "1" and not prep and dx is not None and side is not main
+            on_main = self.direct_wgrad_main == "1" or (self.direct_wgrad_main == "dec" and id(conv) not in enc_convs)
+            if (on_main and not prep and dx is not None and side is not main
                     and lib.pis_conv3x3_dgrad_direct(B, Hl, Wl, conv.in_channels, conv.out_channels, dz.ld, wsb)
                     and lib.pis_conv3x3_wgrad_ws(B, Hl, Wl, conv.in_channels, conv.out_channels) <= wsb):
                 # a direct layer's weight gradient on the main stream right after its input gradient,
