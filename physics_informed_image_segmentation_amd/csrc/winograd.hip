@@ -1121,6 +1121,25 @@ __global__ __launch_bounds__(256) void wino4_wgrad_out_kernel(const float* __res
   }
 }
 
+// the folded bias gradient (WgradOutBias) of the output transforms' first nb blocks: 256 channels
+// per block, every thread one channel summed over the partial rows in a fixed order
+__device__ __forceinline__ void wgrad_out_bias_block(int N, int accumulate, const WgradOutBias& bias) {
+  const int n = blockIdx.x * 256 + threadIdx.x;
+  if (n >= N) return;
+  const float* pp = bias.part + n;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;  // four chains, combined in a fixed order
+  int r = 0;
+  for (; r + 3 < bias.rows; r += 4) {
+    s0 += pp[(size_t)r * N];
+    s1 += pp[(size_t)(r + 1) * N];
+    s2 += pp[(size_t)(r + 2) * N];
+    s3 += pp[(size_t)(r + 3) * N];
+  }
+  for (; r < bias.rows; ++r) s0 += pp[(size_t)r * N];
+  const float v = ((s0 + s1) + (s2 + s3)) * bias.scale;
+  bias.db[n] = accumulate ? bias.db[n] + v : v;
+}
+
 // The same as a block-tiled pass (NC % 64 == 0: every F(3x3,4x4) layer with 64-multiple channels).
 // The one-thread-per-(n, c) form above ran at 0.7 TB/s in the step (profiles/r4_e: 36 x nsplit
 // dependent-latency loads per thread, 256 blocks of 256 threads for a 256 x 256 layer). Here a
@@ -1135,21 +1154,7 @@ __global__ __launch_bounds__(256) void wino4_wgrad_out_tiled_kernel(const float*
                                                                     int nsplit, int64_t sstride, WgradOutBias bias,
                                                                     int nb) {
   if ((int)blockIdx.x < nb) {
-    const int n = blockIdx.x * 256 + threadIdx.x;
-    if (n < N) {
-      const float* pp = bias.part + n;
-      float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;  // four chains, combined in a fixed order
-      int r = 0;
-      for (; r + 3 < bias.rows; r += 4) {
-        s0 += pp[(size_t)r * N];
-        s1 += pp[(size_t)(r + 1) * N];
-        s2 += pp[(size_t)(r + 2) * N];
-        s3 += pp[(size_t)(r + 3) * N];
-      }
-      for (; r < bias.rows; ++r) s0 += pp[(size_t)r * N];
-      const float v = ((s0 + s1) + (s2 + s3)) * bias.scale;
-      bias.db[n] = accumulate ? bias.db[n] + v : v;
-    }
+    wgrad_out_bias_block(N, accumulate, bias);
     return;
   }
   __shared__ float sm[36][65];
@@ -1222,21 +1227,7 @@ __global__ __launch_bounds__(256) void wino4_wgrad_out_v4_kernel(const float* __
                                                                  int64_t sstride, WgradOutBias bias, int nb) {
   constexpr int L = EPB / 4, G = 256 / L, Q = (36 + G - 1) / G;
   if ((int)blockIdx.x < nb) {  // the bias gradient, as wino4_wgrad_out_tiled_kernel
-    const int n = blockIdx.x * 256 + threadIdx.x;
-    if (n < N) {
-      const float* pp = bias.part + n;
-      float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-      int r = 0;
-      for (; r + 3 < bias.rows; r += 4) {
-        s0 += pp[(size_t)r * N];
-        s1 += pp[(size_t)(r + 1) * N];
-        s2 += pp[(size_t)(r + 2) * N];
-        s3 += pp[(size_t)(r + 3) * N];
-      }
-      for (; r < bias.rows; ++r) s0 += pp[(size_t)r * N];
-      const float v = ((s0 + s1) + (s2 + s3)) * bias.scale;
-      bias.db[n] = accumulate ? bias.db[n] + v : v;
-    }
+    wgrad_out_bias_block(N, accumulate, bias);
     return;
   }
   __shared__ __attribute__((aligned(16))) float sm[36][EPB + 4];
